@@ -1,0 +1,805 @@
+// PCPS acquisition engine for MI355X (gfx950).
+//
+// Restates pcps_acquisition::acquisition_core
+// (src/algorithms/acquisition/gnuradio_blocks/pcps_acquisition.cc:615-882) as a
+// batched grid over (block, Doppler bin, PRN):
+//
+//   K_wipe    (init)  w_d[n] = exp(j*phi_n), phi accumulated in fp32 exactly like the
+//                     generic volk_gnsssdr_s32f_sincos_32fc (pcps_acquisition.cc:233-246,298-305)
+//   K_code    (init)  Cf_p = FFT(code_p placed in the FFT buffer)       (:176-209)
+//   K_forward         X_{b,d} = FFT(x_b .* w_d)                          (:658-662)
+//   K_correlate       per (b,d,p): |IFFT(X_{b,d} .* conj(Cf_p))|^2 in LDS, fused with the
+//                     row reductions (max, first argmax, sum); the D x N magnitude grid
+//                     of the reference never reaches HBM                  (:664-679)
+//   K_reduce          per (b,p): grid maximum with the reference tie-break, CFAR input power,
+//                     Gnss_Synchro fields                                (:511-543, :697-713)
+//   K_second          per (b,p), peak-ratio mode only: recompute row d*, second peak outside
+//                     the +-1 chip window with the reference's wrap      (:546-612)
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "fft_lds.h"
+#include "fft_plan.h"
+#include "gsdr_internal.h"
+
+namespace
+{
+
+using gsdr::fft::Plan;
+
+struct RowStat
+{
+    float max;
+    uint32_t idx;
+    float sum;
+    uint32_t pad;
+};
+
+struct AcqParams
+{
+    uint32_t N;          // fft size
+    uint32_t consumed;   // valid samples per block
+    uint32_t lead_zeros; // zero samples placed before the code (sampled_ms != ms_per_code)
+    uint32_t D;
+    uint32_t P;
+    int32_t doppler_max;
+    int32_t doppler_center;
+    int32_t doppler_step;
+    float samples_per_code;
+    uint32_t samples_per_chip;
+    uint32_t dwells;
+    float threshold;
+    int32_t cfar;
+};
+
+template <int IT>
+__device__ __forceinline__ float2 load_item(const void* __restrict__ p, size_t i)
+{
+    if constexpr (IT == GSDR_ITEM_GR_COMPLEX)
+        {
+            return reinterpret_cast<const float2*>(p)[i];
+        }
+    else
+        {
+            short2 s = reinterpret_cast<const short2*>(p)[i];
+            return make_float2((float)s.x, (float)s.y);
+        }
+}
+
+__device__ __forceinline__ bool stat_better(float am, uint32_t ai, float bm, uint32_t bi)
+{
+    return am > bm || (am == bm && ai < bi);
+}
+
+// Block-wide (max, first argmax, sum) reduction; result valid in thread 0.
+template <int NT>
+__device__ __forceinline__ void block_reduce_stat(float& m, uint32_t& idx, float& sum, RowStat* scratch)
+{
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1)
+        {
+            float om = __shfl_xor(m, off);
+            uint32_t oi = __shfl_xor(idx, off);
+            float os = __shfl_xor(sum, off);
+            if (stat_better(om, oi, m, idx))
+                {
+                    m = om;
+                    idx = oi;
+                }
+            sum += os;
+        }
+    constexpr int NW = NT / 64;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (NW > 1)
+        {
+            if (lane == 0) scratch[wave] = RowStat{m, idx, sum, 0};
+            __syncthreads();
+            if (threadIdx.x == 0)
+                {
+                    for (int w = 1; w < NW; ++w)
+                        {
+                            RowStat s = scratch[w];
+                            if (stat_better(s.max, s.idx, m, idx))
+                                {
+                                    m = s.max;
+                                    idx = s.idx;
+                                }
+                            sum += s.sum;
+                        }
+                }
+        }
+}
+
+// ---------------------------------------------------------------- K_wipe
+// One workgroup per Doppler bin.  Lane 0 replays the generic sincos phase
+// accumulation (KERN/s32f_sincos_32fc.h:390-403) sequentially in fp32; the
+// workgroup then evaluates cos/sin in parallel.
+__global__ void __launch_bounds__(256) acq_wipeoff_kernel(float2* __restrict__ wipe, uint32_t N, float fs,
+    int32_t doppler_max, int32_t doppler_center, int32_t doppler_step, int32_t doppler_bias)
+{
+    const uint32_t d = blockIdx.x;
+    float2* row = wipe + (size_t)d * N;
+    if (threadIdx.x == 0)
+        {
+            const int32_t doppler = -doppler_max + doppler_center + doppler_step * (int32_t)d;
+            const float freq = (float)(doppler_bias + doppler);
+            const float phase_step = __fdiv_rn(__fmul_rn(6.283185307179586f, freq), fs);
+            const float inc = -phase_step;
+            float ph = 0.0f;
+            for (uint32_t i = 0; i < N; ++i)
+                {
+                    row[i].x = ph;
+                    ph = __fadd_rn(ph, inc);
+                }
+        }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < N; i += blockDim.x)
+        {
+            float s, c;
+            sincosf(row[i].x, &s, &c);
+            row[i] = make_float2(c, s);
+        }
+}
+
+// ---------------------------------------------------------------- K_code
+template <class PT>
+__global__ void __launch_bounds__(PT::NT) acq_code_fft_kernel(const float2* __restrict__ codes,
+    float2* __restrict__ code_fft, const float2* __restrict__ tw, Plan plan, uint32_t consumed, uint32_t lead)
+{
+    extern __shared__ float2 lds[];
+    const uint32_t p = blockIdx.x;
+    const float2* c = codes + (size_t)p * consumed;
+    float2* out = code_fft + (size_t)p * plan.n;
+    auto load = [&](int i) -> float2 {
+        int k = i - (int)lead;
+        return (k >= 0 && k < (int)consumed) ? c[k] : make_float2(0.f, 0.f);
+    };
+    auto store = [&](int i, float2 v) { out[i] = v; };
+    PT::run(plan, lds, tw, load, store);
+}
+
+// ---------------------------------------------------------------- K_forward
+template <class PT, int IT>
+__global__ void __launch_bounds__(PT::NT) acq_forward_kernel(const void* __restrict__ iq, uint64_t block_stride,
+    const float2* __restrict__ wipe, float2* __restrict__ X, const float2* __restrict__ tw, Plan plan,
+    uint32_t consumed, uint32_t D)
+{
+    extern __shared__ float2 lds[];
+    const uint32_t d = blockIdx.x, b = blockIdx.y;
+    const size_t base = (size_t)b * block_stride;
+    const float2* w = wipe + (size_t)d * plan.n;
+    float2* out = X + ((size_t)b * D + d) * plan.n;
+    auto load = [&](int i) -> float2 {
+        if (i >= (int)consumed) return make_float2(0.f, 0.f);
+        return gsdr::fft::cmul(load_item<IT>(iq, base + i), w[i]);
+    };
+    auto store = [&](int i, float2 v) { out[i] = v; };
+    PT::run(plan, lds, tw, load, store);
+}
+
+// ---------------------------------------------------------------- K_correlate
+// blockIdx.x = d*P + p (consecutive workgroups share the spectrum X_{b,d}), blockIdx.y = b.
+// GRID: also write the full |R|^2 row (the reference's grid dump).
+template <class PT, bool GRID>
+__global__ void __launch_bounds__(PT::NT) acq_correlate_kernel(const float2* __restrict__ X,
+    const float2* __restrict__ code_fft, RowStat* __restrict__ stats, float* __restrict__ grid,
+    const float2* __restrict__ tw, Plan plan, uint32_t D, uint32_t P, uint32_t prn_slot_for_grid)
+{
+    extern __shared__ float2 lds[];
+    RowStat* scratch = reinterpret_cast<RowStat*>(lds + plan.n);
+    const uint32_t N = plan.n;
+    uint32_t d, p;
+    if (GRID)
+        {
+            d = blockIdx.x;
+            p = prn_slot_for_grid;
+        }
+    else
+        {
+            d = blockIdx.x / P;
+            p = blockIdx.x - d * P;
+        }
+    const uint32_t b = blockIdx.y;
+    const float2* x = X + ((size_t)b * D + d) * N;
+    const float2* c = code_fft + (size_t)p * N;
+    float best = -1.0f, sum = 0.0f;
+    uint32_t bidx = 0xffffffffu;
+    // conj(X . conj(C)) = conj(X) . C ; |IFFT(Y)| = |FFT(conj(Y))|
+    auto load = [&](int i) -> float2 {
+        float2 a = x[i], k = c[i];
+        return make_float2(a.x * k.x + a.y * k.y, a.x * k.y - a.y * k.x);
+    };
+    auto store = [&](int i, float2 v) {
+        const float m = v.x * v.x + v.y * v.y;
+        if (GRID) grid[(size_t)d * N + i] = m;
+        if (stat_better(m, (uint32_t)i, best, bidx))
+            {
+                best = m;
+                bidx = (uint32_t)i;
+            }
+        sum += m;
+    };
+    PT::run(plan, lds, tw, load, store);
+    if (!GRID)
+        {
+            block_reduce_stat<PT::NT>(best, bidx, sum, scratch);
+            if (threadIdx.x == 0) stats[((size_t)b * P + p) * D + d] = RowStat{best, bidx, sum, 0};
+        }
+}
+
+// ---------------------------------------------------------------- K_reduce
+// One wave per (b, p).  Rows are scanned in increasing d by each lane and merged
+// with the (max desc, d asc) order, reproducing the reference's strict '>' scan.
+__global__ void __launch_bounds__(64) acq_reduce_kernel(const RowStat* __restrict__ stats,
+    gsdr_acq_result* __restrict__ res, const uint32_t* __restrict__ prn_ids, AcqParams ap, uint64_t stamp0,
+    uint64_t block_stride)
+{
+    const uint32_t bp = blockIdx.x;  // b*P + p
+    const uint32_t b = bp / ap.P, p = bp - b * ap.P;
+    const RowStat* s = stats + (size_t)bp * ap.D;
+    float m = -1.0f;
+    uint32_t dsel = 0xffffffffu, tsel = 0;
+    for (uint32_t d = threadIdx.x; d < ap.D; d += 64)
+        {
+            RowStat r = s[d];
+            if (r.max > m)
+                {
+                    m = r.max;
+                    dsel = d;
+                    tsel = r.idx;
+                }
+        }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1)
+        {
+            float om = __shfl_xor(m, off);
+            uint32_t od = __shfl_xor(dsel, off);
+            uint32_t ot = __shfl_xor(tsel, off);
+            if (stat_better(om, od, m, dsel))
+                {
+                    m = om;
+                    dsel = od;
+                    tsel = ot;
+                }
+        }
+    if (threadIdx.x != 0) return;
+    gsdr_acq_result r;
+    r.prn = prn_ids[p];
+    r.doppler_index = dsel;
+    r.code_phase = tsel;
+    r.doppler_hz = -ap.doppler_max + ap.doppler_center + ap.doppler_step * (int32_t)dsel;
+    r.peak = m;
+    r.second_peak = 0.0f;
+    r.input_power = 0.0f;
+    r.test_statistic = 0.0f;
+    r.acq_delay_samples = (double)fmodf((float)tsel, ap.samples_per_code);
+    r.samplestamp = stamp0 + (uint64_t)b * block_stride;
+    r.positive = 0;
+    r.reserved = 0;
+    if (ap.cfar)
+        {
+            const uint32_t opp = (dsel + ap.D / 2) % ap.D;
+            const float acc = s[opp].sum;
+            // float(accumulate) / int32 in float, then / 2.0 / counter in double (pcps_acquisition.cc:533)
+            const float ip = (float)((double)(acc / (float)(int32_t)ap.N) / 2.0 / (double)ap.dwells);
+            r.input_power = ip;
+            r.test_statistic = m / ip;
+            r.positive = r.test_statistic > ap.threshold ? 1 : 0;
+        }
+    res[bp] = r;
+}
+
+// ---------------------------------------------------------------- K_second
+// Peak-ratio statistic: recompute row d* of (b, p) and take the maximum outside
+// the cyclic exclusion range [e1, e2) built as in pcps_acquisition.cc:580-604.
+template <class PT>
+__global__ void __launch_bounds__(PT::NT) acq_second_peak_kernel(const float2* __restrict__ X,
+    const float2* __restrict__ code_fft, gsdr_acq_result* __restrict__ res, const float2* __restrict__ tw,
+    Plan plan, AcqParams ap)
+{
+    extern __shared__ float2 lds[];
+    RowStat* scratch = reinterpret_cast<RowStat*>(lds + plan.n);
+    const uint32_t bp = blockIdx.x;
+    const uint32_t b = bp / ap.P, p = bp - b * ap.P;
+    const uint32_t N = plan.n;
+    const uint32_t d = res[bp].doppler_index;
+    const int32_t ti = (int32_t)res[bp].code_phase;
+    int32_t e1 = ti - (int32_t)ap.samples_per_chip;
+    int32_t e2 = ti + (int32_t)ap.samples_per_chip;
+    if (e1 < 0)
+        e1 = (int32_t)N + e1;
+    else if (e2 >= (int32_t)N)
+        e2 = e2 - (int32_t)N;
+    const float2* x = X + ((size_t)b * ap.D + d) * N;
+    const float2* c = code_fft + (size_t)p * N;
+    float best = 0.0f, sum = 0.0f;
+    uint32_t bidx = 0;
+    auto load = [&](int i) -> float2 {
+        float2 a = x[i], k = c[i];
+        return make_float2(a.x * k.x + a.y * k.y, a.x * k.y - a.y * k.x);
+    };
+    auto store = [&](int i, float2 v) {
+        const bool excluded = (e1 < e2) ? (i >= e1 && i < e2) : (i >= e1 || i < e2);
+        const float m = excluded ? 0.0f : v.x * v.x + v.y * v.y;
+        if (stat_better(m, (uint32_t)i, best, bidx))
+            {
+                best = m;
+                bidx = (uint32_t)i;
+            }
+    };
+    PT::run(plan, lds, tw, load, store);
+    block_reduce_stat<PT::NT>(best, bidx, sum, scratch);
+    if (threadIdx.x == 0)
+        {
+            gsdr_acq_result r = res[bp];
+            r.second_peak = best;
+            r.test_statistic = r.peak / best;
+            r.positive = r.test_statistic > ap.threshold ? 1 : 0;
+            res[bp] = r;
+        }
+}
+
+}  // namespace
+
+// ====================================================================== handle
+struct gsdr_acq
+{
+    int device{0};
+    gsdr_acq_conf conf{};
+    uint32_t N{0}, D{0}, consumed{0}, lead{0};
+    float threshold{0.0f};
+    int nt{256};
+    int variant{0};
+    Plan plan{};
+    size_t lds_bytes{0};
+    hipStream_t stream{nullptr};
+    float2* d_tw{nullptr};
+    float2* d_wipe{nullptr};
+    float2* d_code_fft{nullptr};
+    float2* d_code_stage{nullptr};
+    uint32_t* d_prn{nullptr};
+    uint32_t nprn{0};
+    float2* d_X{nullptr};
+    RowStat* d_stats{nullptr};
+    gsdr_acq_result* d_res{nullptr};
+    void* d_iq{nullptr};
+    float* d_grid{nullptr};
+    std::mutex mu;
+};
+
+namespace
+{
+
+using gsdr::fft::RuntimePlan;
+using gsdr::fft::StaticPlan;
+
+size_t item_bytes(int it) { return it == GSDR_ITEM_CSHORT ? 4 : 8; }
+
+// FFT variants: compile-time plans for the sample rates GNSS front-ends use
+// (2/4/8/16 Msps at 1 ms), runtime-planned fallbacks for every other 2^a3^b5^c size.
+#define GSDR_ACQ_VARIANTS(X)               \
+    X(1, (StaticPlan<256, 20, 20, 10>))    \
+    X(2, (StaticPlan<512, 20, 20, 20>))    \
+    X(3, (StaticPlan<1024, 16, 10, 10, 10>)) \
+    X(4, (StaticPlan<256, 20, 10, 10>))    \
+    X(10, (RuntimePlan<256>))              \
+    X(11, (RuntimePlan<512>))              \
+    X(12, (RuntimePlan<1024>))
+
+template <class PT>
+int set_lds_attrs(size_t bytes)
+{
+    GSDR_HIP(hipFuncSetAttribute((const void*)acq_code_fft_kernel<PT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (int)bytes));
+    GSDR_HIP(hipFuncSetAttribute((const void*)acq_forward_kernel<PT, GSDR_ITEM_GR_COMPLEX>,
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+    GSDR_HIP(hipFuncSetAttribute((const void*)acq_forward_kernel<PT, GSDR_ITEM_CSHORT>,
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+    GSDR_HIP(hipFuncSetAttribute((const void*)acq_correlate_kernel<PT, false>,
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+    GSDR_HIP(hipFuncSetAttribute((const void*)acq_correlate_kernel<PT, true>,
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+    GSDR_HIP(hipFuncSetAttribute((const void*)acq_second_peak_kernel<PT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (int)bytes));
+    return GSDR_OK;
+}
+
+AcqParams params_of(const gsdr_acq* a)
+{
+    AcqParams ap{};
+    ap.N = a->N;
+    ap.consumed = a->consumed;
+    ap.lead_zeros = a->lead;
+    ap.D = a->D;
+    ap.P = a->nprn;
+    ap.doppler_max = a->conf.doppler_max;
+    ap.doppler_center = a->conf.doppler_center;
+    ap.doppler_step = (int32_t)a->conf.doppler_step;
+    ap.samples_per_code = a->conf.samples_per_code;
+    ap.samples_per_chip = a->conf.samples_per_chip;
+    ap.dwells = 1;
+    ap.threshold = a->threshold;
+    ap.cfar = a->conf.pfa > 0.0f ? 1 : 0;
+    return ap;
+}
+
+int rebuild_wipeoffs(gsdr_acq* a)
+{
+    hipLaunchKernelGGL(acq_wipeoff_kernel, dim3(a->D), dim3(256), 0, a->stream, a->d_wipe, a->N,
+        (float)a->conf.fs_in, a->conf.doppler_max, a->conf.doppler_center, (int32_t)a->conf.doppler_step,
+        a->conf.doppler_bias);
+    GSDR_HIP(hipGetLastError());
+    GSDR_HIP(hipStreamSynchronize(a->stream));
+    return GSDR_OK;
+}
+
+void compute_threshold(gsdr_acq* a)
+{
+    // calculate_threshold, pcps_acquisition.cc:894-909 (dwells == 1, no bit transition)
+    const float pfa = a->conf.pfa;
+    if (pfa <= 0.0f) return;
+    const int num_bins = (int)(a->N * a->D);
+    const double p = std::pow(1.0 - (double)pfa, 1.0 / (double)(float)num_bins);
+    a->threshold = (float)(2.0 * gsdr::gamma_p_inv_int(2 * (int)a->conf.max_dwells, p));
+}
+
+template <class PT>
+void launch_forward(gsdr_acq* a, const void* iq, int item_type, uint32_t nblocks, uint64_t stride, hipStream_t s)
+{
+    if (item_type == GSDR_ITEM_GR_COMPLEX)
+        hipLaunchKernelGGL((acq_forward_kernel<PT, GSDR_ITEM_GR_COMPLEX>), dim3(a->D, nblocks), dim3(PT::NT),
+            a->lds_bytes, s, iq, stride, a->d_wipe, a->d_X, a->d_tw, a->plan, a->consumed, a->D);
+    else
+        hipLaunchKernelGGL((acq_forward_kernel<PT, GSDR_ITEM_CSHORT>), dim3(a->D, nblocks), dim3(PT::NT),
+            a->lds_bytes, s, iq, stride, a->d_wipe, a->d_X, a->d_tw, a->plan, a->consumed, a->D);
+}
+
+template <class PT>
+int launch_all(gsdr_acq* a, const void* iq, int item_type, uint32_t nblocks, uint64_t stride, uint64_t stamp0,
+    gsdr_acq_result* res, hipStream_t s)
+{
+    const size_t lds = a->lds_bytes;
+    launch_forward<PT>(a, iq, item_type, nblocks, stride, s);
+    GSDR_HIP(hipGetLastError());
+    hipLaunchKernelGGL((acq_correlate_kernel<PT, false>), dim3(a->D * a->nprn, nblocks), dim3(PT::NT), lds, s,
+        a->d_X, a->d_code_fft, a->d_stats, (float*)nullptr, a->d_tw, a->plan, a->D, a->nprn, 0u);
+    GSDR_HIP(hipGetLastError());
+    AcqParams ap = params_of(a);
+    hipLaunchKernelGGL(acq_reduce_kernel, dim3(nblocks * a->nprn), dim3(64), 0, s, a->d_stats, res, a->d_prn, ap,
+        stamp0, stride);
+    GSDR_HIP(hipGetLastError());
+    if (!ap.cfar)
+        {
+            hipLaunchKernelGGL((acq_second_peak_kernel<PT>), dim3(nblocks * a->nprn), dim3(PT::NT), lds, s, a->d_X,
+                a->d_code_fft, res, a->d_tw, a->plan, ap);
+            GSDR_HIP(hipGetLastError());
+        }
+    return GSDR_OK;
+}
+
+template <class PT>
+int launch_code_fft(gsdr_acq* a, uint32_t nprn)
+{
+    hipLaunchKernelGGL((acq_code_fft_kernel<PT>), dim3(nprn), dim3(PT::NT), a->lds_bytes, a->stream, a->d_code_stage,
+        a->d_code_fft, a->d_tw, a->plan, a->consumed, a->lead);
+    GSDR_HIP(hipGetLastError());
+    return GSDR_OK;
+}
+
+template <class PT>
+int launch_dump(gsdr_acq* a, bool grid, uint32_t prn_slot)
+{
+    launch_forward<PT>(a, a->d_iq, a->conf.item_type, 1, a->consumed, a->stream);
+    GSDR_HIP(hipGetLastError());
+    if (grid)
+        {
+            hipLaunchKernelGGL((acq_correlate_kernel<PT, true>), dim3(a->D, 1), dim3(PT::NT), a->lds_bytes, a->stream,
+                a->d_X, a->d_code_fft, a->d_stats, a->d_grid, a->d_tw, a->plan, a->D, a->nprn, prn_slot);
+            GSDR_HIP(hipGetLastError());
+        }
+    return GSDR_OK;
+}
+
+// op: 0 run, 1 code fft, 2 dump spectra, 3 dump grid, 4 set attributes
+int dispatch(gsdr_acq* a, int op, const void* iq, uint32_t nblocks, uint64_t stride, uint64_t stamp0,
+    gsdr_acq_result* res, hipStream_t s, uint32_t aux)
+{
+#define GSDR_CASE(ID, PT)                                                                               \
+    case ID:                                                                                            \
+        switch (op)                                                                                     \
+            {                                                                                           \
+            case 0: return launch_all<GSDR_UNPAREN PT>(a, iq, a->conf.item_type, nblocks, stride, stamp0, res, s); \
+            case 1: return launch_code_fft<GSDR_UNPAREN PT>(a, aux);                                     \
+            case 2: return launch_dump<GSDR_UNPAREN PT>(a, false, 0);                                    \
+            case 3: return launch_dump<GSDR_UNPAREN PT>(a, true, aux);                                   \
+            default: return set_lds_attrs<GSDR_UNPAREN PT>(a->lds_bytes);                                \
+            }
+#define GSDR_UNPAREN(...) __VA_ARGS__
+    switch (a->variant)
+        {
+            GSDR_ACQ_VARIANTS(GSDR_CASE)
+        default: gsdr::set_error("internal: bad FFT variant %d", a->variant); return GSDR_E_STATE;
+        }
+#undef GSDR_CASE
+#undef GSDR_UNPAREN
+}
+
+// Pick a compile-time plan when one matches N, else the smallest workgroup that
+// admits a runtime plan.
+bool choose_variant(gsdr_acq* a)
+{
+    const int N = (int)a->N;
+    struct S
+    {
+        int id, n, nt;
+        gsdr::fft::Plan p;
+    };
+    const S statics[] = {
+        {1, StaticPlan<256, 20, 20, 10>::N, 256, StaticPlan<256, 20, 20, 10>::plan()},
+        {2, StaticPlan<512, 20, 20, 20>::N, 512, StaticPlan<512, 20, 20, 20>::plan()},
+        {3, StaticPlan<1024, 16, 10, 10, 10>::N, 1024, StaticPlan<1024, 16, 10, 10, 10>::plan()},
+        {4, StaticPlan<256, 20, 10, 10>::N, 256, StaticPlan<256, 20, 10, 10>::plan()},
+    };
+    for (const S& st : statics)
+        if (st.n == N)
+            {
+                a->variant = st.id;
+                a->nt = st.nt;
+                a->plan = st.p;
+                return true;
+            }
+    const int ids[] = {10, 11, 12};
+    const int nts[] = {256, 512, 1024};
+    for (int i = 0; i < 3; ++i)
+        if (gsdr::fft::make_plan(N, nts[i], a->plan) && a->plan.nstages >= 2)
+            {
+                a->variant = ids[i];
+                a->nt = nts[i];
+                return true;
+            }
+    return false;
+}
+
+}  // namespace
+
+// ====================================================================== ABI
+extern "C" {
+
+int gsdr_acq_create(int device, const gsdr_acq_conf* conf, gsdr_acq** out)
+{
+    GSDR_REQUIRE(conf && out, GSDR_E_ARG, "gsdr_acq_create: null argument");
+    *out = nullptr;
+    GSDR_REQUIRE(conf->fs_in > 0 && conf->consumed_samples > 0, GSDR_E_ARG, "gsdr_acq_create: fs_in and consumed_samples must be > 0");
+    GSDR_REQUIRE(conf->doppler_step > 0, GSDR_E_ARG, "gsdr_acq_create: doppler_step must be > 0");
+    GSDR_REQUIRE(conf->item_type == GSDR_ITEM_GR_COMPLEX || conf->item_type == GSDR_ITEM_CSHORT, GSDR_E_ARG,
+        "gsdr_acq_create: unknown item type %d", conf->item_type);
+    GSDR_REQUIRE(conf->max_prns > 0 && conf->max_blocks > 0, GSDR_E_ARG, "gsdr_acq_create: capacities must be > 0");
+    GSDR_REQUIRE(conf->pfa >= 0.0f && conf->pfa <= 1.0f, GSDR_E_ARG, "gsdr_acq_create: pfa outside [0,1]");
+    GSDR_REQUIRE(conf->max_dwells <= 1, GSDR_E_UNSUPPORTED, "gsdr_acq_create: max_dwells > 1 not implemented yet");
+    GSDR_REQUIRE(conf->bit_transition_flag == 0, GSDR_E_UNSUPPORTED, "gsdr_acq_create: bit_transition_flag not implemented yet");
+    int ndev = 0;
+    GSDR_HIP(hipGetDeviceCount(&ndev));
+    GSDR_REQUIRE(device >= 0 && device < ndev, GSDR_E_ARG, "gsdr_acq_create: device %d of %d", device, ndev);
+    gsdr::DeviceGuard g(device);
+
+    gsdr_acq* a = new (std::nothrow) gsdr_acq();
+    GSDR_REQUIRE(a, GSDR_E_ALLOC, "gsdr_acq_create: out of host memory");
+    a->device = device;
+    a->conf = *conf;
+    if (a->conf.max_dwells == 0) a->conf.max_dwells = 1;
+    a->consumed = conf->consumed_samples;
+    // pcps_acquisition.cc:85-92
+    uint32_t N = conf->fft_size;
+    if (N == 0) N = (conf->sampled_ms == conf->ms_per_code || conf->sampled_ms == 0) ? a->consumed : 2 * a->consumed;
+    if (N < a->consumed)
+        {
+            delete a;
+            gsdr::set_error("gsdr_acq_create: fft_size %u < consumed_samples %u", N, a->consumed);
+            return GSDR_E_ARG;
+        }
+    a->N = N;
+    a->lead = N - a->consumed;
+    a->D = conf->num_doppler_bins;
+    if (a->D == 0)
+        a->D = (uint32_t)std::ceil((double)(conf->doppler_max - (-conf->doppler_max)) / (double)conf->doppler_step);
+    if (a->D == 0)
+        {
+            delete a;
+            gsdr::set_error("gsdr_acq_create: zero Doppler bins");
+            return GSDR_E_ARG;
+        }
+    const bool ok = choose_variant(a);
+    a->lds_bytes = (size_t)N * sizeof(float2) + 16 * sizeof(RowStat);
+    if (!ok || a->lds_bytes > 160 * 1024)
+        {
+            delete a;
+            gsdr::set_error("gsdr_acq_create: FFT size %u not supported by the LDS engine (needs 2^a*3^b*5^c and <= 20352 points)", N);
+            return GSDR_E_UNSUPPORTED;
+        }
+    int rc = dispatch(a, 4, nullptr, 0, 0, 0, nullptr, nullptr, 0);
+    if (rc != GSDR_OK)
+        {
+            delete a;
+            return rc;
+        }
+    const size_t nP = conf->max_prns, nB = conf->max_blocks;
+    hipError_t e = hipStreamCreateWithFlags(&a->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMalloc(&a->d_tw, N * sizeof(float2));
+    if (e == hipSuccess) e = hipMalloc(&a->d_wipe, (size_t)a->D * N * sizeof(float2));
+    if (e == hipSuccess) e = hipMalloc(&a->d_code_fft, nP * N * sizeof(float2));
+    if (e == hipSuccess) e = hipMalloc(&a->d_code_stage, nP * a->consumed * sizeof(float2));
+    if (e == hipSuccess) e = hipMalloc(&a->d_prn, nP * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc(&a->d_X, nB * a->D * N * sizeof(float2));
+    if (e == hipSuccess) e = hipMalloc(&a->d_stats, nB * nP * a->D * sizeof(RowStat));
+    if (e == hipSuccess) e = hipMalloc(&a->d_res, nB * nP * sizeof(gsdr_acq_result));
+    if (e == hipSuccess) e = hipMalloc(&a->d_iq, nB * a->consumed * item_bytes(conf->item_type));
+    if (e == hipSuccess) e = hipMalloc(&a->d_grid, (size_t)a->D * N * sizeof(float));
+    if (e != hipSuccess)
+        {
+            gsdr::set_error("gsdr_acq_create: device allocation failed: %s", hipGetErrorString(e));
+            gsdr_acq_destroy(a);
+            return GSDR_E_ALLOC;
+        }
+    // twiddles W_N^m in double, rounded once
+    std::vector<float2> tw(N);
+    for (uint32_t m = 0; m < N; ++m)
+        {
+            const double ang = 2.0 * M_PI * (double)m / (double)N;
+            tw[m] = make_float2((float)std::cos(ang), (float)(-std::sin(ang)));
+        }
+    if ((e = hipMemcpy(a->d_tw, tw.data(), N * sizeof(float2), hipMemcpyHostToDevice)) != hipSuccess)
+        {
+            gsdr::set_error("gsdr_acq_create: twiddle upload: %s", hipGetErrorString(e));
+            gsdr_acq_destroy(a);
+            return GSDR_E_DEVICE;
+        }
+    rc = rebuild_wipeoffs(a);
+    if (rc != GSDR_OK)
+        {
+            gsdr_acq_destroy(a);
+            return rc;
+        }
+    compute_threshold(a);
+    *out = a;
+    return GSDR_OK;
+}
+
+void gsdr_acq_destroy(gsdr_acq* a)
+{
+    if (!a) return;
+    gsdr::DeviceGuard g(a->device);
+    if (a->stream) (void)hipStreamSynchronize(a->stream);
+    void* bufs[] = {a->d_tw, a->d_wipe, a->d_code_fft, a->d_code_stage, a->d_prn, a->d_X, a->d_stats, a->d_res,
+        a->d_iq, a->d_grid};
+    for (void* p : bufs)
+        if (p) (void)hipFree(p);
+    if (a->stream) (void)hipStreamDestroy(a->stream);
+    delete a;
+}
+
+int gsdr_acq_get_dims(const gsdr_acq* a, uint32_t* D, uint32_t* N)
+{
+    GSDR_REQUIRE(a, GSDR_E_ARG, "gsdr_acq_get_dims: null handle");
+    if (D) *D = a->D;
+    if (N) *N = a->N;
+    return GSDR_OK;
+}
+
+int gsdr_acq_set_local_codes(gsdr_acq* a, const float* codes, const uint32_t* prn, uint32_t nprn)
+{
+    GSDR_REQUIRE(a && codes && prn, GSDR_E_ARG, "gsdr_acq_set_local_codes: null argument");
+    GSDR_REQUIRE(nprn > 0 && nprn <= a->conf.max_prns, GSDR_E_ARG, "gsdr_acq_set_local_codes: nprn %u outside [1,%u]",
+        nprn, a->conf.max_prns);
+    std::lock_guard<std::mutex> lk(a->mu);
+    gsdr::DeviceGuard g(a->device);
+    GSDR_HIP(hipMemcpyAsync(a->d_code_stage, codes, (size_t)nprn * a->consumed * sizeof(float2),
+        hipMemcpyHostToDevice, a->stream));
+    GSDR_HIP(hipMemcpyAsync(a->d_prn, prn, nprn * sizeof(uint32_t), hipMemcpyHostToDevice, a->stream));
+    int rc = dispatch(a, 1, nullptr, 0, 0, 0, nullptr, nullptr, nprn);
+    if (rc != GSDR_OK) return rc;
+    GSDR_HIP(hipStreamSynchronize(a->stream));
+    a->nprn = nprn;
+    return GSDR_OK;
+}
+
+int gsdr_acq_set_doppler(gsdr_acq* a, int32_t doppler_max, uint32_t doppler_step, int32_t doppler_center)
+{
+    GSDR_REQUIRE(a, GSDR_E_ARG, "gsdr_acq_set_doppler: null handle");
+    GSDR_REQUIRE(doppler_step > 0, GSDR_E_ARG, "gsdr_acq_set_doppler: doppler_step must be > 0");
+    std::lock_guard<std::mutex> lk(a->mu);
+    gsdr::DeviceGuard g(a->device);
+    const uint32_t D = (uint32_t)std::ceil((double)(doppler_max - (-doppler_max)) / (double)doppler_step);
+    GSDR_REQUIRE(a->conf.num_doppler_bins != 0 || D == a->D, GSDR_E_UNSUPPORTED,
+        "gsdr_acq_set_doppler: changing the number of Doppler bins (%u -> %u) requires a new handle", a->D, D);
+    a->conf.doppler_max = doppler_max;
+    a->conf.doppler_step = doppler_step;
+    a->conf.doppler_center = doppler_center;
+    int rc = rebuild_wipeoffs(a);
+    if (rc != GSDR_OK) return rc;
+    compute_threshold(a);
+    return GSDR_OK;
+}
+
+int gsdr_acq_set_threshold(gsdr_acq* a, float threshold)
+{
+    GSDR_REQUIRE(a, GSDR_E_ARG, "gsdr_acq_set_threshold: null handle");
+    a->threshold = threshold;
+    return GSDR_OK;
+}
+
+int gsdr_acq_get_threshold(const gsdr_acq* a, float* threshold)
+{
+    GSDR_REQUIRE(a && threshold, GSDR_E_ARG, "gsdr_acq_get_threshold: null argument");
+    *threshold = a->threshold;
+    return GSDR_OK;
+}
+
+int gsdr_acq_run_device(gsdr_acq* a, const void* iq_dev, uint32_t nblocks, uint64_t stride, uint64_t stamp0,
+    gsdr_acq_result* out_dev, void* stream)
+{
+    GSDR_REQUIRE(a && iq_dev && out_dev, GSDR_E_ARG, "gsdr_acq_run_device: null argument");
+    GSDR_REQUIRE(a->nprn > 0, GSDR_E_STATE, "gsdr_acq_run_device: set_local_codes first");
+    GSDR_REQUIRE(nblocks > 0 && nblocks <= a->conf.max_blocks, GSDR_E_ARG, "gsdr_acq_run_device: nblocks %u outside [1,%u]",
+        nblocks, a->conf.max_blocks);
+    GSDR_REQUIRE(stride >= a->consumed || nblocks == 1, GSDR_E_ARG, "gsdr_acq_run_device: block stride %llu < consumed %u",
+        (unsigned long long)stride, a->consumed);
+    gsdr::DeviceGuard g(a->device);
+    hipStream_t s = stream ? (hipStream_t)stream : a->stream;
+    return dispatch(a, 0, iq_dev, nblocks, stride, stamp0, out_dev, s, 0);
+}
+
+int gsdr_acq_run(gsdr_acq* a, const void* iq_host, uint32_t nblocks, uint64_t stamp0, gsdr_acq_result* out)
+{
+    GSDR_REQUIRE(a && iq_host && out, GSDR_E_ARG, "gsdr_acq_run: null argument");
+    GSDR_REQUIRE(a->nprn > 0, GSDR_E_STATE, "gsdr_acq_run: set_local_codes first");
+    GSDR_REQUIRE(nblocks > 0 && nblocks <= a->conf.max_blocks, GSDR_E_ARG, "gsdr_acq_run: nblocks %u outside [1,%u]",
+        nblocks, a->conf.max_blocks);
+    std::lock_guard<std::mutex> lk(a->mu);
+    gsdr::DeviceGuard g(a->device);
+    const size_t bytes = (size_t)nblocks * a->consumed * item_bytes(a->conf.item_type);
+    GSDR_HIP(hipMemcpyAsync(a->d_iq, iq_host, bytes, hipMemcpyHostToDevice, a->stream));
+    int rc = dispatch(a, 0, a->d_iq, nblocks, a->consumed, stamp0, a->d_res, a->stream, 0);
+    if (rc != GSDR_OK) return rc;
+    GSDR_HIP(hipMemcpyAsync(out, a->d_res, (size_t)nblocks * a->nprn * sizeof(gsdr_acq_result), hipMemcpyDeviceToHost,
+        a->stream));
+    GSDR_HIP(hipStreamSynchronize(a->stream));
+    return GSDR_OK;
+}
+
+int gsdr_acq_dump_spectra(gsdr_acq* a, const void* iq_host, float* spectra_host)
+{
+    GSDR_REQUIRE(a && iq_host && spectra_host, GSDR_E_ARG, "gsdr_acq_dump_spectra: null argument");
+    std::lock_guard<std::mutex> lk(a->mu);
+    gsdr::DeviceGuard g(a->device);
+    GSDR_HIP(hipMemcpyAsync(a->d_iq, iq_host, (size_t)a->consumed * item_bytes(a->conf.item_type),
+        hipMemcpyHostToDevice, a->stream));
+    int rc = dispatch(a, 2, nullptr, 1, 0, 0, nullptr, a->stream, 0);
+    if (rc != GSDR_OK) return rc;
+    GSDR_HIP(hipMemcpyAsync(spectra_host, a->d_X, (size_t)a->D * a->N * sizeof(float2), hipMemcpyDeviceToHost,
+        a->stream));
+    GSDR_HIP(hipStreamSynchronize(a->stream));
+    return GSDR_OK;
+}
+
+int gsdr_acq_dump_grid(gsdr_acq* a, const void* iq_host, uint32_t prn_slot, float* grid_host)
+{
+    GSDR_REQUIRE(a && iq_host && grid_host, GSDR_E_ARG, "gsdr_acq_dump_grid: null argument");
+    GSDR_REQUIRE(prn_slot < a->nprn, GSDR_E_ARG, "gsdr_acq_dump_grid: prn_slot %u >= nprn %u", prn_slot, a->nprn);
+    std::lock_guard<std::mutex> lk(a->mu);
+    gsdr::DeviceGuard g(a->device);
+    GSDR_HIP(hipMemcpyAsync(a->d_iq, iq_host, (size_t)a->consumed * item_bytes(a->conf.item_type),
+        hipMemcpyHostToDevice, a->stream));
+    int rc = dispatch(a, 3, nullptr, 1, 0, 0, nullptr, a->stream, prn_slot);
+    if (rc != GSDR_OK) return rc;
+    GSDR_HIP(hipMemcpyAsync(grid_host, a->d_grid, (size_t)a->D * a->N * sizeof(float), hipMemcpyDeviceToHost,
+        a->stream));
+    GSDR_HIP(hipStreamSynchronize(a->stream));
+    return GSDR_OK;
+}
+
+}  // extern "C"

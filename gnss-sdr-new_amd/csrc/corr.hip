@@ -1,0 +1,554 @@
+// Tracking multicorrelator engine for MI355X (gfx950).
+//
+// One fused launch replaces, for every job (channel-epoch) of a batch, the pair
+//   volk_gnsssdr_32f_xn_resampler_32f_xn            (K code replicas written to memory)
+//   volk_gnsssdr_32fc_32f_rotator_dot_prod_32fc_xn  (carrier rotator + K dot products)
+// behind Cpu_Multicorrelator_Real_Codes::Carrier_wipeoff_multicorrelator_resampler
+// (src/algorithms/tracking/libs/cpu_multicorrelator_real_codes.cc:103-144), and the
+// complex-replica pair behind Cpu_Multicorrelator (cpu_multicorrelator.cc:73-100).
+//
+// Per workgroup (one job): the channel's code replica is staged in LDS; each lane
+// streams IQ samples (coalesced), regenerates the carrier phasor from an fp64
+// phase (the reference's phasor recursion with its float-rounded phase_inc, but
+// without its accumulated rounding), computes every tap's code index with the
+// reference's exact float association (no FMA contraction), and
+// accumulates K complex sums in VGPRs; wave64 shuffles + an LDS pass reduce them.
+// The K x N resampled-code matrix of the reference never exists.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <complex>
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "gsdr_internal.h"
+
+namespace
+{
+
+constexpr int kMaxTaps = 8;
+constexpr int kCorrThreads = 256;
+constexpr int kMaxCodeSamples = 16384;  // LDS-staged replica capacity (floats; complex codes use 2x)
+
+struct ChanDev
+{
+    const float* code;  // L floats (real) or 2L floats (complex)
+    int32_t L;
+    int32_t ntaps;
+    int32_t high_dyn;
+    int32_t cplx;
+    float shifts[kMaxTaps];
+};
+
+// Host-derived rotator model of one job (the reference builds phase_offset and
+// phase_inc on the host too, cpu_multicorrelator_real_codes.cc:114-123).
+struct JobAux
+{
+    double psi0;   // arg(cos(rem), -sin(rem)) in float
+    double theta;  // arg(exp(-j*step)) in float
+    double theta_rate;
+    int32_t valid;
+    int32_t pad;
+};
+
+template <int IT>
+__device__ __forceinline__ float2 load_item(const void* __restrict__ p, int64_t i)
+{
+    if constexpr (IT == GSDR_ITEM_GR_COMPLEX)
+        {
+            return reinterpret_cast<const float2*>(p)[i];
+        }
+    else
+        {
+            short2 s = reinterpret_cast<const short2*>(p)[i];
+            return make_float2((float)s.x, (float)s.y);
+        }
+}
+
+__device__ __forceinline__ int wrap_mod(int idx, int L)
+{
+    int r = idx % L;
+    return r < 0 ? r + L : r;
+}
+
+// KERN/32f_xn_resampler_32f_xn.h:73 (generic) / :384-390 (a_avx).
+__device__ __forceinline__ int code_index(float step, float shift, float rem, int n, int L, int assoc)
+{
+    const float a = __fmul_rn(step, (float)n);
+    float t;
+    if (assoc == GSDR_ASSOC_GENERIC)
+        t = __fsub_rn(__fadd_rn(a, shift), rem);
+    else
+        t = __fadd_rn(a, __fsub_rn(shift, rem));
+    return wrap_mod((int)floorf(t), L);
+}
+
+// KERN/32f_xn_high_dynamics_resampler_32f_xn.h:75-79 (tap 0).
+__device__ __forceinline__ int code_index_hd(float step, float rate, float shift0, float rem, uint32_t m, int L)
+{
+    const float a = __fmul_rn(step, (float)m);
+    const float b = __fmul_rn(rate, (float)(m * m));
+    const float t = __fsub_rn(__fadd_rn(__fadd_rn(a, b), shift0), rem);
+    return wrap_mod((int)floorf(t), L);
+}
+
+__device__ __forceinline__ void rotator_model_device(const gsdr_corr_job& j, double& psi0, double& th, double& thr)
+{
+    float s, c;
+    sincosf(j.rem_carr_phase_rad, &s, &c);
+    psi0 = atan2(-(double)s, (double)c);
+    sincosf(-j.carr_phase_step_rad, &s, &c);
+    th = atan2((double)s, (double)c);
+    sincosf(-j.carr_phase_rate_step_rad, &s, &c);
+    thr = atan2((double)s, (double)c);
+}
+
+// Streaming body: one lane per sample, K taps accumulated in VGPRs.
+template <int IT, bool CPLX>
+__device__ __forceinline__ void corr_accumulate(const gsdr_corr_job& job, const ChanDev& ch, const float* s_code,
+    const int* s_hdshift, double psi0, double th, double thr, const void* __restrict__ iq, int64_t iq_items, int assoc,
+    float2 (&acc)[kMaxTaps])
+{
+    const int L = ch.L;
+    const int K = ch.ntaps;
+    const int N = job.n_samples;
+    const bool hd = ch.high_dyn != 0;
+    const float rem = job.rem_code_phase_chips, step = job.code_phase_step_chips, rate = job.code_phase_rate_step_chips;
+    constexpr double kTwoPi = 6.283185307179586476925286766559;
+    constexpr double kInvTwoPi = 0.15915494309189533576888376337251;
+    for (int n = threadIdx.x; n < N; n += kCorrThreads)
+        {
+            const int64_t item = job.sample_offset + n;
+            const float2 x = (item >= 0 && item < iq_items) ? load_item<IT>(iq, item) : make_float2(0.f, 0.f);
+            double phi = psi0 + (double)n * th;
+            if (hd && n > 0)
+                {
+                    const double m1 = (double)(n - 1);
+                    phi += m1 * m1 * thr;
+                }
+            const double kk = rint(phi * kInvTwoPi);
+            const float a = (float)fma(-kk, kTwoPi, phi);
+            float s, c;
+            sincosf(a, &s, &c);
+            const float2 t = make_float2(x.x * c - x.y * s, x.x * s + x.y * c);
+#pragma unroll
+            for (int k = 0; k < kMaxTaps; ++k)
+                {
+                    if (k < K)
+                        {
+                            int idx;
+                            if (hd)
+                                {
+                                    const uint32_t m = (uint32_t)((n + s_hdshift[k]) % N);
+                                    idx = code_index_hd(step, rate, ch.shifts[0], rem, m, L);
+                                }
+                            else
+                                {
+                                    idx = code_index(step, ch.shifts[k], rem, n, L, assoc);
+                                }
+                            if (CPLX)
+                                {
+                                    const float cr = s_code[2 * idx], ci = s_code[2 * idx + 1];
+                                    acc[k].x += t.x * cr - t.y * ci;
+                                    acc[k].y += t.x * ci + t.y * cr;
+                                }
+                            else
+                                {
+                                    const float cv = s_code[idx];
+                                    acc[k].x += t.x * cv;
+                                    acc[k].y += t.y * cv;
+                                }
+                        }
+                }
+        }
+}
+
+template <int IT>
+__global__ void __launch_bounds__(kCorrThreads) corr_kernel(const gsdr_corr_job* __restrict__ jobs,
+    const JobAux* __restrict__ aux, const ChanDev* __restrict__ chans, const void* __restrict__ iq, int64_t iq_items,
+    float2* __restrict__ out, int max_taps, int assoc)
+{
+    extern __shared__ float s_code[];
+    __shared__ double s_model[3];
+    __shared__ int s_hdshift[kMaxTaps];
+    __shared__ float2 s_red[kCorrThreads / 64][kMaxTaps];
+
+    const gsdr_corr_job job = jobs[blockIdx.x];
+    const ChanDev ch = chans[job.channel];
+    const int K = ch.ntaps;
+
+    // stage the replica
+    const int code_floats = ch.cplx ? 2 * ch.L : ch.L;
+    for (int i = threadIdx.x; i < code_floats; i += kCorrThreads) s_code[i] = ch.code[i];
+    if (threadIdx.x == 0)
+        {
+            double psi0, th, thr;
+            if (aux && aux[blockIdx.x].valid)
+                {
+                    psi0 = aux[blockIdx.x].psi0;
+                    th = aux[blockIdx.x].theta;
+                    thr = aux[blockIdx.x].theta_rate;
+                }
+            else
+                {
+                    rotator_model_device(job, psi0, th, thr);
+                }
+            s_model[0] = psi0;
+            s_model[1] = th;
+            s_model[2] = thr;
+            // high-dynamics taps 1..K-1 are sample-shifted copies of tap 0
+            // (KERN/32f_xn_high_dynamics_resampler_32f_xn.h:84-91)
+            unsigned int sh = 0;
+            s_hdshift[0] = 0;
+            for (int k = 1; k < K && k < kMaxTaps; ++k)
+                {
+                    sh += (int)roundf((ch.shifts[k] - ch.shifts[k - 1]) / job.code_phase_step_chips);
+                    s_hdshift[k] = (int)sh;
+                }
+        }
+    __syncthreads();
+
+    float2 acc[kMaxTaps];
+#pragma unroll
+    for (int k = 0; k < kMaxTaps; ++k) acc[k] = make_float2(0.f, 0.f);
+    if (ch.cplx)
+        corr_accumulate<IT, true>(job, ch, s_code, s_hdshift, s_model[0], s_model[1], s_model[2], iq, iq_items, assoc, acc);
+    else
+        corr_accumulate<IT, false>(job, ch, s_code, s_hdshift, s_model[0], s_model[1], s_model[2], iq, iq_items, assoc, acc);
+
+    // wave64 reduction, then across the workgroup's waves in a fixed order
+#pragma unroll
+    for (int k = 0; k < kMaxTaps; ++k)
+        {
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1)
+                {
+                    acc[k].x += __shfl_xor(acc[k].x, off);
+                    acc[k].y += __shfl_xor(acc[k].y, off);
+                }
+        }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0)
+        {
+#pragma unroll
+            for (int k = 0; k < kMaxTaps; ++k) s_red[wave][k] = acc[k];
+        }
+    __syncthreads();
+    if (threadIdx.x < K)
+        {
+            float2 r = make_float2(0.f, 0.f);
+#pragma unroll
+            for (int w = 0; w < kCorrThreads / 64; ++w)
+                {
+                    r.x += s_red[w][threadIdx.x].x;
+                    r.y += s_red[w][threadIdx.x].y;
+                }
+            out[(size_t)blockIdx.x * max_taps + threadIdx.x] = r;
+        }
+}
+
+__global__ void corr_index_kernel(const ChanDev* __restrict__ chans, int channel, float rem, float step, int n_total,
+    int assoc, int32_t* __restrict__ out)
+{
+    const ChanDev ch = chans[channel];
+    const int n = blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= n_total) return;
+    for (int k = 0; k < ch.ntaps; ++k) out[(size_t)k * n_total + n] = code_index(step, ch.shifts[k], rem, n, ch.L, assoc);
+}
+
+}  // namespace
+
+struct gsdr_corr
+{
+    int device{0};
+    int max_channels{0}, max_len{0}, max_taps{0};
+    int assoc{GSDR_ASSOC_AVX};
+    hipStream_t stream{nullptr};
+    std::vector<ChanDev> chans;       // host mirror of the descriptors
+    std::vector<float*> code_bufs;    // per-channel device replica buffers
+    std::vector<int> code_caps;
+    ChanDev* d_chans{nullptr};
+    gsdr_corr_job* d_jobs{nullptr};
+    JobAux* d_aux{nullptr};
+    int jobs_cap{0};
+    void* d_iq{nullptr};
+    float2* d_out{nullptr};
+    std::vector<JobAux> h_aux;
+    int max_code_floats{0};  // largest staged replica over configured channels (sizes the LDS)
+    std::mutex mu;
+};
+
+namespace
+{
+
+size_t item_bytes(int it) { return it == GSDR_ITEM_CSHORT ? 4 : 8; }
+
+// The reference's host-side phasors, bit for bit (std::cos/std::sin/std::exp on
+// float, cpu_multicorrelator_real_codes.cc:114-123), reduced to their angles.
+JobAux host_model(const gsdr_corr_job& j)
+{
+    JobAux a{};
+    const std::complex<float> off(std::cos(j.rem_carr_phase_rad), -std::sin(j.rem_carr_phase_rad));
+    const std::complex<float> inc = std::exp(std::complex<float>(0.0f, -j.carr_phase_step_rad));
+    const std::complex<float> rate = std::exp(std::complex<float>(0.0f, -j.carr_phase_rate_step_rad));
+    a.psi0 = std::atan2((double)off.imag(), (double)off.real());
+    a.theta = std::atan2((double)inc.imag(), (double)inc.real());
+    a.theta_rate = std::atan2((double)rate.imag(), (double)rate.real());
+    a.valid = 1;
+    return a;
+}
+
+int ensure_jobs(gsdr_corr* c, int njobs)
+{
+    if (njobs <= c->jobs_cap) return GSDR_OK;
+    int cap = c->jobs_cap ? c->jobs_cap : 64;
+    while (cap < njobs) cap *= 2;
+    if (c->d_jobs) GSDR_HIP(hipFree(c->d_jobs));
+    if (c->d_aux) GSDR_HIP(hipFree(c->d_aux));
+    c->d_jobs = nullptr;
+    c->d_aux = nullptr;
+    c->jobs_cap = 0;
+    GSDR_HIP(hipMalloc(&c->d_jobs, cap * sizeof(gsdr_corr_job)));
+    GSDR_HIP(hipMalloc(&c->d_aux, cap * sizeof(JobAux)));
+    c->jobs_cap = cap;
+    return GSDR_OK;
+}
+
+int launch(gsdr_corr* c, const gsdr_corr_job* d_jobs, const JobAux* d_aux, int njobs, const void* iq, int item_type,
+    int64_t iq_items, float* out, hipStream_t s)
+{
+    if (njobs == 0) return GSDR_OK;
+    const size_t lds = (size_t)c->max_code_floats * sizeof(float);
+    if (item_type == GSDR_ITEM_GR_COMPLEX)
+        hipLaunchKernelGGL((corr_kernel<GSDR_ITEM_GR_COMPLEX>), dim3(njobs), dim3(kCorrThreads), lds, s, d_jobs, d_aux,
+            c->d_chans, iq, iq_items, (float2*)out, c->max_taps, c->assoc);
+    else
+        hipLaunchKernelGGL((corr_kernel<GSDR_ITEM_CSHORT>), dim3(njobs), dim3(kCorrThreads), lds, s, d_jobs, d_aux,
+            c->d_chans, iq, iq_items, (float2*)out, c->max_taps, c->assoc);
+    GSDR_HIP(hipGetLastError());
+    return GSDR_OK;
+}
+
+int set_code_common(gsdr_corr* c, int ch, int L, const float* code, const float* shifts, int ntaps, int cplx)
+{
+    GSDR_REQUIRE(c && code && shifts, GSDR_E_ARG, "set_local_code_and_taps: null argument");
+    GSDR_REQUIRE(ch >= 0 && ch < c->max_channels, GSDR_E_ARG, "set_local_code_and_taps: channel %d outside [0,%d)", ch,
+        c->max_channels);
+    GSDR_REQUIRE(ntaps >= 1 && ntaps <= c->max_taps, GSDR_E_ARG, "set_local_code_and_taps: %d taps outside [1,%d]", ntaps,
+        c->max_taps);
+    const int floats = cplx ? 2 * L : L;
+    GSDR_REQUIRE(L >= 1 && floats <= 2 * kMaxCodeSamples, GSDR_E_UNSUPPORTED,
+        "set_local_code_and_taps: code length %d outside the LDS-staged capacity", L);
+    std::lock_guard<std::mutex> lk(c->mu);
+    gsdr::DeviceGuard g(c->device);
+    if (c->code_caps[ch] < floats)
+        {
+            if (c->code_bufs[ch]) GSDR_HIP(hipFree(c->code_bufs[ch]));
+            c->code_bufs[ch] = nullptr;
+            c->code_caps[ch] = 0;
+            GSDR_HIP(hipMalloc(&c->code_bufs[ch], floats * sizeof(float)));
+            c->code_caps[ch] = floats;
+        }
+    GSDR_HIP(hipMemcpyAsync(c->code_bufs[ch], code, floats * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    ChanDev& d = c->chans[ch];
+    d.code = c->code_bufs[ch];
+    d.L = L;
+    d.ntaps = ntaps;
+    d.cplx = cplx;
+    for (int k = 0; k < kMaxTaps; ++k) d.shifts[k] = k < ntaps ? shifts[k] : 0.0f;
+    if (floats > c->max_code_floats) c->max_code_floats = floats;
+    GSDR_HIP(hipMemcpyAsync(c->d_chans + ch, &d, sizeof(ChanDev), hipMemcpyHostToDevice, c->stream));
+    GSDR_HIP(hipStreamSynchronize(c->stream));
+    return GSDR_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gsdr_corr_create(int device, int max_channels, int max_len, int max_taps, gsdr_corr** out)
+{
+    GSDR_REQUIRE(out, GSDR_E_ARG, "gsdr_corr_create: null argument");
+    *out = nullptr;
+    GSDR_REQUIRE(max_channels > 0 && max_len > 0, GSDR_E_ARG, "gsdr_corr_create: capacities must be > 0");
+    GSDR_REQUIRE(max_taps >= 1 && max_taps <= kMaxTaps, GSDR_E_UNSUPPORTED, "gsdr_corr_create: max_taps %d outside [1,%d]",
+        max_taps, kMaxTaps);
+    int ndev = 0;
+    GSDR_HIP(hipGetDeviceCount(&ndev));
+    GSDR_REQUIRE(device >= 0 && device < ndev, GSDR_E_ARG, "gsdr_corr_create: device %d of %d", device, ndev);
+    gsdr::DeviceGuard g(device);
+    gsdr_corr* c = new (std::nothrow) gsdr_corr();
+    GSDR_REQUIRE(c, GSDR_E_ALLOC, "gsdr_corr_create: out of host memory");
+    c->device = device;
+    c->max_channels = max_channels;
+    c->max_len = max_len;
+    c->max_taps = max_taps;
+    c->chans.assign(max_channels, ChanDev{});
+    for (auto& d : c->chans) d.ntaps = 0;
+    c->code_bufs.assign(max_channels, nullptr);
+    c->code_caps.assign(max_channels, 0);
+    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMalloc(&c->d_chans, max_channels * sizeof(ChanDev));
+    if (e == hipSuccess) e = hipMemset(c->d_chans, 0, max_channels * sizeof(ChanDev));
+    if (e == hipSuccess) e = hipMalloc(&c->d_iq, (size_t)max_len * 8);
+    if (e == hipSuccess) e = hipMalloc(&c->d_out, (size_t)max_taps * sizeof(float2));
+    if (e != hipSuccess)
+        {
+            gsdr::set_error("gsdr_corr_create: %s", hipGetErrorString(e));
+            gsdr_corr_destroy(c);
+            return GSDR_E_ALLOC;
+        }
+    const size_t lds = (size_t)2 * kMaxCodeSamples * sizeof(float);
+    GSDR_HIP(hipFuncSetAttribute((const void*)corr_kernel<GSDR_ITEM_GR_COMPLEX>,
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    GSDR_HIP(hipFuncSetAttribute((const void*)corr_kernel<GSDR_ITEM_CSHORT>,
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    if (ensure_jobs(c, 64) != GSDR_OK)
+        {
+            gsdr_corr_destroy(c);
+            return GSDR_E_ALLOC;
+        }
+    *out = c;
+    return GSDR_OK;
+}
+
+void gsdr_corr_destroy(gsdr_corr* c)
+{
+    if (!c) return;
+    gsdr::DeviceGuard g(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (float* p : c->code_bufs)
+        if (p) (void)hipFree(p);
+    void* bufs[] = {c->d_chans, c->d_jobs, c->d_aux, c->d_iq, c->d_out};
+    for (void* p : bufs)
+        if (p) (void)hipFree(p);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int gsdr_corr_set_local_code_and_taps(gsdr_corr* c, int ch, int L, const float* code, const float* shifts, int ntaps)
+{
+    return set_code_common(c, ch, L, code, shifts, ntaps, 0);
+}
+
+int gsdr_corr_set_local_code_and_taps_complex(gsdr_corr* c, int ch, int L, const float* code, const float* shifts,
+    int ntaps)
+{
+    return set_code_common(c, ch, L, code, shifts, ntaps, 1);
+}
+
+int gsdr_corr_set_high_dynamics_resampler(gsdr_corr* c, int ch, int enable)
+{
+    GSDR_REQUIRE(c, GSDR_E_ARG, "set_high_dynamics_resampler: null handle");
+    GSDR_REQUIRE(ch >= 0 && ch < c->max_channels, GSDR_E_ARG, "set_high_dynamics_resampler: channel %d", ch);
+    std::lock_guard<std::mutex> lk(c->mu);
+    gsdr::DeviceGuard g(c->device);
+    c->chans[ch].high_dyn = enable ? 1 : 0;
+    GSDR_HIP(hipMemcpyAsync(c->d_chans + ch, &c->chans[ch], sizeof(ChanDev), hipMemcpyHostToDevice, c->stream));
+    GSDR_HIP(hipStreamSynchronize(c->stream));
+    return GSDR_OK;
+}
+
+int gsdr_corr_set_resampler_assoc(gsdr_corr* c, int assoc)
+{
+    GSDR_REQUIRE(c, GSDR_E_ARG, "set_resampler_assoc: null handle");
+    GSDR_REQUIRE(assoc == GSDR_ASSOC_GENERIC || assoc == GSDR_ASSOC_AVX, GSDR_E_ARG, "set_resampler_assoc: %d", assoc);
+    c->assoc = assoc;
+    return GSDR_OK;
+}
+
+int gsdr_corr_run_batch(gsdr_corr* c, const gsdr_corr_job* jobs, int njobs, const void* iq_dev, int item_type,
+    int64_t iq_items, float* out_dev, void* stream)
+{
+    GSDR_REQUIRE(c && (jobs || njobs == 0) && iq_dev && out_dev, GSDR_E_ARG, "gsdr_corr_run_batch: null argument");
+    GSDR_REQUIRE(item_type == GSDR_ITEM_GR_COMPLEX || item_type == GSDR_ITEM_CSHORT, GSDR_E_ARG,
+        "gsdr_corr_run_batch: item type %d", item_type);
+    std::lock_guard<std::mutex> lk(c->mu);
+    gsdr::DeviceGuard g(c->device);
+    c->h_aux.resize(njobs);
+    for (int j = 0; j < njobs; ++j)
+        {
+            const gsdr_corr_job& jb = jobs[j];
+            GSDR_REQUIRE(jb.channel >= 0 && jb.channel < c->max_channels && c->chans[jb.channel].ntaps > 0, GSDR_E_STATE,
+                "gsdr_corr_run_batch: job %d uses channel %d without a local code", j, jb.channel);
+            GSDR_REQUIRE(jb.n_samples >= 0 && jb.n_samples <= c->max_len, GSDR_E_ARG,
+                "gsdr_corr_run_batch: job %d length %d outside [0,%d]", j, jb.n_samples, c->max_len);
+            c->h_aux[j] = host_model(jb);
+        }
+    int rc = ensure_jobs(c, njobs);
+    if (rc != GSDR_OK) return rc;
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    GSDR_HIP(hipMemcpyAsync(c->d_jobs, jobs, njobs * sizeof(gsdr_corr_job), hipMemcpyHostToDevice, s));
+    GSDR_HIP(hipMemcpyAsync(c->d_aux, c->h_aux.data(), njobs * sizeof(JobAux), hipMemcpyHostToDevice, s));
+    return launch(c, c->d_jobs, c->d_aux, njobs, iq_dev, item_type, iq_items, out_dev, s);
+}
+
+int gsdr_corr_run_batch_device(gsdr_corr* c, const gsdr_corr_job* jobs_dev, int njobs, const void* iq_dev,
+    int item_type, int64_t iq_items, float* out_dev, void* stream)
+{
+    GSDR_REQUIRE(c && (jobs_dev || njobs == 0) && iq_dev && out_dev, GSDR_E_ARG,
+        "gsdr_corr_run_batch_device: null argument");
+    gsdr::DeviceGuard g(c->device);
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    return launch(c, jobs_dev, nullptr, njobs, iq_dev, item_type, iq_items, out_dev, s);
+}
+
+int gsdr_corr_run(gsdr_corr* c, int ch, const void* sig_in_host, int item_type, float rem_carr, float carr_step,
+    float carr_rate, float rem_code, float code_step, float code_rate, int n, float* out_host)
+{
+    GSDR_REQUIRE(c && sig_in_host && out_host, GSDR_E_ARG, "gsdr_corr_run: null argument");
+    GSDR_REQUIRE(n >= 0 && n <= c->max_len, GSDR_E_ARG, "gsdr_corr_run: length %d outside [0,%d]", n, c->max_len);
+    GSDR_REQUIRE(ch >= 0 && ch < c->max_channels && c->chans[ch].ntaps > 0, GSDR_E_STATE,
+        "gsdr_corr_run: channel %d has no local code", ch);
+    GSDR_REQUIRE(item_type == GSDR_ITEM_GR_COMPLEX || item_type == GSDR_ITEM_CSHORT, GSDR_E_ARG,
+        "gsdr_corr_run: item type %d", item_type);
+    gsdr_corr_job jb{};
+    jb.channel = ch;
+    jb.n_samples = n;
+    jb.sample_offset = 0;
+    jb.rem_carr_phase_rad = rem_carr;
+    jb.carr_phase_step_rad = carr_step;
+    jb.carr_phase_rate_step_rad = carr_rate;
+    jb.rem_code_phase_chips = rem_code;
+    jb.code_phase_step_chips = code_step;
+    jb.code_phase_rate_step_chips = code_rate;
+    {
+        std::lock_guard<std::mutex> lk(c->mu);
+        gsdr::DeviceGuard g(c->device);
+        GSDR_HIP(hipMemcpyAsync(c->d_iq, sig_in_host, (size_t)n * item_bytes(item_type), hipMemcpyHostToDevice,
+            c->stream));
+    }
+    int rc = gsdr_corr_run_batch(c, &jb, 1, c->d_iq, item_type, n, (float*)c->d_out, c->stream);
+    if (rc != GSDR_OK) return rc;
+    std::lock_guard<std::mutex> lk(c->mu);
+    gsdr::DeviceGuard g(c->device);
+    GSDR_HIP(hipMemcpyAsync(out_host, c->d_out, (size_t)c->chans[ch].ntaps * sizeof(float2), hipMemcpyDeviceToHost,
+        c->stream));
+    GSDR_HIP(hipStreamSynchronize(c->stream));
+    return GSDR_OK;
+}
+
+int gsdr_corr_dump_indices(gsdr_corr* c, int ch, float rem, float step, int n, int32_t* idx_host)
+{
+    GSDR_REQUIRE(c && idx_host, GSDR_E_ARG, "gsdr_corr_dump_indices: null argument");
+    GSDR_REQUIRE(ch >= 0 && ch < c->max_channels && c->chans[ch].ntaps > 0, GSDR_E_STATE,
+        "gsdr_corr_dump_indices: channel %d has no local code", ch);
+    GSDR_REQUIRE(n > 0, GSDR_E_ARG, "gsdr_corr_dump_indices: n must be > 0");
+    std::lock_guard<std::mutex> lk(c->mu);
+    gsdr::DeviceGuard g(c->device);
+    const int K = c->chans[ch].ntaps;
+    int32_t* d_idx = nullptr;
+    GSDR_HIP(hipMalloc(&d_idx, (size_t)K * n * sizeof(int32_t)));
+    hipLaunchKernelGGL(corr_index_kernel, dim3((n + 255) / 256), dim3(256), 0, c->stream, c->d_chans, ch, rem, step, n,
+        c->assoc, d_idx);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(idx_host, d_idx, (size_t)K * n * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    (void)hipFree(d_idx);
+    GSDR_HIP(e);
+    return GSDR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,60 @@
+// Internal helpers shared by the acquisition and tracking translation units.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <string>
+
+#include "gsdr.h"
+
+namespace gsdr
+{
+
+void set_error(const char* fmt, ...);
+
+// Map a HIP status to GSDR_E_DEVICE with a message naming the call site.
+#define GSDR_HIP(call)                                                                              \
+    do                                                                                              \
+        {                                                                                           \
+            hipError_t e_ = (call);                                                                 \
+            if (e_ != hipSuccess)                                                                   \
+                {                                                                                   \
+                    ::gsdr::set_error("%s:%d %s: %s", __FILE__, __LINE__, #call, hipGetErrorString(e_)); \
+                    return GSDR_E_DEVICE;                                                           \
+                }                                                                                   \
+        }                                                                                           \
+    while (0)
+
+#define GSDR_REQUIRE(cond, code, ...)                \
+    do                                               \
+        {                                            \
+            if (!(cond))                             \
+                {                                    \
+                    ::gsdr::set_error(__VA_ARGS__);  \
+                    return (code);                   \
+                }                                    \
+        }                                            \
+    while (0)
+
+// RAII device switch: the ABI is called from arbitrary host threads.
+struct DeviceGuard
+{
+    int prev{-1};
+    explicit DeviceGuard(int dev)
+    {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard()
+    {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+// Inverse regularised lower incomplete gamma for integer shape a:
+// returns x with P(a, x) = p.  (Boost gamma_p_inv, used by calculate_threshold.)
+double gamma_p_inv_int(int a, double p);
+
+}  // namespace gsdr

@@ -1,0 +1,332 @@
+"""Python front-end of libgsdr.so (the MI355X acquisition + tracking correlator
+engine).  Thin ctypes layer over the C ABI declared in include/gsdr.h; used by the
+tests, bench.py and __graft_entry__.  It has no compute of its own and no CPU
+fallback: if the HIP library cannot be loaded, every entry point raises.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.environ.get("GSDR_LIB", os.path.join(_PKG, "build", "libgsdr.so"))
+
+GSDR_OK = 0
+GSDR_E_ARG = -1
+GSDR_E_DEVICE = -2
+GSDR_E_ALLOC = -3
+GSDR_E_STATE = -4
+GSDR_E_UNSUPPORTED = -5
+
+ITEM_GR_COMPLEX = 0
+ITEM_CSHORT = 1
+ASSOC_GENERIC = 0
+ASSOC_AVX = 1
+
+# Every symbol include/gsdr.h declares (checked by tests/test_abi.py).
+EXPORTED = [
+    "gsdr_last_error", "gsdr_abi_version", "gsdr_device_count",
+    "gsdr_acq_create", "gsdr_acq_destroy", "gsdr_acq_get_dims", "gsdr_acq_set_local_codes",
+    "gsdr_acq_set_doppler", "gsdr_acq_set_threshold", "gsdr_acq_get_threshold", "gsdr_acq_run",
+    "gsdr_acq_run_device", "gsdr_acq_dump_grid", "gsdr_acq_dump_spectra",
+    "gsdr_corr_create", "gsdr_corr_destroy", "gsdr_corr_set_local_code_and_taps",
+    "gsdr_corr_set_local_code_and_taps_complex", "gsdr_corr_set_high_dynamics_resampler",
+    "gsdr_corr_set_resampler_assoc", "gsdr_corr_run", "gsdr_corr_run_batch", "gsdr_corr_run_batch_device",
+    "gsdr_corr_dump_indices",
+]
+
+
+class GsdrError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("gsdr error %d: %s" % (code, msg))
+        self.code = code
+
+
+class AcqConf(ctypes.Structure):
+    _fields_ = [
+        ("fs_in", ctypes.c_int64),
+        ("consumed_samples", ctypes.c_uint32),
+        ("fft_size", ctypes.c_uint32),
+        ("samples_per_code", ctypes.c_float),
+        ("samples_per_chip", ctypes.c_uint32),
+        ("doppler_max", ctypes.c_int32),
+        ("doppler_step", ctypes.c_uint32),
+        ("doppler_center", ctypes.c_int32),
+        ("doppler_bias", ctypes.c_int32),
+        ("num_doppler_bins", ctypes.c_uint32),
+        ("pfa", ctypes.c_float),
+        ("max_dwells", ctypes.c_uint32),
+        ("bit_transition_flag", ctypes.c_int32),
+        ("item_type", ctypes.c_int32),
+        ("max_prns", ctypes.c_uint32),
+        ("max_blocks", ctypes.c_uint32),
+        ("sampled_ms", ctypes.c_uint32),
+        ("ms_per_code", ctypes.c_uint32),
+    ]
+
+
+class AcqResult(ctypes.Structure):
+    _fields_ = [
+        ("prn", ctypes.c_uint32),
+        ("doppler_index", ctypes.c_uint32),
+        ("code_phase", ctypes.c_uint32),
+        ("doppler_hz", ctypes.c_int32),
+        ("peak", ctypes.c_float),
+        ("input_power", ctypes.c_float),
+        ("second_peak", ctypes.c_float),
+        ("test_statistic", ctypes.c_float),
+        ("acq_delay_samples", ctypes.c_double),
+        ("samplestamp", ctypes.c_uint64),
+        ("positive", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+    ]
+
+
+ACQ_RESULT_DTYPE = np.dtype([
+    ("prn", np.uint32), ("doppler_index", np.uint32), ("code_phase", np.uint32), ("doppler_hz", np.int32),
+    ("peak", np.float32), ("input_power", np.float32), ("second_peak", np.float32),
+    ("test_statistic", np.float32), ("acq_delay_samples", np.float64), ("samplestamp", np.uint64),
+    ("positive", np.int32), ("reserved", np.int32)])
+assert ACQ_RESULT_DTYPE.itemsize == ctypes.sizeof(AcqResult)
+
+
+class CorrJob(ctypes.Structure):
+    _fields_ = [
+        ("channel", ctypes.c_int32),
+        ("n_samples", ctypes.c_int32),
+        ("sample_offset", ctypes.c_int64),
+        ("rem_carr_phase_rad", ctypes.c_float),
+        ("carr_phase_step_rad", ctypes.c_float),
+        ("carr_phase_rate_step_rad", ctypes.c_float),
+        ("rem_code_phase_chips", ctypes.c_float),
+        ("code_phase_step_chips", ctypes.c_float),
+        ("code_phase_rate_step_chips", ctypes.c_float),
+    ]
+
+
+CORR_JOB_DTYPE = np.dtype([
+    ("channel", np.int32), ("n_samples", np.int32), ("sample_offset", np.int64),
+    ("rem_carr_phase_rad", np.float32), ("carr_phase_step_rad", np.float32),
+    ("carr_phase_rate_step_rad", np.float32), ("rem_code_phase_chips", np.float32),
+    ("code_phase_step_chips", np.float32), ("code_phase_rate_step_chips", np.float32)])
+assert CORR_JOB_DTYPE.itemsize == ctypes.sizeof(CorrJob)
+
+_lib = None
+
+
+def load():
+    """Load libgsdr.so (raises OSError if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise OSError("libgsdr.so not built: %s (run __graft_entry__.build())" % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    P, I, U32, U64, I64, F = (ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int64,
+                              ctypes.c_float)
+    L.gsdr_last_error.restype = ctypes.c_char_p
+    L.gsdr_abi_version.restype = I
+    L.gsdr_device_count.argtypes = [P]
+    L.gsdr_acq_create.argtypes = [I, ctypes.POINTER(AcqConf), P]
+    L.gsdr_acq_destroy.argtypes = [P]
+    L.gsdr_acq_destroy.restype = None
+    L.gsdr_acq_get_dims.argtypes = [P, P, P]
+    L.gsdr_acq_set_local_codes.argtypes = [P, P, P, U32]
+    L.gsdr_acq_set_doppler.argtypes = [P, ctypes.c_int32, U32, ctypes.c_int32]
+    L.gsdr_acq_set_threshold.argtypes = [P, F]
+    L.gsdr_acq_get_threshold.argtypes = [P, P]
+    L.gsdr_acq_run.argtypes = [P, P, U32, U64, P]
+    L.gsdr_acq_run_device.argtypes = [P, P, U32, U64, U64, P, P]
+    L.gsdr_acq_dump_grid.argtypes = [P, P, U32, P]
+    L.gsdr_acq_dump_spectra.argtypes = [P, P, P]
+    L.gsdr_corr_create.argtypes = [I, I, I, I, P]
+    L.gsdr_corr_destroy.argtypes = [P]
+    L.gsdr_corr_destroy.restype = None
+    L.gsdr_corr_set_local_code_and_taps.argtypes = [P, I, I, P, P, I]
+    L.gsdr_corr_set_local_code_and_taps_complex.argtypes = [P, I, I, P, P, I]
+    L.gsdr_corr_set_high_dynamics_resampler.argtypes = [P, I, I]
+    L.gsdr_corr_set_resampler_assoc.argtypes = [P, I]
+    L.gsdr_corr_run.argtypes = [P, I, P, I, F, F, F, F, F, F, I, P]
+    L.gsdr_corr_run_batch.argtypes = [P, P, I, P, I, I64, P, P]
+    L.gsdr_corr_run_batch_device.argtypes = [P, P, I, P, I, I64, P, P]
+    L.gsdr_corr_dump_indices.argtypes = [P, I, F, F, I, P]
+    _lib = L
+    return L
+
+
+def _check(rc):
+    if rc != GSDR_OK:
+        raise GsdrError(rc, load().gsdr_last_error().decode(errors="replace"))
+
+
+def _ptr(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def device_count():
+    n = ctypes.c_int(0)
+    _check(load().gsdr_device_count(ctypes.byref(n)))
+    return n.value
+
+
+class Acquisition:
+    """Batched PCPS acquisition (pcps_acquisition equivalent) on one GPU."""
+
+    def __init__(self, fs_in, consumed_samples, doppler_max, doppler_step, pfa=0.0, max_prns=32, max_blocks=1,
+                 samples_per_code=None, samples_per_chip=None, num_doppler_bins=0, doppler_center=0,
+                 doppler_bias=0, item_type=ITEM_GR_COMPLEX, fft_size=0, sampled_ms=1, ms_per_code=1,
+                 chip_rate=1023000.0, device=0):
+        L = load()
+        c = AcqConf()
+        c.fs_in = int(fs_in)
+        c.consumed_samples = int(consumed_samples)
+        c.fft_size = int(fft_size)
+        spms = np.float32(np.float32(fs_in) * np.float32(0.001))
+        c.samples_per_code = float(samples_per_code if samples_per_code is not None else spms * ms_per_code)
+        c.samples_per_chip = int(samples_per_chip if samples_per_chip is not None
+                                 else int(np.ceil(float(np.float32(fs_in)) / chip_rate)))
+        c.doppler_max = int(doppler_max)
+        c.doppler_step = int(doppler_step)
+        c.doppler_center = int(doppler_center)
+        c.doppler_bias = int(doppler_bias)
+        c.num_doppler_bins = int(num_doppler_bins)
+        c.pfa = float(pfa)
+        c.max_dwells = 1
+        c.bit_transition_flag = 0
+        c.item_type = int(item_type)
+        c.max_prns = int(max_prns)
+        c.max_blocks = int(max_blocks)
+        c.sampled_ms = int(sampled_ms)
+        c.ms_per_code = int(ms_per_code)
+        self.conf = c
+        self._h = ctypes.c_void_p()
+        _check(L.gsdr_acq_create(int(device), ctypes.byref(c), ctypes.byref(self._h)))
+        D, N = ctypes.c_uint32(), ctypes.c_uint32()
+        _check(L.gsdr_acq_get_dims(self._h, ctypes.byref(D), ctypes.byref(N)))
+        self.num_doppler_bins, self.fft_size = D.value, N.value
+        self.nprn = 0
+        self.item_type = item_type
+
+    def close(self):
+        if self._h:
+            load().gsdr_acq_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_local_codes(self, codes, prns):
+        codes = np.ascontiguousarray(codes, np.complex64)
+        prns = np.ascontiguousarray(prns, np.uint32)
+        assert codes.ndim == 2 and codes.shape[0] == len(prns)
+        _check(load().gsdr_acq_set_local_codes(self._h, _ptr(codes), _ptr(prns), len(prns)))
+        self.nprn = len(prns)
+
+    def set_doppler(self, doppler_max, doppler_step, doppler_center=0):
+        _check(load().gsdr_acq_set_doppler(self._h, int(doppler_max), int(doppler_step), int(doppler_center)))
+
+    def set_threshold(self, t):
+        _check(load().gsdr_acq_set_threshold(self._h, float(t)))
+
+    @property
+    def threshold(self):
+        t = ctypes.c_float()
+        _check(load().gsdr_acq_get_threshold(self._h, ctypes.byref(t)))
+        return t.value
+
+    def _items(self, iq):
+        if self.item_type == ITEM_CSHORT:
+            return np.ascontiguousarray(iq, np.int16)
+        return np.ascontiguousarray(iq, np.complex64)
+
+    def run(self, iq, nblocks=1, stamp0=0):
+        """Synchronous drop-in: host IQ of nblocks*consumed items -> structured array [nblocks, nprn]."""
+        iq = self._items(iq)
+        out = np.zeros(nblocks * self.nprn, ACQ_RESULT_DTYPE)
+        _check(load().gsdr_acq_run(self._h, _ptr(iq), int(nblocks), int(stamp0), _ptr(out)))
+        return out.reshape(nblocks, self.nprn)
+
+    def run_device(self, iq_dev_ptr, nblocks, stride_items, stamp0, out_dev_ptr, stream_ptr=0):
+        _check(load().gsdr_acq_run_device(self._h, ctypes.c_void_p(iq_dev_ptr), int(nblocks), int(stride_items),
+                                          int(stamp0), ctypes.c_void_p(out_dev_ptr), ctypes.c_void_p(stream_ptr)))
+
+    def dump_grid(self, iq, prn_slot):
+        iq = self._items(iq)
+        g = np.zeros((self.num_doppler_bins, self.fft_size), np.float32)
+        _check(load().gsdr_acq_dump_grid(self._h, _ptr(iq), int(prn_slot), _ptr(g)))
+        return g
+
+    def dump_spectra(self, iq):
+        iq = self._items(iq)
+        X = np.zeros((self.num_doppler_bins, self.fft_size), np.complex64)
+        _check(load().gsdr_acq_dump_spectra(self._h, _ptr(iq), _ptr(X)))
+        return X
+
+
+class Correlator:
+    """Batched tracking multicorrelator (Cpu_Multicorrelator_Real_Codes equivalent)."""
+
+    def __init__(self, max_channels, max_len, max_taps=8, device=0):
+        self._h = ctypes.c_void_p()
+        _check(load().gsdr_corr_create(int(device), int(max_channels), int(max_len), int(max_taps),
+                                       ctypes.byref(self._h)))
+        self.max_taps = max_taps
+        self.ntaps = {}
+
+    def close(self):
+        if self._h:
+            load().gsdr_corr_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_local_code_and_taps(self, channel, code, shifts):
+        if np.iscomplexobj(code):
+            code = np.ascontiguousarray(code, np.complex64)
+            shifts = np.ascontiguousarray(shifts, np.float32)
+            _check(load().gsdr_corr_set_local_code_and_taps_complex(self._h, channel, len(code), _ptr(code),
+                                                                    _ptr(shifts), len(shifts)))
+        else:
+            code = np.ascontiguousarray(code, np.float32)
+            shifts = np.ascontiguousarray(shifts, np.float32)
+            _check(load().gsdr_corr_set_local_code_and_taps(self._h, channel, len(code), _ptr(code), _ptr(shifts),
+                                                            len(shifts)))
+        self.ntaps[channel] = len(shifts)
+
+    def set_high_dynamics_resampler(self, channel, enable):
+        _check(load().gsdr_corr_set_high_dynamics_resampler(self._h, channel, int(bool(enable))))
+
+    def set_resampler_assoc(self, assoc):
+        _check(load().gsdr_corr_set_resampler_assoc(self._h, int(assoc)))
+
+    def run(self, channel, sig, rem_carr, carr_step, rem_code, code_step, n, carr_rate=0.0, code_rate=0.0,
+            item_type=ITEM_GR_COMPLEX):
+        """Carrier_wipeoff_multicorrelator_resampler (7-argument form), synchronous."""
+        sig = np.ascontiguousarray(sig, np.int16 if item_type == ITEM_CSHORT else np.complex64)
+        out = np.zeros(self.ntaps[channel], np.complex64)
+        _check(load().gsdr_corr_run(self._h, channel, _ptr(sig), item_type, rem_carr, carr_step, carr_rate, rem_code,
+                                    code_step, code_rate, int(n), _ptr(out)))
+        return out
+
+    def run_batch(self, jobs, iq_dev_ptr, iq_items, out_dev_ptr, item_type=ITEM_GR_COMPLEX, stream_ptr=0):
+        jobs = np.ascontiguousarray(jobs, CORR_JOB_DTYPE)
+        _check(load().gsdr_corr_run_batch(self._h, _ptr(jobs), len(jobs), ctypes.c_void_p(iq_dev_ptr), item_type,
+                                          int(iq_items), ctypes.c_void_p(out_dev_ptr), ctypes.c_void_p(stream_ptr)))
+
+    def run_batch_device(self, jobs_dev_ptr, njobs, iq_dev_ptr, iq_items, out_dev_ptr, item_type=ITEM_GR_COMPLEX,
+                         stream_ptr=0):
+        _check(load().gsdr_corr_run_batch_device(self._h, ctypes.c_void_p(jobs_dev_ptr), int(njobs),
+                                                 ctypes.c_void_p(iq_dev_ptr), item_type, int(iq_items),
+                                                 ctypes.c_void_p(out_dev_ptr), ctypes.c_void_p(stream_ptr)))
+
+    def dump_indices(self, channel, rem_code, code_step, n):
+        out = np.zeros((self.ntaps[channel], n), np.int32)
+        _check(load().gsdr_corr_dump_indices(self._h, channel, rem_code, code_step, int(n), _ptr(out)))
+        return out

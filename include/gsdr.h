@@ -1,0 +1,219 @@
+/*
+ * gsdr.h — C ABI of the MI355X-native GNSS acquisition + tracking correlator engine.
+ *
+ * This is the drop-in boundary for GNSS-SDR's two data-parallel hot paths:
+ *
+ *  - PCPS acquisition: replaces the compute of pcps_acquisition
+ *    (src/algorithms/acquisition/gnuradio_blocks/pcps_acquisition.cc:176-209
+ *    set_local_code, :233-305 Doppler grid, :511-612 statistics, :615-882
+ *    acquisition_core, :894-909 calculate_threshold), batched over PRNs and over
+ *    consecutive input blocks.
+ *
+ *  - Tracking multicorrelator: replaces Cpu_Multicorrelator_Real_Codes
+ *    (src/algorithms/tracking/libs/cpu_multicorrelator_real_codes.h:37-61, .cc:36-167)
+ *    and Cpu_Multicorrelator (src/algorithms/tracking/libs/cpu_multicorrelator.h:37-58),
+ *    i.e. the VOLK-GNSSSDR resampler + rotator-dot-product pair, fused into one
+ *    HIP launch batched over channels.
+ *
+ * Conventions
+ *  - Every function returns int: GSDR_OK (0) or a negative GSDR_E* code.  The
+ *    thread-local message of the last failure is gsdr_last_error().  No C++
+ *    exception crosses this boundary.
+ *  - Plain pointers and sizes only.  "host" pointers are ordinary CPU memory;
+ *    "dev" pointers are HIP device memory on the handle's device; "stream" is a
+ *    hipStream_t passed as void* (NULL = the handle's own stream).
+ *  - Complex samples are interleaved float pairs (gr_complex / std::complex<float>),
+ *    cshort samples are interleaved int16 pairs (lv_16sc_t).
+ *  - A handle is owned by one caller at a time; distinct handles may be used
+ *    concurrently from different threads (GNU Radio thread-per-block model).
+ */
+#ifndef GSDR_H
+#define GSDR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GSDR_ABI_VERSION 1
+
+#define GSDR_OK 0
+#define GSDR_E_ARG (-1)         /* invalid argument (≙ std::invalid_argument in Acq_Conf) */
+#define GSDR_E_DEVICE (-2)      /* HIP runtime / device error */
+#define GSDR_E_ALLOC (-3)       /* device or host allocation failed */
+#define GSDR_E_STATE (-4)       /* call not valid in the handle's current state */
+#define GSDR_E_UNSUPPORTED (-5) /* configuration outside what the engine implements */
+
+/* Sample item types (Acq_Conf::item_type, acq_conf.h:42; item_type_size). */
+#define GSDR_ITEM_GR_COMPLEX 0 /* complex<float>, 8 bytes */
+#define GSDR_ITEM_CSHORT 1     /* complex<int16>, 4 bytes */
+
+/* Float association used for the resampler code-phase index:
+ * GSDR_ASSOC_GENERIC: floor((step*n + shift) - rem)   KERN/32f_xn_resampler_32f_xn.h:73
+ * GSDR_ASSOC_AVX:     floor(step*n + (shift - rem))   KERN/32f_xn_resampler_32f_xn.h:384-390
+ * The x86 VOLK dispatcher selects the AVX protokernel, so that is the default. */
+#define GSDR_ASSOC_GENERIC 0
+#define GSDR_ASSOC_AVX 1
+
+const char* gsdr_last_error(void);
+int gsdr_abi_version(void);
+/* Number of HIP devices visible to this process. */
+int gsdr_device_count(int* count);
+
+/* ======================================================================== */
+/* Acquisition — PCPS (pcps_acquisition)                                     */
+/* ======================================================================== */
+
+typedef struct gsdr_acq gsdr_acq;
+
+/* Mirrors the Acq_Conf fields (acq_conf.h:33-82) that drive acquisition_core. */
+typedef struct gsdr_acq_conf
+{
+    int64_t fs_in;                /* sampling rate after optional resampling [sps]   (resampled_fs) */
+    uint32_t consumed_samples;    /* samples per block = sampled_ms*samples_per_ms    (pcps_acquisition.cc:71) */
+    uint32_t fft_size;            /* 0 -> derived as in pcps_acquisition.cc:85-92 */
+    float samples_per_code;       /* Acq_Conf::samples_per_code */
+    uint32_t samples_per_chip;    /* Acq_Conf::samples_per_chip (peak-ratio exclusion window) */
+    int32_t doppler_max;          /* [Hz] */
+    uint32_t doppler_step;        /* [Hz] */
+    int32_t doppler_center;       /* [Hz] */
+    int32_t doppler_bias;         /* [Hz] FDMA bias (is_fdma, pcps_acquisition.cc:212-230) */
+    uint32_t num_doppler_bins;    /* 0 -> ceil(2*doppler_max/doppler_step)            (pcps_acquisition.cc:264) */
+    float pfa;                    /* > 0: CFAR max/input-power statistic; == 0: first/second peak */
+    uint32_t max_dwells;          /* only 1 is implemented in this version */
+    int32_t bit_transition_flag;  /* only 0 is implemented in this version */
+    int32_t item_type;            /* GSDR_ITEM_* */
+    uint32_t max_prns;            /* capacity: PRNs per batch */
+    uint32_t max_blocks;          /* capacity: blocks per call */
+    uint32_t sampled_ms;          /* Acq_Conf::sampled_ms */
+    uint32_t ms_per_code;         /* Acq_Conf::ms_per_code */
+} gsdr_acq_conf;
+
+/* One acquisition outcome per (block, PRN): the Gnss_Synchro fields written by
+ * acquisition_core (pcps_acquisition.cc:697-713) plus the statistic inputs. */
+typedef struct gsdr_acq_result
+{
+    uint32_t prn;
+    uint32_t doppler_index;   /* d* */
+    uint32_t code_phase;      /* indext: n* in the (effective) FFT row */
+    int32_t doppler_hz;       /* Acq_doppler_hz */
+    float peak;               /* grid maximum |R|^2 */
+    float input_power;        /* CFAR: mean |R|^2 of row (d*+D/2)%D / 2 / dwells; 0 for peak-ratio */
+    float second_peak;        /* peak-ratio: second peak outside +-1 chip; 0 for CFAR */
+    float test_statistic;     /* d_test_statistics */
+    double acq_delay_samples; /* Acq_delay_samples = fmod(indext, samples_per_code) */
+    uint64_t samplestamp;     /* Acq_samplestamp_samples */
+    int32_t positive;         /* test_statistic > threshold */
+    int32_t reserved;
+} gsdr_acq_result;
+
+int gsdr_acq_create(int device, const gsdr_acq_conf* conf, gsdr_acq** out);
+void gsdr_acq_destroy(gsdr_acq* acq);
+
+/* Doppler bins D actually used, and the FFT size. */
+int gsdr_acq_get_dims(const gsdr_acq* acq, uint32_t* num_doppler_bins, uint32_t* fft_size);
+
+/* set_local_code for a batch of PRNs (pcps_acquisition.cc:176-209): codes is
+ * nprn rows of consumed_samples complex<float> (host); the engine places each in
+ * the FFT buffer, transforms and conjugates on the device.  prn[] are the PRN ids
+ * reported back in gsdr_acq_result. */
+int gsdr_acq_set_local_codes(gsdr_acq* acq, const float* codes, const uint32_t* prn, uint32_t nprn);
+
+/* Doppler setters (AcquisitionInterface, acquisition_interface.h:56-59).  They
+ * rebuild the Doppler wipe-off grid on the device. */
+int gsdr_acq_set_doppler(gsdr_acq* acq, int32_t doppler_max, uint32_t doppler_step, int32_t doppler_center);
+
+/* Threshold: set explicitly (set_threshold) or computed from pfa exactly as
+ * calculate_threshold (pcps_acquisition.cc:894-909). */
+int gsdr_acq_set_threshold(gsdr_acq* acq, float threshold);
+int gsdr_acq_get_threshold(const gsdr_acq* acq, float* threshold);
+
+/* Synchronous drop-in: nblocks consecutive blocks of consumed_samples items
+ * (item_type) from host memory; block i has sample stamp stamp0 + i*consumed.
+ * out: nblocks*nprn results, block-major (host). */
+int gsdr_acq_run(gsdr_acq* acq, const void* iq_host, uint32_t nblocks, uint64_t stamp0, gsdr_acq_result* out);
+
+/* Device-resident form: iq_dev holds nblocks blocks, block i starting at item
+ * i*block_stride_items.  Results are written to out_dev (device memory,
+ * nblocks*nprn).  Asynchronous on stream; no host synchronisation. */
+int gsdr_acq_run_device(gsdr_acq* acq, const void* iq_dev, uint32_t nblocks, uint64_t block_stride_items,
+    uint64_t stamp0, gsdr_acq_result* out_dev, void* stream);
+
+/* The reference's acquisition grid dump (pcps_acquisition.cc:408-508): writes the
+ * |R|^2 grid of PRN slot `prn_slot` for one host block into grid_host
+ * (D rows of fft_size floats, Doppler-major).  Synchronous. */
+int gsdr_acq_dump_grid(gsdr_acq* acq, const void* iq_host, uint32_t prn_slot, float* grid_host);
+
+/* Debug/verification: device forward spectrum for one host block,
+ * D rows x fft_size complex<float> (= FFT(x .* w_d)). */
+int gsdr_acq_dump_spectra(gsdr_acq* acq, const void* iq_host, float* spectra_host);
+
+/* ======================================================================== */
+/* Tracking multicorrelator (Cpu_Multicorrelator_Real_Codes / Cpu_Multicorrelator) */
+/* ======================================================================== */
+
+typedef struct gsdr_corr gsdr_corr;
+
+/* One correlation request: the 6 NCO parameters of
+ * Carrier_wipeoff_multicorrelator_resampler (cpu_multicorrelator_real_codes.cc:103-126),
+ * in the units dll_pll_veml_tracking passes them (do_correlation_step,
+ * dll_pll_veml_tracking.cc:1064-1089): code terms already multiplied by samples/chip. */
+typedef struct gsdr_corr_job
+{
+    int32_t channel;              /* correlator slot holding code + taps */
+    int32_t n_samples;            /* signal_length_samples */
+    int64_t sample_offset;        /* first input item of this job within the IQ buffer */
+    float rem_carr_phase_rad;
+    float carr_phase_step_rad;
+    float carr_phase_rate_step_rad;
+    float rem_code_phase_chips;
+    float code_phase_step_chips;
+    float code_phase_rate_step_chips;
+} gsdr_corr_job;
+
+/* init(max_signal_length_samples, n_correlators) for max_channels slots. */
+int gsdr_corr_create(int device, int max_channels, int max_len, int max_taps, gsdr_corr** out);
+void gsdr_corr_destroy(gsdr_corr* corr);
+
+/* set_local_code_and_taps (cpu_multicorrelator_real_codes.cc:53-63); unlike the
+ * reference (which keeps the caller's pointers) the code and shifts are copied
+ * to the device, so the caller's arrays need not outlive the call. */
+int gsdr_corr_set_local_code_and_taps(gsdr_corr* corr, int channel, int code_length_chips, const float* code,
+    const float* shifts_chips, int n_taps);
+/* Cpu_Multicorrelator::set_local_code_and_taps (complex replicas, cpu_multicorrelator.cc:54-62). */
+int gsdr_corr_set_local_code_and_taps_complex(gsdr_corr* corr, int channel, int code_length_chips,
+    const float* code_cf32, const float* shifts_chips, int n_taps);
+/* set_high_dynamics_resampler (cpu_multicorrelator_real_codes.cc:161-165). */
+int gsdr_corr_set_high_dynamics_resampler(gsdr_corr* corr, int channel, int enable);
+/* Float association of the code-phase index (GSDR_ASSOC_*), default GSDR_ASSOC_AVX. */
+int gsdr_corr_set_resampler_assoc(gsdr_corr* corr, int assoc);
+
+/* Synchronous drop-in for one channel: Carrier_wipeoff_multicorrelator_resampler
+ * (7-argument form) on host samples; writes n_taps complex<float> to corr_out_host.
+ * item_type selects gr_complex or cshort input. */
+int gsdr_corr_run(gsdr_corr* corr, int channel, const void* sig_in_host, int item_type, float rem_carr_phase_rad,
+    float carr_phase_step_rad, float carr_phase_rate_step_rad, float rem_code_phase_chips,
+    float code_phase_step_chips, float code_phase_rate_step_chips, int signal_length_samples, float* corr_out_host);
+
+/* Batched form: njobs jobs over one device IQ buffer (iq_dev, iq_items items of
+ * item_type).  Writes, for job j, n_taps(channel) complex<float> at
+ * out_dev + 2*j*max_taps.  jobs_host is copied; asynchronous on stream. */
+int gsdr_corr_run_batch(gsdr_corr* corr, const gsdr_corr_job* jobs_host, int njobs, const void* iq_dev,
+    int item_type, int64_t iq_items, float* out_dev, void* stream);
+
+/* Same, with the job table already in device memory (graph-capturable). */
+int gsdr_corr_run_batch_device(gsdr_corr* corr, const gsdr_corr_job* jobs_dev, int njobs, const void* iq_dev,
+    int item_type, int64_t iq_items, float* out_dev, void* stream);
+
+/* Debug/verification: the resampled code indices of one channel, as the
+ * kernel computes them (n_taps rows x n samples int32, host). */
+int gsdr_corr_dump_indices(gsdr_corr* corr, int channel, float rem_code_phase_chips, float code_phase_step_chips,
+    int n, int32_t* idx_host);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GSDR_H */

@@ -1,0 +1,176 @@
+"""ORACLE — test infrastructure only.
+
+Restatement of GNSS-SDR's Parallel Code Phase Search acquisition core
+(src/algorithms/acquisition/gnuradio_blocks/pcps_acquisition.cc) with numpy.
+The FFT library boundary (FFTW3f through gr-fft in the reference) is restated
+with numpy's pocketfft: in complex128 ("exact", default) or complex64.  Both
+directions are unnormalised like FFTW (gnss_sdr_fft.h:22-63).
+
+Pinned by the reference's own acquisition validation tests on its IQ captures
+(tests/test_oracle_golden.py: GPS_L1_CA_ID_1_Fs_4Msps_2ms.dat, delay 524 samples
+/ Doppler 1680 Hz within the reference's 0.5 chip / 666 Hz tolerances).
+"""
+import math
+
+import numpy as np
+from scipy.special import gammaincinv
+
+from . import volk
+
+TWO_PI = 6.283185307179586
+
+
+def num_doppler_bins(doppler_max, doppler_step):
+    """pcps_acquisition.cc:264 — ceil((dmax - (-dmax)) / step)."""
+    return int(math.ceil(float(int(doppler_max) - int(-doppler_max)) / float(doppler_step)))
+
+
+def doppler_hz(d, doppler_max, doppler_step, doppler_center=0):
+    """pcps_acquisition.cc:302 and :537."""
+    return -int(doppler_max) + int(doppler_center) + int(doppler_step) * int(d)
+
+
+def doppler_wipeoffs(fs, N, doppler_max, doppler_step, D, doppler_center=0, doppler_bias=0):
+    """update_grid_doppler_wipeoffs (:298-305) + update_local_carrier (:233-246):
+    phase_step = float(TWO_PI) * f / float(fs) in float32, then the generic
+    s32f_sincos with -phase_step (fp32 accumulated phase)."""
+    f32 = np.float32
+    w = np.empty((D, N), np.complex64)
+    for d in range(D):
+        f = f32(doppler_bias + doppler_hz(d, doppler_max, doppler_step, doppler_center))
+        step = f32(TWO_PI) * f / f32(fs)
+        w[d] = volk.s32f_sincos_32fc(float(-step), N)
+    return w
+
+
+def fft_code(code, fft_size, consumed, bit_transition=False, dtype=np.complex128):
+    """set_local_code (:176-209): place code in the FFT buffer, FFT, conjugate."""
+    buf = np.zeros(fft_size, dtype)
+    if bit_transition:
+        off = fft_size // 2
+        buf[off:] = code[:off]
+    elif fft_size == consumed:
+        buf[:] = code[:consumed]
+    else:
+        buf[fft_size - consumed:] = code[:consumed]
+    return np.conj(np.fft.fft(buf)).astype(dtype)
+
+
+def magnitude_grid(x, wipe, code_fft, bit_transition=False, dtype=np.complex128):
+    """The Doppler loop of acquisition_core (:655-686): |IFFT(FFT(x*w_d) . Cconj)|^2,
+    unnormalised inverse (FFTW rev = N * numpy.ifft).  Returns float32 [D][Neff]."""
+    D, N = wipe.shape
+    xs = x.astype(dtype)
+    t = xs[None, :] * wipe.astype(dtype)
+    if dtype == np.complex64:
+        t = t.astype(np.complex64)
+    X = np.fft.fft(t, axis=1)
+    R = np.fft.ifft(X * code_fft[None, :].astype(dtype), axis=1) * N
+    M = (R.real.astype(np.float64) ** 2 + R.imag.astype(np.float64) ** 2)
+    if bit_transition:
+        M = M[:, N // 2:]
+    return M.astype(np.float32)
+
+
+def max_to_input_power_statistic(M, dwells=1):
+    """pcps_acquisition.cc:511-543 (first-step branch).  Returns
+    (index_time, index_doppler, grid_max, input_power, statistic)."""
+    D, Neff = M.shape
+    gmax = np.float32(0.0)
+    di = 0
+    ti = 0
+    for i in range(D):
+        t = volk.index_max_32u(M[i])
+        if M[i, t] > gmax:
+            gmax = M[i, t]
+            di = i
+            ti = t
+    opp = (di + D // 2) % D
+    acc = np.float32(0.0)
+    # std::accumulate in float; vectorised sequential sum via cumsum (strictly ordered)
+    acc = np.cumsum(M[opp], dtype=np.float32)[-1]
+    # float accumulate / int32 is a float division; then / 2.0 / counter in double (:533)
+    input_power = np.float32(float(np.float32(acc) / np.float32(Neff)) / 2.0 / dwells)
+    return ti, di, np.float32(gmax), input_power, np.float32(gmax / input_power)
+
+
+def first_vs_second_peak_statistic(M, samples_per_chip, fft_size):
+    """pcps_acquisition.cc:546-612, including its one-sided wrap of the exclusion
+    window.  Returns (index_time, index_doppler, first, second, statistic)."""
+    D, _ = M.shape
+    first = np.float32(0.0)
+    di = 0
+    ti = 0
+    for i in range(D):
+        t = volk.index_max_32u(M[i])
+        if M[i, t] > first:
+            first = M[i, t]
+            di = i
+            ti = t
+    e1 = ti - samples_per_chip
+    e2 = ti + samples_per_chip
+    if e1 < 0:
+        e1 = fft_size + e1
+    elif e2 >= fft_size:
+        e2 = e2 - fft_size
+    tmp = M[di].copy()
+    idx = e1
+    while True:
+        tmp[idx] = 0.0
+        idx += 1
+        if idx == fft_size:
+            idx = 0
+        if idx == e2:
+            break
+    second = tmp[volk.index_max_32u(tmp)]
+    return ti, di, np.float32(first), np.float32(second), np.float32(first / second)
+
+
+def threshold(pfa, fft_size, D, max_dwells=1, bit_transition=False):
+    """calculate_threshold (:894-909) with Boost gamma_p_inv == scipy gammaincinv."""
+    if pfa <= 0.0:
+        return None
+    neff = fft_size // 2 if bit_transition else fft_size
+    nb = neff * D
+    a = 2.0 * (1 if bit_transition else max_dwells)
+    p = math.pow(1.0 - float(np.float32(pfa)), 1.0 / float(np.float32(nb)))
+    return float(np.float32(2.0 * gammaincinv(a, p)))
+
+
+class AcqResult:
+    __slots__ = ("index_time", "index_doppler", "doppler_hz", "peak", "input_power", "second_peak",
+                 "test_statistic", "delay_samples")
+
+    def __repr__(self):
+        return "AcqResult(t=%d, d=%d, dop=%d, peak=%g, stat=%g)" % (
+            self.index_time, self.index_doppler, self.doppler_hz, self.peak, self.test_statistic)
+
+
+def acquire(x, code, fs, doppler_max, doppler_step, D=None, pfa=0.0, samples_per_chip=None,
+            samples_per_code=None, doppler_center=0, dwells=1, dtype=np.complex128, wipe=None, M_out=None):
+    """One acquisition_core pass (single dwell, no bit transition) for one PRN.
+    x, code: complex64[N].  Returns AcqResult."""
+    N = len(x)
+    if D is None:
+        D = num_doppler_bins(doppler_max, doppler_step)
+    if wipe is None:
+        wipe = doppler_wipeoffs(fs, N, doppler_max, doppler_step, D, doppler_center)
+    cf = fft_code(code, N, N, dtype=dtype)
+    M = magnitude_grid(x, wipe, cf, dtype=dtype)
+    if M_out is not None:
+        M_out.append(M)
+    r = AcqResult()
+    if samples_per_chip is None:
+        samples_per_chip = int(math.ceil(float(np.float32(fs)) / 1023000.0))
+    if samples_per_code is None:
+        samples_per_code = float(np.float32(np.float32(fs) * np.float32(0.001)))
+    if pfa > 0.0:
+        ti, di, gmax, ip, stat = max_to_input_power_statistic(M, dwells)
+        r.peak, r.input_power, r.second_peak = gmax, ip, np.float32(0)
+    else:
+        ti, di, first, second, stat = first_vs_second_peak_statistic(M, samples_per_chip, N)
+        r.peak, r.input_power, r.second_peak = first, np.float32(0), second
+    r.index_time, r.index_doppler, r.test_statistic = int(ti), int(di), stat
+    r.doppler_hz = doppler_hz(di, doppler_max, doppler_step, doppler_center)
+    r.delay_samples = float(np.fmod(np.float32(ti), np.float32(samples_per_code)))
+    return r

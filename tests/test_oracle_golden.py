@@ -1,0 +1,71 @@
+"""Pins the oracle against the reference's own golden data (CPU only).
+
+- GPS code generator vs the IS-GPS-200 'first 10 chips' table (PRN 1-32).
+- PCPS restatement vs the reference's acquisition validation test
+  (src/tests/unit-tests/signal-processing-blocks/acquisition/gps_l1_ca_pcps_acquisition_test.cc:283-366):
+  PRN 1 on GPS_L1_CA_ID_1_Fs_4Msps_2ms.dat, 4 Msps, 1 ms, +-5 kHz / 100 Hz,
+  expected delay 524 samples (|err| < 0.5 chip) and Doppler 1680 Hz (|err| <= 666 Hz).
+- calculate_threshold for config C1 (pfa 0.01, N 4000, D 80) = 40.6733.
+"""
+import numpy as np
+import pytest
+
+from oracle import pcps, replica, volk
+from gsdr import synth
+
+
+def test_gps_first_10_chips_known_answer():
+    for prn in range(1, 33):
+        assert replica.first_10_chips_octal(prn) == replica.IS_GPS_200_FIRST10[prn - 1], prn
+
+
+def test_synth_code_generator_matches_oracle():
+    for prn in (1, 7, 19, 32):
+        np.testing.assert_array_equal(synth.gps_ca_chips(prn), replica.gps_l1_ca_code_float(prn))
+        np.testing.assert_array_equal(synth.gps_ca_sampled(prn, 4000000), replica.gps_l1_ca_code_complex_sampled(prn, 4000000))
+
+
+@pytest.mark.parametrize("dtype", [np.complex128, np.complex64])
+def test_oracle_pcps_reproduces_reference_validation(gps_capture, dtype):
+    x = gps_capture[:4000]
+    code = replica.gps_l1_ca_code_complex_sampled(1, 4000000)
+    r = pcps.acquire(x, code, 4000000, 5000, 100, pfa=0.0, dtype=dtype)
+    delay_err_chips = abs(524 - r.delay_samples) * 1023 / 4000
+    assert delay_err_chips < 0.5
+    assert abs(1680 - r.doppler_hz) <= 666
+    assert r.test_statistic > 0.001  # the test's set_threshold(0.001): positive acquisition
+
+
+def test_oracle_threshold_c1():
+    assert abs(pcps.threshold(0.01, 4000, 80) - 40.6733) < 1e-3
+    assert pcps.num_doppler_bins(10000, 250) == 80
+
+
+def test_oracle_resampler_associations_agree_almost_everywhere():
+    rng = np.random.default_rng(1)
+    L, N = 1023, 4000
+    shifts = np.array([-0.5, 0.0, 0.5], np.float32)
+    total = diff = 0
+    for _ in range(20):
+        rem = float(rng.uniform(-0.5, 0.5))
+        step = float(np.float32(1.023e6 / 4e6 * (1 + rng.uniform(-1e-5, 1e-5))))
+        g = volk.resampler_index(rem, step, shifts, L, N, assoc=0)
+        a = volk.resampler_index(rem, step, shifts, L, N, assoc=1)
+        total += g.size
+        diff += int(np.count_nonzero(g != a))
+        assert g.min() >= 0 and g.max() < L
+    assert diff < total * 1e-3  # rare chip-boundary flips only
+
+
+def test_oracle_rotator_generic_close_to_exact():
+    rng = np.random.default_rng(2)
+    N = 16000
+    code = synth.gps_ca_chips(3)
+    sig = (rng.standard_normal(N) + 1j * rng.standard_normal(N)).astype(np.complex64)
+    sig += 4 * synth.gps_l1_iq(16e6, N, [synth.Satellite(3, 1234.0, 100.0, 60.0)], noise=False)
+    args = dict(rem_carr=0.3, carr_step=float(np.float32(2 * np.pi * 1234.0 / 16e6)), rem_code=0.1,
+                code_step=float(np.float32(1.023e6 / 16e6)), N=N)
+    shifts = np.array([-0.5, -0.25, 0.0, 0.25, 0.5], np.float32)
+    g = volk.multicorrelator_real_codes(sig, code, shifts, **args)
+    e = volk.multicorrelator_real_codes_exact(sig, code, shifts, **args)
+    assert np.max(np.abs(g - e) / np.abs(e)) < 1e-4

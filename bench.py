@@ -1,0 +1,281 @@
+#!/usr/bin/env python3
+"""Benchmark: IQ Msamples/s processed (acquisition + tracking) on BASELINE config C2.
+
+One step = one batch of B consecutive 1 ms blocks of synthetic GPS L1 C/A IQ at
+4 Msps already resident in HBM; for every block:
+  - a full PCPS acquisition grid: 32 PRNs x 81 Doppler bins (+-10 kHz, 250 Hz), CFAR
+    (pfa 0.01) — pcps_acquisition::acquisition_core for all PRNs of the block;
+  - one 3-tap E-P-L correlator epoch (N = 4000 samples) for each of the 8 tracked
+    channels — Cpu_Multicorrelator_Real_Codes, one launch per epoch, epochs in order.
+Whole-job throughput = blocks * 4000 samples * ranks / max-over-ranks wall time.
+
+Multi-GPU: one process per GPU (torch.distributed.run); every rank processes its
+own independent stream shard (weak scaling, no data-path collective).
+
+Also reports: the dominant kernel's roofline (algorithmic bytes / average launch
+time from HIP events recorded on the launch stream) and a CPU baseline (the
+oracle restatement, timed on this host on a bounded sample, rank 0 at N=1 only).
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "gnss-sdr-new_amd"))
+sys.path.insert(0, ROOT)
+
+METRIC = "IQ Msamples/s processed (acq+track), 32 PRN × 81 Doppler; % HBM roofline"
+FS = 4000000
+N = 4000               # samples per 1 ms block (consumed_samples = fft_size)
+P = 32                 # PRNs searched per block
+D = 81                 # Doppler bins (inclusive +-10 kHz grid at 250 Hz)
+DMAX, DSTEP = 10000, 250
+PFA = 0.01
+CHANNELS = 8           # tracked satellites
+TAPS = 3               # E, P, L
+HBM_PEAK = 8.0e12      # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def acq_bytes_per_block():
+    """B_acq = 8N(1 + D + P*D) + 16*P*D per N-sample block."""
+    return 8 * N * (1 + D + P * D) + 16 * P * D
+
+
+def correlate_kernel_bytes_per_block():
+    """Dominant kernel's share: each P*D cell streams its N-point spectrum once (8N)
+    and writes a 16-byte row-statistics tuple."""
+    return 8 * N * P * D + 16 * P * D
+
+
+def trk_bytes_per_epoch():
+    """B_trk = 8N + 8K per channel-epoch."""
+    return 8 * N + 8 * TAPS
+
+
+def make_workload(blocks, rank):
+    from gsdr import synth
+    sats = synth.random_constellation(CHANNELS, seed_offset=100 + rank)
+    iq = synth.gps_l1_iq(FS, blocks * N, sats, seed_offset=100 + rank)
+    codes = np.stack([synth.gps_ca_sampled(p, FS) for p in range(1, P + 1)])
+    # tracking job table: channel c, epoch e, aligned to the code start of the
+    # true signal, NCO parameters from the simulated truth (open loop)
+    import gsdr
+    jobs = np.zeros(blocks * CHANNELS, gsdr.CORR_JOB_DTYPE)
+    for e in range(blocks):
+        for c, s in enumerate(sats):
+            chips_per_sample = 1.023e6 / FS
+            start = e * N + int(round((s.code_delay_chips / 1.023e6) * FS)) % N
+            rem_code = start * chips_per_sample - s.code_delay_chips
+            rem_code -= round(rem_code)
+            # phase_offset = exp(-j*rem) and phase_inc = exp(-j*step) wipe off exp(+j*(2*pi*f*t + theta))
+            carr = (2 * np.pi * s.doppler_hz * start / FS + s.phase) % (2 * np.pi)
+            jobs[e * CHANNELS + c] = (c, N, start, np.float32(carr), np.float32(2 * np.pi * s.doppler_hz / FS), 0.0,
+                                      np.float32(-rem_code), np.float32(chips_per_sample), 0.0)
+    return sats, iq, codes, jobs
+
+
+def cpu_baseline(iq, codes, sats, jobs, budget_s=12.0):
+    """Oracle restatement on this host's CPU (1 thread): numpy pocketfft complex64
+    PCPS (acquisition_core + CFAR statistic) for all 32 PRNs x 81 bins of a block,
+    plus the scalar generic VOLK correlator for every channel-epoch of the block."""
+    from oracle import pcps, volk
+    wipe = pcps.doppler_wipeoffs(FS, N, DMAX, DSTEP, D)
+    cconj = np.conj(np.fft.fft(codes.astype(np.complex64), axis=1)).astype(np.complex64)
+    shifts = np.array([-0.5, 0.0, 0.5], np.float32)
+    chips = [None] * CHANNELS
+    from gsdr import synth
+    for c, s in enumerate(sats):
+        chips[c] = synth.gps_ca_chips(s.prn)
+
+    def one_block(b):
+        x = iq[b * N:(b + 1) * N]
+        X = np.fft.fft(x[None, :] * wipe, axis=1).astype(np.complex64)
+        for p in range(P):
+            R = np.fft.ifft(X * cconj[p][None, :], axis=1) * N
+            M = (R.real * R.real + R.imag * R.imag).astype(np.float32)
+            pcps.max_to_input_power_statistic(M)
+        for c in range(CHANNELS):
+            j = jobs[b * CHANNELS + c]
+            seg = iq[j["sample_offset"]:j["sample_offset"] + N]
+            if len(seg) < N:
+                seg = np.concatenate([seg, np.zeros(N - len(seg), np.complex64)])
+            volk.multicorrelator_real_codes(seg, chips[c], shifts, float(j["rem_carr_phase_rad"]),
+                                            float(j["carr_phase_step_rad"]), float(j["rem_code_phase_chips"]),
+                                            float(j["code_phase_step_chips"]), N)
+
+    t0 = time.perf_counter()
+    one_block(0)
+    t1 = time.perf_counter() - t0
+    nblk = int(max(1, min(len(iq) // N, math.ceil(budget_s / max(t1, 1e-3)))))
+    t0 = time.perf_counter()
+    for b in range(nblk):
+        one_block(b)
+    dt = time.perf_counter() - t0
+    return {"value": round(nblk * N / dt / 1e6, 5), "unit": "Msamples/s", "cores": 1, "kind": "port",
+            "sample": "%d blocks of 1 ms (4000 samples): 32 PRN x 81 Doppler CFAR PCPS (numpy pocketfft complex64) "
+                      "+ 8 x 3-tap generic VOLK correlator epochs each; %.1f s on one host core" % (nblk, dt)}
+
+
+def load_pmc_traffic():
+    """HBM bytes per launch of the dominant kernel, from the committed rocprofv3 PMC
+    summary (profiles/pmc_*.json, written by profiles/collect_pmc.py), if present."""
+    best = None
+    pdir = os.path.join(ROOT, "profiles")
+    if not os.path.isdir(pdir):
+        return None
+    for f in sorted(os.listdir(pdir)):
+        if f.startswith("pmc_") and f.endswith(".json"):
+            try:
+                d = json.load(open(os.path.join(pdir, f)))
+                best = d
+            except Exception:
+                pass
+    return best
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--blocks", type=int, default=64, help="1 ms blocks per step")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-profile-events", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import gsdr
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    B = args.blocks
+
+    sats, iq, codes, jobs = make_workload(B, rank)
+    iq_dev = torch.from_numpy(iq.view(np.float32).copy()).to(dev)
+    jobs_dev = torch.from_numpy(jobs.view(np.uint8).copy()).to(dev)
+    res_dev = torch.zeros(B * P * gsdr.ACQ_RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    trk_dev = torch.zeros(B * CHANNELS * TAPS * 2, dtype=torch.float32, device=dev)
+
+    acq = gsdr.Acquisition(FS, N, DMAX, DSTEP, pfa=PFA, max_prns=P, max_blocks=B, num_doppler_bins=D, device=local)
+    acq.set_local_codes(codes, np.arange(1, P + 1))
+    corr = gsdr.Correlator(CHANNELS, N, max_taps=TAPS, device=local)
+    shifts = np.array([-0.5, 0.0, 0.5], np.float32)
+    from gsdr import synth
+    for c, s in enumerate(sats):
+        corr.set_local_code_and_taps(c, synth.gps_ca_chips(s.prn), shifts)
+
+    stream = torch.cuda.current_stream(dev)
+    sptr = stream.cuda_stream
+
+    def step():
+        acq.run_device(iq_dev.data_ptr(), B, N, 0, res_dev.data_ptr(), sptr)
+        corr.run_epochs(jobs_dev.data_ptr(), CHANNELS, B, iq_dev.data_ptr(), B * N, trk_dev.data_ptr(),
+                        stream_ptr=sptr)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    # sanity: the visible satellites are acquired and tracked with a strong prompt
+    res = res_dev.cpu().numpy().view(gsdr.ACQ_RESULT_DTYPE).reshape(B, P)
+    det = {int(r["prn"]) for r in res[0] if r["positive"]}
+    vis = {s.prn for s in sats}
+    trk = trk_dev.cpu().numpy().view(np.complex64).reshape(B, CHANNELS, TAPS)
+    prompt_ratio = float(np.median(np.abs(trk[:, :, 1]) / np.maximum(np.abs(trk[:, :, 0]), 1e-9)))
+
+    if not args.no_profile_events:
+        acq.set_profiling(True)
+        corr.set_profiling(True)
+        acq.read_profile()
+        corr.read_profile()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    stage_ms, stage_n = (np.zeros(4), np.zeros(4, np.uint32))
+    trk_ms, trk_n = 0.0, 0
+    if not args.no_profile_events:
+        stage_ms, stage_n = acq.read_profile()
+        trk_ms, trk_n = corr.read_profile()
+
+    samples = world * args.steps * B * N
+    value = samples / elapsed / 1e6
+    ms_per_step = elapsed / args.steps * 1e3
+
+    line = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "Msamples/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (seeded GPS L1 C/A IQ, 8 visible PRNs at 45 dB-Hz + AWGN, per-rank shard)",
+        "config": {
+            "workload": "C2: GPS L1 C/A 4 Msps; per 1 ms block a 32 PRN x 81 Doppler (+-10 kHz, 250 Hz) CFAR PCPS "
+                        "grid + one 3-tap E-P-L correlator epoch for each of 8 tracked channels",
+            "blocks_per_step": B, "fs_sps": FS, "fft_size": N, "prns": P, "doppler_bins": D, "channels": CHANNELS,
+            "taps": TAPS, "item_type": "gr_complex", "parallelism": "blocks sharded per rank (dp%d)" % world,
+        },
+        "real_time_factor": round(value * 1e6 / FS, 2),
+    }
+    if not args.no_profile_events and stage_n[1] > 0:
+        corr_launch_s = stage_ms[1] / stage_n[1] / 1e3
+        achieved = correlate_kernel_bytes_per_block() * B / corr_launch_s
+        pmc = load_pmc_traffic()
+        traffic = None
+        if pmc and pmc.get("kernel") == "acq_correlate_kernel" and pmc.get("blocks") == B:
+            traffic = pmc.get("hbm_bytes_per_launch")
+        line["roofline"] = {
+            "bound": "hbm", "achieved": round(achieved / 1e9, 2), "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK, 4), "traffic": traffic,
+            "kernel": "acq_correlate_kernel", "avg_launch_us": round(corr_launch_s * 1e6, 2),
+            "algorithmic_bytes_per_launch": correlate_kernel_bytes_per_block() * B,
+        }
+        line["stages_us_per_step"] = {
+            "acq_forward": round(stage_ms[0] / max(stage_n[0], 1) * 1e3, 2),
+            "acq_correlate": round(stage_ms[1] / max(stage_n[1], 1) * 1e3, 2),
+            "acq_reduce": round(stage_ms[2] / max(stage_n[2], 1) * 1e3, 2),
+            "trk_correlator_all_epochs": round(trk_ms / max(args.steps, 1) * 1e3, 2),
+        }
+        line["acq_roof_frac_whole_pipeline"] = round(
+            acq_bytes_per_block() * B / ((stage_ms[:3].sum() / args.steps) / 1e3) / HBM_PEAK, 4)
+    line["check"] = {"visible": len(vis), "acquired_block0": len(vis & det), "median_prompt_over_early": round(prompt_ratio, 2)}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(iq, codes, sats, jobs)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

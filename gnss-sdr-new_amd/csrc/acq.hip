@@ -369,6 +369,15 @@ struct gsdr_acq
     gsdr_acq_result* d_res{nullptr};
     void* d_iq{nullptr};
     float* d_grid{nullptr};
+    // stage profiling (gsdr_acq_set_profiling)
+    struct ProfRec
+    {
+        hipEvent_t a, b;
+        int stage;
+    };
+    bool profiling{false};
+    std::vector<ProfRec> prof_recs;
+    std::vector<hipEvent_t> prof_pool;
     std::mutex mu;
 };
 
@@ -448,6 +457,42 @@ void compute_threshold(gsdr_acq* a)
     a->threshold = (float)(2.0 * gsdr::gamma_p_inv_int(2 * (int)a->conf.max_dwells, p));
 }
 
+// Event bracket around one stage launch when profiling is on.
+struct StageTimer
+{
+    gsdr_acq* a;
+    hipStream_t s;
+    hipEvent_t ev0{nullptr};
+    StageTimer(gsdr_acq* a_, hipStream_t s_) : a(a_), s(s_) {}
+    hipEvent_t take()
+    {
+        hipEvent_t e = nullptr;
+        if (!a->prof_pool.empty())
+            {
+                e = a->prof_pool.back();
+                a->prof_pool.pop_back();
+            }
+        else if (hipEventCreate(&e) != hipSuccess)
+            e = nullptr;
+        return e;
+    }
+    void begin()
+    {
+        if (!a->profiling) return;
+        ev0 = take();
+        if (ev0) (void)hipEventRecord(ev0, s);
+    }
+    void end(int stage)
+    {
+        if (!a->profiling || !ev0) return;
+        hipEvent_t ev1 = take();
+        if (!ev1) return;
+        (void)hipEventRecord(ev1, s);
+        a->prof_recs.push_back({ev0, ev1, stage});
+        ev0 = nullptr;
+    }
+};
+
 template <class PT>
 void launch_forward(gsdr_acq* a, const void* iq, int item_type, uint32_t nblocks, uint64_t stride, hipStream_t s)
 {
@@ -464,20 +509,29 @@ int launch_all(gsdr_acq* a, const void* iq, int item_type, uint32_t nblocks, uin
     gsdr_acq_result* res, hipStream_t s)
 {
     const size_t lds = a->lds_bytes;
+    StageTimer t(a, s);
+    t.begin();
     launch_forward<PT>(a, iq, item_type, nblocks, stride, s);
     GSDR_HIP(hipGetLastError());
+    t.end(0);
+    t.begin();
     hipLaunchKernelGGL((acq_correlate_kernel<PT, false>), dim3(a->D * a->nprn, nblocks), dim3(PT::NT), lds, s,
         a->d_X, a->d_code_fft, a->d_stats, (float*)nullptr, a->d_tw, a->plan, a->D, a->nprn, 0u);
     GSDR_HIP(hipGetLastError());
+    t.end(1);
     AcqParams ap = params_of(a);
+    t.begin();
     hipLaunchKernelGGL(acq_reduce_kernel, dim3(nblocks * a->nprn), dim3(64), 0, s, a->d_stats, res, a->d_prn, ap,
         stamp0, stride);
     GSDR_HIP(hipGetLastError());
+    t.end(2);
     if (!ap.cfar)
         {
+            t.begin();
             hipLaunchKernelGGL((acq_second_peak_kernel<PT>), dim3(nblocks * a->nprn), dim3(PT::NT), lds, s, a->d_X,
                 a->d_code_fft, res, a->d_tw, a->plan, ap);
             GSDR_HIP(hipGetLastError());
+            t.end(3);
         }
     return GSDR_OK;
 }
@@ -674,6 +728,12 @@ void gsdr_acq_destroy(gsdr_acq* a)
     if (!a) return;
     gsdr::DeviceGuard g(a->device);
     if (a->stream) (void)hipStreamSynchronize(a->stream);
+    for (auto& r : a->prof_recs)
+        {
+            (void)hipEventDestroy(r.a);
+            (void)hipEventDestroy(r.b);
+        }
+    for (hipEvent_t e : a->prof_pool) (void)hipEventDestroy(e);
     void* bufs[] = {a->d_tw, a->d_wipe, a->d_code_fft, a->d_code_stage, a->d_prn, a->d_X, a->d_stats, a->d_res,
         a->d_iq, a->d_grid};
     for (void* p : bufs)
@@ -799,6 +859,38 @@ int gsdr_acq_dump_grid(gsdr_acq* a, const void* iq_host, uint32_t prn_slot, floa
     GSDR_HIP(hipMemcpyAsync(grid_host, a->d_grid, (size_t)a->D * a->N * sizeof(float), hipMemcpyDeviceToHost,
         a->stream));
     GSDR_HIP(hipStreamSynchronize(a->stream));
+    return GSDR_OK;
+}
+
+int gsdr_acq_set_profiling(gsdr_acq* a, int enable)
+{
+    GSDR_REQUIRE(a, GSDR_E_ARG, "gsdr_acq_set_profiling: null handle");
+    std::lock_guard<std::mutex> lk(a->mu);
+    a->profiling = enable != 0;
+    return GSDR_OK;
+}
+
+int gsdr_acq_read_profile(gsdr_acq* a, double* stage_ms, uint32_t* launches)
+{
+    GSDR_REQUIRE(a && stage_ms && launches, GSDR_E_ARG, "gsdr_acq_read_profile: null argument");
+    std::lock_guard<std::mutex> lk(a->mu);
+    gsdr::DeviceGuard g(a->device);
+    for (int i = 0; i < 4; ++i)
+        {
+            stage_ms[i] = 0.0;
+            launches[i] = 0;
+        }
+    for (auto& r : a->prof_recs)
+        {
+            GSDR_HIP(hipEventSynchronize(r.b));
+            float ms = 0.0f;
+            GSDR_HIP(hipEventElapsedTime(&ms, r.a, r.b));
+            stage_ms[r.stage] += ms;
+            launches[r.stage] += 1;
+            a->prof_pool.push_back(r.a);
+            a->prof_pool.push_back(r.b);
+        }
+    a->prof_recs.clear();
     return GSDR_OK;
 }
 

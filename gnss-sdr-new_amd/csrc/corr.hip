@@ -29,7 +29,10 @@ namespace
 
 constexpr int kMaxTaps = 8;
 constexpr int kCorrThreads = 256;
-constexpr int kMaxCodeSamples = 16384;  // LDS-staged replica capacity (floats; complex codes use 2x)
+constexpr int kSamplesPerThread = 4;
+constexpr int kChunk = kCorrThreads * kSamplesPerThread;  // samples per workgroup
+constexpr int kMaxCodeSamples = 16384;                    // replica length limit (floats; complex codes 2x)
+constexpr int kSpanCap = 4096;                            // LDS-staged replica span per chunk (entries)
 
 struct ChanDev
 {
@@ -104,120 +107,116 @@ __device__ __forceinline__ void rotator_model_device(const gsdr_corr_job& j, dou
     thr = atan2((double)s, (double)c);
 }
 
-// Streaming body: one lane per sample, K taps accumulated in VGPRs.
-template <int IT, bool CPLX>
-__device__ __forceinline__ void corr_accumulate(const gsdr_corr_job& job, const ChanDev& ch, const float* s_code,
-    const int* s_hdshift, double psi0, double th, double thr, const void* __restrict__ iq, int64_t iq_items, int assoc,
-    float2 (&acc)[kMaxTaps])
+// Unwrapped code index floor(...) with the reference's float association.
+__device__ __forceinline__ int raw_index(float step, float shift, float rem, int n, int assoc)
 {
-    const int L = ch.L;
-    const int K = ch.ntaps;
-    const int N = job.n_samples;
-    const bool hd = ch.high_dyn != 0;
-    const float rem = job.rem_code_phase_chips, step = job.code_phase_step_chips, rate = job.code_phase_rate_step_chips;
-    constexpr double kTwoPi = 6.283185307179586476925286766559;
-    constexpr double kInvTwoPi = 0.15915494309189533576888376337251;
-    for (int n = threadIdx.x; n < N; n += kCorrThreads)
-        {
-            const int64_t item = job.sample_offset + n;
-            const float2 x = (item >= 0 && item < iq_items) ? load_item<IT>(iq, item) : make_float2(0.f, 0.f);
-            double phi = psi0 + (double)n * th;
-            if (hd && n > 0)
-                {
-                    const double m1 = (double)(n - 1);
-                    phi += m1 * m1 * thr;
-                }
-            const double kk = rint(phi * kInvTwoPi);
-            const float a = (float)fma(-kk, kTwoPi, phi);
-            float s, c;
-            sincosf(a, &s, &c);
-            const float2 t = make_float2(x.x * c - x.y * s, x.x * s + x.y * c);
-#pragma unroll
-            for (int k = 0; k < kMaxTaps; ++k)
-                {
-                    if (k < K)
-                        {
-                            int idx;
-                            if (hd)
-                                {
-                                    const uint32_t m = (uint32_t)((n + s_hdshift[k]) % N);
-                                    idx = code_index_hd(step, rate, ch.shifts[0], rem, m, L);
-                                }
-                            else
-                                {
-                                    idx = code_index(step, ch.shifts[k], rem, n, L, assoc);
-                                }
-                            if (CPLX)
-                                {
-                                    const float cr = s_code[2 * idx], ci = s_code[2 * idx + 1];
-                                    acc[k].x += t.x * cr - t.y * ci;
-                                    acc[k].y += t.x * ci + t.y * cr;
-                                }
-                            else
-                                {
-                                    const float cv = s_code[idx];
-                                    acc[k].x += t.x * cv;
-                                    acc[k].y += t.y * cv;
-                                }
-                        }
-                }
-        }
+    const float a = __fmul_rn(step, (float)n);
+    const float t = (assoc == GSDR_ASSOC_GENERIC) ? __fsub_rn(__fadd_rn(a, shift), rem) : __fadd_rn(a, __fsub_rn(shift, rem));
+    return (int)floorf(t);
 }
 
-template <int IT>
-__global__ void __launch_bounds__(kCorrThreads) corr_kernel(const gsdr_corr_job* __restrict__ jobs,
-    const JobAux* __restrict__ aux, const ChanDev* __restrict__ chans, const void* __restrict__ iq, int64_t iq_items,
-    float2* __restrict__ out, int max_taps, int assoc)
+// Span staging modes of one chunk's replica.
+enum SpanMode
 {
-    extern __shared__ float s_code[];
-    __shared__ double s_model[3];
-    __shared__ int s_hdshift[kMaxTaps];
-    __shared__ float2 s_red[kCorrThreads / 64][kMaxTaps];
+    kSpanLds = 1,     // code[(lo + i) mod L] staged in LDS, lookup s_code[raw - lo]
+    kSpanGlobal = 2,  // lookup the replica in global memory (L1/L2-resident) with the modulo
+};
 
-    const gsdr_corr_job job = jobs[blockIdx.x];
-    const ChanDev ch = chans[job.channel];
-    const int K = ch.ntaps;
-
-    // stage the replica
-    const int code_floats = ch.cplx ? 2 * ch.L : ch.L;
-    for (int i = threadIdx.x; i < code_floats; i += kCorrThreads) s_code[i] = ch.code[i];
-    if (threadIdx.x == 0)
-        {
-            double psi0, th, thr;
-            if (aux && aux[blockIdx.x].valid)
-                {
-                    psi0 = aux[blockIdx.x].psi0;
-                    th = aux[blockIdx.x].theta;
-                    thr = aux[blockIdx.x].theta_rate;
-                }
-            else
-                {
-                    rotator_model_device(job, psi0, th, thr);
-                }
-            s_model[0] = psi0;
-            s_model[1] = th;
-            s_model[2] = thr;
-            // high-dynamics taps 1..K-1 are sample-shifted copies of tap 0
-            // (KERN/32f_xn_high_dynamics_resampler_32f_xn.h:84-91)
-            unsigned int sh = 0;
-            s_hdshift[0] = 0;
-            for (int k = 1; k < K && k < kMaxTaps; ++k)
-                {
-                    sh += (int)roundf((ch.shifts[k] - ch.shifts[k - 1]) / job.code_phase_step_chips);
-                    s_hdshift[k] = (int)sh;
-                }
-        }
-    __syncthreads();
-
+// Streaming body of one chunk: lane-interleaved samples (coalesced loads), the carrier
+// phasor anchored once per lane in fp64 and advanced by exp(j*theta*kCorrThreads),
+// K taps accumulated in VGPRs.
+template <int IT, bool CPLX, bool HD>
+__device__ __forceinline__ void chunk_accumulate(const gsdr_corr_job& job, const ChanDev& ch, const float* s_code,
+    int mode, int lo, const int* s_hdshift, double psi0, double th, double thr, float2 wstep, int n0, int n1,
+    const void* __restrict__ iq, int64_t iq_items, int assoc, float2 (*s_red)[kMaxTaps])
+{
     float2 acc[kMaxTaps];
 #pragma unroll
     for (int k = 0; k < kMaxTaps; ++k) acc[k] = make_float2(0.f, 0.f);
-    if (ch.cplx)
-        corr_accumulate<IT, true>(job, ch, s_code, s_hdshift, s_model[0], s_model[1], s_model[2], iq, iq_items, assoc, acc);
-    else
-        corr_accumulate<IT, false>(job, ch, s_code, s_hdshift, s_model[0], s_model[1], s_model[2], iq, iq_items, assoc, acc);
-
-    // wave64 reduction, then across the workgroup's waves in a fixed order
+    const int L = ch.L;
+    const int K = ch.ntaps;
+    const int N = job.n_samples;
+    const float rem = job.rem_code_phase_chips, step = job.code_phase_step_chips, rate = job.code_phase_rate_step_chips;
+    constexpr double kTwoPi = 6.283185307179586476925286766559;
+    constexpr double kInvTwoPi = 0.15915494309189533576888376337251;
+    const float* code_g = ch.code;
+    float2 ph = make_float2(1.f, 0.f);
+    if (!HD)
+        {
+            const double phi = psi0 + (double)(n0 + (int)threadIdx.x) * th;
+            const float a = (float)fma(-rint(phi * kInvTwoPi), kTwoPi, phi);
+            float sn, cs;
+            sincosf(a, &sn, &cs);
+            ph = make_float2(cs, sn);
+        }
+#pragma unroll
+    for (int it = 0; it < kSamplesPerThread; ++it)
+        {
+            const int n = n0 + (int)threadIdx.x + it * kCorrThreads;
+            if (n < n1)
+                {
+                    const int64_t item = job.sample_offset + n;
+                    const float2 x = (item >= 0 && item < iq_items) ? load_item<IT>(iq, item) : make_float2(0.f, 0.f);
+                    float2 r = ph;
+                    if (HD)
+                        {
+                            double phi = psi0 + (double)n * th;
+                            if (n > 0)
+                                {
+                                    const double m1 = (double)(n - 1);
+                                    phi += m1 * m1 * thr;
+                                }
+                            const float a = (float)fma(-rint(phi * kInvTwoPi), kTwoPi, phi);
+                            float sn, cs;
+                            sincosf(a, &sn, &cs);
+                            r = make_float2(cs, sn);
+                        }
+                    const float2 t = make_float2(x.x * r.x - x.y * r.y, x.x * r.y + x.y * r.x);
+#pragma unroll
+                    for (int k = 0; k < kMaxTaps; ++k)
+                        {
+                            if (k < K)
+                                {
+                                    float cr, ci = 0.0f;
+                                    if (HD)
+                                        {
+                                            const uint32_t m = (uint32_t)((n + s_hdshift[k]) % N);
+                                            const int idx = code_index_hd(step, rate, ch.shifts[0], rem, m, L);
+                                            cr = CPLX ? code_g[2 * idx] : code_g[idx];
+                                            if (CPLX) ci = code_g[2 * idx + 1];
+                                        }
+                                    else
+                                        {
+                                            const int raw = raw_index(step, ch.shifts[k], rem, n, assoc);
+                                            if (mode == kSpanLds)
+                                                {
+                                                    const int i = raw - lo;
+                                                    cr = CPLX ? s_code[2 * i] : s_code[i];
+                                                    if (CPLX) ci = s_code[2 * i + 1];
+                                                }
+                                            else
+                                                {
+                                                    const int idx = wrap_mod(raw, L);
+                                                    cr = CPLX ? code_g[2 * idx] : code_g[idx];
+                                                    if (CPLX) ci = code_g[2 * idx + 1];
+                                                }
+                                        }
+                                    if (CPLX)
+                                        {
+                                            acc[k].x += t.x * cr - t.y * ci;
+                                            acc[k].y += t.x * ci + t.y * cr;
+                                        }
+                                    else
+                                        {
+                                            acc[k].x += t.x * cr;
+                                            acc[k].y += t.y * cr;
+                                        }
+                                }
+                        }
+                }
+            if (!HD) ph = make_float2(ph.x * wstep.x - ph.y * wstep.y, ph.x * wstep.y + ph.y * wstep.x);
+        }
+    // wave64 reduction into s_red[wave]
 #pragma unroll
     for (int k = 0; k < kMaxTaps; ++k)
         {
@@ -228,23 +227,197 @@ __global__ void __launch_bounds__(kCorrThreads) corr_kernel(const gsdr_corr_job*
                     acc[k].y += __shfl_xor(acc[k].y, off);
                 }
         }
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (lane == 0)
+    if ((threadIdx.x & 63) == 0)
         {
 #pragma unroll
-            for (int k = 0; k < kMaxTaps; ++k) s_red[wave][k] = acc[k];
+            for (int k = 0; k < kMaxTaps; ++k) s_red[threadIdx.x >> 6][k] = acc[k];
+        }
+}
+
+// grid = (chunks, jobs).  Workgroup (c, j) correlates samples [c*kChunk, (c+1)*kChunk)
+// of job j; the last workgroup of a job to finish sums the chunk partials in chunk
+// order (deterministic) and writes the K outputs.
+template <int IT>
+__global__ void __launch_bounds__(kCorrThreads) corr_kernel(const gsdr_corr_job* __restrict__ jobs,
+    const JobAux* __restrict__ aux, const ChanDev* __restrict__ chans, const void* __restrict__ iq, int64_t iq_items,
+    float2* __restrict__ out, int max_taps, int assoc, float2* __restrict__ partials, unsigned int* __restrict__ counters,
+    int max_chunks)
+{
+    extern __shared__ float s_code[];
+    __shared__ double s_model[3];
+    __shared__ float2 s_wstep;
+    __shared__ int s_hdshift[kMaxTaps];
+    __shared__ int s_lo, s_span, s_mode, s_last;
+    __shared__ float2 s_red[kCorrThreads / 64][kMaxTaps];
+
+    const int jb = blockIdx.y, chunk = blockIdx.x;
+    const gsdr_corr_job job = jobs[jb];
+    const ChanDev ch = chans[job.channel];
+    const int K = ch.ntaps;
+    const int N = job.n_samples;
+    const int nchunks = N > 0 ? (N + kChunk - 1) / kChunk : 1;
+    if (chunk >= nchunks) return;
+    const int n0 = chunk * kChunk;
+    const int n1 = min(N, n0 + kChunk);
+    const bool hd = ch.high_dyn != 0;
+
+    if (threadIdx.x == 0)
+        {
+            double psi0, th, thr;
+            if (aux && aux[jb].valid)
+                {
+                    psi0 = aux[jb].psi0;
+                    th = aux[jb].theta;
+                    thr = aux[jb].theta_rate;
+                }
+            else
+                {
+                    rotator_model_device(job, psi0, th, thr);
+                }
+            s_model[0] = psi0;
+            s_model[1] = th;
+            s_model[2] = thr;
+            const double w = th * (double)kCorrThreads;
+            float sn, cs;
+            sincosf((float)fma(-rint(w * 0.15915494309189533576888376337251), 6.283185307179586476925286766559, w), &sn,
+                &cs);
+            s_wstep = make_float2(cs, sn);
+            // high-dynamics taps 1..K-1 are sample-shifted copies of tap 0
+            // (KERN/32f_xn_high_dynamics_resampler_32f_xn.h:84-91)
+            unsigned int sh = 0;
+            s_hdshift[0] = 0;
+#pragma unroll
+            for (int k = 1; k < kMaxTaps; ++k)
+                {
+                    if (k < K) sh += (int)roundf((ch.shifts[k] - ch.shifts[k - 1]) / job.code_phase_step_chips);
+                    s_hdshift[k] = (int)sh;
+                }
+            // replica span of this chunk: the index is monotone in n for step > 0
+            int mode = kSpanGlobal, lo = 0, span = 0;
+            const float step = job.code_phase_step_chips, rem = job.rem_code_phase_chips;
+            if (!hd && step > 0.0f && n1 > n0)
+                {
+                    int mn = INT_MAX, mx = INT_MIN;
+#pragma unroll
+                    for (int k = 0; k < kMaxTaps; ++k)
+                        {
+                            if (k < K)
+                                {
+                                    mn = min(mn, raw_index(step, ch.shifts[k], rem, n0, assoc));
+                                    mx = max(mx, raw_index(step, ch.shifts[k], rem, n1 - 1, assoc));
+                                }
+                        }
+                    if (mx >= mn && mx - mn + 1 <= kSpanCap)
+                        {
+                            mode = kSpanLds;
+                            lo = mn;
+                            span = mx - mn + 1;
+                        }
+                }
+            s_mode = mode;
+            s_lo = lo;
+            s_span = span;
         }
     __syncthreads();
-    if (threadIdx.x < K)
+    const int mode = s_mode, lo = s_lo, span = s_span, L = ch.L;
+    if (mode == kSpanLds)
         {
-            float2 r = make_float2(0.f, 0.f);
-#pragma unroll
-            for (int w = 0; w < kCorrThreads / 64; ++w)
+            if (ch.cplx)
                 {
-                    r.x += s_red[w][threadIdx.x].x;
-                    r.y += s_red[w][threadIdx.x].y;
+                    for (int i = threadIdx.x; i < span; i += kCorrThreads)
+                        {
+                            const int idx = wrap_mod(lo + i, L);
+                            s_code[2 * i] = ch.code[2 * idx];
+                            s_code[2 * i + 1] = ch.code[2 * idx + 1];
+                        }
                 }
-            out[(size_t)blockIdx.x * max_taps + threadIdx.x] = r;
+            else
+                {
+                    for (int i = threadIdx.x; i < span; i += kCorrThreads) s_code[i] = ch.code[wrap_mod(lo + i, L)];
+                }
+        }
+    __syncthreads();
+
+    const double psi0 = s_model[0], th = s_model[1], thr = s_model[2];
+    const float2 ws = s_wstep;
+    if (hd)
+        {
+            if (ch.cplx)
+                chunk_accumulate<IT, true, true>(job, ch, s_code, mode, lo, s_hdshift, psi0, th, thr, ws, n0, n1, iq,
+                    iq_items, assoc, s_red);
+            else
+                chunk_accumulate<IT, false, true>(job, ch, s_code, mode, lo, s_hdshift, psi0, th, thr, ws, n0, n1, iq,
+                    iq_items, assoc, s_red);
+        }
+    else
+        {
+            if (ch.cplx)
+                chunk_accumulate<IT, true, false>(job, ch, s_code, mode, lo, s_hdshift, psi0, th, thr, ws, n0, n1, iq,
+                    iq_items, assoc, s_red);
+            else
+                chunk_accumulate<IT, false, false>(job, ch, s_code, mode, lo, s_hdshift, psi0, th, thr, ws, n0, n1, iq,
+                    iq_items, assoc, s_red);
+        }
+
+    const int wave = threadIdx.x >> 6;
+    __syncthreads();
+    if (nchunks == 1)
+        {
+            if (threadIdx.x < K)
+                {
+                    float2 r = make_float2(0.f, 0.f);
+#pragma unroll
+                    for (int w = 0; w < kCorrThreads / 64; ++w)
+                        {
+                            r.x += s_red[w][threadIdx.x].x;
+                            r.y += s_red[w][threadIdx.x].y;
+                        }
+                    out[(size_t)jb * max_taps + threadIdx.x] = r;
+                }
+            return;
+        }
+    // cross-chunk hand-off (MI355X_MICROARCH.md, inter-workgroup visibility): wave 0
+    // stores the partials, drains, releases at agent scope, then one atomic arrival.
+    if (wave == 0)
+        {
+            if (threadIdx.x < K)
+                {
+                    float2 r = make_float2(0.f, 0.f);
+#pragma unroll
+                    for (int w = 0; w < kCorrThreads / 64; ++w)
+                        {
+                            r.x += s_red[w][threadIdx.x].x;
+                            r.y += s_red[w][threadIdx.x].y;
+                        }
+                    partials[((size_t)jb * max_chunks + chunk) * kMaxTaps + threadIdx.x] = r;
+                }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (threadIdx.x == 0)
+                {
+                    const unsigned int prev = atomicAdd(&counters[jb], 1u);
+                    s_last = (prev == (unsigned int)(nchunks - 1)) ? 1 : 0;
+                }
+        }
+    __syncthreads();
+    if (!s_last) return;
+    if (wave == 0)
+        {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (threadIdx.x < K)
+                {
+                    float2 r = make_float2(0.f, 0.f);
+                    for (int c = 0; c < nchunks; ++c)
+                        {
+                            const float2 v = partials[((size_t)jb * max_chunks + c) * kMaxTaps + threadIdx.x];
+                            r.x += v.x;
+                            r.y += v.y;
+                        }
+                    out[(size_t)jb * max_taps + threadIdx.x] = r;
+                }
+            if (threadIdx.x == 0) counters[jb] = 0u;  // re-armed for the next launch on this stream
         }
 }
 
@@ -271,11 +444,17 @@ struct gsdr_corr
     ChanDev* d_chans{nullptr};
     gsdr_corr_job* d_jobs{nullptr};
     JobAux* d_aux{nullptr};
+    float2* d_partials{nullptr};      // jobs_cap x max_chunks x kMaxTaps chunk partial sums
+    unsigned int* d_counters{nullptr};  // per-job arrival counters (self re-arming)
+    int max_chunks{1};
     int jobs_cap{0};
     void* d_iq{nullptr};
     float2* d_out{nullptr};
     std::vector<JobAux> h_aux;
     int max_code_floats{0};  // largest staged replica over configured channels (sizes the LDS)
+    bool profiling{false};
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_recs;
+    std::vector<hipEvent_t> prof_pool;
     std::mutex mu;
 };
 
@@ -304,13 +483,19 @@ int ensure_jobs(gsdr_corr* c, int njobs)
     if (njobs <= c->jobs_cap) return GSDR_OK;
     int cap = c->jobs_cap ? c->jobs_cap : 64;
     while (cap < njobs) cap *= 2;
-    if (c->d_jobs) GSDR_HIP(hipFree(c->d_jobs));
-    if (c->d_aux) GSDR_HIP(hipFree(c->d_aux));
+    void* bufs[] = {c->d_jobs, c->d_aux, c->d_partials, c->d_counters};
+    for (void* p : bufs)
+        if (p) GSDR_HIP(hipFree(p));
     c->d_jobs = nullptr;
     c->d_aux = nullptr;
+    c->d_partials = nullptr;
+    c->d_counters = nullptr;
     c->jobs_cap = 0;
     GSDR_HIP(hipMalloc(&c->d_jobs, cap * sizeof(gsdr_corr_job)));
     GSDR_HIP(hipMalloc(&c->d_aux, cap * sizeof(JobAux)));
+    GSDR_HIP(hipMalloc(&c->d_partials, (size_t)cap * c->max_chunks * kMaxTaps * sizeof(float2)));
+    GSDR_HIP(hipMalloc(&c->d_counters, cap * sizeof(unsigned int)));
+    GSDR_HIP(hipMemset(c->d_counters, 0, cap * sizeof(unsigned int)));
     c->jobs_cap = cap;
     return GSDR_OK;
 }
@@ -319,14 +504,37 @@ int launch(gsdr_corr* c, const gsdr_corr_job* d_jobs, const JobAux* d_aux, int n
     int64_t iq_items, float* out, hipStream_t s)
 {
     if (njobs == 0) return GSDR_OK;
-    const size_t lds = (size_t)c->max_code_floats * sizeof(float);
+    int rc = ensure_jobs(c, njobs);  // partial/counter workspace sized for this batch
+    if (rc != GSDR_OK) return rc;
+    const size_t lds = (size_t)2 * kSpanCap * sizeof(float);
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (c->profiling)
+        {
+            for (hipEvent_t* e : {&e0, &e1})
+                {
+                    if (!c->prof_pool.empty())
+                        {
+                            *e = c->prof_pool.back();
+                            c->prof_pool.pop_back();
+                        }
+                    else
+                        GSDR_HIP(hipEventCreate(e));
+                }
+            GSDR_HIP(hipEventRecord(e0, s));
+        }
+    const dim3 grid(c->max_chunks, njobs);
     if (item_type == GSDR_ITEM_GR_COMPLEX)
-        hipLaunchKernelGGL((corr_kernel<GSDR_ITEM_GR_COMPLEX>), dim3(njobs), dim3(kCorrThreads), lds, s, d_jobs, d_aux,
-            c->d_chans, iq, iq_items, (float2*)out, c->max_taps, c->assoc);
+        hipLaunchKernelGGL((corr_kernel<GSDR_ITEM_GR_COMPLEX>), grid, dim3(kCorrThreads), lds, s, d_jobs, d_aux,
+            c->d_chans, iq, iq_items, (float2*)out, c->max_taps, c->assoc, c->d_partials, c->d_counters, c->max_chunks);
     else
-        hipLaunchKernelGGL((corr_kernel<GSDR_ITEM_CSHORT>), dim3(njobs), dim3(kCorrThreads), lds, s, d_jobs, d_aux,
-            c->d_chans, iq, iq_items, (float2*)out, c->max_taps, c->assoc);
+        hipLaunchKernelGGL((corr_kernel<GSDR_ITEM_CSHORT>), grid, dim3(kCorrThreads), lds, s, d_jobs, d_aux,
+            c->d_chans, iq, iq_items, (float2*)out, c->max_taps, c->assoc, c->d_partials, c->d_counters, c->max_chunks);
     GSDR_HIP(hipGetLastError());
+    if (c->profiling)
+        {
+            GSDR_HIP(hipEventRecord(e1, s));
+            c->prof_recs.push_back({e0, e1});
+        }
     return GSDR_OK;
 }
 
@@ -384,6 +592,7 @@ int gsdr_corr_create(int device, int max_channels, int max_len, int max_taps, gs
     c->max_channels = max_channels;
     c->max_len = max_len;
     c->max_taps = max_taps;
+    c->max_chunks = (max_len + kChunk - 1) / kChunk;
     c->chans.assign(max_channels, ChanDev{});
     for (auto& d : c->chans) d.ntaps = 0;
     c->code_bufs.assign(max_channels, nullptr);
@@ -399,7 +608,7 @@ int gsdr_corr_create(int device, int max_channels, int max_len, int max_taps, gs
             gsdr_corr_destroy(c);
             return GSDR_E_ALLOC;
         }
-    const size_t lds = (size_t)2 * kMaxCodeSamples * sizeof(float);
+    const size_t lds = (size_t)2 * kSpanCap * sizeof(float);
     GSDR_HIP(hipFuncSetAttribute((const void*)corr_kernel<GSDR_ITEM_GR_COMPLEX>,
         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     GSDR_HIP(hipFuncSetAttribute((const void*)corr_kernel<GSDR_ITEM_CSHORT>,
@@ -418,9 +627,15 @@ void gsdr_corr_destroy(gsdr_corr* c)
     if (!c) return;
     gsdr::DeviceGuard g(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (auto& r : c->prof_recs)
+        {
+            (void)hipEventDestroy(r.first);
+            (void)hipEventDestroy(r.second);
+        }
+    for (hipEvent_t e : c->prof_pool) (void)hipEventDestroy(e);
     for (float* p : c->code_bufs)
         if (p) (void)hipFree(p);
-    void* bufs[] = {c->d_chans, c->d_jobs, c->d_aux, c->d_iq, c->d_out};
+    void* bufs[] = {c->d_chans, c->d_jobs, c->d_aux, c->d_partials, c->d_counters, c->d_iq, c->d_out};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -548,6 +763,54 @@ int gsdr_corr_dump_indices(gsdr_corr* c, int ch, float rem, float step, int n, i
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     (void)hipFree(d_idx);
     GSDR_HIP(e);
+    return GSDR_OK;
+}
+
+int gsdr_corr_run_epochs(gsdr_corr* c, const gsdr_corr_job* jobs_dev, int jobs_per_epoch, int n_epochs,
+    const void* iq_dev, int item_type, int64_t iq_items, float* out_dev, void* stream)
+{
+    GSDR_REQUIRE(c && jobs_dev && iq_dev && out_dev, GSDR_E_ARG, "gsdr_corr_run_epochs: null argument");
+    GSDR_REQUIRE(jobs_per_epoch >= 0 && n_epochs >= 0, GSDR_E_ARG, "gsdr_corr_run_epochs: negative count");
+    GSDR_REQUIRE(item_type == GSDR_ITEM_GR_COMPLEX || item_type == GSDR_ITEM_CSHORT, GSDR_E_ARG,
+        "gsdr_corr_run_epochs: item type %d", item_type);
+    std::lock_guard<std::mutex> lk(c->mu);
+    gsdr::DeviceGuard g(c->device);
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    for (int e = 0; e < n_epochs; ++e)
+        {
+            int rc = launch(c, jobs_dev + (size_t)e * jobs_per_epoch, nullptr, jobs_per_epoch, iq_dev, item_type, iq_items,
+                out_dev + (size_t)2 * e * jobs_per_epoch * c->max_taps, s);
+            if (rc != GSDR_OK) return rc;
+        }
+    return GSDR_OK;
+}
+
+int gsdr_corr_set_profiling(gsdr_corr* c, int enable)
+{
+    GSDR_REQUIRE(c, GSDR_E_ARG, "gsdr_corr_set_profiling: null handle");
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->profiling = enable != 0;
+    return GSDR_OK;
+}
+
+int gsdr_corr_read_profile(gsdr_corr* c, double* kernel_ms, uint32_t* launches)
+{
+    GSDR_REQUIRE(c && kernel_ms && launches, GSDR_E_ARG, "gsdr_corr_read_profile: null argument");
+    std::lock_guard<std::mutex> lk(c->mu);
+    gsdr::DeviceGuard g(c->device);
+    *kernel_ms = 0.0;
+    *launches = 0;
+    for (auto& r : c->prof_recs)
+        {
+            GSDR_HIP(hipEventSynchronize(r.second));
+            float ms = 0.0f;
+            GSDR_HIP(hipEventElapsedTime(&ms, r.first, r.second));
+            *kernel_ms += ms;
+            *launches += 1;
+            c->prof_pool.push_back(r.first);
+            c->prof_pool.push_back(r.second);
+        }
+    c->prof_recs.clear();
     return GSDR_OK;
 }
 

@@ -28,11 +28,12 @@ EXPORTED = [
     "gsdr_last_error", "gsdr_abi_version", "gsdr_device_count",
     "gsdr_acq_create", "gsdr_acq_destroy", "gsdr_acq_get_dims", "gsdr_acq_set_local_codes",
     "gsdr_acq_set_doppler", "gsdr_acq_set_threshold", "gsdr_acq_get_threshold", "gsdr_acq_run",
-    "gsdr_acq_run_device", "gsdr_acq_dump_grid", "gsdr_acq_dump_spectra",
+    "gsdr_acq_run_device", "gsdr_acq_dump_grid", "gsdr_acq_dump_spectra", "gsdr_acq_set_profiling",
+    "gsdr_acq_read_profile",
     "gsdr_corr_create", "gsdr_corr_destroy", "gsdr_corr_set_local_code_and_taps",
     "gsdr_corr_set_local_code_and_taps_complex", "gsdr_corr_set_high_dynamics_resampler",
     "gsdr_corr_set_resampler_assoc", "gsdr_corr_run", "gsdr_corr_run_batch", "gsdr_corr_run_batch_device",
-    "gsdr_corr_dump_indices",
+    "gsdr_corr_dump_indices", "gsdr_corr_run_epochs", "gsdr_corr_set_profiling", "gsdr_corr_read_profile",
 ]
 
 
@@ -150,6 +151,11 @@ def load():
     L.gsdr_corr_run_batch.argtypes = [P, P, I, P, I, I64, P, P]
     L.gsdr_corr_run_batch_device.argtypes = [P, P, I, P, I, I64, P, P]
     L.gsdr_corr_dump_indices.argtypes = [P, I, F, F, I, P]
+    L.gsdr_acq_set_profiling.argtypes = [P, I]
+    L.gsdr_acq_read_profile.argtypes = [P, P, P]
+    L.gsdr_corr_run_epochs.argtypes = [P, P, I, I, P, I, I64, P, P]
+    L.gsdr_corr_set_profiling.argtypes = [P, I]
+    L.gsdr_corr_read_profile.argtypes = [P, P, P]
     _lib = L
     return L
 
@@ -253,6 +259,16 @@ class Acquisition:
         _check(load().gsdr_acq_run_device(self._h, ctypes.c_void_p(iq_dev_ptr), int(nblocks), int(stride_items),
                                           int(stamp0), ctypes.c_void_p(out_dev_ptr), ctypes.c_void_p(stream_ptr)))
 
+    def set_profiling(self, enable):
+        _check(load().gsdr_acq_set_profiling(self._h, int(bool(enable))))
+
+    def read_profile(self):
+        """(stage_ms[4], launches[4]): forward, correlate, reduce, second peak."""
+        ms = np.zeros(4, np.float64)
+        n = np.zeros(4, np.uint32)
+        _check(load().gsdr_acq_read_profile(self._h, _ptr(ms), _ptr(n)))
+        return ms, n
+
     def dump_grid(self, iq, prn_slot):
         iq = self._items(iq)
         g = np.zeros((self.num_doppler_bins, self.fft_size), np.float32)
@@ -325,6 +341,21 @@ class Correlator:
         _check(load().gsdr_corr_run_batch_device(self._h, ctypes.c_void_p(jobs_dev_ptr), int(njobs),
                                                  ctypes.c_void_p(iq_dev_ptr), item_type, int(iq_items),
                                                  ctypes.c_void_p(out_dev_ptr), ctypes.c_void_p(stream_ptr)))
+
+    def run_epochs(self, jobs_dev_ptr, jobs_per_epoch, n_epochs, iq_dev_ptr, iq_items, out_dev_ptr,
+                   item_type=ITEM_GR_COMPLEX, stream_ptr=0):
+        _check(load().gsdr_corr_run_epochs(self._h, ctypes.c_void_p(jobs_dev_ptr), int(jobs_per_epoch), int(n_epochs),
+                                           ctypes.c_void_p(iq_dev_ptr), item_type, int(iq_items),
+                                           ctypes.c_void_p(out_dev_ptr), ctypes.c_void_p(stream_ptr)))
+
+    def set_profiling(self, enable):
+        _check(load().gsdr_corr_set_profiling(self._h, int(bool(enable))))
+
+    def read_profile(self):
+        ms = ctypes.c_double()
+        n = ctypes.c_uint32()
+        _check(load().gsdr_corr_read_profile(self._h, ctypes.byref(ms), ctypes.byref(n)))
+        return ms.value, n.value
 
     def dump_indices(self, channel, rem_code, code_step, n):
         out = np.zeros((self.ntaps[channel], n), np.int32)

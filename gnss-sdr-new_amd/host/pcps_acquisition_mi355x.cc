@@ -1,0 +1,277 @@
+#include "pcps_acquisition_mi355x.h"
+
+#include <cmath>
+#include <cstring>
+#include <iostream>
+#include <stdexcept>
+
+pcps_acquisition_mi355x::pcps_acquisition_mi355x(const Acq_Conf& conf, int device)
+    : d_acq_parameters(conf),
+      d_device(device),
+      d_doppler_step(static_cast<uint32_t>(conf.doppler_step)),
+      d_consumed_samples(static_cast<uint32_t>(conf.sampled_ms * conf.samples_per_ms * (conf.bit_transition_flag ? 2.0 : 1.0)))
+{
+    d_data_buffer.resize(static_cast<size_t>(d_consumed_samples) * conf.it_size);
+}
+
+pcps_acquisition_mi355x::~pcps_acquisition_mi355x() { gsdr_acq_destroy(d_engine); }
+
+void pcps_acquisition_mi355x::ensure_engine()
+{
+    const int32_t dmax = d_acq_parameters.doppler_max;
+    if (d_engine && dmax == d_engine_dmax && d_doppler_step == d_engine_step) return;
+    gsdr_acq_destroy(d_engine);
+    d_engine = nullptr;
+    gsdr_acq_conf c{};
+    c.fs_in = d_acq_parameters.resampled_fs ? d_acq_parameters.resampled_fs : d_acq_parameters.fs_in;
+    c.consumed_samples = d_consumed_samples;
+    c.fft_size = 0;
+    c.samples_per_code = d_acq_parameters.samples_per_code;
+    c.samples_per_chip = d_acq_parameters.samples_per_chip;
+    c.doppler_max = dmax;
+    c.doppler_step = d_doppler_step;
+    c.doppler_center = d_doppler_center;
+    c.pfa = d_acq_parameters.use_CFAR_algorithm_flag ? d_acq_parameters.pfa : 0.0F;
+    c.max_dwells = d_acq_parameters.max_dwells;
+    c.bit_transition_flag = d_acq_parameters.bit_transition_flag ? 1 : 0;
+    c.item_type = d_acq_parameters.item_type == "cshort" ? GSDR_ITEM_CSHORT : GSDR_ITEM_GR_COMPLEX;
+    c.max_prns = 1;
+    c.max_blocks = 1;
+    c.sampled_ms = d_acq_parameters.sampled_ms;
+    c.ms_per_code = d_acq_parameters.ms_per_code;
+    if (gsdr_acq_create(d_device, &c, &d_engine) != GSDR_OK)
+        {
+            d_engine = nullptr;
+            throw std::runtime_error(std::string("pcps_acquisition_mi355x: ") + gsdr_last_error());
+        }
+    d_engine_dmax = dmax;
+    d_engine_step = d_doppler_step;
+    uint32_t D = 0, N = 0;
+    gsdr_acq_get_dims(d_engine, &D, &N);
+    d_num_doppler_bins = D;
+    if (d_code_set)
+        {
+            const uint32_t prn = d_gnss_synchro ? d_gnss_synchro->PRN : 0;
+            gsdr_acq_set_local_codes(d_engine, reinterpret_cast<const float*>(d_code.data()), &prn, 1);
+        }
+}
+
+// pcps_acquisition::init (:249-296): reset Gnss_Synchro acquisition fields and
+// (re)build the Doppler grid for the current doppler_max / step / center.
+void pcps_acquisition_mi355x::init()
+{
+    std::lock_guard<std::mutex> lk(d_setlock);
+    if (d_gnss_synchro)
+        {
+            d_gnss_synchro->Flag_valid_acquisition = false;
+            d_gnss_synchro->Flag_valid_symbol_output = false;
+            d_gnss_synchro->Flag_valid_pseudorange = false;
+            d_gnss_synchro->Flag_valid_word = false;
+            d_gnss_synchro->Acq_doppler_step = 0U;
+            d_gnss_synchro->Acq_delay_samples = 0.0;
+            d_gnss_synchro->Acq_doppler_hz = 0.0;
+            d_gnss_synchro->Acq_samplestamp_samples = 0ULL;
+        }
+    d_mag = 0.0F;
+    d_input_power = 0.0F;
+    ensure_engine();
+    gsdr_acq_set_doppler(d_engine, d_acq_parameters.doppler_max, d_doppler_step, d_doppler_center);
+}
+
+void pcps_acquisition_mi355x::set_doppler_center(int32_t doppler_center)
+{
+    std::lock_guard<std::mutex> lk(d_setlock);
+    if (doppler_center != d_doppler_center)
+        {
+            d_doppler_center = doppler_center;
+            if (d_engine) gsdr_acq_set_doppler(d_engine, d_acq_parameters.doppler_max, d_doppler_step, d_doppler_center);
+        }
+}
+
+// set_local_code (:176-209): the GPU places, transforms and conjugates the replica.
+void pcps_acquisition_mi355x::set_local_code(std::complex<float>* code)
+{
+    std::lock_guard<std::mutex> lk(d_setlock);
+    d_code.assign(code, code + d_consumed_samples);
+    d_code_set = true;
+    ensure_engine();
+    const uint32_t prn = d_gnss_synchro ? d_gnss_synchro->PRN : 0;
+    if (gsdr_acq_set_local_codes(d_engine, reinterpret_cast<const float*>(d_code.data()), &prn, 1) != GSDR_OK)
+        std::cerr << "pcps_acquisition_mi355x: set_local_code: " << gsdr_last_error() << '\n';
+}
+
+void pcps_acquisition_mi355x::set_active(bool active)
+{
+    std::lock_guard<std::mutex> lk(d_setlock);
+    d_active = active;
+}
+
+// set_state (:318-342)
+void pcps_acquisition_mi355x::set_state(int32_t state)
+{
+    std::lock_guard<std::mutex> lk(d_setlock);
+    d_state = state;
+    if (d_state == 1)
+        {
+            if (d_gnss_synchro)
+                {
+                    d_gnss_synchro->Acq_delay_samples = 0.0;
+                    d_gnss_synchro->Acq_doppler_hz = 0.0;
+                    d_gnss_synchro->Acq_samplestamp_samples = 0ULL;
+                    d_gnss_synchro->Acq_doppler_step = 0U;
+                }
+            d_mag = 0.0F;
+            d_test_statistics = 0.0F;
+            d_active = true;
+        }
+    else if (d_state != 0)
+        {
+            std::cerr << "State can only be set to 0 or 1\n";
+        }
+}
+
+bool pcps_acquisition_mi355x::start()
+{
+    d_sample_counter = 0ULL;
+    calculate_threshold();
+    return true;
+}
+
+// calculate_threshold (:894-909): computed by the engine from pfa.
+void pcps_acquisition_mi355x::calculate_threshold()
+{
+    if (d_acq_parameters.pfa <= 0.0F) return;
+    ensure_engine();
+    gsdr_acq_get_threshold(d_engine, &d_threshold);
+}
+
+void pcps_acquisition_mi355x::send_positive_acquisition()
+{
+    d_positive_acq = 1;
+    if (d_events) d_events(1);
+}
+
+void pcps_acquisition_mi355x::send_negative_acquisition()
+{
+    d_positive_acq = 0;
+    if (d_events) d_events(2);
+}
+
+// acquisition_core (:615-882) for the single-dwell, single-step configuration.
+void pcps_acquisition_mi355x::acquisition_core(uint64_t samp_count)
+{
+    d_mag = 0.0F;
+    d_num_noncoherent_integrations_counter++;
+    gsdr_acq_set_threshold(d_engine, d_threshold);
+    gsdr_acq_result r{};
+    if (gsdr_acq_run(d_engine, d_data_buffer.data(), 1, samp_count, &r) != GSDR_OK)
+        {
+            // device error -> negative acquisition, the reference's failure convention
+            std::cerr << "pcps_acquisition_mi355x: " << gsdr_last_error() << '\n';
+            d_state = 0;
+            d_active = false;
+            d_num_noncoherent_integrations_counter = 0;
+            send_negative_acquisition();
+            return;
+        }
+    d_mag = r.peak;
+    d_input_power = r.input_power;
+    d_test_statistics = r.test_statistic;
+    if (d_gnss_synchro)
+        {
+            if (d_acq_parameters.use_automatic_resampler)
+                {
+                    d_gnss_synchro->Acq_delay_samples = r.acq_delay_samples * d_acq_parameters.resampler_ratio -
+                                                        static_cast<double>(d_acq_parameters.resampler_latency_samples);
+                    d_gnss_synchro->Acq_samplestamp_samples =
+                        static_cast<uint64_t>(std::rint(static_cast<double>(samp_count) * d_acq_parameters.resampler_ratio));
+                }
+            else
+                {
+                    d_gnss_synchro->Acq_delay_samples = r.acq_delay_samples;
+                    d_gnss_synchro->Acq_samplestamp_samples = samp_count;
+                }
+            d_gnss_synchro->Acq_doppler_hz = static_cast<double>(r.doppler_hz);
+        }
+    // decision and dwell FSM (:781-829, non-bit-transition branch, one step)
+    if (d_test_statistics > d_threshold)
+        {
+            d_active = false;
+            send_positive_acquisition();
+            d_state = 0;
+        }
+    else
+        {
+            d_buffer_count = 0;
+            d_state = 1;
+        }
+    if (d_num_noncoherent_integrations_counter == d_acq_parameters.max_dwells)
+        {
+            if (d_state != 0) send_negative_acquisition();
+            d_state = 0;
+            d_active = false;
+        }
+    if (d_num_noncoherent_integrations_counter == d_acq_parameters.max_dwells || d_positive_acq == 1)
+        {
+            d_num_noncoherent_integrations_counter = 0U;
+            d_positive_acq = 0;
+        }
+}
+
+// general_work (:912-1050) with blocking acquisition.
+int pcps_acquisition_mi355x::work(const void* in, int ninput_items)
+{
+    std::unique_lock<std::mutex> lk(d_setlock);
+    if (!d_active)
+        {
+            if (!d_acq_parameters.blocking_on_standby)
+                {
+                    d_sample_counter += static_cast<uint64_t>(ninput_items);
+                    return ninput_items;
+                }
+            return 0;
+        }
+    switch (d_state)
+        {
+        case 0:
+            {
+                if (d_gnss_synchro)
+                    {
+                        d_gnss_synchro->Acq_delay_samples = 0.0;
+                        d_gnss_synchro->Acq_doppler_hz = 0.0;
+                        d_gnss_synchro->Acq_samplestamp_samples = 0ULL;
+                        d_gnss_synchro->Acq_doppler_step = 0U;
+                    }
+                d_mag = 0.0F;
+                d_state = 1;
+                d_buffer_count = 0U;
+                if (!d_acq_parameters.blocking_on_standby)
+                    {
+                        d_sample_counter += static_cast<uint64_t>(ninput_items);
+                        return ninput_items;
+                    }
+                return 0;
+            }
+        case 1:
+            {
+                uint32_t inc = (static_cast<uint32_t>(ninput_items) + d_buffer_count <= d_consumed_samples)
+                                   ? static_cast<uint32_t>(ninput_items)
+                                   : d_consumed_samples - d_buffer_count;
+                const size_t isz = d_acq_parameters.it_size;
+                std::memcpy(d_data_buffer.data() + static_cast<size_t>(d_buffer_count) * isz, in, static_cast<size_t>(inc) * isz);
+                if (d_buffer_count >= d_consumed_samples) d_state = 2;
+                d_buffer_count += inc;
+                d_sample_counter += static_cast<uint64_t>(inc);
+                return static_cast<int>(inc);
+            }
+        case 2:
+            {
+                lk.unlock();
+                acquisition_core(d_sample_counter);
+                d_buffer_count = 0U;
+                return 0;
+            }
+        default:
+            return 0;
+        }
+}

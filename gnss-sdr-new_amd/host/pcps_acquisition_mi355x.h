@@ -1,0 +1,89 @@
+// pcps_acquisition on the MI355X engine: the public method set of
+// src/algorithms/acquisition/gnuradio_blocks/pcps_acquisition.h:84-286 with the
+// GNU Radio plumbing replaced by work() (general_work's state machine,
+// pcps_acquisition.cc:912-1050) and an event callback (the "events" message
+// port: 1 positive, 2 negative).  acquisition_core runs on the GPU through
+// gsdr_acq_run (include/gsdr.h).
+#ifndef GSDR_HOST_PCPS_ACQUISITION_MI355X_H
+#define GSDR_HOST_PCPS_ACQUISITION_MI355X_H
+
+#include <complex>
+#include <cstdint>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <vector>
+
+#include "acq_conf.h"
+#include "gnss_synchro.h"
+#include "gsdr.h"
+
+class pcps_acquisition_mi355x
+{
+public:
+    explicit pcps_acquisition_mi355x(const Acq_Conf& conf, int device = 0);
+    ~pcps_acquisition_mi355x();
+    pcps_acquisition_mi355x(const pcps_acquisition_mi355x&) = delete;
+    pcps_acquisition_mi355x& operator=(const pcps_acquisition_mi355x&) = delete;
+
+    void set_gnss_synchro(Gnss_Synchro* p_gnss_synchro) { d_gnss_synchro = p_gnss_synchro; }
+    uint32_t mag() const { return static_cast<uint32_t>(d_mag); }
+    void init();
+    void set_local_code(std::complex<float>* code);
+    void set_active(bool active);
+    void set_state(int32_t state);
+    void set_channel(uint32_t channel) { d_channel = channel; }
+    void set_threshold(float threshold) { d_threshold = threshold; }
+    void set_doppler_max(uint32_t doppler_max) { d_acq_parameters.doppler_max = static_cast<int32_t>(doppler_max); }
+    void set_doppler_step(uint32_t doppler_step) { d_doppler_step = doppler_step; }
+    void set_doppler_center(int32_t doppler_center);
+    void set_resampler_latency(uint32_t latency_samples) { d_acq_parameters.resampler_latency_samples = latency_samples; }
+    void set_event_handler(std::function<void(int)> h) { d_events = std::move(h); }
+    // start(): sample counter reset and threshold from pfa (pcps_acquisition.cc:885-891)
+    bool start();
+    void calculate_threshold();
+
+    // general_work: consumes up to ninput_items items of it_size bytes; returns the
+    // number consumed (consume_each).  Runs acquisition_core when the buffer is full.
+    int work(const void* in, int ninput_items);
+
+    float threshold() const { return d_threshold; }
+    float test_statistics() const { return d_test_statistics; }
+    float input_power() const { return d_input_power; }
+    uint32_t num_doppler_bins() const { return d_num_doppler_bins; }
+
+private:
+    void acquisition_core(uint64_t samp_count);
+    void ensure_engine();
+    void send_positive_acquisition();
+    void send_negative_acquisition();
+
+    Acq_Conf d_acq_parameters;
+    int d_device;
+    gsdr_acq* d_engine{nullptr};
+    int32_t d_engine_dmax{0};
+    uint32_t d_engine_step{0};
+    Gnss_Synchro* d_gnss_synchro{nullptr};
+    std::function<void(int)> d_events;
+    std::vector<uint8_t> d_data_buffer;
+    std::vector<std::complex<float>> d_code;
+    bool d_code_set{false};
+    uint64_t d_sample_counter{0};
+    float d_threshold{0.0F};
+    float d_mag{0.0F};
+    float d_input_power{0.0F};
+    float d_test_statistics{0.0F};
+    int32_t d_state{0};
+    int32_t d_positive_acq{0};
+    int32_t d_doppler_center{0};
+    uint32_t d_channel{0};
+    uint32_t d_doppler_step;
+    uint32_t d_num_noncoherent_integrations_counter{0};
+    uint32_t d_consumed_samples;
+    uint32_t d_num_doppler_bins{0};
+    uint32_t d_buffer_count{0};
+    bool d_active{false};
+    std::mutex d_setlock;
+};
+
+#endif

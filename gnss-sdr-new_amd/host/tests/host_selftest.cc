@@ -1,0 +1,187 @@
+// Host-side drop-in self-test, written like the reference's unit tests:
+//  1. GpsL1CaPcpsAcquisitionTest.ValidationOfResults
+//     (src/tests/unit-tests/signal-processing-blocks/acquisition/gps_l1_ca_pcps_acquisition_test.cc:283-366)
+//     on the reference capture, through the adapter + block mirror + GPU engine.
+//  2. Hip_Multicorrelator_Real_Codes / Hip_Multicorrelator on the acquired signal,
+//     checked against an fp64 evaluation of the reference's phasor model.
+// Usage: host_selftest <GPS_L1_CA_ID_1_Fs_4Msps_2ms.dat>
+#include <cmath>
+#include <complex>
+#include <cstdio>
+#include <fstream>
+#include <iostream>
+#include <string>
+#include <vector>
+
+#include "gnss_replicas.h"
+#include "gps_l1_ca_pcps_acquisition_mi355x.h"
+#include "hip_multicorrelator_real_codes.h"
+
+namespace
+{
+int failures = 0;
+#define EXPECT(cond, msg)                                              \
+    do                                                                 \
+        {                                                              \
+            if (!(cond))                                               \
+                {                                                      \
+                    std::cerr << "FAIL: " << msg << " (" #cond ")\n"; \
+                    ++failures;                                        \
+                }                                                      \
+        }                                                              \
+    while (0)
+
+std::vector<std::complex<float>> read_capture(const std::string& path)
+{
+    std::ifstream f(path, std::ios::binary);
+    std::vector<std::complex<float>> v;
+    if (!f) return v;
+    f.seekg(0, std::ios::end);
+    const auto bytes = static_cast<size_t>(f.tellg());
+    f.seekg(0);
+    v.resize(bytes / sizeof(std::complex<float>));
+    f.read(reinterpret_cast<char*>(v.data()), static_cast<std::streamsize>(v.size() * sizeof(std::complex<float>)));
+    return v;
+}
+
+// fp64 value of the reference rotator/resampler for real codes (generic association).
+std::vector<std::complex<double>> exact_correlation(const std::complex<float>* x, const std::vector<float>& code,
+    const std::vector<float>& shifts, float rem_carr, float carr_step, float rem_code, float code_step, int n)
+{
+    const std::complex<float> off(std::cos(rem_carr), -std::sin(rem_carr));
+    const std::complex<float> inc = std::exp(std::complex<float>(0.0F, -carr_step));
+    const double psi = std::atan2(static_cast<double>(off.imag()), static_cast<double>(off.real()));
+    const double th = std::atan2(static_cast<double>(inc.imag()), static_cast<double>(inc.real()));
+    const int L = static_cast<int>(code.size());
+    std::vector<std::complex<double>> out(shifts.size());
+    for (int i = 0; i < n; ++i)
+        {
+            const std::complex<double> t = std::complex<double>(x[i]) * std::polar(1.0, psi + th * i);
+            for (size_t k = 0; k < shifts.size(); ++k)
+                {
+                    volatile float a = code_step * static_cast<float>(i);
+                    volatile float b = shifts[k] - rem_code;
+                    int idx = static_cast<int>(std::floor(a + b));
+                    idx = ((idx % L) + L) % L;
+                    out[k] += t * static_cast<double>(code[idx]);
+                }
+        }
+    return out;
+}
+
+void test_acquisition_validation(const std::vector<std::complex<float>>& capture)
+{
+    InMemoryConfiguration config;
+    config.set_property("GNSS-SDR.internal_fs_sps", "4000000");
+    config.set_property("Acquisition_1C.implementation", "GPS_L1_CA_PCPS_Acquisition_MI355X");
+    config.set_property("Acquisition_1C.item_type", "gr_complex");
+    config.set_property("Acquisition_1C.coherent_integration_time_ms", "1");
+    config.set_property("Acquisition_1C.dump", "false");
+    config.set_property("Acquisition_1C.threshold", "0.00001");
+    config.set_property("Acquisition_1C.doppler_max", "5000");
+    config.set_property("Acquisition_1C.doppler_step", "100");
+    config.set_property("Acquisition_1C.repeat_satellite", "false");
+
+    Gnss_Synchro gnss_synchro{};
+    gnss_synchro.Channel_ID = 0;
+    gnss_synchro.System = 'G';
+    gnss_synchro.Signal[0] = '1';
+    gnss_synchro.Signal[1] = 'C';
+    gnss_synchro.PRN = 1;
+
+    GpsL1CaPcpsAcquisitionMI355X acquisition(&config, "Acquisition_1C", 1, 0);
+    int rx_message = 0;
+    acquisition.get_block()->set_event_handler([&](int ev) { rx_message = ev; });
+    acquisition.set_channel(1);
+    acquisition.set_gnss_synchro(&gnss_synchro);
+    acquisition.set_threshold(0.001);
+    acquisition.set_doppler_max(5000);
+    acquisition.set_doppler_step(100);
+    acquisition.set_local_code();
+    acquisition.set_state(1);
+    acquisition.init();
+    acquisition.get_block()->start();
+
+    // feed the file like a GNU Radio file_source, 1024 items per general_work call
+    size_t pos = 0;
+    int guard = 0;
+    while (rx_message == 0 && guard++ < 10000)
+        {
+            const int n = static_cast<int>(std::min<size_t>(1024, capture.size() - pos));
+            const int used = acquisition.get_block()->work(capture.data() + pos, n);
+            pos += static_cast<size_t>(used);
+            if (n == 0 && used == 0 && pos >= capture.size()) break;
+        }
+    EXPECT(rx_message == 1, "Acquisition failure. Expected message: 1=ACQ SUCCESS.");
+    const double delay_error_samples = std::abs(524.0 - gnss_synchro.Acq_delay_samples);
+    const auto delay_error_chips = static_cast<float>(delay_error_samples * 1023 / 4000);
+    const double doppler_error_hz = std::abs(1680.0 - gnss_synchro.Acq_doppler_hz);
+    EXPECT(doppler_error_hz <= 666, "Doppler error exceeds 666 Hz");
+    EXPECT(delay_error_chips < 0.5, "Delay error exceeds 0.5 chips");
+    EXPECT(acquisition.get_block()->num_doppler_bins() == 100, "D = ceil(2*5000/100)");
+    std::printf("acquisition: message %d delay %.1f samples doppler %.0f Hz stat %.3f stamp %llu\n", rx_message,
+        gnss_synchro.Acq_delay_samples, gnss_synchro.Acq_doppler_hz, acquisition.get_block()->test_statistics(),
+        static_cast<unsigned long long>(gnss_synchro.Acq_samplestamp_samples));
+}
+
+void test_multicorrelator(const std::vector<std::complex<float>>& capture)
+{
+    const int n = 4000;
+    const auto code = gps_l1_ca_code_gen_float(1, 0);
+    std::vector<float> shifts = {-0.5F, 0.0F, 0.5F};
+    Hip_Multicorrelator_Real_Codes corr;
+    corr.set_high_dynamics_resampler(false);  // dll_pll_veml_tracking sets it from high_dyn=false
+    EXPECT(corr.init(2 * n, 3), "init");
+    EXPECT(corr.set_local_code_and_taps(1023, code.data(), shifts.data()), "set_local_code_and_taps");
+    std::vector<std::complex<float>> out(3);
+    // align to the acquired code phase: start at sample 524, Doppler 1700 Hz
+    const std::complex<float>* sig = capture.data() + 524;
+    corr.set_input_output_vectors(out.data(), sig);
+    const float carr_step = static_cast<float>(2.0 * M_PI * 1700.0 / 4e6);
+    const float code_step = static_cast<float>(1.023e6 / 4e6);
+    EXPECT(corr.Carrier_wipeoff_multicorrelator_resampler(0.0F, carr_step, 0.0F, 0.0F, code_step, 0.0F, n), "run");
+    const auto ref = exact_correlation(sig, code, shifts, 0.0F, carr_step, 0.0F, code_step, n);
+    double num = 0.0, den = 0.0;
+    for (int k = 0; k < 3; ++k)
+        {
+            num += std::norm(std::complex<double>(out[k]) - ref[k]);
+            den += std::norm(ref[k]);
+        }
+    const double rel = std::sqrt(num / den);
+    EXPECT(rel < 1e-5, "real-code taps vs fp64 evaluation");
+    EXPECT(std::abs(out[1]) > std::abs(out[0]) && std::abs(out[1]) > std::abs(out[2]), "prompt is the largest tap");
+    std::printf("multicorrelator: |E| %.1f |P| %.1f |L| %.1f rel err %.2e\n", std::abs(out[0]), std::abs(out[1]),
+        std::abs(out[2]), rel);
+
+    // complex-replica drop-in on the same data: code (0, +-1) gives taps rotated by +j
+    const auto ccode = gps_l1_ca_code_gen_complex(1, 0);
+    Hip_Multicorrelator cc;
+    EXPECT(cc.init(2 * n, 3), "complex init");
+    EXPECT(cc.set_local_code_and_taps(1023, ccode.data(), shifts.data()), "complex set_local_code_and_taps");
+    std::vector<std::complex<float>> cout3(3);
+    cc.set_input_output_vectors(cout3.data(), sig);
+    EXPECT(cc.Carrier_wipeoff_multicorrelator_resampler(0.0F, carr_step, 0.0F, code_step, n), "complex run");
+    double cnum = 0.0;
+    for (int k = 0; k < 3; ++k) cnum += std::norm(std::complex<double>(cout3[k]) - std::complex<double>(0, 1) * ref[k]);
+    EXPECT(std::sqrt(cnum / den) < 1e-5, "complex-code taps");
+}
+}  // namespace
+
+int main(int argc, char** argv)
+{
+    if (argc < 2)
+        {
+            std::cerr << "usage: host_selftest <GPS_L1_CA_ID_1_Fs_4Msps_2ms.dat>\n";
+            return 2;
+        }
+    const auto capture = read_capture(argv[1]);
+    if (capture.size() < 8000)
+        {
+            std::cerr << "cannot read capture " << argv[1] << '\n';
+            return 2;
+        }
+    test_acquisition_validation(capture);
+    test_multicorrelator(capture);
+    if (failures == 0) std::printf("host_selftest: PASS\n");
+    return failures == 0 ? 0 : 1;
+}

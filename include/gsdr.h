@@ -146,6 +146,16 @@ int gsdr_acq_run_device(gsdr_acq* acq, const void* iq_dev, uint32_t nblocks, uin
  * (D rows of fft_size floats, Doppler-major).  Synchronous. */
 int gsdr_acq_dump_grid(gsdr_acq* acq, const void* iq_host, uint32_t prn_slot, float* grid_host);
 
+/* Stage profiling with HIP events recorded on the launch stream (observability,
+ * the role of the reference's per-block timing prints).  When enabled, every
+ * gsdr_acq_run / gsdr_acq_run_device call records device time per stage:
+ * [0] forward FFT (x .* w_d), [1] fused correlate (code product + inverse FFT +
+ * |.|^2 + row statistics), [2] grid reduction, [3] second-peak pass.
+ * gsdr_acq_read_profile synchronises, returns the sums since the last read
+ * (milliseconds) and the number of launches per stage, and resets them. */
+int gsdr_acq_set_profiling(gsdr_acq* acq, int enable);
+int gsdr_acq_read_profile(gsdr_acq* acq, double* stage_ms, uint32_t* launches);
+
 /* Debug/verification: device forward spectrum for one host block,
  * D rows x fft_size complex<float> (= FFT(x .* w_d)). */
 int gsdr_acq_dump_spectra(gsdr_acq* acq, const void* iq_host, float* spectra_host);
@@ -206,6 +216,18 @@ int gsdr_corr_run_batch(gsdr_corr* corr, const gsdr_corr_job* jobs_host, int njo
 /* Same, with the job table already in device memory (graph-capturable). */
 int gsdr_corr_run_batch_device(gsdr_corr* corr, const gsdr_corr_job* jobs_dev, int njobs, const void* iq_dev,
     int item_type, int64_t iq_items, float* out_dev, void* stream);
+
+/* Multi-epoch schedule: n_epochs consecutive batches of jobs_per_epoch jobs
+ * (jobs_dev holds n_epochs*jobs_per_epoch jobs, epoch-major).  Epoch e is one
+ * launch queued behind epoch e-1 on the stream — the launch order a tracking
+ * loop imposes — issued from native code.  Output of job j of epoch e at
+ * out_dev + 2*(e*jobs_per_epoch + j)*max_taps. */
+int gsdr_corr_run_epochs(gsdr_corr* corr, const gsdr_corr_job* jobs_dev, int jobs_per_epoch, int n_epochs,
+    const void* iq_dev, int item_type, int64_t iq_items, float* out_dev, void* stream);
+
+/* Kernel-time profiling with HIP events (see gsdr_acq_set_profiling). */
+int gsdr_corr_set_profiling(gsdr_corr* corr, int enable);
+int gsdr_corr_read_profile(gsdr_corr* corr, double* kernel_ms, uint32_t* launches);
 
 /* Debug/verification: the resampled code indices of one channel, as the
  * kernel computes them (n_taps rows x n samples int32, host). */

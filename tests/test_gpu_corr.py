@@ -174,3 +174,46 @@ def test_batched_channels_from_device_buffer(item_type):
                                                       float(j["code_phase_step_chips"]), int(j["n_samples"]))
         assert vnorm_rel(o[ch], exact) <= 1e-5
         assert vnorm_rel(o[ch], ref) <= 1e-3  # mostly noise taps here: bounded by the generic kernel's fp32 error
+
+
+@pytest.mark.parametrize("N", [1, 100, 1023, 1024, 1025, 5000, 20000])
+def test_chunk_boundaries(N):
+    """Jobs shorter than, equal to and straddling the per-workgroup chunk."""
+    fs = 4e6
+    code = synth.gps_ca_chips(2)
+    shifts = np.array([-0.5, 0.0, 0.5], np.float32)
+    x = _signal(fs, max(N, 1), 2, 900.0, 0.0, seed=N)
+    corr = gsdr.Correlator(1, 20000, max_taps=3)
+    corr.set_local_code_and_taps(0, code, shifts)
+    args = (0.2, float(np.float32(2 * np.pi * 900.0 / fs)), 0.05, float(np.float32(1.023e6 / fs)))
+    got = corr.run(0, x, *args, N)
+    exact = volk.multicorrelator_real_codes_exact(x, code, shifts, *args, N)
+    assert vnorm_rel(got, exact) <= 1e-5
+
+
+def test_run_epochs_matches_per_epoch_batches():
+    """gsdr_corr_run_epochs: n_epochs launches in order over one job table."""
+    fs, N, C, E = 4e6, 4000, 4, 6
+    sats = synth.random_constellation(C, seed_offset=31)
+    x = synth.gps_l1_iq(fs, N * (E + 1), sats, seed_offset=31)
+    shifts = np.array([-0.5, 0.0, 0.5], np.float32)
+    corr = gsdr.Correlator(C, N, max_taps=3)
+    for c, s in enumerate(sats):
+        corr.set_local_code_and_taps(c, synth.gps_ca_chips(s.prn), shifts)
+    jobs = np.zeros(C * E, gsdr.CORR_JOB_DTYPE)
+    for e in range(E):
+        for c, s in enumerate(sats):
+            jobs[e * C + c] = (c, N, e * N + 17 * c, 0.1 * e, np.float32(2 * np.pi * s.doppler_hz / fs), 0.0, 0.0,
+                               np.float32(1.023e6 / fs), 0.0)
+    dev = torch.from_numpy(x.view(np.float32)).cuda()
+    jdev = torch.from_numpy(jobs.view(np.uint8)).cuda()
+    out = torch.zeros(C * E * 3 * 2, dtype=torch.float32, device="cuda")
+    corr.run_epochs(jdev.data_ptr(), C, E, dev.data_ptr(), len(x), out.data_ptr())
+    torch.cuda.synchronize()
+    o = out.cpu().numpy().view(np.complex64).reshape(E * C, 3)
+    for i, j in enumerate(jobs):
+        seg = x[j["sample_offset"]:j["sample_offset"] + N]
+        ref = volk.multicorrelator_real_codes_exact(seg, synth.gps_ca_chips(sats[j["channel"]].prn), shifts,
+                                                    float(j["rem_carr_phase_rad"]), float(j["carr_phase_step_rad"]),
+                                                    0.0, float(j["code_phase_step_chips"]), N)
+        assert vnorm_rel(o[i], ref) <= 2e-5

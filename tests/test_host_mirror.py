@@ -33,7 +33,7 @@ int main() {
   cfg.set_property("Acquisition_1C.pfa", "0.01");
   cfg.set_property("Acquisition_1C.doppler_max", "10000");
   Acq_Conf a; a.SetFromConfiguration(&cfg, "Acquisition_1C", 1023000.0, 2000000.0);
-  std::printf("%lld %u %.9g %.9g %d %d %d\n", (long long)a.fs_in, a.samples_per_chip, a.samples_per_ms,
+  std::printf("%lld %u %.17g %.17g %d %d %d\n", (long long)a.fs_in, a.samples_per_chip, a.samples_per_ms,
               a.samples_per_code, a.doppler_max, (int)a.use_CFAR_algorithm_flag, (int)a.it_size);
   return 0;
 }

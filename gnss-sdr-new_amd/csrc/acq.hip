@@ -193,18 +193,38 @@ __global__ void __launch_bounds__(PT::NT) acq_correlate_kernel(const float2* __r
     extern __shared__ float2 lds[];
     RowStat* scratch = reinterpret_cast<RowStat*>(lds + plan.n);
     const uint32_t N = plan.n;
-    uint32_t d, p;
+    uint32_t d, p, b;
     if (GRID)
         {
             d = blockIdx.x;
             p = prn_slot_for_grid;
+            b = blockIdx.y;
         }
     else
         {
-            d = blockIdx.x / P;
-            p = blockIdx.x - d * P;
+            // XCD-aware mapping (cdna_hip_programming.md T1): workgroups are dealt
+            // round-robin over the 8 XCDs (id % 8), so give all P workgroups of one
+            // (b, d) spectrum the same id % 8 — X_{b,d} is then fetched into one
+            // XCD's L2 once instead of into all eight.  Speed only, never correctness.
+            const uint32_t nrows = gridDim.y * D;  // (b, d) rows
+            const uint32_t id = blockIdx.y * gridDim.x + blockIdx.x;
+            const uint32_t full = nrows >> 3;     // rows in the XCD-balanced part
+            uint32_t row;
+            if (id < full * 8u * P)
+                {
+                    const uint32_t xcd = id & 7u, slot = id >> 3;
+                    row = (slot / P) * 8u + xcd;
+                    p = slot - (slot / P) * P;
+                }
+            else
+                {
+                    const uint32_t t = id - full * 8u * P;  // the last nrows % 8 rows, linear
+                    row = full * 8u + t / P;
+                    p = t - (t / P) * P;
+                }
+            b = row / D;
+            d = row - b * D;
         }
-    const uint32_t b = blockIdx.y;
     const float2* x = X + ((size_t)b * D + d) * N;
     const float2* c = code_fft + (size_t)p * N;
     float best = -1.0f, sum = 0.0f;

@@ -376,8 +376,11 @@ __global__ void __launch_bounds__(kCorrThreads) corr_kernel(const gsdr_corr_job*
                 }
             return;
         }
-    // cross-chunk hand-off (MI355X_MICROARCH.md, inter-workgroup visibility): wave 0
-    // stores the partials, drains, releases at agent scope, then one atomic arrival.
+    // cross-chunk hand-off without cache-maintenance fences (MI355X_MICROARCH.md,
+    // "Valid forms", table row 1): wave 0 writes its partials with agent-scope
+    // (sc1, write-through) stores, drains them, then one lane arrives on the job's
+    // counter with an agent-scope atomic; the last arriver reads every partial with
+    // agent-scope (sc1) loads after its atomic has returned.
     if (wave == 0)
         {
             if (threadIdx.x < K)
@@ -389,36 +392,38 @@ __global__ void __launch_bounds__(kCorrThreads) corr_kernel(const gsdr_corr_job*
                             r.x += s_red[w][threadIdx.x].x;
                             r.y += s_red[w][threadIdx.x].y;
                         }
-                    partials[((size_t)jb * max_chunks + chunk) * kMaxTaps + threadIdx.x] = r;
+                    unsigned long long bits;
+                    __builtin_memcpy(&bits, &r, sizeof(bits));
+                    __hip_atomic_store(reinterpret_cast<unsigned long long*>(
+                                           &partials[((size_t)jb * max_chunks + chunk) * kMaxTaps + threadIdx.x]),
+                        bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (threadIdx.x == 0)
                 {
-                    const unsigned int prev = atomicAdd(&counters[jb], 1u);
+                    const unsigned int prev =
+                        __hip_atomic_fetch_add(&counters[jb], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     s_last = (prev == (unsigned int)(nchunks - 1)) ? 1 : 0;
                 }
         }
     __syncthreads();
     if (!s_last) return;
-    if (wave == 0)
+    if (threadIdx.x < K)
         {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (threadIdx.x < K)
+            float2 r = make_float2(0.f, 0.f);
+            for (int c = 0; c < nchunks; ++c)
                 {
-                    float2 r = make_float2(0.f, 0.f);
-                    for (int c = 0; c < nchunks; ++c)
-                        {
-                            const float2 v = partials[((size_t)jb * max_chunks + c) * kMaxTaps + threadIdx.x];
-                            r.x += v.x;
-                            r.y += v.y;
-                        }
-                    out[(size_t)jb * max_taps + threadIdx.x] = r;
+                    const unsigned long long bits = __hip_atomic_load(reinterpret_cast<unsigned long long*>(
+                                                                          &partials[((size_t)jb * max_chunks + c) * kMaxTaps + threadIdx.x]),
+                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    float2 v;
+                    __builtin_memcpy(&v, &bits, sizeof(v));
+                    r.x += v.x;
+                    r.y += v.y;
                 }
-            if (threadIdx.x == 0) counters[jb] = 0u;  // re-armed for the next launch on this stream
+            out[(size_t)jb * max_taps + threadIdx.x] = r;
         }
+    if (threadIdx.x == 0) counters[jb] = 0u;  // re-armed for the next launch on this stream
 }
 
 __global__ void corr_index_kernel(const ChanDev* __restrict__ chans, int channel, float rem, float step, int n_total,

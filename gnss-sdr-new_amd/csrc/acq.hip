@@ -18,12 +18,14 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
 #include <vector>
 
 #include "fft_lds.h"
+#include "fft_multi.h"
 #include "fft_plan.h"
 #include "gsdr_internal.h"
 
@@ -31,6 +33,9 @@ namespace
 {
 
 using gsdr::fft::Plan;
+
+// Default correlate variant at N = 4000 (see GSDR_CORR_VARIANTS).
+constexpr int kDefaultCorrVariant4000 = 7;
 
 struct RowStat
 {
@@ -252,6 +257,179 @@ __global__ void __launch_bounds__(PT::NT) acq_correlate_kernel(const float2* __r
         }
 }
 
+// ---------------------------------------------------------------- K_correlate (multi)
+// PB PRNs per workgroup: the PB transforms share the X_{b,d} loads and every
+// twiddle load, and interleave their dependency chains.  1-D grid over
+// (row = b*D + d, PRN group), XCD-aware like acq_correlate_kernel.
+template <class MP>
+__global__ void __launch_bounds__(MP::NT) acq_correlate_multi_kernel(const float2* __restrict__ X,
+    const float2* __restrict__ code_fft, RowStat* __restrict__ stats, const float2* __restrict__ tw, uint32_t D,
+    uint32_t P, uint32_t nblocks)
+{
+    constexpr int PB = MP::PB;
+    constexpr int NT = MP::NT;
+    constexpr int NW = NT / 64;
+    constexpr uint32_t N = MP::N;
+    extern __shared__ float2 lds[];
+    RowStat* scratch = reinterpret_cast<RowStat*>(lds + PB * MP::STRIDE);
+    const uint32_t G = (P + PB - 1) / PB;
+    const uint32_t nrows = nblocks * D;
+    const uint32_t id = blockIdx.x;
+    const uint32_t full = nrows >> 3;
+    uint32_t row, g;
+    if (id < full * 8u * G)
+        {
+            const uint32_t xcd = id & 7u, slot = id >> 3;
+            row = (slot / G) * 8u + xcd;
+            g = slot - (slot / G) * G;
+        }
+    else
+        {
+            const uint32_t t = id - full * 8u * G;
+            row = full * 8u + t / G;
+            g = t - (t / G) * G;
+        }
+    const uint32_t b = row / D, d = row - (row / D) * D;
+    const uint32_t p0 = g * PB;
+    const float2* x = X + (size_t)row * N;
+    const float2* c[PB];
+#pragma unroll
+    for (int t = 0; t < PB; ++t) c[t] = code_fft + (size_t)min(p0 + t, P - 1) * N;
+    float best[PB], sum[PB];
+    uint32_t bidx[PB];
+#pragma unroll
+    for (int t = 0; t < PB; ++t)
+        {
+            best[t] = -1.0f;
+            sum[t] = 0.0f;
+            bidx[t] = 0xffffffffu;
+        }
+    auto load = [&](int, int, int i, float2(&out)[PB]) {
+        const float2 a = x[i];
+#pragma unroll
+        for (int t = 0; t < PB; ++t)
+            {
+                const float2 k = c[t][i];
+                out[t] = make_float2(a.x * k.x + a.y * k.y, a.x * k.y - a.y * k.x);
+            }
+    };
+    auto store = [&](int i, const float2(&in)[PB]) {
+#pragma unroll
+        for (int t = 0; t < PB; ++t)
+            {
+                const float m = in[t].x * in[t].x + in[t].y * in[t].y;
+                if (stat_better(m, (uint32_t)i, best[t], bidx[t]))
+                    {
+                        best[t] = m;
+                        bidx[t] = (uint32_t)i;
+                    }
+                sum[t] += m;
+            }
+    };
+    MP::run(lds, tw, load, store);
+#pragma unroll
+    for (int t = 0; t < PB; ++t)
+        {
+            block_reduce_stat<NT>(best[t], bidx[t], sum[t], scratch + t * NW);
+            if (threadIdx.x == 0 && p0 + t < P) stats[((size_t)b * P + p0 + t) * D + d] = RowStat{best[t], bidx[t], sum[t], 0};
+        }
+}
+
+// ---------------------------------------------------------------- K_correlate (sequential PRN group)
+// One workgroup per (row = b*D + d, group of PG PRNs).  The lane's first-stage
+// inputs of X_{b,d} stay in VGPRs for the whole group; the next PRN's code-spectrum
+// values are loaded into the registers the current product has just consumed
+// (right after the first FFT stage), so their latency hides behind stages 2..S.
+template <class MP, int PG>
+__global__ void __launch_bounds__(MP::NT) acq_correlate_seq_kernel(const float2* __restrict__ X,
+    const float2* __restrict__ code_fft, RowStat* __restrict__ stats, const float2* __restrict__ tw, uint32_t D,
+    uint32_t P, uint32_t nblocks)
+{
+    static_assert(MP::PB == 1, "sequential kernel runs one transform at a time");
+    constexpr int NT = MP::NT;
+    constexpr int NW = NT / 64;
+    constexpr int R1 = MP::R1, BPT1 = MP::BPT1, NB1 = MP::NB1;
+    constexpr uint32_t N = MP::N;
+    extern __shared__ float2 lds[];
+    RowStat* scratch = reinterpret_cast<RowStat*>(lds + MP::STRIDE);
+    const uint32_t G = (P + PG - 1) / PG;
+    const uint32_t nrows = nblocks * D;
+    const uint32_t id = blockIdx.x;
+    const uint32_t full = nrows >> 3;
+    uint32_t row, g;
+    if (id < full * 8u * G)
+        {
+            const uint32_t xcd = id & 7u, slot = id >> 3;
+            row = (slot / G) * 8u + xcd;
+            g = slot - (slot / G) * G;
+        }
+    else
+        {
+            const uint32_t t = id - full * 8u * G;
+            row = full * 8u + t / G;
+            g = t - (t / G) * G;
+        }
+    const uint32_t b = row / D, d = row - (row / D) * D;
+    const uint32_t p0 = g * PG;
+    const int np = (int)min((uint32_t)PG, P - p0);
+    const float2* x = X + (size_t)row * N;
+    float2 xr[BPT1][R1], cr[BPT1][R1];
+    {
+        const float2* c = code_fft + (size_t)p0 * N;
+#pragma unroll
+        for (int bb = 0; bb < BPT1; ++bb)
+            {
+                const int j = (int)threadIdx.x + bb * NT;
+                if (j < NB1)
+                    {
+#pragma unroll
+                        for (int r = 0; r < R1; ++r)
+                            {
+                                xr[bb][r] = x[j + r * NB1];
+                                cr[bb][r] = c[j + r * NB1];
+                            }
+                    }
+            }
+    }
+    for (int q = 0; q < np; ++q)
+        {
+            float best = -1.0f, sum = 0.0f;
+            uint32_t bidx = 0xffffffffu;
+            auto load = [&](int bb, int r, int, float2(&out)[1]) {
+                const float2 a = xr[bb][r], k = cr[bb][r];
+                out[0] = make_float2(a.x * k.x + a.y * k.y, a.x * k.y - a.y * k.x);
+            };
+            auto hook = [&]() {
+                if (q + 1 < np)
+                    {
+                        const float2* c = code_fft + (size_t)(p0 + q + 1) * N;
+#pragma unroll
+                        for (int bb = 0; bb < BPT1; ++bb)
+                            {
+                                const int j = (int)threadIdx.x + bb * NT;
+                                if (j < NB1)
+                                    {
+#pragma unroll
+                                        for (int r = 0; r < R1; ++r) cr[bb][r] = c[j + r * NB1];
+                                    }
+                            }
+                    }
+            };
+            auto store = [&](int i, const float2(&in)[1]) {
+                const float m = in[0].x * in[0].x + in[0].y * in[0].y;
+                if (stat_better(m, (uint32_t)i, best, bidx))
+                    {
+                        best = m;
+                        bidx = (uint32_t)i;
+                    }
+                sum += m;
+            };
+            MP::run(lds, tw, load, store, hook);
+            block_reduce_stat<NT>(best, bidx, sum, scratch + (q & 1) * NW);
+            if (threadIdx.x == 0) stats[((size_t)b * P + p0 + q) * D + d] = RowStat{best, bidx, sum, 0};
+        }
+}
+
 // ---------------------------------------------------------------- K_reduce
 // One wave per (b, p).  Rows are scanned in increasing d by each lane and merged
 // with the (max desc, d asc) order, reproducing the reference's strict '>' scan.
@@ -375,6 +553,8 @@ struct gsdr_acq
     float threshold{0.0f};
     int nt{256};
     int variant{0};
+    int corr_variant{0};      // 0: single-transform correlate kernel; >0: GSDR_CORR_VARIANTS id
+    size_t corr_lds_bytes{0};
     Plan plan{};
     size_t lds_bytes{0};
     hipStream_t stream{nullptr};
@@ -419,6 +599,27 @@ size_t item_bytes(int it) { return it == GSDR_ITEM_CSHORT ? 4 : 8; }
     X(10, (RuntimePlan<256>))              \
     X(11, (RuntimePlan<512>))              \
     X(12, (RuntimePlan<1024>))
+
+using gsdr::fft::MultiPlan;
+
+// Correlate-kernel variants for N = 4000 (env GSDR_ACQ_CORR_VARIANT selects one;
+// 0 = the single-transform kernel of the plan variant).
+#define GSDR_CORR_VARIANTS(X)                                \
+    X(5, (MultiPlan<256, 1, false, false, 25, 16, 10>))     \
+    X(7, (MultiPlan<256, 1, false, true, 25, 16, 10>))      \
+    X(8, (MultiPlan<256, 1, false, true, 20, 20, 10>))      \
+    X(11, (MultiPlan<256, 1, true, true, 20, 20, 10>))      \
+    X(12, (MultiPlan<256, 1, false, true, 16, 25, 10>))     \
+    X(13, (MultiPlan<256, 1, false, true, 16, 10, 25>))
+
+// Sequential-PRN-group variants: (id, plan, PRNs per workgroup).
+#define GSDR_SEQ_VARIANTS(X)                                      \
+    X(20, (MultiPlan<256, 1, false, true, 16, 25, 10>), 4)       \
+    X(21, (MultiPlan<256, 1, false, true, 16, 25, 10>), 8)       \
+    X(22, (MultiPlan<256, 1, false, true, 16, 25, 10>), 16)      \
+    X(23, (MultiPlan<256, 1, false, true, 25, 16, 10>), 8)       \
+    X(24, (MultiPlan<256, 1, false, true, 20, 20, 10>), 8)       \
+    X(25, (MultiPlan<256, 1, false, true, 16, 10, 25>), 8)
 
 template <class PT>
 int set_lds_attrs(size_t bytes)
@@ -513,6 +714,73 @@ struct StageTimer
     }
 };
 
+int launch_corr_variant(gsdr_acq* a, uint32_t nblocks, hipStream_t s)
+{
+#define GSDR_CV_CASE(ID, MP)                                                                                    \
+    case ID:                                                                                                    \
+        {                                                                                                       \
+            using M = GSDR_UNPAREN MP;                                                                          \
+            const uint32_t groups = (a->nprn + M::PB - 1) / M::PB;                                              \
+            hipLaunchKernelGGL((acq_correlate_multi_kernel<M>), dim3(nblocks * a->D * groups), dim3(M::NT),     \
+                a->corr_lds_bytes, s, a->d_X, a->d_code_fft, a->d_stats, a->d_tw, a->D, a->nprn, nblocks);      \
+            return GSDR_OK;                                                                                     \
+        }
+#define GSDR_SQ_CASE(ID, MP, PG)                                                                                \
+    case ID:                                                                                                    \
+        {                                                                                                       \
+            using M = GSDR_UNPAREN MP;                                                                          \
+            const uint32_t groups = (a->nprn + (PG)-1) / (PG);                                                  \
+            hipLaunchKernelGGL((acq_correlate_seq_kernel<M, PG>), dim3(nblocks * a->D * groups), dim3(M::NT),  \
+                a->corr_lds_bytes, s, a->d_X, a->d_code_fft, a->d_stats, a->d_tw, a->D, a->nprn, nblocks);      \
+            return GSDR_OK;                                                                                     \
+        }
+#define GSDR_UNPAREN(...) __VA_ARGS__
+    switch (a->corr_variant)
+        {
+            GSDR_CORR_VARIANTS(GSDR_CV_CASE)
+            GSDR_SEQ_VARIANTS(GSDR_SQ_CASE)
+        default: gsdr::set_error("internal: bad correlate variant %d", a->corr_variant); return GSDR_E_STATE;
+        }
+#undef GSDR_CV_CASE
+#undef GSDR_SQ_CASE
+#undef GSDR_UNPAREN
+}
+
+// Select and configure a correlate variant (N must be 4000).
+int setup_corr_variant(gsdr_acq* a, int v)
+{
+#define GSDR_CV_SETUP(ID, MP)                                                                                   \
+    case ID:                                                                                                    \
+        {                                                                                                       \
+            using M = GSDR_UNPAREN MP;                                                                          \
+            a->corr_lds_bytes = M::lds_bytes() + (size_t)M::PB * (M::NT / 64) * sizeof(RowStat);               \
+            GSDR_HIP(hipFuncSetAttribute((const void*)acq_correlate_multi_kernel<M>,                           \
+                hipFuncAttributeMaxDynamicSharedMemorySize, (int)a->corr_lds_bytes));                           \
+            a->corr_variant = ID;                                                                               \
+            return GSDR_OK;                                                                                     \
+        }
+#define GSDR_SQ_SETUP(ID, MP, PG)                                                                               \
+    case ID:                                                                                                    \
+        {                                                                                                       \
+            using M = GSDR_UNPAREN MP;                                                                          \
+            a->corr_lds_bytes = M::lds_bytes() + (size_t)2 * (M::NT / 64) * sizeof(RowStat);                   \
+            GSDR_HIP(hipFuncSetAttribute((const void*)acq_correlate_seq_kernel<M, PG>,                         \
+                hipFuncAttributeMaxDynamicSharedMemorySize, (int)a->corr_lds_bytes));                           \
+            a->corr_variant = ID;                                                                               \
+            return GSDR_OK;                                                                                     \
+        }
+#define GSDR_UNPAREN(...) __VA_ARGS__
+    switch (v)
+        {
+            GSDR_CORR_VARIANTS(GSDR_CV_SETUP)
+            GSDR_SEQ_VARIANTS(GSDR_SQ_SETUP)
+        default: a->corr_variant = 0; return GSDR_OK;
+        }
+#undef GSDR_CV_SETUP
+#undef GSDR_SQ_SETUP
+#undef GSDR_UNPAREN
+}
+
 template <class PT>
 void launch_forward(gsdr_acq* a, const void* iq, int item_type, uint32_t nblocks, uint64_t stride, hipStream_t s)
 {
@@ -535,8 +803,16 @@ int launch_all(gsdr_acq* a, const void* iq, int item_type, uint32_t nblocks, uin
     GSDR_HIP(hipGetLastError());
     t.end(0);
     t.begin();
-    hipLaunchKernelGGL((acq_correlate_kernel<PT, false>), dim3(a->D * a->nprn, nblocks), dim3(PT::NT), lds, s,
-        a->d_X, a->d_code_fft, a->d_stats, (float*)nullptr, a->d_tw, a->plan, a->D, a->nprn, 0u);
+    if (a->corr_variant > 0)
+        {
+            int rc = launch_corr_variant(a, nblocks, s);
+            if (rc != GSDR_OK) return rc;
+        }
+    else
+        {
+            hipLaunchKernelGGL((acq_correlate_kernel<PT, false>), dim3(a->D * a->nprn, nblocks), dim3(PT::NT), lds, s,
+                a->d_X, a->d_code_fft, a->d_stats, (float*)nullptr, a->d_tw, a->plan, a->D, a->nprn, 0u);
+        }
     GSDR_HIP(hipGetLastError());
     t.end(1);
     AcqParams ap = params_of(a);
@@ -696,6 +972,12 @@ int gsdr_acq_create(int device, const gsdr_acq_conf* conf, gsdr_acq** out)
             return GSDR_E_UNSUPPORTED;
         }
     int rc = dispatch(a, 4, nullptr, 0, 0, 0, nullptr, nullptr, 0);
+    if (rc == GSDR_OK && N == 4000)
+        {
+            int v = kDefaultCorrVariant4000;
+            if (const char* e = std::getenv("GSDR_ACQ_CORR_VARIANT")) v = std::atoi(e);
+            rc = setup_corr_variant(a, v);
+        }
     if (rc != GSDR_OK)
         {
             delete a;

@@ -29,7 +29,7 @@ namespace
 
 constexpr int kMaxTaps = 8;
 constexpr int kCorrThreads = 256;
-constexpr int kSamplesPerThread = 4;
+constexpr int kSamplesPerThread = 16;
 constexpr int kChunk = kCorrThreads * kSamplesPerThread;  // samples per workgroup
 constexpr int kMaxCodeSamples = 16384;                    // replica length limit (floats; complex codes 2x)
 constexpr int kSpanCap = 4096;                            // LDS-staged replica span per chunk (entries)
@@ -128,7 +128,7 @@ enum SpanMode
 template <int IT, bool CPLX, bool HD>
 __device__ __forceinline__ void chunk_accumulate(const gsdr_corr_job& job, const ChanDev& ch, const float* s_code,
     int mode, int lo, const int* s_hdshift, double psi0, double th, double thr, float2 wstep, int n0, int n1,
-    const void* __restrict__ iq, int64_t iq_items, int assoc, float2 (*s_red)[kMaxTaps])
+    const float2 (&xs)[kSamplesPerThread], int assoc, float2 (*s_red)[kMaxTaps])
 {
     float2 acc[kMaxTaps];
 #pragma unroll
@@ -155,8 +155,7 @@ __device__ __forceinline__ void chunk_accumulate(const gsdr_corr_job& job, const
             const int n = n0 + (int)threadIdx.x + it * kCorrThreads;
             if (n < n1)
                 {
-                    const int64_t item = job.sample_offset + n;
-                    const float2 x = (item >= 0 && item < iq_items) ? load_item<IT>(iq, item) : make_float2(0.f, 0.f);
+                    const float2 x = xs[it];
                     float2 r = ph;
                     if (HD)
                         {
@@ -261,6 +260,17 @@ __global__ void __launch_bounds__(kCorrThreads) corr_kernel(const gsdr_corr_job*
     const int n1 = min(N, n0 + kChunk);
     const bool hd = ch.high_dyn != 0;
 
+    // issue this lane's IQ loads first: they depend on the job only, so their
+    // latency overlaps the replica-span staging below
+    float2 xs[kSamplesPerThread];
+#pragma unroll
+    for (int it = 0; it < kSamplesPerThread; ++it)
+        {
+            const int n = n0 + (int)threadIdx.x + it * kCorrThreads;
+            const int64_t item = job.sample_offset + n;
+            xs[it] = (n < n1 && item >= 0 && item < iq_items) ? load_item<IT>(iq, item) : make_float2(0.f, 0.f);
+        }
+
     if (threadIdx.x == 0)
         {
             double psi0, th, thr;
@@ -343,20 +353,20 @@ __global__ void __launch_bounds__(kCorrThreads) corr_kernel(const gsdr_corr_job*
     if (hd)
         {
             if (ch.cplx)
-                chunk_accumulate<IT, true, true>(job, ch, s_code, mode, lo, s_hdshift, psi0, th, thr, ws, n0, n1, iq,
-                    iq_items, assoc, s_red);
+                chunk_accumulate<IT, true, true>(job, ch, s_code, mode, lo, s_hdshift, psi0, th, thr, ws, n0, n1, xs,
+                    assoc, s_red);
             else
-                chunk_accumulate<IT, false, true>(job, ch, s_code, mode, lo, s_hdshift, psi0, th, thr, ws, n0, n1, iq,
-                    iq_items, assoc, s_red);
+                chunk_accumulate<IT, false, true>(job, ch, s_code, mode, lo, s_hdshift, psi0, th, thr, ws, n0, n1, xs,
+                    assoc, s_red);
         }
     else
         {
             if (ch.cplx)
-                chunk_accumulate<IT, true, false>(job, ch, s_code, mode, lo, s_hdshift, psi0, th, thr, ws, n0, n1, iq,
-                    iq_items, assoc, s_red);
+                chunk_accumulate<IT, true, false>(job, ch, s_code, mode, lo, s_hdshift, psi0, th, thr, ws, n0, n1, xs,
+                    assoc, s_red);
             else
-                chunk_accumulate<IT, false, false>(job, ch, s_code, mode, lo, s_hdshift, psi0, th, thr, ws, n0, n1, iq,
-                    iq_items, assoc, s_red);
+                chunk_accumulate<IT, false, false>(job, ch, s_code, mode, lo, s_hdshift, psi0, th, thr, ws, n0, n1, xs,
+                    assoc, s_red);
         }
 
     const int wave = threadIdx.x >> 6;

@@ -26,6 +26,7 @@
 
 #include "fft_lds.h"
 #include "fft_multi.h"
+#include "fft_pk.h"
 #include "fft_plan.h"
 #include "gsdr_internal.h"
 
@@ -35,7 +36,7 @@ namespace
 using gsdr::fft::Plan;
 
 // Default correlate variant at N = 4000 (see GSDR_CORR_VARIANTS).
-constexpr int kDefaultCorrVariant4000 = 7;
+constexpr int kDefaultCorrVariant4000 = 30;
 
 struct RowStat
 {
@@ -430,6 +431,102 @@ __global__ void __launch_bounds__(MP::NT) acq_correlate_seq_kernel(const float2*
         }
 }
 
+// ---------------------------------------------------------------- K_correlate (packed f32)
+// The sequential-PRN-group kernel on the packed-f32 FFT (fft_pk.h): one workgroup
+// per (row = b*D + d, group of PG PRNs), XCD-aware; the lane's first-stage inputs
+// of X_{b,d} stay in VGPRs for the whole group and the next PRN's code-spectrum
+// values are fetched by the hook while the current transform runs.  The last
+// stage visits each lane's outputs in increasing index order, so a strict '>'
+// keeps the lane's first maximum (the reference's index_max semantics).
+template <class MP, int PG, int WPE>
+__global__ void __launch_bounds__(MP::NT) __attribute__((amdgpu_waves_per_eu(WPE))) acq_correlate_pk_kernel(const float2* __restrict__ X,
+    const float2* __restrict__ code_fft, RowStat* __restrict__ stats, const float2* __restrict__ tw, uint32_t D,
+    uint32_t P, uint32_t nblocks)
+{
+    using gsdr::pk::c2;
+    constexpr int NT = MP::NT;
+    constexpr int NW = NT / 64;
+    constexpr int R1 = MP::R1, BPT1 = MP::BPT1, NB1 = MP::NB1;
+    constexpr uint32_t N = MP::N;
+    extern __shared__ float2 lds_raw[];
+    c2* lds = reinterpret_cast<c2*>(lds_raw);
+    RowStat* scratch = reinterpret_cast<RowStat*>(lds_raw + N);
+    const uint32_t G = (P + PG - 1) / PG;
+    const uint32_t nrows = nblocks * D;
+    const uint32_t id = blockIdx.x;
+    const uint32_t full = nrows >> 3;
+    uint32_t row, g;
+    if (id < full * 8u * G)
+        {
+            const uint32_t xcd = id & 7u, slot = id >> 3;
+            row = (slot / G) * 8u + xcd;
+            g = slot - (slot / G) * G;
+        }
+    else
+        {
+            const uint32_t t = id - full * 8u * G;
+            row = full * 8u + t / G;
+            g = t - (t / G) * G;
+        }
+    const uint32_t b = row / D, d = row - (row / D) * D;
+    const uint32_t p0 = g * PG;
+    const int np = (int)min((uint32_t)PG, P - p0);
+    const c2* x = reinterpret_cast<const c2*>(X) + (size_t)row * N;
+    c2 xr[BPT1][R1], cr[BPT1][R1];
+    {
+        const c2* c = reinterpret_cast<const c2*>(code_fft) + (size_t)p0 * N;
+#pragma unroll
+        for (int bb = 0; bb < BPT1; ++bb)
+            {
+                const int j = (int)threadIdx.x + bb * NT;
+                if (NB1 % NT == 0 || j < NB1)
+                    {
+#pragma unroll
+                        for (int r = 0; r < R1; ++r)
+                            {
+                                xr[bb][r] = x[j + r * NB1];
+                                cr[bb][r] = c[j + r * NB1];
+                            }
+                    }
+            }
+    }
+    for (int q = 0; q < np; ++q)
+        {
+            float best = -1.0f, sum = 0.0f;
+            uint32_t bidx = 0xffffffffu;
+            // conj(X . conj(C)) = conj(X) . C ; |IFFT(Y)| = |FFT(conj(Y))|
+            auto load = [&](int bb, int r, int) -> c2 { return gsdr::pk::conj_mul(xr[bb][r], cr[bb][r]); };
+            auto hook = [&]() {
+                if (q + 1 < np)
+                    {
+                        const c2* c = reinterpret_cast<const c2*>(code_fft) + (size_t)(p0 + q + 1) * N;
+#pragma unroll
+                        for (int bb = 0; bb < BPT1; ++bb)
+                            {
+                                const int j = (int)threadIdx.x + bb * NT;
+                                if (NB1 % NT == 0 || j < NB1)
+                                    {
+#pragma unroll
+                                        for (int r = 0; r < R1; ++r) cr[bb][r] = c[j + r * NB1];
+                                    }
+                            }
+                    }
+            };
+            auto store = [&](int i, c2 v) {
+                const float m = __builtin_fmaf(v.x, v.x, v.y * v.y);
+                if (m > best)
+                    {
+                        best = m;
+                        bidx = (uint32_t)i;
+                    }
+                sum += m;
+            };
+            MP::run(lds, tw, load, store, hook);
+            block_reduce_stat<NT>(best, bidx, sum, scratch + (q & 1) * NW);
+            if (threadIdx.x == 0) stats[((size_t)b * P + p0 + q) * D + d] = RowStat{best, bidx, sum, 0};
+        }
+}
+
 // ---------------------------------------------------------------- K_reduce
 // One wave per (b, p).  Rows are scanned in increasing d by each lane and merged
 // with the (max desc, d asc) order, reproducing the reference's strict '>' scan.
@@ -621,6 +718,17 @@ using gsdr::fft::MultiPlan;
     X(24, (MultiPlan<256, 1, false, true, 20, 20, 10>), 8)       \
     X(25, (MultiPlan<256, 1, false, true, 16, 10, 25>), 8)
 
+// Packed-f32 variants: (id, plan, PRNs per workgroup).
+#define GSDR_PK_VARIANTS(X)                                              \
+    X(30, (gsdr::pk::PkPlan<256, true, 25, 16, 10>), 1, 1)              \
+    X(31, (gsdr::pk::PkPlan<256, true, 25, 16, 10>), 1, 5)              \
+    X(32, (gsdr::pk::PkPlan<256, true, 25, 16, 10>), 2, 5)              \
+    X(33, (gsdr::pk::PkPlan<256, true, 20, 20, 10>), 1, 5)              \
+    X(34, (gsdr::pk::PkPlan<256, false, 25, 16, 10>), 1, 5)             \
+    X(35, (gsdr::pk::PkPlan<256, true, 20, 20, 10>), 1, 1)              \
+    X(36, (gsdr::pk::PkPlan<256, true, 25, 16, 10>), 4, 4)              \
+    X(37, (gsdr::pk::PkPlan<256, true, 20, 20, 10>), 2, 5)
+
 template <class PT>
 int set_lds_attrs(size_t bytes)
 {
@@ -734,15 +842,26 @@ int launch_corr_variant(gsdr_acq* a, uint32_t nblocks, hipStream_t s)
                 a->corr_lds_bytes, s, a->d_X, a->d_code_fft, a->d_stats, a->d_tw, a->D, a->nprn, nblocks);      \
             return GSDR_OK;                                                                                     \
         }
+#define GSDR_PK_CASE(ID, MP, PG, WPE)                                                                                \
+    case ID:                                                                                                    \
+        {                                                                                                       \
+            using M = GSDR_UNPAREN MP;                                                                          \
+            const uint32_t groups = (a->nprn + (PG)-1) / (PG);                                                  \
+            hipLaunchKernelGGL((acq_correlate_pk_kernel<M, PG, WPE>), dim3(nblocks * a->D * groups), dim3(M::NT),   \
+                a->corr_lds_bytes, s, a->d_X, a->d_code_fft, a->d_stats, a->d_tw, a->D, a->nprn, nblocks);      \
+            return GSDR_OK;                                                                                     \
+        }
 #define GSDR_UNPAREN(...) __VA_ARGS__
     switch (a->corr_variant)
         {
             GSDR_CORR_VARIANTS(GSDR_CV_CASE)
             GSDR_SEQ_VARIANTS(GSDR_SQ_CASE)
+            GSDR_PK_VARIANTS(GSDR_PK_CASE)
         default: gsdr::set_error("internal: bad correlate variant %d", a->corr_variant); return GSDR_E_STATE;
         }
 #undef GSDR_CV_CASE
 #undef GSDR_SQ_CASE
+#undef GSDR_PK_CASE
 #undef GSDR_UNPAREN
 }
 
@@ -769,15 +888,27 @@ int setup_corr_variant(gsdr_acq* a, int v)
             a->corr_variant = ID;                                                                               \
             return GSDR_OK;                                                                                     \
         }
+#define GSDR_PK_SETUP(ID, MP, PG, WPE)                                                                               \
+    case ID:                                                                                                    \
+        {                                                                                                       \
+            using M = GSDR_UNPAREN MP;                                                                          \
+            a->corr_lds_bytes = M::lds_bytes() + (size_t)2 * (M::NT / 64) * sizeof(RowStat);                   \
+            GSDR_HIP(hipFuncSetAttribute((const void*)acq_correlate_pk_kernel<M, PG, WPE>,                          \
+                hipFuncAttributeMaxDynamicSharedMemorySize, (int)a->corr_lds_bytes));                           \
+            a->corr_variant = ID;                                                                               \
+            return GSDR_OK;                                                                                     \
+        }
 #define GSDR_UNPAREN(...) __VA_ARGS__
     switch (v)
         {
             GSDR_CORR_VARIANTS(GSDR_CV_SETUP)
             GSDR_SEQ_VARIANTS(GSDR_SQ_SETUP)
+            GSDR_PK_VARIANTS(GSDR_PK_SETUP)
         default: a->corr_variant = 0; return GSDR_OK;
         }
 #undef GSDR_CV_SETUP
 #undef GSDR_SQ_SETUP
+#undef GSDR_PK_SETUP
 #undef GSDR_UNPAREN
 }
 

@@ -2,11 +2,15 @@
 """Benchmark: IQ Msamples/s processed (acquisition + tracking) on BASELINE config C2.
 
 One step = one batch of B consecutive 1 ms blocks of synthetic GPS L1 C/A IQ at
-4 Msps already resident in HBM; for every block:
-  - a full PCPS acquisition grid: 32 PRNs x 81 Doppler bins (+-10 kHz, 250 Hz), CFAR
-    (pfa 0.01) — pcps_acquisition::acquisition_core for all PRNs of the block;
-  - one 3-tap E-P-L correlator epoch (N = 4000 samples) for each of the 8 tracked
-    channels — Cpu_Multicorrelator_Real_Codes, one launch per epoch, epochs in order.
+4 Msps already resident in HBM; over the batch:
+  - a full PCPS acquisition grid per block: 32 PRNs x 81 Doppler bins (+-10 kHz,
+    250 Hz), CFAR (pfa 0.01) -- pcps_acquisition::acquisition_core for all PRNs;
+  - closed-loop DLL/PLL tracking of the 8 visible satellites over the same span:
+    every general_work call of dll_pll_veml_tracking (3-tap E-P-L correlation of
+    4000 samples + discriminators + loop filters + NCO update + lock detectors),
+    device-resident (gsdr_trk_run_device), the channel state restored to the same
+    start each step so every step re-tracks the same 64 ms.
+Acquisition and tracking run on two HIP streams (they are independent work).
 Whole-job throughput = blocks * 4000 samples * ranks / max-over-ranks wall time.
 
 Multi-GPU: one process per GPU (torch.distributed.run); every rank processes its
@@ -57,40 +61,47 @@ def trk_bytes_per_epoch():
     return 8 * N + 8 * TAPS
 
 
+def acq_result_for(s):
+    """What acquisition reports for satellite s at stamp 0: code-start sample, grid Doppler."""
+    tau = s.code_delay_chips / 1.023e6 * FS
+    return float(round(tau) % N), float(DSTEP * round(s.doppler_hz / DSTEP))
+
+
+def trk_conf(nch):
+    import gsdr
+    c = gsdr.trk_conf_default()
+    c["fs_in"] = FS
+    c["pll_bw_hz"] = 40.0   # conf/gnss-sdr_GPS_L1_gr_complex.conf:66-67
+    c["dll_bw_hz"] = 4.0
+    c["max_channels"] = nch
+    return c
+
+
 def make_workload(blocks, rank):
     from gsdr import synth
     sats = synth.random_constellation(CHANNELS, seed_offset=100 + rank)
     iq = synth.gps_l1_iq(FS, blocks * N, sats, seed_offset=100 + rank)
     codes = np.stack([synth.gps_ca_sampled(p, FS) for p in range(1, P + 1)])
-    # tracking job table: channel c, epoch e, aligned to the code start of the
-    # true signal, NCO parameters from the simulated truth (open loop)
-    import gsdr
-    jobs = np.zeros(blocks * CHANNELS, gsdr.CORR_JOB_DTYPE)
-    for e in range(blocks):
-        for c, s in enumerate(sats):
-            chips_per_sample = 1.023e6 / FS
-            start = e * N + int(round((s.code_delay_chips / 1.023e6) * FS)) % N
-            rem_code = start * chips_per_sample - s.code_delay_chips
-            rem_code -= round(rem_code)
-            # phase_offset = exp(-j*rem) and phase_inc = exp(-j*step) wipe off exp(+j*(2*pi*f*t + theta))
-            carr = (2 * np.pi * s.doppler_hz * start / FS + s.phase) % (2 * np.pi)
-            jobs[e * CHANNELS + c] = (c, N, start, np.float32(carr), np.float32(2 * np.pi * s.doppler_hz / FS), 0.0,
-                                      np.float32(-rem_code), np.float32(chips_per_sample), 0.0)
-    return sats, iq, codes, jobs
+    return sats, iq, codes
 
 
-def cpu_baseline(iq, codes, sats, jobs, budget_s=12.0):
+def cpu_baseline(iq, codes, sats, budget_s=12.0):
     """Oracle restatement on this host's CPU (1 thread): numpy pocketfft complex64
     PCPS (acquisition_core + CFAR statistic) for all 32 PRNs x 81 bins of a block,
-    plus the scalar generic VOLK correlator for every channel-epoch of the block."""
-    from oracle import pcps, volk
+    plus the C restatement of dll_pll_veml_tracking (generic VOLK correlator + loop)
+    for every channel's general_work call in the block."""
+    from oracle import pcps, trk
+    from gsdr import synth
     wipe = pcps.doppler_wipeoffs(FS, N, DMAX, DSTEP, D)
     cconj = np.conj(np.fft.fft(codes.astype(np.complex64), axis=1)).astype(np.complex64)
-    shifts = np.array([-0.5, 0.0, 0.5], np.float32)
-    chips = [None] * CHANNELS
-    from gsdr import synth
-    for c, s in enumerate(sats):
-        chips[c] = synth.gps_ca_chips(s.prn)
+    chans = []
+    for s in sats:
+        o = trk.Channel(trk_conf(1).view(trk.TRK_CONF_DTYPE))
+        delay, dop = acq_result_for(s)
+        first = o.start(synth.gps_ca_chips(s.prn), delay, dop, 0, 0)
+        chans.append([o, first])
+    rec = np.zeros(1, trk.TRK_EPOCH_DTYPE)
+    L = trk._lib()
 
     def one_block(b):
         x = iq[b * N:(b + 1) * N]
@@ -99,26 +110,24 @@ def cpu_baseline(iq, codes, sats, jobs, budget_s=12.0):
             R = np.fft.ifft(X * cconj[p][None, :], axis=1) * N
             M = (R.real * R.real + R.imag * R.imag).astype(np.float32)
             pcps.max_to_input_power_statistic(M)
-        for c in range(CHANNELS):
-            j = jobs[b * CHANNELS + c]
-            seg = iq[j["sample_offset"]:j["sample_offset"] + N]
-            if len(seg) < N:
-                seg = np.concatenate([seg, np.zeros(N - len(seg), np.complex64)])
-            volk.multicorrelator_real_codes(seg, chips[c], shifts, float(j["rem_carr_phase_rad"]),
-                                            float(j["carr_phase_step_rad"]), float(j["rem_code_phase_chips"]),
-                                            float(j["code_phase_step_chips"]), N)
+        for c in chans:
+            o, n = c
+            if n + N <= len(iq):
+                L.orc_trk_call(o._h, iq[n:].ctypes.data, n, rec.ctypes.data)
+                c[1] = n + int(rec["consumed"][0])
 
     t0 = time.perf_counter()
     one_block(0)
     t1 = time.perf_counter() - t0
-    nblk = int(max(1, min(len(iq) // N, math.ceil(budget_s / max(t1, 1e-3)))))
+    nblk = int(max(1, min(len(iq) // N - 1, math.ceil(budget_s / max(t1, 1e-3)))))
     t0 = time.perf_counter()
-    for b in range(nblk):
+    for b in range(1, nblk + 1):
         one_block(b)
     dt = time.perf_counter() - t0
     return {"value": round(nblk * N / dt / 1e6, 5), "unit": "Msamples/s", "cores": 1, "kind": "port",
             "sample": "%d blocks of 1 ms (4000 samples): 32 PRN x 81 Doppler CFAR PCPS (numpy pocketfft complex64) "
-                      "+ 8 x 3-tap generic VOLK correlator epochs each; %.1f s on one host core" % (nblk, dt)}
+                      "+ one dll_pll_veml_tracking call (C restatement: generic VOLK 3-tap correlator + DLL/PLL) "
+                      "for each of 8 channels; %.1f s on one host core" % (nblk, dt)}
 
 
 def load_pmc_traffic():
@@ -164,27 +173,27 @@ def main():
     dev = torch.device("cuda", local)
     B = args.blocks
 
-    sats, iq, codes, jobs = make_workload(B, rank)
+    sats, iq, codes = make_workload(B, rank)
     iq_dev = torch.from_numpy(iq.view(np.float32).copy()).to(dev)
-    jobs_dev = torch.from_numpy(jobs.view(np.uint8).copy()).to(dev)
     res_dev = torch.zeros(B * P * gsdr.ACQ_RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
-    trk_dev = torch.zeros(B * CHANNELS * TAPS * 2, dtype=torch.float32, device=dev)
+    trk_out = torch.zeros(CHANNELS * B * gsdr.TRK_EPOCH_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    trk_n = torch.zeros(CHANNELS, dtype=torch.int32, device=dev)
 
     acq = gsdr.Acquisition(FS, N, DMAX, DSTEP, pfa=PFA, max_prns=P, max_blocks=B, num_doppler_bins=D, device=local)
     acq.set_local_codes(codes, np.arange(1, P + 1))
-    corr = gsdr.Correlator(CHANNELS, N, max_taps=TAPS, device=local)
-    shifts = np.array([-0.5, 0.0, 0.5], np.float32)
+    trk = gsdr.Tracking(trk_conf(CHANNELS), device=local)
     from gsdr import synth
     for c, s in enumerate(sats):
-        corr.set_local_code_and_taps(c, synth.gps_ca_chips(s.prn), shifts)
-
-    stream = torch.cuda.current_stream(dev)
-    sptr = stream.cuda_stream
+        delay, dop = acq_result_for(s)
+        trk.start(c, s.prn, synth.gps_ca_chips(s.prn), delay, dop, 0, 0)
+    acq_stream = torch.cuda.Stream(dev)
+    trk_stream = torch.cuda.Stream(dev)
+    trk.save_state(0, trk_stream.cuda_stream)
 
     def step():
-        acq.run_device(iq_dev.data_ptr(), B, N, 0, res_dev.data_ptr(), sptr)
-        corr.run_epochs(jobs_dev.data_ptr(), CHANNELS, B, iq_dev.data_ptr(), B * N, trk_dev.data_ptr(),
-                        stream_ptr=sptr)
+        acq.run_device(iq_dev.data_ptr(), B, N, 0, res_dev.data_ptr(), acq_stream.cuda_stream)
+        trk.restore_state(0, trk_stream.cuda_stream)
+        trk.run_device(iq_dev.data_ptr(), 0, B * N, B, trk_out.data_ptr(), trk_n.data_ptr(), trk_stream.cuda_stream)
 
     for _ in range(args.warmup):
         step()
@@ -193,14 +202,18 @@ def main():
     res = res_dev.cpu().numpy().view(gsdr.ACQ_RESULT_DTYPE).reshape(B, P)
     det = {int(r["prn"]) for r in res[0] if r["positive"]}
     vis = {s.prn for s in sats}
-    trk = trk_dev.cpu().numpy().view(np.complex64).reshape(B, CHANNELS, TAPS)
-    prompt_ratio = float(np.median(np.abs(trk[:, :, 1]) / np.maximum(np.abs(trk[:, :, 0]), 1e-9)))
+    recs = trk_out.cpu().numpy().view(gsdr.TRK_EPOCH_DTYPE).reshape(CHANNELS, B)
+    nrec = trk_n.cpu().numpy()
+    taps = np.stack([recs[c][nrec[c] - 1]["taps"][:6].view(np.complex64) for c in range(CHANNELS)])
+    prompt_ratio = float(np.median(np.abs(taps[:, 1]) / np.maximum(np.abs(taps[:, 0]), 1e-9)))
+    dop_err = float(np.max([abs(recs[c][nrec[c] - 1]["carrier_doppler_hz"] - sats[c].doppler_hz)
+                            for c in range(CHANNELS)]))
 
     if not args.no_profile_events:
         acq.set_profiling(True)
-        corr.set_profiling(True)
+        trk.set_profiling(True)
         acq.read_profile()
-        corr.read_profile()
+        trk.read_profile()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -217,10 +230,10 @@ def main():
         elapsed = float(t.item())
 
     stage_ms, stage_n = (np.zeros(4), np.zeros(4, np.uint32))
-    trk_ms, trk_n = 0.0, 0
+    trk_ms, trk_launches = 0.0, 0
     if not args.no_profile_events:
         stage_ms, stage_n = acq.read_profile()
-        trk_ms, trk_n = corr.read_profile()
+        trk_ms, trk_launches = trk.read_profile()
 
     samples = world * args.steps * B * N
     value = samples / elapsed / 1e6
@@ -241,7 +254,8 @@ def main():
         "data": "synthetic (seeded GPS L1 C/A IQ, 8 visible PRNs at 45 dB-Hz + AWGN, per-rank shard)",
         "config": {
             "workload": "C2: GPS L1 C/A 4 Msps; per 1 ms block a 32 PRN x 81 Doppler (+-10 kHz, 250 Hz) CFAR PCPS "
-                        "grid + one 3-tap E-P-L correlator epoch for each of 8 tracked channels",
+                        "grid + closed-loop DLL/PLL tracking (3-tap E-P-L, dll_pll_veml_tracking) of 8 channels "
+                        "over the same span",
             "blocks_per_step": B, "fs_sps": FS, "fft_size": N, "prns": P, "doppler_bins": D, "channels": CHANNELS,
             "taps": TAPS, "item_type": "gr_complex", "parallelism": "blocks sharded per rank (dp%d)" % world,
         },
@@ -264,13 +278,15 @@ def main():
             "acq_forward": round(stage_ms[0] / max(stage_n[0], 1) * 1e3, 2),
             "acq_correlate": round(stage_ms[1] / max(stage_n[1], 1) * 1e3, 2),
             "acq_reduce": round(stage_ms[2] / max(stage_n[2], 1) * 1e3, 2),
-            "trk_correlator_all_epochs": round(trk_ms / max(args.steps, 1) * 1e3, 2),
+            "trk_loop_all_epochs": round(trk_ms / max(trk_launches, 1) * 1e3, 2),
         }
         line["acq_roof_frac_whole_pipeline"] = round(
             acq_bytes_per_block() * B / ((stage_ms[:3].sum() / args.steps) / 1e3) / HBM_PEAK, 4)
-    line["check"] = {"visible": len(vis), "acquired_block0": len(vis & det), "median_prompt_over_early": round(prompt_ratio, 2)}
+    line["check"] = {"visible": len(vis), "acquired_block0": len(vis & det),
+                     "median_prompt_over_early": round(prompt_ratio, 2), "trk_calls_per_channel": int(nrec.min()),
+                     "max_doppler_err_hz": round(dop_err, 2)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(iq, codes, sats, jobs)
+        line["cpu_baseline"] = cpu_baseline(iq, codes, sats)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist is not None:

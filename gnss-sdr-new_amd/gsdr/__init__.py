@@ -34,7 +34,34 @@ EXPORTED = [
     "gsdr_corr_set_local_code_and_taps_complex", "gsdr_corr_set_high_dynamics_resampler",
     "gsdr_corr_set_resampler_assoc", "gsdr_corr_run", "gsdr_corr_run_batch", "gsdr_corr_run_batch_device",
     "gsdr_corr_dump_indices", "gsdr_corr_run_epochs", "gsdr_corr_set_profiling", "gsdr_corr_read_profile",
+    "gsdr_trk_conf_default", "gsdr_trk_create", "gsdr_trk_destroy", "gsdr_trk_start", "gsdr_trk_stop",
+    "gsdr_trk_run_device", "gsdr_trk_run", "gsdr_trk_get_channel", "gsdr_trk_save_state", "gsdr_trk_restore_state",
+    "gsdr_trk_set_profiling", "gsdr_trk_read_profile",
 ]
+
+SIGNAL_GPS_1C = 0
+TRK_F_VALID_OUTPUT, TRK_F_LOSS_OF_LOCK, TRK_F_PLL_180, TRK_F_BIT_SYNC = 1, 2, 4, 8
+
+# include/gsdr.h gsdr_trk_conf / gsdr_trk_epoch (C layout)
+TRK_CONF_DTYPE = np.dtype([
+    ("fs_in", "f8"), ("carrier_lock_th", "f8"), ("vector_length", "u4"), ("signal", "i4"), ("item_type", "i4"),
+    ("max_channels", "u4"), ("fll_bw_hz", "f4"), ("pll_bw_hz", "f4"), ("dll_bw_hz", "f4"), ("pll_bw_narrow_hz", "f4"),
+    ("dll_bw_narrow_hz", "f4"), ("early_late_space_chips", "f4"), ("very_early_late_space_chips", "f4"),
+    ("early_late_space_narrow_chips", "f4"), ("very_early_late_space_narrow_chips", "f4"),
+    ("cn0_smoother_alpha", "f4"), ("carrier_lock_test_smoother_alpha", "f4"), ("pull_in_time_s", "u4"),
+    ("bit_synchronization_time_limit_s", "u4"), ("pll_filter_order", "i4"), ("dll_filter_order", "i4"),
+    ("extend_correlation_symbols", "i4"), ("cn0_samples", "i4"), ("cn0_smoother_samples", "i4"),
+    ("carrier_lock_test_smoother_samples", "i4"), ("cn0_min", "i4"), ("max_code_lock_fail", "i4"),
+    ("max_carrier_lock_fail", "i4"), ("enable_fll_pull_in", "i4"), ("enable_fll_steady_state", "i4"),
+    ("carrier_aiding", "i4"), ("high_dyn", "i4")], align=True)
+assert TRK_CONF_DTYPE.itemsize == 136
+
+TRK_EPOCH_DTYPE = np.dtype([
+    ("sample_counter", "u8"), ("state", "i4"), ("consumed", "i4"), ("taps", "f4", (10,)),
+    ("rem_carr_phase_rad", "f4"), ("flags", "i4"), ("carrier_doppler_hz", "f8"), ("code_freq_chips", "f8"),
+    ("rem_code_phase_samples", "f8"), ("acc_carrier_phase_rad", "f8"), ("cn0_db_hz", "f8"),
+    ("carrier_lock_test", "f8"), ("prompt_i", "f8"), ("prompt_q", "f8"), ("evm", "f8")], align=True)
+assert TRK_EPOCH_DTYPE.itemsize == 136
 
 
 class GsdrError(RuntimeError):
@@ -156,6 +183,20 @@ def load():
     L.gsdr_corr_run_epochs.argtypes = [P, P, I, I, P, I, I64, P, P]
     L.gsdr_corr_set_profiling.argtypes = [P, I]
     L.gsdr_corr_read_profile.argtypes = [P, P, P]
+    L.gsdr_trk_conf_default.argtypes = [P]
+    L.gsdr_trk_conf_default.restype = None
+    L.gsdr_trk_create.argtypes = [I, P, P]
+    L.gsdr_trk_destroy.argtypes = [P]
+    L.gsdr_trk_destroy.restype = None
+    L.gsdr_trk_start.argtypes = [P, I, U32, P, I, ctypes.c_double, ctypes.c_double, U64, U64, P]
+    L.gsdr_trk_stop.argtypes = [P, I]
+    L.gsdr_trk_run_device.argtypes = [P, P, U64, U64, U32, P, P, P]
+    L.gsdr_trk_run.argtypes = [P, P, U64, U64, U32, P, P]
+    L.gsdr_trk_get_channel.argtypes = [P, I, P, P, P, P]
+    L.gsdr_trk_save_state.argtypes = [P, I, P]
+    L.gsdr_trk_restore_state.argtypes = [P, I, P]
+    L.gsdr_trk_set_profiling.argtypes = [P, I]
+    L.gsdr_trk_read_profile.argtypes = [P, P, P]
     _lib = L
     return L
 
@@ -361,3 +402,79 @@ class Correlator:
         out = np.zeros((self.ntaps[channel], n), np.int32)
         _check(load().gsdr_corr_dump_indices(self._h, channel, rem_code, code_step, int(n), _ptr(out)))
         return out
+
+
+def trk_conf_default():
+    """Dll_Pll_Conf defaults (gsdr_trk_conf_default) as a one-element structured array."""
+    c = np.zeros(1, TRK_CONF_DTYPE)
+    load().gsdr_trk_conf_default(_ptr(c))
+    return c
+
+
+class Tracking:
+    """Device-resident DLL/PLL tracking (dll_pll_veml_tracking) for a pool of channels."""
+
+    def __init__(self, conf, device=0):
+        self.conf = np.ascontiguousarray(conf, TRK_CONF_DTYPE).copy()
+        self._h = ctypes.c_void_p()
+        _check(load().gsdr_trk_create(int(device), _ptr(self.conf), ctypes.byref(self._h)))
+        self.max_channels = int(self.conf["max_channels"][0])
+
+    def close(self):
+        if self._h:
+            load().gsdr_trk_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def start(self, ch, prn, code, acq_delay_samples, acq_doppler_hz, acq_samplestamp, nitems_read):
+        code = np.ascontiguousarray(code, np.float32)
+        first = ctypes.c_uint64()
+        _check(load().gsdr_trk_start(self._h, int(ch), int(prn), _ptr(code), len(code), float(acq_delay_samples),
+                                     float(acq_doppler_hz), int(acq_samplestamp), int(nitems_read),
+                                     ctypes.byref(first)))
+        return first.value
+
+    def stop(self, ch):
+        _check(load().gsdr_trk_stop(self._h, int(ch)))
+
+    def run(self, iq, iq_first_sample, max_epochs):
+        """Synchronous: host IQ -> (records [max_channels, max_epochs], counts [max_channels])."""
+        item = int(self.conf["item_type"][0])
+        iq = np.ascontiguousarray(iq, np.int16 if item == ITEM_CSHORT else np.complex64)
+        n_items = len(iq) // 2 if item == ITEM_CSHORT else len(iq)
+        out = np.zeros(self.max_channels * max_epochs, TRK_EPOCH_DTYPE)
+        n = np.zeros(self.max_channels, np.uint32)
+        _check(load().gsdr_trk_run(self._h, _ptr(iq), int(iq_first_sample), int(n_items), int(max_epochs), _ptr(out),
+                                   _ptr(n)))
+        return out.reshape(self.max_channels, max_epochs), n
+
+    def run_device(self, iq_dev_ptr, iq_first_sample, iq_items, max_epochs, out_dev_ptr, nout_dev_ptr, stream_ptr=0):
+        _check(load().gsdr_trk_run_device(self._h, ctypes.c_void_p(iq_dev_ptr), int(iq_first_sample), int(iq_items),
+                                          int(max_epochs), ctypes.c_void_p(out_dev_ptr), ctypes.c_void_p(nout_dev_ptr),
+                                          ctypes.c_void_p(stream_ptr)))
+
+    def channel(self, ch):
+        st, nxt, dop, cn0 = ctypes.c_int32(), ctypes.c_uint64(), ctypes.c_double(), ctypes.c_double()
+        _check(load().gsdr_trk_get_channel(self._h, int(ch), ctypes.byref(st), ctypes.byref(nxt), ctypes.byref(dop),
+                                           ctypes.byref(cn0)))
+        return {"state": st.value, "next_sample": nxt.value, "carrier_doppler_hz": dop.value, "cn0_db_hz": cn0.value}
+
+    def save_state(self, slot=0, stream_ptr=0):
+        _check(load().gsdr_trk_save_state(self._h, int(slot), ctypes.c_void_p(stream_ptr)))
+
+    def restore_state(self, slot=0, stream_ptr=0):
+        _check(load().gsdr_trk_restore_state(self._h, int(slot), ctypes.c_void_p(stream_ptr)))
+
+    def set_profiling(self, enable):
+        _check(load().gsdr_trk_set_profiling(self._h, int(bool(enable))))
+
+    def read_profile(self):
+        ms = ctypes.c_double()
+        n = ctypes.c_uint32()
+        _check(load().gsdr_trk_read_profile(self._h, ctypes.byref(ms), ctypes.byref(n)))
+        return ms.value, n.value

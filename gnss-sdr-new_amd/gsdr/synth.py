@@ -55,14 +55,34 @@ def gps_ca_sampled(prn, fs, n=None):
     return c
 
 
+GPS_L1_HZ = 1.57542e9
+GPS_PREAMBLE = (1, 0, 0, 0, 1, 0, 1, 1)  # TLM preamble 10001011 (GPS_L1_CA.h:61-73)
+
+
 class Satellite:
-    def __init__(self, prn, doppler_hz, code_delay_chips, cn0_dbhz=45.0, phase=0.0, bit_period_ms=20):
+    """preamble_every_bits: when set, the navigation bit stream carries the GPS TLM
+    preamble every that many bits (bit synchronisation in tracking needs it);
+    code_doppler: the code rate follows the carrier Doppler (1 + f_d / f_L1)."""
+
+    def __init__(self, prn, doppler_hz, code_delay_chips, cn0_dbhz=45.0, phase=0.0, bit_period_ms=20,
+                 preamble_every_bits=None, code_doppler=False):
         self.prn = prn
         self.doppler_hz = doppler_hz
         self.code_delay_chips = code_delay_chips
         self.cn0_dbhz = cn0_dbhz
         self.phase = phase
         self.bit_period_ms = bit_period_ms
+        self.preamble_every_bits = preamble_every_bits
+        self.code_doppler = code_doppler
+
+    def nav_bits(self, nbits):
+        bits_rng = np.random.default_rng(SEED + 77 * self.prn)
+        bits = np.where(bits_rng.random(nbits) < 0.5, -1.0, 1.0)
+        if self.preamble_every_bits:
+            pre = np.array([1.0 if b else -1.0 for b in GPS_PREAMBLE])
+            for k in range(0, nbits - len(pre) + 1, self.preamble_every_bits):
+                bits[k:k + len(pre)] = pre
+        return bits
 
 
 def random_constellation(n_visible=8, seed_offset=0, cn0_dbhz=45.0, max_doppler=9000.0, prns=None):
@@ -84,12 +104,13 @@ def gps_l1_iq(fs, n_samples, sats, seed_offset=0, t0_samples=0, noise=True, dtyp
     for s in sats:
         chips = gps_ca_chips(s.prn)
         amp = np.sqrt(10.0 ** (s.cn0_dbhz / 10.0) / fs)
-        code_phase = t * 1.023e6 - s.code_delay_chips
+        rate = 1.023e6 * (1.0 + s.doppler_hz / GPS_L1_HZ) if s.code_doppler else 1.023e6
+        code_phase = t * rate - s.code_delay_chips
         c = chips[np.floor(code_phase).astype(np.int64) % 1023]
-        bits_rng = np.random.default_rng(SEED + 77 * s.prn)
         nbits = int(np.ceil((t[-1] + 1) * 1000 / s.bit_period_ms)) + 2
-        bits = np.where(bits_rng.random(nbits) < 0.5, -1.0, 1.0)
-        b = bits[np.floor(t * 1000 / s.bit_period_ms).astype(np.int64)]
+        bits = s.nav_bits(nbits)
+        # bit edges follow the code epochs (20 code periods per bit)
+        b = bits[np.floor(code_phase / 1023.0 / s.bit_period_ms).astype(np.int64) % nbits]
         out += amp * c * b * np.exp(1j * (2 * np.pi * s.doppler_hz * t + s.phase))
     if noise:
         out += (rng.standard_normal(n_samples) + 1j * rng.standard_normal(n_samples)) * np.sqrt(0.5)

@@ -234,6 +234,135 @@ int gsdr_corr_read_profile(gsdr_corr* corr, double* kernel_ms, uint32_t* launche
 int gsdr_corr_dump_indices(gsdr_corr* corr, int channel, float rem_code_phase_chips, float code_phase_step_chips,
     int n, int32_t* idx_host);
 
+/* ======================================================================== */
+/* Tracking — device-resident DLL/PLL loop (dll_pll_veml_tracking)           */
+/* ======================================================================== */
+/*
+ * Replaces the per-epoch work of dll_pll_veml_tracking::general_work
+ * (src/algorithms/tracking/gnuradio_blocks/dll_pll_veml_tracking.cc:1784-2152):
+ * do_correlation_step (:1064-1089), run_dll_pll (:1092-1179),
+ * update_tracking_vars (:1216-1287), cn0_and_tracking_lock_status (:970-1056),
+ * the bit-synchronisation preamble search (acquire_secondary, :923-967) and the
+ * state machine (states 2 and 4).  One handle owns a pool of channels; a launch
+ * advances every active channel by up to max_epochs general_work calls over a
+ * device-resident IQ buffer without returning to the host (one workgroup per
+ * channel loops over its epochs: the tracking loop is sequential in time per
+ * channel, parallel across channels).
+ */
+typedef struct gsdr_trk gsdr_trk;
+
+#define GSDR_SIGNAL_GPS_1C 0 /* GPS L1 C/A (dll_pll_veml_tracking.cc:170-191) */
+
+/* Mirrors Dll_Pll_Conf (src/algorithms/tracking/libs/dll_pll_conf.h:30-84);
+ * gsdr_trk_conf_default() fills the reference defaults (incl. the gflags
+ * defaults gnss_sdr_flags.cc:45-54 for cn0_samples, cn0_min, max_lock_fail,
+ * max_carrier_lock_fail and carrier_lock_th). */
+typedef struct gsdr_trk_conf
+{
+    double fs_in;
+    double carrier_lock_th;
+    uint32_t vector_length; /* correlation length; 0 -> round(fs_in / 1000) (gps_l1_ca_dll_pll_tracking.cc:42) */
+    int32_t signal;         /* GSDR_SIGNAL_* */
+    int32_t item_type;      /* GSDR_ITEM_* */
+    uint32_t max_channels;
+    float fll_bw_hz;
+    float pll_bw_hz;
+    float dll_bw_hz;
+    float pll_bw_narrow_hz;
+    float dll_bw_narrow_hz;
+    float early_late_space_chips;
+    float very_early_late_space_chips;
+    float early_late_space_narrow_chips;
+    float very_early_late_space_narrow_chips;
+    float cn0_smoother_alpha;
+    float carrier_lock_test_smoother_alpha;
+    uint32_t pull_in_time_s;
+    uint32_t bit_synchronization_time_limit_s;
+    int32_t pll_filter_order;
+    int32_t dll_filter_order;
+    int32_t extend_correlation_symbols; /* only 1 in this version */
+    int32_t cn0_samples;
+    int32_t cn0_smoother_samples;
+    int32_t carrier_lock_test_smoother_samples;
+    int32_t cn0_min;
+    int32_t max_code_lock_fail;
+    int32_t max_carrier_lock_fail;
+    int32_t enable_fll_pull_in;
+    int32_t enable_fll_steady_state;
+    int32_t carrier_aiding;
+    int32_t high_dyn; /* only 0 in this version */
+} gsdr_trk_conf;
+
+/* One general_work call of one channel (written for every call that ran a
+ * correlation or changed state).  Gnss_Synchro fields as general_work fills them
+ * (:2000-2017, :2121-2127) plus the loop state after the call. */
+typedef struct gsdr_trk_epoch
+{
+    uint64_t sample_counter;       /* nitems_read(0) at the start of the call */
+    int32_t state;                 /* d_state at the start of the call */
+    int32_t consumed;              /* consume_each() count */
+    float taps[10];                /* correlator outputs of the call: E,P,L (3 taps) or VE,E,P,L,VL */
+    float rem_carr_phase_rad;      /* after the call */
+    int32_t flags;                 /* GSDR_TRK_F_* */
+    double carrier_doppler_hz;     /* Carrier_Doppler_hz */
+    double code_freq_chips;
+    double rem_code_phase_samples; /* Code_phase_samples */
+    double acc_carrier_phase_rad;  /* Carrier_phase_rads */
+    double cn0_db_hz;              /* CN0_dB_hz */
+    double carrier_lock_test;
+    double prompt_i;               /* Prompt_I (valid output only) */
+    double prompt_q;               /* Prompt_Q (valid output only) */
+    double evm;                    /* EVM (fork indicator, :1027-1053) */
+} gsdr_trk_epoch;
+
+#define GSDR_TRK_F_VALID_OUTPUT 1 /* Flag_valid_symbol_output: a Gnss_Synchro was emitted */
+#define GSDR_TRK_F_LOSS_OF_LOCK 2 /* event 3 (loss of lock), channel back to state 0 */
+#define GSDR_TRK_F_PLL_180 4      /* Flag_PLL_180_deg_phase_locked */
+#define GSDR_TRK_F_BIT_SYNC 8     /* preamble / bit synchronisation locked in this call (2 -> 4) */
+
+void gsdr_trk_conf_default(gsdr_trk_conf* conf);
+int gsdr_trk_create(int device, const gsdr_trk_conf* conf, gsdr_trk** out);
+void gsdr_trk_destroy(gsdr_trk* trk);
+
+/* start_tracking (:640-882) for channel ch with the acquisition results of
+ * Gnss_Synchro (Acq_delay_samples, Acq_doppler_hz, Acq_samplestamp_samples) and
+ * the PRN's tracking code replica (code_samples = samples_per_chip * code length
+ * floats, e.g. gps_l1_ca_code_gen_float), followed by the state-1 pull-in call
+ * (:1813-1844) executed at input position nitems_read.  *first_sample receives
+ * the absolute input index of the first correlation (nitems_read + offset). */
+int gsdr_trk_start(gsdr_trk* trk, int ch, uint32_t prn, const float* code, int code_samples,
+    double acq_delay_samples, double acq_doppler_hz, uint64_t acq_samplestamp, uint64_t nitems_read,
+    uint64_t* first_sample);
+/* stop_tracking: channel to state 0 (standby). */
+int gsdr_trk_stop(gsdr_trk* trk, int ch);
+
+/* Advance every channel in states 2..4 by up to max_epochs general_work calls
+ * over iq_dev, which holds iq_items items whose first item is absolute input
+ * sample iq_first_sample.  A channel stops early when its next call would read
+ * past the buffer.  out_dev: max_channels * max_epochs records, channel-major
+ * (record e of channel c at c*max_epochs + e); n_out_dev: per-channel record
+ * count (device).  Asynchronous on stream (NULL = the handle's own stream). */
+int gsdr_trk_run_device(gsdr_trk* trk, const void* iq_dev, uint64_t iq_first_sample, uint64_t iq_items,
+    uint32_t max_epochs, gsdr_trk_epoch* out_dev, uint32_t* n_out_dev, void* stream);
+
+/* Host form of the same call (synchronous): copies the records back. */
+int gsdr_trk_run(gsdr_trk* trk, const void* iq_host, uint64_t iq_first_sample, uint64_t iq_items,
+    uint32_t max_epochs, gsdr_trk_epoch* out_host, uint32_t* n_out_host);
+
+/* Channel snapshot: current state, next input index, Doppler and CN0. */
+int gsdr_trk_get_channel(gsdr_trk* trk, int ch, int32_t* state, uint64_t* next_sample, double* carrier_doppler_hz,
+    double* cn0_db_hz);
+
+/* Device-side copy of every channel's loop state into / out of snapshot slot
+ * `slot` (0 or 1); asynchronous on stream.  Lets a caller replay the same input
+ * span from the same loop state (benchmarks, what-if re-tracking). */
+int gsdr_trk_save_state(gsdr_trk* trk, int slot, void* stream);
+int gsdr_trk_restore_state(gsdr_trk* trk, int slot, void* stream);
+
+/* Kernel-time profiling with HIP events (see gsdr_acq_set_profiling). */
+int gsdr_trk_set_profiling(gsdr_trk* trk, int enable);
+int gsdr_trk_read_profile(gsdr_trk* trk, double* kernel_ms, uint32_t* launches);
+
 #ifdef __cplusplus
 }
 #endif

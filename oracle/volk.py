@@ -25,8 +25,8 @@ def build():
 def lib():
     global _lib
     if _lib is None:
-        src = os.path.join(_HERE, "volk_oracle.c")
-        if not os.path.exists(_SO) or os.path.getmtime(_SO) < os.path.getmtime(src):
+        srcs = [os.path.join(_HERE, f) for f in ("volk_oracle.c", "trk_oracle.c")]
+        if not os.path.exists(_SO) or os.path.getmtime(_SO) < max(os.path.getmtime(f) for f in srcs):
             build()
         L = ctypes.CDLL(_SO)
         L.orc_resampler_32f_xn.argtypes = [_p, _p, _f, _f, _p, _u, _i, _u, _i]

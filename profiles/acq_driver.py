@@ -25,25 +25,27 @@ def main():
     import gsdr
     from gsdr import synth
     B = a.blocks
-    sats, iq, codes, jobs = bench.make_workload(B, 0)
+    sats, iq, codes = bench.make_workload(B, 0)
     dev = torch.device("cuda", 0)
     iq_dev = torch.from_numpy(iq.view(np.float32).copy()).to(dev)
-    jobs_dev = torch.from_numpy(jobs.view(np.uint8).copy()).to(dev)
     res_dev = torch.zeros(B * bench.P * gsdr.ACQ_RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
-    trk_dev = torch.zeros(B * bench.CHANNELS * bench.TAPS * 2, dtype=torch.float32, device=dev)
+    trk_out = torch.zeros(bench.CHANNELS * B * gsdr.TRK_EPOCH_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    trk_n = torch.zeros(bench.CHANNELS, dtype=torch.int32, device=dev)
     acq = gsdr.Acquisition(bench.FS, bench.N, bench.DMAX, bench.DSTEP, pfa=bench.PFA, max_prns=bench.P, max_blocks=B,
                            num_doppler_bins=bench.D)
     acq.set_local_codes(codes, np.arange(1, bench.P + 1))
-    corr = gsdr.Correlator(bench.CHANNELS, bench.N, max_taps=bench.TAPS)
+    trk = gsdr.Tracking(bench.trk_conf(bench.CHANNELS))
     for c, s in enumerate(sats):
-        corr.set_local_code_and_taps(c, synth.gps_ca_chips(s.prn), np.array([-0.5, 0.0, 0.5], np.float32))
+        delay, dop = bench.acq_result_for(s)
+        trk.start(c, s.prn, synth.gps_ca_chips(s.prn), delay, dop, 0, 0)
+    trk.save_state(0)
     sptr = torch.cuda.current_stream(dev).cuda_stream
     for _ in range(a.iters):
         if a.what in ("acq", "both"):
             acq.run_device(iq_dev.data_ptr(), B, bench.N, 0, res_dev.data_ptr(), sptr)
         if a.what in ("trk", "both"):
-            corr.run_epochs(jobs_dev.data_ptr(), bench.CHANNELS, B, iq_dev.data_ptr(), B * bench.N,
-                            trk_dev.data_ptr(), stream_ptr=sptr)
+            trk.restore_state(0, sptr)
+            trk.run_device(iq_dev.data_ptr(), 0, B * bench.N, B, trk_out.data_ptr(), trk_n.data_ptr(), sptr)
     torch.cuda.synchronize(dev)
     print("done")
 

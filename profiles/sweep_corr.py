@@ -19,7 +19,7 @@ def main():
     import gsdr
     variants = [int(v) for v in (sys.argv[1].split(",") if len(sys.argv) > 1 else "0,1,2,3,4,5,6".split(","))]
     B = 64
-    sats, iq, codes, jobs = bench.make_workload(B, 0)
+    sats, iq, codes = bench.make_workload(B, 0)
     dev = torch.device("cuda", 0)
     iq_dev = torch.from_numpy(iq.view(np.float32).copy()).to(dev)
     sptr = torch.cuda.current_stream(dev).cuda_stream

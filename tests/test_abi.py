@@ -73,3 +73,35 @@ def test_create_without_device_fails_cleanly():
         gsdr.Acquisition(4000000, 4000, 10000, 250)
     with pytest.raises(gsdr.GsdrError):
         gsdr.Correlator(4, 16000)
+
+
+def test_tracking_struct_layouts_match_c_compiler(tmp_path):
+    """numpy mirrors of gsdr_trk_conf / gsdr_trk_epoch vs sizeof/offsetof."""
+    src = tmp_path / "trk_layout.c"
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "gsdr.h"', "int main(void){"]
+    pairs = (("gsdr_trk_conf", gsdr.TRK_CONF_DTYPE), ("gsdr_trk_epoch", gsdr.TRK_EPOCH_DTYPE))
+    for cname, dt in pairs:
+        lines.append('printf("%s %%zu\\n", sizeof(%s));' % (cname, cname))
+        for f in dt.names:
+            lines.append('printf("%s.%s %%zu\\n", offsetof(%s, %s));' % (cname, f, cname, f))
+    lines.append("return 0;}")
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "trk_layout"
+    subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)])
+    got = dict(l.split() for l in subprocess.check_output([str(exe)], text=True).splitlines())
+    for cname, dt in pairs:
+        assert int(got[cname]) == dt.itemsize, cname
+        for f in dt.names:
+            assert int(got[cname + "." + f]) == dt.fields[f][1], (cname, f)
+
+
+def test_tracking_conf_default_is_host_only():
+    """gsdr_trk_conf_default needs no device and carries Dll_Pll_Conf's defaults."""
+    c = gsdr.trk_conf_default()
+    assert float(c["fs_in"][0]) == 2000000.0
+    assert int(c["cn0_samples"][0]) == 20 and int(c["cn0_min"][0]) == 25
+    assert int(c["pll_filter_order"][0]) == 3 and int(c["dll_filter_order"][0]) == 2
+    assert abs(float(c["carrier_lock_th"][0]) - 0.7) < 1e-12
+    if gsdr.device_count() == 0:
+        with pytest.raises(gsdr.GsdrError):
+            gsdr.Tracking(c)

@@ -1,0 +1,96 @@
+"""The tracking oracle (oracle/trk_oracle.c) against the reference's own unit-test
+expectations, plus behavioural checks of the restated channel on synthetic IQ.
+
+Pins: src/tests/unit-tests/signal-processing-blocks/tracking/
+tracking_loop_filter_test.cc:22-206 (all six filter configurations) and
+discriminator_test.cc:35-70 (BPSK early-minus-late).  The channel state machine
+has no numeric golden vector in the reference; its behaviour is checked here
+(pull-in, bit synchronisation, CN0 and Doppler of a known synthetic signal).
+"""
+import numpy as np
+import pytest
+
+from gsdr import synth
+from oracle import trk
+
+STEP = np.array([0.0, 0.0, 1.0, 0.0, 0.0, 0.0], np.float32)
+
+
+@pytest.mark.parametrize("order,last,expected", [
+    (1, False, [0.0, 0.0, 20.0, 0.0, 0.0, 0.0]),                       # :39-50 (g1 = 4 * 5)
+    (1, True, [0.0, 0.0, 0.01, 0.02, 0.02, 0.02]),                     # :72
+    (2, False, [0.0, 0.0, 13.37778, 0.0889, 0.0889, 0.0889]),          # :103
+    (2, True, [0.0, 0.0, 0.006689, 0.013422, 0.013511, 0.013600]),     # :134
+    (3, False, [0.0, 0.0, 15.31877, 0.04494, 0.04520, 0.04546]),       # :165
+    (3, True, [0.0, 0.0, 0.007659, 0.015341, 0.015386, 0.015432]),     # :196
+])
+def test_loop_filter_golden(order, last, expected):
+    got = trk.loop_filter_run(order, last, 5.0, 0.001, STEP)
+    np.testing.assert_allclose(got, expected, atol=1e-4)
+
+
+def test_dll_e_minus_l_bpsk_golden():
+    """discriminator_test.cc:35-70: BPSK correlation 1-|tau|; output == err inside +-2*spacing."""
+    for A in (1 + 0j, -1 + 0j, 1j, 1 + 1j):
+        for spacing in (0.5, 0.25, 0.1, 0.01):
+            for err in (0.0, 0.01, 0.1, 0.25, -0.25, -0.1, -0.01):
+                bpsk = lambda x: 0.0 if abs(x) > 1.0 else 1.0 - abs(x)
+                E = complex(np.complex64(A * np.float32(bpsk(err - spacing))))
+                L = complex(np.complex64(A * np.float32(bpsk(err + spacing))))
+                d = trk.dll_nc_e_minus_l_normalized(E, L, spacing, 1.0, 1.0)
+                if abs(err) < 2.0 * spacing:
+                    assert abs(d - err) <= 1e-4, (A, spacing, err, d)
+                else:
+                    assert err * d >= 0.0
+
+
+def _conf(fs):
+    c = trk.conf_default()
+    c["fs_in"] = fs
+    c["pll_bw_hz"] = 40.0   # conf/gnss-sdr_GPS_L1_gr_complex.conf:66-67
+    c["dll_bw_hz"] = 4.0
+    c["pull_in_time_s"] = 0  # leave pull-in after the first whole second
+    return c
+
+
+def test_channel_tracks_synthetic_gps_signal():
+    fs = 2.0e6
+    sat = synth.Satellite(7, 1234.5, 300.3, 45.0, 0.7, preamble_every_bits=50, code_doppler=True)
+    iq = synth.gps_l1_iq(fs, int(3.2 * fs), [sat], seed_offset=5)
+    ch = trk.Channel(_conf(fs))
+    tau = sat.code_delay_chips / (1.023e6 * (1 + sat.doppler_hz / 1.57542e9)) * fs
+    first = ch.start(synth.gps_ca_chips(7), float(round(tau)), 1250.0, 0, 2000)
+    recs, _ = ch.run(iq, 0, first, 4000)
+    assert len(recs) > 3000
+    # states: pull-in (2) then bit synchronisation to narrow tracking (4)
+    assert recs["state"][0] == 2 and recs["state"][-1] == 4
+    sync = np.nonzero(recs["flags"] & trk.F_BIT_SYNC)[0]
+    assert len(sync) == 1
+    # consumption = one code period (+-1 sample) per call, contiguous input
+    assert np.all(np.abs(recs["consumed"] - 2000) <= 1)
+    assert np.all(np.diff(recs["sample_counter"].astype(np.int64)) == recs["consumed"][:-1])
+    late = recs[-500:]
+    assert abs(np.mean(late["carrier_doppler_hz"]) - sat.doppler_hz) < 2.0
+    assert abs(np.mean(late["cn0_db_hz"]) - 45.0) < 1.5
+    assert np.mean(late["carrier_lock_test"]) > 0.85
+    # valid outputs: one per navigation bit (20 ms), prompt sign = the bit sign
+    out = recs[(recs["flags"] & trk.F_VALID_OUTPUT) != 0]
+    assert len(out) > 50
+    assert np.all(np.abs(out["prompt_i"]) > 5 * np.abs(out["prompt_q"]))
+    assert not np.any(recs["flags"] & trk.F_LOSS_OF_LOCK)
+
+
+def test_channel_loses_lock_on_noise():
+    """Noise only: the carrier lock detector fails (the m2m4 CN0 of pure noise sits
+    near 26.7 dB-Hz, above cn0_min, so the code test passes) and, with a short
+    max_carrier_lock_fail, the channel drops to state 0 with a loss-of-lock record
+    (cn0_and_tracking_lock_status, :989-1025)."""
+    fs = 2.0e6
+    iq = synth.gps_l1_iq(fs, int(1.6 * fs), [], seed_offset=9)
+    c = _conf(fs)
+    c["max_carrier_lock_fail"] = 50
+    ch = trk.Channel(c)
+    first = ch.start(synth.gps_ca_chips(3), 100.0, 500.0, 0, 2000)
+    recs, _ = ch.run(iq, 0, first, 4000)
+    assert recs["flags"][-1] & trk.F_LOSS_OF_LOCK
+    assert ch.state == 0

@@ -186,14 +186,15 @@ def main():
     for c, s in enumerate(sats):
         delay, dop = acq_result_for(s)
         trk.start(c, s.prn, synth.gps_ca_chips(s.prn), delay, dop, 0, 0)
-    acq_stream = torch.cuda.Stream(dev)
-    trk_stream = torch.cuda.Stream(dev)
-    trk.save_state(0, trk_stream.cuda_stream)
+    # each handle launches on its own HIP stream (created with the handle, so each
+    # gets its own hardware queue); the tracking launch goes first so its few
+    # long-lived workgroups are resident before the acquisition grid fills the chip
+    trk.save_state(0)
 
     def step():
-        acq.run_device(iq_dev.data_ptr(), B, N, 0, res_dev.data_ptr(), acq_stream.cuda_stream)
-        trk.restore_state(0, trk_stream.cuda_stream)
-        trk.run_device(iq_dev.data_ptr(), 0, B * N, B, trk_out.data_ptr(), trk_n.data_ptr(), trk_stream.cuda_stream)
+        trk.restore_state(0)
+        trk.run_device(iq_dev.data_ptr(), 0, B * N, B, trk_out.data_ptr(), trk_n.data_ptr())
+        acq.run_device(iq_dev.data_ptr(), B, N, 0, res_dev.data_ptr())
 
     for _ in range(args.warmup):
         step()

@@ -240,7 +240,8 @@ __device__ inline float sm_smooth(Smoother& s, float raw)  // exponential_smooth
 }
 
 // ------------------------------------------------------------------ channel state
-struct TrkChan
+// Scalar loop state: lives in lane 0's registers for a whole launch.
+struct TrkHot
 {
     // configuration (Dll_Pll_Conf + signal constants)
     double fs_in, code_period, code_chip_rate, signal_carrier_freq, carrier_lock_threshold;
@@ -252,9 +253,8 @@ struct TrkChan
     int32_t n_taps, code_samples;
     float shifts[kMaxTrkTaps];
     uint32_t preamble[5];
-    // loop objects
+    // loop objects without history arrays
     Smoother cn0_sm, lock_sm;
-    LoopFilter code_filter;
     CarrierFilter carrier_filter;
     // state (dll_pll_veml_tracking.h:117-209)
     double acq_code_phase_samples, acq_carrier_doppler_hz, current_correlation_time_s;
@@ -265,7 +265,6 @@ struct TrkChan
     double rem_code_phase_samples;
     float2 taps[kMaxTrkTaps];
     float2 E_accu, P_accu, P_accu_old, L_accu, P_data_accu;
-    float2 prompt_buffer[kMaxCn0];
     uint32_t circ[5];  // signs of the last kPreambleLen prompts (1 = real < 0), newest at bit 0
     int32_t circ_size;
     uint64_t acq_sample_stamp, next_sample;
@@ -275,6 +274,15 @@ struct TrkChan
     int32_t pull_in_transitory, cloop, acc_carrier_phase_initialized, flag_pll_180;
     uint32_t prn;
     int32_t assoc;
+};
+
+// Device-memory image of one channel: the scalars plus the dynamically indexed
+// histories (kept in LDS during a launch).
+struct TrkChan
+{
+    TrkHot h;
+    LoopFilter code_filter;
+    float2 prompt_buffer[kMaxCn0];
 };
 
 struct Prep  // lane-0 -> workgroup broadcast of one epoch's NCO
@@ -352,7 +360,7 @@ __device__ inline float carrier_lock_detector(const float2* b, int length)  // :
     return nbd / nbp;
 }
 
-__device__ inline void clear_tracking_vars(TrkChan& t)  // :1192-1213
+__device__ inline void clear_tracking_vars(TrkHot& t)  // :1192-1213
 {
     for (int k = 0; k < kMaxTrkTaps; ++k) t.taps[k] = make_float2(0.f, 0.f);
     t.P_accu_old = make_float2(0.f, 0.f);
@@ -369,20 +377,20 @@ __device__ inline void clear_tracking_vars(TrkChan& t)  // :1192-1213
     t.code_phase_rate_step_chips = 0.0;
 }
 
-__device__ inline int cn0_and_lock(TrkChan& t, double coh)  // :970-1056
+__device__ inline int cn0_and_lock(TrkHot& t, float2* pbuf, double coh)  // :970-1056
 {
     const int n = t.cn0_samples;
     if (t.cn0_estimation_counter < n)
         {
-            t.prompt_buffer[t.cn0_estimation_counter] = t.P_accu;
+            pbuf[t.cn0_estimation_counter] = t.P_accu;
             t.cn0_estimation_counter++;
             return 1;
         }
-    t.prompt_buffer[t.cn0_estimation_counter % n] = t.P_accu;
+    pbuf[t.cn0_estimation_counter % n] = t.P_accu;
     t.cn0_estimation_counter++;
-    const float raw = cn0_m2m4(t.prompt_buffer, n, (float)coh);
+    const float raw = cn0_m2m4(pbuf, n, (float)coh);
     t.cn0_db_hz = (double)sm_smooth(t.cn0_sm, raw);
-    t.carrier_lock_test = (double)sm_smooth(t.lock_sm, carrier_lock_detector(t.prompt_buffer, 1));
+    t.carrier_lock_test = (double)sm_smooth(t.lock_sm, carrier_lock_detector(pbuf, 1));
     if (!t.pull_in_transitory)
         {
             if (t.carrier_lock_test < t.carrier_lock_threshold)
@@ -402,21 +410,21 @@ __device__ inline int cn0_and_lock(TrkChan& t, double coh)  // :970-1056
         }
     // EVM (fork indicator, :1027-1053)
     float d, s = 0;
-    for (int i = 0; i < n; i++) s = s + t.prompt_buffer[i].x * t.prompt_buffer[i].x;
+    for (int i = 0; i < n; i++) s = s + pbuf[i].x * pbuf[i].x;
     d = s / (float)n;
     d = sqrtf(d);
     s = 0;
     for (int i = 0; i < n; i++)
         {
-            const float a = fabsf(t.prompt_buffer[i].x / d) - 1.0F;
-            const float b = fabsf(t.prompt_buffer[i].y / d) - 0.0F;
+            const float a = fabsf(pbuf[i].x / d) - 1.0F;
+            const float b = fabsf(pbuf[i].y / d) - 0.0F;
             s = s + a * a + b * b;
         }
     t.evm = sqrt((double)(s / (float)n / 1.0F));
     return 1;
 }
 
-__device__ inline void run_dll_pll(TrkChan& t)  // :1092-1179 (no Doppler correction)
+__device__ inline void run_dll_pll(TrkHot& t, LoopFilter& lf)  // :1092-1179 (no Doppler correction)
 {
     t.carr_phase_error_hz = pll_cloop_two_quadrant_atan(t.P_accu) / kTwoPi;
     if ((t.pull_in_transitory && t.enable_fll_pull_in) || t.enable_fll_steady_state)
@@ -437,12 +445,12 @@ __device__ inline void run_dll_pll(TrkChan& t)  // :1092-1179 (no Doppler correc
         }
     t.carrier_doppler_hz = t.carr_error_filt_hz;
     t.code_error_chips = dll_nc_e_minus_l(t.E_accu, t.L_accu, t.spc, 1.0F, 1.0F);
-    t.code_error_filt_chips = (double)lf_apply(t.code_filter, (float)t.code_error_chips);
+    t.code_error_filt_chips = (double)lf_apply(lf, (float)t.code_error_chips);
     t.code_freq_chips = t.code_chip_rate - t.code_error_filt_chips;
     if (t.carrier_aiding) t.code_freq_chips += t.carrier_doppler_hz * t.code_chip_rate / t.signal_carrier_freq;
 }
 
-__device__ inline void update_tracking_vars(TrkChan& t)  // :1216-1287 (high_dyn = false)
+__device__ inline void update_tracking_vars(TrkHot& t)  // :1216-1287 (high_dyn = false)
 {
     const double T_chip = 1.0 / t.code_freq_chips;
     const double T_prn = T_chip * (double)t.code_length_chips;
@@ -459,7 +467,7 @@ __device__ inline void update_tracking_vars(TrkChan& t)  // :1216-1287 (high_dyn
     t.rem_code_phase_chips = t.code_freq_chips * t.rem_code_phase_samples / t.fs_in;
 }
 
-__device__ inline void circ_push(TrkChan& t, float2 prompt)
+__device__ inline void circ_push(TrkHot& t, float2 prompt)
 {
     // shift the 160-bit register left by one, new sign in at bit 0
     const uint32_t in = prompt.x < 0.0F ? 1u : 0u;
@@ -475,7 +483,7 @@ __device__ inline void circ_push(TrkChan& t, float2 prompt)
 
 // acquire_secondary (:923-967): corr = sum over the buffer of +-1 by sign match
 // = 160 - 2 * mismatches; |corr| == 160 only on a full match or full inversion.
-__device__ inline int acquire_secondary(TrkChan& t)
+__device__ inline int acquire_secondary(TrkHot& t)
 {
     int mism = 0;
     for (int w = 0; w < 5; ++w) mism += __popc(t.circ[w] ^ t.preamble[w]);
@@ -499,7 +507,7 @@ struct EpochOut
 };
 
 // One general_work call after the correlation (taps in t.taps): states 2 and 4.
-__device__ inline void after_correlation(TrkChan& t, uint64_t nitems_read, EpochOut& o)
+__device__ inline void after_correlation(TrkHot& t, LoopFilter& lf, float2* pbuf, uint64_t nitems_read, EpochOut& o)
 {
     o.flags = 0;
     o.prompt_i = 0.0;
@@ -512,7 +520,7 @@ __device__ inline void after_correlation(TrkChan& t, uint64_t nitems_read, Epoch
             t.spc = t.early_late_space_chips;
             if ((uint64_t)t.bit_sync_limit_s < (nitems_read - t.acq_sample_stamp) / (uint64_t)(int)t.fs_in)
                 t.carrier_lock_fail_counter = 300000;
-            if (!cn0_and_lock(t, t.code_period))
+            if (!cn0_and_lock(t, pbuf, t.code_period))
                 {
                     clear_tracking_vars(t);
                     t.state = 0;
@@ -521,7 +529,7 @@ __device__ inline void after_correlation(TrkChan& t, uint64_t nitems_read, Epoch
             else
                 {
                     int next_state = 0;
-                    run_dll_pll(t);
+                    run_dll_pll(t, lf);
                     update_tracking_vars(t);
                     if (!t.pull_in_transitory)
                         {
@@ -553,7 +561,7 @@ __device__ inline void after_correlation(TrkChan& t, uint64_t nitems_read, Epoch
             t.current_data_symbol++;
             t.current_data_symbol %= t.symbols_per_bit;
             t.cloop = 1;
-            if (!cn0_and_lock(t, t.code_period * (double)t.extend_correlation_symbols))
+            if (!cn0_and_lock(t, pbuf, t.code_period * (double)t.extend_correlation_symbols))
                 {
                     clear_tracking_vars(t);
                     t.state = 0;
@@ -561,7 +569,7 @@ __device__ inline void after_correlation(TrkChan& t, uint64_t nitems_read, Epoch
                 }
             else
                 {
-                    run_dll_pll(t);
+                    run_dll_pll(t, lf);
                     update_tracking_vars(t);
                     if (!t.acc_carrier_phase_initialized)
                         {
@@ -605,63 +613,75 @@ __device__ __forceinline__ int wrap_code(int raw, int L)
     return raw;
 }
 
-// grid = channels; one 256-lane workgroup per channel.
+// grid = channels; one 256-lane workgroup per channel.  Lane 0 holds the scalar
+// loop state in registers for the whole launch; the histories indexed at run
+// time (prompt buffer, DLL filter) and the replica sit in LDS.
 template <int IT>
 __global__ void __launch_bounds__(kTrkThreads) trk_kernel(TrkChan* __restrict__ chans, const float* const* __restrict__ codes,
     const void* __restrict__ iq, uint64_t iq_first, uint64_t iq_items, uint32_t max_epochs,
     gsdr_trk_epoch* __restrict__ out, uint32_t* __restrict__ nout)
 {
     extern __shared__ float s_code[];
-    __shared__ TrkChan st;
+    __shared__ LoopFilter s_lf;
+    __shared__ float2 s_pbuf[kMaxCn0];
+    __shared__ float s_shifts[kMaxTrkTaps];
+    __shared__ int s_meta[4];  // state, n_taps, code_samples, vector_length
     __shared__ Prep prep;
     __shared__ float2 s_red[kTrkThreads / 64][kMaxTrkTaps];
     const int ch = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    {
-        const uint32_t* src = reinterpret_cast<const uint32_t*>(chans + ch);
-        uint32_t* dst = reinterpret_cast<uint32_t*>(&st);
-        for (int i = tid; i < (int)(sizeof(TrkChan) / 4); i += kTrkThreads) dst[i] = src[i];
-    }
+    TrkChan* gc = chans + ch;
+    TrkHot t;
+    if (tid == 0)
+        {
+            t = gc->h;
+            s_lf = gc->code_filter;
+            s_meta[0] = t.state;
+            s_meta[1] = t.n_taps;
+            s_meta[2] = t.code_samples;
+            s_meta[3] = t.vector_length;
+            for (int k = 0; k < kMaxTrkTaps; ++k) s_shifts[k] = t.shifts[k];
+        }
+    if (tid < kMaxCn0) s_pbuf[tid] = gc->prompt_buffer[tid];
     __syncthreads();
-    if (st.state != 2 && st.state != 4)
+    if (s_meta[0] != 2 && s_meta[0] != 4)
         {
             if (tid == 0) nout[ch] = 0;
             return;
         }
-    const int L = st.code_samples;
+    const int K = s_meta[1];
+    const int L = s_meta[2];
+    const int vl = s_meta[3];
     {
         const float* c = codes[ch];
         for (int i = tid; i < L; i += kTrkThreads) s_code[i] = c[i];
     }
-    const int K = st.n_taps;
-    const int vl = st.vector_length;
     uint32_t e = 0;
     for (;; ++e)
         {
             if (tid == 0)
                 {
                     Prep p{};
-                    const int64_t off = (int64_t)(st.next_sample - iq_first);
-                    p.go = (e < max_epochs) && (st.state == 2 || st.state == 4) && st.next_sample >= iq_first &&
+                    const int64_t off = (int64_t)(t.next_sample - iq_first);
+                    p.go = (e < max_epochs) && (t.state == 2 || t.state == 4) && t.next_sample >= iq_first &&
                            (uint64_t)off + (uint64_t)vl <= iq_items;
                     p.off = off;
                     if (p.go)
                         {
-                            // do_correlation_step's float arguments (:1069-1075)
-                            const float rem_carr = st.rem_carr_phase_rad;
-                            const float carr_step = (float)st.carrier_phase_step_rad;
-                            p.rem_code = (float)st.rem_code_phase_chips * (float)st.code_samples_per_chip;
-                            p.code_step = (float)st.code_phase_step_chips * (float)st.code_samples_per_chip;
-                            // the reference's phasors (cpu_multicorrelator_real_codes.cc:114-123) as angles
-                            float s, c;
-                            sincosf(rem_carr, &s, &c);
-                            p.psi0 = atan2(-(double)s, (double)c);
-                            sincosf(-carr_step, &s, &c);
-                            p.theta = atan2((double)s, (double)c);
+                            // do_correlation_step's float arguments (:1069-1075); the
+                            // reference's phasors (cos r, -sin r) and exp(-j step)
+                            // (cpu_multicorrelator_real_codes.cc:114-123) as angles
+                            const float rem_carr = t.rem_carr_phase_rad;
+                            const float carr_step = (float)t.carrier_phase_step_rad;
+                            p.rem_code = (float)t.rem_code_phase_chips * (float)t.code_samples_per_chip;
+                            p.code_step = (float)t.code_phase_step_chips * (float)t.code_samples_per_chip;
+                            p.psi0 = -(double)rem_carr;
+                            p.theta = -(double)carr_step;
                             const double w = p.theta * (double)kTrkThreads;
+                            float sn, cs;
                             sincosf((float)fma(-rint(w * 0.15915494309189533576888376337251), 6.283185307179586476925286766559, w),
-                                &s, &c);
-                            p.wstep = make_float2(c, s);
+                                &sn, &cs);
+                            p.wstep = make_float2(cs, sn);
                         }
                     prep = p;
                 }
@@ -682,7 +702,7 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(TrkChan* __restrict__ 
             }
             float sh_rem[kMaxTrkTaps];
 #pragma unroll
-            for (int k = 0; k < kMaxTrkTaps; ++k) sh_rem[k] = __fsub_rn(st.shifts[k], p.rem_code);
+            for (int k = 0; k < kMaxTrkTaps; ++k) sh_rem[k] = __fsub_rn(s_shifts[k], p.rem_code);
             for (int n = tid; n < vl; n += kTrkThreads)
                 {
                     const float2 x = load_iq<IT>(iq, p.off + n);
@@ -720,60 +740,66 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(TrkChan* __restrict__ 
             __syncthreads();
             if (tid == 0)
                 {
-                    for (int k = 0; k < K; ++k)
+#pragma unroll
+                    for (int k = 0; k < kMaxTrkTaps; ++k)
                         {
                             float2 r = make_float2(0.f, 0.f);
-                            for (int w = 0; w < kTrkThreads / 64; ++w)
+                            if (k < K)
                                 {
-                                    r.x += s_red[w][k].x;
-                                    r.y += s_red[w][k].y;
+                                    for (int w = 0; w < kTrkThreads / 64; ++w)
+                                        {
+                                            r.x += s_red[w][k].x;
+                                            r.y += s_red[w][k].y;
+                                        }
                                 }
-                            st.taps[k] = r;
+                            t.taps[k] = r;
                         }
-                    const uint64_t n_read = st.next_sample;
-                    const int32_t state0 = st.state;
+                    const uint64_t n_read = t.next_sample;
+                    const int32_t state0 = t.state;
                     // pull-in transitory check at the top of general_work (:1794-1803)
-                    if (st.pull_in_transitory &&
-                        (uint64_t)st.pull_in_time_s < (n_read - st.acq_sample_stamp) / (uint64_t)(int)st.fs_in)
+                    if (t.pull_in_transitory &&
+                        (uint64_t)t.pull_in_time_s < (n_read - t.acq_sample_stamp) / (uint64_t)(int)t.fs_in)
                         {
-                            st.pull_in_transitory = 0;
-                            st.carrier_lock_fail_counter = 0;
-                            st.code_lock_fail_counter = 0;
+                            t.pull_in_transitory = 0;
+                            t.carrier_lock_fail_counter = 0;
+                            t.code_lock_fail_counter = 0;
                         }
                     EpochOut o;
-                    after_correlation(st, n_read, o);
+                    after_correlation(t, s_lf, s_pbuf, n_read, o);
                     gsdr_trk_epoch r;
                     r.sample_counter = n_read;
                     r.state = state0;
-                    r.consumed = st.current_prn_length_samples;
+                    r.consumed = t.current_prn_length_samples;
+#pragma unroll
                     for (int k = 0; k < 5; ++k)
                         {
-                            r.taps[2 * k] = k < K ? st.taps[k].x : 0.0f;
-                            r.taps[2 * k + 1] = k < K ? st.taps[k].y : 0.0f;
+                            r.taps[2 * k] = t.taps[k].x;
+                            r.taps[2 * k + 1] = t.taps[k].y;
                         }
-                    r.rem_carr_phase_rad = st.rem_carr_phase_rad;
+                    r.rem_carr_phase_rad = t.rem_carr_phase_rad;
                     r.flags = o.flags;
-                    r.carrier_doppler_hz = st.carrier_doppler_hz;
-                    r.code_freq_chips = st.code_freq_chips;
-                    r.rem_code_phase_samples = st.rem_code_phase_samples;
-                    r.acc_carrier_phase_rad = st.acc_carrier_phase_rad;
-                    r.cn0_db_hz = st.cn0_db_hz;
-                    r.carrier_lock_test = st.carrier_lock_test;
+                    r.carrier_doppler_hz = t.carrier_doppler_hz;
+                    r.code_freq_chips = t.code_freq_chips;
+                    r.rem_code_phase_samples = t.rem_code_phase_samples;
+                    r.acc_carrier_phase_rad = t.acc_carrier_phase_rad;
+                    r.cn0_db_hz = t.cn0_db_hz;
+                    r.carrier_lock_test = t.carrier_lock_test;
                     r.prompt_i = o.prompt_i;
                     r.prompt_q = o.prompt_q;
-                    r.evm = st.evm;
+                    r.evm = t.evm;
                     out[(size_t)ch * max_epochs + e] = r;
-                    st.next_sample = n_read + (uint64_t)(int64_t)st.current_prn_length_samples;
+                    t.next_sample = n_read + (uint64_t)(int64_t)t.current_prn_length_samples;
                 }
             // the next iteration's lane-0 prep follows the update; its barrier orders s_red reuse
         }
     __syncthreads();
-    {
-        const uint32_t* src = reinterpret_cast<const uint32_t*>(&st);
-        uint32_t* dst = reinterpret_cast<uint32_t*>(chans + ch);
-        for (int i = tid; i < (int)(sizeof(TrkChan) / 4); i += kTrkThreads) dst[i] = src[i];
-    }
-    if (tid == 0) nout[ch] = e;
+    if (tid == 0)
+        {
+            gc->h = t;
+            gc->code_filter = s_lf;
+            nout[ch] = e;
+        }
+    if (tid < kMaxCn0) gc->prompt_buffer[tid] = s_pbuf[tid];
 }
 
 void preamble_register(uint32_t reg[5])
@@ -823,9 +849,10 @@ namespace
 size_t trk_item_bytes(int it) { return it == GSDR_ITEM_CSHORT ? 4 : 8; }
 
 // constructor (dll_pll_veml_tracking.cc:85-560) for one channel slot, GPS L1 C/A
-void init_channel(const gsdr_trk_conf& c, TrkChan& t)
+void init_channel(const gsdr_trk_conf& c, TrkChan& ch)
 {
-    std::memset(&t, 0, sizeof(t));
+    std::memset(&ch, 0, sizeof(ch));
+    TrkHot& t = ch.h;
     t.fs_in = c.fs_in;
     t.code_period = kGpsCaPeriod;
     t.code_chip_rate = kGpsCaRate;
@@ -853,10 +880,10 @@ void init_channel(const gsdr_trk_conf& c, TrkChan& t)
     preamble_register(t.preamble);
     t.spc = c.early_late_space_chips;
     t.code_freq_chips = t.code_chip_rate;
-    t.code_filter.T = (float)t.code_period;
-    t.code_filter.bw = c.dll_bw_hz;
-    t.code_filter.order = c.dll_filter_order;
-    lf_update(t.code_filter);
+    ch.code_filter.T = (float)t.code_period;
+    ch.code_filter.bw = c.dll_bw_hz;
+    ch.code_filter.order = c.dll_filter_order;
+    lf_update(ch.code_filter);
     cf_set_params(t.carrier_filter, c.fll_bw_hz, c.pll_bw_hz, c.pll_filter_order);
     // Exponential_Smoother defaults + dll_pll_veml_tracking.cc:540-552
     t.cn0_sm.alpha = c.cn0_smoother_alpha;
@@ -996,7 +1023,7 @@ int gsdr_trk_create(int device, const gsdr_trk_conf* conf, gsdr_trk** out)
     k->h_chans.resize(nch);
     for (auto& t : k->h_chans) init_channel(k->conf, t);
     k->code_bufs.assign(nch, nullptr);
-    k->lds_bytes = (size_t)kMaxCodeFloats * sizeof(float);
+    k->lds_bytes = 1024 * sizeof(float);  // grows with the longest replica started (gsdr_trk_start)
     hipError_t e = hipStreamCreateWithFlags(&k->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipMalloc(&k->d_chans, nch * sizeof(TrkChan));
     if (e == hipSuccess) e = hipMalloc(&k->d_snap[0], nch * sizeof(TrkChan));
@@ -1008,10 +1035,10 @@ int gsdr_trk_create(int device, const gsdr_trk_conf* conf, gsdr_trk** out)
     if (e == hipSuccess) e = hipMemcpy(k->d_chans, k->h_chans.data(), nch * sizeof(TrkChan), hipMemcpyHostToDevice);
     if (e == hipSuccess)
         e = hipFuncSetAttribute((const void*)trk_kernel<GSDR_ITEM_GR_COMPLEX>, hipFuncAttributeMaxDynamicSharedMemorySize,
-            (int)k->lds_bytes);
+            (int)(kMaxCodeFloats * sizeof(float)));
     if (e == hipSuccess)
         e = hipFuncSetAttribute((const void*)trk_kernel<GSDR_ITEM_CSHORT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-            (int)k->lds_bytes);
+            (int)(kMaxCodeFloats * sizeof(float)));
     if (e != hipSuccess)
         {
             gsdr::set_error("gsdr_trk_create: %s", hipGetErrorString(e));
@@ -1055,7 +1082,8 @@ int gsdr_trk_start(gsdr_trk* k, int ch, uint32_t prn, const float* code, int cod
     // the device copy is authoritative between launches (the loop runs there)
     GSDR_HIP(hipMemcpyAsync(&k->h_chans[ch], k->d_chans + ch, sizeof(TrkChan), hipMemcpyDeviceToHost, k->stream));
     GSDR_HIP(hipStreamSynchronize(k->stream));
-    TrkChan& t = k->h_chans[ch];
+    TrkChan& tc = k->h_chans[ch];
+    TrkHot& t = tc.h;
     // start_tracking (:640-882)
     t.prn = prn;
     t.code_samples = code_samples;
@@ -1080,12 +1108,12 @@ int gsdr_trk_start(gsdr_trk* k, int ch, uint32_t prn, const float* code, int cod
     t.shifts[2] = k->conf.early_late_space_chips * (float)t.code_samples_per_chip;
     t.current_correlation_time_s = t.code_period;
     cf_set_params(t.carrier_filter, k->conf.fll_bw_hz, k->conf.pll_bw_hz, k->conf.pll_filter_order);
-    t.code_filter.bw = k->conf.dll_bw_hz;
-    lf_update(t.code_filter);
-    t.code_filter.T = (float)t.code_period;
-    lf_update(t.code_filter);
+    tc.code_filter.bw = k->conf.dll_bw_hz;
+    lf_update(tc.code_filter);
+    tc.code_filter.T = (float)t.code_period;
+    lf_update(tc.code_filter);
     cf_initialize(t.carrier_filter, (float)t.acq_carrier_doppler_hz);
-    lf_initialize(t.code_filter, 0.0F);
+    lf_initialize(tc.code_filter, 0.0F);
     t.cloop = 1;
     t.pull_in_transitory = 1;
     t.circ_size = 0;
@@ -1109,9 +1137,10 @@ int gsdr_trk_start(gsdr_trk* k, int ch, uint32_t prn, const float* code, int cod
     sm_reset(t.lock_sm);
     t.next_sample = nitems_read + (uint64_t)(int64_t)offset;
     *first_sample = t.next_sample;
+    k->lds_bytes = std::max(k->lds_bytes, (size_t)code_samples * sizeof(float));
     GSDR_HIP(hipMemcpyAsync(k->code_bufs[ch], code, (size_t)code_samples * sizeof(float), hipMemcpyHostToDevice,
         k->stream));
-    GSDR_HIP(hipMemcpyAsync(k->d_chans + ch, &t, sizeof(TrkChan), hipMemcpyHostToDevice, k->stream));
+    GSDR_HIP(hipMemcpyAsync(k->d_chans + ch, &tc, sizeof(TrkChan), hipMemcpyHostToDevice, k->stream));
     GSDR_HIP(hipStreamSynchronize(k->stream));
     return GSDR_OK;
 }
@@ -1123,7 +1152,8 @@ int gsdr_trk_stop(gsdr_trk* k, int ch)
     std::lock_guard<std::mutex> lk(k->mu);
     gsdr::DeviceGuard g(k->device);
     const int32_t zero = 0;
-    GSDR_HIP(hipMemcpyAsync(reinterpret_cast<char*>(k->d_chans + ch) + offsetof(TrkChan, state), &zero, sizeof(zero),
+    GSDR_HIP(hipMemcpyAsync(reinterpret_cast<char*>(k->d_chans + ch) + offsetof(TrkChan, h) + offsetof(TrkHot, state),
+        &zero, sizeof(zero),
         hipMemcpyHostToDevice, k->stream));
     GSDR_HIP(hipStreamSynchronize(k->stream));
     return GSDR_OK;
@@ -1175,7 +1205,7 @@ int gsdr_trk_get_channel(gsdr_trk* k, int ch, int32_t* state, uint64_t* next_sam
     gsdr::DeviceGuard g(k->device);
     GSDR_HIP(hipMemcpyAsync(&k->h_chans[ch], k->d_chans + ch, sizeof(TrkChan), hipMemcpyDeviceToHost, k->stream));
     GSDR_HIP(hipStreamSynchronize(k->stream));
-    const TrkChan& t = k->h_chans[ch];
+    const TrkHot& t = k->h_chans[ch].h;
     if (state) *state = t.state;
     if (next_sample) *next_sample = t.next_sample;
     if (doppler) *doppler = t.carrier_doppler_hz;

@@ -78,21 +78,21 @@ __device__ __forceinline__ int wrap_mod(int idx, int L)
 // KERN/32f_xn_resampler_32f_xn.h:73 (generic) / :384-390 (a_avx).
 __device__ __forceinline__ int code_index(float step, float shift, float rem, int n, int L, int assoc)
 {
-    const float a = __fmul_rn(step, (float)n);
+    const float a = gsdr::mul_rn(step, (float)n);
     float t;
     if (assoc == GSDR_ASSOC_GENERIC)
-        t = __fsub_rn(__fadd_rn(a, shift), rem);
+        t = gsdr::sub_rn(gsdr::add_rn(a, shift), rem);
     else
-        t = __fadd_rn(a, __fsub_rn(shift, rem));
+        t = gsdr::add_rn(a, gsdr::sub_rn(shift, rem));
     return wrap_mod((int)floorf(t), L);
 }
 
 // KERN/32f_xn_high_dynamics_resampler_32f_xn.h:75-79 (tap 0).
 __device__ __forceinline__ int code_index_hd(float step, float rate, float shift0, float rem, uint32_t m, int L)
 {
-    const float a = __fmul_rn(step, (float)m);
-    const float b = __fmul_rn(rate, (float)(m * m));
-    const float t = __fsub_rn(__fadd_rn(__fadd_rn(a, b), shift0), rem);
+    const float a = gsdr::mul_rn(step, (float)m);
+    const float b = gsdr::mul_rn(rate, (float)(m * m));
+    const float t = gsdr::sub_rn(gsdr::add_rn(gsdr::add_rn(a, b), shift0), rem);
     return wrap_mod((int)floorf(t), L);
 }
 
@@ -110,8 +110,8 @@ __device__ __forceinline__ void rotator_model_device(const gsdr_corr_job& j, dou
 // Unwrapped code index floor(...) with the reference's float association.
 __device__ __forceinline__ int raw_index(float step, float shift, float rem, int n, int assoc)
 {
-    const float a = __fmul_rn(step, (float)n);
-    const float t = (assoc == GSDR_ASSOC_GENERIC) ? __fsub_rn(__fadd_rn(a, shift), rem) : __fadd_rn(a, __fsub_rn(shift, rem));
+    const float a = gsdr::mul_rn(step, (float)n);
+    const float t = (assoc == GSDR_ASSOC_GENERIC) ? gsdr::sub_rn(gsdr::add_rn(a, shift), rem) : gsdr::add_rn(a, gsdr::sub_rn(shift, rem));
     return (int)floorf(t);
 }
 

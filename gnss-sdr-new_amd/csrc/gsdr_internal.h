@@ -53,6 +53,27 @@ struct DeviceGuard
     }
 };
 
+// Single-rounding float operations that the backend may not fuse into an FMA
+// (the reference's code index floor(step*n + (shift - rem)) flips
+// at chip boundaries, so each product and sum must round exactly as on x86).
+// HIP's __fmul_rn/__fadd_rn are plain operators whose contraction follows the
+// caller's context; these carry an explicit contract(off).
+__device__ __forceinline__ float mul_rn(float a, float b)
+{
+#pragma clang fp contract(off)
+    return a * b;
+}
+__device__ __forceinline__ float add_rn(float a, float b)
+{
+#pragma clang fp contract(off)
+    return a + b;
+}
+__device__ __forceinline__ float sub_rn(float a, float b)
+{
+#pragma clang fp contract(off)
+    return a - b;
+}
+
 // Inverse regularised lower incomplete gamma for integer shape a:
 // returns x with P(a, x) = p.  (Boost gamma_p_inv, used by calculate_threshold.)
 double gamma_p_inv_int(int a, double p);

@@ -26,6 +26,8 @@
 #include <algorithm>
 #include <cmath>
 #include <cstddef>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -40,11 +42,14 @@
 namespace
 {
 
-constexpr int kTrkThreads = 256;
+constexpr int kTrkThreads = 512;
 constexpr int kMaxCn0 = 64;         // cn0_samples capacity
 constexpr int kMaxTrkTaps = 5;
 constexpr int kMaxCodeFloats = 16384;
 constexpr int kPreambleLen = 160;   // GPS_CA_PREAMBLE_LENGTH_SYMBOLS (GPS_L1_CA.h:61)
+constexpr int kSpl = 8;                       // samples per lane per correlation chunk
+constexpr int kWinCore = kSpl * kTrkThreads;  // 4096: the next call's window staged in LDS
+constexpr int kHalo = 16;                     // slack around the predicted next start
 
 // MATH_CONSTANTS.h:47-50
 constexpr double kGnssPi = 3.1415926535898;
@@ -292,6 +297,8 @@ struct Prep  // lane-0 -> workgroup broadcast of one epoch's NCO
     float rem_code, code_step;
     int64_t off;
     int32_t go;
+    int32_t woff;  // >= 0: this call's samples are in the LDS window at that offset
+    int32_t fast;  // every code index of the call lies in [-L, 2L): branch-free wrap
 };
 
 // ------------------------------------------------------------------ lane-0 loop body
@@ -507,7 +514,8 @@ struct EpochOut
 };
 
 // One general_work call after the correlation (taps in t.taps): states 2 and 4.
-__device__ inline void after_correlation(TrkHot& t, LoopFilter& lf, float2* pbuf, uint64_t nitems_read, EpochOut& o)
+__device__ inline void after_correlation(TrkHot& t, LoopFilter& lf, float2* pbuf, uint64_t nitems_read, EpochOut& o,
+    uint64_t* ts = nullptr)
 {
     o.flags = 0;
     o.prompt_i = 0.0;
@@ -520,7 +528,9 @@ __device__ inline void after_correlation(TrkHot& t, LoopFilter& lf, float2* pbuf
             t.spc = t.early_late_space_chips;
             if ((uint64_t)t.bit_sync_limit_s < (nitems_read - t.acq_sample_stamp) / (uint64_t)(int)t.fs_in)
                 t.carrier_lock_fail_counter = 300000;
-            if (!cn0_and_lock(t, pbuf, t.code_period))
+            const int lock_ok = cn0_and_lock(t, pbuf, t.code_period);
+            if (ts) ts[0] = clock64();
+            if (!lock_ok)
                 {
                     clear_tracking_vars(t);
                     t.state = 0;
@@ -530,7 +540,9 @@ __device__ inline void after_correlation(TrkHot& t, LoopFilter& lf, float2* pbuf
                 {
                     int next_state = 0;
                     run_dll_pll(t, lf);
+                    if (ts) ts[1] = clock64();
                     update_tracking_vars(t);
+                    if (ts) ts[2] = clock64();
                     if (!t.pull_in_transitory)
                         {
                             circ_push(t, t.taps[1]);
@@ -613,28 +625,99 @@ __device__ __forceinline__ int wrap_code(int raw, int L)
     return raw;
 }
 
+// One correlation chunk of kSpl samples per lane (n = n0 + tid + j*256), KT taps,
+// no branches inside: samples past the end are zero and their index clamped.
+template <int IT, bool FROM_WIN, bool FAST, int KT>
+__device__ __forceinline__ void correlate_chunk(const void* __restrict__ iq, const float2* s_win, const float* s_code,
+    const Prep& p, int n0, int vl, int L, const float (&sh_rem)[kMaxTrkTaps], float2& ph, float2 (&acc)[kMaxTrkTaps])
+{
+    float2 xs[kSpl];
+#pragma unroll
+    for (int j = 0; j < kSpl; ++j)
+        {
+            const int n = n0 + (int)threadIdx.x + j * kTrkThreads;
+            const int nc = min(n, vl - 1);
+            const float2 v = FROM_WIN ? s_win[p.woff + nc] : load_iq<IT>(iq, p.off + nc);
+            xs[j] = n < vl ? v : make_float2(0.f, 0.f);
+        }
+#pragma unroll
+    for (int j = 0; j < kSpl; ++j)
+        {
+            const int n = min(n0 + (int)threadIdx.x + j * kTrkThreads, vl - 1);
+            const float2 x = xs[j];
+            const float2 tt = make_float2(x.x * ph.x - x.y * ph.y, x.x * ph.y + x.y * ph.x);
+            const float a = gsdr::mul_rn(p.code_step, (float)n);
+#pragma unroll
+            for (int k = 0; k < KT; ++k)
+                {
+                    // a_avx association: floor(step*n + (shift - rem))
+                    int raw = (int)floorf(gsdr::add_rn(a, sh_rem[k]));
+                    if (FAST)
+                        {
+                            raw += raw < 0 ? L : 0;
+                            raw -= raw >= L ? L : 0;
+                        }
+                    else
+                        raw = wrap_code(raw, L);
+                    const float cv = s_code[raw];
+                    acc[k].x += tt.x * cv;
+                    acc[k].y += tt.y * cv;
+                }
+            ph = make_float2(ph.x * p.wstep.x - ph.y * p.wstep.y, ph.x * p.wstep.y + ph.y * p.wstep.x);
+        }
+}
+
+template <int IT, int KT>
+__device__ __forceinline__ void correlate_call(const void* __restrict__ iq, const float2* s_win, const float* s_code,
+    const Prep& p, int vl, int L, const float (&sh_rem)[kMaxTrkTaps], float2& ph, float2 (&acc)[kMaxTrkTaps])
+{
+    for (int n0 = 0; n0 < vl; n0 += kWinCore)
+        {
+            if (p.woff >= 0)
+                {
+                    if (p.fast)
+                        correlate_chunk<IT, true, true, KT>(iq, s_win, s_code, p, n0, vl, L, sh_rem, ph, acc);
+                    else
+                        correlate_chunk<IT, true, false, KT>(iq, s_win, s_code, p, n0, vl, L, sh_rem, ph, acc);
+                }
+            else
+                {
+                    if (p.fast)
+                        correlate_chunk<IT, false, true, KT>(iq, s_win, s_code, p, n0, vl, L, sh_rem, ph, acc);
+                    else
+                        correlate_chunk<IT, false, false, KT>(iq, s_win, s_code, p, n0, vl, L, sh_rem, ph, acc);
+                }
+        }
+}
+
 // grid = channels; one 256-lane workgroup per channel.  Lane 0 holds the scalar
 // loop state in registers for the whole launch; the histories indexed at run
-// time (prompt buffer, DLL filter) and the replica sit in LDS.
+// time (prompt buffer, DLL filter), the replica and the next call's input window
+// sit in LDS.  While lane 0 runs the loop update of call e, every lane fetches the
+// samples call e+1 will most likely read (the consumed count is one code period
+// +-1 sample) into the LDS window, so the update hides the HBM latency.
 template <int IT>
 __global__ void __launch_bounds__(kTrkThreads) trk_kernel(TrkChan* __restrict__ chans, const float* const* __restrict__ codes,
     const void* __restrict__ iq, uint64_t iq_first, uint64_t iq_items, uint32_t max_epochs,
-    gsdr_trk_epoch* __restrict__ out, uint32_t* __restrict__ nout)
+    gsdr_trk_epoch* __restrict__ out, uint32_t* __restrict__ nout, int code_pad, uint64_t* __restrict__ timing)
 {
-    extern __shared__ float s_code[];
+    extern __shared__ float s_dyn[];
+    float* s_code = s_dyn;
+    float2* s_win = reinterpret_cast<float2*>(s_dyn + code_pad);
     __shared__ LoopFilter s_lf;
     __shared__ float2 s_pbuf[kMaxCn0];
     __shared__ float s_shifts[kMaxTrkTaps];
     __shared__ int s_meta[4];  // state, n_taps, code_samples, vector_length
     __shared__ Prep prep;
     __shared__ float2 s_red[kTrkThreads / 64][kMaxTrkTaps];
+    __shared__ TrkHot s_hot;  // lane 0 copies it into registers only around its loop update
     const int ch = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     TrkChan* gc = chans + ch;
-    TrkHot t;
     if (tid == 0)
         {
-            t = gc->h;
+            const TrkHot t = gc->h;
+            s_hot = t;
             s_lf = gc->code_filter;
             s_meta[0] = t.state;
             s_meta[1] = t.n_taps;
@@ -652,20 +735,28 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(TrkChan* __restrict__ 
     const int K = s_meta[1];
     const int L = s_meta[2];
     const int vl = s_meta[3];
+    const bool use_window = vl <= kWinCore;
     {
         const float* c = codes[ch];
         for (int i = tid; i < L; i += kTrkThreads) s_code[i] = c[i];
     }
+    int64_t win_base = INT64_MIN;  // absolute-index base of the staged window (uniform)
     uint32_t e = 0;
     for (;; ++e)
         {
+            uint64_t tm0 = 0, tm1 = 0, tm2 = 0, tmA = 0, tmB = 0, tmC = 0;
+            if (timing && tid == 0) tm0 = clock64();
             if (tid == 0)
                 {
+                    const TrkHot& t = s_hot;
                     Prep p{};
                     const int64_t off = (int64_t)(t.next_sample - iq_first);
                     p.go = (e < max_epochs) && (t.state == 2 || t.state == 4) && t.next_sample >= iq_first &&
                            (uint64_t)off + (uint64_t)vl <= iq_items;
                     p.off = off;
+                    p.woff = -1;
+                    if (use_window && win_base != INT64_MIN && off >= win_base && off - win_base + vl <= kWinCore + kHalo)
+                        p.woff = (int32_t)(off - win_base);
                     if (p.go)
                         {
                             // do_correlation_step's float arguments (:1069-1075); the
@@ -677,6 +768,18 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(TrkChan* __restrict__ 
                             p.code_step = (float)t.code_phase_step_chips * (float)t.code_samples_per_chip;
                             p.psi0 = -(double)rem_carr;
                             p.theta = -(double)carr_step;
+                            // index range of the call (monotone in n for step > 0)
+                            float smin = 1e30f, smax = -1e30f;
+                            for (int k = 0; k < t.n_taps; ++k)
+                                {
+                                    const float sr = gsdr::sub_rn(t.shifts[k], p.rem_code);
+                                    smin = fminf(smin, sr);
+                                    smax = fmaxf(smax, sr);
+                                }
+                            const float lo = floorf(smin);
+                            const float hi = floorf(gsdr::add_rn(gsdr::mul_rn(p.code_step, (float)(vl - 1)), smax));
+                            const float Lf = (float)t.code_samples;
+                            p.fast = p.code_step >= 0.0f && lo >= -Lf && hi < 2.0f * Lf;
                             const double w = p.theta * (double)kTrkThreads;
                             float sn, cs;
                             sincosf((float)fma(-rint(w * 0.15915494309189533576888376337251), 6.283185307179586476925286766559, w),
@@ -687,8 +790,10 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(TrkChan* __restrict__ 
                 }
             __syncthreads();
             if (!prep.go) break;
+            if (timing && tid == 0) tm1 = clock64();
             // ---- correlation: lane-interleaved samples, fp64 phasor anchor + fp32 steps
             const Prep p = prep;
+            if (timing && tid == 0) tmA = clock64();
             float2 acc[kMaxTrkTaps];
 #pragma unroll
             for (int k = 0; k < kMaxTrkTaps; ++k) acc[k] = make_float2(0.f, 0.f);
@@ -702,34 +807,24 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(TrkChan* __restrict__ 
             }
             float sh_rem[kMaxTrkTaps];
 #pragma unroll
-            for (int k = 0; k < kMaxTrkTaps; ++k) sh_rem[k] = __fsub_rn(s_shifts[k], p.rem_code);
-            for (int n = tid; n < vl; n += kTrkThreads)
-                {
-                    const float2 x = load_iq<IT>(iq, p.off + n);
-                    const float2 tt = make_float2(x.x * ph.x - x.y * ph.y, x.x * ph.y + x.y * ph.x);
-                    const float a = __fmul_rn(p.code_step, (float)n);
-#pragma unroll
-                    for (int k = 0; k < kMaxTrkTaps; ++k)
-                        {
-                            if (k < K)
-                                {
-                                    // a_avx association: floor(step*n + (shift - rem))
-                                    const int raw = (int)floorf(__fadd_rn(a, sh_rem[k]));
-                                    const float cv = s_code[wrap_code(raw, L)];
-                                    acc[k].x += tt.x * cv;
-                                    acc[k].y += tt.y * cv;
-                                }
-                        }
-                    ph = make_float2(ph.x * p.wstep.x - ph.y * p.wstep.y, ph.x * p.wstep.y + ph.y * p.wstep.x);
-                }
+            for (int k = 0; k < kMaxTrkTaps; ++k) sh_rem[k] = gsdr::sub_rn(s_shifts[k], p.rem_code);
+            if (timing && tid == 0) tmB = clock64();
+            if (K <= 3)
+                correlate_call<IT, 3>(iq, s_win, s_code, p, vl, L, sh_rem, ph, acc);
+            else
+                correlate_call<IT, kMaxTrkTaps>(iq, s_win, s_code, p, vl, L, sh_rem, ph, acc);
+            if (timing && tid == 0) tmC = clock64();
 #pragma unroll
             for (int k = 0; k < kMaxTrkTaps; ++k)
                 {
-#pragma unroll
-                    for (int off = 32; off > 0; off >>= 1)
+                    if (k < K)
                         {
-                            acc[k].x += __shfl_xor(acc[k].x, off);
-                            acc[k].y += __shfl_xor(acc[k].y, off);
+#pragma unroll
+                            for (int off = 32; off > 0; off >>= 1)
+                                {
+                                    acc[k].x += __shfl_xor(acc[k].x, off);
+                                    acc[k].y += __shfl_xor(acc[k].y, off);
+                                }
                         }
                 }
             if (lane == 0)
@@ -737,9 +832,29 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(TrkChan* __restrict__ 
 #pragma unroll
                     for (int k = 0; k < kMaxTrkTaps; ++k) s_red[wave][k] = acc[k];
                 }
-            __syncthreads();
+            __syncthreads();  // partials visible; every read of the LDS window done
+            if (timing && tid == 0) tm2 = clock64();
+            // ---- fetch the window the next call most likely reads: [off + vl - kHalo/2, +kWinCore+kHalo)
+            float2 wv[kSpl];
+            float2 wh = make_float2(0.f, 0.f);
+            const int64_t nb = p.off + vl - kHalo / 2;
+            if (use_window)
+                {
+#pragma unroll
+                    for (int j = 0; j < kSpl; ++j)
+                        {
+                            const int64_t i = nb + tid + j * kTrkThreads;
+                            wv[j] = (i >= 0 && (uint64_t)i < iq_items) ? load_iq<IT>(iq, i) : make_float2(0.f, 0.f);
+                        }
+                    if (tid < kHalo)
+                        {
+                            const int64_t i = nb + kWinCore + tid;
+                            wh = (i >= 0 && (uint64_t)i < iq_items) ? load_iq<IT>(iq, i) : make_float2(0.f, 0.f);
+                        }
+                }
             if (tid == 0)
                 {
+                    TrkHot t = s_hot;
 #pragma unroll
                     for (int k = 0; k < kMaxTrkTaps; ++k)
                         {
@@ -765,7 +880,9 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(TrkChan* __restrict__ 
                             t.code_lock_fail_counter = 0;
                         }
                     EpochOut o;
-                    after_correlation(t, s_lf, s_pbuf, n_read, o);
+                    const uint64_t tmD = timing ? clock64() : 0;
+                    after_correlation(t, s_lf, s_pbuf, n_read, o, timing ? timing + ((size_t)ch * max_epochs + e) * 12 + 8 : nullptr);
+                    const uint64_t tmE = timing ? clock64() : 0;
                     gsdr_trk_epoch r;
                     r.sample_counter = n_read;
                     r.state = state0;
@@ -789,13 +906,34 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(TrkChan* __restrict__ 
                     r.evm = t.evm;
                     out[(size_t)ch * max_epochs + e] = r;
                     t.next_sample = n_read + (uint64_t)(int64_t)t.current_prn_length_samples;
+                    s_hot = t;
+                    if (timing)
+                        {
+                            uint64_t* tr = timing + ((size_t)ch * max_epochs + e) * 12;
+                            tr[0] = tm0;
+                            tr[1] = tm1;
+                            tr[2] = tmA;
+                            tr[3] = tmB;
+                            tr[4] = tmC;
+                            tr[5] = tm2;
+                            tr[6] = tmD;
+                            tr[7] = tmE;
+                            tr[11] = clock64();
+                        }
                 }
-            // the next iteration's lane-0 prep follows the update; its barrier orders s_red reuse
+            if (use_window)
+                {
+#pragma unroll
+                    for (int j = 0; j < kSpl; ++j) s_win[tid + j * kTrkThreads] = wv[j];
+                    if (tid < kHalo) s_win[kWinCore + tid] = wh;
+                    win_base = nb;
+                }
+            // the next iteration's prep barrier orders the window writes and s_red reuse
         }
     __syncthreads();
     if (tid == 0)
         {
-            gc->h = t;
+            gc->h = s_hot;
             gc->code_filter = s_lf;
             nout[ch] = e;
         }
@@ -837,6 +975,13 @@ struct gsdr_trk
     void* d_iq{nullptr};
     uint64_t iq_cap{0};
     size_t lds_bytes{0};
+    int code_pad{1024};  // floats reserved for the replica ahead of the LDS window
+    // GSDR_TRK_TIMING=1: per-phase clock64 stamps of every call, summarised on destroy
+    bool timing_on{false};
+    uint64_t* d_timing{nullptr};
+    size_t timing_cap{0};
+    double tsum[11]{};
+    uint64_t tcount{0};
     bool profiling{false};
     std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_recs;
     std::vector<hipEvent_t> prof_pool;
@@ -918,9 +1063,25 @@ int ensure_out(gsdr_trk* k, uint32_t max_epochs)
     return GSDR_OK;
 }
 
+size_t lds_for(int code_pad) { return (size_t)code_pad * sizeof(float) + (size_t)(kWinCore + kHalo) * sizeof(float2); }
+
 int launch(gsdr_trk* k, const void* iq, uint64_t iq_first, uint64_t iq_items, uint32_t max_epochs, gsdr_trk_epoch* out,
     uint32_t* nout, hipStream_t s)
 {
+    uint64_t* timing = nullptr;
+    if (k->timing_on)
+        {
+            const size_t need = (size_t)k->conf.max_channels * max_epochs * 12;
+            if (need > k->timing_cap)
+                {
+                    if (k->d_timing) GSDR_HIP(hipFree(k->d_timing));
+                    k->d_timing = nullptr;
+                    k->timing_cap = 0;
+                    GSDR_HIP(hipMalloc(&k->d_timing, need * sizeof(uint64_t)));
+                    k->timing_cap = need;
+                }
+            timing = k->d_timing;
+        }
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (k->profiling)
         {
@@ -939,15 +1100,33 @@ int launch(gsdr_trk* k, const void* iq, uint64_t iq_first, uint64_t iq_items, ui
     const dim3 grid(k->conf.max_channels);
     if (k->conf.item_type == GSDR_ITEM_GR_COMPLEX)
         hipLaunchKernelGGL((trk_kernel<GSDR_ITEM_GR_COMPLEX>), grid, dim3(kTrkThreads), k->lds_bytes, s, k->d_chans,
-            (const float* const*)k->d_codes, iq, iq_first, iq_items, max_epochs, out, nout);
+            (const float* const*)k->d_codes, iq, iq_first, iq_items, max_epochs, out, nout, k->code_pad, timing);
     else
         hipLaunchKernelGGL((trk_kernel<GSDR_ITEM_CSHORT>), grid, dim3(kTrkThreads), k->lds_bytes, s, k->d_chans,
-            (const float* const*)k->d_codes, iq, iq_first, iq_items, max_epochs, out, nout);
+            (const float* const*)k->d_codes, iq, iq_first, iq_items, max_epochs, out, nout, k->code_pad, timing);
     GSDR_HIP(hipGetLastError());
     if (k->profiling)
         {
             GSDR_HIP(hipEventRecord(e1, s));
             k->prof_recs.push_back({e0, e1});
+        }
+    if (timing)
+        {
+            const uint32_t nch = k->conf.max_channels;
+            std::vector<uint64_t> tm((size_t)nch * max_epochs * 12);
+            std::vector<uint32_t> cnt(nch);
+            GSDR_HIP(hipMemcpyAsync(tm.data(), timing, tm.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+            GSDR_HIP(hipMemcpyAsync(cnt.data(), nout, nch * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+            GSDR_HIP(hipStreamSynchronize(s));
+            for (uint32_t c = 0; c < nch; ++c)
+                for (uint32_t e = 0; e < cnt[c]; ++e)
+                    {
+                        const uint64_t* r = &tm[((size_t)c * max_epochs + e) * 12];
+                        const int seq[] = {0, 1, 2, 3, 4, 5, 6, 8, 9, 10, 7, 11};
+                        for (int q = 0; q + 1 < 12; ++q)
+                            if (r[seq[q + 1]] >= r[seq[q]]) k->tsum[q] += (double)(r[seq[q + 1]] - r[seq[q]]);
+                        k->tcount++;
+                    }
         }
     return GSDR_OK;
 }
@@ -1023,7 +1202,9 @@ int gsdr_trk_create(int device, const gsdr_trk_conf* conf, gsdr_trk** out)
     k->h_chans.resize(nch);
     for (auto& t : k->h_chans) init_channel(k->conf, t);
     k->code_bufs.assign(nch, nullptr);
-    k->lds_bytes = 1024 * sizeof(float);  // grows with the longest replica started (gsdr_trk_start)
+    k->code_pad = 1024;  // grows with the longest replica started (gsdr_trk_start)
+    k->lds_bytes = lds_for(k->code_pad);
+    if (const char* tv = std::getenv("GSDR_TRK_TIMING")) k->timing_on = std::atoi(tv) != 0;
     hipError_t e = hipStreamCreateWithFlags(&k->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipMalloc(&k->d_chans, nch * sizeof(TrkChan));
     if (e == hipSuccess) e = hipMalloc(&k->d_snap[0], nch * sizeof(TrkChan));
@@ -1035,10 +1216,10 @@ int gsdr_trk_create(int device, const gsdr_trk_conf* conf, gsdr_trk** out)
     if (e == hipSuccess) e = hipMemcpy(k->d_chans, k->h_chans.data(), nch * sizeof(TrkChan), hipMemcpyHostToDevice);
     if (e == hipSuccess)
         e = hipFuncSetAttribute((const void*)trk_kernel<GSDR_ITEM_GR_COMPLEX>, hipFuncAttributeMaxDynamicSharedMemorySize,
-            (int)(kMaxCodeFloats * sizeof(float)));
+            (int)lds_for(kMaxCodeFloats));
     if (e == hipSuccess)
         e = hipFuncSetAttribute((const void*)trk_kernel<GSDR_ITEM_CSHORT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-            (int)(kMaxCodeFloats * sizeof(float)));
+            (int)lds_for(kMaxCodeFloats));
     if (e != hipSuccess)
         {
             gsdr::set_error("gsdr_trk_create: %s", hipGetErrorString(e));
@@ -1054,6 +1235,15 @@ void gsdr_trk_destroy(gsdr_trk* k)
     if (!k) return;
     gsdr::DeviceGuard g(k->device);
     if (k->stream) (void)hipStreamSynchronize(k->stream);
+    if (k->timing_on && k->tcount)
+        {
+            static const char* names[] = {"prep", "barrier", "anchor", "samples", "reduce+barrier", "to-update",
+                "cn0+lock", "dll/pll", "nco", "rest", "record"};
+            std::fprintf(stderr, "gsdr_trk timing: %llu calls, clock64 ticks per call:", (unsigned long long)k->tcount);
+            for (int q = 0; q < 11; ++q) std::fprintf(stderr, " %s %.0f", names[q], k->tsum[q] / k->tcount);
+            std::fprintf(stderr, "\n");
+        }
+    if (k->d_timing) (void)hipFree(k->d_timing);
     for (auto& r : k->prof_recs)
         {
             (void)hipEventDestroy(r.first);
@@ -1137,7 +1327,8 @@ int gsdr_trk_start(gsdr_trk* k, int ch, uint32_t prn, const float* code, int cod
     sm_reset(t.lock_sm);
     t.next_sample = nitems_read + (uint64_t)(int64_t)offset;
     *first_sample = t.next_sample;
-    k->lds_bytes = std::max(k->lds_bytes, (size_t)code_samples * sizeof(float));
+    k->code_pad = std::max(k->code_pad, (code_samples + 1) & ~1);
+    k->lds_bytes = lds_for(k->code_pad);
     GSDR_HIP(hipMemcpyAsync(k->code_bufs[ch], code, (size_t)code_samples * sizeof(float), hipMemcpyHostToDevice,
         k->stream));
     GSDR_HIP(hipMemcpyAsync(k->d_chans + ch, &tc, sizeof(TrkChan), hipMemcpyHostToDevice, k->stream));

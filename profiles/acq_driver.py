@@ -47,6 +47,8 @@ def main():
             trk.restore_state(0, sptr)
             trk.run_device(iq_dev.data_ptr(), 0, B * bench.N, B, trk_out.data_ptr(), trk_n.data_ptr(), sptr)
     torch.cuda.synchronize(dev)
+    trk.close()
+    acq.close()
     print("done")
 
 

@@ -74,18 +74,6 @@ struct LoopFilter  // Tracking_loop_filter (tracking_loop_filter.cc)
     float bw, T;
 };
 
-struct CarrierFilter  // Tracking_FLL_PLL_filter (tracking_FLL_PLL_filter.cc)
-{
-    float w, w0p3, w0f2, x, a2, w0f, a3, w0p2, b3, w0p;
-    int order;
-};
-
-struct Smoother  // Exponential_Smoother; the init buffer's in-order float sum is kept running
-{
-    float alpha, one_minus_alpha, old, min_value, offset, init_sum;
-    int samples_init, counter, initializing, nbuf;
-};
-
 __host__ __device__ inline void lf_update(LoopFilter& f)  // :98-197
 {
     float g1, g2, g3, wn;
@@ -151,138 +139,60 @@ __device__ inline float lf_apply(LoopFilter& f, float in)  // :58-93
     return r;
 }
 
-__host__ __device__ inline void cf_set_params(CarrierFilter& p, float fll_bw, float pll_bw, int order)  // :23-58
+// Per-channel configuration: read-only inside the kernel (a separate restrict
+// array, so its fields are fetched with scalar loads into SGPRs).
+struct CfConst  // Tracking_FLL_PLL_filter coefficients
 {
-    p.order = order;
-    if (order == 3)
-        {
-            p.b3 = 2.400F;
-            p.a3 = 1.100F;
-            p.a2 = 1.414F;
-            p.w0p = pll_bw / 0.7845F;
-            p.w0p2 = p.w0p * p.w0p;
-            p.w0p3 = p.w0p2 * p.w0p;
-            p.w0f = fll_bw / 0.53F;
-            p.w0f2 = p.w0f * p.w0f;
-        }
-    else
-        {
-            p.a2 = 1.414F;
-            p.w0p = pll_bw / 0.53F;
-            p.w0p2 = p.w0p * p.w0p;
-            p.w0f = fll_bw / 0.25F;
-        }
-}
+    float w0p3, w0f2, a2, w0f, a3, w0p2, b3, w0p;
+    int order;
+};
 
-__host__ __device__ inline void cf_initialize(CarrierFilter& p, float dop)  // :61-74
+struct SmConst  // Exponential_Smoother parameters
 {
-    if (p.order == 3)
-        {
-            p.x = 2.0F * dop;
-            p.w = 0;
-        }
-    else
-        {
-            p.w = dop;
-            p.x = 0;
-        }
-}
+    float alpha, one_minus_alpha, min_value, offset;
+    int samples_init;
+};
 
-__device__ inline float cf_error(CarrierFilter& p, float fll, float pll, float t)  // :77-101
+struct TrkConst
 {
-    float e;
-    if (p.order == 3)
-        {
-            p.w = p.w + t * (p.w0p3 * pll + p.w0f2 * fll);
-            p.x = p.x + t * (0.5F * p.w + p.a2 * p.w0f * fll + p.a3 * p.w0p2 * pll);
-            e = 0.5F * p.x + p.b3 * p.w0p * pll;
-        }
-    else
-        {
-            const float wn = p.w + pll * p.w0p2 * t + fll * p.w0f * t;
-            e = 0.5F * (wn + p.w) + p.a2 * p.w0p * pll;
-            p.w = wn;
-        }
-    return e;
-}
-
-__host__ __device__ inline void sm_reset(Smoother& s)
-{
-    s.initializing = 1;
-    s.counter = 0;
-    s.nbuf = 0;
-    s.init_sum = 0.0F;
-}
-
-__device__ inline float sm_smooth(Smoother& s, float raw)  // exponential_smoother.cc:84-110
-{
-    float v;
-    if (s.initializing)
-        {
-            s.counter++;
-            v = raw;
-            s.init_sum = s.init_sum + v;
-            s.nbuf++;
-            if (s.counter == s.samples_init)
-                {
-                    s.old = s.init_sum / (float)s.nbuf;
-                    if (s.old < (s.min_value + s.offset))
-                        {
-                            s.counter = 0;
-                            s.nbuf = 0;
-                            s.init_sum = 0.0F;
-                        }
-                    else
-                        s.initializing = 0;
-                }
-        }
-    else
-        {
-            v = s.alpha * raw + s.one_minus_alpha * s.old;
-            s.old = v;
-        }
-    return v;
-}
-
-// ------------------------------------------------------------------ channel state
-// Scalar loop state: lives in lane 0's registers for a whole launch.
-struct TrkHot
-{
-    // configuration (Dll_Pll_Conf + signal constants)
-    double fs_in, code_period, code_chip_rate, signal_carrier_freq, carrier_lock_threshold;
+    double fs_in, code_period, code_chip_rate, signal_carrier_freq, carrier_lock_threshold, current_correlation_time_s;
+    uint64_t acq_sample_stamp;
+    uint64_t pull_in_span;   // (pull_in_time_s + 1) * (int)fs_in: the integer-second test of :1797 flips there
+    uint64_t bit_sync_span;  // (bit_synchronization_time_limit_s + 1) * (int)fs_in (:1866)
     float early_late_space_chips;
-    int32_t vector_length, code_length_chips, code_samples_per_chip, symbols_per_bit;
-    int32_t cn0_samples, cn0_min, max_code_lock_fail, max_carrier_lock_fail;
-    uint32_t pull_in_time_s, bit_sync_limit_s;
-    int32_t extend_correlation_symbols, enable_fll_pull_in, enable_fll_steady_state, carrier_aiding;
-    int32_t n_taps, code_samples;
     float shifts[kMaxTrkTaps];
     uint32_t preamble[5];
-    // loop objects without history arrays
-    Smoother cn0_sm, lock_sm;
-    CarrierFilter carrier_filter;
-    // state (dll_pll_veml_tracking.h:117-209)
-    double acq_code_phase_samples, acq_carrier_doppler_hz, current_correlation_time_s;
-    double carr_phase_error_hz, carr_freq_error_hz, carr_error_filt_hz, code_error_chips, code_error_filt_chips;
+    int32_t vector_length, code_length_chips, code_samples_per_chip, symbols_per_bit;
+    int32_t cn0_samples, cn0_min, max_code_lock_fail, max_carrier_lock_fail;
+    int32_t extend_correlation_symbols, enable_fll_pull_in, enable_fll_steady_state, carrier_aiding;
+    int32_t n_taps, code_samples;
+    uint32_t prn;
+    CfConst cf;
+    SmConst sm[2];  // 0: CN0, 1: carrier lock test
+};
+
+// Mutable scalar loop state (dll_pll_veml_tracking.h:117-209 minus the
+// per-call temporaries): in wave 0's registers for a whole launch.
+struct TrkHot
+{
     double code_freq_chips, carrier_doppler_hz, acc_carrier_phase_rad, rem_code_phase_chips;
     double carrier_lock_test, cn0_db_hz, evm;
     double carrier_phase_step_rad, carrier_phase_rate_step_rad, code_phase_step_chips, code_phase_rate_step_chips;
     double rem_code_phase_samples;
-    float2 taps[kMaxTrkTaps];
+    uint64_t next_sample;
     float2 E_accu, P_accu, P_accu_old, L_accu, P_data_accu;
-    uint32_t circ[5];  // signs of the last kPreambleLen prompts (1 = real < 0), newest at bit 0
+    float cf_w, cf_x;                  // Tracking_FLL_PLL_filter state
+    float sm_old[2], sm_sum[2];        // smoothers: value and running init sum
+    int32_t sm_counter[2], sm_init[2];
+    uint32_t circ[5];                  // signs of the last kPreambleLen prompts (1 = real < 0), newest at bit 0
     int32_t circ_size;
-    uint64_t acq_sample_stamp, next_sample;
     float rem_carr_phase_rad, spc;
     int32_t state, current_prn_length_samples, current_symbol, current_data_symbol, cn0_estimation_counter;
     int32_t carrier_lock_fail_counter, code_lock_fail_counter;
     int32_t pull_in_transitory, cloop, acc_carrier_phase_initialized, flag_pll_180;
-    uint32_t prn;
-    int32_t assoc;
 };
 
-// Device-memory image of one channel: the scalars plus the dynamically indexed
-// histories (kept in LDS during a launch).
+// Device-memory image of the mutable part of one channel.
 struct TrkChan
 {
     TrkHot h;
@@ -290,7 +200,7 @@ struct TrkChan
     float2 prompt_buffer[kMaxCn0];
 };
 
-struct Prep  // lane-0 -> workgroup broadcast of one epoch's NCO
+struct Prep  // lane-0 -> workgroup broadcast of one call's NCO
 {
     double psi0, theta;
     float2 wstep;
@@ -301,7 +211,66 @@ struct Prep  // lane-0 -> workgroup broadcast of one epoch's NCO
     int32_t fast;  // every code index of the call lies in [-L, 2L): branch-free wrap
 };
 
-// ------------------------------------------------------------------ lane-0 loop body
+// ------------------------------------------------------------------ wave-0 loop body
+// The loop update runs on all 64 lanes of wave 0 with identical (uniform)
+// values; the loops over the CN0 buffer put one element on each lane and sum in
+// the reference's element order with readlane, so results are bit-identical to
+// the sequential code.  Memory writes are done by lane 0.
+__device__ __forceinline__ float lane_f(float v, int i) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), i)); }
+
+__device__ inline float cf_error(const CfConst& k, TrkHot& t, float fll, float pll, float tc)  // :77-101
+{
+    float e;
+    if (k.order == 3)
+        {
+            t.cf_w = t.cf_w + tc * (k.w0p3 * pll + k.w0f2 * fll);
+            t.cf_x = t.cf_x + tc * (0.5F * t.cf_w + k.a2 * k.w0f * fll + k.a3 * k.w0p2 * pll);
+            e = 0.5F * t.cf_x + k.b3 * k.w0p * pll;
+        }
+    else
+        {
+            const float wn = t.cf_w + pll * k.w0p2 * tc + fll * k.w0f * tc;
+            e = 0.5F * (wn + t.cf_w) + k.a2 * k.w0p * pll;
+            t.cf_w = wn;
+        }
+    return e;
+}
+
+__device__ inline float sm_smooth(const SmConst& k, TrkHot& t, int w, float raw)  // exponential_smoother.cc:84-110
+{
+    float v;
+    if (t.sm_init[w])
+        {
+            t.sm_counter[w]++;
+            v = raw;
+            t.sm_sum[w] = t.sm_sum[w] + v;
+            if (t.sm_counter[w] == k.samples_init)
+                {
+                    t.sm_old[w] = t.sm_sum[w] / (float)t.sm_counter[w];
+                    if (t.sm_old[w] < (k.min_value + k.offset))
+                        {
+                            t.sm_counter[w] = 0;
+                            t.sm_sum[w] = 0.0F;
+                        }
+                    else
+                        t.sm_init[w] = 0;
+                }
+        }
+    else
+        {
+            v = k.alpha * raw + k.one_minus_alpha * t.sm_old[w];
+            t.sm_old[w] = v;
+        }
+    return v;
+}
+
+__host__ __device__ inline void sm_reset(TrkHot& t, int w)
+{
+    t.sm_init[w] = 1;
+    t.sm_counter[w] = 0;
+    t.sm_sum[w] = 0.0F;
+}
+
 __device__ inline double pll_cloop_two_quadrant_atan(float2 p)  // tracking_discriminators.cc:92-99
 {
     if (p.x != 0.0F) return (double)atanf(p.y / p.x);
@@ -331,51 +300,9 @@ __device__ inline double dll_nc_e_minus_l(float2 e, float2 l, float spc, float s
     return (double)((y - slope * spc) / slope) * (pe - pl) / s;
 }
 
-__device__ inline float cn0_m2m4(const float2* b, int length, float coh)  // lock_detectors.cc:90-120
-{
-    float snr, psig = 0.0F, m2 = 0.0F, m4 = 0.0F, aux;
-    const float n = (float)length;
-    for (int i = 0; i < length; i++)
-        {
-            psig += fabsf(b[i].x);
-            aux = b[i].y * b[i].y + b[i].x * b[i].x;
-            m2 += aux;
-            m4 += (aux * aux);
-        }
-    psig /= n;
-    psig = psig * psig;
-    m2 /= n;
-    m4 /= n;
-    aux = sqrtf(2.0F * m2 * m2 - m4);
-    if (isnan(aux))
-        snr = psig / (m2 - psig);
-    else
-        snr = aux / (m2 - aux);
-    return 10.0F * log10f(snr) - 10.0F * log10f(coh);
-}
-
-__device__ inline float carrier_lock_detector(const float2* b, int length)  // :133-148
-{
-    float si = 0.0F, sq = 0.0F;
-    for (int i = 0; i < length; i++)
-        {
-            si += b[i].x;
-            sq += b[i].y;
-        }
-    const float nbp = si * si + sq * sq;
-    const float nbd = si * si - sq * sq;
-    return nbd / nbp;
-}
-
 __device__ inline void clear_tracking_vars(TrkHot& t)  // :1192-1213
 {
-    for (int k = 0; k < kMaxTrkTaps; ++k) t.taps[k] = make_float2(0.f, 0.f);
     t.P_accu_old = make_float2(0.f, 0.f);
-    t.carr_phase_error_hz = 0.0;
-    t.carr_freq_error_hz = 0.0;
-    t.carr_error_filt_hz = 0.0;
-    t.code_error_chips = 0.0;
-    t.code_error_filt_chips = 0.0;
     t.current_symbol = 0;
     t.current_data_symbol = 0;
     t.circ_size = 0;
@@ -384,94 +311,127 @@ __device__ inline void clear_tracking_vars(TrkHot& t)  // :1192-1213
     t.code_phase_rate_step_chips = 0.0;
 }
 
-__device__ inline int cn0_and_lock(TrkHot& t, float2* pbuf, double coh)  // :970-1056
+// cn0_and_tracking_lock_status (:970-1056) with cn0_m2m4_estimator and
+// carrier_lock_detector (lock_detectors.cc:90-148); wave 0, lane = element.
+__device__ inline int cn0_and_lock(const TrkConst& c, TrkHot& t, float2* pbuf, double coh, int lane)
 {
-    const int n = t.cn0_samples;
+    const int n = c.cn0_samples;
     if (t.cn0_estimation_counter < n)
         {
-            pbuf[t.cn0_estimation_counter] = t.P_accu;
+            if (lane == 0) pbuf[t.cn0_estimation_counter] = t.P_accu;
             t.cn0_estimation_counter++;
             return 1;
         }
-    pbuf[t.cn0_estimation_counter % n] = t.P_accu;
+    const int widx = t.cn0_estimation_counter % n;
+    float2 ei = make_float2(0.f, 0.f);
+    if (lane < n) ei = lane == widx ? t.P_accu : pbuf[lane];
+    if (lane == 0) pbuf[widx] = t.P_accu;
     t.cn0_estimation_counter++;
-    const float raw = cn0_m2m4(pbuf, n, (float)coh);
-    t.cn0_db_hz = (double)sm_smooth(t.cn0_sm, raw);
-    t.carrier_lock_test = (double)sm_smooth(t.lock_sm, carrier_lock_detector(pbuf, 1));
+    // cn0_m2m4_estimator: Psig += |re|; aux = im*im + re*re; m2 += aux; m4 += aux*aux
+    const float a_i = fabsf(ei.x);
+    const float aux_i = ei.y * ei.y + ei.x * ei.x;
+    const float aux2_i = aux_i * aux_i;
+    float psig = 0.0F, m2 = 0.0F, m4 = 0.0F;
+    for (int i = 0; i < n; i++)
+        {
+            psig += lane_f(a_i, i);
+            m2 += lane_f(aux_i, i);
+            m4 += lane_f(aux2_i, i);
+        }
+    const float fn = (float)n;
+    psig /= fn;
+    psig = psig * psig;
+    m2 /= fn;
+    m4 /= fn;
+    float aux = sqrtf(2.0F * m2 * m2 - m4);
+    float snr;
+    if (isnan(aux))
+        snr = psig / (m2 - psig);
+    else
+        snr = aux / (m2 - aux);
+    const float raw = 10.0F * log10f(snr) - 10.0F * log10f((float)coh);
+    t.cn0_db_hz = (double)sm_smooth(c.sm[0], t, 0, raw);
+    // carrier_lock_detector(buffer, 1): element 0 only
+    const float si = 0.0F + lane_f(ei.x, 0), sq = 0.0F + lane_f(ei.y, 0);
+    const float lock = (si * si - sq * sq) / (si * si + sq * sq);
+    t.carrier_lock_test = (double)sm_smooth(c.sm[1], t, 1, lock);
     if (!t.pull_in_transitory)
         {
-            if (t.carrier_lock_test < t.carrier_lock_threshold)
+            if (t.carrier_lock_test < c.carrier_lock_threshold)
                 t.carrier_lock_fail_counter++;
             else if (t.carrier_lock_fail_counter > 0)
                 t.carrier_lock_fail_counter--;
-            if (t.cn0_db_hz < t.cn0_min)
+            if (t.cn0_db_hz < c.cn0_min)
                 t.code_lock_fail_counter++;
             else if (t.code_lock_fail_counter > 0)
                 t.code_lock_fail_counter--;
         }
-    if (t.carrier_lock_fail_counter > t.max_carrier_lock_fail || t.code_lock_fail_counter > t.max_code_lock_fail)
+    if (t.carrier_lock_fail_counter > c.max_carrier_lock_fail || t.code_lock_fail_counter > c.max_code_lock_fail)
         {
             t.carrier_lock_fail_counter = 0;
             t.code_lock_fail_counter = 0;
             return 0;
         }
     // EVM (fork indicator, :1027-1053)
-    float d, s = 0;
-    for (int i = 0; i < n; i++) s = s + pbuf[i].x * pbuf[i].x;
-    d = s / (float)n;
+    const float sq_i = ei.x * ei.x;
+    float s = 0;
+    for (int i = 0; i < n; i++) s = s + lane_f(sq_i, i);
+    float d = s / fn;
     d = sqrtf(d);
+    const float ea = fabsf(ei.x / d) - 1.0F;
+    const float eb = fabsf(ei.y / d) - 0.0F;
+    const float aa_i = ea * ea, bb_i = eb * eb;
     s = 0;
     for (int i = 0; i < n; i++)
         {
-            const float a = fabsf(pbuf[i].x / d) - 1.0F;
-            const float b = fabsf(pbuf[i].y / d) - 0.0F;
-            s = s + a * a + b * b;
+            s = s + lane_f(aa_i, i);
+            s = s + lane_f(bb_i, i);
         }
-    t.evm = sqrt((double)(s / (float)n / 1.0F));
+    t.evm = sqrt((double)(s / fn / 1.0F));
     return 1;
 }
 
-__device__ inline void run_dll_pll(TrkHot& t, LoopFilter& lf)  // :1092-1179 (no Doppler correction)
+__device__ inline void run_dll_pll(const TrkConst& c, TrkHot& t, LoopFilter& lf)  // :1092-1179 (no Doppler correction)
 {
-    t.carr_phase_error_hz = pll_cloop_two_quadrant_atan(t.P_accu) / kTwoPi;
-    if ((t.pull_in_transitory && t.enable_fll_pull_in) || t.enable_fll_steady_state)
+    const double carr_phase_error_hz = pll_cloop_two_quadrant_atan(t.P_accu) / kTwoPi;
+    double carr_error_filt_hz;
+    if ((t.pull_in_transitory && c.enable_fll_pull_in) || c.enable_fll_steady_state)
         {
-            t.carr_freq_error_hz = fll_diff_atan(t.P_accu_old, t.P_accu, 0, t.current_correlation_time_s) / kTwoPi;
+            const double carr_freq_error_hz = fll_diff_atan(t.P_accu_old, t.P_accu, 0, c.current_correlation_time_s) / kTwoPi;
             t.P_accu_old = t.P_accu;
-            if (t.pull_in_transitory && t.enable_fll_pull_in)
-                t.carr_error_filt_hz = (double)cf_error(t.carrier_filter, (float)t.carr_freq_error_hz, 0.0F,
-                    (float)t.current_correlation_time_s);
+            if (t.pull_in_transitory && c.enable_fll_pull_in)
+                carr_error_filt_hz = (double)cf_error(c.cf, t, (float)carr_freq_error_hz, 0.0F,
+                    (float)c.current_correlation_time_s);
             else
-                t.carr_error_filt_hz = (double)cf_error(t.carrier_filter, (float)t.carr_freq_error_hz,
-                    (float)t.carr_phase_error_hz, (float)t.current_correlation_time_s);
+                carr_error_filt_hz = (double)cf_error(c.cf, t, (float)carr_freq_error_hz, (float)carr_phase_error_hz,
+                    (float)c.current_correlation_time_s);
         }
     else
         {
-            t.carr_error_filt_hz = (double)cf_error(t.carrier_filter, 0, (float)t.carr_phase_error_hz,
-                (float)t.current_correlation_time_s);
+            carr_error_filt_hz = (double)cf_error(c.cf, t, 0, (float)carr_phase_error_hz, (float)c.current_correlation_time_s);
         }
-    t.carrier_doppler_hz = t.carr_error_filt_hz;
-    t.code_error_chips = dll_nc_e_minus_l(t.E_accu, t.L_accu, t.spc, 1.0F, 1.0F);
-    t.code_error_filt_chips = (double)lf_apply(lf, (float)t.code_error_chips);
-    t.code_freq_chips = t.code_chip_rate - t.code_error_filt_chips;
-    if (t.carrier_aiding) t.code_freq_chips += t.carrier_doppler_hz * t.code_chip_rate / t.signal_carrier_freq;
+    t.carrier_doppler_hz = carr_error_filt_hz;
+    const double code_error_chips = dll_nc_e_minus_l(t.E_accu, t.L_accu, t.spc, 1.0F, 1.0F);
+    const double code_error_filt_chips = (double)lf_apply(lf, (float)code_error_chips);
+    t.code_freq_chips = c.code_chip_rate - code_error_filt_chips;
+    if (c.carrier_aiding) t.code_freq_chips += t.carrier_doppler_hz * c.code_chip_rate / c.signal_carrier_freq;
 }
 
-__device__ inline void update_tracking_vars(TrkHot& t)  // :1216-1287 (high_dyn = false)
+__device__ inline void update_tracking_vars(const TrkConst& c, TrkHot& t)  // :1216-1287 (high_dyn = false)
 {
     const double T_chip = 1.0 / t.code_freq_chips;
-    const double T_prn = T_chip * (double)t.code_length_chips;
-    const double T_prn_samples = T_prn * t.fs_in;
+    const double T_prn = T_chip * (double)c.code_length_chips;
+    const double T_prn_samples = T_prn * c.fs_in;
     const double K_blk = T_prn_samples + t.rem_code_phase_samples;
     t.current_prn_length_samples = (int32_t)floor(K_blk);
-    t.carrier_phase_step_rad = kTwoPi * t.carrier_doppler_hz / t.fs_in;
+    t.carrier_phase_step_rad = kTwoPi * t.carrier_doppler_hz / c.fs_in;
     const double len = (double)t.current_prn_length_samples;
     t.rem_carr_phase_rad += (float)(t.carrier_phase_step_rad * len + 0.5 * t.carrier_phase_rate_step_rad * len * len);
     t.rem_carr_phase_rad = (float)fmod((double)t.rem_carr_phase_rad, kTwoPi);
     t.acc_carrier_phase_rad -= (t.carrier_phase_step_rad * len + 0.5 * t.carrier_phase_rate_step_rad * len * len);
-    t.code_phase_step_chips = t.code_freq_chips / t.fs_in;
+    t.code_phase_step_chips = t.code_freq_chips / c.fs_in;
     t.rem_code_phase_samples = K_blk - len;
-    t.rem_code_phase_chips = t.code_freq_chips * t.rem_code_phase_samples / t.fs_in;
+    t.rem_code_phase_chips = t.code_freq_chips * t.rem_code_phase_samples / c.fs_in;
 }
 
 __device__ inline void circ_push(TrkHot& t, float2 prompt)
@@ -490,13 +450,13 @@ __device__ inline void circ_push(TrkHot& t, float2 prompt)
 
 // acquire_secondary (:923-967): corr = sum over the buffer of +-1 by sign match
 // = 160 - 2 * mismatches; |corr| == 160 only on a full match or full inversion.
-__device__ inline int acquire_secondary(TrkHot& t)
+__device__ inline int acquire_secondary(const TrkConst& c, TrkHot& t)
 {
     int mism = 0;
-    for (int w = 0; w < 5; ++w) mism += __popc(t.circ[w] ^ t.preamble[w]);
+    for (int w = 0; w < 5; ++w) mism += __popc(t.circ[w] ^ c.preamble[w]);
     if (mism == 0)
         {
-            t.flag_pll_180 = 0;  // corr = +160 (string '1' <-> real >= 0 mismatch accounted in the register)
+            t.flag_pll_180 = 0;
             return 1;
         }
     if (mism == kPreambleLen)
@@ -513,24 +473,23 @@ struct EpochOut
     double prompt_i, prompt_q;
 };
 
-// One general_work call after the correlation (taps in t.taps): states 2 and 4.
-__device__ inline void after_correlation(TrkHot& t, LoopFilter& lf, float2* pbuf, uint64_t nitems_read, EpochOut& o,
-    uint64_t* ts = nullptr)
+// One general_work call after the correlation (taps given): states 2 and 4.
+__device__ inline void after_correlation(const TrkConst& c, TrkHot& t, LoopFilter& lf, float2* pbuf,
+    const float2 (&taps)[kMaxTrkTaps], uint64_t nitems_read, int lane, EpochOut& o)
 {
     o.flags = 0;
     o.prompt_i = 0.0;
     o.prompt_q = 0.0;
+    const float2 tE = taps[0], tP = taps[1], tL = taps[2];
     if (t.state == 2)
         {
-            t.E_accu = t.taps[0];
-            t.P_accu = t.taps[1];
-            t.L_accu = t.taps[2];
-            t.spc = t.early_late_space_chips;
-            if ((uint64_t)t.bit_sync_limit_s < (nitems_read - t.acq_sample_stamp) / (uint64_t)(int)t.fs_in)
+            t.E_accu = tE;
+            t.P_accu = tP;
+            t.L_accu = tL;
+            t.spc = c.early_late_space_chips;
+            if (nitems_read < c.acq_sample_stamp || nitems_read - c.acq_sample_stamp >= c.bit_sync_span)
                 t.carrier_lock_fail_counter = 300000;
-            const int lock_ok = cn0_and_lock(t, pbuf, t.code_period);
-            if (ts) ts[0] = clock64();
-            if (!lock_ok)
+            if (!cn0_and_lock(c, t, pbuf, c.code_period, lane))
                 {
                     clear_tracking_vars(t);
                     t.state = 0;
@@ -539,14 +498,12 @@ __device__ inline void after_correlation(TrkHot& t, LoopFilter& lf, float2* pbuf
             else
                 {
                     int next_state = 0;
-                    run_dll_pll(t, lf);
-                    if (ts) ts[1] = clock64();
-                    update_tracking_vars(t);
-                    if (ts) ts[2] = clock64();
+                    run_dll_pll(c, t, lf);
+                    update_tracking_vars(c, t);
                     if (!t.pull_in_transitory)
                         {
-                            circ_push(t, t.taps[1]);
-                            if (t.circ_size == kPreambleLen) next_state = acquire_secondary(t);
+                            circ_push(t, tP);
+                            if (t.circ_size == kPreambleLen) next_state = acquire_secondary(c, t);
                         }
                     if (next_state)
                         {
@@ -562,18 +519,18 @@ __device__ inline void after_correlation(TrkHot& t, LoopFilter& lf, float2* pbuf
         }
     else  // state 4
         {
-            t.E_accu.x += t.taps[0].x;
-            t.E_accu.y += t.taps[0].y;
-            t.P_accu.x += t.taps[1].x;
-            t.P_accu.y += t.taps[1].y;
-            t.L_accu.x += t.taps[2].x;
-            t.L_accu.y += t.taps[2].y;
-            t.P_data_accu.x += t.taps[1].x;
-            t.P_data_accu.y += t.taps[1].y;
+            t.E_accu.x += tE.x;
+            t.E_accu.y += tE.y;
+            t.P_accu.x += tP.x;
+            t.P_accu.y += tP.y;
+            t.L_accu.x += tL.x;
+            t.L_accu.y += tL.y;
+            t.P_data_accu.x += tP.x;
+            t.P_data_accu.y += tP.y;
             t.current_data_symbol++;
-            t.current_data_symbol %= t.symbols_per_bit;
+            t.current_data_symbol %= c.symbols_per_bit;
             t.cloop = 1;
-            if (!cn0_and_lock(t, pbuf, t.code_period * (double)t.extend_correlation_symbols))
+            if (!cn0_and_lock(c, t, pbuf, c.code_period * (double)c.extend_correlation_symbols, lane))
                 {
                     clear_tracking_vars(t);
                     t.state = 0;
@@ -581,8 +538,8 @@ __device__ inline void after_correlation(TrkHot& t, LoopFilter& lf, float2* pbuf
                 }
             else
                 {
-                    run_dll_pll(t, lf);
-                    update_tracking_vars(t);
+                    run_dll_pll(c, t, lf);
+                    update_tracking_vars(c, t);
                     if (!t.acc_carrier_phase_initialized)
                         {
                             t.acc_carrier_phase_rad = -(double)t.rem_carr_phase_rad;
@@ -625,8 +582,8 @@ __device__ __forceinline__ int wrap_code(int raw, int L)
     return raw;
 }
 
-// One correlation chunk of kSpl samples per lane (n = n0 + tid + j*256), KT taps,
-// no branches inside: samples past the end are zero and their index clamped.
+// One correlation chunk of kSpl samples per lane (n = n0 + tid + j*kTrkThreads),
+// KT taps, no branches inside: samples past the end are zero and their index clamped.
 template <int IT, bool FROM_WIN, bool FAST, int KT>
 __device__ __forceinline__ void correlate_chunk(const void* __restrict__ iq, const float2* s_win, const float* s_code,
     const Prep& p, int n0, int vl, int L, const float (&sh_rem)[kMaxTrkTaps], float2& ph, float2 (&acc)[kMaxTrkTaps])
@@ -690,65 +647,64 @@ __device__ __forceinline__ void correlate_call(const void* __restrict__ iq, cons
         }
 }
 
-// grid = channels; one 256-lane workgroup per channel.  Lane 0 holds the scalar
-// loop state in registers for the whole launch; the histories indexed at run
-// time (prompt buffer, DLL filter), the replica and the next call's input window
-// sit in LDS.  While lane 0 runs the loop update of call e, every lane fetches the
-// samples call e+1 will most likely read (the consumed count is one code period
-// +-1 sample) into the LDS window, so the update hides the HBM latency.
+// grid = channels; one kTrkThreads-lane workgroup per channel.  Wave 0 holds the
+// mutable loop state in registers for the whole launch (uniform across its
+// lanes); the configuration comes through scalar loads; the histories indexed at
+// run time (CN0 buffer, DLL filter), the replica and the next call's input window
+// sit in LDS.  While wave 0 runs the loop update of call e, every lane fetches
+// the samples call e+1 will most likely read (the consumed count is one code
+// period +-1 sample), so the update hides the HBM latency.
 template <int IT>
-__global__ void __launch_bounds__(kTrkThreads) trk_kernel(TrkChan* __restrict__ chans, const float* const* __restrict__ codes,
-    const void* __restrict__ iq, uint64_t iq_first, uint64_t iq_items, uint32_t max_epochs,
-    gsdr_trk_epoch* __restrict__ out, uint32_t* __restrict__ nout, int code_pad, uint64_t* __restrict__ timing)
+__global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __restrict__ consts,
+    TrkChan* __restrict__ chans, const float* const* __restrict__ codes, const void* __restrict__ iq, uint64_t iq_first,
+    uint64_t iq_items, uint32_t max_epochs, gsdr_trk_epoch* __restrict__ out, uint32_t* __restrict__ nout, int code_pad,
+    uint64_t* __restrict__ timing)
 {
     extern __shared__ float s_dyn[];
     float* s_code = s_dyn;
     float2* s_win = reinterpret_cast<float2*>(s_dyn + code_pad);
     __shared__ LoopFilter s_lf;
     __shared__ float2 s_pbuf[kMaxCn0];
-    __shared__ float s_shifts[kMaxTrkTaps];
-    __shared__ int s_meta[4];  // state, n_taps, code_samples, vector_length
+    __shared__ int s_state;
     __shared__ Prep prep;
     __shared__ float2 s_red[kTrkThreads / 64][kMaxTrkTaps];
-    __shared__ TrkHot s_hot;  // lane 0 copies it into registers only around its loop update
     const int ch = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const TrkConst& c = consts[ch];
     TrkChan* gc = chans + ch;
+    // The tracking loop is a latency chain that shares its CUs with the
+    // acquisition grid running on another queue: raise the issue priority.
+    __builtin_amdgcn_s_setprio(3);
+    TrkHot t;
+    if (wave == 0) t = gc->h;
     if (tid == 0)
         {
-            const TrkHot t = gc->h;
-            s_hot = t;
             s_lf = gc->code_filter;
-            s_meta[0] = t.state;
-            s_meta[1] = t.n_taps;
-            s_meta[2] = t.code_samples;
-            s_meta[3] = t.vector_length;
-            for (int k = 0; k < kMaxTrkTaps; ++k) s_shifts[k] = t.shifts[k];
+            s_state = t.state;
         }
     if (tid < kMaxCn0) s_pbuf[tid] = gc->prompt_buffer[tid];
     __syncthreads();
-    if (s_meta[0] != 2 && s_meta[0] != 4)
+    if (s_state != 2 && s_state != 4)
         {
             if (tid == 0) nout[ch] = 0;
             return;
         }
-    const int K = s_meta[1];
-    const int L = s_meta[2];
-    const int vl = s_meta[3];
+    const int K = c.n_taps;
+    const int L = c.code_samples;
+    const int vl = c.vector_length;
     const bool use_window = vl <= kWinCore;
     {
-        const float* c = codes[ch];
-        for (int i = tid; i < L; i += kTrkThreads) s_code[i] = c[i];
+        const float* cd = codes[ch];
+        for (int i = tid; i < L; i += kTrkThreads) s_code[i] = cd[i];
     }
     int64_t win_base = INT64_MIN;  // absolute-index base of the staged window (uniform)
     uint32_t e = 0;
     for (;; ++e)
         {
-            uint64_t tm0 = 0, tm1 = 0, tm2 = 0, tmA = 0, tmB = 0, tmC = 0;
+            uint64_t tm0 = 0, tm1 = 0, tm2 = 0;
             if (timing && tid == 0) tm0 = clock64();
             if (tid == 0)
                 {
-                    const TrkHot& t = s_hot;
                     Prep p{};
                     const int64_t off = (int64_t)(t.next_sample - iq_first);
                     p.go = (e < max_epochs) && (t.state == 2 || t.state == 4) && t.next_sample >= iq_first &&
@@ -764,21 +720,21 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(TrkChan* __restrict__ 
                             // (cpu_multicorrelator_real_codes.cc:114-123) as angles
                             const float rem_carr = t.rem_carr_phase_rad;
                             const float carr_step = (float)t.carrier_phase_step_rad;
-                            p.rem_code = (float)t.rem_code_phase_chips * (float)t.code_samples_per_chip;
-                            p.code_step = (float)t.code_phase_step_chips * (float)t.code_samples_per_chip;
+                            p.rem_code = (float)t.rem_code_phase_chips * (float)c.code_samples_per_chip;
+                            p.code_step = (float)t.code_phase_step_chips * (float)c.code_samples_per_chip;
                             p.psi0 = -(double)rem_carr;
                             p.theta = -(double)carr_step;
                             // index range of the call (monotone in n for step > 0)
                             float smin = 1e30f, smax = -1e30f;
-                            for (int k = 0; k < t.n_taps; ++k)
+                            for (int k = 0; k < K; ++k)
                                 {
-                                    const float sr = gsdr::sub_rn(t.shifts[k], p.rem_code);
+                                    const float sr = gsdr::sub_rn(c.shifts[k], p.rem_code);
                                     smin = fminf(smin, sr);
                                     smax = fmaxf(smax, sr);
                                 }
                             const float lo = floorf(smin);
                             const float hi = floorf(gsdr::add_rn(gsdr::mul_rn(p.code_step, (float)(vl - 1)), smax));
-                            const float Lf = (float)t.code_samples;
+                            const float Lf = (float)L;
                             p.fast = p.code_step >= 0.0f && lo >= -Lf && hi < 2.0f * Lf;
                             const double w = p.theta * (double)kTrkThreads;
                             float sn, cs;
@@ -793,7 +749,6 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(TrkChan* __restrict__ 
             if (timing && tid == 0) tm1 = clock64();
             // ---- correlation: lane-interleaved samples, fp64 phasor anchor + fp32 steps
             const Prep p = prep;
-            if (timing && tid == 0) tmA = clock64();
             float2 acc[kMaxTrkTaps];
 #pragma unroll
             for (int k = 0; k < kMaxTrkTaps; ++k) acc[k] = make_float2(0.f, 0.f);
@@ -807,13 +762,11 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(TrkChan* __restrict__ 
             }
             float sh_rem[kMaxTrkTaps];
 #pragma unroll
-            for (int k = 0; k < kMaxTrkTaps; ++k) sh_rem[k] = gsdr::sub_rn(s_shifts[k], p.rem_code);
-            if (timing && tid == 0) tmB = clock64();
+            for (int k = 0; k < kMaxTrkTaps; ++k) sh_rem[k] = gsdr::sub_rn(c.shifts[k], p.rem_code);
             if (K <= 3)
                 correlate_call<IT, 3>(iq, s_win, s_code, p, vl, L, sh_rem, ph, acc);
             else
                 correlate_call<IT, kMaxTrkTaps>(iq, s_win, s_code, p, vl, L, sh_rem, ph, acc);
-            if (timing && tid == 0) tmC = clock64();
 #pragma unroll
             for (int k = 0; k < kMaxTrkTaps; ++k)
                 {
@@ -852,74 +805,71 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(TrkChan* __restrict__ 
                             wh = (i >= 0 && (uint64_t)i < iq_items) ? load_iq<IT>(iq, i) : make_float2(0.f, 0.f);
                         }
                 }
-            if (tid == 0)
+            if (wave == 0)
                 {
-                    TrkHot t = s_hot;
+                    float2 taps[kMaxTrkTaps];
 #pragma unroll
                     for (int k = 0; k < kMaxTrkTaps; ++k)
                         {
                             float2 r = make_float2(0.f, 0.f);
                             if (k < K)
                                 {
+#pragma unroll
                                     for (int w = 0; w < kTrkThreads / 64; ++w)
                                         {
                                             r.x += s_red[w][k].x;
                                             r.y += s_red[w][k].y;
                                         }
                                 }
-                            t.taps[k] = r;
+                            taps[k] = r;
                         }
                     const uint64_t n_read = t.next_sample;
                     const int32_t state0 = t.state;
-                    // pull-in transitory check at the top of general_work (:1794-1803)
+                    // pull-in transitory check at the top of general_work (:1794-1803):
+                    // pull_in_time_s < (nitems_read - stamp) / (int)fs_in, integer division
                     if (t.pull_in_transitory &&
-                        (uint64_t)t.pull_in_time_s < (n_read - t.acq_sample_stamp) / (uint64_t)(int)t.fs_in)
+                        (n_read < c.acq_sample_stamp || n_read - c.acq_sample_stamp >= c.pull_in_span))
                         {
                             t.pull_in_transitory = 0;
                             t.carrier_lock_fail_counter = 0;
                             t.code_lock_fail_counter = 0;
                         }
                     EpochOut o;
-                    const uint64_t tmD = timing ? clock64() : 0;
-                    after_correlation(t, s_lf, s_pbuf, n_read, o, timing ? timing + ((size_t)ch * max_epochs + e) * 12 + 8 : nullptr);
-                    const uint64_t tmE = timing ? clock64() : 0;
-                    gsdr_trk_epoch r;
-                    r.sample_counter = n_read;
-                    r.state = state0;
-                    r.consumed = t.current_prn_length_samples;
+                    after_correlation(c, t, s_lf, s_pbuf, taps, n_read, lane, o);
+                    if (lane == 0)
+                        {
+                            gsdr_trk_epoch r;
+                            r.sample_counter = n_read;
+                            r.state = state0;
+                            r.consumed = t.current_prn_length_samples;
 #pragma unroll
-                    for (int k = 0; k < 5; ++k)
-                        {
-                            r.taps[2 * k] = t.taps[k].x;
-                            r.taps[2 * k + 1] = t.taps[k].y;
+                            for (int k = 0; k < 5; ++k)
+                                {
+                                    r.taps[2 * k] = taps[k].x;
+                                    r.taps[2 * k + 1] = taps[k].y;
+                                }
+                            r.rem_carr_phase_rad = t.rem_carr_phase_rad;
+                            r.flags = o.flags;
+                            r.carrier_doppler_hz = t.carrier_doppler_hz;
+                            r.code_freq_chips = t.code_freq_chips;
+                            r.rem_code_phase_samples = t.rem_code_phase_samples;
+                            r.acc_carrier_phase_rad = t.acc_carrier_phase_rad;
+                            r.cn0_db_hz = t.cn0_db_hz;
+                            r.carrier_lock_test = t.carrier_lock_test;
+                            r.prompt_i = o.prompt_i;
+                            r.prompt_q = o.prompt_q;
+                            r.evm = t.evm;
+                            out[(size_t)ch * max_epochs + e] = r;
+                            if (timing)
+                                {
+                                    uint64_t* tr = timing + ((size_t)ch * max_epochs + e) * 4;
+                                    tr[0] = tm0;
+                                    tr[1] = tm1;
+                                    tr[2] = tm2;
+                                    tr[3] = clock64();
+                                }
                         }
-                    r.rem_carr_phase_rad = t.rem_carr_phase_rad;
-                    r.flags = o.flags;
-                    r.carrier_doppler_hz = t.carrier_doppler_hz;
-                    r.code_freq_chips = t.code_freq_chips;
-                    r.rem_code_phase_samples = t.rem_code_phase_samples;
-                    r.acc_carrier_phase_rad = t.acc_carrier_phase_rad;
-                    r.cn0_db_hz = t.cn0_db_hz;
-                    r.carrier_lock_test = t.carrier_lock_test;
-                    r.prompt_i = o.prompt_i;
-                    r.prompt_q = o.prompt_q;
-                    r.evm = t.evm;
-                    out[(size_t)ch * max_epochs + e] = r;
                     t.next_sample = n_read + (uint64_t)(int64_t)t.current_prn_length_samples;
-                    s_hot = t;
-                    if (timing)
-                        {
-                            uint64_t* tr = timing + ((size_t)ch * max_epochs + e) * 12;
-                            tr[0] = tm0;
-                            tr[1] = tm1;
-                            tr[2] = tmA;
-                            tr[3] = tmB;
-                            tr[4] = tmC;
-                            tr[5] = tm2;
-                            tr[6] = tmD;
-                            tr[7] = tmE;
-                            tr[11] = clock64();
-                        }
                 }
             if (use_window)
                 {
@@ -933,7 +883,7 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(TrkChan* __restrict__ 
     __syncthreads();
     if (tid == 0)
         {
-            gc->h = s_hot;
+            gc->h = t;
             gc->code_filter = s_lf;
             nout[ch] = e;
         }
@@ -964,7 +914,9 @@ struct gsdr_trk
     int device{0};
     gsdr_trk_conf conf{};
     hipStream_t stream{nullptr};
+    std::vector<TrkConst> h_consts;
     std::vector<TrkChan> h_chans;
+    TrkConst* d_consts{nullptr};
     TrkChan* d_chans{nullptr};
     TrkChan* d_snap[2]{nullptr, nullptr};
     std::vector<float*> code_bufs;
@@ -994,61 +946,89 @@ namespace
 size_t trk_item_bytes(int it) { return it == GSDR_ITEM_CSHORT ? 4 : 8; }
 
 // constructor (dll_pll_veml_tracking.cc:85-560) for one channel slot, GPS L1 C/A
-void init_channel(const gsdr_trk_conf& c, TrkChan& ch)
+// Tracking_FLL_PLL_filter::set_params (tracking_FLL_PLL_filter.cc:23-58)
+void cf_set_params(CfConst& p, float fll_bw, float pll_bw, int order)
 {
+    p = CfConst{};
+    p.order = order;
+    if (order == 3)
+        {
+            p.b3 = 2.400F;
+            p.a3 = 1.100F;
+            p.a2 = 1.414F;
+            p.w0p = pll_bw / 0.7845F;
+            p.w0p2 = p.w0p * p.w0p;
+            p.w0p3 = p.w0p2 * p.w0p;
+            p.w0f = fll_bw / 0.53F;
+            p.w0f2 = p.w0f * p.w0f;
+        }
+    else
+        {
+            p.a2 = 1.414F;
+            p.w0p = pll_bw / 0.53F;
+            p.w0p2 = p.w0p * p.w0p;
+            p.w0f = fll_bw / 0.25F;
+        }
+}
+
+// Exponential_Smoother::set_alpha (exponential_smoother.cc:29-41)
+void sm_set(SmConst& k, float alpha, float min_value, float offset, int samples)
+{
+    k.alpha = alpha;
+    if (k.alpha < 0) k.alpha = 0;
+    if (k.alpha > 1) k.alpha = 1;
+    k.one_minus_alpha = 1.0F - k.alpha;
+    k.min_value = min_value;
+    k.offset = offset;
+    k.samples_init = std::max(1, samples);
+}
+
+// constructor (dll_pll_veml_tracking.cc:85-560) for one channel slot, GPS L1 C/A
+void init_channel(const gsdr_trk_conf& cf, TrkConst& c, TrkChan& ch)
+{
+    std::memset(&c, 0, sizeof(c));
     std::memset(&ch, 0, sizeof(ch));
+    c.fs_in = cf.fs_in;
+    c.code_period = kGpsCaPeriod;
+    c.code_chip_rate = kGpsCaRate;
+    c.signal_carrier_freq = kGpsL1Hz;
+    c.carrier_lock_threshold = cf.carrier_lock_th;
+    c.current_correlation_time_s = c.code_period;
+    c.early_late_space_chips = cf.early_late_space_chips;
+    c.vector_length = (int32_t)cf.vector_length;
+    c.code_length_chips = kGpsCaLength;
+    c.code_samples_per_chip = 1;
+    c.symbols_per_bit = kGpsCaSymbolsPerBit;
+    c.cn0_samples = cf.cn0_samples;
+    c.cn0_min = cf.cn0_min;
+    c.max_code_lock_fail = cf.max_code_lock_fail;
+    c.max_carrier_lock_fail = cf.max_carrier_lock_fail;
+    const uint64_t fsi = (uint64_t)(int64_t)(int)cf.fs_in;
+    c.pull_in_span = ((uint64_t)cf.pull_in_time_s + 1) * fsi;
+    c.bit_sync_span = ((uint64_t)cf.bit_synchronization_time_limit_s + 1) * fsi;
+    c.extend_correlation_symbols = cf.extend_correlation_symbols;
+    c.enable_fll_pull_in = cf.enable_fll_pull_in;
+    c.enable_fll_steady_state = cf.enable_fll_steady_state;
+    c.carrier_aiding = cf.carrier_aiding;
+    c.n_taps = 3;
+    c.shifts[0] = -cf.early_late_space_chips * (float)c.code_samples_per_chip;
+    c.shifts[1] = 0.0F;
+    c.shifts[2] = cf.early_late_space_chips * (float)c.code_samples_per_chip;
+    preamble_register(c.preamble);
+    cf_set_params(c.cf, cf.fll_bw_hz, cf.pll_bw_hz, cf.pll_filter_order);
+    // Exponential_Smoother defaults (exponential_smoother.h:58-63) + dll_pll_veml_tracking.cc:540-552
+    sm_set(c.sm[0], cf.cn0_smoother_alpha, 25.0F, 12.0F, cf.cn0_smoother_samples / (int)(c.code_period * 1000.0));
+    sm_set(c.sm[1], cf.carrier_lock_test_smoother_alpha, -1.0F, 0.0F, cf.carrier_lock_test_smoother_samples);
     TrkHot& t = ch.h;
-    t.fs_in = c.fs_in;
-    t.code_period = kGpsCaPeriod;
-    t.code_chip_rate = kGpsCaRate;
-    t.signal_carrier_freq = kGpsL1Hz;
-    t.carrier_lock_threshold = c.carrier_lock_th;
-    t.early_late_space_chips = c.early_late_space_chips;
-    t.vector_length = (int32_t)c.vector_length;
-    t.code_length_chips = kGpsCaLength;
-    t.code_samples_per_chip = 1;
-    t.symbols_per_bit = kGpsCaSymbolsPerBit;
-    t.cn0_samples = c.cn0_samples;
-    t.cn0_min = c.cn0_min;
-    t.max_code_lock_fail = c.max_code_lock_fail;
-    t.max_carrier_lock_fail = c.max_carrier_lock_fail;
-    t.pull_in_time_s = c.pull_in_time_s;
-    t.bit_sync_limit_s = c.bit_synchronization_time_limit_s;
-    t.extend_correlation_symbols = c.extend_correlation_symbols;
-    t.enable_fll_pull_in = c.enable_fll_pull_in;
-    t.enable_fll_steady_state = c.enable_fll_steady_state;
-    t.carrier_aiding = c.carrier_aiding;
-    t.n_taps = 3;
-    t.shifts[0] = -c.early_late_space_chips * (float)t.code_samples_per_chip;
-    t.shifts[1] = 0.0F;
-    t.shifts[2] = c.early_late_space_chips * (float)t.code_samples_per_chip;
-    preamble_register(t.preamble);
-    t.spc = c.early_late_space_chips;
-    t.code_freq_chips = t.code_chip_rate;
-    ch.code_filter.T = (float)t.code_period;
-    ch.code_filter.bw = c.dll_bw_hz;
-    ch.code_filter.order = c.dll_filter_order;
-    lf_update(ch.code_filter);
-    cf_set_params(t.carrier_filter, c.fll_bw_hz, c.pll_bw_hz, c.pll_filter_order);
-    // Exponential_Smoother defaults + dll_pll_veml_tracking.cc:540-552
-    t.cn0_sm.alpha = c.cn0_smoother_alpha;
-    if (t.cn0_sm.alpha < 0) t.cn0_sm.alpha = 0;
-    if (t.cn0_sm.alpha > 1) t.cn0_sm.alpha = 1;
-    t.cn0_sm.one_minus_alpha = 1.0F - t.cn0_sm.alpha;
-    t.cn0_sm.min_value = 25.0F;
-    t.cn0_sm.offset = 12.0F;
-    t.cn0_sm.samples_init = std::max(1, c.cn0_smoother_samples / (int)(t.code_period * 1000.0));
-    sm_reset(t.cn0_sm);
-    t.lock_sm.alpha = c.carrier_lock_test_smoother_alpha;
-    if (t.lock_sm.alpha < 0) t.lock_sm.alpha = 0;
-    if (t.lock_sm.alpha > 1) t.lock_sm.alpha = 1;
-    t.lock_sm.one_minus_alpha = 1.0F - t.lock_sm.alpha;
-    t.lock_sm.min_value = -1.0F;
-    t.lock_sm.offset = 0.0F;
-    t.lock_sm.samples_init = std::max(1, c.carrier_lock_test_smoother_samples);
-    sm_reset(t.lock_sm);
+    t.spc = cf.early_late_space_chips;
+    t.code_freq_chips = c.code_chip_rate;
+    sm_reset(t, 0);
+    sm_reset(t, 1);
     t.state = 0;
-    t.assoc = GSDR_ASSOC_AVX;
+    ch.code_filter.T = (float)c.code_period;
+    ch.code_filter.bw = cf.dll_bw_hz;
+    ch.code_filter.order = cf.dll_filter_order;
+    lf_update(ch.code_filter);
 }
 
 int ensure_out(gsdr_trk* k, uint32_t max_epochs)
@@ -1071,7 +1051,7 @@ int launch(gsdr_trk* k, const void* iq, uint64_t iq_first, uint64_t iq_items, ui
     uint64_t* timing = nullptr;
     if (k->timing_on)
         {
-            const size_t need = (size_t)k->conf.max_channels * max_epochs * 12;
+            const size_t need = (size_t)k->conf.max_channels * max_epochs * 4;
             if (need > k->timing_cap)
                 {
                     if (k->d_timing) GSDR_HIP(hipFree(k->d_timing));
@@ -1099,10 +1079,10 @@ int launch(gsdr_trk* k, const void* iq, uint64_t iq_first, uint64_t iq_items, ui
         }
     const dim3 grid(k->conf.max_channels);
     if (k->conf.item_type == GSDR_ITEM_GR_COMPLEX)
-        hipLaunchKernelGGL((trk_kernel<GSDR_ITEM_GR_COMPLEX>), grid, dim3(kTrkThreads), k->lds_bytes, s, k->d_chans,
+        hipLaunchKernelGGL((trk_kernel<GSDR_ITEM_GR_COMPLEX>), grid, dim3(kTrkThreads), k->lds_bytes, s, k->d_consts, k->d_chans,
             (const float* const*)k->d_codes, iq, iq_first, iq_items, max_epochs, out, nout, k->code_pad, timing);
     else
-        hipLaunchKernelGGL((trk_kernel<GSDR_ITEM_CSHORT>), grid, dim3(kTrkThreads), k->lds_bytes, s, k->d_chans,
+        hipLaunchKernelGGL((trk_kernel<GSDR_ITEM_CSHORT>), grid, dim3(kTrkThreads), k->lds_bytes, s, k->d_consts, k->d_chans,
             (const float* const*)k->d_codes, iq, iq_first, iq_items, max_epochs, out, nout, k->code_pad, timing);
     GSDR_HIP(hipGetLastError());
     if (k->profiling)
@@ -1113,7 +1093,7 @@ int launch(gsdr_trk* k, const void* iq, uint64_t iq_first, uint64_t iq_items, ui
     if (timing)
         {
             const uint32_t nch = k->conf.max_channels;
-            std::vector<uint64_t> tm((size_t)nch * max_epochs * 12);
+            std::vector<uint64_t> tm((size_t)nch * max_epochs * 4);
             std::vector<uint32_t> cnt(nch);
             GSDR_HIP(hipMemcpyAsync(tm.data(), timing, tm.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
             GSDR_HIP(hipMemcpyAsync(cnt.data(), nout, nch * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
@@ -1121,10 +1101,9 @@ int launch(gsdr_trk* k, const void* iq, uint64_t iq_first, uint64_t iq_items, ui
             for (uint32_t c = 0; c < nch; ++c)
                 for (uint32_t e = 0; e < cnt[c]; ++e)
                     {
-                        const uint64_t* r = &tm[((size_t)c * max_epochs + e) * 12];
-                        const int seq[] = {0, 1, 2, 3, 4, 5, 6, 8, 9, 10, 7, 11};
-                        for (int q = 0; q + 1 < 12; ++q)
-                            if (r[seq[q + 1]] >= r[seq[q]]) k->tsum[q] += (double)(r[seq[q + 1]] - r[seq[q]]);
+                        const uint64_t* r = &tm[((size_t)c * max_epochs + e) * 4];
+                        for (int q = 0; q < 3; ++q)
+                            if (r[q + 1] >= r[q]) k->tsum[q] += (double)(r[q + 1] - r[q]);
                         k->tcount++;
                     }
         }
@@ -1199,13 +1178,15 @@ int gsdr_trk_create(int device, const gsdr_trk_conf* conf, gsdr_trk** out)
     if (k->conf.vector_length == 0)
         k->conf.vector_length = (uint32_t)std::lround(conf->fs_in / (kGpsCaRate / kGpsCaLength));
     const uint32_t nch = k->conf.max_channels;
+    k->h_consts.resize(nch);
     k->h_chans.resize(nch);
-    for (auto& t : k->h_chans) init_channel(k->conf, t);
+    for (uint32_t c = 0; c < nch; ++c) init_channel(k->conf, k->h_consts[c], k->h_chans[c]);
     k->code_bufs.assign(nch, nullptr);
     k->code_pad = 1024;  // grows with the longest replica started (gsdr_trk_start)
     k->lds_bytes = lds_for(k->code_pad);
     if (const char* tv = std::getenv("GSDR_TRK_TIMING")) k->timing_on = std::atoi(tv) != 0;
     hipError_t e = hipStreamCreateWithFlags(&k->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMalloc(&k->d_consts, nch * sizeof(TrkConst));
     if (e == hipSuccess) e = hipMalloc(&k->d_chans, nch * sizeof(TrkChan));
     if (e == hipSuccess) e = hipMalloc(&k->d_snap[0], nch * sizeof(TrkChan));
     if (e == hipSuccess) e = hipMalloc(&k->d_snap[1], nch * sizeof(TrkChan));
@@ -1213,6 +1194,7 @@ int gsdr_trk_create(int device, const gsdr_trk_conf* conf, gsdr_trk** out)
     if (e == hipSuccess) e = hipMalloc(&k->d_nout, nch * sizeof(uint32_t));
     for (uint32_t c = 0; c < nch && e == hipSuccess; ++c) e = hipMalloc(&k->code_bufs[c], kMaxCodeFloats * sizeof(float));
     if (e == hipSuccess) e = hipMemcpy(k->d_codes, k->code_bufs.data(), nch * sizeof(float*), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(k->d_consts, k->h_consts.data(), nch * sizeof(TrkConst), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(k->d_chans, k->h_chans.data(), nch * sizeof(TrkChan), hipMemcpyHostToDevice);
     if (e == hipSuccess)
         e = hipFuncSetAttribute((const void*)trk_kernel<GSDR_ITEM_GR_COMPLEX>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1237,10 +1219,9 @@ void gsdr_trk_destroy(gsdr_trk* k)
     if (k->stream) (void)hipStreamSynchronize(k->stream);
     if (k->timing_on && k->tcount)
         {
-            static const char* names[] = {"prep", "barrier", "anchor", "samples", "reduce+barrier", "to-update",
-                "cn0+lock", "dll/pll", "nco", "rest", "record"};
+            static const char* names[] = {"prep", "correlate", "update"};
             std::fprintf(stderr, "gsdr_trk timing: %llu calls, clock64 ticks per call:", (unsigned long long)k->tcount);
-            for (int q = 0; q < 11; ++q) std::fprintf(stderr, " %s %.0f", names[q], k->tsum[q] / k->tcount);
+            for (int q = 0; q < 3; ++q) std::fprintf(stderr, " %s %.0f", names[q], k->tsum[q] / k->tcount);
             std::fprintf(stderr, "\n");
         }
     if (k->d_timing) (void)hipFree(k->d_timing);
@@ -1252,7 +1233,7 @@ void gsdr_trk_destroy(gsdr_trk* k)
     for (hipEvent_t e : k->prof_pool) (void)hipEventDestroy(e);
     for (float* p : k->code_bufs)
         if (p) (void)hipFree(p);
-    void* bufs[] = {k->d_chans, k->d_snap[0], k->d_snap[1], k->d_codes, k->d_nout, k->d_out, k->d_iq};
+    void* bufs[] = {k->d_consts, k->d_chans, k->d_snap[0], k->d_snap[1], k->d_codes, k->d_nout, k->d_out, k->d_iq};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     if (k->stream) (void)hipStreamDestroy(k->stream);
@@ -1272,18 +1253,17 @@ int gsdr_trk_start(gsdr_trk* k, int ch, uint32_t prn, const float* code, int cod
     // the device copy is authoritative between launches (the loop runs there)
     GSDR_HIP(hipMemcpyAsync(&k->h_chans[ch], k->d_chans + ch, sizeof(TrkChan), hipMemcpyDeviceToHost, k->stream));
     GSDR_HIP(hipStreamSynchronize(k->stream));
+    TrkConst& c = k->h_consts[ch];
     TrkChan& tc = k->h_chans[ch];
     TrkHot& t = tc.h;
     // start_tracking (:640-882)
-    t.prn = prn;
-    t.code_samples = code_samples;
-    t.acq_code_phase_samples = acq_delay_samples;
-    t.acq_carrier_doppler_hz = acq_doppler_hz;
-    t.acq_sample_stamp = acq_samplestamp;
-    t.carrier_doppler_hz = t.acq_carrier_doppler_hz;
-    t.carrier_phase_step_rad = kTwoPi * t.carrier_doppler_hz / t.fs_in;
+    c.prn = prn;
+    c.code_samples = code_samples;
+    c.acq_sample_stamp = acq_samplestamp;
+    double acq_code_phase_samples = acq_delay_samples;
+    t.carrier_doppler_hz = acq_doppler_hz;
+    t.carrier_phase_step_rad = kTwoPi * t.carrier_doppler_hz / c.fs_in;
     t.carrier_phase_rate_step_rad = 0.0;
-    for (int i = 0; i < kMaxTrkTaps; ++i) t.taps[i] = make_float2(0.f, 0.f);
     t.carrier_lock_fail_counter = 0;
     t.code_lock_fail_counter = 0;
     t.rem_code_phase_samples = 0.0;
@@ -1294,15 +1274,26 @@ int gsdr_trk_start(gsdr_trk* k, int ch, uint32_t prn, const float* code, int cod
     t.carrier_lock_test = 1.0;
     t.cn0_db_hz = 0.0;
     t.evm = 0.0;
-    t.shifts[0] = -k->conf.early_late_space_chips * (float)t.code_samples_per_chip;
-    t.shifts[2] = k->conf.early_late_space_chips * (float)t.code_samples_per_chip;
-    t.current_correlation_time_s = t.code_period;
-    cf_set_params(t.carrier_filter, k->conf.fll_bw_hz, k->conf.pll_bw_hz, k->conf.pll_filter_order);
+    c.shifts[0] = -k->conf.early_late_space_chips * (float)c.code_samples_per_chip;
+    c.shifts[2] = k->conf.early_late_space_chips * (float)c.code_samples_per_chip;
+    c.current_correlation_time_s = c.code_period;
+    cf_set_params(c.cf, k->conf.fll_bw_hz, k->conf.pll_bw_hz, k->conf.pll_filter_order);
     tc.code_filter.bw = k->conf.dll_bw_hz;
     lf_update(tc.code_filter);
-    tc.code_filter.T = (float)t.code_period;
+    tc.code_filter.T = (float)c.code_period;
     lf_update(tc.code_filter);
-    cf_initialize(t.carrier_filter, (float)t.acq_carrier_doppler_hz);
+    // Tracking_FLL_PLL_filter::initialize (tracking_FLL_PLL_filter.cc:61-74)
+    const float dop0 = (float)acq_doppler_hz;
+    if (c.cf.order == 3)
+        {
+            t.cf_x = 2.0F * dop0;
+            t.cf_w = 0;
+        }
+    else
+        {
+            t.cf_w = dop0;
+            t.cf_x = 0;
+        }
     lf_initialize(tc.code_filter, 0.0F);
     t.cloop = 1;
     t.pull_in_transitory = 1;
@@ -1310,27 +1301,28 @@ int gsdr_trk_start(gsdr_trk* k, int ch, uint32_t prn, const float* code, int cod
     for (int w = 0; w < 5; ++w) t.circ[w] = 0u;
     t.acc_carrier_phase_initialized = 0;
     // state 1: pull-in alignment (:1813-1844)
-    const int64_t diff = (int64_t)nitems_read - (int64_t)t.acq_sample_stamp;
-    const double delta = (double)diff - t.acq_code_phase_samples;
-    t.code_freq_chips = t.code_chip_rate;
-    t.code_phase_step_chips = t.code_freq_chips / t.fs_in;
+    const int64_t diff = (int64_t)nitems_read - (int64_t)c.acq_sample_stamp;
+    const double delta = (double)diff - acq_code_phase_samples;
+    t.code_freq_chips = c.code_chip_rate;
+    t.code_phase_step_chips = t.code_freq_chips / c.fs_in;
     t.code_phase_rate_step_chips = 0.0;
     const double T_chip_mod = 1.0 / t.code_freq_chips;
-    const double T_prn_mod = T_chip_mod * (double)t.code_length_chips;
-    const double T_prn_mod_samples = T_prn_mod * t.fs_in;
-    t.acq_code_phase_samples = T_prn_mod_samples - std::fmod(delta, T_prn_mod_samples);
+    const double T_prn_mod = T_chip_mod * (double)c.code_length_chips;
+    const double T_prn_mod_samples = T_prn_mod * c.fs_in;
+    acq_code_phase_samples = T_prn_mod_samples - std::fmod(delta, T_prn_mod_samples);
     t.current_prn_length_samples = (int32_t)std::round(T_prn_mod_samples);
-    const int32_t offset = (int32_t)std::round(t.acq_code_phase_samples);
+    const int32_t offset = (int32_t)std::round(acq_code_phase_samples);
     t.acc_carrier_phase_rad -= t.carrier_phase_step_rad * (double)offset;
     t.state = 2;
-    sm_reset(t.cn0_sm);
-    sm_reset(t.lock_sm);
+    sm_reset(t, 0);
+    sm_reset(t, 1);
     t.next_sample = nitems_read + (uint64_t)(int64_t)offset;
     *first_sample = t.next_sample;
     k->code_pad = std::max(k->code_pad, (code_samples + 1) & ~1);
     k->lds_bytes = lds_for(k->code_pad);
     GSDR_HIP(hipMemcpyAsync(k->code_bufs[ch], code, (size_t)code_samples * sizeof(float), hipMemcpyHostToDevice,
         k->stream));
+    GSDR_HIP(hipMemcpyAsync(k->d_consts + ch, &c, sizeof(TrkConst), hipMemcpyHostToDevice, k->stream));
     GSDR_HIP(hipMemcpyAsync(k->d_chans + ch, &tc, sizeof(TrkChan), hipMemcpyHostToDevice, k->stream));
     GSDR_HIP(hipStreamSynchronize(k->stream));
     return GSDR_OK;

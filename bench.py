@@ -155,6 +155,8 @@ def main():
     ap.add_argument("--blocks", type=int, default=64, help="1 ms blocks per step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile-events", action="store_true")
+    ap.add_argument("--cu-partition", action="store_true",
+                    help="give the tracking stream CHANNELS CUs of its own and acquisition the rest")
     args = ap.parse_args()
 
     import torch
@@ -186,9 +188,14 @@ def main():
     for c, s in enumerate(sats):
         delay, dop = acq_result_for(s)
         trk.start(c, s.prn, synth.gps_ca_chips(s.prn), delay, dop, 0, 0)
-    # each handle launches on its own HIP stream (created with the handle, so each
-    # gets its own hardware queue); the tracking launch goes first so its few
-    # long-lived workgroups are resident before the acquisition grid fills the chip
+    # each handle launches on its own HIP stream (its own hardware queue).  The
+    # tracking pool is a latency chain of one workgroup per channel that needs a
+    # whole CU; give it CHANNELS CUs (one per XCD for 8) and the acquisition grid
+    # the other 248, so neither waits for the other's workgroups to drain.
+    if args.cu_partition:
+        trk_mask, acq_mask = gsdr.cu_partition(CHANNELS)
+        trk.set_cu_mask(trk_mask)
+        acq.set_cu_mask(acq_mask)
     trk.save_state(0)
 
     def step():
@@ -259,6 +266,7 @@ def main():
                         "over the same span",
             "blocks_per_step": B, "fs_sps": FS, "fft_size": N, "prns": P, "doppler_bins": D, "channels": CHANNELS,
             "taps": TAPS, "item_type": "gr_complex", "parallelism": "blocks sharded per rank (dp%d)" % world,
+            "cu_partition": {"tracking": CHANNELS, "acquisition": 256 - CHANNELS} if args.cu_partition else None,
         },
         "real_time_factor": round(value * 1e6 / FS, 2),
     }
@@ -290,6 +298,8 @@ def main():
         line["cpu_baseline"] = cpu_baseline(iq, codes, sats)
     if rank == 0:
         print(json.dumps(line), flush=True)
+    trk.close()
+    acq.close()
     if dist is not None:
         dist.destroy_process_group()
 

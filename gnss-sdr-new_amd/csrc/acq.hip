@@ -36,7 +36,7 @@ namespace
 using gsdr::fft::Plan;
 
 // Default correlate variant at N = 4000 (see GSDR_CORR_VARIANTS).
-constexpr int kDefaultCorrVariant4000 = 30;
+constexpr int kDefaultCorrVariant4000 = 35;
 
 struct RowStat
 {
@@ -721,13 +721,14 @@ using gsdr::fft::MultiPlan;
 // Packed-f32 variants: (id, plan, PRNs per workgroup).
 #define GSDR_PK_VARIANTS(X)                                              \
     X(30, (gsdr::pk::PkPlan<256, true, 25, 16, 10>), 1, 1)              \
-    X(31, (gsdr::pk::PkPlan<256, true, 25, 16, 10>), 1, 5)              \
-    X(32, (gsdr::pk::PkPlan<256, true, 25, 16, 10>), 2, 5)              \
-    X(33, (gsdr::pk::PkPlan<256, true, 20, 20, 10>), 1, 5)              \
-    X(34, (gsdr::pk::PkPlan<256, false, 25, 16, 10>), 1, 5)             \
+    X(31, (gsdr::pk::PkPlan<512, true, 25, 16, 10>), 1, 1)              \
+    X(32, (gsdr::pk::PkPlan<512, true, 20, 20, 10>), 1, 1)              \
+    X(33, (gsdr::pk::PkPlan<448, true, 25, 16, 10>), 1, 1)              \
+    X(34, (gsdr::pk::PkPlan<512, true, 10, 20, 20>), 1, 1)              \
     X(35, (gsdr::pk::PkPlan<256, true, 20, 20, 10>), 1, 1)              \
-    X(36, (gsdr::pk::PkPlan<256, true, 25, 16, 10>), 4, 4)              \
-    X(37, (gsdr::pk::PkPlan<256, true, 20, 20, 10>), 2, 5)
+    X(36, (gsdr::pk::PkPlan<512, true, 16, 25, 10>), 1, 1)              \
+    X(37, (gsdr::pk::PkPlan<512, true, 25, 16, 10>), 2, 1)              \
+    X(38, (gsdr::pk::PkPlan<384, true, 25, 16, 10>), 1, 1)
 
 template <class PT>
 int set_lds_attrs(size_t bytes)
@@ -1293,6 +1294,14 @@ int gsdr_acq_dump_grid(gsdr_acq* a, const void* iq_host, uint32_t prn_slot, floa
         a->stream));
     GSDR_HIP(hipStreamSynchronize(a->stream));
     return GSDR_OK;
+}
+
+int gsdr_acq_set_cu_mask(gsdr_acq* a, const uint32_t* mask, int n_words)
+{
+    GSDR_REQUIRE(a, GSDR_E_ARG, "gsdr_acq_set_cu_mask: null handle");
+    std::lock_guard<std::mutex> lk(a->mu);
+    gsdr::DeviceGuard g(a->device);
+    return gsdr::replace_stream(&a->stream, mask, n_words);
 }
 
 int gsdr_acq_set_profiling(gsdr_acq* a, int enable)

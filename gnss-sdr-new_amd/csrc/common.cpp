@@ -1,4 +1,5 @@
 // Error reporting, device queries and the threshold's special function.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -66,6 +67,30 @@ double gamma_p_inv_int(int a, double p)
             x = xn;
         }
     return (double)x;
+}
+
+int replace_stream(hipStream_t* stream, const uint32_t* mask, int n_words)
+{
+    GSDR_REQUIRE(n_words >= 0 && (n_words == 0 || mask), GSDR_E_ARG, "cu mask: bad argument");
+    hipStream_t s = nullptr;
+    if (n_words == 0)
+        {
+            GSDR_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        }
+    else
+        {
+            bool any = false;
+            for (int i = 0; i < n_words; ++i) any |= mask[i] != 0u;
+            GSDR_REQUIRE(any, GSDR_E_ARG, "cu mask: no CU selected");
+            GSDR_HIP(hipExtStreamCreateWithCUMask(&s, (uint32_t)n_words, mask));
+        }
+    if (*stream)
+        {
+            (void)hipStreamSynchronize(*stream);
+            (void)hipStreamDestroy(*stream);
+        }
+    *stream = s;
+    return GSDR_OK;
 }
 
 }  // namespace gsdr

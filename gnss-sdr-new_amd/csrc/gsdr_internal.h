@@ -74,6 +74,10 @@ __device__ __forceinline__ float sub_rn(float a, float b)
     return a - b;
 }
 
+// Replace *stream (if any) with a new non-blocking stream on the current device,
+// restricted to the CUs in mask[0..n_words) (all CUs when n_words == 0).
+int replace_stream(hipStream_t* stream, const uint32_t* mask, int n_words);
+
 // Inverse regularised lower incomplete gamma for integer shape a:
 // returns x with P(a, x) = p.  (Boost gamma_p_inv, used by calculate_threshold.)
 double gamma_p_inv_int(int a, double p);

@@ -932,7 +932,9 @@ struct gsdr_trk
     bool timing_on{false};
     uint64_t* d_timing{nullptr};
     size_t timing_cap{0};
-    double tsum[11]{};
+    double tsum[4]{};
+    uint32_t timing_epochs{0};
+    uint32_t* timing_nout{nullptr};
     uint64_t tcount{0};
     bool profiling{false};
     std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_recs;
@@ -1043,7 +1045,17 @@ int ensure_out(gsdr_trk* k, uint32_t max_epochs)
     return GSDR_OK;
 }
 
-size_t lds_for(int code_pad) { return (size_t)code_pad * sizeof(float) + (size_t)(kWinCore + kHalo) * sizeof(float2); }
+// Dynamic LDS of a launch: the replica and the input window, padded up to a whole
+// CU's LDS so that no workgroup of another kernel (the acquisition grid on the
+// other queue) can share the CU with a tracking workgroup -- the loop is a
+// latency chain and co-resident FFT waves would slow every call down.
+constexpr size_t kCuLds = 160 * 1024;
+constexpr size_t kStaticLdsMargin = 4 * 1024;  // the kernel's static __shared__ arrays
+size_t lds_for(int code_pad)
+{
+    const size_t need = (size_t)code_pad * sizeof(float) + (size_t)(kWinCore + kHalo) * sizeof(float2);
+    return std::max(need, kCuLds - kStaticLdsMargin);
+}
 
 int launch(gsdr_trk* k, const void* iq, uint64_t iq_first, uint64_t iq_items, uint32_t max_epochs, gsdr_trk_epoch* out,
     uint32_t* nout, hipStream_t s)
@@ -1092,20 +1104,8 @@ int launch(gsdr_trk* k, const void* iq, uint64_t iq_first, uint64_t iq_items, ui
         }
     if (timing)
         {
-            const uint32_t nch = k->conf.max_channels;
-            std::vector<uint64_t> tm((size_t)nch * max_epochs * 4);
-            std::vector<uint32_t> cnt(nch);
-            GSDR_HIP(hipMemcpyAsync(tm.data(), timing, tm.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-            GSDR_HIP(hipMemcpyAsync(cnt.data(), nout, nch * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-            GSDR_HIP(hipStreamSynchronize(s));
-            for (uint32_t c = 0; c < nch; ++c)
-                for (uint32_t e = 0; e < cnt[c]; ++e)
-                    {
-                        const uint64_t* r = &tm[((size_t)c * max_epochs + e) * 4];
-                        for (int q = 0; q < 3; ++q)
-                            if (r[q + 1] >= r[q]) k->tsum[q] += (double)(r[q + 1] - r[q]);
-                        k->tcount++;
-                    }
+            k->timing_epochs = max_epochs;  // summarised (last launch) on destroy, no sync here
+            k->timing_nout = nout;
         }
     return GSDR_OK;
 }
@@ -1217,11 +1217,32 @@ void gsdr_trk_destroy(gsdr_trk* k)
     if (!k) return;
     gsdr::DeviceGuard g(k->device);
     if (k->stream) (void)hipStreamSynchronize(k->stream);
+    if (k->timing_on && k->d_timing && k->timing_epochs)
+        {
+            const uint32_t nch = k->conf.max_channels, me = k->timing_epochs;
+            std::vector<uint64_t> tm((size_t)nch * me * 4);
+            std::vector<uint32_t> cnt(nch);
+            if (hipMemcpy(tm.data(), k->d_timing, tm.size() * sizeof(uint64_t), hipMemcpyDeviceToHost) == hipSuccess &&
+                hipMemcpy(cnt.data(), k->timing_nout, nch * sizeof(uint32_t), hipMemcpyDeviceToHost) == hipSuccess)
+                for (uint32_t c = 0; c < nch; ++c)
+                    for (uint32_t e = 0; e < cnt[c] && e < me; ++e)
+                        {
+                            const uint64_t* r = &tm[((size_t)c * me + e) * 4];
+                            for (int q = 0; q < 3; ++q)
+                                if (r[q + 1] >= r[q]) k->tsum[q] += (double)(r[q + 1] - r[q]);
+                            if (e + 1 < cnt[c] && e + 1 < me)
+                                {
+                                    const uint64_t next0 = tm[((size_t)c * me + e + 1) * 4];
+                                    if (next0 >= r[3]) k->tsum[3] += (double)(next0 - r[3]);
+                                }
+                            k->tcount++;
+                        }
+        }
     if (k->timing_on && k->tcount)
         {
-            static const char* names[] = {"prep", "correlate", "update"};
+            static const char* names[] = {"prep", "correlate", "update", "window-write"};
             std::fprintf(stderr, "gsdr_trk timing: %llu calls, clock64 ticks per call:", (unsigned long long)k->tcount);
-            for (int q = 0; q < 3; ++q) std::fprintf(stderr, " %s %.0f", names[q], k->tsum[q] / k->tcount);
+            for (int q = 0; q < 4; ++q) std::fprintf(stderr, " %s %.0f", names[q], k->tsum[q] / k->tcount);
             std::fprintf(stderr, "\n");
         }
     if (k->d_timing) (void)hipFree(k->d_timing);
@@ -1412,6 +1433,14 @@ int gsdr_trk_restore_state(gsdr_trk* k, int slot, void* stream)
     hipStream_t s = stream ? (hipStream_t)stream : k->stream;
     GSDR_HIP(hipMemcpyAsync(k->d_chans, k->d_snap[slot], k->conf.max_channels * sizeof(TrkChan), hipMemcpyDeviceToDevice, s));
     return GSDR_OK;
+}
+
+int gsdr_trk_set_cu_mask(gsdr_trk* k, const uint32_t* mask, int n_words)
+{
+    GSDR_REQUIRE(k, GSDR_E_ARG, "gsdr_trk_set_cu_mask: null handle");
+    std::lock_guard<std::mutex> lk(k->mu);
+    gsdr::DeviceGuard g(k->device);
+    return gsdr::replace_stream(&k->stream, mask, n_words);
 }
 
 int gsdr_trk_set_profiling(gsdr_trk* k, int enable)

@@ -36,7 +36,7 @@ EXPORTED = [
     "gsdr_corr_dump_indices", "gsdr_corr_run_epochs", "gsdr_corr_set_profiling", "gsdr_corr_read_profile",
     "gsdr_trk_conf_default", "gsdr_trk_create", "gsdr_trk_destroy", "gsdr_trk_start", "gsdr_trk_stop",
     "gsdr_trk_run_device", "gsdr_trk_run", "gsdr_trk_get_channel", "gsdr_trk_save_state", "gsdr_trk_restore_state",
-    "gsdr_trk_set_profiling", "gsdr_trk_read_profile",
+    "gsdr_trk_set_profiling", "gsdr_trk_read_profile", "gsdr_acq_set_cu_mask", "gsdr_trk_set_cu_mask",
 ]
 
 SIGNAL_GPS_1C = 0
@@ -197,6 +197,8 @@ def load():
     L.gsdr_trk_restore_state.argtypes = [P, I, P]
     L.gsdr_trk_set_profiling.argtypes = [P, I]
     L.gsdr_trk_read_profile.argtypes = [P, P, P]
+    L.gsdr_acq_set_cu_mask.argtypes = [P, P, I]
+    L.gsdr_trk_set_cu_mask.argtypes = [P, P, I]
     _lib = L
     return L
 
@@ -302,6 +304,10 @@ class Acquisition:
 
     def set_profiling(self, enable):
         _check(load().gsdr_acq_set_profiling(self._h, int(bool(enable))))
+
+    def set_cu_mask(self, mask_words):
+        m = np.ascontiguousarray(mask_words, np.uint32)
+        _check(load().gsdr_acq_set_cu_mask(self._h, _ptr(m) if len(m) else None, len(m)))
 
     def read_profile(self):
         """(stage_ms[4], launches[4]): forward, correlate, reduce, second peak."""
@@ -473,8 +479,24 @@ class Tracking:
     def set_profiling(self, enable):
         _check(load().gsdr_trk_set_profiling(self._h, int(bool(enable))))
 
+    def set_cu_mask(self, mask_words):
+        m = np.ascontiguousarray(mask_words, np.uint32)
+        _check(load().gsdr_trk_set_cu_mask(self._h, _ptr(m) if len(m) else None, len(m)))
+
     def read_profile(self):
         ms = ctypes.c_double()
         n = ctypes.c_uint32()
         _check(load().gsdr_trk_read_profile(self._h, ctypes.byref(ms), ctypes.byref(n)))
         return ms.value, n.value
+
+
+def cu_partition(n_reserved, n_cus=256):
+    """CU masks (hipExtStreamCreateWithCUMask numbering: bit i = CU i//8 of XCD i%8)
+    giving the first n_reserved CUs, spread over the 8 XCDs, to one stream and the
+    rest to another.  Returns (reserved_mask, rest_mask) as uint32 word arrays."""
+    words = (n_cus + 31) // 32
+    res = np.zeros(words, np.uint32)
+    for i in range(n_reserved):
+        res[i // 32] |= np.uint32(1 << (i % 32))
+    full = np.full(words, 0xFFFFFFFF, np.uint32)
+    return res, full & ~res

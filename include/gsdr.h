@@ -361,6 +361,15 @@ int gsdr_trk_restore_state(gsdr_trk* trk, int slot, void* stream);
 
 /* Kernel-time profiling with HIP events (see gsdr_acq_set_profiling). */
 int gsdr_trk_set_profiling(gsdr_trk* trk, int enable);
+
+/* Compute-unit partitioning (MI355X: 256 CUs in 8 XCDs).  Recreates the handle's
+ * own stream (the one used when a call passes stream = NULL) restricted to the CUs
+ * whose bits are set in mask[0..n_words) -- bit i selects CU i/8 of XCD i%8
+ * (hipExtStreamCreateWithCUMask numbering).  A latency-bound tracking pool can so
+ * own a few CUs while the throughput-bound acquisition grid fills the rest.
+ * n_words = 0 restores an unrestricted stream. */
+int gsdr_acq_set_cu_mask(gsdr_acq* acq, const uint32_t* mask, int n_words);
+int gsdr_trk_set_cu_mask(gsdr_trk* trk, const uint32_t* mask, int n_words);
 int gsdr_trk_read_profile(gsdr_trk* trk, double* kernel_ms, uint32_t* launches);
 
 #ifdef __cplusplus

@@ -527,6 +527,81 @@ __global__ void __launch_bounds__(MP::NT) __attribute__((amdgpu_waves_per_eu(WPE
         }
 }
 
+// ---------------------------------------------------------------- K_correlate (packed f32, multi-transform)
+// PB PRNs of one row (b, d) per workgroup, transformed together on the packed
+// multi-transform plan (fft_pk.h PkMultiPlan), whose butterfly packing keeps the
+// waves full; one XCD-aware 1-D grid over (row, PRN group) as above.
+template <class MP, int WPE>
+__global__ void __launch_bounds__(MP::NT) __attribute__((amdgpu_waves_per_eu(WPE))) acq_correlate_pkm_kernel(
+    const float2* __restrict__ X, const float2* __restrict__ code_fft, RowStat* __restrict__ stats,
+    const float2* __restrict__ tw, uint32_t D, uint32_t P, uint32_t nblocks)
+{
+    using gsdr::pk::c2;
+    constexpr int NT = MP::NT;
+    constexpr int NW = NT / 64;
+    constexpr int PB = MP::PB;
+    constexpr uint32_t N = MP::N;
+    extern __shared__ float2 lds_raw[];
+    c2* lds = reinterpret_cast<c2*>(lds_raw);
+    RowStat* scratch = reinterpret_cast<RowStat*>(lds_raw + (size_t)PB * MP::STRIDE);
+    const uint32_t G = (P + PB - 1) / PB;
+    const uint32_t nrows = nblocks * D;
+    const uint32_t id = blockIdx.x;
+    const uint32_t full = nrows >> 3;
+    uint32_t row, g;
+    if (id < full * 8u * G)
+        {
+            const uint32_t xcd = id & 7u, slot = id >> 3;
+            row = (slot / G) * 8u + xcd;
+            g = slot - (slot / G) * G;
+        }
+    else
+        {
+            const uint32_t t = id - full * 8u * G;
+            row = full * 8u + t / G;
+            g = t - (t / G) * G;
+        }
+    const uint32_t b = row / D, d = row - (row / D) * D;
+    const uint32_t p0 = g * PB;
+    const int np = (int)min((uint32_t)PB, P - p0);
+    const c2* x = reinterpret_cast<const c2*>(X) + (size_t)row * N;
+    const c2* cb = reinterpret_cast<const c2*>(code_fft) + (size_t)p0 * N;
+    float best[PB], sum[PB];
+    uint32_t bidx[PB];
+#pragma unroll
+    for (int t = 0; t < PB; ++t)
+        {
+            best[t] = -1.0f;
+            sum[t] = 0.0f;
+            bidx[t] = 0xffffffffu;
+        }
+    // conj(X . conj(C)) = conj(X) . C ; |IFFT(Y)| = |FFT(conj(Y))|.  A partial last
+    // group repeats its last PRN in the idle transforms (results discarded).
+    auto load = [&](int t, int, int i) -> c2 {
+        const int tc = PB == 1 ? 0 : min(t, np - 1);
+        return gsdr::pk::conj_mul(x[i], cb[(size_t)tc * N + i]);
+    };
+    auto store = [&](auto T, int i, c2 v) {
+        constexpr int t = decltype(T)::value;
+        const float m = __builtin_fmaf(v.x, v.x, v.y * v.y);
+        if (m > best[t])
+            {
+                best[t] = m;
+                bidx[t] = (uint32_t)i;
+            }
+        sum[t] += m;
+    };
+    MP::run(lds, tw, load, store);
+#pragma unroll
+    for (int t = 0; t < PB; ++t) block_reduce_stat<NT>(best[t], bidx[t], sum[t], scratch + t * NW);
+    if (threadIdx.x == 0)
+        {
+#pragma unroll
+            for (int t = 0; t < PB; ++t)
+                if (t < np) stats[((size_t)b * P + p0 + t) * D + d] = RowStat{best[t], bidx[t], sum[t], 0};
+        }
+}
+
 // ---------------------------------------------------------------- K_reduce
 // One wave per (b, p).  Rows are scanned in increasing d by each lane and merged
 // with the (max desc, d asc) order, reproducing the reference's strict '>' scan.
@@ -730,6 +805,12 @@ using gsdr::fft::MultiPlan;
     X(37, (gsdr::pk::PkPlan<512, true, 25, 16, 10>), 2, 1)              \
     X(38, (gsdr::pk::PkPlan<384, true, 25, 16, 10>), 1, 1)
 
+// Packed multi-transform variants: (id, plan, waves per EU hint).
+#define GSDR_PKM_VARIANTS(X)                                              \
+    X(43, (gsdr::pk::PkMultiPlan<256, 1, false, 20, 20, 10>), 1)        \
+    X(45, (gsdr::pk::PkMultiPlan<320, 2, true, 25, 16, 10>), 1)         \
+    X(47, (gsdr::pk::PkMultiPlan<256, 1, false, 25, 16, 10>), 1)
+
 template <class PT>
 int set_lds_attrs(size_t bytes)
 {
@@ -852,17 +933,28 @@ int launch_corr_variant(gsdr_acq* a, uint32_t nblocks, hipStream_t s)
                 a->corr_lds_bytes, s, a->d_X, a->d_code_fft, a->d_stats, a->d_tw, a->D, a->nprn, nblocks);      \
             return GSDR_OK;                                                                                     \
         }
+#define GSDR_PKM_CASE(ID, MP, WPE)                                                                              \
+    case ID:                                                                                                    \
+        {                                                                                                       \
+            using M = GSDR_UNPAREN MP;                                                                          \
+            const uint32_t groups = (a->nprn + M::PB - 1) / M::PB;                                              \
+            hipLaunchKernelGGL((acq_correlate_pkm_kernel<M, WPE>), dim3(nblocks * a->D * groups), dim3(M::NT),  \
+                a->corr_lds_bytes, s, a->d_X, a->d_code_fft, a->d_stats, a->d_tw, a->D, a->nprn, nblocks);      \
+            return GSDR_OK;                                                                                     \
+        }
 #define GSDR_UNPAREN(...) __VA_ARGS__
     switch (a->corr_variant)
         {
             GSDR_CORR_VARIANTS(GSDR_CV_CASE)
             GSDR_SEQ_VARIANTS(GSDR_SQ_CASE)
             GSDR_PK_VARIANTS(GSDR_PK_CASE)
+            GSDR_PKM_VARIANTS(GSDR_PKM_CASE)
         default: gsdr::set_error("internal: bad correlate variant %d", a->corr_variant); return GSDR_E_STATE;
         }
 #undef GSDR_CV_CASE
 #undef GSDR_SQ_CASE
 #undef GSDR_PK_CASE
+#undef GSDR_PKM_CASE
 #undef GSDR_UNPAREN
 }
 
@@ -899,17 +991,29 @@ int setup_corr_variant(gsdr_acq* a, int v)
             a->corr_variant = ID;                                                                               \
             return GSDR_OK;                                                                                     \
         }
+#define GSDR_PKM_SETUP(ID, MP, WPE)                                                                             \
+    case ID:                                                                                                    \
+        {                                                                                                       \
+            using M = GSDR_UNPAREN MP;                                                                          \
+            a->corr_lds_bytes = M::lds_bytes() + (size_t)M::PB * (M::NT / 64) * sizeof(RowStat);               \
+            GSDR_HIP(hipFuncSetAttribute((const void*)acq_correlate_pkm_kernel<M, WPE>,                        \
+                hipFuncAttributeMaxDynamicSharedMemorySize, (int)a->corr_lds_bytes));                           \
+            a->corr_variant = ID;                                                                               \
+            return GSDR_OK;                                                                                     \
+        }
 #define GSDR_UNPAREN(...) __VA_ARGS__
     switch (v)
         {
             GSDR_CORR_VARIANTS(GSDR_CV_SETUP)
             GSDR_SEQ_VARIANTS(GSDR_SQ_SETUP)
             GSDR_PK_VARIANTS(GSDR_PK_SETUP)
+            GSDR_PKM_VARIANTS(GSDR_PKM_SETUP)
         default: a->corr_variant = 0; return GSDR_OK;
         }
 #undef GSDR_CV_SETUP
 #undef GSDR_SQ_SETUP
 #undef GSDR_PK_SETUP
+#undef GSDR_PKM_SETUP
 #undef GSDR_UNPAREN
 }
 

@@ -1,8 +1,18 @@
 #!/usr/bin/env python3
-"""Summarise rocprofv3 --pmc counter CSVs (one directory per pass) for one kernel:
-per-dispatch counter values averaged over the dispatches whose name matches."""
+"""Summarise rocprofv3 --pmc counter CSVs (one directory per pass): per-dispatch
+counter values averaged over the dispatches whose kernel name matches.
+
+  pmc_summary.py ROOT [match]      text table for one kernel (default "correlate")
+  pmc_summary.py --json ROOT       JSON for the acquisition kernels, with the HBM
+                                   bytes per launch derived as MI355X_MICROARCH.md
+                                   ("HBM [CDNA4]") prescribes: FETCH_SIZE and
+                                   WRITE_SIZE are KiB; on gfx950 FETCH_SIZE reports
+                                   half the bytes of a wide coalesced read, so
+                                   fetched bytes = 2 * FETCH_SIZE * 1024.
+"""
 import csv
 import glob
+import json
 import os
 import sys
 from collections import defaultdict
@@ -10,7 +20,7 @@ from collections import defaultdict
 
 def summarise(root, match):
     vals = defaultdict(list)
-    for f in sorted(glob.glob(os.path.join(root, "*", "run_counter_collection.csv"))):
+    for f in sorted(glob.glob(os.path.join(root, "*", "**", "*counter_collection.csv"), recursive=True)):
         per = defaultdict(float)
         for r in csv.DictReader(open(f)):
             if match not in r["Kernel_Name"]:
@@ -21,7 +31,35 @@ def summarise(root, match):
     return {c: sum(v) / len(v) for c, v in vals.items()}
 
 
+KERNELS = {"acq_correlate_kernel": "acq_correlate", "acq_forward_kernel": "acq_forward_kernel"}
+
+
+def as_json(root):
+    out = {"source": "rocprofv3 --kernel-trace --pmc, profiles/acq_driver.py --what acq (C2, 64 blocks)",
+           "blocks": 64, "kernels": {}}
+    for name, match in KERNELS.items():
+        s = summarise(root, match)
+        if not s:
+            continue
+        k = {"counters": {c: round(v, 1) for c, v in sorted(s.items())}}
+        if "FETCH_SIZE" in s and "WRITE_SIZE" in s:
+            fetched = 2.0 * s["FETCH_SIZE"] * 1024.0
+            written = s["WRITE_SIZE"] * 1024.0
+            k["hbm_read_bytes_per_launch"] = fetched
+            k["hbm_write_bytes_per_launch"] = written
+            k["hbm_bytes_per_launch"] = fetched + written
+        out["kernels"][name] = k
+    c = out["kernels"].get("acq_correlate_kernel", {})
+    # bench.py reads these two keys for the roofline "traffic" field
+    out["kernel"] = "acq_correlate_kernel"
+    out["hbm_bytes_per_launch"] = c.get("hbm_bytes_per_launch")
+    return out
+
+
 if __name__ == "__main__":
-    root, match = sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "correlate"
-    for c, v in sorted(summarise(root, match).items()):
-        print("%-28s %16.1f" % (c, v))
+    if sys.argv[1] == "--json":
+        print(json.dumps(as_json(sys.argv[2]), indent=1))
+    else:
+        root, match = sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "correlate"
+        for c, v in sorted(summarise(root, match).items()):
+            print("%-28s %16.1f" % (c, v))

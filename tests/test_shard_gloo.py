@@ -1,0 +1,106 @@
+"""Multi-process (world_size 2, gloo, CPU) coverage of the sharded path: block
+and channel partitions tile the work, per-rank acquisition of its block span
+(oracle restatement) merged on the host equals the single-process result, and
+the benchmark's barrier + max-over-ranks timing reduction."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from gsdr import shard, synth
+from oracle import pcps
+
+FS, N, DMAX, DSTEP = 2000000, 2000, 5000, 500
+PRNS = (3, 7, 19)
+BLOCKS = 5
+
+
+def _stream():
+    sats = synth.random_constellation(3, seed_offset=7, cn0_dbhz=55.0, max_doppler=4000.0, prns=PRNS)
+    return synth.gps_l1_iq(FS, BLOCKS * N, sats, seed_offset=7)
+
+
+def _acq_blocks(x, lo, hi):
+    D = int(np.ceil(2 * DMAX / DSTEP))
+    wipe = pcps.doppler_wipeoffs(FS, N, DMAX, DSTEP, D)
+    codes = [pcps.fft_code(synth.gps_ca_sampled(p, FS), N, N) for p in PRNS]
+    out = np.zeros((hi - lo, len(PRNS), 3))
+    for i, b in enumerate(range(lo, hi)):
+        blk = x[b * N:(b + 1) * N]
+        for k, c in enumerate(codes):
+            ti, di, _, _, stat = pcps.max_to_input_power_statistic(pcps.magnitude_grid(blk, wipe, c))
+            out[i, k] = (ti, di, stat)
+    return out
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        x = _stream()
+        lo, hi = shard.block_range(BLOCKS, world, rank)
+        mine = torch.from_numpy(_acq_blocks(x, lo, hi))
+        # host-side result merge (object gather: spans differ in length)
+        gathered = [None] * world
+        dist.all_gather_object(gathered, mine.numpy())
+        chans = shard.channels_of(12, world, rank).tolist()
+        all_ch = [None] * world
+        dist.all_gather_object(all_ch, chans)
+        # bench.py: barrier, then max over ranks of the elapsed time
+        dist.barrier()
+        t = torch.tensor([1.0 + rank], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        if rank == 0:
+            q.put((gathered, all_ch, float(t.item())))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_partitions_tile_the_work():
+    for total in (0, 1, 5, 64, 1000):
+        for world in (1, 2, 3, 8):
+            spans = [shard.block_range(total, world, r) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == total
+            assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
+            assert max(h - l for l, h in spans) - min(h - l for l, h in spans) <= 1
+    for world in (1, 2, 8):
+        ids = np.concatenate([shard.channels_of(256, world, r) for r in range(world)])
+        assert sorted(ids.tolist()) == list(range(256))
+    with pytest.raises(ValueError):
+        shard.block_range(4, 2, 2)
+
+
+def test_two_rank_gloo_matches_single_process():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    world = 2
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    os.environ["PYTHONPATH"] = os.pathsep.join([here, root, os.path.join(root, "gnss-sdr-new_amd"),
+                                                os.environ.get("PYTHONPATH", "")])
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    gathered, all_ch, tmax = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    merged = shard.merge_blocks(gathered, BLOCKS, world)
+    single = _acq_blocks(_stream(), 0, BLOCKS)
+    np.testing.assert_array_equal(merged[..., :2], single[..., :2])
+    np.testing.assert_allclose(merged[..., 2], single[..., 2], rtol=0, atol=0)
+    assert sorted(sum(all_ch, [])) == list(range(12))
+    assert tmax == 2.0
+    recs = shard.merge_channels([[("r0", c) for c in all_ch[0]], [("r1", c) for c in all_ch[1]]], 12, world)
+    assert [r[1] for r in recs] == list(range(12))

@@ -123,3 +123,165 @@ def to_cshort(iq, scale=1000.0):
     a[0::2] = iq.real * scale
     a[1::2] = iq.imag * scale
     return np.clip(np.rint(a), -32768, 32767).astype(np.int16)
+
+
+# ---------------------------------------------------------------- Galileo E1, BeiDou B1I
+# Code tables: Galileo OS SIS ICD memory codes (data/galileo_e1_codes.bin, see
+# tools/extract_galileo_e1_codes.py); BeiDou B1I Gold codes from the ICD's G1/G2
+# registers and phase assignment.
+import os as _os
+
+GAL_E1_HZ = 1.57542e9
+BDS_B1I_HZ = 1.561098e9
+_GAL_TABLE = None
+GAL_E1C_SECONDARY = "0011100000001010110110010"
+BDS_B1I_NH = "00000100110101001110"
+
+
+def gal_e1_chips(prn, pilot=False):
+    """+-1 chips (logic 0 -> +1) of E1-B (data) or E1-C (pilot) PRN 1..50."""
+    global _GAL_TABLE
+    if _GAL_TABLE is None:
+        path = _os.path.join(_os.path.dirname(_os.path.abspath(__file__)), "data", "galileo_e1_codes.bin")
+        _GAL_TABLE = np.unpackbits(np.fromfile(path, np.uint8).reshape(100, 512), axis=1)[:, :4092]
+    return (1.0 - 2.0 * _GAL_TABLE[(50 if pilot else 0) + prn - 1]).astype(np.float32)
+
+
+def gal_e1_sinboc11(prn, pilot=False):
+    """Tracking replica: sinBOC(1,1) at 2 samples per chip (+c, -c) -- 8184 floats."""
+    c = gal_e1_chips(prn, pilot)
+    return np.stack([c, -c], axis=1).reshape(-1)
+
+
+def _f32_upsample_index(n, fs_in, fs_out):
+    """idx = (int)(t_out*(i+1)*fs_in + 1) - 1 in float32, last one forced (the
+    reference replica samplers' index rule)."""
+    f32 = np.float32
+    i = np.arange(n, dtype=np.float32)
+    idx = (((f32(1.0) / f32(fs_out)) * (i + f32(1.0))) * f32(fs_in) + f32(1)).astype(np.int64).astype(np.int32) - 1
+    return idx
+
+
+def gal_e1_sampled(prn, fs, pilot=False, cboc=False):
+    """Acquisition replica at fs (complex, real part), one 4 ms code period: the
+    sinBOC(1,1) (or CBOC(6,1,1/11) at 12 samples/chip) chip stream resampled to fs."""
+    c = gal_e1_chips(prn, pilot)
+    if cboc:
+        a = np.float32(np.sqrt(np.float32(10.0) / np.float32(11.0)))
+        b = np.float32(np.sqrt(np.float32(1.0) / np.float32(11.0)))
+        s11 = np.repeat(np.array([1.0] * 6 + [-1.0] * 6, np.float32)[None, :], 4092, 0) * c[:, None]
+        s61 = np.repeat(np.array([1.0, -1.0] * 6, np.float32)[None, :], 4092, 0) * c[:, None]
+        sub = (a * s11 + b * s61) if not pilot else (a * s11 - b * s61)
+        src, rate = sub.reshape(-1).astype(np.float32), 12 * 1023000
+    else:
+        src, rate = gal_e1_sinboc11(prn, pilot), 2 * 1023000
+    n = int(float(fs) / (1023000.0 / 4092.0))
+    if fs != rate:
+        idx = _f32_upsample_index(n, float(rate), fs)
+        idx[-1] = len(src) - 1
+        src = src[idx]
+    return src.astype(np.complex64)
+
+
+def _bds_registers():
+    init = [int("01010101010"[10 - i]) for i in range(11)]
+    return list(init), list(init)
+
+
+def bds_b1i_chips(prn):
+    """+-1 chips of BeiDou B1I PRN 1..63 (G1 xor phase-selected G2 taps; logic 1 -> +1)."""
+    ph = {1: (1, 3), 2: (1, 4), 3: (1, 5), 4: (1, 6), 5: (1, 8), 6: (1, 9), 7: (1, 10), 8: (1, 11), 9: (2, 7),
+          10: (3, 4), 11: (3, 5), 12: (3, 6), 13: (3, 8), 14: (3, 9), 15: (3, 10), 16: (3, 11), 17: (4, 5),
+          18: (4, 6), 19: (4, 8), 20: (4, 9), 21: (4, 10), 22: (4, 11), 23: (5, 6), 24: (5, 8), 25: (5, 9),
+          26: (5, 10), 27: (5, 11), 28: (6, 8), 29: (6, 9), 30: (6, 10), 31: (6, 11), 32: (8, 9), 33: (8, 10),
+          34: (8, 11), 35: (9, 10), 36: (9, 11), 37: (10, 11)}
+    ph3 = {38: (1, 2, 7), 39: (1, 3, 4), 40: (1, 3, 6), 41: (1, 3, 8), 42: (1, 3, 10), 43: (1, 3, 11),
+           44: (1, 4, 5), 45: (1, 4, 9), 46: (1, 5, 6), 47: (1, 5, 8), 48: (1, 5, 10), 49: (1, 5, 11), 50: (1, 6, 9),
+           51: (1, 8, 9), 52: (1, 9, 10), 53: (1, 9, 11), 54: (2, 3, 7), 55: (2, 5, 7), 56: (2, 7, 9),
+           57: (3, 4, 5), 58: (3, 4, 9), 59: (3, 5, 6), 60: (3, 5, 8), 61: (3, 5, 10), 62: (3, 5, 11),
+           63: (3, 6, 9)}
+    taps = ph[prn] if prn in ph else ph3[prn]
+    g1r, g2r = _bds_registers()
+    g1 = np.zeros(2046, np.int8)
+    g2 = np.zeros(2046, np.int8)
+    for i in range(2046):
+        g1[i] = g1r[0]
+        v = 0
+        for t in taps:
+            v ^= g2r[11 - t]
+        g2[i] = v
+        f1 = g1r[0] ^ g1r[1] ^ g1r[2] ^ g1r[3] ^ g1r[4] ^ g1r[10]
+        f2 = g2r[0] ^ g2r[2] ^ g2r[3] ^ g2r[6] ^ g2r[7] ^ g2r[8] ^ g2r[9] ^ g2r[10]
+        g1r = g1r[1:] + [f1]
+        g2r = g2r[1:] + [f2]
+    return np.where((g1 ^ g2) == 1, 1.0, -1.0).astype(np.float32)
+
+
+def bds_b1i_sampled(prn, fs):
+    """Acquisition replica at fs (complex, real +-1), one 1 ms code period."""
+    n = int(float(fs) / (2046000.0 / 2046.0))
+    f32 = np.float32
+    i = np.arange(n, dtype=np.float32)
+    idx = ((((f32(1.0) / f32(fs)) * (i + f32(1))) / (f32(1.0) / f32(2046000))) + f32(1)).astype(np.int64).astype(np.int32) - 1
+    idx[-1] = 2045
+    return bds_b1i_chips(prn)[idx].astype(np.complex64)
+
+
+class GalileoSatellite:
+    """E1 OS signal: (E1-B data - E1-C pilot x secondary) / sqrt(2), CBOC(6,1,1/11)
+    subcarriers, 4 ms symbols on E1-B."""
+
+    def __init__(self, prn, doppler_hz, code_delay_chips, cn0_dbhz=45.0, phase=0.0):
+        self.prn, self.doppler_hz, self.code_delay_chips = prn, doppler_hz, code_delay_chips
+        self.cn0_dbhz, self.phase = cn0_dbhz, phase
+
+
+def gal_e1_iq(fs, n_samples, sats, seed_offset=0, noise=True, dtype=np.complex64):
+    rng = np.random.default_rng(SEED + 2000 + seed_offset)
+    t = np.arange(n_samples, dtype=np.float64) / fs
+    out = np.zeros(n_samples, np.complex128)
+    a, b = np.sqrt(10.0 / 11.0), np.sqrt(1.0 / 11.0)
+    sec = np.array([1.0 if c == "0" else -1.0 for c in GAL_E1C_SECONDARY])
+    for s in sats:
+        amp = np.sqrt(10.0 ** (s.cn0_dbhz / 10.0) / fs)
+        cp = t * 1.023e6 - s.code_delay_chips          # chips
+        chip = np.floor(cp).astype(np.int64)
+        frac = cp - chip
+        s11 = np.where(frac < 0.5, 1.0, -1.0)
+        s61 = np.where(np.floor(frac * 12).astype(np.int64) % 2 == 0, 1.0, -1.0)
+        epoch = np.floor_divide(chip, 4092)
+        cb = gal_e1_chips(s.prn)[chip % 4092]
+        cc = gal_e1_chips(s.prn, pilot=True)[chip % 4092]
+        brng = np.random.default_rng(SEED + 91 * s.prn)
+        nb = int(epoch.max() - epoch.min()) + 2
+        bits = np.where(brng.random(nb) < 0.5, -1.0, 1.0)
+        d = bits[(epoch - epoch.min()) % nb]
+        e1b = cb * d * (a * s11 + b * s61)
+        e1c = cc * sec[epoch % 25] * (a * s11 - b * s61)
+        out += amp * (e1b - e1c) / np.sqrt(2.0) * np.exp(1j * (2 * np.pi * s.doppler_hz * t + s.phase))
+    if noise:
+        out += (rng.standard_normal(n_samples) + 1j * rng.standard_normal(n_samples)) * np.sqrt(0.5)
+    return out.astype(dtype)
+
+
+def bds_b1i_iq(fs, n_samples, sats, seed_offset=0, noise=True, dtype=np.complex64):
+    """B1I D1 signal: code x NH(20) x 50 bps data; sats are Satellite objects whose
+    code_delay_chips is in B1I chips (2.046 Mcps)."""
+    rng = np.random.default_rng(SEED + 3000 + seed_offset)
+    t = np.arange(n_samples, dtype=np.float64) / fs
+    out = np.zeros(n_samples, np.complex128)
+    nh = np.array([1.0 if c == "0" else -1.0 for c in BDS_B1I_NH])
+    for s in sats:
+        amp = np.sqrt(10.0 ** (s.cn0_dbhz / 10.0) / fs)
+        cp = t * 2.046e6 - s.code_delay_chips
+        chip = np.floor(cp).astype(np.int64)
+        epoch = np.floor_divide(chip, 2046)
+        c = bds_b1i_chips(s.prn)[chip % 2046]
+        bit = np.floor_divide(epoch, 20)
+        nb = int(bit.max() - bit.min()) + 2
+        bits = np.where(np.random.default_rng(SEED + 53 * s.prn).random(nb) < 0.5, -1.0, 1.0)
+        out += amp * c * nh[epoch % 20] * bits[(bit - bit.min()) % nb] * np.exp(
+            1j * (2 * np.pi * s.doppler_hz * t + s.phase))
+    if noise:
+        out += (rng.standard_normal(n_samples) + 1j * rng.standard_normal(n_samples)) * np.sqrt(0.5)
+    return out.astype(dtype)

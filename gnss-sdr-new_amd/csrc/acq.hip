@@ -21,9 +21,11 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <type_traits>
 #include <new>
 #include <vector>
 
+#include "fft_4step.h"
 #include "fft_lds.h"
 #include "fft_multi.h"
 #include "fft_pk.h"
@@ -35,7 +37,7 @@ namespace
 
 using gsdr::fft::Plan;
 
-// Default correlate variant at N = 4000 (see GSDR_CORR_VARIANTS).
+// Default correlate variant at N = 4000 (see GSDR_PK_VARIANTS).
 constexpr int kDefaultCorrVariant4000 = 35;
 
 struct RowStat
@@ -155,7 +157,7 @@ __global__ void __launch_bounds__(256) acq_wipeoff_kernel(float2* __restrict__ w
 // ---------------------------------------------------------------- K_code
 template <class PT>
 __global__ void __launch_bounds__(PT::NT) acq_code_fft_kernel(const float2* __restrict__ codes,
-    float2* __restrict__ code_fft, const float2* __restrict__ tw, Plan plan, uint32_t consumed, uint32_t lead)
+    float2* __restrict__ code_fft, const float2* __restrict__ tw, typename PT::PlanT plan, uint32_t consumed, uint32_t lead)
 {
     extern __shared__ float2 lds[];
     const uint32_t p = blockIdx.x;
@@ -172,7 +174,7 @@ __global__ void __launch_bounds__(PT::NT) acq_code_fft_kernel(const float2* __re
 // ---------------------------------------------------------------- K_forward
 template <class PT, int IT>
 __global__ void __launch_bounds__(PT::NT) acq_forward_kernel(const void* __restrict__ iq, uint64_t block_stride,
-    const float2* __restrict__ wipe, float2* __restrict__ X, const float2* __restrict__ tw, Plan plan,
+    const float2* __restrict__ wipe, float2* __restrict__ X, const float2* __restrict__ tw, typename PT::PlanT plan,
     uint32_t consumed, uint32_t D)
 {
     extern __shared__ float2 lds[];
@@ -194,10 +196,10 @@ __global__ void __launch_bounds__(PT::NT) acq_forward_kernel(const void* __restr
 template <class PT, bool GRID>
 __global__ void __launch_bounds__(PT::NT) acq_correlate_kernel(const float2* __restrict__ X,
     const float2* __restrict__ code_fft, RowStat* __restrict__ stats, float* __restrict__ grid,
-    const float2* __restrict__ tw, Plan plan, uint32_t D, uint32_t P, uint32_t prn_slot_for_grid)
+    const float2* __restrict__ tw, typename PT::PlanT plan, uint32_t D, uint32_t P, uint32_t prn_slot_for_grid)
 {
     extern __shared__ float2 lds[];
-    RowStat* scratch = reinterpret_cast<RowStat*>(lds + plan.n);
+    RowStat* scratch = reinterpret_cast<RowStat*>(lds + gsdr::fft::lds_elems_dev(plan));
     const uint32_t N = plan.n;
     uint32_t d, p, b;
     if (GRID)
@@ -255,179 +257,6 @@ __global__ void __launch_bounds__(PT::NT) acq_correlate_kernel(const float2* __r
         {
             block_reduce_stat<PT::NT>(best, bidx, sum, scratch);
             if (threadIdx.x == 0) stats[((size_t)b * P + p) * D + d] = RowStat{best, bidx, sum, 0};
-        }
-}
-
-// ---------------------------------------------------------------- K_correlate (multi)
-// PB PRNs per workgroup: the PB transforms share the X_{b,d} loads and every
-// twiddle load, and interleave their dependency chains.  1-D grid over
-// (row = b*D + d, PRN group), XCD-aware like acq_correlate_kernel.
-template <class MP>
-__global__ void __launch_bounds__(MP::NT) acq_correlate_multi_kernel(const float2* __restrict__ X,
-    const float2* __restrict__ code_fft, RowStat* __restrict__ stats, const float2* __restrict__ tw, uint32_t D,
-    uint32_t P, uint32_t nblocks)
-{
-    constexpr int PB = MP::PB;
-    constexpr int NT = MP::NT;
-    constexpr int NW = NT / 64;
-    constexpr uint32_t N = MP::N;
-    extern __shared__ float2 lds[];
-    RowStat* scratch = reinterpret_cast<RowStat*>(lds + PB * MP::STRIDE);
-    const uint32_t G = (P + PB - 1) / PB;
-    const uint32_t nrows = nblocks * D;
-    const uint32_t id = blockIdx.x;
-    const uint32_t full = nrows >> 3;
-    uint32_t row, g;
-    if (id < full * 8u * G)
-        {
-            const uint32_t xcd = id & 7u, slot = id >> 3;
-            row = (slot / G) * 8u + xcd;
-            g = slot - (slot / G) * G;
-        }
-    else
-        {
-            const uint32_t t = id - full * 8u * G;
-            row = full * 8u + t / G;
-            g = t - (t / G) * G;
-        }
-    const uint32_t b = row / D, d = row - (row / D) * D;
-    const uint32_t p0 = g * PB;
-    const float2* x = X + (size_t)row * N;
-    const float2* c[PB];
-#pragma unroll
-    for (int t = 0; t < PB; ++t) c[t] = code_fft + (size_t)min(p0 + t, P - 1) * N;
-    float best[PB], sum[PB];
-    uint32_t bidx[PB];
-#pragma unroll
-    for (int t = 0; t < PB; ++t)
-        {
-            best[t] = -1.0f;
-            sum[t] = 0.0f;
-            bidx[t] = 0xffffffffu;
-        }
-    auto load = [&](int, int, int i, float2(&out)[PB]) {
-        const float2 a = x[i];
-#pragma unroll
-        for (int t = 0; t < PB; ++t)
-            {
-                const float2 k = c[t][i];
-                out[t] = make_float2(a.x * k.x + a.y * k.y, a.x * k.y - a.y * k.x);
-            }
-    };
-    auto store = [&](int i, const float2(&in)[PB]) {
-#pragma unroll
-        for (int t = 0; t < PB; ++t)
-            {
-                const float m = in[t].x * in[t].x + in[t].y * in[t].y;
-                if (stat_better(m, (uint32_t)i, best[t], bidx[t]))
-                    {
-                        best[t] = m;
-                        bidx[t] = (uint32_t)i;
-                    }
-                sum[t] += m;
-            }
-    };
-    MP::run(lds, tw, load, store);
-#pragma unroll
-    for (int t = 0; t < PB; ++t)
-        {
-            block_reduce_stat<NT>(best[t], bidx[t], sum[t], scratch + t * NW);
-            if (threadIdx.x == 0 && p0 + t < P) stats[((size_t)b * P + p0 + t) * D + d] = RowStat{best[t], bidx[t], sum[t], 0};
-        }
-}
-
-// ---------------------------------------------------------------- K_correlate (sequential PRN group)
-// One workgroup per (row = b*D + d, group of PG PRNs).  The lane's first-stage
-// inputs of X_{b,d} stay in VGPRs for the whole group; the next PRN's code-spectrum
-// values are loaded into the registers the current product has just consumed
-// (right after the first FFT stage), so their latency hides behind stages 2..S.
-template <class MP, int PG>
-__global__ void __launch_bounds__(MP::NT) acq_correlate_seq_kernel(const float2* __restrict__ X,
-    const float2* __restrict__ code_fft, RowStat* __restrict__ stats, const float2* __restrict__ tw, uint32_t D,
-    uint32_t P, uint32_t nblocks)
-{
-    static_assert(MP::PB == 1, "sequential kernel runs one transform at a time");
-    constexpr int NT = MP::NT;
-    constexpr int NW = NT / 64;
-    constexpr int R1 = MP::R1, BPT1 = MP::BPT1, NB1 = MP::NB1;
-    constexpr uint32_t N = MP::N;
-    extern __shared__ float2 lds[];
-    RowStat* scratch = reinterpret_cast<RowStat*>(lds + MP::STRIDE);
-    const uint32_t G = (P + PG - 1) / PG;
-    const uint32_t nrows = nblocks * D;
-    const uint32_t id = blockIdx.x;
-    const uint32_t full = nrows >> 3;
-    uint32_t row, g;
-    if (id < full * 8u * G)
-        {
-            const uint32_t xcd = id & 7u, slot = id >> 3;
-            row = (slot / G) * 8u + xcd;
-            g = slot - (slot / G) * G;
-        }
-    else
-        {
-            const uint32_t t = id - full * 8u * G;
-            row = full * 8u + t / G;
-            g = t - (t / G) * G;
-        }
-    const uint32_t b = row / D, d = row - (row / D) * D;
-    const uint32_t p0 = g * PG;
-    const int np = (int)min((uint32_t)PG, P - p0);
-    const float2* x = X + (size_t)row * N;
-    float2 xr[BPT1][R1], cr[BPT1][R1];
-    {
-        const float2* c = code_fft + (size_t)p0 * N;
-#pragma unroll
-        for (int bb = 0; bb < BPT1; ++bb)
-            {
-                const int j = (int)threadIdx.x + bb * NT;
-                if (j < NB1)
-                    {
-#pragma unroll
-                        for (int r = 0; r < R1; ++r)
-                            {
-                                xr[bb][r] = x[j + r * NB1];
-                                cr[bb][r] = c[j + r * NB1];
-                            }
-                    }
-            }
-    }
-    for (int q = 0; q < np; ++q)
-        {
-            float best = -1.0f, sum = 0.0f;
-            uint32_t bidx = 0xffffffffu;
-            auto load = [&](int bb, int r, int, float2(&out)[1]) {
-                const float2 a = xr[bb][r], k = cr[bb][r];
-                out[0] = make_float2(a.x * k.x + a.y * k.y, a.x * k.y - a.y * k.x);
-            };
-            auto hook = [&]() {
-                if (q + 1 < np)
-                    {
-                        const float2* c = code_fft + (size_t)(p0 + q + 1) * N;
-#pragma unroll
-                        for (int bb = 0; bb < BPT1; ++bb)
-                            {
-                                const int j = (int)threadIdx.x + bb * NT;
-                                if (j < NB1)
-                                    {
-#pragma unroll
-                                        for (int r = 0; r < R1; ++r) cr[bb][r] = c[j + r * NB1];
-                                    }
-                            }
-                    }
-            };
-            auto store = [&](int i, const float2(&in)[1]) {
-                const float m = in[0].x * in[0].x + in[0].y * in[0].y;
-                if (stat_better(m, (uint32_t)i, best, bidx))
-                    {
-                        best = m;
-                        bidx = (uint32_t)i;
-                    }
-                sum += m;
-            };
-            MP::run(lds, tw, load, store, hook);
-            block_reduce_stat<NT>(best, bidx, sum, scratch + (q & 1) * NW);
-            if (threadIdx.x == 0) stats[((size_t)b * P + p0 + q) * D + d] = RowStat{best, bidx, sum, 0};
         }
 }
 
@@ -670,10 +499,10 @@ __global__ void __launch_bounds__(64) acq_reduce_kernel(const RowStat* __restric
 template <class PT>
 __global__ void __launch_bounds__(PT::NT) acq_second_peak_kernel(const float2* __restrict__ X,
     const float2* __restrict__ code_fft, gsdr_acq_result* __restrict__ res, const float2* __restrict__ tw,
-    Plan plan, AcqParams ap)
+    typename PT::PlanT plan, AcqParams ap)
 {
     extern __shared__ float2 lds[];
-    RowStat* scratch = reinterpret_cast<RowStat*>(lds + plan.n);
+    RowStat* scratch = reinterpret_cast<RowStat*>(lds + gsdr::fft::lds_elems_dev(plan));
     const uint32_t bp = blockIdx.x;
     const uint32_t b = bp / ap.P, p = bp - b * ap.P;
     const uint32_t N = plan.n;
@@ -725,9 +554,10 @@ struct gsdr_acq
     float threshold{0.0f};
     int nt{256};
     int variant{0};
-    int corr_variant{0};      // 0: single-transform correlate kernel; >0: GSDR_CORR_VARIANTS id
+    int corr_variant{0};      // 0: single-transform correlate kernel; >0: GSDR_PK(M)_VARIANTS id
     size_t corr_lds_bytes{0};
     Plan plan{};
+    gsdr::fft::Plan4 plan4{};  // four-step plan (variants 20-22, N beyond one workgroup's LDS)
     size_t lds_bytes{0};
     hipStream_t stream{nullptr};
     float2* d_tw{nullptr};
@@ -741,6 +571,9 @@ struct gsdr_acq
     gsdr_acq_result* d_res{nullptr};
     void* d_iq{nullptr};
     float* d_grid{nullptr};
+    float2* d_tw_sub{nullptr};   // four-step: W_N2 table
+    float2* d_scratch{nullptr};  // four-step: slot rows of N complex
+    uint32_t* d_slots{nullptr};  // four-step: slot occupancy bitmap
     // stage profiling (gsdr_acq_set_profiling)
     struct ProfRec
     {
@@ -756,6 +589,7 @@ struct gsdr_acq
 namespace
 {
 
+using gsdr::fft::FourStepPlan;
 using gsdr::fft::RuntimePlan;
 using gsdr::fft::StaticPlan;
 
@@ -770,40 +604,18 @@ size_t item_bytes(int it) { return it == GSDR_ITEM_CSHORT ? 4 : 8; }
     X(4, (StaticPlan<256, 20, 10, 10>))    \
     X(10, (RuntimePlan<256>))              \
     X(11, (RuntimePlan<512>))              \
-    X(12, (RuntimePlan<1024>))
+    X(12, (RuntimePlan<1024>))             \
+    X(20, (FourStepPlan<256>))             \
+    X(22, (FourStepPlan<1024>))
 
-using gsdr::fft::MultiPlan;
 
 // Correlate-kernel variants for N = 4000 (env GSDR_ACQ_CORR_VARIANT selects one;
 // 0 = the single-transform kernel of the plan variant).
-#define GSDR_CORR_VARIANTS(X)                                \
-    X(5, (MultiPlan<256, 1, false, false, 25, 16, 10>))     \
-    X(7, (MultiPlan<256, 1, false, true, 25, 16, 10>))      \
-    X(8, (MultiPlan<256, 1, false, true, 20, 20, 10>))      \
-    X(11, (MultiPlan<256, 1, true, true, 20, 20, 10>))      \
-    X(12, (MultiPlan<256, 1, false, true, 16, 25, 10>))     \
-    X(13, (MultiPlan<256, 1, false, true, 16, 10, 25>))
-
-// Sequential-PRN-group variants: (id, plan, PRNs per workgroup).
-#define GSDR_SEQ_VARIANTS(X)                                      \
-    X(20, (MultiPlan<256, 1, false, true, 16, 25, 10>), 4)       \
-    X(21, (MultiPlan<256, 1, false, true, 16, 25, 10>), 8)       \
-    X(22, (MultiPlan<256, 1, false, true, 16, 25, 10>), 16)      \
-    X(23, (MultiPlan<256, 1, false, true, 25, 16, 10>), 8)       \
-    X(24, (MultiPlan<256, 1, false, true, 20, 20, 10>), 8)       \
-    X(25, (MultiPlan<256, 1, false, true, 16, 10, 25>), 8)
-
 // Packed-f32 variants: (id, plan, PRNs per workgroup).
 #define GSDR_PK_VARIANTS(X)                                              \
     X(30, (gsdr::pk::PkPlan<256, true, 25, 16, 10>), 1, 1)              \
-    X(31, (gsdr::pk::PkPlan<512, true, 25, 16, 10>), 1, 1)              \
-    X(32, (gsdr::pk::PkPlan<512, true, 20, 20, 10>), 1, 1)              \
-    X(33, (gsdr::pk::PkPlan<448, true, 25, 16, 10>), 1, 1)              \
-    X(34, (gsdr::pk::PkPlan<512, true, 10, 20, 20>), 1, 1)              \
     X(35, (gsdr::pk::PkPlan<256, true, 20, 20, 10>), 1, 1)              \
-    X(36, (gsdr::pk::PkPlan<512, true, 16, 25, 10>), 1, 1)              \
-    X(37, (gsdr::pk::PkPlan<512, true, 25, 16, 10>), 2, 1)              \
-    X(38, (gsdr::pk::PkPlan<384, true, 25, 16, 10>), 1, 1)
+    X(37, (gsdr::pk::PkPlan<512, true, 25, 16, 10>), 2, 1)
 
 // Packed multi-transform variants: (id, plan, waves per EU hint).
 #define GSDR_PKM_VARIANTS(X)                                              \
@@ -906,24 +718,6 @@ struct StageTimer
 
 int launch_corr_variant(gsdr_acq* a, uint32_t nblocks, hipStream_t s)
 {
-#define GSDR_CV_CASE(ID, MP)                                                                                    \
-    case ID:                                                                                                    \
-        {                                                                                                       \
-            using M = GSDR_UNPAREN MP;                                                                          \
-            const uint32_t groups = (a->nprn + M::PB - 1) / M::PB;                                              \
-            hipLaunchKernelGGL((acq_correlate_multi_kernel<M>), dim3(nblocks * a->D * groups), dim3(M::NT),     \
-                a->corr_lds_bytes, s, a->d_X, a->d_code_fft, a->d_stats, a->d_tw, a->D, a->nprn, nblocks);      \
-            return GSDR_OK;                                                                                     \
-        }
-#define GSDR_SQ_CASE(ID, MP, PG)                                                                                \
-    case ID:                                                                                                    \
-        {                                                                                                       \
-            using M = GSDR_UNPAREN MP;                                                                          \
-            const uint32_t groups = (a->nprn + (PG)-1) / (PG);                                                  \
-            hipLaunchKernelGGL((acq_correlate_seq_kernel<M, PG>), dim3(nblocks * a->D * groups), dim3(M::NT),  \
-                a->corr_lds_bytes, s, a->d_X, a->d_code_fft, a->d_stats, a->d_tw, a->D, a->nprn, nblocks);      \
-            return GSDR_OK;                                                                                     \
-        }
 #define GSDR_PK_CASE(ID, MP, PG, WPE)                                                                                \
     case ID:                                                                                                    \
         {                                                                                                       \
@@ -945,14 +739,10 @@ int launch_corr_variant(gsdr_acq* a, uint32_t nblocks, hipStream_t s)
 #define GSDR_UNPAREN(...) __VA_ARGS__
     switch (a->corr_variant)
         {
-            GSDR_CORR_VARIANTS(GSDR_CV_CASE)
-            GSDR_SEQ_VARIANTS(GSDR_SQ_CASE)
             GSDR_PK_VARIANTS(GSDR_PK_CASE)
             GSDR_PKM_VARIANTS(GSDR_PKM_CASE)
         default: gsdr::set_error("internal: bad correlate variant %d", a->corr_variant); return GSDR_E_STATE;
         }
-#undef GSDR_CV_CASE
-#undef GSDR_SQ_CASE
 #undef GSDR_PK_CASE
 #undef GSDR_PKM_CASE
 #undef GSDR_UNPAREN
@@ -961,26 +751,6 @@ int launch_corr_variant(gsdr_acq* a, uint32_t nblocks, hipStream_t s)
 // Select and configure a correlate variant (N must be 4000).
 int setup_corr_variant(gsdr_acq* a, int v)
 {
-#define GSDR_CV_SETUP(ID, MP)                                                                                   \
-    case ID:                                                                                                    \
-        {                                                                                                       \
-            using M = GSDR_UNPAREN MP;                                                                          \
-            a->corr_lds_bytes = M::lds_bytes() + (size_t)M::PB * (M::NT / 64) * sizeof(RowStat);               \
-            GSDR_HIP(hipFuncSetAttribute((const void*)acq_correlate_multi_kernel<M>,                           \
-                hipFuncAttributeMaxDynamicSharedMemorySize, (int)a->corr_lds_bytes));                           \
-            a->corr_variant = ID;                                                                               \
-            return GSDR_OK;                                                                                     \
-        }
-#define GSDR_SQ_SETUP(ID, MP, PG)                                                                               \
-    case ID:                                                                                                    \
-        {                                                                                                       \
-            using M = GSDR_UNPAREN MP;                                                                          \
-            a->corr_lds_bytes = M::lds_bytes() + (size_t)2 * (M::NT / 64) * sizeof(RowStat);                   \
-            GSDR_HIP(hipFuncSetAttribute((const void*)acq_correlate_seq_kernel<M, PG>,                         \
-                hipFuncAttributeMaxDynamicSharedMemorySize, (int)a->corr_lds_bytes));                           \
-            a->corr_variant = ID;                                                                               \
-            return GSDR_OK;                                                                                     \
-        }
 #define GSDR_PK_SETUP(ID, MP, PG, WPE)                                                                               \
     case ID:                                                                                                    \
         {                                                                                                       \
@@ -1004,17 +774,23 @@ int setup_corr_variant(gsdr_acq* a, int v)
 #define GSDR_UNPAREN(...) __VA_ARGS__
     switch (v)
         {
-            GSDR_CORR_VARIANTS(GSDR_CV_SETUP)
-            GSDR_SEQ_VARIANTS(GSDR_SQ_SETUP)
             GSDR_PK_VARIANTS(GSDR_PK_SETUP)
             GSDR_PKM_VARIANTS(GSDR_PKM_SETUP)
         default: a->corr_variant = 0; return GSDR_OK;
         }
-#undef GSDR_CV_SETUP
-#undef GSDR_SQ_SETUP
 #undef GSDR_PK_SETUP
 #undef GSDR_PKM_SETUP
 #undef GSDR_UNPAREN
+}
+
+// The plan object a plan type's kernels take (LDS plan or four-step plan).
+template <class PT>
+const typename PT::PlanT& plan_of(const gsdr_acq* a)
+{
+    if constexpr (std::is_same<typename PT::PlanT, gsdr::fft::Plan4>::value)
+        return a->plan4;
+    else
+        return a->plan;
 }
 
 template <class PT>
@@ -1022,10 +798,10 @@ void launch_forward(gsdr_acq* a, const void* iq, int item_type, uint32_t nblocks
 {
     if (item_type == GSDR_ITEM_GR_COMPLEX)
         hipLaunchKernelGGL((acq_forward_kernel<PT, GSDR_ITEM_GR_COMPLEX>), dim3(a->D, nblocks), dim3(PT::NT),
-            a->lds_bytes, s, iq, stride, a->d_wipe, a->d_X, a->d_tw, a->plan, a->consumed, a->D);
+            a->lds_bytes, s, iq, stride, a->d_wipe, a->d_X, a->d_tw, plan_of<PT>(a), a->consumed, a->D);
     else
         hipLaunchKernelGGL((acq_forward_kernel<PT, GSDR_ITEM_CSHORT>), dim3(a->D, nblocks), dim3(PT::NT),
-            a->lds_bytes, s, iq, stride, a->d_wipe, a->d_X, a->d_tw, a->plan, a->consumed, a->D);
+            a->lds_bytes, s, iq, stride, a->d_wipe, a->d_X, a->d_tw, plan_of<PT>(a), a->consumed, a->D);
 }
 
 template <class PT>
@@ -1047,7 +823,7 @@ int launch_all(gsdr_acq* a, const void* iq, int item_type, uint32_t nblocks, uin
     else
         {
             hipLaunchKernelGGL((acq_correlate_kernel<PT, false>), dim3(a->D * a->nprn, nblocks), dim3(PT::NT), lds, s,
-                a->d_X, a->d_code_fft, a->d_stats, (float*)nullptr, a->d_tw, a->plan, a->D, a->nprn, 0u);
+                a->d_X, a->d_code_fft, a->d_stats, (float*)nullptr, a->d_tw, plan_of<PT>(a), a->D, a->nprn, 0u);
         }
     GSDR_HIP(hipGetLastError());
     t.end(1);
@@ -1061,7 +837,7 @@ int launch_all(gsdr_acq* a, const void* iq, int item_type, uint32_t nblocks, uin
         {
             t.begin();
             hipLaunchKernelGGL((acq_second_peak_kernel<PT>), dim3(nblocks * a->nprn), dim3(PT::NT), lds, s, a->d_X,
-                a->d_code_fft, res, a->d_tw, a->plan, ap);
+                a->d_code_fft, res, a->d_tw, plan_of<PT>(a), ap);
             GSDR_HIP(hipGetLastError());
             t.end(3);
         }
@@ -1072,7 +848,7 @@ template <class PT>
 int launch_code_fft(gsdr_acq* a, uint32_t nprn)
 {
     hipLaunchKernelGGL((acq_code_fft_kernel<PT>), dim3(nprn), dim3(PT::NT), a->lds_bytes, a->stream, a->d_code_stage,
-        a->d_code_fft, a->d_tw, a->plan, a->consumed, a->lead);
+        a->d_code_fft, a->d_tw, plan_of<PT>(a), a->consumed, a->lead);
     GSDR_HIP(hipGetLastError());
     return GSDR_OK;
 }
@@ -1085,7 +861,7 @@ int launch_dump(gsdr_acq* a, bool grid, uint32_t prn_slot)
     if (grid)
         {
             hipLaunchKernelGGL((acq_correlate_kernel<PT, true>), dim3(a->D, 1), dim3(PT::NT), a->lds_bytes, a->stream,
-                a->d_X, a->d_code_fft, a->d_stats, a->d_grid, a->d_tw, a->plan, a->D, a->nprn, prn_slot);
+                a->d_X, a->d_code_fft, a->d_stats, a->d_grid, a->d_tw, plan_of<PT>(a), a->D, a->nprn, prn_slot);
             GSDR_HIP(hipGetLastError());
         }
     return GSDR_OK;
@@ -1117,6 +893,8 @@ int dispatch(gsdr_acq* a, int op, const void* iq, uint32_t nblocks, uint64_t str
 
 // Pick a compile-time plan when one matches N, else the smallest workgroup that
 // admits a runtime plan.
+constexpr size_t kLdsBytes = 160 * 1024;
+
 bool choose_variant(gsdr_acq* a)
 {
     const int N = (int)a->N;
@@ -1142,12 +920,35 @@ bool choose_variant(gsdr_acq* a)
     const int ids[] = {10, 11, 12};
     const int nts[] = {256, 512, 1024};
     for (int i = 0; i < 3; ++i)
-        if (gsdr::fft::make_plan(N, nts[i], a->plan) && a->plan.nstages >= 2)
+        if (gsdr::fft::make_plan(N, nts[i], a->plan) && a->plan.nstages >= 2 &&
+            (size_t)N * sizeof(float2) + 16 * sizeof(RowStat) <= kLdsBytes)
             {
                 a->variant = ids[i];
                 a->nt = nts[i];
                 return true;
             }
+    // four-step (fft_4step.h): N = R * N2, the largest register radix R whose N2
+    // has an LDS plan
+    const int radices[] = {25, 20, 16, 12, 10, 8};
+    for (int R : radices)
+        {
+            if (N % R != 0) continue;
+            const int N2 = N / R;
+            if ((size_t)N2 * sizeof(float2) + 16 * sizeof(RowStat) > kLdsBytes) continue;
+            for (int i = 0; i < 3; i += 2)  // 256 or 1024 threads (variants 20, 22)
+                {
+                    Plan sub{};
+                    if (!gsdr::fft::make_plan(N2, nts[i], sub) || sub.nstages < 2) continue;
+                    a->variant = 20 + i;
+                    a->nt = nts[i];
+                    a->plan4 = gsdr::fft::Plan4{};
+                    a->plan4.n = N;
+                    a->plan4.r1 = R;
+                    a->plan4.sub = sub;
+                    a->plan.n = N;  // buffer sizes
+                    return true;
+                }
+        }
     return false;
 }
 
@@ -1200,11 +1001,13 @@ int gsdr_acq_create(int device, const gsdr_acq_conf* conf, gsdr_acq** out)
             return GSDR_E_ARG;
         }
     const bool ok = choose_variant(a);
-    a->lds_bytes = (size_t)N * sizeof(float2) + 16 * sizeof(RowStat);
-    if (!ok || a->lds_bytes > 160 * 1024)
+    const bool four = a->variant >= 20;
+    a->lds_bytes = (size_t)(four ? a->plan4.sub.n : N) * sizeof(float2) + 16 * sizeof(RowStat);
+    if (!ok || a->lds_bytes > kLdsBytes)
         {
             delete a;
-            gsdr::set_error("gsdr_acq_create: FFT size %u not supported by the LDS engine (needs 2^a*3^b*5^c and <= 20352 points)", N);
+            gsdr::set_error("gsdr_acq_create: FFT size %u not supported (needs 2^a*3^b*5^c; up to 20352 points in "
+                            "LDS, larger sizes as R*N2 with R in {8,10,12,16,20,25} and N2 <= 20352)", N);
             return GSDR_E_UNSUPPORTED;
         }
     int rc = dispatch(a, 4, nullptr, 0, 0, 0, nullptr, nullptr, 0);
@@ -1231,6 +1034,33 @@ int gsdr_acq_create(int device, const gsdr_acq_conf* conf, gsdr_acq** out)
     if (e == hipSuccess) e = hipMalloc(&a->d_res, nB * nP * sizeof(gsdr_acq_result));
     if (e == hipSuccess) e = hipMalloc(&a->d_iq, nB * a->consumed * item_bytes(conf->item_type));
     if (e == hipSuccess) e = hipMalloc(&a->d_grid, (size_t)a->D * N * sizeof(float));
+    if (four)
+        {
+            // scratch slots: at least the resident workgroup count of the chip
+            // (256 CUs x 32 waves / waves per workgroup), capped at 4 GiB
+            int nslots = 256 * 32 / (a->nt / 64);
+            while (nslots > 64 && (size_t)nslots * N * sizeof(float2) > (4ull << 30)) nslots /= 2;
+            nslots = (nslots + 31) / 32 * 32;
+            a->plan4.nwords = nslots / 32;
+            if (e == hipSuccess) e = hipMalloc(&a->d_tw_sub, (size_t)a->plan4.sub.n * sizeof(float2));
+            if (e == hipSuccess) e = hipMalloc(&a->d_scratch, (size_t)nslots * N * sizeof(float2));
+            if (e == hipSuccess) e = hipMalloc(&a->d_slots, (size_t)a->plan4.nwords * sizeof(uint32_t));
+            if (e == hipSuccess) e = hipMemset(a->d_slots, 0, (size_t)a->plan4.nwords * sizeof(uint32_t));
+            if (e == hipSuccess)
+                {
+                    const int N2 = a->plan4.sub.n;
+                    std::vector<float2> t2(N2);
+                    for (int m = 0; m < N2; ++m)
+                        {
+                            const double ang = 2.0 * M_PI * (double)m / (double)N2;
+                            t2[m] = make_float2((float)std::cos(ang), (float)(-std::sin(ang)));
+                        }
+                    e = hipMemcpy(a->d_tw_sub, t2.data(), N2 * sizeof(float2), hipMemcpyHostToDevice);
+                }
+            a->plan4.tw_sub = a->d_tw_sub;
+            a->plan4.scratch = a->d_scratch;
+            a->plan4.slots = a->d_slots;
+        }
     if (e != hipSuccess)
         {
             gsdr::set_error("gsdr_acq_create: device allocation failed: %s", hipGetErrorString(e));
@@ -1273,7 +1103,7 @@ void gsdr_acq_destroy(gsdr_acq* a)
         }
     for (hipEvent_t e : a->prof_pool) (void)hipEventDestroy(e);
     void* bufs[] = {a->d_tw, a->d_wipe, a->d_code_fft, a->d_code_stage, a->d_prn, a->d_X, a->d_stats, a->d_res,
-        a->d_iq, a->d_grid};
+        a->d_iq, a->d_grid, a->d_tw_sub, a->d_scratch, a->d_slots};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     if (a->stream) (void)hipStreamDestroy(a->stream);

@@ -329,6 +329,7 @@ struct StaticPlan
     static constexpr int NT = NT_;
     static constexpr int N = (Rs * ...);
     static constexpr int nstages = sizeof...(Rs);
+    using PlanT = Plan;
     template <class Load, class Store>
     __device__ __forceinline__ static void run(const Plan&, float2* lds, const float2* __restrict__ tw, Load load,
         Store store)
@@ -351,6 +352,7 @@ struct RuntimePlan
 {
     static constexpr int NT = NT_;
     static constexpr int N = 0;
+    using PlanT = Plan;
     template <class Load, class Store>
     __device__ __forceinline__ static void run(const Plan& p, float2* lds, const float2* __restrict__ tw, Load load,
         Store store)

@@ -79,3 +79,41 @@ def test_beidou_b1i_synthetic_batch(fs):
     assert exact >= len(prns) - 1
     det = {int(r["prn"]) for r in res if r["positive"]}
     assert set(vis) <= det
+
+
+@pytest.mark.parametrize("fs,N,pfa", [(8000000, 32000, 0.01), (25000000, 25000, 0.0), (8000000, 64000, 0.01),
+                                      (25000000, 100000, 0.01)])
+def test_large_fft_four_step(fs, N, pfa):
+    """N beyond one workgroup's LDS (four-step FFT, fft_4step.h): Galileo E1 at 8 Msps
+    (4 ms: 32000; 8 ms: 64000), BeiDou B1I at 25 Msps (1 ms: 25000), Galileo at
+    25 Msps (100000) -- configs C4/C5.  Parity with the oracle grid statistics."""
+    dmax, dstep = 2000, 500
+    rng = np.random.default_rng(N)
+    if N == 25000:
+        sats = [synth.Satellite(p, float(rng.uniform(-1500, 1500)), float(rng.uniform(0, 2046)), 50.0, 0.3)
+                for p in (3, 11)]
+        x = synth.bds_b1i_iq(fs, N, sats, seed_offset=2)
+        prns = np.array([3, 5, 11])
+        codes = np.stack([synth.bds_b1i_sampled(int(p), fs) for p in prns])
+        chip, spcode, ms = 2046000.0, float(N), 1
+    else:
+        sats = [synth.GalileoSatellite(p, float(rng.uniform(-1500, 1500)), float(rng.uniform(0, 4092)), 50.0, 0.3)
+                for p in (4, 19)]
+        x = synth.gal_e1_iq(fs, N, sats, seed_offset=2)
+        prns = np.array([4, 7, 19])
+        one = [synth.gal_e1_sampled(int(p), fs) for p in prns]
+        codes = np.stack([np.resize(c, N) for c in one])
+        chip, spcode, ms = 1023000.0, float(len(one[0])), N * 1000 // fs
+    acq = gsdr.Acquisition(fs, N, dmax, dstep, pfa=pfa, max_prns=len(prns), chip_rate=chip, sampled_ms=ms,
+                           ms_per_code=ms, samples_per_code=spcode)
+    assert acq.fft_size == N
+    acq.set_local_codes(codes, prns)
+    res = acq.run(x)[0]
+    grids = _oracle_grids(x, codes, fs, dmax, dstep, acq.num_doppler_bins)
+    spc = int(np.ceil(fs / chip))
+    for i in range(len(prns)):
+        _check_result(res[i], grids[i], pfa, spc, fs, dmax, dstep, spcode)
+    # the forward spectra themselves (first Doppler row)
+    X = acq.dump_spectra(x)
+    ref = np.fft.fft(x.astype(np.complex128) * pcps.doppler_wipeoffs(fs, N, dmax, dstep, acq.num_doppler_bins)[0])
+    assert np.linalg.norm(X[0] - ref) / np.linalg.norm(ref) < 2e-6

@@ -60,9 +60,11 @@ struct AcqParams
     int32_t doppler_step;
     float samples_per_code;
     uint32_t samples_per_chip;
-    uint32_t dwells;
+    uint32_t dwells;      // max_dwells K (non-coherent dwells per acquisition attempt)
     float threshold;
     int32_t cfar;
+    uint32_t eff;         // effective FFT size (N/2 with bit_transition_flag, else N)
+    uint32_t out_off;     // first output index of the effective window (N - eff)
 };
 
 template <int IT>
@@ -159,13 +161,17 @@ template <class PT>
 __global__ void __launch_bounds__(PT::NT) acq_code_fft_kernel(const float2* __restrict__ codes,
     float2* __restrict__ code_fft, const float2* __restrict__ tw, typename PT::PlanT plan, uint32_t consumed, uint32_t lead)
 {
+    // set_local_code (pcps_acquisition.cc:176-209): [0 x lead, code[0 .. N - lead)];
+    // lead = N - consumed, or N/2 with bit_transition_flag (then only the first N/2
+    // code samples of the consumed-long row are used)
     extern __shared__ float2 lds[];
     const uint32_t p = blockIdx.x;
     const float2* c = codes + (size_t)p * consumed;
     float2* out = code_fft + (size_t)p * plan.n;
+    const int valid = (int)plan.n - (int)lead;
     auto load = [&](int i) -> float2 {
         int k = i - (int)lead;
-        return (k >= 0 && k < (int)consumed) ? c[k] : make_float2(0.f, 0.f);
+        return (k >= 0 && k < valid) ? c[k] : make_float2(0.f, 0.f);
     };
     auto store = [&](int i, float2 v) { out[i] = v; };
     PT::run(plan, lds, tw, load, store);
@@ -431,6 +437,252 @@ __global__ void __launch_bounds__(MP::NT) __attribute__((amdgpu_waves_per_eu(WPE
         }
 }
 
+// ---------------------------------------------------------------- general path (dwells, bit transition)
+// acquisition_core with max_dwells K > 1 (non-coherent accumulation of |R|^2 over
+// K consecutive blocks, pcps_acquisition.cc:667-675) and/or bit_transition_flag
+// (outputs [N/2, N) of each transform, :671).  One workgroup per (attempt b, d, p)
+// runs the K transforms of dwells k = 0..K-1 (blocks b*K + k); each lane adds |R|^2
+// into its own entries of a pooled global row (every plan maps an output index to
+// the same lane in every transform, so no synchronisation is needed) and row
+// statistics of the accumulated grid are emitted after every dwell:
+// stats[((b*P + p)*K + k)*D + d].
+__device__ __forceinline__ int pool_acquire(uint32_t* slots, int nwords)
+{
+    __shared__ int s_slot;
+    if (threadIdx.x == 0)
+        {
+            int w = (int)((blockIdx.x + blockIdx.y * gridDim.x) % (unsigned)nwords);
+            for (;;)
+                {
+                    const uint32_t cur = __hip_atomic_load(&slots[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (cur != 0xffffffffu)
+                        {
+                            const int bit = __builtin_ctz(~cur);
+                            const uint32_t old =
+                                __hip_atomic_fetch_or(&slots[w], 1u << bit, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                            if (!(old & (1u << bit)))
+                                {
+                                    s_slot = w * 32 + bit;
+                                    break;
+                                }
+                        }
+                    else
+                        {
+                            w = w + 1 == nwords ? 0 : w + 1;
+                            __builtin_amdgcn_s_sleep(2);
+                        }
+                }
+        }
+    __syncthreads();
+    return s_slot;
+}
+
+__device__ __forceinline__ void pool_release(uint32_t* slots, int slot)
+{
+    __syncthreads();
+    if (threadIdx.x == 0)
+        __hip_atomic_fetch_and(&slots[slot >> 5], ~(1u << (slot & 31)), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <class PT>
+__global__ void __launch_bounds__(PT::NT) acq_correlate_dwell_kernel(const float2* __restrict__ X,
+    const float2* __restrict__ code_fft, RowStat* __restrict__ stats, const float2* __restrict__ tw,
+    typename PT::PlanT plan, AcqParams ap, float* __restrict__ acc_pool, uint32_t* __restrict__ acc_slots,
+    int acc_words)
+{
+    extern __shared__ float2 lds[];
+    RowStat* scratch = reinterpret_cast<RowStat*>(lds + gsdr::fft::lds_elems_dev(plan));
+    const uint32_t N = plan.n;
+    const uint32_t d = blockIdx.x / ap.P, p = blockIdx.x - d * ap.P, b = blockIdx.y;
+    const uint32_t K = ap.dwells;
+    const int slot = K > 1 ? pool_acquire(acc_slots, acc_words) : 0;
+    float* acc = acc_pool + (size_t)slot * ap.eff;
+    const float2* c = code_fft + (size_t)p * N;
+    for (uint32_t k = 0; k < K; ++k)
+        {
+            const float2* x = X + ((size_t)(b * K + k) * ap.D + d) * N;
+            float best = -1.0f, sum = 0.0f;
+            uint32_t bidx = 0xffffffffu;
+            auto load = [&](int i) -> float2 {
+                float2 a = x[i], q = c[i];
+                return make_float2(a.x * q.x + a.y * q.y, a.x * q.y - a.y * q.x);
+            };
+            auto store = [&](int i, float2 v) {
+                const int j = i - (int)ap.out_off;
+                if (j < 0) return;
+                float m = v.x * v.x + v.y * v.y;
+                if (K > 1)
+                    {
+                        if (k > 0) m = acc[j] + m;  // volk_32f_x2_add_32f(grid, grid, tmp)
+                        acc[j] = m;
+                    }
+                if (stat_better(m, (uint32_t)j, best, bidx))
+                    {
+                        best = m;
+                        bidx = (uint32_t)j;
+                    }
+                sum += m;
+            };
+            PT::run(plan, lds, tw, load, store);
+            block_reduce_stat<PT::NT>(best, bidx, sum, scratch);
+            if (threadIdx.x == 0) stats[(((size_t)b * ap.P + p) * K + k) * ap.D + d] = RowStat{best, bidx, sum, 0};
+        }
+    if (K > 1) pool_release(acc_slots, slot);
+}
+
+// One wave per (attempt b, PRN p): the statistic after every dwell k (the grid
+// maximum of the accumulated grid, strict '>' scan order; CFAR input power of row
+// (d*+D/2)%D divided by the dwell counter k+1, pcps_acquisition.cc:533), written to
+// resk[(b*P + p)*K + k]; with CFAR also the decision (first positive dwell, else
+// the last, :781-869) into res[b*P + p] with num_dwells.
+__global__ void __launch_bounds__(64) acq_reduce_dwell_kernel(const RowStat* __restrict__ stats,
+    gsdr_acq_result* __restrict__ resk, gsdr_acq_result* __restrict__ res, const uint32_t* __restrict__ prn_ids,
+    AcqParams ap, uint64_t stamp0, uint64_t block_stride)
+{
+    const uint32_t bp = blockIdx.x;
+    const uint32_t b = bp / ap.P, p = bp - b * ap.P;
+    const uint32_t K = ap.dwells;
+    bool done = false;
+    for (uint32_t k = 0; k < K && !done; ++k)
+        {
+            const RowStat* s = stats + ((size_t)bp * K + k) * ap.D;
+            float m = -1.0f;
+            uint32_t dsel = 0xffffffffu, tsel = 0;
+            for (uint32_t d = threadIdx.x; d < ap.D; d += 64)
+                {
+                    RowStat r = s[d];
+                    if (r.max > m)
+                        {
+                            m = r.max;
+                            dsel = d;
+                            tsel = r.idx;
+                        }
+                }
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1)
+                {
+                    float om = __shfl_xor(m, off);
+                    uint32_t od = __shfl_xor(dsel, off);
+                    uint32_t ot = __shfl_xor(tsel, off);
+                    if (stat_better(om, od, m, dsel))
+                        {
+                            m = om;
+                            dsel = od;
+                            tsel = ot;
+                        }
+                }
+            gsdr_acq_result r;
+            r.prn = prn_ids[p];
+            r.doppler_index = dsel;
+            r.code_phase = tsel;
+            r.doppler_hz = -ap.doppler_max + ap.doppler_center + ap.doppler_step * (int32_t)dsel;
+            r.peak = m;
+            r.second_peak = 0.0f;
+            r.input_power = 0.0f;
+            r.test_statistic = 0.0f;
+            r.acq_delay_samples = (double)fmodf((float)tsel, ap.samples_per_code);
+            r.samplestamp = stamp0 + (uint64_t)(b * K + k) * block_stride;
+            r.positive = 0;
+            r.num_dwells = (int32_t)(k + 1);
+            if (ap.cfar)
+                {
+                    const uint32_t opp = (dsel + ap.D / 2) % ap.D;
+                    const float acc = s[opp].sum;
+                    const float ip = (float)((double)(acc / (float)(int32_t)ap.eff) / 2.0 / (double)(k + 1));
+                    r.input_power = ip;
+                    r.test_statistic = m / ip;
+                    r.positive = r.test_statistic > ap.threshold ? 1 : 0;
+                    done = r.positive || k + 1 == K;
+                    if (done && threadIdx.x == 0) res[bp] = r;
+                }
+            if (threadIdx.x == 0) resk[(size_t)bp * K + k] = r;
+        }
+}
+
+// Peak-ratio statistic per dwell: the accumulated row d*_k over dwells 0..k,
+// maximum outside the exclusion window (as acq_second_peak_kernel).  grid (K, B*P).
+template <class PT>
+__global__ void __launch_bounds__(PT::NT) acq_second_peak_dwell_kernel(const float2* __restrict__ X,
+    const float2* __restrict__ code_fft, gsdr_acq_result* __restrict__ resk, const float2* __restrict__ tw,
+    typename PT::PlanT plan, AcqParams ap, float* __restrict__ acc_pool, uint32_t* __restrict__ acc_slots,
+    int acc_words)
+{
+    extern __shared__ float2 lds[];
+    RowStat* scratch = reinterpret_cast<RowStat*>(lds + gsdr::fft::lds_elems_dev(plan));
+    const uint32_t kk = blockIdx.x, bp = blockIdx.y;
+    const uint32_t K = ap.dwells;
+    const uint32_t b = bp / ap.P, p = bp - b * ap.P;
+    const uint32_t N = plan.n;
+    gsdr_acq_result* rr = resk + (size_t)bp * K + kk;
+    const uint32_t d = rr->doppler_index;
+    const int32_t ti = (int32_t)rr->code_phase;
+    // the reference wraps the exclusion window at d_fft_size even when the rows
+    // hold the effective N/2 outputs (bit transition; :580-590)
+    const int32_t E = (int32_t)ap.N;
+    int32_t e1 = ti - (int32_t)ap.samples_per_chip;
+    int32_t e2 = ti + (int32_t)ap.samples_per_chip;
+    if (e1 < 0)
+        e1 = E + e1;
+    else if (e2 >= E)
+        e2 = e2 - E;
+    const int slot = kk > 0 ? pool_acquire(acc_slots, acc_words) : 0;
+    float* acc = acc_pool + (size_t)slot * ap.eff;
+    const float2* c = code_fft + (size_t)p * N;
+    float best = 0.0f, sum = 0.0f;
+    uint32_t bidx = 0;
+    for (uint32_t k = 0; k <= kk; ++k)
+        {
+            const float2* x = X + ((size_t)(b * K + k) * ap.D + d) * N;
+            const bool last = k == kk;
+            auto load = [&](int i) -> float2 {
+                float2 a = x[i], q = c[i];
+                return make_float2(a.x * q.x + a.y * q.y, a.x * q.y - a.y * q.x);
+            };
+            auto store = [&](int i, float2 v) {
+                const int j = i - (int)ap.out_off;
+                if (j < 0) return;
+                float m = v.x * v.x + v.y * v.y;
+                if (kk > 0)
+                    {
+                        if (k > 0) m = acc[j] + m;
+                        if (!last) acc[j] = m;
+                    }
+                if (last)
+                    {
+                        const bool excluded = (e1 < e2) ? (j >= e1 && j < e2) : (j >= e1 || j < e2);
+                        if (excluded) m = 0.0f;
+                        if (stat_better(m, (uint32_t)j, best, bidx))
+                            {
+                                best = m;
+                                bidx = (uint32_t)j;
+                            }
+                    }
+            };
+            PT::run(plan, lds, tw, load, store);
+        }
+    block_reduce_stat<PT::NT>(best, bidx, sum, scratch);
+    if (threadIdx.x == 0)
+        {
+            gsdr_acq_result r = *rr;
+            r.second_peak = best;
+            r.test_statistic = r.peak / best;
+            r.positive = r.test_statistic > ap.threshold ? 1 : 0;
+            *rr = r;
+        }
+    if (kk > 0) pool_release(acc_slots, slot);
+}
+
+// Peak-ratio decision over the dwells: the first positive dwell, else the last.
+__global__ void acq_decide_kernel(const gsdr_acq_result* __restrict__ resk, gsdr_acq_result* __restrict__ res,
+    uint32_t K, uint32_t n)
+{
+    const uint32_t bp = blockIdx.x * blockDim.x + threadIdx.x;
+    if (bp >= n) return;
+    uint32_t k = 0;
+    while (k + 1 < K && !resk[(size_t)bp * K + k].positive) ++k;
+    res[bp] = resk[(size_t)bp * K + k];
+}
+
 // ---------------------------------------------------------------- K_reduce
 // One wave per (b, p).  Rows are scanned in increasing d by each lane and merged
 // with the (max desc, d asc) order, reproducing the reference's strict '>' scan.
@@ -479,7 +731,7 @@ __global__ void __launch_bounds__(64) acq_reduce_kernel(const RowStat* __restric
     r.acq_delay_samples = (double)fmodf((float)tsel, ap.samples_per_code);
     r.samplestamp = stamp0 + (uint64_t)b * block_stride;
     r.positive = 0;
-    r.reserved = 0;
+    r.num_dwells = 1;
     if (ap.cfar)
         {
             const uint32_t opp = (dsel + ap.D / 2) % ap.D;
@@ -551,6 +803,13 @@ struct gsdr_acq
     int device{0};
     gsdr_acq_conf conf{};
     uint32_t N{0}, D{0}, consumed{0}, lead{0};
+    uint32_t K{1};       // max_dwells
+    uint32_t eff{0};     // effective FFT size (outputs [N - eff, N))
+    bool general{false}; // dwells > 1 or bit transition: the general kernels
+    gsdr_acq_result* d_resk{nullptr};  // per-dwell results (general path)
+    float* d_acc{nullptr};             // pooled |R|^2 accumulation rows (general path)
+    uint32_t* d_acc_slots{nullptr};
+    int acc_words{0};
     float threshold{0.0f};
     int nt{256};
     int variant{0};
@@ -638,6 +897,10 @@ int set_lds_attrs(size_t bytes)
         hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
     GSDR_HIP(hipFuncSetAttribute((const void*)acq_second_peak_kernel<PT>, hipFuncAttributeMaxDynamicSharedMemorySize,
         (int)bytes));
+    GSDR_HIP(hipFuncSetAttribute((const void*)acq_correlate_dwell_kernel<PT>,
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+    GSDR_HIP(hipFuncSetAttribute((const void*)acq_second_peak_dwell_kernel<PT>,
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
     return GSDR_OK;
 }
 
@@ -654,9 +917,11 @@ AcqParams params_of(const gsdr_acq* a)
     ap.doppler_step = (int32_t)a->conf.doppler_step;
     ap.samples_per_code = a->conf.samples_per_code;
     ap.samples_per_chip = a->conf.samples_per_chip;
-    ap.dwells = 1;
+    ap.dwells = a->K;
     ap.threshold = a->threshold;
     ap.cfar = a->conf.pfa > 0.0f ? 1 : 0;
+    ap.eff = a->eff;
+    ap.out_off = a->N - a->eff;
     return ap;
 }
 
@@ -672,10 +937,12 @@ int rebuild_wipeoffs(gsdr_acq* a)
 
 void compute_threshold(gsdr_acq* a)
 {
-    // calculate_threshold, pcps_acquisition.cc:894-909 (dwells == 1, no bit transition)
+    // calculate_threshold, pcps_acquisition.cc:894-909: effective FFT size (N/2
+    // with bit transition) x bins, 2*dwells degrees of freedom (max_dwells is 1
+    // with bit transition)
     const float pfa = a->conf.pfa;
     if (pfa <= 0.0f) return;
-    const int num_bins = (int)(a->N * a->D);
+    const int num_bins = (int)(a->eff * a->D);
     const double p = std::pow(1.0 - (double)pfa, 1.0 / (double)(float)num_bins);
     a->threshold = (float)(2.0 * gsdr::gamma_p_inv_int(2 * (int)a->conf.max_dwells, p));
 }
@@ -804,12 +1071,51 @@ void launch_forward(gsdr_acq* a, const void* iq, int item_type, uint32_t nblocks
             a->lds_bytes, s, iq, stride, a->d_wipe, a->d_X, a->d_tw, plan_of<PT>(a), a->consumed, a->D);
 }
 
+// General path (max_dwells > 1 and/or bit_transition_flag): forward spectra of
+// all nblocks*K blocks, the dwell-accumulating correlate kernel, per-dwell
+// statistics and the dwell decision.
+template <class PT>
+int launch_general(gsdr_acq* a, const void* iq, int item_type, uint32_t nblocks, uint64_t stride, uint64_t stamp0,
+    gsdr_acq_result* res, hipStream_t s, StageTimer& t)
+{
+    const size_t lds = a->lds_bytes;
+    const uint32_t K = a->K;
+    t.begin();
+    launch_forward<PT>(a, iq, item_type, nblocks * K, stride, s);
+    GSDR_HIP(hipGetLastError());
+    t.end(0);
+    AcqParams ap = params_of(a);
+    t.begin();
+    hipLaunchKernelGGL((acq_correlate_dwell_kernel<PT>), dim3(a->D * a->nprn, nblocks), dim3(PT::NT), lds, s, a->d_X,
+        a->d_code_fft, a->d_stats, a->d_tw, plan_of<PT>(a), ap, a->d_acc, a->d_acc_slots, a->acc_words);
+    GSDR_HIP(hipGetLastError());
+    t.end(1);
+    t.begin();
+    hipLaunchKernelGGL(acq_reduce_dwell_kernel, dim3(nblocks * a->nprn), dim3(64), 0, s, a->d_stats, a->d_resk, res,
+        a->d_prn, ap, stamp0, stride);
+    GSDR_HIP(hipGetLastError());
+    t.end(2);
+    if (!ap.cfar)
+        {
+            t.begin();
+            hipLaunchKernelGGL((acq_second_peak_dwell_kernel<PT>), dim3(K, nblocks * a->nprn), dim3(PT::NT), lds, s,
+                a->d_X, a->d_code_fft, a->d_resk, a->d_tw, plan_of<PT>(a), ap, a->d_acc, a->d_acc_slots,
+                a->acc_words);
+            const uint32_t n = nblocks * a->nprn;
+            hipLaunchKernelGGL(acq_decide_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a->d_resk, res, K, n);
+            GSDR_HIP(hipGetLastError());
+            t.end(3);
+        }
+    return GSDR_OK;
+}
+
 template <class PT>
 int launch_all(gsdr_acq* a, const void* iq, int item_type, uint32_t nblocks, uint64_t stride, uint64_t stamp0,
     gsdr_acq_result* res, hipStream_t s)
 {
     const size_t lds = a->lds_bytes;
     StageTimer t(a, s);
+    if (a->general) return launch_general<PT>(a, iq, item_type, nblocks, stride, stamp0, res, s, t);
     t.begin();
     launch_forward<PT>(a, iq, item_type, nblocks, stride, s);
     GSDR_HIP(hipGetLastError());
@@ -967,8 +1273,6 @@ int gsdr_acq_create(int device, const gsdr_acq_conf* conf, gsdr_acq** out)
         "gsdr_acq_create: unknown item type %d", conf->item_type);
     GSDR_REQUIRE(conf->max_prns > 0 && conf->max_blocks > 0, GSDR_E_ARG, "gsdr_acq_create: capacities must be > 0");
     GSDR_REQUIRE(conf->pfa >= 0.0f && conf->pfa <= 1.0f, GSDR_E_ARG, "gsdr_acq_create: pfa outside [0,1]");
-    GSDR_REQUIRE(conf->max_dwells <= 1, GSDR_E_UNSUPPORTED, "gsdr_acq_create: max_dwells > 1 not implemented yet");
-    GSDR_REQUIRE(conf->bit_transition_flag == 0, GSDR_E_UNSUPPORTED, "gsdr_acq_create: bit_transition_flag not implemented yet");
     int ndev = 0;
     GSDR_HIP(hipGetDeviceCount(&ndev));
     GSDR_REQUIRE(device >= 0 && device < ndev, GSDR_E_ARG, "gsdr_acq_create: device %d of %d", device, ndev);
@@ -979,6 +1283,10 @@ int gsdr_acq_create(int device, const gsdr_acq_conf* conf, gsdr_acq** out)
     a->device = device;
     a->conf = *conf;
     if (a->conf.max_dwells == 0) a->conf.max_dwells = 1;
+    // bit transition: every call decides on its own (the dwell counter is reset,
+    // pcps_acquisition.cc:871-879) and the threshold uses one dwell (:908)
+    if (a->conf.bit_transition_flag) a->conf.max_dwells = 1;
+    a->K = a->conf.max_dwells;
     a->consumed = conf->consumed_samples;
     // pcps_acquisition.cc:85-92
     uint32_t N = conf->fft_size;
@@ -991,6 +1299,19 @@ int gsdr_acq_create(int device, const gsdr_acq_conf* conf, gsdr_acq** out)
         }
     a->N = N;
     a->lead = N - a->consumed;
+    a->eff = N;
+    if (conf->bit_transition_flag)
+        {
+            if (N % 2 != 0)
+                {
+                    delete a;
+                    gsdr::set_error("gsdr_acq_create: bit_transition_flag needs an even fft_size (%u)", N);
+                    return GSDR_E_ARG;
+                }
+            a->lead = N / 2;
+            a->eff = N / 2;
+        }
+    a->general = a->K > 1 || conf->bit_transition_flag;
     a->D = conf->num_doppler_bins;
     if (a->D == 0)
         a->D = (uint32_t)std::ceil((double)(conf->doppler_max - (-conf->doppler_max)) / (double)conf->doppler_step);
@@ -1011,7 +1332,7 @@ int gsdr_acq_create(int device, const gsdr_acq_conf* conf, gsdr_acq** out)
             return GSDR_E_UNSUPPORTED;
         }
     int rc = dispatch(a, 4, nullptr, 0, 0, 0, nullptr, nullptr, 0);
-    if (rc == GSDR_OK && N == 4000)
+    if (rc == GSDR_OK && N == 4000 && !a->general)
         {
             int v = kDefaultCorrVariant4000;
             if (const char* e = std::getenv("GSDR_ACQ_CORR_VARIANT")) v = std::atoi(e);
@@ -1029,10 +1350,21 @@ int gsdr_acq_create(int device, const gsdr_acq_conf* conf, gsdr_acq** out)
     if (e == hipSuccess) e = hipMalloc(&a->d_code_fft, nP * N * sizeof(float2));
     if (e == hipSuccess) e = hipMalloc(&a->d_code_stage, nP * a->consumed * sizeof(float2));
     if (e == hipSuccess) e = hipMalloc(&a->d_prn, nP * sizeof(uint32_t));
-    if (e == hipSuccess) e = hipMalloc(&a->d_X, nB * a->D * N * sizeof(float2));
-    if (e == hipSuccess) e = hipMalloc(&a->d_stats, nB * nP * a->D * sizeof(RowStat));
+    if (e == hipSuccess) e = hipMalloc(&a->d_X, nB * a->K * a->D * N * sizeof(float2));
+    if (e == hipSuccess) e = hipMalloc(&a->d_stats, nB * nP * a->K * a->D * sizeof(RowStat));
     if (e == hipSuccess) e = hipMalloc(&a->d_res, nB * nP * sizeof(gsdr_acq_result));
-    if (e == hipSuccess) e = hipMalloc(&a->d_iq, nB * a->consumed * item_bytes(conf->item_type));
+    if (e == hipSuccess) e = hipMalloc(&a->d_iq, nB * a->K * a->consumed * item_bytes(conf->item_type));
+    if (a->general)
+        {
+            // accumulation rows held by running workgroups only: the chip's resident
+            // workgroup count bounds the pool
+            const int nslots = 256 * 32 / (a->nt / 64);
+            a->acc_words = (nslots + 31) / 32;
+            if (e == hipSuccess) e = hipMalloc(&a->d_resk, nB * nP * a->K * sizeof(gsdr_acq_result));
+            if (e == hipSuccess) e = hipMalloc(&a->d_acc, (size_t)a->acc_words * 32 * a->eff * sizeof(float));
+            if (e == hipSuccess) e = hipMalloc(&a->d_acc_slots, (size_t)a->acc_words * sizeof(uint32_t));
+            if (e == hipSuccess) e = hipMemset(a->d_acc_slots, 0, (size_t)a->acc_words * sizeof(uint32_t));
+        }
     if (e == hipSuccess) e = hipMalloc(&a->d_grid, (size_t)a->D * N * sizeof(float));
     if (four)
         {
@@ -1103,7 +1435,7 @@ void gsdr_acq_destroy(gsdr_acq* a)
         }
     for (hipEvent_t e : a->prof_pool) (void)hipEventDestroy(e);
     void* bufs[] = {a->d_tw, a->d_wipe, a->d_code_fft, a->d_code_stage, a->d_prn, a->d_X, a->d_stats, a->d_res,
-        a->d_iq, a->d_grid, a->d_tw_sub, a->d_scratch, a->d_slots};
+        a->d_iq, a->d_grid, a->d_tw_sub, a->d_scratch, a->d_slots, a->d_resk, a->d_acc, a->d_acc_slots};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     if (a->stream) (void)hipStreamDestroy(a->stream);
@@ -1189,7 +1521,7 @@ int gsdr_acq_run(gsdr_acq* a, const void* iq_host, uint32_t nblocks, uint64_t st
         nblocks, a->conf.max_blocks);
     std::lock_guard<std::mutex> lk(a->mu);
     gsdr::DeviceGuard g(a->device);
-    const size_t bytes = (size_t)nblocks * a->consumed * item_bytes(a->conf.item_type);
+    const size_t bytes = (size_t)nblocks * a->K * a->consumed * item_bytes(a->conf.item_type);
     GSDR_HIP(hipMemcpyAsync(a->d_iq, iq_host, bytes, hipMemcpyHostToDevice, a->stream));
     int rc = dispatch(a, 0, a->d_iq, nblocks, a->consumed, stamp0, a->d_res, a->stream, 0);
     if (rc != GSDR_OK) return rc;

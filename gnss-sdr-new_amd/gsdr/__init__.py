@@ -106,7 +106,7 @@ class AcqResult(ctypes.Structure):
         ("acq_delay_samples", ctypes.c_double),
         ("samplestamp", ctypes.c_uint64),
         ("positive", ctypes.c_int32),
-        ("reserved", ctypes.c_int32),
+        ("num_dwells", ctypes.c_int32),
     ]
 
 
@@ -114,7 +114,7 @@ ACQ_RESULT_DTYPE = np.dtype([
     ("prn", np.uint32), ("doppler_index", np.uint32), ("code_phase", np.uint32), ("doppler_hz", np.int32),
     ("peak", np.float32), ("input_power", np.float32), ("second_peak", np.float32),
     ("test_statistic", np.float32), ("acq_delay_samples", np.float64), ("samplestamp", np.uint64),
-    ("positive", np.int32), ("reserved", np.int32)])
+    ("positive", np.int32), ("num_dwells", np.int32)])
 assert ACQ_RESULT_DTYPE.itemsize == ctypes.sizeof(AcqResult)
 
 
@@ -224,7 +224,7 @@ class Acquisition:
     def __init__(self, fs_in, consumed_samples, doppler_max, doppler_step, pfa=0.0, max_prns=32, max_blocks=1,
                  samples_per_code=None, samples_per_chip=None, num_doppler_bins=0, doppler_center=0,
                  doppler_bias=0, item_type=ITEM_GR_COMPLEX, fft_size=0, sampled_ms=1, ms_per_code=1,
-                 chip_rate=1023000.0, device=0):
+                 chip_rate=1023000.0, max_dwells=1, bit_transition=False, device=0):
         L = load()
         c = AcqConf()
         c.fs_in = int(fs_in)
@@ -240,8 +240,8 @@ class Acquisition:
         c.doppler_bias = int(doppler_bias)
         c.num_doppler_bins = int(num_doppler_bins)
         c.pfa = float(pfa)
-        c.max_dwells = 1
-        c.bit_transition_flag = 0
+        c.max_dwells = int(max_dwells)
+        c.bit_transition_flag = int(bool(bit_transition))
         c.item_type = int(item_type)
         c.max_prns = int(max_prns)
         c.max_blocks = int(max_blocks)
@@ -255,6 +255,7 @@ class Acquisition:
         self.num_doppler_bins, self.fft_size = D.value, N.value
         self.nprn = 0
         self.item_type = item_type
+        self.dwells = 1 if bit_transition else max(1, int(max_dwells))
 
     def close(self):
         if self._h:
@@ -292,7 +293,8 @@ class Acquisition:
         return np.ascontiguousarray(iq, np.complex64)
 
     def run(self, iq, nblocks=1, stamp0=0):
-        """Synchronous drop-in: host IQ of nblocks*consumed items -> structured array [nblocks, nprn]."""
+        """Synchronous drop-in: host IQ of nblocks*max_dwells*consumed items (nblocks
+        attempts of max_dwells blocks) -> structured array [nblocks, nprn]."""
         iq = self._items(iq)
         out = np.zeros(nblocks * self.nprn, ACQ_RESULT_DTYPE)
         _check(load().gsdr_acq_run(self._h, _ptr(iq), int(nblocks), int(stamp0), _ptr(out)))

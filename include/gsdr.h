@@ -82,8 +82,8 @@ typedef struct gsdr_acq_conf
     int32_t doppler_bias;         /* [Hz] FDMA bias (is_fdma, pcps_acquisition.cc:212-230) */
     uint32_t num_doppler_bins;    /* 0 -> ceil(2*doppler_max/doppler_step)            (pcps_acquisition.cc:264) */
     float pfa;                    /* > 0: CFAR max/input-power statistic; == 0: first/second peak */
-    uint32_t max_dwells;          /* only 1 is implemented in this version */
-    int32_t bit_transition_flag;  /* only 0 is implemented in this version */
+    uint32_t max_dwells;          /* non-coherent dwells per acquisition attempt (forced to 1 with bit_transition_flag) */
+    int32_t bit_transition_flag;  /* consumed = 2 x sampled span, code in the second half, outputs [N/2, N) */
     int32_t item_type;            /* GSDR_ITEM_* */
     uint32_t max_prns;            /* capacity: PRNs per batch */
     uint32_t max_blocks;          /* capacity: blocks per call */
@@ -106,7 +106,7 @@ typedef struct gsdr_acq_result
     double acq_delay_samples; /* Acq_delay_samples = fmod(indext, samples_per_code) */
     uint64_t samplestamp;     /* Acq_samplestamp_samples */
     int32_t positive;         /* test_statistic > threshold */
-    int32_t reserved;
+    int32_t num_dwells;       /* dwells integrated when the decision was taken (1..max_dwells) */
 } gsdr_acq_result;
 
 int gsdr_acq_create(int device, const gsdr_acq_conf* conf, gsdr_acq** out);
@@ -130,13 +130,17 @@ int gsdr_acq_set_doppler(gsdr_acq* acq, int32_t doppler_max, uint32_t doppler_st
 int gsdr_acq_set_threshold(gsdr_acq* acq, float threshold);
 int gsdr_acq_get_threshold(const gsdr_acq* acq, float* threshold);
 
-/* Synchronous drop-in: nblocks consecutive blocks of consumed_samples items
- * (item_type) from host memory; block i has sample stamp stamp0 + i*consumed.
- * out: nblocks*nprn results, block-major (host). */
+/* Synchronous drop-in: nblocks acquisition attempts over consecutive blocks of
+ * consumed_samples items (item_type) from host memory.  Attempt i integrates up
+ * to max_dwells blocks (block j = i*max_dwells + k for dwell k, sample stamp
+ * stamp0 + j*consumed) and reports, per PRN, the first dwell whose statistic
+ * crosses the threshold or else the last (acquisition_core's dwell loop,
+ * pcps_acquisition.cc:781-869); with max_dwells = 1 an attempt is one block.
+ * out: nblocks*nprn results, attempt-major (host). */
 int gsdr_acq_run(gsdr_acq* acq, const void* iq_host, uint32_t nblocks, uint64_t stamp0, gsdr_acq_result* out);
 
-/* Device-resident form: iq_dev holds nblocks blocks, block i starting at item
- * i*block_stride_items.  Results are written to out_dev (device memory,
+/* Device-resident form: iq_dev holds nblocks*max_dwells blocks, block j starting
+ * at item j*block_stride_items.  Results are written to out_dev (device memory,
  * nblocks*nprn).  Asynchronous on stream; no host synchronisation. */
 int gsdr_acq_run_device(gsdr_acq* acq, const void* iq_dev, uint32_t nblocks, uint64_t block_stride_items,
     uint64_t stamp0, gsdr_acq_result* out_dev, void* stream);

@@ -1,0 +1,1109 @@
+// Shared implementation of the PCPS acquisition engine (see acq.hip for the
+// kernel map): kernels, the handle, launch templates.  Included by acq.hip (ABI)
+// and by the variant translation units that instantiate the launch templates per
+// FFT plan type, so the plan groups compile in parallel.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <type_traits>
+#include <new>
+#include <vector>
+
+#include "fft_4step.h"
+#include "fft_lds.h"
+#include "fft_multi.h"
+#include "fft_pk.h"
+#include "fft_plan.h"
+#include "gsdr_internal.h"
+
+namespace
+{
+
+using gsdr::fft::Plan;
+
+// Default correlate variant at N = 4000 (see GSDR_PK_VARIANTS).
+constexpr int kDefaultCorrVariant4000 = 35;
+
+struct RowStat
+{
+    float max;
+    uint32_t idx;
+    float sum;
+    uint32_t pad;
+};
+
+struct AcqParams
+{
+    uint32_t N;          // fft size
+    uint32_t consumed;   // valid samples per block
+    uint32_t lead_zeros; // zero samples placed before the code (sampled_ms != ms_per_code)
+    uint32_t D;
+    uint32_t P;
+    int32_t doppler_max;
+    int32_t doppler_center;
+    int32_t doppler_step;
+    float samples_per_code;
+    uint32_t samples_per_chip;
+    uint32_t dwells;      // max_dwells K (non-coherent dwells per acquisition attempt)
+    float threshold;
+    int32_t cfar;
+    uint32_t eff;         // effective FFT size (N/2 with bit_transition_flag, else N)
+    uint32_t out_off;     // first output index of the effective window (N - eff)
+};
+
+template <int IT>
+__device__ __forceinline__ float2 load_item(const void* __restrict__ p, size_t i)
+{
+    if constexpr (IT == GSDR_ITEM_GR_COMPLEX)
+        {
+            return reinterpret_cast<const float2*>(p)[i];
+        }
+    else
+        {
+            short2 s = reinterpret_cast<const short2*>(p)[i];
+            return make_float2((float)s.x, (float)s.y);
+        }
+}
+
+__device__ __forceinline__ bool stat_better(float am, uint32_t ai, float bm, uint32_t bi)
+{
+    return am > bm || (am == bm && ai < bi);
+}
+
+// Block-wide (max, first argmax, sum) reduction; result valid in thread 0.
+template <int NT>
+__device__ __forceinline__ void block_reduce_stat(float& m, uint32_t& idx, float& sum, RowStat* scratch)
+{
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1)
+        {
+            float om = __shfl_xor(m, off);
+            uint32_t oi = __shfl_xor(idx, off);
+            float os = __shfl_xor(sum, off);
+            if (stat_better(om, oi, m, idx))
+                {
+                    m = om;
+                    idx = oi;
+                }
+            sum += os;
+        }
+    constexpr int NW = NT / 64;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (NW > 1)
+        {
+            if (lane == 0) scratch[wave] = RowStat{m, idx, sum, 0};
+            __syncthreads();
+            if (threadIdx.x == 0)
+                {
+                    for (int w = 1; w < NW; ++w)
+                        {
+                            RowStat s = scratch[w];
+                            if (stat_better(s.max, s.idx, m, idx))
+                                {
+                                    m = s.max;
+                                    idx = s.idx;
+                                }
+                            sum += s.sum;
+                        }
+                }
+        }
+}
+
+// ---------------------------------------------------------------- K_wipe
+// One workgroup per Doppler bin.  Lane 0 replays the generic sincos phase
+// accumulation (KERN/s32f_sincos_32fc.h:390-403) sequentially in fp32; the
+// workgroup then evaluates cos/sin in parallel.
+__global__ void __launch_bounds__(256) acq_wipeoff_kernel(float2* __restrict__ wipe, uint32_t N, float fs,
+    int32_t doppler_max, int32_t doppler_center, int32_t doppler_step, int32_t doppler_bias)
+{
+    const uint32_t d = blockIdx.x;
+    float2* row = wipe + (size_t)d * N;
+    if (threadIdx.x == 0)
+        {
+            const int32_t doppler = -doppler_max + doppler_center + doppler_step * (int32_t)d;
+            const float freq = (float)(doppler_bias + doppler);
+            const float phase_step = __fdiv_rn(__fmul_rn(6.283185307179586f, freq), fs);
+            const float inc = -phase_step;
+            float ph = 0.0f;
+            for (uint32_t i = 0; i < N; ++i)
+                {
+                    row[i].x = ph;
+                    ph = __fadd_rn(ph, inc);
+                }
+        }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < N; i += blockDim.x)
+        {
+            float s, c;
+            sincosf(row[i].x, &s, &c);
+            row[i] = make_float2(c, s);
+        }
+}
+
+// ---------------------------------------------------------------- K_code
+template <class PT>
+__global__ void __launch_bounds__(PT::NT) acq_code_fft_kernel(const float2* __restrict__ codes,
+    float2* __restrict__ code_fft, const float2* __restrict__ tw, typename PT::PlanT plan, uint32_t consumed, uint32_t lead)
+{
+    // set_local_code (pcps_acquisition.cc:176-209): [0 x lead, code[0 .. N - lead)];
+    // lead = N - consumed, or N/2 with bit_transition_flag (then only the first N/2
+    // code samples of the consumed-long row are used)
+    extern __shared__ float2 lds[];
+    const uint32_t p = blockIdx.x;
+    const float2* c = codes + (size_t)p * consumed;
+    float2* out = code_fft + (size_t)p * plan.n;
+    const int valid = (int)plan.n - (int)lead;
+    auto load = [&](int i) -> float2 {
+        int k = i - (int)lead;
+        return (k >= 0 && k < valid) ? c[k] : make_float2(0.f, 0.f);
+    };
+    auto store = [&](int i, float2 v) { out[i] = v; };
+    PT::run(plan, lds, tw, load, store);
+}
+
+// ---------------------------------------------------------------- K_forward
+template <class PT, int IT>
+__global__ void __launch_bounds__(PT::NT) acq_forward_kernel(const void* __restrict__ iq, uint64_t block_stride,
+    const float2* __restrict__ wipe, float2* __restrict__ X, const float2* __restrict__ tw, typename PT::PlanT plan,
+    uint32_t consumed, uint32_t D)
+{
+    extern __shared__ float2 lds[];
+    const uint32_t d = blockIdx.x, b = blockIdx.y;
+    const size_t base = (size_t)b * block_stride;
+    const float2* w = wipe + (size_t)d * plan.n;
+    float2* out = X + ((size_t)b * D + d) * plan.n;
+    auto load = [&](int i) -> float2 {
+        if (i >= (int)consumed) return make_float2(0.f, 0.f);
+        return gsdr::fft::cmul(load_item<IT>(iq, base + i), w[i]);
+    };
+    auto store = [&](int i, float2 v) { out[i] = v; };
+    PT::run(plan, lds, tw, load, store);
+}
+
+// ---------------------------------------------------------------- K_correlate
+// blockIdx.x = d*P + p (consecutive workgroups share the spectrum X_{b,d}), blockIdx.y = b.
+// GRID: also write the full |R|^2 row (the reference's grid dump).
+template <class PT, bool GRID>
+__global__ void __launch_bounds__(PT::NT) acq_correlate_kernel(const float2* __restrict__ X,
+    const float2* __restrict__ code_fft, RowStat* __restrict__ stats, float* __restrict__ grid,
+    const float2* __restrict__ tw, typename PT::PlanT plan, uint32_t D, uint32_t P, uint32_t prn_slot_for_grid)
+{
+    extern __shared__ float2 lds[];
+    RowStat* scratch = reinterpret_cast<RowStat*>(lds + gsdr::fft::lds_elems_dev(plan));
+    const uint32_t N = plan.n;
+    uint32_t d, p, b;
+    if (GRID)
+        {
+            d = blockIdx.x;
+            p = prn_slot_for_grid;
+            b = blockIdx.y;
+        }
+    else
+        {
+            // XCD-aware mapping (cdna_hip_programming.md T1): workgroups are dealt
+            // round-robin over the 8 XCDs (id % 8), so give all P workgroups of one
+            // (b, d) spectrum the same id % 8 — X_{b,d} is then fetched into one
+            // XCD's L2 once instead of into all eight.  Speed only, never correctness.
+            const uint32_t nrows = gridDim.y * D;  // (b, d) rows
+            const uint32_t id = blockIdx.y * gridDim.x + blockIdx.x;
+            const uint32_t full = nrows >> 3;     // rows in the XCD-balanced part
+            uint32_t row;
+            if (id < full * 8u * P)
+                {
+                    const uint32_t xcd = id & 7u, slot = id >> 3;
+                    row = (slot / P) * 8u + xcd;
+                    p = slot - (slot / P) * P;
+                }
+            else
+                {
+                    const uint32_t t = id - full * 8u * P;  // the last nrows % 8 rows, linear
+                    row = full * 8u + t / P;
+                    p = t - (t / P) * P;
+                }
+            b = row / D;
+            d = row - b * D;
+        }
+    const float2* x = X + ((size_t)b * D + d) * N;
+    const float2* c = code_fft + (size_t)p * N;
+    float best = -1.0f, sum = 0.0f;
+    uint32_t bidx = 0xffffffffu;
+    // conj(X . conj(C)) = conj(X) . C ; |IFFT(Y)| = |FFT(conj(Y))|
+    auto load = [&](int i) -> float2 {
+        float2 a = x[i], k = c[i];
+        return make_float2(a.x * k.x + a.y * k.y, a.x * k.y - a.y * k.x);
+    };
+    auto store = [&](int i, float2 v) {
+        const float m = v.x * v.x + v.y * v.y;
+        if (GRID) grid[(size_t)d * N + i] = m;
+        if (stat_better(m, (uint32_t)i, best, bidx))
+            {
+                best = m;
+                bidx = (uint32_t)i;
+            }
+        sum += m;
+    };
+    PT::run(plan, lds, tw, load, store);
+    if (!GRID)
+        {
+            block_reduce_stat<PT::NT>(best, bidx, sum, scratch);
+            if (threadIdx.x == 0) stats[((size_t)b * P + p) * D + d] = RowStat{best, bidx, sum, 0};
+        }
+}
+
+// ---------------------------------------------------------------- K_correlate (packed f32)
+// The sequential-PRN-group kernel on the packed-f32 FFT (fft_pk.h): one workgroup
+// per (row = b*D + d, group of PG PRNs), XCD-aware; the lane's first-stage inputs
+// of X_{b,d} stay in VGPRs for the whole group and the next PRN's code-spectrum
+// values are fetched by the hook while the current transform runs.  The last
+// stage visits each lane's outputs in increasing index order, so a strict '>'
+// keeps the lane's first maximum (the reference's index_max semantics).
+template <class MP, int PG, int WPE>
+__global__ void __launch_bounds__(MP::NT) __attribute__((amdgpu_waves_per_eu(WPE))) acq_correlate_pk_kernel(const float2* __restrict__ X,
+    const float2* __restrict__ code_fft, RowStat* __restrict__ stats, const float2* __restrict__ tw, uint32_t D,
+    uint32_t P, uint32_t nblocks)
+{
+    using gsdr::pk::c2;
+    constexpr int NT = MP::NT;
+    constexpr int NW = NT / 64;
+    constexpr int R1 = MP::R1, BPT1 = MP::BPT1, NB1 = MP::NB1;
+    constexpr uint32_t N = MP::N;
+    extern __shared__ float2 lds_raw[];
+    c2* lds = reinterpret_cast<c2*>(lds_raw);
+    RowStat* scratch = reinterpret_cast<RowStat*>(lds_raw + N);
+    const uint32_t G = (P + PG - 1) / PG;
+    const uint32_t nrows = nblocks * D;
+    const uint32_t id = blockIdx.x;
+    const uint32_t full = nrows >> 3;
+    uint32_t row, g;
+    if (id < full * 8u * G)
+        {
+            const uint32_t xcd = id & 7u, slot = id >> 3;
+            row = (slot / G) * 8u + xcd;
+            g = slot - (slot / G) * G;
+        }
+    else
+        {
+            const uint32_t t = id - full * 8u * G;
+            row = full * 8u + t / G;
+            g = t - (t / G) * G;
+        }
+    const uint32_t b = row / D, d = row - (row / D) * D;
+    const uint32_t p0 = g * PG;
+    const int np = (int)min((uint32_t)PG, P - p0);
+    const c2* x = reinterpret_cast<const c2*>(X) + (size_t)row * N;
+    c2 xr[BPT1][R1], cr[BPT1][R1];
+    {
+        const c2* c = reinterpret_cast<const c2*>(code_fft) + (size_t)p0 * N;
+#pragma unroll
+        for (int bb = 0; bb < BPT1; ++bb)
+            {
+                const int j = (int)threadIdx.x + bb * NT;
+                if (NB1 % NT == 0 || j < NB1)
+                    {
+#pragma unroll
+                        for (int r = 0; r < R1; ++r)
+                            {
+                                xr[bb][r] = x[j + r * NB1];
+                                cr[bb][r] = c[j + r * NB1];
+                            }
+                    }
+            }
+    }
+    for (int q = 0; q < np; ++q)
+        {
+            float best = -1.0f, sum = 0.0f;
+            uint32_t bidx = 0xffffffffu;
+            // conj(X . conj(C)) = conj(X) . C ; |IFFT(Y)| = |FFT(conj(Y))|
+            auto load = [&](int bb, int r, int) -> c2 { return gsdr::pk::conj_mul(xr[bb][r], cr[bb][r]); };
+            auto hook = [&]() {
+                if (q + 1 < np)
+                    {
+                        const c2* c = reinterpret_cast<const c2*>(code_fft) + (size_t)(p0 + q + 1) * N;
+#pragma unroll
+                        for (int bb = 0; bb < BPT1; ++bb)
+                            {
+                                const int j = (int)threadIdx.x + bb * NT;
+                                if (NB1 % NT == 0 || j < NB1)
+                                    {
+#pragma unroll
+                                        for (int r = 0; r < R1; ++r) cr[bb][r] = c[j + r * NB1];
+                                    }
+                            }
+                    }
+            };
+            auto store = [&](int i, c2 v) {
+                const float m = __builtin_fmaf(v.x, v.x, v.y * v.y);
+                if (m > best)
+                    {
+                        best = m;
+                        bidx = (uint32_t)i;
+                    }
+                sum += m;
+            };
+            MP::run(lds, tw, load, store, hook);
+            block_reduce_stat<NT>(best, bidx, sum, scratch + (q & 1) * NW);
+            if (threadIdx.x == 0) stats[((size_t)b * P + p0 + q) * D + d] = RowStat{best, bidx, sum, 0};
+        }
+}
+
+// ---------------------------------------------------------------- K_correlate (packed f32, multi-transform)
+// PB PRNs of one row (b, d) per workgroup, transformed together on the packed
+// multi-transform plan (fft_pk.h PkMultiPlan), whose butterfly packing keeps the
+// waves full; one XCD-aware 1-D grid over (row, PRN group) as above.
+template <class MP, int WPE>
+__global__ void __launch_bounds__(MP::NT) __attribute__((amdgpu_waves_per_eu(WPE))) acq_correlate_pkm_kernel(
+    const float2* __restrict__ X, const float2* __restrict__ code_fft, RowStat* __restrict__ stats,
+    const float2* __restrict__ tw, uint32_t D, uint32_t P, uint32_t nblocks)
+{
+    using gsdr::pk::c2;
+    constexpr int NT = MP::NT;
+    constexpr int NW = NT / 64;
+    constexpr int PB = MP::PB;
+    constexpr uint32_t N = MP::N;
+    extern __shared__ float2 lds_raw[];
+    c2* lds = reinterpret_cast<c2*>(lds_raw);
+    RowStat* scratch = reinterpret_cast<RowStat*>(lds_raw + (size_t)PB * MP::STRIDE);
+    const uint32_t G = (P + PB - 1) / PB;
+    const uint32_t nrows = nblocks * D;
+    const uint32_t id = blockIdx.x;
+    const uint32_t full = nrows >> 3;
+    uint32_t row, g;
+    if (id < full * 8u * G)
+        {
+            const uint32_t xcd = id & 7u, slot = id >> 3;
+            row = (slot / G) * 8u + xcd;
+            g = slot - (slot / G) * G;
+        }
+    else
+        {
+            const uint32_t t = id - full * 8u * G;
+            row = full * 8u + t / G;
+            g = t - (t / G) * G;
+        }
+    const uint32_t b = row / D, d = row - (row / D) * D;
+    const uint32_t p0 = g * PB;
+    const int np = (int)min((uint32_t)PB, P - p0);
+    const c2* x = reinterpret_cast<const c2*>(X) + (size_t)row * N;
+    const c2* cb = reinterpret_cast<const c2*>(code_fft) + (size_t)p0 * N;
+    float best[PB], sum[PB];
+    uint32_t bidx[PB];
+#pragma unroll
+    for (int t = 0; t < PB; ++t)
+        {
+            best[t] = -1.0f;
+            sum[t] = 0.0f;
+            bidx[t] = 0xffffffffu;
+        }
+    // conj(X . conj(C)) = conj(X) . C ; |IFFT(Y)| = |FFT(conj(Y))|.  A partial last
+    // group repeats its last PRN in the idle transforms (results discarded).
+    auto load = [&](int t, int, int i) -> c2 {
+        const int tc = PB == 1 ? 0 : min(t, np - 1);
+        return gsdr::pk::conj_mul(x[i], cb[(size_t)tc * N + i]);
+    };
+    auto store = [&](auto T, int i, c2 v) {
+        constexpr int t = decltype(T)::value;
+        const float m = __builtin_fmaf(v.x, v.x, v.y * v.y);
+        if (m > best[t])
+            {
+                best[t] = m;
+                bidx[t] = (uint32_t)i;
+            }
+        sum[t] += m;
+    };
+    MP::run(lds, tw, load, store);
+#pragma unroll
+    for (int t = 0; t < PB; ++t) block_reduce_stat<NT>(best[t], bidx[t], sum[t], scratch + t * NW);
+    if (threadIdx.x == 0)
+        {
+#pragma unroll
+            for (int t = 0; t < PB; ++t)
+                if (t < np) stats[((size_t)b * P + p0 + t) * D + d] = RowStat{best[t], bidx[t], sum[t], 0};
+        }
+}
+
+// ---------------------------------------------------------------- general path (dwells, bit transition)
+// acquisition_core with max_dwells K > 1 (non-coherent accumulation of |R|^2 over
+// K consecutive blocks, pcps_acquisition.cc:667-675) and/or bit_transition_flag
+// (outputs [N/2, N) of each transform, :671).  One workgroup per (attempt b, d, p)
+// runs the K transforms of dwells k = 0..K-1 (blocks b*K + k); each lane adds |R|^2
+// into its own entries of a pooled global row (every plan maps an output index to
+// the same lane in every transform, so no synchronisation is needed) and row
+// statistics of the accumulated grid are emitted after every dwell:
+// stats[((b*P + p)*K + k)*D + d].
+__device__ __forceinline__ int pool_acquire(uint32_t* slots, int nwords)
+{
+    __shared__ int s_slot;
+    if (threadIdx.x == 0)
+        {
+            int w = (int)((blockIdx.x + blockIdx.y * gridDim.x) % (unsigned)nwords);
+            for (;;)
+                {
+                    const uint32_t cur = __hip_atomic_load(&slots[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (cur != 0xffffffffu)
+                        {
+                            const int bit = __builtin_ctz(~cur);
+                            const uint32_t old =
+                                __hip_atomic_fetch_or(&slots[w], 1u << bit, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                            if (!(old & (1u << bit)))
+                                {
+                                    s_slot = w * 32 + bit;
+                                    break;
+                                }
+                        }
+                    else
+                        {
+                            w = w + 1 == nwords ? 0 : w + 1;
+                            __builtin_amdgcn_s_sleep(2);
+                        }
+                }
+        }
+    __syncthreads();
+    return s_slot;
+}
+
+__device__ __forceinline__ void pool_release(uint32_t* slots, int slot)
+{
+    __syncthreads();
+    if (threadIdx.x == 0)
+        __hip_atomic_fetch_and(&slots[slot >> 5], ~(1u << (slot & 31)), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <class PT>
+__global__ void __launch_bounds__(PT::NT) acq_correlate_dwell_kernel(const float2* __restrict__ X,
+    const float2* __restrict__ code_fft, RowStat* __restrict__ stats, const float2* __restrict__ tw,
+    typename PT::PlanT plan, AcqParams ap, float* __restrict__ acc_pool, uint32_t* __restrict__ acc_slots,
+    int acc_words)
+{
+    extern __shared__ float2 lds[];
+    RowStat* scratch = reinterpret_cast<RowStat*>(lds + gsdr::fft::lds_elems_dev(plan));
+    const uint32_t N = plan.n;
+    const uint32_t d = blockIdx.x / ap.P, p = blockIdx.x - d * ap.P, b = blockIdx.y;
+    const uint32_t K = ap.dwells;
+    const int slot = K > 1 ? pool_acquire(acc_slots, acc_words) : 0;
+    float* acc = acc_pool + (size_t)slot * ap.eff;
+    const float2* c = code_fft + (size_t)p * N;
+    for (uint32_t k = 0; k < K; ++k)
+        {
+            const float2* x = X + ((size_t)(b * K + k) * ap.D + d) * N;
+            float best = -1.0f, sum = 0.0f;
+            uint32_t bidx = 0xffffffffu;
+            auto load = [&](int i) -> float2 {
+                float2 a = x[i], q = c[i];
+                return make_float2(a.x * q.x + a.y * q.y, a.x * q.y - a.y * q.x);
+            };
+            auto store = [&](int i, float2 v) {
+                const int j = i - (int)ap.out_off;
+                if (j < 0) return;
+                float m = v.x * v.x + v.y * v.y;
+                if (K > 1)
+                    {
+                        if (k > 0) m = acc[j] + m;  // volk_32f_x2_add_32f(grid, grid, tmp)
+                        acc[j] = m;
+                    }
+                if (stat_better(m, (uint32_t)j, best, bidx))
+                    {
+                        best = m;
+                        bidx = (uint32_t)j;
+                    }
+                sum += m;
+            };
+            PT::run(plan, lds, tw, load, store);
+            block_reduce_stat<PT::NT>(best, bidx, sum, scratch);
+            if (threadIdx.x == 0) stats[(((size_t)b * ap.P + p) * K + k) * ap.D + d] = RowStat{best, bidx, sum, 0};
+        }
+    if (K > 1) pool_release(acc_slots, slot);
+}
+
+// One wave per (attempt b, PRN p): the statistic after every dwell k (the grid
+// maximum of the accumulated grid, strict '>' scan order; CFAR input power of row
+// (d*+D/2)%D divided by the dwell counter k+1, pcps_acquisition.cc:533), written to
+// resk[(b*P + p)*K + k]; with CFAR also the decision (first positive dwell, else
+// the last, :781-869) into res[b*P + p] with num_dwells.
+__global__ void __launch_bounds__(64) acq_reduce_dwell_kernel(const RowStat* __restrict__ stats,
+    gsdr_acq_result* __restrict__ resk, gsdr_acq_result* __restrict__ res, const uint32_t* __restrict__ prn_ids,
+    AcqParams ap, uint64_t stamp0, uint64_t block_stride)
+{
+    const uint32_t bp = blockIdx.x;
+    const uint32_t b = bp / ap.P, p = bp - b * ap.P;
+    const uint32_t K = ap.dwells;
+    bool done = false;
+    for (uint32_t k = 0; k < K && !done; ++k)
+        {
+            const RowStat* s = stats + ((size_t)bp * K + k) * ap.D;
+            float m = -1.0f;
+            uint32_t dsel = 0xffffffffu, tsel = 0;
+            for (uint32_t d = threadIdx.x; d < ap.D; d += 64)
+                {
+                    RowStat r = s[d];
+                    if (r.max > m)
+                        {
+                            m = r.max;
+                            dsel = d;
+                            tsel = r.idx;
+                        }
+                }
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1)
+                {
+                    float om = __shfl_xor(m, off);
+                    uint32_t od = __shfl_xor(dsel, off);
+                    uint32_t ot = __shfl_xor(tsel, off);
+                    if (stat_better(om, od, m, dsel))
+                        {
+                            m = om;
+                            dsel = od;
+                            tsel = ot;
+                        }
+                }
+            gsdr_acq_result r;
+            r.prn = prn_ids[p];
+            r.doppler_index = dsel;
+            r.code_phase = tsel;
+            r.doppler_hz = -ap.doppler_max + ap.doppler_center + ap.doppler_step * (int32_t)dsel;
+            r.peak = m;
+            r.second_peak = 0.0f;
+            r.input_power = 0.0f;
+            r.test_statistic = 0.0f;
+            r.acq_delay_samples = (double)fmodf((float)tsel, ap.samples_per_code);
+            r.samplestamp = stamp0 + (uint64_t)(b * K + k) * block_stride;
+            r.positive = 0;
+            r.num_dwells = (int32_t)(k + 1);
+            if (ap.cfar)
+                {
+                    const uint32_t opp = (dsel + ap.D / 2) % ap.D;
+                    const float acc = s[opp].sum;
+                    const float ip = (float)((double)(acc / (float)(int32_t)ap.eff) / 2.0 / (double)(k + 1));
+                    r.input_power = ip;
+                    r.test_statistic = m / ip;
+                    r.positive = r.test_statistic > ap.threshold ? 1 : 0;
+                    done = r.positive || k + 1 == K;
+                    if (done && threadIdx.x == 0) res[bp] = r;
+                }
+            if (threadIdx.x == 0) resk[(size_t)bp * K + k] = r;
+        }
+}
+
+// Peak-ratio statistic per dwell: the accumulated row d*_k over dwells 0..k,
+// maximum outside the exclusion window (as acq_second_peak_kernel).  grid (K, B*P).
+template <class PT>
+__global__ void __launch_bounds__(PT::NT) acq_second_peak_dwell_kernel(const float2* __restrict__ X,
+    const float2* __restrict__ code_fft, gsdr_acq_result* __restrict__ resk, const float2* __restrict__ tw,
+    typename PT::PlanT plan, AcqParams ap, float* __restrict__ acc_pool, uint32_t* __restrict__ acc_slots,
+    int acc_words)
+{
+    extern __shared__ float2 lds[];
+    RowStat* scratch = reinterpret_cast<RowStat*>(lds + gsdr::fft::lds_elems_dev(plan));
+    const uint32_t kk = blockIdx.x, bp = blockIdx.y;
+    const uint32_t K = ap.dwells;
+    const uint32_t b = bp / ap.P, p = bp - b * ap.P;
+    const uint32_t N = plan.n;
+    gsdr_acq_result* rr = resk + (size_t)bp * K + kk;
+    const uint32_t d = rr->doppler_index;
+    const int32_t ti = (int32_t)rr->code_phase;
+    // the reference wraps the exclusion window at d_fft_size even when the rows
+    // hold the effective N/2 outputs (bit transition; :580-590)
+    const int32_t E = (int32_t)ap.N;
+    int32_t e1 = ti - (int32_t)ap.samples_per_chip;
+    int32_t e2 = ti + (int32_t)ap.samples_per_chip;
+    if (e1 < 0)
+        e1 = E + e1;
+    else if (e2 >= E)
+        e2 = e2 - E;
+    const int slot = kk > 0 ? pool_acquire(acc_slots, acc_words) : 0;
+    float* acc = acc_pool + (size_t)slot * ap.eff;
+    const float2* c = code_fft + (size_t)p * N;
+    float best = 0.0f, sum = 0.0f;
+    uint32_t bidx = 0;
+    for (uint32_t k = 0; k <= kk; ++k)
+        {
+            const float2* x = X + ((size_t)(b * K + k) * ap.D + d) * N;
+            const bool last = k == kk;
+            auto load = [&](int i) -> float2 {
+                float2 a = x[i], q = c[i];
+                return make_float2(a.x * q.x + a.y * q.y, a.x * q.y - a.y * q.x);
+            };
+            auto store = [&](int i, float2 v) {
+                const int j = i - (int)ap.out_off;
+                if (j < 0) return;
+                float m = v.x * v.x + v.y * v.y;
+                if (kk > 0)
+                    {
+                        if (k > 0) m = acc[j] + m;
+                        if (!last) acc[j] = m;
+                    }
+                if (last)
+                    {
+                        const bool excluded = (e1 < e2) ? (j >= e1 && j < e2) : (j >= e1 || j < e2);
+                        if (excluded) m = 0.0f;
+                        if (stat_better(m, (uint32_t)j, best, bidx))
+                            {
+                                best = m;
+                                bidx = (uint32_t)j;
+                            }
+                    }
+            };
+            PT::run(plan, lds, tw, load, store);
+        }
+    block_reduce_stat<PT::NT>(best, bidx, sum, scratch);
+    if (threadIdx.x == 0)
+        {
+            gsdr_acq_result r = *rr;
+            r.second_peak = best;
+            r.test_statistic = r.peak / best;
+            r.positive = r.test_statistic > ap.threshold ? 1 : 0;
+            *rr = r;
+        }
+    if (kk > 0) pool_release(acc_slots, slot);
+}
+
+// Peak-ratio decision over the dwells: the first positive dwell, else the last.
+__global__ void acq_decide_kernel(const gsdr_acq_result* __restrict__ resk, gsdr_acq_result* __restrict__ res,
+    uint32_t K, uint32_t n)
+{
+    const uint32_t bp = blockIdx.x * blockDim.x + threadIdx.x;
+    if (bp >= n) return;
+    uint32_t k = 0;
+    while (k + 1 < K && !resk[(size_t)bp * K + k].positive) ++k;
+    res[bp] = resk[(size_t)bp * K + k];
+}
+
+// ---------------------------------------------------------------- K_reduce
+// One wave per (b, p).  Rows are scanned in increasing d by each lane and merged
+// with the (max desc, d asc) order, reproducing the reference's strict '>' scan.
+__global__ void __launch_bounds__(64) acq_reduce_kernel(const RowStat* __restrict__ stats,
+    gsdr_acq_result* __restrict__ res, const uint32_t* __restrict__ prn_ids, AcqParams ap, uint64_t stamp0,
+    uint64_t block_stride)
+{
+    const uint32_t bp = blockIdx.x;  // b*P + p
+    const uint32_t b = bp / ap.P, p = bp - b * ap.P;
+    const RowStat* s = stats + (size_t)bp * ap.D;
+    float m = -1.0f;
+    uint32_t dsel = 0xffffffffu, tsel = 0;
+    for (uint32_t d = threadIdx.x; d < ap.D; d += 64)
+        {
+            RowStat r = s[d];
+            if (r.max > m)
+                {
+                    m = r.max;
+                    dsel = d;
+                    tsel = r.idx;
+                }
+        }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1)
+        {
+            float om = __shfl_xor(m, off);
+            uint32_t od = __shfl_xor(dsel, off);
+            uint32_t ot = __shfl_xor(tsel, off);
+            if (stat_better(om, od, m, dsel))
+                {
+                    m = om;
+                    dsel = od;
+                    tsel = ot;
+                }
+        }
+    if (threadIdx.x != 0) return;
+    gsdr_acq_result r;
+    r.prn = prn_ids[p];
+    r.doppler_index = dsel;
+    r.code_phase = tsel;
+    r.doppler_hz = -ap.doppler_max + ap.doppler_center + ap.doppler_step * (int32_t)dsel;
+    r.peak = m;
+    r.second_peak = 0.0f;
+    r.input_power = 0.0f;
+    r.test_statistic = 0.0f;
+    r.acq_delay_samples = (double)fmodf((float)tsel, ap.samples_per_code);
+    r.samplestamp = stamp0 + (uint64_t)b * block_stride;
+    r.positive = 0;
+    r.num_dwells = 1;
+    if (ap.cfar)
+        {
+            const uint32_t opp = (dsel + ap.D / 2) % ap.D;
+            const float acc = s[opp].sum;
+            // float(accumulate) / int32 in float, then / 2.0 / counter in double (pcps_acquisition.cc:533)
+            const float ip = (float)((double)(acc / (float)(int32_t)ap.N) / 2.0 / (double)ap.dwells);
+            r.input_power = ip;
+            r.test_statistic = m / ip;
+            r.positive = r.test_statistic > ap.threshold ? 1 : 0;
+        }
+    res[bp] = r;
+}
+
+// ---------------------------------------------------------------- K_second
+// Peak-ratio statistic: recompute row d* of (b, p) and take the maximum outside
+// the cyclic exclusion range [e1, e2) built as in pcps_acquisition.cc:580-604.
+template <class PT>
+__global__ void __launch_bounds__(PT::NT) acq_second_peak_kernel(const float2* __restrict__ X,
+    const float2* __restrict__ code_fft, gsdr_acq_result* __restrict__ res, const float2* __restrict__ tw,
+    typename PT::PlanT plan, AcqParams ap)
+{
+    extern __shared__ float2 lds[];
+    RowStat* scratch = reinterpret_cast<RowStat*>(lds + gsdr::fft::lds_elems_dev(plan));
+    const uint32_t bp = blockIdx.x;
+    const uint32_t b = bp / ap.P, p = bp - b * ap.P;
+    const uint32_t N = plan.n;
+    const uint32_t d = res[bp].doppler_index;
+    const int32_t ti = (int32_t)res[bp].code_phase;
+    int32_t e1 = ti - (int32_t)ap.samples_per_chip;
+    int32_t e2 = ti + (int32_t)ap.samples_per_chip;
+    if (e1 < 0)
+        e1 = (int32_t)N + e1;
+    else if (e2 >= (int32_t)N)
+        e2 = e2 - (int32_t)N;
+    const float2* x = X + ((size_t)b * ap.D + d) * N;
+    const float2* c = code_fft + (size_t)p * N;
+    float best = 0.0f, sum = 0.0f;
+    uint32_t bidx = 0;
+    auto load = [&](int i) -> float2 {
+        float2 a = x[i], k = c[i];
+        return make_float2(a.x * k.x + a.y * k.y, a.x * k.y - a.y * k.x);
+    };
+    auto store = [&](int i, float2 v) {
+        const bool excluded = (e1 < e2) ? (i >= e1 && i < e2) : (i >= e1 || i < e2);
+        const float m = excluded ? 0.0f : v.x * v.x + v.y * v.y;
+        if (stat_better(m, (uint32_t)i, best, bidx))
+            {
+                best = m;
+                bidx = (uint32_t)i;
+            }
+    };
+    PT::run(plan, lds, tw, load, store);
+    block_reduce_stat<PT::NT>(best, bidx, sum, scratch);
+    if (threadIdx.x == 0)
+        {
+            gsdr_acq_result r = res[bp];
+            r.second_peak = best;
+            r.test_statistic = r.peak / best;
+            r.positive = r.test_statistic > ap.threshold ? 1 : 0;
+            res[bp] = r;
+        }
+}
+
+}  // namespace
+
+// ====================================================================== handle
+struct gsdr_acq
+{
+    int device{0};
+    gsdr_acq_conf conf{};
+    uint32_t N{0}, D{0}, consumed{0}, lead{0};
+    uint32_t K{1};       // max_dwells
+    uint32_t eff{0};     // effective FFT size (outputs [N - eff, N))
+    bool general{false}; // dwells > 1 or bit transition: the general kernels
+    gsdr_acq_result* d_resk{nullptr};  // per-dwell results (general path)
+    float* d_acc{nullptr};             // pooled |R|^2 accumulation rows (general path)
+    uint32_t* d_acc_slots{nullptr};
+    int acc_words{0};
+    float threshold{0.0f};
+    int nt{256};
+    int variant{0};
+    int corr_variant{0};      // 0: single-transform correlate kernel; >0: GSDR_PK(M)_VARIANTS id
+    size_t corr_lds_bytes{0};
+    Plan plan{};
+    gsdr::fft::Plan4 plan4{};  // four-step plan (variants 20-22, N beyond one workgroup's LDS)
+    size_t lds_bytes{0};
+    hipStream_t stream{nullptr};
+    float2* d_tw{nullptr};
+    float2* d_wipe{nullptr};
+    float2* d_code_fft{nullptr};
+    float2* d_code_stage{nullptr};
+    uint32_t* d_prn{nullptr};
+    uint32_t nprn{0};
+    float2* d_X{nullptr};
+    RowStat* d_stats{nullptr};
+    gsdr_acq_result* d_res{nullptr};
+    void* d_iq{nullptr};
+    float* d_grid{nullptr};
+    float2* d_tw_sub{nullptr};   // four-step: W_N2 table
+    float2* d_scratch{nullptr};  // four-step: slot rows of N complex
+    uint32_t* d_slots{nullptr};  // four-step: slot occupancy bitmap
+    // stage profiling (gsdr_acq_set_profiling)
+    struct ProfRec
+    {
+        hipEvent_t a, b;
+        int stage;
+    };
+    bool profiling{false};
+    std::vector<ProfRec> prof_recs;
+    std::vector<hipEvent_t> prof_pool;
+    std::mutex mu;
+};
+
+namespace
+{
+
+using gsdr::fft::FourStepPlan;
+using gsdr::fft::RuntimePlan;
+using gsdr::fft::StaticPlan;
+
+size_t item_bytes(int it) { return it == GSDR_ITEM_CSHORT ? 4 : 8; }
+
+// FFT variants (gsdr_acq::variant): 1-4 compile-time plans for the sample rates
+// GNSS front-ends use (2/4/8/16 Msps at 1 ms, acq_v_static.hip), 10-12 runtime
+// LDS plans for every other 2^a3^b5^c size (acq_v_runtime.hip), 20/22 the
+// four-step FFT beyond one workgroup's LDS (acq_v_four.hip).
+
+
+// Correlate-kernel variants for N = 4000 (env GSDR_ACQ_CORR_VARIANT selects one;
+// 0 = the single-transform kernel of the plan variant).
+// Packed-f32 variants: (id, plan, PRNs per workgroup).
+#define GSDR_PK_VARIANTS(X)                                              \
+    X(30, (gsdr::pk::PkPlan<256, true, 25, 16, 10>), 1, 1)              \
+    X(35, (gsdr::pk::PkPlan<256, true, 20, 20, 10>), 1, 1)              \
+    X(37, (gsdr::pk::PkPlan<512, true, 25, 16, 10>), 2, 1)
+
+// Packed multi-transform variants: (id, plan, waves per EU hint).
+#define GSDR_PKM_VARIANTS(X)                                              \
+    X(43, (gsdr::pk::PkMultiPlan<256, 1, false, 20, 20, 10>), 1)        \
+    X(45, (gsdr::pk::PkMultiPlan<320, 2, true, 25, 16, 10>), 1)         \
+    X(47, (gsdr::pk::PkMultiPlan<256, 1, false, 25, 16, 10>), 1)
+
+template <class PT>
+int set_lds_attrs(size_t bytes)
+{
+    GSDR_HIP(hipFuncSetAttribute((const void*)acq_code_fft_kernel<PT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (int)bytes));
+    GSDR_HIP(hipFuncSetAttribute((const void*)acq_forward_kernel<PT, GSDR_ITEM_GR_COMPLEX>,
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+    GSDR_HIP(hipFuncSetAttribute((const void*)acq_forward_kernel<PT, GSDR_ITEM_CSHORT>,
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+    GSDR_HIP(hipFuncSetAttribute((const void*)acq_correlate_kernel<PT, false>,
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+    GSDR_HIP(hipFuncSetAttribute((const void*)acq_correlate_kernel<PT, true>,
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+    GSDR_HIP(hipFuncSetAttribute((const void*)acq_second_peak_kernel<PT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (int)bytes));
+    GSDR_HIP(hipFuncSetAttribute((const void*)acq_correlate_dwell_kernel<PT>,
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+    GSDR_HIP(hipFuncSetAttribute((const void*)acq_second_peak_dwell_kernel<PT>,
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+    return GSDR_OK;
+}
+
+AcqParams params_of(const gsdr_acq* a)
+{
+    AcqParams ap{};
+    ap.N = a->N;
+    ap.consumed = a->consumed;
+    ap.lead_zeros = a->lead;
+    ap.D = a->D;
+    ap.P = a->nprn;
+    ap.doppler_max = a->conf.doppler_max;
+    ap.doppler_center = a->conf.doppler_center;
+    ap.doppler_step = (int32_t)a->conf.doppler_step;
+    ap.samples_per_code = a->conf.samples_per_code;
+    ap.samples_per_chip = a->conf.samples_per_chip;
+    ap.dwells = a->K;
+    ap.threshold = a->threshold;
+    ap.cfar = a->conf.pfa > 0.0f ? 1 : 0;
+    ap.eff = a->eff;
+    ap.out_off = a->N - a->eff;
+    return ap;
+}
+
+int rebuild_wipeoffs(gsdr_acq* a)
+{
+    hipLaunchKernelGGL(acq_wipeoff_kernel, dim3(a->D), dim3(256), 0, a->stream, a->d_wipe, a->N,
+        (float)a->conf.fs_in, a->conf.doppler_max, a->conf.doppler_center, (int32_t)a->conf.doppler_step,
+        a->conf.doppler_bias);
+    GSDR_HIP(hipGetLastError());
+    GSDR_HIP(hipStreamSynchronize(a->stream));
+    return GSDR_OK;
+}
+
+void compute_threshold(gsdr_acq* a)
+{
+    // calculate_threshold, pcps_acquisition.cc:894-909: effective FFT size (N/2
+    // with bit transition) x bins, 2*dwells degrees of freedom (max_dwells is 1
+    // with bit transition)
+    const float pfa = a->conf.pfa;
+    if (pfa <= 0.0f) return;
+    const int num_bins = (int)(a->eff * a->D);
+    const double p = std::pow(1.0 - (double)pfa, 1.0 / (double)(float)num_bins);
+    a->threshold = (float)(2.0 * gsdr::gamma_p_inv_int(2 * (int)a->conf.max_dwells, p));
+}
+
+// Event bracket around one stage launch when profiling is on.
+struct StageTimer
+{
+    gsdr_acq* a;
+    hipStream_t s;
+    hipEvent_t ev0{nullptr};
+    StageTimer(gsdr_acq* a_, hipStream_t s_) : a(a_), s(s_) {}
+    hipEvent_t take()
+    {
+        hipEvent_t e = nullptr;
+        if (!a->prof_pool.empty())
+            {
+                e = a->prof_pool.back();
+                a->prof_pool.pop_back();
+            }
+        else if (hipEventCreate(&e) != hipSuccess)
+            e = nullptr;
+        return e;
+    }
+    void begin()
+    {
+        if (!a->profiling) return;
+        ev0 = take();
+        if (ev0) (void)hipEventRecord(ev0, s);
+    }
+    void end(int stage)
+    {
+        if (!a->profiling || !ev0) return;
+        hipEvent_t ev1 = take();
+        if (!ev1) return;
+        (void)hipEventRecord(ev1, s);
+        a->prof_recs.push_back({ev0, ev1, stage});
+        ev0 = nullptr;
+    }
+};
+
+}  // namespace
+
+// Defined in the variant translation units (one per plan-type group, compiled in
+// parallel): acq_pk.hip, acq_v_static.hip, acq_v_runtime.hip, acq_v_four.hip.
+namespace gsdr_acq_impl
+{
+int launch_corr_variant(gsdr_acq* a, uint32_t nblocks, hipStream_t s);
+int setup_corr_variant(gsdr_acq* a, int v);
+int dispatch_static(gsdr_acq* a, int op, const void* iq, uint32_t nblocks, uint64_t stride, uint64_t stamp0,
+    gsdr_acq_result* res, hipStream_t s, uint32_t aux);
+int dispatch_runtime(gsdr_acq* a, int op, const void* iq, uint32_t nblocks, uint64_t stride, uint64_t stamp0,
+    gsdr_acq_result* res, hipStream_t s, uint32_t aux);
+int dispatch_four(gsdr_acq* a, int op, const void* iq, uint32_t nblocks, uint64_t stride, uint64_t stamp0,
+    gsdr_acq_result* res, hipStream_t s, uint32_t aux);
+}  // namespace gsdr_acq_impl
+
+namespace
+{
+using gsdr_acq_impl::launch_corr_variant;
+
+template <class PT>
+const typename PT::PlanT& plan_of(const gsdr_acq* a)
+{
+    if constexpr (std::is_same<typename PT::PlanT, gsdr::fft::Plan4>::value)
+        return a->plan4;
+    else
+        return a->plan;
+}
+
+template <class PT>
+void launch_forward(gsdr_acq* a, const void* iq, int item_type, uint32_t nblocks, uint64_t stride, hipStream_t s)
+{
+    if (item_type == GSDR_ITEM_GR_COMPLEX)
+        hipLaunchKernelGGL((acq_forward_kernel<PT, GSDR_ITEM_GR_COMPLEX>), dim3(a->D, nblocks), dim3(PT::NT),
+            a->lds_bytes, s, iq, stride, a->d_wipe, a->d_X, a->d_tw, plan_of<PT>(a), a->consumed, a->D);
+    else
+        hipLaunchKernelGGL((acq_forward_kernel<PT, GSDR_ITEM_CSHORT>), dim3(a->D, nblocks), dim3(PT::NT),
+            a->lds_bytes, s, iq, stride, a->d_wipe, a->d_X, a->d_tw, plan_of<PT>(a), a->consumed, a->D);
+}
+
+// General path (max_dwells > 1 and/or bit_transition_flag): forward spectra of
+// all nblocks*K blocks, the dwell-accumulating correlate kernel, per-dwell
+// statistics and the dwell decision.
+template <class PT>
+int launch_general(gsdr_acq* a, const void* iq, int item_type, uint32_t nblocks, uint64_t stride, uint64_t stamp0,
+    gsdr_acq_result* res, hipStream_t s, StageTimer& t)
+{
+    const size_t lds = a->lds_bytes;
+    const uint32_t K = a->K;
+    t.begin();
+    launch_forward<PT>(a, iq, item_type, nblocks * K, stride, s);
+    GSDR_HIP(hipGetLastError());
+    t.end(0);
+    AcqParams ap = params_of(a);
+    t.begin();
+    hipLaunchKernelGGL((acq_correlate_dwell_kernel<PT>), dim3(a->D * a->nprn, nblocks), dim3(PT::NT), lds, s, a->d_X,
+        a->d_code_fft, a->d_stats, a->d_tw, plan_of<PT>(a), ap, a->d_acc, a->d_acc_slots, a->acc_words);
+    GSDR_HIP(hipGetLastError());
+    t.end(1);
+    t.begin();
+    hipLaunchKernelGGL(acq_reduce_dwell_kernel, dim3(nblocks * a->nprn), dim3(64), 0, s, a->d_stats, a->d_resk, res,
+        a->d_prn, ap, stamp0, stride);
+    GSDR_HIP(hipGetLastError());
+    t.end(2);
+    if (!ap.cfar)
+        {
+            t.begin();
+            hipLaunchKernelGGL((acq_second_peak_dwell_kernel<PT>), dim3(K, nblocks * a->nprn), dim3(PT::NT), lds, s,
+                a->d_X, a->d_code_fft, a->d_resk, a->d_tw, plan_of<PT>(a), ap, a->d_acc, a->d_acc_slots,
+                a->acc_words);
+            const uint32_t n = nblocks * a->nprn;
+            hipLaunchKernelGGL(acq_decide_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a->d_resk, res, K, n);
+            GSDR_HIP(hipGetLastError());
+            t.end(3);
+        }
+    return GSDR_OK;
+}
+
+template <class PT>
+int launch_all(gsdr_acq* a, const void* iq, int item_type, uint32_t nblocks, uint64_t stride, uint64_t stamp0,
+    gsdr_acq_result* res, hipStream_t s)
+{
+    const size_t lds = a->lds_bytes;
+    StageTimer t(a, s);
+    if (a->general) return launch_general<PT>(a, iq, item_type, nblocks, stride, stamp0, res, s, t);
+    t.begin();
+    launch_forward<PT>(a, iq, item_type, nblocks, stride, s);
+    GSDR_HIP(hipGetLastError());
+    t.end(0);
+    t.begin();
+    if (a->corr_variant > 0)
+        {
+            int rc = launch_corr_variant(a, nblocks, s);
+            if (rc != GSDR_OK) return rc;
+        }
+    else
+        {
+            hipLaunchKernelGGL((acq_correlate_kernel<PT, false>), dim3(a->D * a->nprn, nblocks), dim3(PT::NT), lds, s,
+                a->d_X, a->d_code_fft, a->d_stats, (float*)nullptr, a->d_tw, plan_of<PT>(a), a->D, a->nprn, 0u);
+        }
+    GSDR_HIP(hipGetLastError());
+    t.end(1);
+    AcqParams ap = params_of(a);
+    t.begin();
+    hipLaunchKernelGGL(acq_reduce_kernel, dim3(nblocks * a->nprn), dim3(64), 0, s, a->d_stats, res, a->d_prn, ap,
+        stamp0, stride);
+    GSDR_HIP(hipGetLastError());
+    t.end(2);
+    if (!ap.cfar)
+        {
+            t.begin();
+            hipLaunchKernelGGL((acq_second_peak_kernel<PT>), dim3(nblocks * a->nprn), dim3(PT::NT), lds, s, a->d_X,
+                a->d_code_fft, res, a->d_tw, plan_of<PT>(a), ap);
+            GSDR_HIP(hipGetLastError());
+            t.end(3);
+        }
+    return GSDR_OK;
+}
+
+template <class PT>
+int launch_code_fft(gsdr_acq* a, uint32_t nprn)
+{
+    hipLaunchKernelGGL((acq_code_fft_kernel<PT>), dim3(nprn), dim3(PT::NT), a->lds_bytes, a->stream, a->d_code_stage,
+        a->d_code_fft, a->d_tw, plan_of<PT>(a), a->consumed, a->lead);
+    GSDR_HIP(hipGetLastError());
+    return GSDR_OK;
+}
+
+template <class PT>
+int launch_dump(gsdr_acq* a, bool grid, uint32_t prn_slot)
+{
+    launch_forward<PT>(a, a->d_iq, a->conf.item_type, 1, a->consumed, a->stream);
+    GSDR_HIP(hipGetLastError());
+    if (grid)
+        {
+            hipLaunchKernelGGL((acq_correlate_kernel<PT, true>), dim3(a->D, 1), dim3(PT::NT), a->lds_bytes, a->stream,
+                a->d_X, a->d_code_fft, a->d_stats, a->d_grid, a->d_tw, plan_of<PT>(a), a->D, a->nprn, prn_slot);
+            GSDR_HIP(hipGetLastError());
+        }
+    return GSDR_OK;
+}
+
+
+}  // namespace

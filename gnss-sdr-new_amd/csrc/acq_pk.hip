@@ -1,0 +1,77 @@
+// Packed-f32 correlate-kernel variants for N = 4000 (the C2 bench configuration):
+// launch and one-time setup, selected by gsdr_acq::corr_variant.
+#include "acq_impl.h"
+
+namespace gsdr_acq_impl
+{
+
+int launch_corr_variant(gsdr_acq* a, uint32_t nblocks, hipStream_t s)
+{
+#define GSDR_PK_CASE(ID, MP, PG, WPE)                                                                                \
+    case ID:                                                                                                    \
+        {                                                                                                       \
+            using M = GSDR_UNPAREN MP;                                                                          \
+            const uint32_t groups = (a->nprn + (PG)-1) / (PG);                                                  \
+            hipLaunchKernelGGL((acq_correlate_pk_kernel<M, PG, WPE>), dim3(nblocks * a->D * groups), dim3(M::NT),   \
+                a->corr_lds_bytes, s, a->d_X, a->d_code_fft, a->d_stats, a->d_tw, a->D, a->nprn, nblocks);      \
+            return GSDR_OK;                                                                                     \
+        }
+#define GSDR_PKM_CASE(ID, MP, WPE)                                                                              \
+    case ID:                                                                                                    \
+        {                                                                                                       \
+            using M = GSDR_UNPAREN MP;                                                                          \
+            const uint32_t groups = (a->nprn + M::PB - 1) / M::PB;                                              \
+            hipLaunchKernelGGL((acq_correlate_pkm_kernel<M, WPE>), dim3(nblocks * a->D * groups), dim3(M::NT),  \
+                a->corr_lds_bytes, s, a->d_X, a->d_code_fft, a->d_stats, a->d_tw, a->D, a->nprn, nblocks);      \
+            return GSDR_OK;                                                                                     \
+        }
+#define GSDR_UNPAREN(...) __VA_ARGS__
+    switch (a->corr_variant)
+        {
+            GSDR_PK_VARIANTS(GSDR_PK_CASE)
+            GSDR_PKM_VARIANTS(GSDR_PKM_CASE)
+        default: gsdr::set_error("internal: bad correlate variant %d", a->corr_variant); return GSDR_E_STATE;
+        }
+#undef GSDR_PK_CASE
+#undef GSDR_PKM_CASE
+#undef GSDR_UNPAREN
+}
+
+// Select and configure a correlate variant (N must be 4000).
+int setup_corr_variant(gsdr_acq* a, int v)
+{
+#define GSDR_PK_SETUP(ID, MP, PG, WPE)                                                                               \
+    case ID:                                                                                                    \
+        {                                                                                                       \
+            using M = GSDR_UNPAREN MP;                                                                          \
+            a->corr_lds_bytes = M::lds_bytes() + (size_t)2 * (M::NT / 64) * sizeof(RowStat);                   \
+            GSDR_HIP(hipFuncSetAttribute((const void*)acq_correlate_pk_kernel<M, PG, WPE>,                          \
+                hipFuncAttributeMaxDynamicSharedMemorySize, (int)a->corr_lds_bytes));                           \
+            a->corr_variant = ID;                                                                               \
+            return GSDR_OK;                                                                                     \
+        }
+#define GSDR_PKM_SETUP(ID, MP, WPE)                                                                             \
+    case ID:                                                                                                    \
+        {                                                                                                       \
+            using M = GSDR_UNPAREN MP;                                                                          \
+            a->corr_lds_bytes = M::lds_bytes() + (size_t)M::PB * (M::NT / 64) * sizeof(RowStat);               \
+            GSDR_HIP(hipFuncSetAttribute((const void*)acq_correlate_pkm_kernel<M, WPE>,                        \
+                hipFuncAttributeMaxDynamicSharedMemorySize, (int)a->corr_lds_bytes));                           \
+            a->corr_variant = ID;                                                                               \
+            return GSDR_OK;                                                                                     \
+        }
+#define GSDR_UNPAREN(...) __VA_ARGS__
+    switch (v)
+        {
+            GSDR_PK_VARIANTS(GSDR_PK_SETUP)
+            GSDR_PKM_VARIANTS(GSDR_PKM_SETUP)
+        default: a->corr_variant = 0; return GSDR_OK;
+        }
+#undef GSDR_PK_SETUP
+#undef GSDR_PKM_SETUP
+#undef GSDR_UNPAREN
+}
+
+// The plan object a plan type's kernels take (LDS plan or four-step plan).
+
+}  // namespace gsdr_acq_impl

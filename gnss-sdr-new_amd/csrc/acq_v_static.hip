@@ -1,0 +1,33 @@
+// Acquisition launch templates instantiated for the compile-time FFT plans (1 ms at 2/4/8/16 Msps).
+#include "acq_impl.h"
+
+namespace gsdr_acq_impl
+{
+
+int dispatch_static(gsdr_acq* a, int op, const void* iq, uint32_t nblocks, uint64_t stride, uint64_t stamp0,
+    gsdr_acq_result* res, hipStream_t s, uint32_t aux)
+{
+#define GSDR_CASE(ID, PT)                                                                               \
+    case ID:                                                                                            \
+        switch (op)                                                                                     \
+            {                                                                                           \
+            case 0: return launch_all<GSDR_UNPAREN PT>(a, iq, a->conf.item_type, nblocks, stride, stamp0, res, s); \
+            case 1: return launch_code_fft<GSDR_UNPAREN PT>(a, aux);                                     \
+            case 2: return launch_dump<GSDR_UNPAREN PT>(a, false, 0);                                    \
+            case 3: return launch_dump<GSDR_UNPAREN PT>(a, true, aux);                                   \
+            default: return set_lds_attrs<GSDR_UNPAREN PT>(a->lds_bytes);                                \
+            }
+#define GSDR_UNPAREN(...) __VA_ARGS__
+    switch (a->variant)
+        {
+            GSDR_CASE(1, (StaticPlan<256, 20, 20, 10>))
+            GSDR_CASE(2, (StaticPlan<512, 20, 20, 20>))
+            GSDR_CASE(3, (StaticPlan<1024, 16, 10, 10, 10>))
+            GSDR_CASE(4, (StaticPlan<256, 20, 10, 10>))
+        default: gsdr::set_error("internal: bad FFT variant %d", a->variant); return GSDR_E_STATE;
+        }
+#undef GSDR_CASE
+#undef GSDR_UNPAREN
+}
+
+}  // namespace gsdr_acq_impl

@@ -62,6 +62,22 @@ constexpr double kGpsCaRate = 1.023e6;
 constexpr double kGpsCaPeriod = 0.001;
 constexpr int kGpsCaLength = 1023;
 constexpr int kGpsCaSymbolsPerBit = 20;
+// Galileo_E1.h:32-52
+constexpr double kGalE1Hz = 1.57542e9;
+constexpr double kGalE1Rate = 1.023e6;
+constexpr double kGalE1Period = 0.004;
+constexpr int kGalE1Length = 4092;
+constexpr const char* kGalE1cSecondary = "0011100000001010110110010";
+// Beidou_B1I.h:30-48
+constexpr double kBdsB1Hz = 1.561098e9;
+constexpr double kBdsB1Rate = 2.046e6;
+constexpr double kBdsB1Period = 0.001;
+constexpr int kBdsB1Length = 2046;
+constexpr const char* kBdsB1Nh = "00000100110101001110";
+constexpr const char* kBdsB1GeoPreamble = "1111110000001100001100";
+constexpr const char* kGpsCaPreamble =
+    "1111111111111111111100000000000000000000000000000000000000000000000000000000000011111111111111111111000000000000"
+    "000000001111111111111111111111111111111111111111";
 // GPS_CA_PREAMBLE_SYMBOLS_STR as a 160-bit register, string index i at bit
 // (159 - i) of the 5-word big register (word 4 = most significant)
 // '1' -> 1; built on the host by preamble_register().
@@ -161,7 +177,10 @@ struct TrkConst
     uint64_t bit_sync_span;  // (bit_synchronization_time_limit_s + 1) * (int)fs_in (:1866)
     float early_late_space_chips;
     float shifts[kMaxTrkTaps];
-    uint32_t preamble[5];
+    uint32_t preamble[5];    // secondary code / preamble as the circular-buffer register (acquire_secondary)
+    uint32_t sec_str[5];     // secondary code string bit i = (code[i] == '1') (state-4 wipe-off)
+    uint32_t data_sec_str;   // data secondary code (BeiDou NH), same form
+    int32_t sec_len, data_sec_len, secondary, veml, track_pilot, iE, iP, iL;
     int32_t vector_length, code_length_chips, code_samples_per_chip, symbols_per_bit;
     int32_t cn0_samples, cn0_min, max_code_lock_fail, max_carrier_lock_fail;
     int32_t extend_correlation_symbols, enable_fll_pull_in, enable_fll_steady_state, carrier_aiding;
@@ -180,7 +199,7 @@ struct TrkHot
     double carrier_phase_step_rad, carrier_phase_rate_step_rad, code_phase_step_chips, code_phase_rate_step_chips;
     double rem_code_phase_samples;
     uint64_t next_sample;
-    float2 E_accu, P_accu, P_accu_old, L_accu, P_data_accu;
+    float2 VE_accu, E_accu, P_accu, P_accu_old, L_accu, VL_accu, P_data_accu;
     float cf_w, cf_x;                  // Tracking_FLL_PLL_filter state
     float sm_old[2], sm_sum[2];        // smoothers: value and running init sum
     int32_t sm_counter[2], sm_init[2];
@@ -300,6 +319,18 @@ __device__ inline double dll_nc_e_minus_l(float2 e, float2 l, float spc, float s
     return (double)((y - slope * spc) / slope) * (pe - pl) / s;
 }
 
+// pll_four_quadrant_atan (:86-89); gr::fast_atan2f restated as atan2f
+__device__ inline double pll_four_quadrant_atan(float2 p) { return (double)atan2f(p.y, p.x); }
+
+__device__ inline double dll_nc_vemlp(float2 ve, float2 e, float2 l, float2 vl)  // :139-149
+{
+    const double Early = sqrt((double)(ve.x * ve.x + ve.y * ve.y + e.x * e.x + e.y * e.y));
+    const double Late = sqrt((double)(l.x * l.x + l.y * l.y + vl.x * vl.x + vl.y * vl.y));
+    const double s = Early + Late;
+    if (s == 0.0) return 0.0;
+    return (Early - Late) / s;
+}
+
 __device__ inline void clear_tracking_vars(TrkHot& t)  // :1192-1213
 {
     t.P_accu_old = make_float2(0.f, 0.f);
@@ -393,7 +424,8 @@ __device__ inline int cn0_and_lock(const TrkConst& c, TrkHot& t, float2* pbuf, d
 
 __device__ inline void run_dll_pll(const TrkConst& c, TrkHot& t, LoopFilter& lf)  // :1092-1179 (no Doppler correction)
 {
-    const double carr_phase_error_hz = pll_cloop_two_quadrant_atan(t.P_accu) / kTwoPi;
+    const double carr_phase_error_hz =
+        (t.cloop ? pll_cloop_two_quadrant_atan(t.P_accu) : pll_four_quadrant_atan(t.P_accu)) / kTwoPi;
     double carr_error_filt_hz;
     if ((t.pull_in_transitory && c.enable_fll_pull_in) || c.enable_fll_steady_state)
         {
@@ -411,7 +443,8 @@ __device__ inline void run_dll_pll(const TrkConst& c, TrkHot& t, LoopFilter& lf)
             carr_error_filt_hz = (double)cf_error(c.cf, t, 0, (float)carr_phase_error_hz, (float)c.current_correlation_time_s);
         }
     t.carrier_doppler_hz = carr_error_filt_hz;
-    const double code_error_chips = dll_nc_e_minus_l(t.E_accu, t.L_accu, t.spc, 1.0F, 1.0F);
+    const double code_error_chips =
+        c.veml ? dll_nc_vemlp(t.VE_accu, t.E_accu, t.L_accu, t.VL_accu) : dll_nc_e_minus_l(t.E_accu, t.L_accu, t.spc, 1.0F, 1.0F);
     const double code_error_filt_chips = (double)lf_apply(lf, (float)code_error_chips);
     t.code_freq_chips = c.code_chip_rate - code_error_filt_chips;
     if (c.carrier_aiding) t.code_freq_chips += t.carrier_doppler_hz * c.code_chip_rate / c.signal_carrier_freq;
@@ -445,21 +478,27 @@ __device__ inline void circ_push(TrkHot& t, float2 prompt)
             t.circ[w] = (t.circ[w] << 1) | carry;
             carry = out;
         }
-    if (t.circ_size < kPreambleLen) t.circ_size++;
+    t.circ_size++;
 }
 
 // acquire_secondary (:923-967): corr = sum over the buffer of +-1 by sign match
 // = 160 - 2 * mismatches; |corr| == 160 only on a full match or full inversion.
 __device__ inline int acquire_secondary(const TrkConst& c, TrkHot& t)
 {
+    // the last sec_len pushes sit in register bits [0, sec_len)
     int mism = 0;
-    for (int w = 0; w < 5; ++w) mism += __popc(t.circ[w] ^ c.preamble[w]);
+    for (int w = 0; w < 5; ++w)
+        {
+            const int lo = w * 32;
+            const uint32_t mask = c.sec_len >= lo + 32 ? 0xffffffffu : (c.sec_len > lo ? (1u << (c.sec_len - lo)) - 1u : 0u);
+            mism += __popc((t.circ[w] ^ c.preamble[w]) & mask);
+        }
     if (mism == 0)
         {
             t.flag_pll_180 = 0;
             return 1;
         }
-    if (mism == kPreambleLen)
+    if (mism == c.sec_len)
         {
             t.flag_pll_180 = 1;
             return 1;
@@ -473,25 +512,83 @@ struct EpochOut
     double prompt_i, prompt_q;
 };
 
-// One general_work call after the correlation (taps given): states 2 and 4.
+// save_correlation_results (:1288-1400): secondary-code wipe-off of the tap
+// accumulators, data-symbol accumulation (NH wipe-off / pilot data prompt).
+__device__ inline void save_correlation_results(const TrkConst& c, TrkHot& t, const float2 (&taps)[kMaxTrkTaps + 1])
+{
+    float sg = 1.0F;
+    if (c.secondary)
+        {
+            sg = ((c.sec_str[t.current_symbol >> 5] >> (t.current_symbol & 31)) & 1u) ? -1.0F : 1.0F;
+            t.current_symbol++;
+            t.current_symbol %= c.sec_len;
+        }
+    auto acc = [](float2& a, float2 b, float g) {
+        if (g > 0)
+            {
+                a.x += b.x;
+                a.y += b.y;
+            }
+        else
+            {
+                a.x -= b.x;
+                a.y -= b.y;
+            }
+    };
+    if (c.veml)
+        {
+            acc(t.VE_accu, taps[0], sg);
+            acc(t.VL_accu, taps[4], sg);
+        }
+    acc(t.E_accu, taps[c.iE], sg);
+    acc(t.P_accu, taps[c.iP], sg);
+    acc(t.L_accu, taps[c.iL], sg);
+    const float2 pd = c.track_pilot ? taps[kMaxTrkTaps] : taps[c.iP];
+    if (c.symbols_per_bit > 1)
+        {
+            if (c.data_sec_len > 0)
+                {
+                    acc(t.P_data_accu, pd, ((c.data_sec_str >> t.current_data_symbol) & 1u) ? -1.0F : 1.0F);
+                    t.current_data_symbol++;
+                    t.current_data_symbol %= c.data_sec_len;
+                }
+            else
+                {
+                    acc(t.P_data_accu, pd, 1.0F);
+                    t.current_data_symbol++;
+                    t.current_data_symbol %= c.symbols_per_bit;
+                }
+        }
+    else
+        t.P_data_accu = pd;
+    t.cloop = c.track_pilot ? 0 : 1;
+}
+
+// One general_work call after the correlation (taps given; slot kMaxTrkTaps is
+// the pilot-tracking data prompt): states 2 and 4.
 __device__ inline void after_correlation(const TrkConst& c, TrkHot& t, LoopFilter& lf, float2* pbuf,
-    const float2 (&taps)[kMaxTrkTaps], uint64_t nitems_read, int lane, EpochOut& o)
+    const float2 (&taps)[kMaxTrkTaps + 1], uint64_t nitems_read, int lane, EpochOut& o)
 {
     o.flags = 0;
     o.prompt_i = 0.0;
     o.prompt_q = 0.0;
-    const float2 tE = taps[0], tP = taps[1], tL = taps[2];
     if (t.state == 2)
         {
-            t.E_accu = tE;
-            t.P_accu = tP;
-            t.L_accu = tL;
+            if (c.veml)
+                {
+                    t.VE_accu = taps[0];
+                    t.VL_accu = taps[4];
+                }
+            t.E_accu = taps[c.iE];
+            t.P_accu = taps[c.iP];
+            t.L_accu = taps[c.iL];
             t.spc = c.early_late_space_chips;
             if (nitems_read < c.acq_sample_stamp || nitems_read - c.acq_sample_stamp >= c.bit_sync_span)
                 t.carrier_lock_fail_counter = 300000;
             if (!cn0_and_lock(c, t, pbuf, c.code_period, lane))
                 {
                     clear_tracking_vars(t);
+                    if (c.track_pilot) t.P_data_accu = make_float2(0.f, 0.f);
                     t.state = 0;
                     o.flags |= GSDR_TRK_F_LOSS_OF_LOCK;
                 }
@@ -502,12 +599,17 @@ __device__ inline void after_correlation(const TrkConst& c, TrkHot& t, LoopFilte
                     update_tracking_vars(c, t);
                     if (!t.pull_in_transitory)
                         {
-                            circ_push(t, tP);
-                            if (t.circ_size == kPreambleLen) next_state = acquire_secondary(c, t);
+                            if (c.secondary || c.symbols_per_bit > 1)
+                                {
+                                    circ_push(t, taps[c.iP]);
+                                    if (t.circ_size >= c.sec_len) next_state = acquire_secondary(c, t);
+                                }
+                            else
+                                next_state = 1;
                         }
                     if (next_state)
                         {
-                            t.E_accu = t.P_accu = t.L_accu = t.P_data_accu = make_float2(0.f, 0.f);
+                            t.VE_accu = t.E_accu = t.P_accu = t.L_accu = t.VL_accu = t.P_data_accu = make_float2(0.f, 0.f);
                             t.circ_size = 0;
                             for (int w = 0; w < 5; ++w) t.circ[w] = 0u;
                             t.current_symbol = 0;
@@ -519,20 +621,11 @@ __device__ inline void after_correlation(const TrkConst& c, TrkHot& t, LoopFilte
         }
     else  // state 4
         {
-            t.E_accu.x += tE.x;
-            t.E_accu.y += tE.y;
-            t.P_accu.x += tP.x;
-            t.P_accu.y += tP.y;
-            t.L_accu.x += tL.x;
-            t.L_accu.y += tL.y;
-            t.P_data_accu.x += tP.x;
-            t.P_data_accu.y += tP.y;
-            t.current_data_symbol++;
-            t.current_data_symbol %= c.symbols_per_bit;
-            t.cloop = 1;
+            save_correlation_results(c, t, taps);
             if (!cn0_and_lock(c, t, pbuf, c.code_period * (double)c.extend_correlation_symbols, lane))
                 {
                     clear_tracking_vars(t);
+                    if (c.track_pilot) t.P_data_accu = make_float2(0.f, 0.f);
                     t.state = 0;
                     o.flags |= GSDR_TRK_F_LOSS_OF_LOCK;
                 }
@@ -552,7 +645,7 @@ __device__ inline void after_correlation(const TrkConst& c, TrkHot& t, LoopFilte
                             o.flags |= GSDR_TRK_F_VALID_OUTPUT;
                             t.P_data_accu = make_float2(0.f, 0.f);
                         }
-                    t.E_accu = t.P_accu = t.L_accu = make_float2(0.f, 0.f);
+                    t.VE_accu = t.E_accu = t.P_accu = t.L_accu = t.VL_accu = make_float2(0.f, 0.f);
                 }
         }
     if (t.flag_pll_180) o.flags |= GSDR_TRK_F_PLL_180;
@@ -584,10 +677,15 @@ __device__ __forceinline__ int wrap_code(int raw, int L)
 
 // One correlation chunk of kSpl samples per lane (n = n0 + tid + j*kTrkThreads),
 // KT taps, no branches inside: samples past the end are zero and their index clamped.
-template <int IT, bool FROM_WIN, bool FAST, int KT>
+// DATA: one more accumulator, acc[kMaxTrkTaps], on the data-component replica
+// s_data at the prompt tap's index (the pilot-tracking data correlator of
+// do_correlation_step, whose only tap sits at the prompt shift).
+template <int IT, bool FROM_WIN, bool FAST, int KT, bool DATA>
 __device__ __forceinline__ void correlate_chunk(const void* __restrict__ iq, const float2* s_win, const float* s_code,
-    const Prep& p, int n0, int vl, int L, const float (&sh_rem)[kMaxTrkTaps], float2& ph, float2 (&acc)[kMaxTrkTaps])
+    const float* s_data, const Prep& p, int n0, int vl, int L, const float (&sh_rem)[kMaxTrkTaps], float2& ph,
+    float2 (&acc)[kMaxTrkTaps + 1])
 {
+    constexpr int IPK = KT / 2;  // prompt slot: 1 of E,P,L / 2 of VE,E,P,L,VL
     float2 xs[kSpl];
 #pragma unroll
     for (int j = 0; j < kSpl; ++j)
@@ -619,30 +717,37 @@ __device__ __forceinline__ void correlate_chunk(const void* __restrict__ iq, con
                     const float cv = s_code[raw];
                     acc[k].x += tt.x * cv;
                     acc[k].y += tt.y * cv;
+                    if (DATA && k == IPK)
+                        {
+                            const float dv = s_data[raw];
+                            acc[kMaxTrkTaps].x += tt.x * dv;
+                            acc[kMaxTrkTaps].y += tt.y * dv;
+                        }
                 }
             ph = make_float2(ph.x * p.wstep.x - ph.y * p.wstep.y, ph.x * p.wstep.y + ph.y * p.wstep.x);
         }
 }
 
-template <int IT, int KT>
+template <int IT, int KT, bool DATA>
 __device__ __forceinline__ void correlate_call(const void* __restrict__ iq, const float2* s_win, const float* s_code,
-    const Prep& p, int vl, int L, const float (&sh_rem)[kMaxTrkTaps], float2& ph, float2 (&acc)[kMaxTrkTaps])
+    const float* s_data, const Prep& p, int vl, int L, const float (&sh_rem)[kMaxTrkTaps], float2& ph,
+    float2 (&acc)[kMaxTrkTaps + 1])
 {
     for (int n0 = 0; n0 < vl; n0 += kWinCore)
         {
             if (p.woff >= 0)
                 {
                     if (p.fast)
-                        correlate_chunk<IT, true, true, KT>(iq, s_win, s_code, p, n0, vl, L, sh_rem, ph, acc);
+                        correlate_chunk<IT, true, true, KT, DATA>(iq, s_win, s_code, s_data, p, n0, vl, L, sh_rem, ph, acc);
                     else
-                        correlate_chunk<IT, true, false, KT>(iq, s_win, s_code, p, n0, vl, L, sh_rem, ph, acc);
+                        correlate_chunk<IT, true, false, KT, DATA>(iq, s_win, s_code, s_data, p, n0, vl, L, sh_rem, ph, acc);
                 }
             else
                 {
                     if (p.fast)
-                        correlate_chunk<IT, false, true, KT>(iq, s_win, s_code, p, n0, vl, L, sh_rem, ph, acc);
+                        correlate_chunk<IT, false, true, KT, DATA>(iq, s_win, s_code, s_data, p, n0, vl, L, sh_rem, ph, acc);
                     else
-                        correlate_chunk<IT, false, false, KT>(iq, s_win, s_code, p, n0, vl, L, sh_rem, ph, acc);
+                        correlate_chunk<IT, false, false, KT, DATA>(iq, s_win, s_code, s_data, p, n0, vl, L, sh_rem, ph, acc);
                 }
         }
 }
@@ -656,18 +761,20 @@ __device__ __forceinline__ void correlate_call(const void* __restrict__ iq, cons
 // period +-1 sample), so the update hides the HBM latency.
 template <int IT>
 __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __restrict__ consts,
-    TrkChan* __restrict__ chans, const float* const* __restrict__ codes, const void* __restrict__ iq, uint64_t iq_first,
-    uint64_t iq_items, uint32_t max_epochs, gsdr_trk_epoch* __restrict__ out, uint32_t* __restrict__ nout, int code_pad,
-    uint64_t* __restrict__ timing)
+    TrkChan* __restrict__ chans, const float* const* __restrict__ codes, const float* const* __restrict__ data_codes,
+    const void* __restrict__ iq, uint64_t iq_first, uint64_t iq_items, uint32_t max_epochs, gsdr_trk_epoch* __restrict__ out,
+    uint32_t* __restrict__ nout, int code_pad, int data_pad, uint64_t* __restrict__ timing)
 {
+    // LDS: [replica | data replica (pilot tracking) | next call's input window]
     extern __shared__ float s_dyn[];
     float* s_code = s_dyn;
-    float2* s_win = reinterpret_cast<float2*>(s_dyn + code_pad);
+    float* s_data = s_dyn + code_pad;
+    float2* s_win = reinterpret_cast<float2*>(s_dyn + code_pad + data_pad);
     __shared__ LoopFilter s_lf;
     __shared__ float2 s_pbuf[kMaxCn0];
     __shared__ int s_state;
     __shared__ Prep prep;
-    __shared__ float2 s_red[kTrkThreads / 64][kMaxTrkTaps];
+    __shared__ float2 s_red[kTrkThreads / 64][kMaxTrkTaps + 1];
     const int ch = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const TrkConst& c = consts[ch];
@@ -693,9 +800,15 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
     const int L = c.code_samples;
     const int vl = c.vector_length;
     const bool use_window = vl <= kWinCore;
+    const bool data = c.track_pilot != 0;
     {
         const float* cd = codes[ch];
         for (int i = tid; i < L; i += kTrkThreads) s_code[i] = cd[i];
+        if (data)
+            {
+                const float* dd = data_codes[ch];
+                for (int i = tid; i < L; i += kTrkThreads) s_data[i] = dd[i];
+            }
     }
     int64_t win_base = INT64_MIN;  // absolute-index base of the staged window (uniform)
     uint32_t e = 0;
@@ -749,9 +862,9 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
             if (timing && tid == 0) tm1 = clock64();
             // ---- correlation: lane-interleaved samples, fp64 phasor anchor + fp32 steps
             const Prep p = prep;
-            float2 acc[kMaxTrkTaps];
+            float2 acc[kMaxTrkTaps + 1];
 #pragma unroll
-            for (int k = 0; k < kMaxTrkTaps; ++k) acc[k] = make_float2(0.f, 0.f);
+            for (int k = 0; k <= kMaxTrkTaps; ++k) acc[k] = make_float2(0.f, 0.f);
             float2 ph;
             {
                 const double phi = p.psi0 + (double)tid * p.theta;
@@ -764,13 +877,15 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
 #pragma unroll
             for (int k = 0; k < kMaxTrkTaps; ++k) sh_rem[k] = gsdr::sub_rn(c.shifts[k], p.rem_code);
             if (K <= 3)
-                correlate_call<IT, 3>(iq, s_win, s_code, p, vl, L, sh_rem, ph, acc);
+                correlate_call<IT, 3, false>(iq, s_win, s_code, s_data, p, vl, L, sh_rem, ph, acc);
+            else if (!data)
+                correlate_call<IT, kMaxTrkTaps, false>(iq, s_win, s_code, s_data, p, vl, L, sh_rem, ph, acc);
             else
-                correlate_call<IT, kMaxTrkTaps>(iq, s_win, s_code, p, vl, L, sh_rem, ph, acc);
+                correlate_call<IT, kMaxTrkTaps, true>(iq, s_win, s_code, s_data, p, vl, L, sh_rem, ph, acc);
 #pragma unroll
-            for (int k = 0; k < kMaxTrkTaps; ++k)
+            for (int k = 0; k <= kMaxTrkTaps; ++k)
                 {
-                    if (k < K)
+                    if (k < K || (k == kMaxTrkTaps && data))
                         {
 #pragma unroll
                             for (int off = 32; off > 0; off >>= 1)
@@ -783,7 +898,7 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
             if (lane == 0)
                 {
 #pragma unroll
-                    for (int k = 0; k < kMaxTrkTaps; ++k) s_red[wave][k] = acc[k];
+                    for (int k = 0; k <= kMaxTrkTaps; ++k) s_red[wave][k] = acc[k];
                 }
             __syncthreads();  // partials visible; every read of the LDS window done
             if (timing && tid == 0) tm2 = clock64();
@@ -807,12 +922,12 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                 }
             if (wave == 0)
                 {
-                    float2 taps[kMaxTrkTaps];
+                    float2 taps[kMaxTrkTaps + 1];
 #pragma unroll
-                    for (int k = 0; k < kMaxTrkTaps; ++k)
+                    for (int k = 0; k <= kMaxTrkTaps; ++k)
                         {
                             float2 r = make_float2(0.f, 0.f);
-                            if (k < K)
+                            if (k < K || (k == kMaxTrkTaps && data))
                                 {
 #pragma unroll
                                     for (int w = 0; w < kTrkThreads / 64; ++w)
@@ -859,6 +974,9 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                             r.prompt_i = o.prompt_i;
                             r.prompt_q = o.prompt_q;
                             r.evm = t.evm;
+                            r.data_prompt[0] = data ? taps[kMaxTrkTaps].x : 0.0F;
+                            r.data_prompt[1] = data ? taps[kMaxTrkTaps].y : 0.0F;
+                            r.reserved[0] = r.reserved[1] = 0;
                             out[(size_t)ch * max_epochs + e] = r;
                             if (timing)
                                 {
@@ -890,21 +1008,26 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
     if (tid < kMaxCn0) gc->prompt_buffer[tid] = s_pbuf[tid];
 }
 
-void preamble_register(uint32_t reg[5])
+// A secondary code / preamble string as the register acquire_secondary compares
+// with: the register holds the signs of the last pushes (1 = real < 0), newest at
+// bit 0, so string index i (oldest first) sits at bit len-1-i; a match for
+// real < 0 is character '0' (:923-967), so the register bit is 1 where the
+// character is '0'.  str_bits: bit i = (string[i] == '1').
+void code_registers(const char* str, int len, uint32_t reg[5], uint32_t str_bits[5])
 {
-    // GPS_CA_PREAMBLE_SYMBOLS_STR (GPS_L1_CA.h:73); oldest entry (string index 0)
-    // at register bit 159.  A register bit is 1 where the prompt's real part is
-    // negative; acquire_secondary counts a match for real < 0 against '0', so the
-    // register form of the string is 1 where the character is '0'.
-    static const char kStr[161] =
-        "1111111111111111111100000000000000000000000000000000000000000000000000000000000011111111111111111111000000000000"
-        "000000001111111111111111111111111111111111111111";
-    for (int w = 0; w < 5; ++w) reg[w] = 0u;
-    for (int i = 0; i < kPreambleLen; ++i)
+    for (int w = 0; w < 5; ++w) reg[w] = str_bits[w] = 0u;
+    for (int i = 0; i < len; ++i)
         {
-            const int bit = kPreambleLen - 1 - i;
-            if (kStr[i] == '0') reg[bit >> 5] |= 1u << (bit & 31);
+            const int bit = len - 1 - i;
+            if (str[i] == '0') reg[bit >> 5] |= 1u << (bit & 31);
+            if (str[i] == '1') str_bits[i >> 5] |= 1u << (i & 31);
         }
+}
+
+void set_secondary(TrkConst& c, const char* str, int len)
+{
+    c.sec_len = len;
+    code_registers(str, len, c.preamble, c.sec_str);
 }
 
 }  // namespace
@@ -921,6 +1044,9 @@ struct gsdr_trk
     TrkChan* d_snap[2]{nullptr, nullptr};
     std::vector<float*> code_bufs;
     float** d_codes{nullptr};
+    std::vector<float*> data_code_bufs;  // pilot tracking: data-component replicas
+    float** d_data_codes{nullptr};
+    std::vector<int> data_code_len;
     gsdr_trk_epoch* d_out{nullptr};
     uint32_t* d_nout{nullptr};
     uint32_t out_cap{0};
@@ -928,6 +1054,7 @@ struct gsdr_trk
     uint64_t iq_cap{0};
     size_t lds_bytes{0};
     int code_pad{1024};  // floats reserved for the replica ahead of the LDS window
+    int data_pad{0};     // floats reserved for the data replica (pilot tracking)
     // GSDR_TRK_TIMING=1: per-phase clock64 stamps of every call, summarised on destroy
     bool timing_on{false};
     uint64_t* d_timing{nullptr};
@@ -985,22 +1112,78 @@ void sm_set(SmConst& k, float alpha, float min_value, float offset, int samples)
     k.samples_init = std::max(1, samples);
 }
 
-// constructor (dll_pll_veml_tracking.cc:85-560) for one channel slot, GPS L1 C/A
+// tap shifts (:466-507 / :850-862), in replica samples
+void set_shifts(const gsdr_trk_conf& cf, TrkConst& c)
+{
+    const float spc = (float)c.code_samples_per_chip;
+    if (c.veml)
+        {
+            c.shifts[0] = -cf.very_early_late_space_chips * spc;
+            c.shifts[1] = -cf.early_late_space_chips * spc;
+            c.shifts[2] = 0.0F;
+            c.shifts[3] = cf.early_late_space_chips * spc;
+            c.shifts[4] = cf.very_early_late_space_chips * spc;
+        }
+    else
+        {
+            c.shifts[0] = -cf.early_late_space_chips * spc;
+            c.shifts[1] = 0.0F;
+            c.shifts[2] = cf.early_late_space_chips * spc;
+        }
+}
+
+// signal table of the constructor (dll_pll_veml_tracking.cc:170-430)
+struct SignalParams
+{
+    double carrier_hz, period_s, chip_rate;
+    int length_chips, samples_per_chip, symbols_per_bit, veml;
+};
+SignalParams signal_params(int signal)
+{
+    if (signal == GSDR_SIGNAL_GAL_1B) return {kGalE1Hz, kGalE1Period, kGalE1Rate, kGalE1Length, 2, 1, 1};
+    if (signal == GSDR_SIGNAL_BDS_B1) return {kBdsB1Hz, kBdsB1Period, kBdsB1Rate, kBdsB1Length, 1, 20, 0};
+    return {kGpsL1Hz, kGpsCaPeriod, kGpsCaRate, kGpsCaLength, 1, kGpsCaSymbolsPerBit, 0};
+}
+
+// constructor (dll_pll_veml_tracking.cc:85-560) for one channel slot
 void init_channel(const gsdr_trk_conf& cf, TrkConst& c, TrkChan& ch)
 {
     std::memset(&c, 0, sizeof(c));
     std::memset(&ch, 0, sizeof(ch));
+    const SignalParams sp = signal_params(cf.signal);
     c.fs_in = cf.fs_in;
-    c.code_period = kGpsCaPeriod;
-    c.code_chip_rate = kGpsCaRate;
-    c.signal_carrier_freq = kGpsL1Hz;
+    c.code_period = sp.period_s;
+    c.code_chip_rate = sp.chip_rate;
+    c.signal_carrier_freq = sp.carrier_hz;
+    c.veml = sp.veml;
+    c.iE = c.veml ? 1 : 0;
+    c.iP = c.veml ? 2 : 1;
+    c.iL = c.veml ? 3 : 2;
+    if (cf.signal == GSDR_SIGNAL_GAL_1B)
+        {
+            c.track_pilot = cf.track_pilot ? 1 : 0;
+            c.secondary = c.track_pilot;
+            if (c.secondary) set_secondary(c, kGalE1cSecondary, 25);
+        }
+    else if (cf.signal == GSDR_SIGNAL_BDS_B1)
+        {
+            // D1 by default; gsdr_trk_start switches GEO PRNs to the D2 preamble
+            c.secondary = 1;
+            set_secondary(c, kBdsB1Nh, 20);
+            uint32_t reg[5], bits[5];
+            code_registers(kBdsB1Nh, 20, reg, bits);
+            c.data_sec_len = 20;
+            c.data_sec_str = bits[0];
+        }
+    else
+        set_secondary(c, kGpsCaPreamble, kPreambleLen);
     c.carrier_lock_threshold = cf.carrier_lock_th;
     c.current_correlation_time_s = c.code_period;
     c.early_late_space_chips = cf.early_late_space_chips;
     c.vector_length = (int32_t)cf.vector_length;
-    c.code_length_chips = kGpsCaLength;
-    c.code_samples_per_chip = 1;
-    c.symbols_per_bit = kGpsCaSymbolsPerBit;
+    c.code_length_chips = sp.length_chips;
+    c.code_samples_per_chip = sp.samples_per_chip;
+    c.symbols_per_bit = sp.symbols_per_bit;
     c.cn0_samples = cf.cn0_samples;
     c.cn0_min = cf.cn0_min;
     c.max_code_lock_fail = cf.max_code_lock_fail;
@@ -1012,11 +1195,8 @@ void init_channel(const gsdr_trk_conf& cf, TrkConst& c, TrkChan& ch)
     c.enable_fll_pull_in = cf.enable_fll_pull_in;
     c.enable_fll_steady_state = cf.enable_fll_steady_state;
     c.carrier_aiding = cf.carrier_aiding;
-    c.n_taps = 3;
-    c.shifts[0] = -cf.early_late_space_chips * (float)c.code_samples_per_chip;
-    c.shifts[1] = 0.0F;
-    c.shifts[2] = cf.early_late_space_chips * (float)c.code_samples_per_chip;
-    preamble_register(c.preamble);
+    c.n_taps = c.veml ? 5 : 3;
+    set_shifts(cf, c);
     cf_set_params(c.cf, cf.fll_bw_hz, cf.pll_bw_hz, cf.pll_filter_order);
     // Exponential_Smoother defaults (exponential_smoother.h:58-63) + dll_pll_veml_tracking.cc:540-552
     sm_set(c.sm[0], cf.cn0_smoother_alpha, 25.0F, 12.0F, cf.cn0_smoother_samples / (int)(c.code_period * 1000.0));
@@ -1051,9 +1231,9 @@ int ensure_out(gsdr_trk* k, uint32_t max_epochs)
 // latency chain and co-resident FFT waves would slow every call down.
 constexpr size_t kCuLds = 160 * 1024;
 constexpr size_t kStaticLdsMargin = 4 * 1024;  // the kernel's static __shared__ arrays
-size_t lds_for(int code_pad)
+size_t lds_for(int code_pad, int data_pad)
 {
-    const size_t need = (size_t)code_pad * sizeof(float) + (size_t)(kWinCore + kHalo) * sizeof(float2);
+    const size_t need = (size_t)(code_pad + data_pad) * sizeof(float) + (size_t)(kWinCore + kHalo) * sizeof(float2);
     return std::max(need, kCuLds - kStaticLdsMargin);
 }
 
@@ -1092,10 +1272,12 @@ int launch(gsdr_trk* k, const void* iq, uint64_t iq_first, uint64_t iq_items, ui
     const dim3 grid(k->conf.max_channels);
     if (k->conf.item_type == GSDR_ITEM_GR_COMPLEX)
         hipLaunchKernelGGL((trk_kernel<GSDR_ITEM_GR_COMPLEX>), grid, dim3(kTrkThreads), k->lds_bytes, s, k->d_consts, k->d_chans,
-            (const float* const*)k->d_codes, iq, iq_first, iq_items, max_epochs, out, nout, k->code_pad, timing);
+            (const float* const*)k->d_codes, (const float* const*)k->d_data_codes, iq, iq_first, iq_items, max_epochs, out,
+            nout, k->code_pad, k->data_pad, timing);
     else
         hipLaunchKernelGGL((trk_kernel<GSDR_ITEM_CSHORT>), grid, dim3(kTrkThreads), k->lds_bytes, s, k->d_consts, k->d_chans,
-            (const float* const*)k->d_codes, iq, iq_first, iq_items, max_epochs, out, nout, k->code_pad, timing);
+            (const float* const*)k->d_codes, (const float* const*)k->d_data_codes, iq, iq_first, iq_items, max_epochs, out,
+            nout, k->code_pad, k->data_pad, timing);
     GSDR_HIP(hipGetLastError());
     if (k->profiling)
         {
@@ -1154,8 +1336,8 @@ int gsdr_trk_create(int device, const gsdr_trk_conf* conf, gsdr_trk** out)
     *out = nullptr;
     GSDR_REQUIRE(conf->fs_in > 0.0, GSDR_E_ARG, "gsdr_trk_create: fs_in must be > 0");
     GSDR_REQUIRE(conf->max_channels > 0, GSDR_E_ARG, "gsdr_trk_create: max_channels must be > 0");
-    GSDR_REQUIRE(conf->signal == GSDR_SIGNAL_GPS_1C, GSDR_E_UNSUPPORTED, "gsdr_trk_create: signal %d not implemented",
-        conf->signal);
+    GSDR_REQUIRE(conf->signal >= GSDR_SIGNAL_GPS_1C && conf->signal <= GSDR_SIGNAL_BDS_B1, GSDR_E_UNSUPPORTED,
+        "gsdr_trk_create: signal %d not implemented", conf->signal);
     GSDR_REQUIRE(conf->item_type == GSDR_ITEM_GR_COMPLEX || conf->item_type == GSDR_ITEM_CSHORT, GSDR_E_ARG,
         "gsdr_trk_create: unknown item type %d", conf->item_type);
     GSDR_REQUIRE(conf->extend_correlation_symbols == 1, GSDR_E_UNSUPPORTED,
@@ -1175,15 +1357,24 @@ int gsdr_trk_create(int device, const gsdr_trk_conf* conf, gsdr_trk** out)
     GSDR_REQUIRE(k, GSDR_E_ALLOC, "gsdr_trk_create: out of host memory");
     k->device = device;
     k->conf = *conf;
-    if (k->conf.vector_length == 0)
-        k->conf.vector_length = (uint32_t)std::lround(conf->fs_in / (kGpsCaRate / kGpsCaLength));
+    // GPS L1 C/A and BeiDou B1I force track_pilot off (dll_pll_veml_tracking.cc:183, :402)
+    if (k->conf.signal != GSDR_SIGNAL_GAL_1B) k->conf.track_pilot = 0;
+    {
+        // the adapters' vector_length = round(fs_in / (chip rate / code length))
+        const SignalParams sp = signal_params(k->conf.signal);
+        if (k->conf.vector_length == 0)
+            k->conf.vector_length = (uint32_t)std::lround(conf->fs_in / (sp.chip_rate / (double)sp.length_chips));
+    }
     const uint32_t nch = k->conf.max_channels;
     k->h_consts.resize(nch);
     k->h_chans.resize(nch);
     for (uint32_t c = 0; c < nch; ++c) init_channel(k->conf, k->h_consts[c], k->h_chans[c]);
     k->code_bufs.assign(nch, nullptr);
+    k->data_code_bufs.assign(nch, nullptr);
+    k->data_code_len.assign(nch, 0);
     k->code_pad = 1024;  // grows with the longest replica started (gsdr_trk_start)
-    k->lds_bytes = lds_for(k->code_pad);
+    k->data_pad = 0;
+    k->lds_bytes = lds_for(k->code_pad, k->data_pad);
     if (const char* tv = std::getenv("GSDR_TRK_TIMING")) k->timing_on = std::atoi(tv) != 0;
     hipError_t e = hipStreamCreateWithFlags(&k->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipMalloc(&k->d_consts, nch * sizeof(TrkConst));
@@ -1194,14 +1385,19 @@ int gsdr_trk_create(int device, const gsdr_trk_conf* conf, gsdr_trk** out)
     if (e == hipSuccess) e = hipMalloc(&k->d_nout, nch * sizeof(uint32_t));
     for (uint32_t c = 0; c < nch && e == hipSuccess; ++c) e = hipMalloc(&k->code_bufs[c], kMaxCodeFloats * sizeof(float));
     if (e == hipSuccess) e = hipMemcpy(k->d_codes, k->code_bufs.data(), nch * sizeof(float*), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(&k->d_data_codes, nch * sizeof(float*));
+    if (k->conf.track_pilot)
+        for (uint32_t c = 0; c < nch && e == hipSuccess; ++c)
+            e = hipMalloc(&k->data_code_bufs[c], kMaxCodeFloats * sizeof(float));
+    if (e == hipSuccess) e = hipMemcpy(k->d_data_codes, k->data_code_bufs.data(), nch * sizeof(float*), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(k->d_consts, k->h_consts.data(), nch * sizeof(TrkConst), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(k->d_chans, k->h_chans.data(), nch * sizeof(TrkChan), hipMemcpyHostToDevice);
     if (e == hipSuccess)
         e = hipFuncSetAttribute((const void*)trk_kernel<GSDR_ITEM_GR_COMPLEX>, hipFuncAttributeMaxDynamicSharedMemorySize,
-            (int)lds_for(kMaxCodeFloats));
+            (int)(kCuLds - kStaticLdsMargin));
     if (e == hipSuccess)
         e = hipFuncSetAttribute((const void*)trk_kernel<GSDR_ITEM_CSHORT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-            (int)lds_for(kMaxCodeFloats));
+            (int)(kCuLds - kStaticLdsMargin));
     if (e != hipSuccess)
         {
             gsdr::set_error("gsdr_trk_create: %s", hipGetErrorString(e));
@@ -1254,7 +1450,10 @@ void gsdr_trk_destroy(gsdr_trk* k)
     for (hipEvent_t e : k->prof_pool) (void)hipEventDestroy(e);
     for (float* p : k->code_bufs)
         if (p) (void)hipFree(p);
-    void* bufs[] = {k->d_consts, k->d_chans, k->d_snap[0], k->d_snap[1], k->d_codes, k->d_nout, k->d_out, k->d_iq};
+    for (float* p : k->data_code_bufs)
+        if (p) (void)hipFree(p);
+    void* bufs[] = {k->d_consts, k->d_chans, k->d_snap[0], k->d_snap[1], k->d_codes, k->d_data_codes, k->d_nout, k->d_out,
+        k->d_iq};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     if (k->stream) (void)hipStreamDestroy(k->stream);
@@ -1269,6 +1468,9 @@ int gsdr_trk_start(gsdr_trk* k, int ch, uint32_t prn, const float* code, int cod
         k->conf.max_channels);
     GSDR_REQUIRE(code_samples >= 1 && code_samples <= kMaxCodeFloats, GSDR_E_UNSUPPORTED,
         "gsdr_trk_start: code replica of %d samples outside [1,%d]", code_samples, kMaxCodeFloats);
+    GSDR_REQUIRE(!k->conf.track_pilot || k->data_code_len[ch] == code_samples, GSDR_E_STATE,
+        "gsdr_trk_start: pilot tracking needs gsdr_trk_set_data_code with %d samples for channel %d first", code_samples,
+        ch);
     std::lock_guard<std::mutex> lk(k->mu);
     gsdr::DeviceGuard g(k->device);
     // the device copy is authoritative between launches (the loop runs there)
@@ -1279,6 +1481,29 @@ int gsdr_trk_start(gsdr_trk* k, int ch, uint32_t prn, const float* code, int cod
     TrkHot& t = tc.h;
     // start_tracking (:640-882)
     c.prn = prn;
+    if (k->conf.signal == GSDR_SIGNAL_BDS_B1)
+        {
+            uint32_t reg[5], bits[5];
+            if ((prn > 0 && prn < 6) || prn > 58)
+                {
+                    // GEO (D2): D2 preamble search, 2 symbols per bit (:762-778)
+                    c.symbols_per_bit = 2;
+                    c.secondary = 0;
+                    set_secondary(c, kBdsB1GeoPreamble, 22);
+                    c.data_sec_len = 0;
+                    c.data_sec_str = 0;
+                }
+            else
+                {
+                    // D1: NH code, wiped from the data symbols too (:779-795)
+                    c.symbols_per_bit = 20;
+                    c.secondary = 1;
+                    set_secondary(c, kBdsB1Nh, 20);
+                    code_registers(kBdsB1Nh, 20, reg, bits);
+                    c.data_sec_len = 20;
+                    c.data_sec_str = bits[0];
+                }
+        }
     c.code_samples = code_samples;
     c.acq_sample_stamp = acq_samplestamp;
     double acq_code_phase_samples = acq_delay_samples;
@@ -1295,8 +1520,7 @@ int gsdr_trk_start(gsdr_trk* k, int ch, uint32_t prn, const float* code, int cod
     t.carrier_lock_test = 1.0;
     t.cn0_db_hz = 0.0;
     t.evm = 0.0;
-    c.shifts[0] = -k->conf.early_late_space_chips * (float)c.code_samples_per_chip;
-    c.shifts[2] = k->conf.early_late_space_chips * (float)c.code_samples_per_chip;
+    set_shifts(k->conf, c);
     c.current_correlation_time_s = c.code_period;
     cf_set_params(c.cf, k->conf.fll_bw_hz, k->conf.pll_bw_hz, k->conf.pll_filter_order);
     tc.code_filter.bw = k->conf.dll_bw_hz;
@@ -1339,13 +1563,36 @@ int gsdr_trk_start(gsdr_trk* k, int ch, uint32_t prn, const float* code, int cod
     sm_reset(t, 1);
     t.next_sample = nitems_read + (uint64_t)(int64_t)offset;
     *first_sample = t.next_sample;
-    k->code_pad = std::max(k->code_pad, (code_samples + 1) & ~1);
-    k->lds_bytes = lds_for(k->code_pad);
+    {
+        const int cp = std::max(k->code_pad, (code_samples + 1) & ~1);
+        const int dp = k->conf.track_pilot ? cp : 0;
+        GSDR_REQUIRE(lds_for(cp, dp) <= kCuLds - kStaticLdsMargin, GSDR_E_UNSUPPORTED,
+            "gsdr_trk_start: replica of %d samples does not fit the LDS next to the input window", code_samples);
+        k->code_pad = cp;
+        k->data_pad = dp;
+    }
+    k->lds_bytes = lds_for(k->code_pad, k->data_pad);
     GSDR_HIP(hipMemcpyAsync(k->code_bufs[ch], code, (size_t)code_samples * sizeof(float), hipMemcpyHostToDevice,
         k->stream));
     GSDR_HIP(hipMemcpyAsync(k->d_consts + ch, &c, sizeof(TrkConst), hipMemcpyHostToDevice, k->stream));
     GSDR_HIP(hipMemcpyAsync(k->d_chans + ch, &tc, sizeof(TrkChan), hipMemcpyHostToDevice, k->stream));
     GSDR_HIP(hipStreamSynchronize(k->stream));
+    return GSDR_OK;
+}
+
+int gsdr_trk_set_data_code(gsdr_trk* k, int ch, const float* data_code, int code_samples)
+{
+    GSDR_REQUIRE(k && data_code, GSDR_E_ARG, "gsdr_trk_set_data_code: null argument");
+    GSDR_REQUIRE(ch >= 0 && ch < (int)k->conf.max_channels, GSDR_E_ARG, "gsdr_trk_set_data_code: channel %d", ch);
+    GSDR_REQUIRE(k->conf.track_pilot, GSDR_E_STATE, "gsdr_trk_set_data_code: the handle does not track a pilot");
+    GSDR_REQUIRE(code_samples >= 1 && code_samples <= kMaxCodeFloats, GSDR_E_UNSUPPORTED,
+        "gsdr_trk_set_data_code: replica of %d samples outside [1,%d]", code_samples, kMaxCodeFloats);
+    std::lock_guard<std::mutex> lk(k->mu);
+    gsdr::DeviceGuard g(k->device);
+    GSDR_HIP(hipMemcpyAsync(k->data_code_bufs[ch], data_code, (size_t)code_samples * sizeof(float),
+        hipMemcpyHostToDevice, k->stream));
+    GSDR_HIP(hipStreamSynchronize(k->stream));
+    k->data_code_len[ch] = code_samples;
     return GSDR_OK;
 }
 

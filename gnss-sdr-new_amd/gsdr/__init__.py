@@ -37,9 +37,12 @@ EXPORTED = [
     "gsdr_trk_conf_default", "gsdr_trk_create", "gsdr_trk_destroy", "gsdr_trk_start", "gsdr_trk_stop",
     "gsdr_trk_run_device", "gsdr_trk_run", "gsdr_trk_get_channel", "gsdr_trk_save_state", "gsdr_trk_restore_state",
     "gsdr_trk_set_profiling", "gsdr_trk_read_profile", "gsdr_acq_set_cu_mask", "gsdr_trk_set_cu_mask",
+    "gsdr_trk_set_data_code",
 ]
 
 SIGNAL_GPS_1C = 0
+SIGNAL_GAL_1B = 1
+SIGNAL_BDS_B1 = 2
 TRK_F_VALID_OUTPUT, TRK_F_LOSS_OF_LOCK, TRK_F_PLL_180, TRK_F_BIT_SYNC = 1, 2, 4, 8
 
 # include/gsdr.h gsdr_trk_conf / gsdr_trk_epoch (C layout)
@@ -53,15 +56,16 @@ TRK_CONF_DTYPE = np.dtype([
     ("extend_correlation_symbols", "i4"), ("cn0_samples", "i4"), ("cn0_smoother_samples", "i4"),
     ("carrier_lock_test_smoother_samples", "i4"), ("cn0_min", "i4"), ("max_code_lock_fail", "i4"),
     ("max_carrier_lock_fail", "i4"), ("enable_fll_pull_in", "i4"), ("enable_fll_steady_state", "i4"),
-    ("carrier_aiding", "i4"), ("high_dyn", "i4")], align=True)
-assert TRK_CONF_DTYPE.itemsize == 136
+    ("carrier_aiding", "i4"), ("high_dyn", "i4"), ("track_pilot", "i4")], align=True)
+assert TRK_CONF_DTYPE.itemsize == 144
 
 TRK_EPOCH_DTYPE = np.dtype([
     ("sample_counter", "u8"), ("state", "i4"), ("consumed", "i4"), ("taps", "f4", (10,)),
     ("rem_carr_phase_rad", "f4"), ("flags", "i4"), ("carrier_doppler_hz", "f8"), ("code_freq_chips", "f8"),
     ("rem_code_phase_samples", "f8"), ("acc_carrier_phase_rad", "f8"), ("cn0_db_hz", "f8"),
-    ("carrier_lock_test", "f8"), ("prompt_i", "f8"), ("prompt_q", "f8"), ("evm", "f8")], align=True)
-assert TRK_EPOCH_DTYPE.itemsize == 136
+    ("carrier_lock_test", "f8"), ("prompt_i", "f8"), ("prompt_q", "f8"), ("evm", "f8"), ("data_prompt", "f4", (2,)),
+    ("reserved", "i4", (2,))], align=True)
+assert TRK_EPOCH_DTYPE.itemsize == 152
 
 
 class GsdrError(RuntimeError):
@@ -190,6 +194,7 @@ def load():
     L.gsdr_trk_destroy.restype = None
     L.gsdr_trk_start.argtypes = [P, I, U32, P, I, ctypes.c_double, ctypes.c_double, U64, U64, P]
     L.gsdr_trk_stop.argtypes = [P, I]
+    L.gsdr_trk_set_data_code.argtypes = [P, I, P, I]
     L.gsdr_trk_run_device.argtypes = [P, P, U64, U64, U32, P, P, P]
     L.gsdr_trk_run.argtypes = [P, P, U64, U64, U32, P, P]
     L.gsdr_trk_get_channel.argtypes = [P, I, P, P, P, P]
@@ -439,8 +444,13 @@ class Tracking:
         except Exception:
             pass
 
-    def start(self, ch, prn, code, acq_delay_samples, acq_doppler_hz, acq_samplestamp, nitems_read):
+    def start(self, ch, prn, code, acq_delay_samples, acq_doppler_hz, acq_samplestamp, nitems_read, data_code=None):
+        """start_tracking + the state-1 pull-in call; data_code: the data component's
+        replica for pilot tracking (Galileo E1 with track_pilot)."""
         code = np.ascontiguousarray(code, np.float32)
+        if data_code is not None:
+            dc = np.ascontiguousarray(data_code, np.float32)
+            _check(load().gsdr_trk_set_data_code(self._h, int(ch), _ptr(dc), len(dc)))
         first = ctypes.c_uint64()
         _check(load().gsdr_trk_start(self._h, int(ch), int(prn), _ptr(code), len(code), float(acq_delay_samples),
                                      float(acq_doppler_hz), int(acq_samplestamp), int(nitems_read),

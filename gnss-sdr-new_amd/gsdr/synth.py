@@ -244,7 +244,8 @@ def gal_e1_iq(fs, n_samples, sats, seed_offset=0, noise=True, dtype=np.complex64
     sec = np.array([1.0 if c == "0" else -1.0 for c in GAL_E1C_SECONDARY])
     for s in sats:
         amp = np.sqrt(10.0 ** (s.cn0_dbhz / 10.0) / fs)
-        cp = t * 1.023e6 - s.code_delay_chips          # chips
+        # the code rate follows the carrier Doppler (1 + f_d / f_E1)
+        cp = t * 1.023e6 * (1.0 + s.doppler_hz / GAL_E1_HZ) - s.code_delay_chips  # chips
         chip = np.floor(cp).astype(np.int64)
         frac = cp - chip
         s11 = np.where(frac < 0.5, 1.0, -1.0)
@@ -264,24 +265,41 @@ def gal_e1_iq(fs, n_samples, sats, seed_offset=0, noise=True, dtype=np.complex64
     return out.astype(dtype)
 
 
+BDS_D2_PREAMBLE_BITS = (1, 1, 1, 0, 0, 0, 1, 0, 0, 1, 0)  # BEIDOU_B1I_GEO_PREAMBLE_SYMBOLS_STR, 2 symbols/bit
+
+
+def bds_is_geo(prn):
+    return 0 < prn < 6 or prn > 58
+
+
 def bds_b1i_iq(fs, n_samples, sats, seed_offset=0, noise=True, dtype=np.complex64):
-    """B1I D1 signal: code x NH(20) x 50 bps data; sats are Satellite objects whose
-    code_delay_chips is in B1I chips (2.046 Mcps)."""
+    """B1I signal; sats are Satellite objects whose code_delay_chips is in B1I chips
+    (2.046 Mcps).  MEO/IGSO (D1): code x NH(20) x 50 bps data.  GEO (PRN 1-5,
+    59-63, D2): code x 500 bps data (2 code periods per bit) carrying the D2
+    preamble every 300 bits."""
     rng = np.random.default_rng(SEED + 3000 + seed_offset)
     t = np.arange(n_samples, dtype=np.float64) / fs
     out = np.zeros(n_samples, np.complex128)
     nh = np.array([1.0 if c == "0" else -1.0 for c in BDS_B1I_NH])
     for s in sats:
         amp = np.sqrt(10.0 ** (s.cn0_dbhz / 10.0) / fs)
-        cp = t * 2.046e6 - s.code_delay_chips
+        cp = t * 2.046e6 * (1.0 + s.doppler_hz / BDS_B1I_HZ) - s.code_delay_chips
         chip = np.floor(cp).astype(np.int64)
         epoch = np.floor_divide(chip, 2046)
         c = bds_b1i_chips(s.prn)[chip % 2046]
-        bit = np.floor_divide(epoch, 20)
+        geo = bds_is_geo(s.prn)
+        per = 2 if geo else 20
+        bit = np.floor_divide(epoch, per)
         nb = int(bit.max() - bit.min()) + 2
         bits = np.where(np.random.default_rng(SEED + 53 * s.prn).random(nb) < 0.5, -1.0, 1.0)
-        out += amp * c * nh[epoch % 20] * bits[(bit - bit.min()) % nb] * np.exp(
-            1j * (2 * np.pi * s.doppler_hz * t + s.phase))
+        if geo:
+            pre = np.array([1.0 if b else -1.0 for b in BDS_D2_PREAMBLE_BITS])
+            for k in range(0, nb - len(pre) + 1, 300):
+                bits[k:k + len(pre)] = pre
+            mod = np.ones_like(cp)
+        else:
+            mod = nh[epoch % 20]
+        out += amp * c * mod * bits[(bit - bit.min()) % nb] * np.exp(1j * (2 * np.pi * s.doppler_hz * t + s.phase))
     if noise:
         out += (rng.standard_normal(n_samples) + 1j * rng.standard_normal(n_samples)) * np.sqrt(0.5)
     return out.astype(dtype)

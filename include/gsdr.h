@@ -256,6 +256,8 @@ int gsdr_corr_dump_indices(gsdr_corr* corr, int channel, float rem_code_phase_ch
 typedef struct gsdr_trk gsdr_trk;
 
 #define GSDR_SIGNAL_GPS_1C 0 /* GPS L1 C/A (dll_pll_veml_tracking.cc:170-191) */
+#define GSDR_SIGNAL_GAL_1B 1 /* Galileo E1 OS, VEML 5 taps, pilot (E1C) or data (E1B) tracking (:258-290) */
+#define GSDR_SIGNAL_BDS_B1 2 /* BeiDou B1I D1 (NH secondary code) / D2 GEO (preamble) (:391-411, :762-795) */
 
 /* Mirrors Dll_Pll_Conf (src/algorithms/tracking/libs/dll_pll_conf.h:30-84);
  * gsdr_trk_conf_default() fills the reference defaults (incl. the gflags
@@ -295,6 +297,7 @@ typedef struct gsdr_trk_conf
     int32_t enable_fll_steady_state;
     int32_t carrier_aiding;
     int32_t high_dyn; /* only 0 in this version */
+    int32_t track_pilot; /* Dll_Pll_Conf::track_pilot (default 1); forced 0 for GPS L1 C/A and BeiDou B1I */
 } gsdr_trk_conf;
 
 /* One general_work call of one channel (written for every call that ran a
@@ -317,6 +320,8 @@ typedef struct gsdr_trk_epoch
     double prompt_i;               /* Prompt_I (valid output only) */
     double prompt_q;               /* Prompt_Q (valid output only) */
     double evm;                    /* EVM (fork indicator, :1027-1053) */
+    float data_prompt[2];          /* pilot tracking: the data-component prompt of the call (d_Prompt_Data[0]) */
+    int32_t reserved[2];
 } gsdr_trk_epoch;
 
 #define GSDR_TRK_F_VALID_OUTPUT 1 /* Flag_valid_symbol_output: a Gnss_Synchro was emitted */
@@ -337,6 +342,11 @@ void gsdr_trk_destroy(gsdr_trk* trk);
 int gsdr_trk_start(gsdr_trk* trk, int ch, uint32_t prn, const float* code, int code_samples,
     double acq_delay_samples, double acq_doppler_hz, uint64_t acq_samplestamp, uint64_t nitems_read,
     uint64_t* first_sample);
+/* Pilot tracking (track_pilot, Galileo E1): the data component's replica for the
+ * extra prompt correlator (d_correlator_data_cpu.set_local_code_and_taps,
+ * dll_pll_veml_tracking.cc:681-689, e.g. galileo_e1_code_gen_sinboc11_float of
+ * E1B), code_samples floats.  Call before gsdr_trk_start for that channel. */
+int gsdr_trk_set_data_code(gsdr_trk* trk, int ch, const float* data_code, int code_samples);
 /* stop_tracking: channel to state 0 (standby). */
 int gsdr_trk_stop(gsdr_trk* trk, int ch);
 

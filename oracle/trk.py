@@ -1,5 +1,6 @@
 """ORACLE — test infrastructure only.  ctypes front-end of oracle/trk_oracle.c,
-the CPU restatement of dll_pll_veml_tracking (GPS L1 C/A) and its loop library."""
+the CPU restatement of dll_pll_veml_tracking (GPS L1 C/A, Galileo E1, BeiDou B1I)
+and its loop library."""
 import ctypes
 
 import numpy as np
@@ -23,15 +24,16 @@ TRK_CONF_DTYPE = np.dtype([
     ("extend_correlation_symbols", "i4"), ("cn0_samples", "i4"), ("cn0_smoother_samples", "i4"),
     ("carrier_lock_test_smoother_samples", "i4"), ("cn0_min", "i4"), ("max_code_lock_fail", "i4"),
     ("max_carrier_lock_fail", "i4"), ("enable_fll_pull_in", "i4"), ("enable_fll_steady_state", "i4"),
-    ("carrier_aiding", "i4"), ("high_dyn", "i4")], align=True)
-assert TRK_CONF_DTYPE.itemsize == 136
+    ("carrier_aiding", "i4"), ("high_dyn", "i4"), ("track_pilot", "i4")], align=True)
+assert TRK_CONF_DTYPE.itemsize == 144
 
 TRK_EPOCH_DTYPE = np.dtype([
     ("sample_counter", "u8"), ("state", "i4"), ("consumed", "i4"), ("taps", "f4", (10,)),
     ("rem_carr_phase_rad", "f4"), ("flags", "i4"), ("carrier_doppler_hz", "f8"), ("code_freq_chips", "f8"),
     ("rem_code_phase_samples", "f8"), ("acc_carrier_phase_rad", "f8"), ("cn0_db_hz", "f8"),
-    ("carrier_lock_test", "f8"), ("prompt_i", "f8"), ("prompt_q", "f8"), ("evm", "f8")], align=True)
-assert TRK_EPOCH_DTYPE.itemsize == 136
+    ("carrier_lock_test", "f8"), ("prompt_i", "f8"), ("prompt_q", "f8"), ("evm", "f8"), ("data_prompt", "f4", (2,)),
+    ("reserved", "i4", (2,))], align=True)
+assert TRK_EPOCH_DTYPE.itemsize == 152
 
 F_VALID_OUTPUT, F_LOSS_OF_LOCK, F_PLL_180, F_BIT_SYNC = 1, 2, 4, 8
 
@@ -47,7 +49,9 @@ def _lib():
         L.orc_trk_create.restype = _p
         L.orc_trk_destroy.argtypes = [_p]
         L.orc_trk_set_assoc.argtypes = [_p, _i]
-        L.orc_trk_start.argtypes = [_p, _p, _i, _d, _d, _u64, _u64, _p]
+        L.orc_trk_start.argtypes = [_p, ctypes.c_uint32, _p, _i, _d, _d, _u64, _u64, _p]
+        L.orc_trk_set_data_code.argtypes = [_p, _p, _i]
+        L.orc_trk_set_data_code.restype = _i
         L.orc_trk_start.restype = _i
         L.orc_trk_call.argtypes = [_p, _p, _u64, _p]
         L.orc_trk_call.restype = _i
@@ -82,7 +86,7 @@ def dll_nc_e_minus_l_normalized(E, L, spc=0.5, slope=1.0, y_intercept=1.0):
 
 
 class Channel:
-    """One dll_pll_veml_tracking channel (GPS L1 C/A)."""
+    """One dll_pll_veml_tracking channel (GPS L1 C/A, Galileo E1, BeiDou B1I)."""
 
     def __init__(self, conf):
         self._conf = np.ascontiguousarray(conf, TRK_CONF_DTYPE)
@@ -106,10 +110,14 @@ class Channel:
     def set_assoc(self, assoc):
         _lib().orc_trk_set_assoc(self._h, assoc)
 
-    def start(self, code, acq_delay_samples, acq_doppler_hz, acq_samplestamp, nitems_read):
+    def start(self, code, acq_delay_samples, acq_doppler_hz, acq_samplestamp, nitems_read, prn=1, data_code=None):
         code = np.ascontiguousarray(code, np.float32)
+        if data_code is not None:
+            dc = np.ascontiguousarray(data_code, np.float32)
+            if _lib().orc_trk_set_data_code(self._h, dc.ctypes.data, len(dc)) != 0:
+                raise ValueError("bad data code replica")
         first = ctypes.c_uint64()
-        rc = _lib().orc_trk_start(self._h, code.ctypes.data, len(code), acq_delay_samples, acq_doppler_hz,
+        rc = _lib().orc_trk_start(self._h, int(prn), code.ctypes.data, len(code), acq_delay_samples, acq_doppler_hz,
                                   acq_samplestamp, nitems_read, ctypes.byref(first))
         if rc != 0:
             raise ValueError("bad code replica")
@@ -140,7 +148,7 @@ class Channel:
         positions; returns this channel's own records."""
         out = np.zeros(len(records), TRK_EPOCH_DTYPE)
         for k, rec in enumerate(records):
-            taps = np.ascontiguousarray(rec["taps"], np.float32)
+            taps = np.concatenate([rec["taps"], rec["data_prompt"]]).astype(np.float32)
             if not _lib().orc_trk_call_taps(self._h, taps.ctypes.data, int(rec["sample_counter"]), out[k:k + 1].ctypes.data):
                 return out[:k]
         return out

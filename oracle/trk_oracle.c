@@ -2,8 +2,9 @@
  * ORACLE — TEST INFRASTRUCTURE ONLY.
  *
  * CPU restatement of GNSS-SDR's DLL/PLL tracking channel, dll_pll_veml_tracking
- * (src/algorithms/tracking/gnuradio_blocks/dll_pll_veml_tracking.cc), for the GPS
- * L1 C/A signal, together with the library pieces it calls:
+ * (src/algorithms/tracking/gnuradio_blocks/dll_pll_veml_tracking.cc), for GPS
+ * L1 C/A, Galileo E1 (VEML, pilot or data tracking) and BeiDou B1I (D1 NH code,
+ * D2 GEO preamble), together with the library pieces it calls:
  *   Tracking_loop_filter        src/algorithms/tracking/libs/tracking_loop_filter.cc:20-267
  *   Tracking_FLL_PLL_filter     src/algorithms/tracking/libs/tracking_FLL_PLL_filter.cc:23-101
  *   discriminators              src/algorithms/tracking/libs/tracking_discriminators.cc:25-149
@@ -17,6 +18,11 @@
  * float/double types of every expression follow the reference member and local
  * types (dll_pll_veml_tracking.h:117-209, the loop-filter headers), built with
  * -ffp-contract=off like the reference's x86-64 build (no FMA contraction).
+ *
+ * gr::fast_atan2f (GNU Radio, behind pll_four_quadrant_atan, tracking_discriminators.cc:86-89;
+ * GNU Radio's version is not pinned by the reference and its source is not in the
+ * tree) is restated as atan2f -- its table/polynomial approximations stay within
+ * ~1e-6 rad of it.
  *
  * Pinning: the loop filters and the E-L discriminator are checked against the
  * reference's own unit-test expectations (tracking_loop_filter_test.cc,
@@ -52,6 +58,26 @@ typedef struct
 static const char GPS_CA_PREAMBLE_SYMBOLS_STR_REF[161] =
     "1111111111111111111100000000000000000000000000000000000000000000000000000000000011111111111111111111000000000000"
     "000000001111111111111111111111111111111111111111";
+
+/* Galileo_E1.h:32-52 */
+#define GALILEO_E1_FREQ_HZ_REF 1.57542e9
+#define GALILEO_E1_CODE_CHIP_RATE_CPS_REF 1.023e6
+#define GALILEO_E1_CODE_PERIOD_S_REF 0.004
+#define GALILEO_E1_B_CODE_LENGTH_CHIPS_REF 4092
+#define GALILEO_E1_C_SECONDARY_CODE_LENGTH_REF 25
+static const char GALILEO_E1_C_SECONDARY_CODE_REF[26] = "0011100000001010110110010";
+
+/* Beidou_B1I.h:30-48 */
+#define BEIDOU_B1I_FREQ_HZ_REF 1.561098e9
+#define BEIDOU_B1I_CODE_RATE_CPS_REF 2.046e6
+#define BEIDOU_B1I_CODE_PERIOD_S_REF 0.001
+#define BEIDOU_B1I_CODE_LENGTH_CHIPS_REF 2046
+#define BEIDOU_B1I_SECONDARY_CODE_LENGTH_REF 20
+#define BEIDOU_B1I_TELEMETRY_SYMBOLS_PER_BIT_REF 20
+#define BEIDOU_B1I_GEO_TELEMETRY_SYMBOLS_PER_BIT_REF 2
+#define BEIDOU_B1I_GEO_PREAMBLE_LENGTH_SYMBOLS_REF 22
+static const char BEIDOU_B1I_SECONDARY_CODE_STR_REF[21] = "00000100110101001110";
+static const char BEIDOU_B1I_GEO_PREAMBLE_SYMBOLS_STR_REF[23] = "1111110000001100001100";
 
 void orc_multicorrelator_real_codes(float* out, const float* sig, const float* code, unsigned int L,
     const float* shifts, int K, float rem_carr, float carr_step, float carr_rate, float rem_code, float code_step,
@@ -358,6 +384,19 @@ static double pll_cloop_two_quadrant_atan(tcf p)
 }
 
 /* dll_nc_e_minus_l_normalized (:110-120); std::abs(complex<float>) = hypotf */
+/* pll_four_quadrant_atan (tracking_discriminators.cc:86-89), fast_atan2f -> atan2f */
+static double pll_four_quadrant_atan(tcf p) { return (double)atan2f(p.im, p.re); }
+
+/* dll_nc_vemlp_normalized (tracking_discriminators.cc:139-149) */
+double orc_dll_nc_vemlp_normalized(tcf ve, tcf e, tcf l, tcf vl)
+{
+    const double Early = sqrt(ve.re * ve.re + ve.im * ve.im + e.re * e.re + e.im * e.im);
+    const double Late = sqrt(l.re * l.re + l.im * l.im + vl.re * vl.re + vl.im * vl.im);
+    const double E_plus_L = Early + Late;
+    if (E_plus_L == 0.0) return 0.0;
+    return (Early - Late) / E_plus_L;
+}
+
 double orc_dll_nc_e_minus_l_normalized(float ere, float eim, float lre, float lim, float spc, float slope,
     float y_intercept)
 {
@@ -418,12 +457,18 @@ typedef struct orc_trk
     /* signal (dll_pll_veml_tracking.cc:170-191) */
     double signal_carrier_freq, code_period, code_chip_rate;
     int32_t code_length_chips, code_samples_per_chip, symbols_per_bit;
-    uint32_t secondary_code_length;
+    uint32_t secondary_code_length, data_secondary_code_length;
     const char* secondary_code_string;
+    const char* data_secondary_code_string;
+    int secondary, veml, track_pilot;
+    int iE, iP, iL; /* tap slots of Early / Prompt / Late (VEML: VE 0, VL 4) */
     int n_taps;
     float shifts[5];
     float code[MAX_CODE];
     int code_samples;
+    float data_code[MAX_CODE];
+    int data_code_samples;
+    tcf prompt_data;
     /* loop objects */
     sm_t cn0_smoother, lock_smoother;
     lf_t code_filter;
@@ -437,9 +482,9 @@ typedef struct orc_trk
     double carrier_phase_step_rad, carrier_phase_rate_step_rad, code_phase_step_chips, code_phase_rate_step_chips;
     double rem_code_phase_samples, EVM;
     tcf taps[5];
-    tcf E_accu, P_accu, P_accu_old, L_accu, P_data_accu;
+    tcf VE_accu, E_accu, P_accu, P_accu_old, L_accu, VL_accu, P_data_accu;
     tcf prompt_buffer[MAX_CN0_SAMPLES];
-    tcf circ[GPS_CA_PREAMBLE_LENGTH_SYMBOLS_REF];
+    tcf circ[GPS_CA_PREAMBLE_LENGTH_SYMBOLS_REF]; /* capacity secondary_code_length <= 160 */
     int circ_size, circ_head;
     uint64_t acq_sample_stamp;
     float rem_carr_phase_rad;
@@ -487,36 +532,80 @@ void orc_trk_conf_default(gsdr_trk_conf* c)
     c->enable_fll_steady_state = 0;
     c->carrier_aiding = 1;
     c->high_dyn = 0;
+    c->track_pilot = 1;
 }
 
-/* constructor (dll_pll_veml_tracking.cc:85-560) for GPS L1 C/A */
+/* constructor (dll_pll_veml_tracking.cc:85-560) and the signal table (:170-430) */
 orc_trk* orc_trk_create(const gsdr_trk_conf* conf)
 {
-    if (conf->signal != GSDR_SIGNAL_GPS_1C || conf->extend_correlation_symbols != 1 || conf->high_dyn ||
-        conf->cn0_samples > MAX_CN0_SAMPLES || conf->cn0_samples < 1)
+    if (conf->signal < GSDR_SIGNAL_GPS_1C || conf->signal > GSDR_SIGNAL_BDS_B1 || conf->extend_correlation_symbols != 1 ||
+        conf->high_dyn || conf->cn0_samples > MAX_CN0_SAMPLES || conf->cn0_samples < 1)
         return NULL;
     orc_trk* t = (orc_trk*)calloc(1, sizeof(orc_trk));
     if (!t) return NULL;
     t->p = *conf;
+    t->data_secondary_code_length = 0;
+    t->data_secondary_code_string = "";
+    if (conf->signal == GSDR_SIGNAL_GPS_1C)
+        {
+            t->signal_carrier_freq = GPS_L1_FREQ_HZ_REF;
+            t->code_period = GPS_L1_CA_CODE_PERIOD_S_REF;
+            t->code_chip_rate = GPS_L1_CA_CODE_RATE_CPS_REF;
+            t->code_samples_per_chip = 1;
+            t->code_length_chips = GPS_L1_CA_CODE_LENGTH_CHIPS_REF;
+            t->secondary = 0;
+            t->p.track_pilot = 0;
+            t->secondary_code_length = GPS_CA_PREAMBLE_LENGTH_SYMBOLS_REF;
+            t->secondary_code_string = GPS_CA_PREAMBLE_SYMBOLS_STR_REF;
+            t->symbols_per_bit = GPS_CA_TELEMETRY_SYMBOLS_PER_BIT_REF;
+        }
+    else if (conf->signal == GSDR_SIGNAL_GAL_1B)
+        {
+            t->signal_carrier_freq = GALILEO_E1_FREQ_HZ_REF;
+            t->code_period = GALILEO_E1_CODE_PERIOD_S_REF;
+            t->code_chip_rate = GALILEO_E1_CODE_CHIP_RATE_CPS_REF;
+            t->code_length_chips = GALILEO_E1_B_CODE_LENGTH_CHIPS_REF;
+            t->symbols_per_bit = 1;
+            t->code_samples_per_chip = 2;
+            t->veml = 1;
+            t->secondary = t->p.track_pilot ? 1 : 0;
+            t->secondary_code_length = t->secondary ? GALILEO_E1_C_SECONDARY_CODE_LENGTH_REF : 0;
+            t->secondary_code_string = t->secondary ? GALILEO_E1_C_SECONDARY_CODE_REF : "";
+        }
+    else
+        {
+            t->signal_carrier_freq = BEIDOU_B1I_FREQ_HZ_REF;
+            t->code_period = BEIDOU_B1I_CODE_PERIOD_S_REF;
+            t->code_chip_rate = BEIDOU_B1I_CODE_RATE_CPS_REF;
+            t->code_length_chips = BEIDOU_B1I_CODE_LENGTH_CHIPS_REF;
+            t->symbols_per_bit = BEIDOU_B1I_TELEMETRY_SYMBOLS_PER_BIT_REF;
+            t->code_samples_per_chip = 1;
+            t->secondary = 1;
+            t->p.track_pilot = 0;
+            t->secondary_code_length = BEIDOU_B1I_SECONDARY_CODE_LENGTH_REF;
+            t->secondary_code_string = BEIDOU_B1I_SECONDARY_CODE_STR_REF;
+            t->data_secondary_code_length = BEIDOU_B1I_SECONDARY_CODE_LENGTH_REF;
+            t->data_secondary_code_string = BEIDOU_B1I_SECONDARY_CODE_STR_REF;
+        }
+    t->track_pilot = t->p.track_pilot;
+    /* adapters: vector_length = round(fs_in / (chip rate / code length)) */
     if (t->p.vector_length == 0)
-        t->p.vector_length = (uint32_t)lround(t->p.fs_in / (GPS_L1_CA_CODE_RATE_CPS_REF / GPS_L1_CA_CODE_LENGTH_CHIPS_REF));
-    t->signal_carrier_freq = GPS_L1_FREQ_HZ_REF;
-    t->code_period = GPS_L1_CA_CODE_PERIOD_S_REF;
-    t->code_chip_rate = GPS_L1_CA_CODE_RATE_CPS_REF;
-    t->code_samples_per_chip = 1;
-    t->code_length_chips = GPS_L1_CA_CODE_LENGTH_CHIPS_REF;
-    t->spc = t->p.early_late_space_chips; /* d_trk_parameters.spc (:185) */
-    t->secondary_code_length = GPS_CA_PREAMBLE_LENGTH_SYMBOLS_REF;
-    t->secondary_code_string = GPS_CA_PREAMBLE_SYMBOLS_STR_REF;
-    t->symbols_per_bit = GPS_CA_TELEMETRY_SYMBOLS_PER_BIT_REF;
+        t->p.vector_length = (uint32_t)lround(t->p.fs_in / (t->code_chip_rate / (double)t->code_length_chips));
+    t->spc = t->p.early_late_space_chips; /* d_trk_parameters.spc */
     t->carrier_lock_threshold = t->p.carrier_lock_th;
     t->code_freq_chips = t->code_chip_rate;
     lf_init(&t->code_filter, (float)t->code_period, t->p.dll_bw_hz, t->p.dll_filter_order, 0);
     pll_set_params(&t->carrier_filter, t->p.fll_bw_hz, t->p.pll_bw_hz, t->p.pll_filter_order);
-    t->n_taps = 3;
-    t->shifts[0] = -t->p.early_late_space_chips * (float)t->code_samples_per_chip;
-    t->shifts[1] = 0.0F;
-    t->shifts[2] = t->p.early_late_space_chips * (float)t->code_samples_per_chip;
+    if (t->veml)
+        {
+            t->n_taps = 5;
+            t->iE = 1, t->iP = 2, t->iL = 3;
+        }
+    else
+        {
+            t->n_taps = 3;
+            t->iE = 0, t->iP = 1, t->iL = 2;
+        }
     sm_init(&t->cn0_smoother);
     sm_set_alpha(&t->cn0_smoother, t->p.cn0_smoother_alpha);
     sm_set_samples(&t->cn0_smoother, t->p.cn0_smoother_samples / (int)(t->code_period * 1000.0));
@@ -530,6 +619,15 @@ orc_trk* orc_trk_create(const gsdr_trk_conf* conf)
     return t;
 }
 
+/* the data component's replica (pilot tracking) */
+int orc_trk_set_data_code(orc_trk* t, const float* code, int code_samples)
+{
+    if (code_samples < 1 || code_samples > MAX_CODE) return -1;
+    memcpy(t->data_code, code, sizeof(float) * (size_t)code_samples);
+    t->data_code_samples = code_samples;
+    return 0;
+}
+
 void orc_trk_destroy(orc_trk* t) { free(t); }
 
 void orc_trk_set_assoc(orc_trk* t, int assoc) { t->assoc = assoc; }
@@ -538,6 +636,11 @@ void orc_trk_set_assoc(orc_trk* t, int assoc) { t->assoc = assoc; }
 static void clear_tracking_vars(orc_trk* t)
 {
     for (int k = 0; k < t->n_taps; ++k) t->taps[k] = (tcf){0.0F, 0.0F};
+    if (t->track_pilot)
+        {
+            t->prompt_data = (tcf){0.0F, 0.0F};
+            t->P_data_accu = (tcf){0.0F, 0.0F};
+        }
     t->P_accu_old = (tcf){0.0F, 0.0F};
     t->carr_phase_error_hz = 0.0;
     t->carr_freq_error_hz = 0.0;
@@ -553,10 +656,33 @@ static void clear_tracking_vars(orc_trk* t)
 }
 
 /* start_tracking (:640-882) + the state-1 pull-in call (:1813-1844) at nitems_read */
-int orc_trk_start(orc_trk* t, const float* code, int code_samples, double acq_delay_samples, double acq_doppler_hz,
-    uint64_t acq_samplestamp, uint64_t nitems_read, uint64_t* first_sample)
+int orc_trk_start(orc_trk* t, uint32_t prn, const float* code, int code_samples, double acq_delay_samples,
+    double acq_doppler_hz, uint64_t acq_samplestamp, uint64_t nitems_read, uint64_t* first_sample)
 {
     if (code_samples < 1 || code_samples > MAX_CODE) return -1;
+    if (t->track_pilot && t->data_code_samples < 1) return -1;
+    if (t->p.signal == GSDR_SIGNAL_BDS_B1)
+        {
+            if ((prn > 0 && prn < 6) || prn > 58)
+                {
+                    /* GEO (D2): preamble search, 2 symbols per bit (:762-778) */
+                    t->symbols_per_bit = BEIDOU_B1I_GEO_TELEMETRY_SYMBOLS_PER_BIT_REF;
+                    t->secondary = 0;
+                    t->secondary_code_length = BEIDOU_B1I_GEO_PREAMBLE_LENGTH_SYMBOLS_REF;
+                    t->secondary_code_string = BEIDOU_B1I_GEO_PREAMBLE_SYMBOLS_STR_REF;
+                    t->data_secondary_code_length = 0;
+                }
+            else
+                {
+                    /* D1: NH code on the data (:779-795) */
+                    t->symbols_per_bit = BEIDOU_B1I_TELEMETRY_SYMBOLS_PER_BIT_REF;
+                    t->secondary = 1;
+                    t->secondary_code_length = BEIDOU_B1I_SECONDARY_CODE_LENGTH_REF;
+                    t->secondary_code_string = BEIDOU_B1I_SECONDARY_CODE_STR_REF;
+                    t->data_secondary_code_length = BEIDOU_B1I_SECONDARY_CODE_LENGTH_REF;
+                    t->data_secondary_code_string = BEIDOU_B1I_SECONDARY_CODE_STR_REF;
+                }
+        }
     memcpy(t->code, code, sizeof(float) * (size_t)code_samples);
     t->code_samples = code_samples;
     t->acq_code_phase_samples = acq_delay_samples;
@@ -576,8 +702,21 @@ int orc_trk_start(orc_trk* t, const float* code, int code_samples, double acq_de
     t->carrier_lock_test = 1.0;
     t->CN0_SNV_dB_Hz = 0.0;
     t->EVM = 0.0;
-    t->shifts[0] = -t->p.early_late_space_chips * (float)t->code_samples_per_chip;
-    t->shifts[2] = t->p.early_late_space_chips * (float)t->code_samples_per_chip;
+    if (t->veml)
+        {
+            t->shifts[0] = -t->p.very_early_late_space_chips * (float)t->code_samples_per_chip;
+            t->shifts[1] = -t->p.early_late_space_chips * (float)t->code_samples_per_chip;
+            t->shifts[2] = 0.0F;
+            t->shifts[3] = t->p.early_late_space_chips * (float)t->code_samples_per_chip;
+            t->shifts[4] = t->p.very_early_late_space_chips * (float)t->code_samples_per_chip;
+        }
+    else
+        {
+            t->shifts[0] = -t->p.early_late_space_chips * (float)t->code_samples_per_chip;
+            t->shifts[1] = 0.0F;
+            t->shifts[2] = t->p.early_late_space_chips * (float)t->code_samples_per_chip;
+        }
+    t->prompt_data = (tcf){0.0F, 0.0F};
     t->current_correlation_time_s = t->code_period;
     pll_set_params(&t->carrier_filter, t->p.fll_bw_hz, t->p.pll_bw_hz, t->p.pll_filter_order);
     t->code_filter.bw = t->p.dll_bw_hz;
@@ -625,6 +764,17 @@ static void do_correlation_step(orc_trk* t, const float* in)
         (float)t->code_phase_step_chips * (float)t->code_samples_per_chip,
         (float)t->code_phase_rate_step_chips * (float)t->code_samples_per_chip, t->p.vector_length, 0, t->assoc);
     for (int k = 0; k < t->n_taps; ++k) t->taps[k] = (tcf){out[2 * k], out[2 * k + 1]};
+    if (t->track_pilot)
+        {
+            /* DATA CORRELATOR (:1078-1088): one tap at the prompt shift on the data code */
+            float dout[2];
+            orc_multicorrelator_real_codes(dout, in, t->data_code, (unsigned)t->data_code_samples, &t->shifts[t->iP], 1,
+                t->rem_carr_phase_rad, (float)t->carrier_phase_step_rad, (float)t->carrier_phase_rate_step_rad,
+                (float)t->rem_code_phase_chips * (float)t->code_samples_per_chip,
+                (float)t->code_phase_step_chips * (float)t->code_samples_per_chip,
+                (float)t->code_phase_rate_step_chips * (float)t->code_samples_per_chip, t->p.vector_length, 0, t->assoc);
+            t->prompt_data = (tcf){dout[0], dout[1]};
+        }
 }
 
 /* cn0_and_tracking_lock_status (:970-1056) */
@@ -680,7 +830,10 @@ static int cn0_and_lock(orc_trk* t, double coh)
 /* run_dll_pll (:1092-1179), enable_doppler_correction = false */
 static void run_dll_pll(orc_trk* t)
 {
-    t->carr_phase_error_hz = pll_cloop_two_quadrant_atan(t->P_accu) / TWO_PI_REF;
+    if (t->cloop)
+        t->carr_phase_error_hz = pll_cloop_two_quadrant_atan(t->P_accu) / TWO_PI_REF;
+    else
+        t->carr_phase_error_hz = pll_four_quadrant_atan(t->P_accu) / TWO_PI_REF;
     if ((t->pull_in_transitory && t->p.enable_fll_pull_in) || t->p.enable_fll_steady_state)
         {
             t->carr_freq_error_hz = fll_diff_atan(t->P_accu_old, t->P_accu, 0, t->current_correlation_time_s) / TWO_PI_REF;
@@ -698,8 +851,11 @@ static void run_dll_pll(orc_trk* t)
                 (float)t->current_correlation_time_s);
         }
     t->carrier_doppler_hz = t->carr_error_filt_hz;
-    t->code_error_chips = orc_dll_nc_e_minus_l_normalized(t->E_accu.re, t->E_accu.im, t->L_accu.re, t->L_accu.im, t->spc,
-        1.0F, 1.0F);
+    if (t->veml)
+        t->code_error_chips = orc_dll_nc_vemlp_normalized(t->VE_accu, t->E_accu, t->L_accu, t->VL_accu);
+    else
+        t->code_error_chips = orc_dll_nc_e_minus_l_normalized(t->E_accu.re, t->E_accu.im, t->L_accu.re, t->L_accu.im,
+            t->spc, 1.0F, 1.0F);
     t->code_error_filt_chips = (double)lf_apply(&t->code_filter, (float)t->code_error_chips);
     t->code_freq_chips = t->code_chip_rate - t->code_error_filt_chips;
     if (t->p.carrier_aiding) t->code_freq_chips += t->carrier_doppler_hz * t->code_chip_rate / t->signal_carrier_freq;
@@ -781,14 +937,69 @@ int orc_trk_call_taps(orc_trk* t, const float* taps, uint64_t nitems_read, gsdr_
     return trk_call(t, NULL, taps, nitems_read, r);
 }
 
+/* taps_in: 12 floats -- five complex tap slots (n_taps used) + the data prompt */
 static void correlate_or_copy(orc_trk* t, const float* in, const float* taps_in)
 {
     if (taps_in)
         {
             for (int k = 0; k < t->n_taps; ++k) t->taps[k] = (tcf){taps_in[2 * k], taps_in[2 * k + 1]};
+            if (t->track_pilot) t->prompt_data = (tcf){taps_in[10], taps_in[11]};
         }
     else
         do_correlation_step(t, in);
+}
+
+static void cadd(tcf* a, tcf b, float sgn)
+{
+    if (sgn > 0)
+        {
+            a->re += b.re;
+            a->im += b.im;
+        }
+    else
+        {
+            a->re -= b.re;
+            a->im -= b.im;
+        }
+}
+
+/* save_correlation_results (:1288-1400) */
+static void save_correlation_results(orc_trk* t)
+{
+    float sg = 1.0F;
+    if (t->secondary)
+        {
+            sg = t->secondary_code_string[t->current_symbol] == '0' ? 1.0F : -1.0F;
+            t->current_symbol++;
+            t->current_symbol %= (int32_t)t->secondary_code_length;
+        }
+    if (t->veml)
+        {
+            cadd(&t->VE_accu, t->taps[0], sg);
+            cadd(&t->VL_accu, t->taps[4], sg);
+        }
+    cadd(&t->E_accu, t->taps[t->iE], sg);
+    cadd(&t->P_accu, t->taps[t->iP], sg);
+    cadd(&t->L_accu, t->taps[t->iL], sg);
+    const tcf pd = t->track_pilot ? t->prompt_data : t->taps[t->iP];
+    if (t->symbols_per_bit > 1)
+        {
+            if (t->data_secondary_code_length > 0)
+                {
+                    cadd(&t->P_data_accu, pd, t->data_secondary_code_string[t->current_data_symbol] == '0' ? 1.0F : -1.0F);
+                    t->current_data_symbol++;
+                    t->current_data_symbol %= (int32_t)t->data_secondary_code_length;
+                }
+            else
+                {
+                    cadd(&t->P_data_accu, pd, 1.0F);
+                    t->current_data_symbol++;
+                    t->current_data_symbol %= t->symbols_per_bit;
+                }
+        }
+    else
+        t->P_data_accu = pd;
+    t->cloop = t->track_pilot ? 0 : 1;
 }
 
 static int trk_call(orc_trk* t, const float* in, const float* taps_in, uint64_t nitems_read, gsdr_trk_epoch* r)
@@ -811,9 +1022,14 @@ static int trk_call(orc_trk* t, const float* in, const float* taps_in, uint64_t 
         case 2:
             {
                 correlate_or_copy(t, in, taps_in);
-                t->E_accu = t->taps[0];
-                t->P_accu = t->taps[1];
-                t->L_accu = t->taps[2];
+                if (t->veml)
+                    {
+                        t->VE_accu = t->taps[0];
+                        t->VL_accu = t->taps[4];
+                    }
+                t->E_accu = t->taps[t->iE];
+                t->P_accu = t->taps[t->iP];
+                t->L_accu = t->taps[t->iL];
                 t->spc = t->p.early_late_space_chips;
                 if ((uint64_t)t->p.bit_synchronization_time_limit_s < (nitems_read - t->acq_sample_stamp) / (uint64_t)(int)t->p.fs_in)
                     t->carrier_lock_fail_counter = 300000;
@@ -830,12 +1046,18 @@ static int trk_call(orc_trk* t, const float* in, const float* taps_in, uint64_t 
                         update_tracking_vars(t);
                         if (!t->pull_in_transitory)
                             {
-                                circ_push(t, t->taps[1]);
-                                if (t->circ_size == (int)t->secondary_code_length) next_state = acquire_secondary(t);
+                                if (t->secondary || t->symbols_per_bit > 1)
+                                    {
+                                        /* secondary code lock / preamble correlation (:1889-1921) */
+                                        circ_push(t, t->taps[t->iP]);
+                                        if (t->circ_size == (int)t->secondary_code_length) next_state = acquire_secondary(t);
+                                    }
+                                else
+                                    next_state = 1;
                             }
                         if (next_state)
                             {
-                                t->E_accu = t->P_accu = t->L_accu = t->P_data_accu = (tcf){0.0F, 0.0F};
+                                t->VE_accu = t->E_accu = t->P_accu = t->P_data_accu = t->L_accu = t->VL_accu = (tcf){0.0F, 0.0F};
                                 t->circ_size = 0;
                                 t->circ_head = 0;
                                 t->current_symbol = 0;
@@ -849,18 +1071,7 @@ static int trk_call(orc_trk* t, const float* in, const float* taps_in, uint64_t 
         case 4:
             {
                 correlate_or_copy(t, in, taps_in);
-                /* save_correlation_results (:1290-1400): no secondary code, no pilot */
-                t->E_accu.re += t->taps[0].re;
-                t->E_accu.im += t->taps[0].im;
-                t->P_accu.re += t->taps[1].re;
-                t->P_accu.im += t->taps[1].im;
-                t->L_accu.re += t->taps[2].re;
-                t->L_accu.im += t->taps[2].im;
-                t->P_data_accu.re += t->taps[1].re;
-                t->P_data_accu.im += t->taps[1].im;
-                t->current_data_symbol++;
-                t->current_data_symbol %= t->symbols_per_bit;
-                t->cloop = 1;
+                save_correlation_results(t);
                 if (!cn0_and_lock(t, t->code_period * (double)t->p.extend_correlation_symbols))
                     {
                         clear_tracking_vars(t);
@@ -881,7 +1092,7 @@ static int trk_call(orc_trk* t, const float* in, const float* taps_in, uint64_t 
                                 fill_output(t, r);
                                 t->P_data_accu = (tcf){0.0F, 0.0F};
                             }
-                        t->E_accu = t->P_accu = t->L_accu = (tcf){0.0F, 0.0F};
+                        t->VE_accu = t->E_accu = t->P_accu = t->L_accu = t->VL_accu = (tcf){0.0F, 0.0F};
                     }
                 break;
             }
@@ -893,6 +1104,8 @@ static int trk_call(orc_trk* t, const float* in, const float* taps_in, uint64_t 
             r->taps[2 * k] = t->taps[k].re;
             r->taps[2 * k + 1] = t->taps[k].im;
         }
+    r->data_prompt[0] = t->prompt_data.re;
+    r->data_prompt[1] = t->prompt_data.im;
     if (loss_of_lock) r->flags |= GSDR_TRK_F_LOSS_OF_LOCK;
     if (t->flag_pll_180) r->flags |= GSDR_TRK_F_PLL_180;
     r->consumed = t->current_prn_length_samples;

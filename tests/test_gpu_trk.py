@@ -202,3 +202,96 @@ def test_stop_and_standby_consume_nothing():
     rec, n = t.run(iq, 0, 50)
     assert list(n) == [0, 0]
     assert t.channel(1)["state"] == 0
+
+
+# ---------------------------------------------------------------- Galileo E1 / BeiDou B1I
+def _conf_sig(fs, sig, nch=1, pilot=1):
+    c = _conf(fs, nch)
+    c["signal"] = sig
+    c["track_pilot"] = pilot
+    c["pll_bw_hz"] = 15.0
+    c["dll_bw_hz"] = 1.0
+    return c
+
+
+def _open_loop_sig(g, iq, code, data_code, fs, acq_dop, shifts_chips, spc, chip_rate, vl, iP):
+    """Check 1 for any signal: every call's taps (and the data prompt) against the
+    oracle correlator fed with the GPU's own incoming NCO state."""
+    shifts = (np.asarray(shifts_chips, np.float32) * np.float32(spc)).astype(np.float32)
+    worst = 0.0
+    for e in range(len(g)):
+        if e == 0:
+            rem_carr, dop, rem_samples, code_freq = 0.0, acq_dop, 0.0, chip_rate
+        else:
+            p = g[e - 1]
+            rem_carr, dop = float(p["rem_carr_phase_rad"]), float(p["carrier_doppler_hz"])
+            rem_samples, code_freq = float(p["rem_code_phase_samples"]), float(p["code_freq_chips"])
+        carr_step = float(np.float32(TWO_PI * dop / fs))
+        rem_code = float(np.float32(np.float32(code_freq * rem_samples / fs) * np.float32(spc)))
+        code_step = float(np.float32(np.float32(code_freq / fs) * np.float32(spc)))
+        n0 = int(g[e]["sample_counter"])
+        x = iq[n0:n0 + vl]
+        ref = volk.multicorrelator_real_codes(x, code, shifts, rem_carr, carr_step, rem_code, code_step, vl)
+        got = g["taps"][e][:2 * len(shifts)].view(np.complex64)
+        worst = max(worst, vnorm_rel(got, ref))
+        if data_code is not None:
+            refd = volk.multicorrelator_real_codes(x, data_code, shifts[iP:iP + 1], rem_carr, carr_step, rem_code,
+                                                   code_step, vl)
+            worst = max(worst, vnorm_rel(g["data_prompt"][e].view(np.complex64), refd))
+    return worst
+
+
+def _oracle_sig(fs, sig, pilot, code, data_code, delay, dop, nitems, prn):
+    ch = trk.Channel(_conf_sig(fs, sig, 1, pilot)[0:1].view(trk.TRK_CONF_DTYPE))
+    first = ch.start(code, delay, dop, 0, nitems, prn=prn, data_code=data_code)
+    return ch, first
+
+
+@pytest.mark.parametrize("pilot", [1, 0])
+def test_galileo_e1_matches_oracle(pilot):
+    """Config C4's signal: Galileo E1 VEML 5 taps (+ the E1B data prompt when
+    tracking the E1C pilot), 4 ms calls, E1C secondary-code lock."""
+    fs = 4.0e6
+    sat = synth.GalileoSatellite(11, 1234.5, 1000.3, 50.0, 0.7)
+    iq = synth.gal_e1_iq(fs, int(1.5 * fs), [sat], seed_offset=5)
+    tau = sat.code_delay_chips / (1.023e6 * (1 + sat.doppler_hz / 1.57542e9)) * fs
+    delay, dop = float(round(tau) % 16000), 1250.0
+    code = synth.gal_e1_sinboc11(11, pilot=bool(pilot))
+    dcode = synth.gal_e1_sinboc11(11) if pilot else None
+    t = gsdr.Tracking(_conf_sig(fs, gsdr.SIGNAL_GAL_1B, 1, pilot))
+    fg = t.start(0, 11, code, delay, dop, 0, 0, data_code=dcode)
+    rec, n = t.run(iq, 0, 400)
+    g = rec[0][:n[0]]
+    free, fo = _oracle_sig(fs, 1, pilot, code, dcode, delay, dop, 0, 11)
+    assert fg == fo
+    el, vel = 0.25, 0.5
+    assert _open_loop_sig(g, iq, code, dcode, fs, dop, [-vel, -el, 0.0, el, vel], 2, 1.023e6, 16000, 2) <= 1e-4
+    _replay_check(g, _oracle_sig(fs, 1, pilot, code, dcode, delay, dop, 0, 11)[0], "gal%d" % pilot)
+    orc, _ = free.run(iq, 0, fo, 400)
+    _free_check(g, orc, "gal%d" % pilot)
+    assert g["state"][-1] == 4 and np.count_nonzero(g["flags"] & gsdr.TRK_F_BIT_SYNC) == 1
+
+
+@pytest.mark.parametrize("prn", [14, 3])
+def test_beidou_b1i_matches_oracle(prn):
+    """Config C5's BeiDou signal: B1I D1 (NH code lock, NH wiped from the 20 ms
+    symbols) and D2 GEO (preamble search, 2 ms symbols)."""
+    fs = 4.0e6
+    s = synth.Satellite(prn, -2262.3, 500.2, 45.0, 0.3)
+    iq = synth.bds_b1i_iq(fs, int(1.5 * fs), [s], seed_offset=7)
+    tau = s.code_delay_chips / (2.046e6 * (1 + s.doppler_hz / 1.561098e9)) * fs
+    delay, dop = float(round(tau) % 4000), -2250.0
+    code = synth.bds_b1i_chips(prn)
+    t = gsdr.Tracking(_conf_sig(fs, gsdr.SIGNAL_BDS_B1))
+    fg = t.start(0, prn, code, delay, dop, 0, 0)
+    rec, n = t.run(iq, 0, 1480)
+    g = rec[0][:n[0]]
+    free, fo = _oracle_sig(fs, 2, 0, code, None, delay, dop, 0, prn)
+    assert fg == fo
+    assert _open_loop_sig(g, iq, code, None, fs, dop, [-0.25, 0.0, 0.25], 1, 2.046e6, 4000, 1) <= 1e-4
+    _replay_check(g, _oracle_sig(fs, 2, 0, code, None, delay, dop, 0, prn)[0], "bds%d" % prn)
+    orc, _ = free.run(iq, 0, fo, 1480)
+    _free_check(g, orc, "bds%d" % prn)
+    assert g["state"][-1] == 4
+    out = np.nonzero(g["flags"] & gsdr.TRK_F_VALID_OUTPUT)[0]
+    assert len(out) > 5 and np.all(np.diff(out) == (2 if synth.bds_is_geo(prn) else 20))

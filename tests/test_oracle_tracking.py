@@ -94,3 +94,66 @@ def test_channel_loses_lock_on_noise():
     recs, _ = ch.run(iq, 0, first, 4000)
     assert recs["flags"][-1] & trk.F_LOSS_OF_LOCK
     assert ch.state == 0
+
+
+def _conf_sig(fs, sig, pilot=1):
+    c = trk.conf_default()
+    c["fs_in"] = fs
+    c["signal"] = sig
+    c["track_pilot"] = pilot
+    c["pull_in_time_s"] = 0
+    c["pll_bw_hz"] = 15.0
+    c["dll_bw_hz"] = 1.0
+    return c
+
+
+@pytest.mark.parametrize("pilot", [1, 0])
+def test_galileo_e1_channel(pilot):
+    """Galileo E1 (dll_pll_veml_tracking.cc:258-290): VEML 5 taps on the sinBOC(1,1)
+    replica at 2 samples/chip, 4 ms calls; pilot tracking locks the E1C secondary
+    code after pull-in and reads the E1B data prompt from the extra correlator."""
+    fs = 4.0e6
+    sat = synth.GalileoSatellite(11, 1234.5, 1000.3, 50.0, 0.7)
+    iq = synth.gal_e1_iq(fs, int(1.6 * fs), [sat], seed_offset=5)
+    ch = trk.Channel(_conf_sig(fs, 1, pilot))
+    assert ch.vector_length == 16000
+    tau = sat.code_delay_chips / (1.023e6 * (1 + sat.doppler_hz / 1.57542e9)) * fs
+    first = ch.start(synth.gal_e1_sinboc11(11, pilot=bool(pilot)), float(round(tau) % 16000), 1250.0, 0, 0, prn=11,
+                     data_code=synth.gal_e1_sinboc11(11) if pilot else None)
+    recs, _ = ch.run(iq, 0, first, 1000)
+    assert len(recs) > 350 and recs["state"][-1] == 4
+    sync = np.nonzero(recs["flags"] & trk.F_BIT_SYNC)[0]
+    assert len(sync) == 1 and 249 <= sync[0] <= 249 + 26 * pilot
+    assert np.all(np.abs(recs["consumed"] - 16000) <= 1)
+    late = recs[-60:]
+    assert abs(np.mean(late["carrier_doppler_hz"]) - sat.doppler_hz) < 3.0
+    taps = late["taps"][:, :10].view(np.complex64)
+    assert np.all(np.abs(taps[:, 2]) > np.abs(taps[:, 1])) and np.all(np.abs(taps[:, 2]) > np.abs(taps[:, 3]))
+    out = recs[(recs["flags"] & trk.F_VALID_OUTPUT) != 0]
+    assert len(out) == len(recs) - sync[0] - 1  # one 4 ms symbol per call after the lock
+    tail = out[-60:]
+    assert np.median(np.abs(tail["prompt_i"]) / (np.abs(tail["prompt_q"]) + 1e-9)) > 3.0
+    if pilot:
+        np.testing.assert_array_equal(tail["prompt_i"], tail["data_prompt"][:, 0].astype(np.float64))
+    assert not np.any(recs["flags"] & trk.F_LOSS_OF_LOCK)
+
+
+@pytest.mark.parametrize("prn,per", [(14, 20), (3, 2)])
+def test_beidou_b1i_channel(prn, per):
+    """BeiDou B1I (:391-411, :762-795): D1 satellites lock the NH code and emit one
+    symbol per 20 ms with the NH wiped; D2 GEO satellites (PRN 1-5, 59-63) search
+    the D2 preamble and emit one symbol per 2 ms."""
+    fs = 4.0e6
+    s = synth.Satellite(prn, -2262.3, 500.2, 45.0, 0.3)
+    iq = synth.bds_b1i_iq(fs, int(1.6 * fs), [s], seed_offset=7)
+    ch = trk.Channel(_conf_sig(fs, 2))
+    assert ch.vector_length == 4000
+    tau = s.code_delay_chips / (2.046e6 * (1 + s.doppler_hz / 1.561098e9)) * fs
+    first = ch.start(synth.bds_b1i_chips(prn), float(round(tau) % 4000), -2250.0, 0, 0, prn=prn)
+    recs, _ = ch.run(iq, 0, first, 1590)
+    sync = np.nonzero(recs["flags"] & trk.F_BIT_SYNC)[0]
+    assert len(sync) == 1 and recs["state"][-1] == 4
+    assert abs(np.mean(recs[-100:]["carrier_doppler_hz"]) - s.doppler_hz) < 2.0
+    out = np.nonzero(recs["flags"] & trk.F_VALID_OUTPUT)[0]
+    assert len(out) > 5 and np.all(np.diff(out) == per)
+    assert not np.any(recs["flags"] & trk.F_LOSS_OF_LOCK)

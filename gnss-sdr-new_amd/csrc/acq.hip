@@ -177,6 +177,7 @@ int gsdr_acq_create(int device, const gsdr_acq_conf* conf, gsdr_acq** out)
         }
     const size_t nP = conf->max_prns, nB = conf->max_blocks;
     hipError_t e = hipStreamCreateWithFlags(&a->stream, hipStreamNonBlocking);
+
     if (e == hipSuccess) e = hipMalloc(&a->d_tw, N * sizeof(float2));
     if (e == hipSuccess) e = hipMalloc(&a->d_wipe, (size_t)a->D * N * sizeof(float2));
     if (e == hipSuccess) e = hipMalloc(&a->d_code_fft, nP * N * sizeof(float2));

@@ -5,6 +5,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -26,7 +27,7 @@ namespace
 using gsdr::fft::Plan;
 
 // Default correlate variant at N = 4000 (see GSDR_PK_VARIANTS).
-constexpr int kDefaultCorrVariant4000 = 35;
+constexpr int kDefaultCorrVariant4000 = 30;
 
 struct RowStat
 {
@@ -172,7 +173,10 @@ __global__ void __launch_bounds__(PT::NT) acq_forward_kernel(const void* __restr
     uint32_t consumed, uint32_t D)
 {
     extern __shared__ float2 lds[];
-    const uint32_t d = blockIdx.x, b = blockIdx.y;
+    // blockIdx.x = block, blockIdx.y = Doppler bin: the workgroups of one wipe-off
+    // row w_d are consecutive, so each XCD's L2 fetches the row once per launch
+    // (with d fastest every row was re-read from HBM for every block)
+    const uint32_t b = blockIdx.x, d = blockIdx.y;
     const size_t base = (size_t)b * block_stride;
     const float2* w = wipe + (size_t)d * plan.n;
     float2* out = X + ((size_t)b * D + d) * plan.n;
@@ -315,8 +319,16 @@ __global__ void __launch_bounds__(MP::NT) __attribute__((amdgpu_waves_per_eu(WPE
     }
     for (int q = 0; q < np; ++q)
         {
-            float best = -1.0f, sum = 0.0f;
-            uint32_t bidx = 0xffffffffu;
+            // Row statistics with a slot-keyed maximum: key = bits(|R|^2) with its 5
+            // low mantissa bits replaced by (31 - slot).  Non-negative floats order
+            // like their bit patterns, so one integer max per output keeps the
+            // lane's largest value and, among equal (truncated) values, the
+            // earliest output -- the reference's first-maximum rule up to 2^-18
+            // relative (the SURVEY H3 near-tie bound is 1e-4).  The truncated value
+            // is the reported peak.
+            static_assert(MP::NSLOTS <= 32, "slot key holds 5 bits");
+            uint32_t key = 0u;
+            float sum = 0.0f;
             // conj(X . conj(C)) = conj(X) . C ; |IFFT(Y)| = |FFT(conj(Y))|
             auto load = [&](int bb, int r, int) -> c2 { return gsdr::pk::conj_mul(xr[bb][r], cr[bb][r]); };
             auto hook = [&]() {
@@ -335,18 +347,38 @@ __global__ void __launch_bounds__(MP::NT) __attribute__((amdgpu_waves_per_eu(WPE
                             }
                     }
             };
-            auto store = [&](int i, c2 v) {
+            auto store = [&](int, c2 v, int slot) {
                 const float m = __builtin_fmaf(v.x, v.x, v.y * v.y);
-                if (m > best)
-                    {
-                        best = m;
-                        bidx = (uint32_t)i;
-                    }
+                key = max(key, (__float_as_uint(m) & ~31u) | (uint32_t)(31 - slot));
                 sum += m;
             };
             MP::run(lds, tw, load, store, hook);
-            block_reduce_stat<NT>(best, bidx, sum, scratch + (q & 1) * NW);
-            if (threadIdx.x == 0) stats[((size_t)b * P + p0 + q) * D + d] = RowStat{best, bidx, sum, 0};
+            // wave: max key, then the lowest lane holding it; workgroup: LDS pass
+            uint32_t wkey = key;
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) wkey = max(wkey, (uint32_t)__shfl_xor((int)wkey, off));
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) sum += __shfl_xor(sum, off);
+            const uint64_t holders = __ballot(key == wkey);
+            const int first = __ffsll((unsigned long long)holders) - 1;
+            const int my_idx = MP::index_of_slot(31 - (int)(key & 31u));
+            const uint32_t widx = (uint32_t)__shfl(my_idx, first);
+            RowStat* sc = scratch + (q & 1) * NW;
+            const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+            if (lane == 0) sc[wave] = RowStat{__uint_as_float(wkey & ~31u), widx, sum, 0};
+            __syncthreads();
+            if (threadIdx.x == 0)
+                {
+                    RowStat best = sc[0];
+#pragma unroll
+                    for (int w = 1; w < NW; ++w)
+                        {
+                            const RowStat o = sc[w];
+                            if (stat_better(o.max, o.idx, best.max, best.idx)) best = RowStat{o.max, o.idx, best.sum, 0};
+                            best.sum += o.sum;
+                        }
+                    stats[((size_t)b * P + p0 + q) * D + d] = RowStat{best.max, best.idx, best.sum, 0};
+                }
         }
 }
 
@@ -671,6 +703,30 @@ __global__ void acq_decide_kernel(const gsdr_acq_result* __restrict__ resk, gsdr
     res[bp] = resk[(size_t)bp * K + k];
 }
 
+// ---------------------------------------------------------------- K_forward (packed f32)
+// X_{b,d} = FFT(x_b .* w_d) on the packed plan (the N = 4000 path, with the packed
+// correlate variants).  Grid (B, D) with the block index fastest, as
+// acq_forward_kernel.
+template <class MP, int IT>
+__global__ void __launch_bounds__(MP::NT) acq_forward_pk_kernel(const void* __restrict__ iq, uint64_t block_stride,
+    const float2* __restrict__ wipe, float2* __restrict__ X, const float2* __restrict__ tw, uint32_t consumed, uint32_t D)
+{
+    using gsdr::pk::c2;
+    extern __shared__ float2 lds_raw[];
+    c2* lds = reinterpret_cast<c2*>(lds_raw);
+    const uint32_t b = blockIdx.x, d = blockIdx.y;
+    constexpr uint32_t N = MP::N;
+    const size_t base = (size_t)b * block_stride;
+    const c2* w = reinterpret_cast<const c2*>(wipe) + (size_t)d * N;
+    c2* out = reinterpret_cast<c2*>(X) + ((size_t)b * D + d) * N;
+    auto load = [&](int, int, int i) -> c2 {
+        if (i >= (int)consumed) return c2{0.f, 0.f};
+        return gsdr::pk::mul(gsdr::pk::from(load_item<IT>(iq, base + i)), w[i]);
+    };
+    auto store = [&](int i, c2 v, int) { out[i] = v; };
+    MP::run(lds, tw, load, store, [] {});
+}
+
 // ---------------------------------------------------------------- K_reduce
 // One wave per (b, p).  Rows are scanned in increasing d by each lane and merged
 // with the (max desc, d asc) order, reproducing the reference's strict '>' scan.
@@ -853,6 +909,8 @@ size_t item_bytes(int it) { return it == GSDR_ITEM_CSHORT ? 4 : 8; }
 // Packed-f32 variants: (id, plan, PRNs per workgroup).
 #define GSDR_PK_VARIANTS(X)                                              \
     X(30, (gsdr::pk::PkPlan<256, true, 25, 16, 10>), 1, 1)              \
+    X(31, (gsdr::pk::PkPlan<256, false, 20, 20, 10>), 1, 1)             \
+    X(32, (gsdr::pk::PkPlan<256, false, 25, 16, 10>), 1, 1)             \
     X(35, (gsdr::pk::PkPlan<256, true, 20, 20, 10>), 1, 1)              \
     X(37, (gsdr::pk::PkPlan<512, true, 25, 16, 10>), 2, 1)
 
@@ -970,6 +1028,7 @@ struct StageTimer
 namespace gsdr_acq_impl
 {
 int launch_corr_variant(gsdr_acq* a, uint32_t nblocks, hipStream_t s);
+int launch_forward_pk(gsdr_acq* a, const void* iq, int item_type, uint32_t nblocks, uint64_t stride, hipStream_t s);
 int setup_corr_variant(gsdr_acq* a, int v);
 int dispatch_static(gsdr_acq* a, int op, const void* iq, uint32_t nblocks, uint64_t stride, uint64_t stamp0,
     gsdr_acq_result* res, hipStream_t s, uint32_t aux);
@@ -982,6 +1041,7 @@ int dispatch_four(gsdr_acq* a, int op, const void* iq, uint32_t nblocks, uint64_
 namespace
 {
 using gsdr_acq_impl::launch_corr_variant;
+using gsdr_acq_impl::launch_forward_pk;
 
 template <class PT>
 const typename PT::PlanT& plan_of(const gsdr_acq* a)
@@ -996,10 +1056,10 @@ template <class PT>
 void launch_forward(gsdr_acq* a, const void* iq, int item_type, uint32_t nblocks, uint64_t stride, hipStream_t s)
 {
     if (item_type == GSDR_ITEM_GR_COMPLEX)
-        hipLaunchKernelGGL((acq_forward_kernel<PT, GSDR_ITEM_GR_COMPLEX>), dim3(a->D, nblocks), dim3(PT::NT),
+        hipLaunchKernelGGL((acq_forward_kernel<PT, GSDR_ITEM_GR_COMPLEX>), dim3(nblocks, a->D), dim3(PT::NT),
             a->lds_bytes, s, iq, stride, a->d_wipe, a->d_X, a->d_tw, plan_of<PT>(a), a->consumed, a->D);
     else
-        hipLaunchKernelGGL((acq_forward_kernel<PT, GSDR_ITEM_CSHORT>), dim3(a->D, nblocks), dim3(PT::NT),
+        hipLaunchKernelGGL((acq_forward_kernel<PT, GSDR_ITEM_CSHORT>), dim3(nblocks, a->D), dim3(PT::NT),
             a->lds_bytes, s, iq, stride, a->d_wipe, a->d_X, a->d_tw, plan_of<PT>(a), a->consumed, a->D);
 }
 
@@ -1049,7 +1109,13 @@ int launch_all(gsdr_acq* a, const void* iq, int item_type, uint32_t nblocks, uin
     StageTimer t(a, s);
     if (a->general) return launch_general<PT>(a, iq, item_type, nblocks, stride, stamp0, res, s, t);
     t.begin();
-    launch_forward<PT>(a, iq, item_type, nblocks, stride, s);
+    if (a->corr_variant > 0)
+        {
+            int rc = launch_forward_pk(a, iq, item_type, nblocks, stride, s);
+            if (rc != GSDR_OK) return rc;
+        }
+    else
+        launch_forward<PT>(a, iq, item_type, nblocks, stride, s);
     GSDR_HIP(hipGetLastError());
     t.end(0);
     t.begin();

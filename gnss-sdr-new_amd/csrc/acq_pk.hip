@@ -37,9 +37,32 @@ int launch_corr_variant(gsdr_acq* a, uint32_t nblocks, hipStream_t s)
 #undef GSDR_UNPAREN
 }
 
+// Forward spectra on the packed plan (N = 4000 with a packed correlate variant).
+using ForwardPk = gsdr::pk::PkPlan<256, true, 25, 16, 10>;
+
+int launch_forward_pk(gsdr_acq* a, const void* iq, int item_type, uint32_t nblocks, uint64_t stride, hipStream_t s)
+{
+    const size_t lds = ForwardPk::lds_bytes();
+    if (item_type == GSDR_ITEM_GR_COMPLEX)
+        hipLaunchKernelGGL((acq_forward_pk_kernel<ForwardPk, GSDR_ITEM_GR_COMPLEX>), dim3(nblocks, a->D),
+            dim3(ForwardPk::NT), lds, s, iq, stride, a->d_wipe, a->d_X, a->d_tw, a->consumed, a->D);
+    else
+        hipLaunchKernelGGL((acq_forward_pk_kernel<ForwardPk, GSDR_ITEM_CSHORT>), dim3(nblocks, a->D),
+            dim3(ForwardPk::NT), lds, s, iq, stride, a->d_wipe, a->d_X, a->d_tw, a->consumed, a->D);
+    GSDR_HIP(hipGetLastError());
+    return GSDR_OK;
+}
+
 // Select and configure a correlate variant (N must be 4000).
 int setup_corr_variant(gsdr_acq* a, int v)
 {
+    {
+        const size_t lds = ForwardPk::lds_bytes();
+        GSDR_HIP(hipFuncSetAttribute((const void*)acq_forward_pk_kernel<ForwardPk, GSDR_ITEM_GR_COMPLEX>,
+            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        GSDR_HIP(hipFuncSetAttribute((const void*)acq_forward_pk_kernel<ForwardPk, GSDR_ITEM_CSHORT>,
+            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    }
 #define GSDR_PK_SETUP(ID, MP, PG, WPE)                                                                               \
     case ID:                                                                                                    \
         {                                                                                                       \

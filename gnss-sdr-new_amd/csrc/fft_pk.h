@@ -312,7 +312,8 @@ __device__ __forceinline__ void stage(c2* lds, const float2* __restrict__ tw, Lo
     if constexpr (LAST)
         {
             // last stage: Ns = N/R and k = j, so output j + r*Ns; r outer, b inner
-            // visits this lane's outputs in increasing index order
+            // visits this lane's outputs in increasing index order, and the
+            // compile-time slot r*BPT + b numbers them in that order
             static_assert(!LAST || Ns * R == N, "last stage");
 #pragma unroll
             for (int r = 0; r < R; ++r)
@@ -321,7 +322,7 @@ __device__ __forceinline__ void stage(c2* lds, const float2* __restrict__ tw, Lo
                     for (int b = 0; b < BPT; ++b)
                         {
                             const int j = (int)threadIdx.x + b * NT;
-                            if (NB % NT == 0 || j < NB) store(j + r * Ns, v[b][r]);
+                            if (NB % NT == 0 || j < NB) store(j + r * Ns, v[b][r], r * BPT + b);
                         }
                 }
         }
@@ -352,6 +353,16 @@ struct PkPlan
     static constexpr int BPT1 = fft::bpt_for(R1);
     static constexpr int NB1 = N / R1;
     static constexpr size_t lds_bytes() { return (size_t)N * sizeof(c2); }
+    // last stage: radix, butterflies per thread, output stride; store(i, v, slot)
+    // receives slot = r*BPTL + b in [0, RL*BPTL), this lane's output order
+    static constexpr int RL = (0, ..., Rs);
+    static constexpr int BPTL = fft::bpt_for(RL);
+    static constexpr int NSL = N / RL;
+    static constexpr int NSLOTS = RL * BPTL;
+    __device__ __forceinline__ static int index_of_slot(int slot)
+    {
+        return (int)threadIdx.x + (slot % BPTL) * NT + (slot / BPTL) * NSL;
+    }
     template <class Load, class Store, class Hook>
     __device__ __forceinline__ static void run(c2* lds, const float2* __restrict__ tw, Load load, Store store, Hook hook)
     {

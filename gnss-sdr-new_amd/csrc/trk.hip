@@ -763,7 +763,7 @@ template <int IT>
 __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __restrict__ consts,
     TrkChan* __restrict__ chans, const float* const* __restrict__ codes, const float* const* __restrict__ data_codes,
     const void* __restrict__ iq, uint64_t iq_first, uint64_t iq_items, uint32_t max_epochs, gsdr_trk_epoch* __restrict__ out,
-    uint32_t* __restrict__ nout, int code_pad, int data_pad, uint64_t* __restrict__ timing)
+    uint32_t* __restrict__ nout, int code_pad, int data_pad, uint64_t* __restrict__ timing, int timing_wall)
 {
     // LDS: [replica | data replica (pilot tracking) | next call's input window]
     extern __shared__ float s_dyn[];
@@ -815,7 +815,7 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
     for (;; ++e)
         {
             uint64_t tm0 = 0, tm1 = 0, tm2 = 0;
-            if (timing && tid == 0) tm0 = clock64();
+            if (timing && tid == 0) tm0 = timing_wall ? wall_clock64() : clock64();
             if (tid == 0)
                 {
                     Prep p{};
@@ -859,7 +859,7 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                 }
             __syncthreads();
             if (!prep.go) break;
-            if (timing && tid == 0) tm1 = clock64();
+            if (timing && tid == 0) tm1 = timing_wall ? wall_clock64() : clock64();
             // ---- correlation: lane-interleaved samples, fp64 phasor anchor + fp32 steps
             const Prep p = prep;
             float2 acc[kMaxTrkTaps + 1];
@@ -901,7 +901,7 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                     for (int k = 0; k <= kMaxTrkTaps; ++k) s_red[wave][k] = acc[k];
                 }
             __syncthreads();  // partials visible; every read of the LDS window done
-            if (timing && tid == 0) tm2 = clock64();
+            if (timing && tid == 0) tm2 = timing_wall ? wall_clock64() : clock64();
             // ---- fetch the window the next call most likely reads: [off + vl - kHalo/2, +kWinCore+kHalo)
             float2 wv[kSpl];
             float2 wh = make_float2(0.f, 0.f);
@@ -984,7 +984,7 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                                     tr[0] = tm0;
                                     tr[1] = tm1;
                                     tr[2] = tm2;
-                                    tr[3] = clock64();
+                                    tr[3] = timing_wall ? wall_clock64() : clock64();
                                 }
                         }
                     t.next_sample = n_read + (uint64_t)(int64_t)t.current_prn_length_samples;
@@ -1057,6 +1057,7 @@ struct gsdr_trk
     int data_pad{0};     // floats reserved for the data replica (pilot tracking)
     // GSDR_TRK_TIMING=1: per-phase clock64 stamps of every call, summarised on destroy
     bool timing_on{false};
+    int timing_wall{0};  // GSDR_TRK_TIMING=2: constant-rate wall clock instead of the shader clock
     uint64_t* d_timing{nullptr};
     size_t timing_cap{0};
     double tsum[4]{};
@@ -1273,11 +1274,11 @@ int launch(gsdr_trk* k, const void* iq, uint64_t iq_first, uint64_t iq_items, ui
     if (k->conf.item_type == GSDR_ITEM_GR_COMPLEX)
         hipLaunchKernelGGL((trk_kernel<GSDR_ITEM_GR_COMPLEX>), grid, dim3(kTrkThreads), k->lds_bytes, s, k->d_consts, k->d_chans,
             (const float* const*)k->d_codes, (const float* const*)k->d_data_codes, iq, iq_first, iq_items, max_epochs, out,
-            nout, k->code_pad, k->data_pad, timing);
+            nout, k->code_pad, k->data_pad, timing, k->timing_wall);
     else
         hipLaunchKernelGGL((trk_kernel<GSDR_ITEM_CSHORT>), grid, dim3(kTrkThreads), k->lds_bytes, s, k->d_consts, k->d_chans,
             (const float* const*)k->d_codes, (const float* const*)k->d_data_codes, iq, iq_first, iq_items, max_epochs, out,
-            nout, k->code_pad, k->data_pad, timing);
+            nout, k->code_pad, k->data_pad, timing, k->timing_wall);
     GSDR_HIP(hipGetLastError());
     if (k->profiling)
         {
@@ -1375,7 +1376,11 @@ int gsdr_trk_create(int device, const gsdr_trk_conf* conf, gsdr_trk** out)
     k->code_pad = 1024;  // grows with the longest replica started (gsdr_trk_start)
     k->data_pad = 0;
     k->lds_bytes = lds_for(k->code_pad, k->data_pad);
-    if (const char* tv = std::getenv("GSDR_TRK_TIMING")) k->timing_on = std::atoi(tv) != 0;
+    if (const char* tv = std::getenv("GSDR_TRK_TIMING"))
+        {
+            k->timing_on = std::atoi(tv) != 0;
+            k->timing_wall = std::atoi(tv) == 2;
+        }
     hipError_t e = hipStreamCreateWithFlags(&k->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipMalloc(&k->d_consts, nch * sizeof(TrkConst));
     if (e == hipSuccess) e = hipMalloc(&k->d_chans, nch * sizeof(TrkChan));
@@ -1437,7 +1442,8 @@ void gsdr_trk_destroy(gsdr_trk* k)
     if (k->timing_on && k->tcount)
         {
             static const char* names[] = {"prep", "correlate", "update", "window-write"};
-            std::fprintf(stderr, "gsdr_trk timing: %llu calls, clock64 ticks per call:", (unsigned long long)k->tcount);
+            std::fprintf(stderr, "gsdr_trk timing: %llu calls, %s ticks per call:", (unsigned long long)k->tcount,
+                k->timing_wall ? "wall_clock64" : "clock64");
             for (int q = 0; q < 4; ++q) std::fprintf(stderr, " %s %.0f", names[q], k->tsum[q] / k->tcount);
             std::fprintf(stderr, "\n");
         }

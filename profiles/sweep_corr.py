@@ -31,12 +31,12 @@ def main():
                                max_blocks=B, num_doppler_bins=bench.D)
         acq.set_local_codes(codes, np.arange(1, bench.P + 1))
         res_dev = torch.zeros(B * bench.P * gsdr.ACQ_RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
-        for _ in range(3):
+        for _ in range(30):  # clocks settle
             acq.run_device(iq_dev.data_ptr(), B, bench.N, 0, res_dev.data_ptr(), sptr)
         torch.cuda.synchronize()
         acq.set_profiling(True)
         acq.read_profile()
-        for _ in range(10):
+        for _ in range(30):
             acq.run_device(iq_dev.data_ptr(), B, bench.N, 0, res_dev.data_ptr(), sptr)
         ms, n = acq.read_profile()
         res = res_dev.cpu().numpy().view(gsdr.ACQ_RESULT_DTYPE).reshape(B, bench.P)

@@ -31,7 +31,7 @@ def summarise(root, match):
     return {c: sum(v) / len(v) for c, v in vals.items()}
 
 
-KERNELS = {"acq_correlate_kernel": "acq_correlate", "acq_forward_kernel": "acq_forward_kernel"}
+KERNELS = {"acq_correlate_kernel": "acq_correlate", "acq_forward_kernel": "acq_forward"}
 
 
 def as_json(root):

@@ -171,7 +171,7 @@ struct SmConst  // Exponential_Smoother parameters
 
 struct TrkConst
 {
-    double fs_in, code_period, code_chip_rate, signal_carrier_freq, carrier_lock_threshold, current_correlation_time_s;
+    double fs_in, code_period, code_chip_rate, signal_carrier_freq, carrier_lock_threshold;
     uint64_t acq_sample_stamp;
     uint64_t pull_in_span;   // (pull_in_time_s + 1) * (int)fs_in: the integer-second test of :1797 flips there
     uint64_t bit_sync_span;  // (bit_synchronization_time_limit_s + 1) * (int)fs_in (:1866)
@@ -181,6 +181,11 @@ struct TrkConst
     uint32_t sec_str[5];     // secondary code string bit i = (code[i] == '1') (state-4 wipe-off)
     uint32_t data_sec_str;   // data secondary code (BeiDou NH), same form
     int32_t sec_len, data_sec_len, secondary, veml, track_pilot, iE, iP, iL;
+    // extended coherent integration (state 3, :1945-1983): narrow taps, loops, time
+    float shifts_narrow[kMaxTrkTaps];
+    float early_late_space_narrow_chips, dll_bw_narrow_hz;
+    double corr_time_ext;
+    int32_t enable_ext;
     int32_t vector_length, code_length_chips, code_samples_per_chip, symbols_per_bit;
     int32_t cn0_samples, cn0_min, max_code_lock_fail, max_carrier_lock_fail;
     int32_t extend_correlation_symbols, enable_fll_pull_in, enable_fll_steady_state, carrier_aiding;
@@ -188,6 +193,7 @@ struct TrkConst
     uint32_t prn;
     CfConst cf;
     SmConst sm[2];  // 0: CN0, 1: carrier lock test
+    CfConst cf_narrow;
 };
 
 // Mutable scalar loop state (dll_pll_veml_tracking.h:117-209 minus the
@@ -209,6 +215,8 @@ struct TrkHot
     int32_t state, current_prn_length_samples, current_symbol, current_data_symbol, cn0_estimation_counter;
     int32_t carrier_lock_fail_counter, code_lock_fail_counter;
     int32_t pull_in_transitory, cloop, acc_carrier_phase_initialized, flag_pll_180;
+    double corr_time;            // d_current_correlation_time_s
+    int32_t narrow, extend_count;  // after the switch to the extended correlator
 };
 
 // Device-memory image of the mutable part of one channel.
@@ -228,6 +236,7 @@ struct Prep  // lane-0 -> workgroup broadcast of one call's NCO
     int32_t go;
     int32_t woff;  // >= 0: this call's samples are in the LDS window at that offset
     int32_t fast;  // every code index of the call lies in [-L, 2L): branch-free wrap
+    int32_t narrow;  // the call uses the narrow tap shifts
 };
 
 // ------------------------------------------------------------------ wave-0 loop body
@@ -429,18 +438,18 @@ __device__ inline void run_dll_pll(const TrkConst& c, TrkHot& t, LoopFilter& lf)
     double carr_error_filt_hz;
     if ((t.pull_in_transitory && c.enable_fll_pull_in) || c.enable_fll_steady_state)
         {
-            const double carr_freq_error_hz = fll_diff_atan(t.P_accu_old, t.P_accu, 0, c.current_correlation_time_s) / kTwoPi;
+            const double carr_freq_error_hz = fll_diff_atan(t.P_accu_old, t.P_accu, 0, t.corr_time) / kTwoPi;
             t.P_accu_old = t.P_accu;
             if (t.pull_in_transitory && c.enable_fll_pull_in)
-                carr_error_filt_hz = (double)cf_error(c.cf, t, (float)carr_freq_error_hz, 0.0F,
-                    (float)c.current_correlation_time_s);
+                carr_error_filt_hz = (double)cf_error(t.narrow ? c.cf_narrow : c.cf, t, (float)carr_freq_error_hz, 0.0F,
+                    (float)t.corr_time);
             else
-                carr_error_filt_hz = (double)cf_error(c.cf, t, (float)carr_freq_error_hz, (float)carr_phase_error_hz,
-                    (float)c.current_correlation_time_s);
+                carr_error_filt_hz = (double)cf_error(t.narrow ? c.cf_narrow : c.cf, t, (float)carr_freq_error_hz, (float)carr_phase_error_hz,
+                    (float)t.corr_time);
         }
     else
         {
-            carr_error_filt_hz = (double)cf_error(c.cf, t, 0, (float)carr_phase_error_hz, (float)c.current_correlation_time_s);
+            carr_error_filt_hz = (double)cf_error(t.narrow ? c.cf_narrow : c.cf, t, 0, (float)carr_phase_error_hz, (float)t.corr_time);
         }
     t.carrier_doppler_hz = carr_error_filt_hz;
     const double code_error_chips =
@@ -614,9 +623,41 @@ __device__ inline void after_correlation(const TrkConst& c, TrkHot& t, LoopFilte
                             for (int w = 0; w < 5; ++w) t.circ[w] = 0u;
                             t.current_symbol = 0;
                             t.current_data_symbol = 0;
-                            t.state = 4;
                             o.flags |= GSDR_TRK_F_BIT_SYNC;
+                            if (c.enable_ext)
+                                {
+                                    // extended correlator: narrow loops and taps (:1945-1983)
+                                    t.extend_count = 0;
+                                    t.corr_time = c.corr_time_ext;
+                                    t.state = 3;
+                                    lf.T = (float)t.corr_time;
+                                    lf_update(lf);
+                                    lf.bw = c.dll_bw_narrow_hz;
+                                    lf_update(lf);
+                                    t.narrow = 1;
+                                    t.spc = c.early_late_space_narrow_chips;
+                                }
+                            else
+                                t.state = 4;
                         }
+                }
+        }
+    else if (t.state == 3)  // coherent integration (:1989-2026)
+        {
+            save_correlation_results(c, t, taps);
+            update_tracking_vars(c, t);
+            if (t.current_data_symbol == 0)
+                {
+                    o.prompt_i = (double)t.P_data_accu.x;
+                    o.prompt_q = (double)t.P_data_accu.y;
+                    o.flags |= GSDR_TRK_F_VALID_OUTPUT;
+                    t.P_data_accu = make_float2(0.f, 0.f);
+                }
+            t.extend_count++;
+            if (t.extend_count == c.extend_correlation_symbols - 1)
+                {
+                    t.extend_count = 0;
+                    t.state = 4;
                 }
         }
     else  // state 4
@@ -646,6 +687,7 @@ __device__ inline void after_correlation(const TrkConst& c, TrkHot& t, LoopFilte
                             t.P_data_accu = make_float2(0.f, 0.f);
                         }
                     t.VE_accu = t.E_accu = t.P_accu = t.L_accu = t.VL_accu = make_float2(0.f, 0.f);
+                    if (c.enable_ext) t.state = 3;
                 }
         }
     if (t.flag_pll_180) o.flags |= GSDR_TRK_F_PLL_180;
@@ -791,7 +833,7 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
         }
     if (tid < kMaxCn0) s_pbuf[tid] = gc->prompt_buffer[tid];
     __syncthreads();
-    if (s_state != 2 && s_state != 4)
+    if (s_state < 2 || s_state > 4)
         {
             if (tid == 0) nout[ch] = 0;
             return;
@@ -820,9 +862,10 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                 {
                     Prep p{};
                     const int64_t off = (int64_t)(t.next_sample - iq_first);
-                    p.go = (e < max_epochs) && (t.state == 2 || t.state == 4) && t.next_sample >= iq_first &&
+                    p.go = (e < max_epochs) && t.state >= 2 && t.state <= 4 && t.next_sample >= iq_first &&
                            (uint64_t)off + (uint64_t)vl <= iq_items;
                     p.off = off;
+                    p.narrow = t.narrow;
                     p.woff = -1;
                     if (use_window && win_base != INT64_MIN && off >= win_base && off - win_base + vl <= kWinCore + kHalo)
                         p.woff = (int32_t)(off - win_base);
@@ -841,7 +884,7 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                             float smin = 1e30f, smax = -1e30f;
                             for (int k = 0; k < K; ++k)
                                 {
-                                    const float sr = gsdr::sub_rn(c.shifts[k], p.rem_code);
+                                    const float sr = gsdr::sub_rn(t.narrow ? c.shifts_narrow[k] : c.shifts[k], p.rem_code);
                                     smin = fminf(smin, sr);
                                     smax = fmaxf(smax, sr);
                                 }
@@ -875,7 +918,8 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
             }
             float sh_rem[kMaxTrkTaps];
 #pragma unroll
-            for (int k = 0; k < kMaxTrkTaps; ++k) sh_rem[k] = gsdr::sub_rn(c.shifts[k], p.rem_code);
+            for (int k = 0; k < kMaxTrkTaps; ++k)
+                sh_rem[k] = gsdr::sub_rn(p.narrow ? c.shifts_narrow[k] : c.shifts[k], p.rem_code);
             if (K <= 3)
                 correlate_call<IT, 3, false>(iq, s_win, s_code, s_data, p, vl, L, sh_rem, ph, acc);
             else if (!data)
@@ -1113,7 +1157,8 @@ void sm_set(SmConst& k, float alpha, float min_value, float offset, int samples)
     k.samples_init = std::max(1, samples);
 }
 
-// tap shifts (:466-507 / :850-862), in replica samples
+// tap shifts (:466-507 / :850-862), in replica samples; the narrow set of the
+// extended correlator (:1963-1977)
 void set_shifts(const gsdr_trk_conf& cf, TrkConst& c)
 {
     const float spc = (float)c.code_samples_per_chip;
@@ -1124,12 +1169,20 @@ void set_shifts(const gsdr_trk_conf& cf, TrkConst& c)
             c.shifts[2] = 0.0F;
             c.shifts[3] = cf.early_late_space_chips * spc;
             c.shifts[4] = cf.very_early_late_space_chips * spc;
+            c.shifts_narrow[0] = -cf.very_early_late_space_narrow_chips * spc;
+            c.shifts_narrow[1] = -cf.early_late_space_narrow_chips * spc;
+            c.shifts_narrow[2] = 0.0F;
+            c.shifts_narrow[3] = cf.early_late_space_narrow_chips * spc;
+            c.shifts_narrow[4] = cf.very_early_late_space_narrow_chips * spc;
         }
     else
         {
             c.shifts[0] = -cf.early_late_space_chips * spc;
             c.shifts[1] = 0.0F;
             c.shifts[2] = cf.early_late_space_chips * spc;
+            c.shifts_narrow[0] = -cf.early_late_space_narrow_chips * spc;
+            c.shifts_narrow[1] = 0.0F;
+            c.shifts_narrow[2] = cf.early_late_space_narrow_chips * spc;
         }
 }
 
@@ -1179,7 +1232,6 @@ void init_channel(const gsdr_trk_conf& cf, TrkConst& c, TrkChan& ch)
     else
         set_secondary(c, kGpsCaPreamble, kPreambleLen);
     c.carrier_lock_threshold = cf.carrier_lock_th;
-    c.current_correlation_time_s = c.code_period;
     c.early_late_space_chips = cf.early_late_space_chips;
     c.vector_length = (int32_t)cf.vector_length;
     c.code_length_chips = sp.length_chips;
@@ -1199,12 +1251,17 @@ void init_channel(const gsdr_trk_conf& cf, TrkConst& c, TrkChan& ch)
     c.n_taps = c.veml ? 5 : 3;
     set_shifts(cf, c);
     cf_set_params(c.cf, cf.fll_bw_hz, cf.pll_bw_hz, cf.pll_filter_order);
+    cf_set_params(c.cf_narrow, cf.fll_bw_hz, cf.pll_bw_narrow_hz, cf.pll_filter_order);
+    c.early_late_space_narrow_chips = cf.early_late_space_narrow_chips;
+    c.dll_bw_narrow_hz = cf.dll_bw_narrow_hz;
+    c.enable_ext = cf.extend_correlation_symbols > 1 ? 1 : 0;
     // Exponential_Smoother defaults (exponential_smoother.h:58-63) + dll_pll_veml_tracking.cc:540-552
     sm_set(c.sm[0], cf.cn0_smoother_alpha, 25.0F, 12.0F, cf.cn0_smoother_samples / (int)(c.code_period * 1000.0));
     sm_set(c.sm[1], cf.carrier_lock_test_smoother_alpha, -1.0F, 0.0F, cf.carrier_lock_test_smoother_samples);
     TrkHot& t = ch.h;
     t.spc = cf.early_late_space_chips;
     t.code_freq_chips = c.code_chip_rate;
+    t.corr_time = c.code_period;
     sm_reset(t, 0);
     sm_reset(t, 1);
     t.state = 0;
@@ -1341,8 +1398,8 @@ int gsdr_trk_create(int device, const gsdr_trk_conf* conf, gsdr_trk** out)
         "gsdr_trk_create: signal %d not implemented", conf->signal);
     GSDR_REQUIRE(conf->item_type == GSDR_ITEM_GR_COMPLEX || conf->item_type == GSDR_ITEM_CSHORT, GSDR_E_ARG,
         "gsdr_trk_create: unknown item type %d", conf->item_type);
-    GSDR_REQUIRE(conf->extend_correlation_symbols == 1, GSDR_E_UNSUPPORTED,
-        "gsdr_trk_create: extend_correlation_symbols > 1 not implemented yet");
+    GSDR_REQUIRE(conf->extend_correlation_symbols >= 1, GSDR_E_ARG,
+        "gsdr_trk_create: extend_correlation_symbols must be >= 1");
     GSDR_REQUIRE(conf->high_dyn == 0, GSDR_E_UNSUPPORTED, "gsdr_trk_create: high_dyn not implemented in the loop");
     GSDR_REQUIRE(conf->cn0_samples >= 1 && conf->cn0_samples <= kMaxCn0, GSDR_E_UNSUPPORTED,
         "gsdr_trk_create: cn0_samples %d outside [1,%d]", conf->cn0_samples, kMaxCn0);
@@ -1527,7 +1584,13 @@ int gsdr_trk_start(gsdr_trk* k, int ch, uint32_t prn, const float* code, int cod
     t.cn0_db_hz = 0.0;
     t.evm = 0.0;
     set_shifts(k->conf, c);
-    c.current_correlation_time_s = c.code_period;
+    t.corr_time = c.code_period;  // :860
+    t.narrow = 0;
+    t.extend_count = 0;
+    c.extend_correlation_symbols = std::max(1, k->conf.extend_correlation_symbols);  // :657
+    if (k->conf.signal == GSDR_SIGNAL_BDS_B1 && ((prn > 0 && prn < 6) || prn > 58))
+        c.extend_correlation_symbols = std::min(c.extend_correlation_symbols, 2);  // GEO (:775-778)
+    c.corr_time_ext = (double)((float)c.extend_correlation_symbols * (float)c.code_period);  // :1949
     cf_set_params(c.cf, k->conf.fll_bw_hz, k->conf.pll_bw_hz, k->conf.pll_filter_order);
     tc.code_filter.bw = k->conf.dll_bw_hz;
     lf_update(tc.code_filter);

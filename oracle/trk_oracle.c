@@ -461,6 +461,7 @@ typedef struct orc_trk
     const char* secondary_code_string;
     const char* data_secondary_code_string;
     int secondary, veml, track_pilot;
+    int extend, extend_count, enable_ext; /* d_extend_correlation_symbols(_count), d_enable_extended_integration */
     int iE, iP, iL; /* tap slots of Early / Prompt / Late (VEML: VE 0, VL 4) */
     int n_taps;
     float shifts[5];
@@ -538,7 +539,7 @@ void orc_trk_conf_default(gsdr_trk_conf* c)
 /* constructor (dll_pll_veml_tracking.cc:85-560) and the signal table (:170-430) */
 orc_trk* orc_trk_create(const gsdr_trk_conf* conf)
 {
-    if (conf->signal < GSDR_SIGNAL_GPS_1C || conf->signal > GSDR_SIGNAL_BDS_B1 || conf->extend_correlation_symbols != 1 ||
+    if (conf->signal < GSDR_SIGNAL_GPS_1C || conf->signal > GSDR_SIGNAL_BDS_B1 || conf->extend_correlation_symbols < 1 ||
         conf->high_dyn || conf->cn0_samples > MAX_CN0_SAMPLES || conf->cn0_samples < 1)
         return NULL;
     orc_trk* t = (orc_trk*)calloc(1, sizeof(orc_trk));
@@ -588,6 +589,10 @@ orc_trk* orc_trk_create(const gsdr_trk_conf* conf)
             t->data_secondary_code_string = BEIDOU_B1I_SECONDARY_CODE_STR_REF;
         }
     t->track_pilot = t->p.track_pilot;
+    /* :511-520 */
+    t->enable_ext = t->p.extend_correlation_symbols > 1;
+    if (!t->enable_ext) t->p.extend_correlation_symbols = 1;
+    t->extend = t->p.extend_correlation_symbols;
     /* adapters: vector_length = round(fs_in / (chip rate / code length)) */
     if (t->p.vector_length == 0)
         t->p.vector_length = (uint32_t)lround(t->p.fs_in / (t->code_chip_rate / (double)t->code_length_chips));
@@ -661,10 +666,14 @@ int orc_trk_start(orc_trk* t, uint32_t prn, const float* code, int code_samples,
 {
     if (code_samples < 1 || code_samples > MAX_CODE) return -1;
     if (t->track_pilot && t->data_code_samples < 1) return -1;
+    t->extend = t->p.extend_correlation_symbols; /* :657 */
+    t->extend_count = 0;
     if (t->p.signal == GSDR_SIGNAL_BDS_B1)
         {
             if ((prn > 0 && prn < 6) || prn > 58)
                 {
+                    if (t->extend > BEIDOU_B1I_GEO_TELEMETRY_SYMBOLS_PER_BIT_REF)
+                        t->extend = BEIDOU_B1I_GEO_TELEMETRY_SYMBOLS_PER_BIT_REF; /* :775-778 */
                     /* GEO (D2): preamble search, 2 symbols per bit (:762-778) */
                     t->symbols_per_bit = BEIDOU_B1I_GEO_TELEMETRY_SYMBOLS_PER_BIT_REF;
                     t->secondary = 0;
@@ -1062,9 +1071,55 @@ static int trk_call(orc_trk* t, const float* in, const float* taps_in, uint64_t 
                                 t->circ_head = 0;
                                 t->current_symbol = 0;
                                 t->current_data_symbol = 0;
-                                t->state = 4;
                                 r->flags |= GSDR_TRK_F_BIT_SYNC;
+                                if (t->enable_ext)
+                                    {
+                                        /* extended correlator: narrow loops and taps (:1945-1983) */
+                                        t->extend_count = 0;
+                                        t->current_correlation_time_s = (double)((float)t->extend * (float)t->code_period);
+                                        t->state = 3;
+                                        t->code_filter.T = (float)t->current_correlation_time_s;
+                                        lf_update(&t->code_filter);
+                                        t->code_filter.bw = t->p.dll_bw_narrow_hz;
+                                        lf_update(&t->code_filter);
+                                        pll_set_params(&t->carrier_filter, t->p.fll_bw_hz, t->p.pll_bw_narrow_hz, t->p.pll_filter_order);
+                                        const float spcf = (float)t->code_samples_per_chip;
+                                        if (t->veml)
+                                            {
+                                                t->shifts[0] = -t->p.very_early_late_space_narrow_chips * spcf;
+                                                t->shifts[1] = -t->p.early_late_space_narrow_chips * spcf;
+                                                t->shifts[3] = t->p.early_late_space_narrow_chips * spcf;
+                                                t->shifts[4] = t->p.very_early_late_space_narrow_chips * spcf;
+                                            }
+                                        else
+                                            {
+                                                t->shifts[0] = -t->p.early_late_space_narrow_chips * spcf;
+                                                t->shifts[2] = t->p.early_late_space_narrow_chips * spcf;
+                                            }
+                                        t->spc = t->p.early_late_space_narrow_chips;
+                                    }
+                                else
+                                    t->state = 4;
                             }
+                    }
+                break;
+            }
+        case 3:
+            {
+                /* coherent integration (:1989-2026) */
+                correlate_or_copy(t, in, taps_in);
+                save_correlation_results(t);
+                update_tracking_vars(t);
+                if (t->current_data_symbol == 0)
+                    {
+                        fill_output(t, r);
+                        t->P_data_accu = (tcf){0.0F, 0.0F};
+                    }
+                t->extend_count++;
+                if (t->extend_count == t->extend - 1)
+                    {
+                        t->extend_count = 0;
+                        t->state = 4;
                     }
                 break;
             }
@@ -1072,7 +1127,7 @@ static int trk_call(orc_trk* t, const float* in, const float* taps_in, uint64_t 
             {
                 correlate_or_copy(t, in, taps_in);
                 save_correlation_results(t);
-                if (!cn0_and_lock(t, t->code_period * (double)t->p.extend_correlation_symbols))
+                if (!cn0_and_lock(t, t->code_period * (double)t->extend))
                     {
                         clear_tracking_vars(t);
                         t->state = 0;
@@ -1093,6 +1148,7 @@ static int trk_call(orc_trk* t, const float* in, const float* taps_in, uint64_t 
                                 t->P_data_accu = (tcf){0.0F, 0.0F};
                             }
                         t->VE_accu = t->E_accu = t->P_accu = t->L_accu = t->VL_accu = (tcf){0.0F, 0.0F};
+                        if (t->enable_ext) t->state = 3;
                     }
                 break;
             }

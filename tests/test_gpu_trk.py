@@ -214,12 +214,15 @@ def _conf_sig(fs, sig, nch=1, pilot=1):
     return c
 
 
-def _open_loop_sig(g, iq, code, data_code, fs, acq_dop, shifts_chips, spc, chip_rate, vl, iP):
+def _open_loop_sig(g, iq, code, data_code, fs, acq_dop, shifts_chips, spc, chip_rate, vl, iP, narrow_chips=None):
     """Check 1 for any signal: every call's taps (and the data prompt) against the
-    oracle correlator fed with the GPU's own incoming NCO state."""
-    shifts = (np.asarray(shifts_chips, np.float32) * np.float32(spc)).astype(np.float32)
+    oracle correlator fed with the GPU's own incoming NCO state (narrow tap shifts
+    in states 3/4 of the extended correlator)."""
+    wide = (np.asarray(shifts_chips, np.float32) * np.float32(spc)).astype(np.float32)
+    narrow = None if narrow_chips is None else (np.asarray(narrow_chips, np.float32) * np.float32(spc)).astype(np.float32)
     worst = 0.0
     for e in range(len(g)):
+        shifts = narrow if (narrow is not None and g["state"][e] in (3, 4)) else wide
         if e == 0:
             rem_carr, dop, rem_samples, code_freq = 0.0, acq_dop, 0.0, chip_rate
         else:
@@ -295,3 +298,50 @@ def test_beidou_b1i_matches_oracle(prn):
     assert g["state"][-1] == 4
     out = np.nonzero(g["flags"] & gsdr.TRK_F_VALID_OUTPUT)[0]
     assert len(out) > 5 and np.all(np.diff(out) == (2 if synth.bds_is_geo(prn) else 20))
+
+
+@pytest.mark.parametrize("sig", ["gal_c4", "gps_ext10"])
+def test_extended_integration_matches_oracle(sig):
+    """Extended coherent integration (state 3, dll_pll_veml_tracking.cc:1945-2026):
+    config C4's Galileo E1 settings (conf/gnss-sdr_galileo_E1_extended_correlator_byte.conf:
+    4 symbols, narrow PLL/DLL, narrow VEML taps) and GPS L1 C/A over 10 ms."""
+    if sig == "gal_c4":
+        fs = 4.0e6
+        sat = synth.GalileoSatellite(11, 1234.5, 1000.3, 50.0, 0.7)
+        iq = synth.gal_e1_iq(fs, int(1.6 * fs), [sat], seed_offset=5)
+        tau = sat.code_delay_chips / (1.023e6 * (1 + sat.doppler_hz / 1.57542e9)) * fs
+        delay, dop, prn = float(round(tau) % 16000), 1250.0, 11
+        code, dcode = synth.gal_e1_sinboc11(11, pilot=True), synth.gal_e1_sinboc11(11)
+        c = _conf_sig(fs, gsdr.SIGNAL_GAL_1B, 1, 1)
+        c["pll_bw_hz"], c["dll_bw_hz"] = 15.0, 1.0
+        c["pll_bw_narrow_hz"], c["dll_bw_narrow_hz"] = 5.0, 0.25
+        c["early_late_space_chips"], c["very_early_late_space_chips"] = 0.15, 0.6
+        c["early_late_space_narrow_chips"], c["very_early_late_space_narrow_chips"] = 0.06, 0.25
+        c["extend_correlation_symbols"] = 4
+        wide, narrow, spc, rate, vl, iP, n_calls, osig = [-0.6, -0.15, 0, 0.15, 0.6], [-0.25, -0.06, 0, 0.06, 0.25], 2, \
+            1.023e6, 16000, 2, 380, 1
+    else:
+        fs = 2.0e6
+        sat = synth.Satellite(7, 1234.5, 300.3, 45.0, 0.7, preamble_every_bits=25, code_doppler=True)
+        iq = synth.gps_l1_iq(fs, int(2.0 * fs), [sat], seed_offset=5)
+        delay, dop = _acq(sat, fs)
+        prn, code, dcode = 7, synth.gps_ca_chips(7), None
+        c = _conf(fs)
+        c["extend_correlation_symbols"] = 10
+        wide, narrow, spc, rate, vl, iP, n_calls, osig = [-0.25, 0, 0.25], [-0.15, 0, 0.15], 1, 1.023e6, 2000, 1, 1990, 0
+    t = gsdr.Tracking(c)
+    fg = t.start(0, prn, code, delay, dop, 0, 0, data_code=dcode)
+    rec, n = t.run(iq, 0, n_calls)
+    g = rec[0][:n[0]]
+    oc = c[0:1].view(trk.TRK_CONF_DTYPE)
+    free = trk.Channel(oc)
+    fo = free.start(code, delay, dop, 0, 0, prn=prn, data_code=dcode)
+    assert fg == fo
+    assert _open_loop_sig(g, iq, code, dcode, fs, dop, wide, spc, rate, vl, iP, narrow) <= 1e-4
+    rep = trk.Channel(oc)
+    rep.start(code, delay, dop, 0, 0, prn=prn, data_code=dcode)
+    _replay_check(g, rep, sig)
+    orc, _ = free.run(iq, 0, fo, n_calls)
+    _free_check(g, orc, sig)
+    st = set(np.unique(g["state"]).tolist())
+    assert {2, 3, 4} <= st

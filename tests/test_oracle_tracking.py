@@ -157,3 +157,29 @@ def test_beidou_b1i_channel(prn, per):
     out = np.nonzero(recs["flags"] & trk.F_VALID_OUTPUT)[0]
     assert len(out) > 5 and np.all(np.diff(out) == per)
     assert not np.any(recs["flags"] & trk.F_LOSS_OF_LOCK)
+
+
+def test_extended_integration_cycle():
+    """State 3 (dll_pll_veml_tracking.cc:1945-2026): after the secondary-code lock
+    the channel alternates extend-1 accumulate-only calls (3) with one loop-update
+    call (4) on the narrow loops and taps; Galileo E1 with 4 symbols (config C4)."""
+    fs = 4.0e6
+    c = _conf_sig(fs, 1, 1)
+    c["extend_correlation_symbols"] = 4
+    c["pll_bw_narrow_hz"] = 5.0
+    c["dll_bw_narrow_hz"] = 0.25
+    c["early_late_space_narrow_chips"] = 0.06
+    c["very_early_late_space_narrow_chips"] = 0.25
+    sat = synth.GalileoSatellite(11, 1234.5, 1000.3, 50.0, 0.7)
+    iq = synth.gal_e1_iq(fs, int(1.6 * fs), [sat], seed_offset=5)
+    ch = trk.Channel(c)
+    tau = sat.code_delay_chips / (1.023e6 * (1 + sat.doppler_hz / 1.57542e9)) * fs
+    first = ch.start(synth.gal_e1_sinboc11(11, pilot=True), float(round(tau) % 16000), 1250.0, 0, 0, prn=11,
+                     data_code=synth.gal_e1_sinboc11(11))
+    recs, _ = ch.run(iq, 0, first, 1000)
+    sync = int(np.nonzero(recs["flags"] & trk.F_BIT_SYNC)[0][0])
+    after = recs["state"][sync + 1:sync + 1 + 16]
+    np.testing.assert_array_equal(after, [3, 3, 3, 4] * 4)
+    assert np.all((recs["flags"][sync + 1:] & trk.F_VALID_OUTPUT) != 0)  # one 4 ms symbol per call
+    assert abs(np.mean(recs[-60:]["carrier_doppler_hz"]) - sat.doppler_hz) < 2.0
+    assert not np.any(recs["flags"] & trk.F_LOSS_OF_LOCK)

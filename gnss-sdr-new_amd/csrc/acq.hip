@@ -164,9 +164,9 @@ int gsdr_acq_create(int device, const gsdr_acq_conf* conf, gsdr_acq** out)
             return GSDR_E_UNSUPPORTED;
         }
     int rc = dispatch(a, 4, nullptr, 0, 0, 0, nullptr, nullptr, 0);
-    if (rc == GSDR_OK && N == 4000 && !a->general)
+    if (rc == GSDR_OK && !a->general && default_pk_variant(N) > 0)
         {
-            int v = kDefaultCorrVariant4000;
+            int v = default_pk_variant(N);
             if (const char* e = std::getenv("GSDR_ACQ_CORR_VARIANT")) v = std::atoi(e);
             rc = gsdr_acq_impl::setup_corr_variant(a, v);
         }

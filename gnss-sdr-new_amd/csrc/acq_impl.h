@@ -29,6 +29,19 @@ using gsdr::fft::Plan;
 // Default correlate variant at N = 4000 (see GSDR_PK_VARIANTS).
 constexpr int kDefaultCorrVariant4000 = 30;
 
+// Default packed variant for an FFT size (0: none, the generic kernels).
+inline int default_pk_variant(uint32_t N)
+{
+    switch (N)
+        {
+        case 4000: return kDefaultCorrVariant4000;
+        case 16000: return 60;
+        case 8000: return 61;
+        case 2000: return 62;
+        default: return 0;
+        }
+}
+
 struct RowStat
 {
     float max;
@@ -379,81 +392,6 @@ __global__ void __launch_bounds__(MP::NT) __attribute__((amdgpu_waves_per_eu(WPE
                         }
                     stats[((size_t)b * P + p0 + q) * D + d] = RowStat{best.max, best.idx, best.sum, 0};
                 }
-        }
-}
-
-// ---------------------------------------------------------------- K_correlate (packed f32, multi-transform)
-// PB PRNs of one row (b, d) per workgroup, transformed together on the packed
-// multi-transform plan (fft_pk.h PkMultiPlan), whose butterfly packing keeps the
-// waves full; one XCD-aware 1-D grid over (row, PRN group) as above.
-template <class MP, int WPE>
-__global__ void __launch_bounds__(MP::NT) __attribute__((amdgpu_waves_per_eu(WPE))) acq_correlate_pkm_kernel(
-    const float2* __restrict__ X, const float2* __restrict__ code_fft, RowStat* __restrict__ stats,
-    const float2* __restrict__ tw, uint32_t D, uint32_t P, uint32_t nblocks)
-{
-    using gsdr::pk::c2;
-    constexpr int NT = MP::NT;
-    constexpr int NW = NT / 64;
-    constexpr int PB = MP::PB;
-    constexpr uint32_t N = MP::N;
-    extern __shared__ float2 lds_raw[];
-    c2* lds = reinterpret_cast<c2*>(lds_raw);
-    RowStat* scratch = reinterpret_cast<RowStat*>(lds_raw + (size_t)PB * MP::STRIDE);
-    const uint32_t G = (P + PB - 1) / PB;
-    const uint32_t nrows = nblocks * D;
-    const uint32_t id = blockIdx.x;
-    const uint32_t full = nrows >> 3;
-    uint32_t row, g;
-    if (id < full * 8u * G)
-        {
-            const uint32_t xcd = id & 7u, slot = id >> 3;
-            row = (slot / G) * 8u + xcd;
-            g = slot - (slot / G) * G;
-        }
-    else
-        {
-            const uint32_t t = id - full * 8u * G;
-            row = full * 8u + t / G;
-            g = t - (t / G) * G;
-        }
-    const uint32_t b = row / D, d = row - (row / D) * D;
-    const uint32_t p0 = g * PB;
-    const int np = (int)min((uint32_t)PB, P - p0);
-    const c2* x = reinterpret_cast<const c2*>(X) + (size_t)row * N;
-    const c2* cb = reinterpret_cast<const c2*>(code_fft) + (size_t)p0 * N;
-    float best[PB], sum[PB];
-    uint32_t bidx[PB];
-#pragma unroll
-    for (int t = 0; t < PB; ++t)
-        {
-            best[t] = -1.0f;
-            sum[t] = 0.0f;
-            bidx[t] = 0xffffffffu;
-        }
-    // conj(X . conj(C)) = conj(X) . C ; |IFFT(Y)| = |FFT(conj(Y))|.  A partial last
-    // group repeats its last PRN in the idle transforms (results discarded).
-    auto load = [&](int t, int, int i) -> c2 {
-        const int tc = PB == 1 ? 0 : min(t, np - 1);
-        return gsdr::pk::conj_mul(x[i], cb[(size_t)tc * N + i]);
-    };
-    auto store = [&](auto T, int i, c2 v) {
-        constexpr int t = decltype(T)::value;
-        const float m = __builtin_fmaf(v.x, v.x, v.y * v.y);
-        if (m > best[t])
-            {
-                best[t] = m;
-                bidx[t] = (uint32_t)i;
-            }
-        sum[t] += m;
-    };
-    MP::run(lds, tw, load, store);
-#pragma unroll
-    for (int t = 0; t < PB; ++t) block_reduce_stat<NT>(best[t], bidx[t], sum[t], scratch + t * NW);
-    if (threadIdx.x == 0)
-        {
-#pragma unroll
-            for (int t = 0; t < PB; ++t)
-                if (t < np) stats[((size_t)b * P + p0 + t) * D + d] = RowStat{best[t], bidx[t], sum[t], 0};
         }
 }
 
@@ -857,7 +795,7 @@ struct gsdr_acq
     float threshold{0.0f};
     int nt{256};
     int variant{0};
-    int corr_variant{0};      // 0: single-transform correlate kernel; >0: GSDR_PK(M)_VARIANTS id
+    int corr_variant{0};      // 0: the generic LDS kernels; >0: a GSDR_PK_VARIANTS id (packed forward + correlate)
     size_t corr_lds_bytes{0};
     Plan plan{};
     gsdr::fft::Plan4 plan4{};  // four-step plan (variants 20-22, N beyond one workgroup's LDS)
@@ -906,19 +844,16 @@ size_t item_bytes(int it) { return it == GSDR_ITEM_CSHORT ? 4 : 8; }
 
 // Correlate-kernel variants for N = 4000 (env GSDR_ACQ_CORR_VARIANT selects one;
 // 0 = the single-transform kernel of the plan variant).
-// Packed-f32 variants: (id, plan, PRNs per workgroup).
+// Packed-f32 correlate (and forward) variants: (id, plan, PRNs per workgroup,
+// waves-per-EU hint).  30/35/37 are N = 4000 plans (30 the default); 60-62 the
+// other compile-time sizes (1 ms at 16 / 8 / 2 Msps).
 #define GSDR_PK_VARIANTS(X)                                              \
     X(30, (gsdr::pk::PkPlan<256, true, 25, 16, 10>), 1, 1)              \
-    X(31, (gsdr::pk::PkPlan<256, false, 20, 20, 10>), 1, 1)             \
-    X(32, (gsdr::pk::PkPlan<256, false, 25, 16, 10>), 1, 1)             \
     X(35, (gsdr::pk::PkPlan<256, true, 20, 20, 10>), 1, 1)              \
-    X(37, (gsdr::pk::PkPlan<512, true, 25, 16, 10>), 2, 1)
-
-// Packed multi-transform variants: (id, plan, waves per EU hint).
-#define GSDR_PKM_VARIANTS(X)                                              \
-    X(43, (gsdr::pk::PkMultiPlan<256, 1, false, 20, 20, 10>), 1)        \
-    X(45, (gsdr::pk::PkMultiPlan<320, 2, true, 25, 16, 10>), 1)         \
-    X(47, (gsdr::pk::PkMultiPlan<256, 1, false, 25, 16, 10>), 1)
+    X(37, (gsdr::pk::PkPlan<512, true, 25, 16, 10>), 2, 1)              \
+    X(60, (gsdr::pk::PkPlan<1024, true, 16, 10, 10, 10>), 1, 1)         \
+    X(61, (gsdr::pk::PkPlan<512, true, 20, 20, 20>), 1, 1)              \
+    X(62, (gsdr::pk::PkPlan<256, true, 20, 10, 10>), 1, 1)
 
 template <class PT>
 int set_lds_attrs(size_t bytes)

@@ -16,53 +16,46 @@ int launch_corr_variant(gsdr_acq* a, uint32_t nblocks, hipStream_t s)
                 a->corr_lds_bytes, s, a->d_X, a->d_code_fft, a->d_stats, a->d_tw, a->D, a->nprn, nblocks);      \
             return GSDR_OK;                                                                                     \
         }
-#define GSDR_PKM_CASE(ID, MP, WPE)                                                                              \
+#define GSDR_UNPAREN(...) __VA_ARGS__
+    switch (a->corr_variant)
+        {
+            GSDR_PK_VARIANTS(GSDR_PK_CASE)
+        default: gsdr::set_error("internal: bad correlate variant %d", a->corr_variant); return GSDR_E_STATE;
+        }
+#undef GSDR_PK_CASE
+#undef GSDR_UNPAREN
+}
+
+// Forward spectra on the packed plan of the selected variant.
+int launch_forward_pk(gsdr_acq* a, const void* iq, int item_type, uint32_t nblocks, uint64_t stride, hipStream_t s)
+{
+#define GSDR_PKF_CASE(ID, MP, PG, WPE)                                                                          \
     case ID:                                                                                                    \
         {                                                                                                       \
             using M = GSDR_UNPAREN MP;                                                                          \
-            const uint32_t groups = (a->nprn + M::PB - 1) / M::PB;                                              \
-            hipLaunchKernelGGL((acq_correlate_pkm_kernel<M, WPE>), dim3(nblocks * a->D * groups), dim3(M::NT),  \
-                a->corr_lds_bytes, s, a->d_X, a->d_code_fft, a->d_stats, a->d_tw, a->D, a->nprn, nblocks);      \
+            if (item_type == GSDR_ITEM_GR_COMPLEX)                                                              \
+                hipLaunchKernelGGL((acq_forward_pk_kernel<M, GSDR_ITEM_GR_COMPLEX>), dim3(nblocks, a->D),       \
+                    dim3(M::NT), M::lds_bytes(), s, iq, stride, a->d_wipe, a->d_X, a->d_tw, a->consumed, a->D); \
+            else                                                                                                \
+                hipLaunchKernelGGL((acq_forward_pk_kernel<M, GSDR_ITEM_CSHORT>), dim3(nblocks, a->D),           \
+                    dim3(M::NT), M::lds_bytes(), s, iq, stride, a->d_wipe, a->d_X, a->d_tw, a->consumed, a->D); \
+            GSDR_HIP(hipGetLastError());                                                                        \
             return GSDR_OK;                                                                                     \
         }
 #define GSDR_UNPAREN(...) __VA_ARGS__
     switch (a->corr_variant)
         {
-            GSDR_PK_VARIANTS(GSDR_PK_CASE)
-            GSDR_PKM_VARIANTS(GSDR_PKM_CASE)
-        default: gsdr::set_error("internal: bad correlate variant %d", a->corr_variant); return GSDR_E_STATE;
+            GSDR_PK_VARIANTS(GSDR_PKF_CASE)
+        default: gsdr::set_error("internal: bad forward variant %d", a->corr_variant); return GSDR_E_STATE;
         }
-#undef GSDR_PK_CASE
-#undef GSDR_PKM_CASE
+#undef GSDR_PKF_CASE
 #undef GSDR_UNPAREN
-}
-
-// Forward spectra on the packed plan (N = 4000 with a packed correlate variant).
-using ForwardPk = gsdr::pk::PkPlan<256, true, 25, 16, 10>;
-
-int launch_forward_pk(gsdr_acq* a, const void* iq, int item_type, uint32_t nblocks, uint64_t stride, hipStream_t s)
-{
-    const size_t lds = ForwardPk::lds_bytes();
-    if (item_type == GSDR_ITEM_GR_COMPLEX)
-        hipLaunchKernelGGL((acq_forward_pk_kernel<ForwardPk, GSDR_ITEM_GR_COMPLEX>), dim3(nblocks, a->D),
-            dim3(ForwardPk::NT), lds, s, iq, stride, a->d_wipe, a->d_X, a->d_tw, a->consumed, a->D);
-    else
-        hipLaunchKernelGGL((acq_forward_pk_kernel<ForwardPk, GSDR_ITEM_CSHORT>), dim3(nblocks, a->D),
-            dim3(ForwardPk::NT), lds, s, iq, stride, a->d_wipe, a->d_X, a->d_tw, a->consumed, a->D);
-    GSDR_HIP(hipGetLastError());
-    return GSDR_OK;
 }
 
 // Select and configure a correlate variant (N must be 4000).
 int setup_corr_variant(gsdr_acq* a, int v)
 {
-    {
-        const size_t lds = ForwardPk::lds_bytes();
-        GSDR_HIP(hipFuncSetAttribute((const void*)acq_forward_pk_kernel<ForwardPk, GSDR_ITEM_GR_COMPLEX>,
-            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        GSDR_HIP(hipFuncSetAttribute((const void*)acq_forward_pk_kernel<ForwardPk, GSDR_ITEM_CSHORT>,
-            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    }
+
 #define GSDR_PK_SETUP(ID, MP, PG, WPE)                                                                               \
     case ID:                                                                                                    \
         {                                                                                                       \
@@ -70,16 +63,15 @@ int setup_corr_variant(gsdr_acq* a, int v)
             a->corr_lds_bytes = M::lds_bytes() + (size_t)2 * (M::NT / 64) * sizeof(RowStat);                   \
             GSDR_HIP(hipFuncSetAttribute((const void*)acq_correlate_pk_kernel<M, PG, WPE>,                          \
                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)a->corr_lds_bytes));                           \
-            a->corr_variant = ID;                                                                               \
-            return GSDR_OK;                                                                                     \
-        }
-#define GSDR_PKM_SETUP(ID, MP, WPE)                                                                             \
-    case ID:                                                                                                    \
-        {                                                                                                       \
-            using M = GSDR_UNPAREN MP;                                                                          \
-            a->corr_lds_bytes = M::lds_bytes() + (size_t)M::PB * (M::NT / 64) * sizeof(RowStat);               \
-            GSDR_HIP(hipFuncSetAttribute((const void*)acq_correlate_pkm_kernel<M, WPE>,                        \
-                hipFuncAttributeMaxDynamicSharedMemorySize, (int)a->corr_lds_bytes));                           \
+            if (M::N != (int)a->N)                                                                              \
+                {                                                                                               \
+                    gsdr::set_error("correlate variant %d is for N = %d, not %u", ID, M::N, a->N);            \
+                    return GSDR_E_UNSUPPORTED;                                                                  \
+                }                                                                                               \
+            GSDR_HIP(hipFuncSetAttribute((const void*)acq_forward_pk_kernel<M, GSDR_ITEM_GR_COMPLEX>,          \
+                hipFuncAttributeMaxDynamicSharedMemorySize, (int)M::lds_bytes()));                              \
+            GSDR_HIP(hipFuncSetAttribute((const void*)acq_forward_pk_kernel<M, GSDR_ITEM_CSHORT>,              \
+                hipFuncAttributeMaxDynamicSharedMemorySize, (int)M::lds_bytes()));                              \
             a->corr_variant = ID;                                                                               \
             return GSDR_OK;                                                                                     \
         }
@@ -87,11 +79,9 @@ int setup_corr_variant(gsdr_acq* a, int v)
     switch (v)
         {
             GSDR_PK_VARIANTS(GSDR_PK_SETUP)
-            GSDR_PKM_VARIANTS(GSDR_PKM_SETUP)
         default: a->corr_variant = 0; return GSDR_OK;
         }
 #undef GSDR_PK_SETUP
-#undef GSDR_PKM_SETUP
 #undef GSDR_UNPAREN
 }
 

@@ -2,17 +2,19 @@
 // Galileo E1 at 8 Msps = 32000, BeiDou/GPS at 25 Msps = 25000, Galileo at 25 Msps
 // = 100000 -- configs C4/C5).
 //
-// N = R * N2 with a register radix R in {8,10,12,16,20,25} and an LDS-sized N2:
-//   input index n = n1 + R*n2, output index k = k2 + N2*k1,
-//   X[k2 + N2 k1] = sum_n1 W_R^{n1 k1} * ( W_N^{n1 k2} * sum_n2 x[n1 + R n2] W_N2^{n2 k2} ).
+// N = R * N2 with a register radix R in {8,10,12,16,20,25} and an LDS-sized N2,
+// decimation in frequency:
+//   input index n = n1*N2 + n2, output index k = k1 + R*k2,
+//   X[k1 + R k2] = sum_n2 W_N2^{n2 k2} ( W_N^{n2 k1} * sum_n1 x[n1 N2 + n2] W_R^{n1 k1} ).
 // One workgroup per transform (the same kernels as the LDS engine, through the
 // plan-type interface PT::run(plan, lds, tw, load, store)):
-//   phase 1: R LDS transforms of length N2 (stride-R input gather, L2-served),
-//            each output scaled by the inter-step twiddle W_N^{n1 k2} (n1 k2 < N,
-//            one table lookup) and written to the workgroup's global scratch row;
-//   phase 2: every lane takes columns k2, loads the R values (coalesced across
-//            lanes), runs the radix-R DFT in registers and hands X[k2 + N2 k1] to
-//            the caller's store functor.
+//   phase 1: every lane takes columns n2, loads x[n1 N2 + n2] for the R values of
+//            n1 (coalesced across lanes, each input read once), runs the radix-R
+//            DFT in registers, scales by the twiddle W_N^{n2 k1} (n2 k1 < N, one
+//            table lookup) and writes row k1 of the workgroup's global scratch
+//            (coalesced);
+//   phase 2: R LDS transforms of length N2 over the scratch rows, handing
+//            X[k1 + R k2] to the caller's store functor.
 // The scratch rows (N complex each) come from a slot pool claimed with one atomic
 // per transform, so any grid shape works with a bounded scratch allocation: a
 // workgroup holds its slot only while it runs, so a free slot always appears.
@@ -41,18 +43,19 @@ inline int lds_elems(const Plan4& p) { return p.sub.n; }
 __device__ __forceinline__ int lds_elems_dev(const Plan& p) { return p.n; }
 __device__ __forceinline__ int lds_elems_dev(const Plan4& p) { return p.sub.n; }
 
-template <int R, class Store>
-__device__ __forceinline__ void four_step_columns(const Plan4& p, const float2* __restrict__ row, Store& store)
+template <int R, class Load>
+__device__ __forceinline__ void four_step_columns(const Plan4& p, float2* __restrict__ row,
+    const float2* __restrict__ tw, Load& load)
 {
     const int N2 = p.sub.n;
-    for (int k2 = (int)threadIdx.x; k2 < N2; k2 += (int)blockDim.x)
+    for (int n2 = (int)threadIdx.x; n2 < N2; n2 += (int)blockDim.x)
         {
             float2 v[R];
 #pragma unroll
-            for (int n1 = 0; n1 < R; ++n1) v[n1] = row[(size_t)n1 * N2 + k2];
+            for (int n1 = 0; n1 < R; ++n1) v[n1] = load(n1 * N2 + n2);
             Dft<R>::run(v);
 #pragma unroll
-            for (int k1 = 0; k1 < R; ++k1) store(k2 + N2 * k1, v[k1]);
+            for (int k1 = 0; k1 < R; ++k1) row[(size_t)k1 * N2 + n2] = k1 == 0 ? v[0] : cmul(v[k1], tw[n2 * k1]);
         }
 }
 
@@ -98,22 +101,23 @@ struct FourStepPlan
         float2* row = p.scratch + (size_t)slot * p.n;
         const int N2 = p.sub.n;
         const int R = p.r1;
-        for (int n1 = 0; n1 < R; ++n1)
-            {
-                auto ld = [&](int i) -> float2 { return load(n1 + R * i); };
-                auto st = [&](int k2, float2 v) { row[(size_t)n1 * N2 + k2] = cmul(v, tw[n1 * k2]); };
-                fft::run<NT>(p.sub, lds, p.tw_sub, ld, st);
-            }
-        __syncthreads();  // the workgroup's scratch row is complete (same CU, same L1)
         switch (R)
             {
-            case 8: four_step_columns<8>(p, row, store); break;
-            case 10: four_step_columns<10>(p, row, store); break;
-            case 12: four_step_columns<12>(p, row, store); break;
-            case 16: four_step_columns<16>(p, row, store); break;
-            case 20: four_step_columns<20>(p, row, store); break;
-            case 25: four_step_columns<25>(p, row, store); break;
+            case 8: four_step_columns<8>(p, row, tw, load); break;
+            case 10: four_step_columns<10>(p, row, tw, load); break;
+            case 12: four_step_columns<12>(p, row, tw, load); break;
+            case 16: four_step_columns<16>(p, row, tw, load); break;
+            case 20: four_step_columns<20>(p, row, tw, load); break;
+            case 25: four_step_columns<25>(p, row, tw, load); break;
             default: break;
+            }
+        __syncthreads();  // the workgroup's scratch row is complete (same CU, same L1)
+        for (int k1 = 0; k1 < R; ++k1)
+            {
+                const float2* rk = row + (size_t)k1 * N2;
+                auto ld = [&](int i) -> float2 { return rk[i]; };
+                auto st = [&](int k2, float2 v) { store(k1 + R * k2, v); };
+                fft::run<NT>(p.sub, lds, p.tw_sub, ld, st);
             }
         __syncthreads();  // every lane's reads of the row have returned
         if (tid == 0)

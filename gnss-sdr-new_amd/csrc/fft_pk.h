@@ -22,8 +22,6 @@
 
 #include <hip/hip_runtime.h>
 
-#include <type_traits>
-
 #include "fft_lds.h"
 #include "fft_multi.h"
 
@@ -370,179 +368,6 @@ struct PkPlan
     }
 };
 
-
-// ---------------------------------------------------------------------------
-// Multi-transform packed plan: PB independent N-point transforms per workgroup,
-// advanced stage by stage together.  N/R butterflies per transform is never a
-// multiple of 64 for N = 4000 (= 2^5 5^3), so a one-transform workgroup leaves
-// lanes idle in every stage (20,20,10 on 256 lanes: 78 % of the issued lanes do
-// work); packing the PB*N/R butterflies of PB transforms onto the workgroup's
-// lanes fills the waves (25,16,10 x 2 on 320 lanes: 100 / 98 / 89 %).
-//
-// Per stage the butterfly -> (transform t, index jj) map is either
-//   INTERLEAVED  j = tid + b*NT over [0, PB*NB): t = j / NB (lane-varying), or
-//   DIRECT       t = b / BPTD, jj = tid + (b % BPTD)*NT (t compile-time),
-// whichever issues fewer wave-iterations; the last stage is always DIRECT so the
-// store functor receives t as a compile-time constant (per-transform row
-// statistics stay in registers).  Optional LDS padding phys(i) = i + i/32 spreads
-// the stride-R writes over the banks.
-template <int I>
-using ic = std::integral_constant<int, I>;
-
-constexpr int ceil_div(int a, int b) { return (a + b - 1) / b; }
-constexpr int min_i(int a, int b) { return a < b ? a : b; }
-
-// active wave-iterations of a map (NT a multiple of 64)
-constexpr int waves_interleaved(int V, int NT)
-{
-    int w = 0;
-    for (int b = 0; b * NT < V; ++b) w += ceil_div(min_i(NT, V - b * NT), 64);
-    return w;
-}
-constexpr int waves_direct(int PB, int NB, int NT)
-{
-    int w = 0;
-    for (int b = 0; b * NT < NB; ++b) w += ceil_div(min_i(NT, NB - b * NT), 64);
-    return PB * w;
-}
-
-template <int I, int PB, class F>
-__device__ __forceinline__ void static_for_impl(F& f)
-{
-    if constexpr (I < PB)
-        {
-            f(ic<I>{});
-            static_for_impl<I + 1, PB>(f);
-        }
-}
-
-template <bool PAD>
-__device__ __forceinline__ int pphys(int i)
-{
-    return PAD ? i + (i >> 5) : i;
-}
-
-template <int R, int NT, int PB, int N, int Ns, int STRIDE, bool PAD, bool FIRST, bool LAST, class Load, class Store>
-__device__ __forceinline__ void mstage(c2* lds, const float2* __restrict__ tw, Load& load, Store& store)
-{
-    constexpr int NB = N / R;
-    constexpr int V = PB * NB;
-    constexpr int TSTRIDE = N / (Ns * R);
-    constexpr bool DIRECT = LAST || waves_direct(PB, NB, NT) <= waves_interleaved(V, NT);
-    constexpr int BPTD = ceil_div(NB, NT);
-    constexpr int NIT = DIRECT ? PB * BPTD : ceil_div(V, NT);
-    const int tid = (int)threadIdx.x;
-    c2 v[NIT][R];
-    int tt[NIT], jj[NIT];
-    bool ok[NIT];
-#pragma unroll
-    for (int b = 0; b < NIT; ++b)
-        {
-            if constexpr (DIRECT)
-                {
-                    tt[b] = b / BPTD;
-                    jj[b] = tid + (b % BPTD) * NT;
-                    ok[b] = (NB % NT == 0) || jj[b] < NB;
-                }
-            else
-                {
-                    const int j = tid + b * NT;
-                    ok[b] = (V % NT == 0) || j < V;
-                    const int t = j / NB;
-                    tt[b] = t;
-                    jj[b] = j - t * NB;
-                }
-            if (ok[b])
-                {
-#pragma unroll
-                    for (int r = 0; r < R; ++r)
-                        {
-                            if constexpr (FIRST)
-                                v[b][r] = load(tt[b], r, jj[b] + r * NB);
-                            else
-                                v[b][r] = lds[tt[b] * STRIDE + pphys<PAD>(jj[b] + r * NB)];
-                        }
-                }
-        }
-    if constexpr (!FIRST) __syncthreads();
-#pragma unroll
-    for (int b = 0; b < NIT; ++b)
-        {
-            if (ok[b])
-                {
-                    int k = 0;
-                    if constexpr (!FIRST)
-                        {
-                            k = jj[b] % Ns;
-                            const c2 w1 = from(tw[k * TSTRIDE]);
-                            c2 w = w1;
-#pragma unroll
-                            for (int r = 1; r < R; ++r)
-                                {
-                                    if (r > 1) w = mul(w, w1);
-                                    v[b][r] = mul(v[b][r], w);
-                                }
-                        }
-                    Dft<R>::run(v[b]);
-                    if constexpr (!LAST)
-                        {
-                            const int base = tt[b] * STRIDE;
-                            const int o = (jj[b] - k) * R + k;
-#pragma unroll
-                            for (int r = 0; r < R; ++r) lds[base + pphys<PAD>(o + r * Ns)] = v[b][r];
-                        }
-                }
-        }
-    if constexpr (LAST)
-        {
-            static_assert(Ns * R == N, "last stage");
-            // per transform: r outer, b inner visits this lane's outputs in increasing index
-            auto per_t = [&](auto T) {
-                constexpr int t = decltype(T)::value;
-#pragma unroll
-                for (int r = 0; r < R; ++r)
-                    {
-#pragma unroll
-                        for (int bd = 0; bd < BPTD; ++bd)
-                            {
-                                const int b = t * BPTD + bd;
-                                if (ok[b]) store(T, jj[b] + r * Ns, v[b][r]);
-                            }
-                    }
-            };
-            static_for_impl<0, PB>(per_t);
-        }
-    else
-        __syncthreads();
-}
-
-template <int NT, int PB, int N, int Ns, int STRIDE, bool PAD, bool FIRST, int R, int... Rest, class Load, class Store>
-__device__ __forceinline__ void mstages(c2* lds, const float2* __restrict__ tw, Load& load, Store& store)
-{
-    constexpr bool LAST = sizeof...(Rest) == 0;
-    mstage<R, NT, PB, N, Ns, STRIDE, PAD, FIRST, LAST>(lds, tw, load, store);
-    if constexpr (!LAST) mstages<NT, PB, N, Ns * R, STRIDE, PAD, false, Rest...>(lds, tw, load, store);
-}
-
-// load(t, r, i) -> c2: input element i of transform t (t lane-varying);
-// store(ic<t>, i, c2): output element i of transform t (t compile-time), visited
-// in increasing i per lane and transform.
-template <int NT_, int PB_, bool PAD_, int... Rs>
-struct PkMultiPlan
-{
-    static constexpr int NT = NT_;
-    static constexpr int PB = PB_;
-    static constexpr bool PAD = PAD_;
-    static constexpr int N = (Rs * ...);
-    static constexpr int STRIDE = PAD ? ((N + (N >> 5) + 2) & ~1) : N;
-    static constexpr size_t lds_bytes() { return (size_t)PB * STRIDE * sizeof(c2); }
-    static_assert(NT % 64 == 0, "whole waves");
-    template <class Load, class Store>
-    __device__ __forceinline__ static void run(c2* lds, const float2* __restrict__ tw, Load load, Store store)
-    {
-        mstages<NT, PB, N, 1, STRIDE, PAD, true, Rs...>(lds, tw, load, store);
-    }
-};
 
 }  // namespace pk
 }  // namespace gsdr

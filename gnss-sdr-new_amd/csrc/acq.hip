@@ -267,7 +267,7 @@ void gsdr_acq_destroy(gsdr_acq* a)
             (void)hipEventDestroy(r.b);
         }
     for (hipEvent_t e : a->prof_pool) (void)hipEventDestroy(e);
-    void* bufs[] = {a->d_tw, a->d_wipe, a->d_code_fft, a->d_code_stage, a->d_prn, a->d_X, a->d_stats, a->d_res,
+    void* bufs[] = {a->st2.d_wipe, a->st2.d_freq, a->d_tw, a->d_wipe, a->d_code_fft, a->d_code_stage, a->d_prn, a->d_X, a->d_stats, a->d_res,
         a->d_iq, a->d_grid, a->d_tw_sub, a->d_scratch, a->d_slots, a->d_resk, a->d_acc, a->d_acc_slots};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
@@ -391,6 +391,101 @@ int gsdr_acq_dump_grid(gsdr_acq* a, const void* iq_host, uint32_t prn_slot, floa
     if (rc != GSDR_OK) return rc;
     GSDR_HIP(hipMemcpyAsync(grid_host, a->d_grid, (size_t)a->D * a->N * sizeof(float), hipMemcpyDeviceToHost,
         a->stream));
+    GSDR_HIP(hipStreamSynchronize(a->stream));
+    return GSDR_OK;
+}
+
+int gsdr_acq_set_step_two(gsdr_acq* a, uint32_t num_doppler_bins_step2, float doppler_step2, float pfa2)
+{
+    GSDR_REQUIRE(a, GSDR_E_ARG, "gsdr_acq_set_step_two: null handle");
+    GSDR_REQUIRE(num_doppler_bins_step2 > 0, GSDR_E_ARG, "gsdr_acq_set_step_two: zero bins");
+    GSDR_REQUIRE(num_doppler_bins_step2 <= a->D * a->conf.max_blocks, GSDR_E_UNSUPPORTED,
+        "gsdr_acq_set_step_two: %u bins exceed the handle's spectrum capacity (%u bins x %u blocks)",
+        num_doppler_bins_step2, a->D, a->conf.max_blocks);
+    std::lock_guard<std::mutex> lk(a->mu);
+    gsdr::DeviceGuard g(a->device);
+    GSDR_HIP(hipStreamSynchronize(a->stream));
+    if (a->st2.d_wipe) (void)hipFree(a->st2.d_wipe);
+    if (a->st2.d_freq) (void)hipFree(a->st2.d_freq);
+    a->st2.d_wipe = nullptr;
+    a->st2.d_freq = nullptr;
+    const size_t rows = (size_t)a->conf.max_prns * num_doppler_bins_step2;
+    GSDR_HIP(hipMalloc(&a->st2.d_wipe, rows * a->N * sizeof(float2)));
+    GSDR_HIP(hipMalloc(&a->st2.d_freq, rows * sizeof(float)));
+    a->st2.nbins = num_doppler_bins_step2;
+    a->st2.step = doppler_step2;
+    // Acq_Conf: pfa_second_step outside (0, 1] falls back to pfa (acq_conf.cc:72-76)
+    a->st2.pfa2 = (pfa2 <= 0.0f || pfa2 > 1.0f) ? a->conf.pfa : pfa2;
+    return GSDR_OK;
+}
+
+int gsdr_acq_get_step_two_threshold(const gsdr_acq* a, float* threshold)
+{
+    GSDR_REQUIRE(a && threshold, GSDR_E_ARG, "gsdr_acq_get_step_two_threshold: null argument");
+    GSDR_REQUIRE(a->st2.nbins > 0, GSDR_E_STATE, "gsdr_acq_get_step_two_threshold: gsdr_acq_set_step_two first");
+    *threshold = step_two_threshold(a);
+    return GSDR_OK;
+}
+
+int gsdr_acq_run_step_two(gsdr_acq* a, const void* iq_host, uint32_t nsel, const uint32_t* prn_slots,
+    const float* doppler_center_hz, const float* coarse_input_power, uint64_t stamp, gsdr_acq_result* out)
+{
+    GSDR_REQUIRE(a && iq_host && prn_slots && doppler_center_hz && coarse_input_power && out, GSDR_E_ARG,
+        "gsdr_acq_run_step_two: null argument");
+    GSDR_REQUIRE(a->st2.nbins > 0, GSDR_E_STATE, "gsdr_acq_run_step_two: gsdr_acq_set_step_two first");
+    GSDR_REQUIRE(nsel > 0 && nsel <= a->nprn, GSDR_E_ARG, "gsdr_acq_run_step_two: %u PRNs outside [1,%u]", nsel,
+        a->nprn);
+    for (uint32_t i = 0; i < nsel; ++i)
+        GSDR_REQUIRE(prn_slots[i] < a->nprn, GSDR_E_ARG, "gsdr_acq_run_step_two: slot %u >= nprn %u", prn_slots[i],
+            a->nprn);
+    std::lock_guard<std::mutex> lk(a->mu);
+    gsdr::DeviceGuard g(a->device);
+    const uint32_t nb = a->st2.nbins;
+    // update_grid_doppler_wipeoffs_step2 (pcps_acquisition.cc:307-314), float arithmetic
+    const float half = (float)std::floor((double)nb / 2.0);
+    std::vector<float> freqs((size_t)nsel * nb);
+    for (uint32_t i = 0; i < nsel; ++i)
+        for (uint32_t d = 0; d < nb; ++d)
+            {
+                volatile float dop = ((float)d - half) * a->st2.step;
+                freqs[(size_t)i * nb + d] = doppler_center_hz[i] + dop;
+            }
+    GSDR_HIP(hipMemcpyAsync(a->d_iq, iq_host, (size_t)a->K * a->consumed * item_bytes(a->conf.item_type),
+        hipMemcpyHostToDevice, a->stream));
+    GSDR_HIP(hipMemcpyAsync(a->st2.d_freq, freqs.data(), freqs.size() * sizeof(float), hipMemcpyHostToDevice,
+        a->stream));
+    hipLaunchKernelGGL(acq_wipeoff_kernel, dim3(nsel * nb), dim3(256), 0, a->stream, a->st2.d_wipe, a->N,
+        (float)a->conf.fs_in, 0, 0, 0, 0, (const float*)a->st2.d_freq);
+    GSDR_HIP(hipGetLastError());
+    // one narrow grid per PRN (each has its own centre): the engine's launches on a
+    // one-PRN view of the handle
+    const uint32_t D0 = a->D, P0 = a->nprn;
+    float2* const wipe0 = a->d_wipe;
+    float2* const code0 = a->d_code_fft;
+    uint32_t* const prn0 = a->d_prn;
+    const float thr = step_two_threshold(a);
+    int rc = GSDR_OK;
+    for (uint32_t i = 0; i < nsel && rc == GSDR_OK; ++i)
+        {
+            a->D = nb;
+            a->nprn = 1;
+            a->d_wipe = a->st2.d_wipe + (size_t)i * nb * a->N;
+            a->d_code_fft = code0 + (size_t)prn_slots[i] * a->N;
+            a->d_prn = prn0 + prn_slots[i];
+            a->st2.active = true;
+            a->st2.center = doppler_center_hz[i];
+            a->st2.ip = coarse_input_power[i];
+            a->st2.threshold = thr;
+            rc = dispatch(a, 0, a->d_iq, 1, a->consumed, stamp, a->d_res + i, a->stream, 0);
+        }
+    a->D = D0;
+    a->nprn = P0;
+    a->d_wipe = wipe0;
+    a->d_code_fft = code0;
+    a->d_prn = prn0;
+    a->st2.active = false;
+    if (rc != GSDR_OK) return rc;
+    GSDR_HIP(hipMemcpyAsync(out, a->d_res, (size_t)nsel * sizeof(gsdr_acq_result), hipMemcpyDeviceToHost, a->stream));
     GSDR_HIP(hipStreamSynchronize(a->stream));
     return GSDR_OK;
 }

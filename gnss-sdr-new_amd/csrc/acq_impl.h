@@ -67,7 +67,21 @@ struct AcqParams
     int32_t cfar;
     uint32_t eff;         // effective FFT size (N/2 with bit_transition_flag, else N)
     uint32_t out_off;     // first output index of the effective window (N - eff)
+    // make_two_steps narrow grid (pcps_acquisition.cc:298-305, :533-540, :717-773)
+    int32_t step_two;     // 1: Doppler from center2/step2, CFAR input power kept from the coarse step
+    float center2;        // d_doppler_center_step_two
+    float step2;          // Acq_Conf::doppler_step2
+    float half2;          // static_cast<float>(floor(num_doppler_bins_step2 / 2.0))
+    float ip2;            // d_input_power of the coarse step (not recomputed in step two, :530-540)
 };
+
+// Acq_doppler_hz of Doppler row d: first step int32 arithmetic (:537); step two
+// static_cast<int32_t>(center2 + (float(d) - half2) * step2) in float (:539).
+__device__ __forceinline__ int32_t doppler_of(const AcqParams& ap, uint32_t d)
+{
+    if (ap.step_two) return (int32_t)gsdr::add_rn(ap.center2, gsdr::mul_rn(gsdr::sub_rn((float)d, ap.half2), ap.step2));
+    return -ap.doppler_max + ap.doppler_center + ap.doppler_step * (int32_t)d;
+}
 
 template <int IT>
 __device__ __forceinline__ float2 load_item(const void* __restrict__ p, size_t i)
@@ -132,14 +146,16 @@ __device__ __forceinline__ void block_reduce_stat(float& m, uint32_t& idx, float
 // accumulation (KERN/s32f_sincos_32fc.h:390-403) sequentially in fp32; the
 // workgroup then evaluates cos/sin in parallel.
 __global__ void __launch_bounds__(256) acq_wipeoff_kernel(float2* __restrict__ wipe, uint32_t N, float fs,
-    int32_t doppler_max, int32_t doppler_center, int32_t doppler_step, int32_t doppler_bias)
+    int32_t doppler_max, int32_t doppler_center, int32_t doppler_step, int32_t doppler_bias,
+    const float* __restrict__ freqs)
 {
     const uint32_t d = blockIdx.x;
     float2* row = wipe + (size_t)d * N;
     if (threadIdx.x == 0)
         {
+            // freqs: the step-two grid (update_grid_doppler_wipeoffs_step2, :307-314)
             const int32_t doppler = -doppler_max + doppler_center + doppler_step * (int32_t)d;
-            const float freq = (float)(doppler_bias + doppler);
+            const float freq = freqs ? freqs[d] : (float)(doppler_bias + doppler);
             const float phase_step = __fdiv_rn(__fmul_rn(6.283185307179586f, freq), fs);
             const float inc = -phase_step;
             float ph = 0.0f;
@@ -533,7 +549,7 @@ __global__ void __launch_bounds__(64) acq_reduce_dwell_kernel(const RowStat* __r
             r.prn = prn_ids[p];
             r.doppler_index = dsel;
             r.code_phase = tsel;
-            r.doppler_hz = -ap.doppler_max + ap.doppler_center + ap.doppler_step * (int32_t)dsel;
+            r.doppler_hz = doppler_of(ap, dsel);
             r.peak = m;
             r.second_peak = 0.0f;
             r.input_power = 0.0f;
@@ -546,7 +562,8 @@ __global__ void __launch_bounds__(64) acq_reduce_dwell_kernel(const RowStat* __r
                 {
                     const uint32_t opp = (dsel + ap.D / 2) % ap.D;
                     const float acc = s[opp].sum;
-                    const float ip = (float)((double)(acc / (float)(int32_t)ap.eff) / 2.0 / (double)(k + 1));
+                    const float ip = ap.step_two ? ap.ip2
+                                                 : (float)((double)(acc / (float)(int32_t)ap.eff) / 2.0 / (double)(k + 1));
                     r.input_power = ip;
                     r.test_statistic = m / ip;
                     r.positive = r.test_statistic > ap.threshold ? 1 : 0;
@@ -705,7 +722,7 @@ __global__ void __launch_bounds__(64) acq_reduce_kernel(const RowStat* __restric
     r.prn = prn_ids[p];
     r.doppler_index = dsel;
     r.code_phase = tsel;
-    r.doppler_hz = -ap.doppler_max + ap.doppler_center + ap.doppler_step * (int32_t)dsel;
+    r.doppler_hz = doppler_of(ap, dsel);
     r.peak = m;
     r.second_peak = 0.0f;
     r.input_power = 0.0f;
@@ -719,7 +736,7 @@ __global__ void __launch_bounds__(64) acq_reduce_kernel(const RowStat* __restric
             const uint32_t opp = (dsel + ap.D / 2) % ap.D;
             const float acc = s[opp].sum;
             // float(accumulate) / int32 in float, then / 2.0 / counter in double (pcps_acquisition.cc:533)
-            const float ip = (float)((double)(acc / (float)(int32_t)ap.N) / 2.0 / (double)ap.dwells);
+            const float ip = ap.step_two ? ap.ip2 : (float)((double)(acc / (float)(int32_t)ap.N) / 2.0 / (double)ap.dwells);
             r.input_power = ip;
             r.test_statistic = m / ip;
             r.positive = r.test_statistic > ap.threshold ? 1 : 0;
@@ -824,6 +841,18 @@ struct gsdr_acq
     bool profiling{false};
     std::vector<ProfRec> prof_recs;
     std::vector<hipEvent_t> prof_pool;
+    // make_two_steps (gsdr_acq_set_step_two / gsdr_acq_run_step_two)
+    struct StepTwo
+    {
+        uint32_t nbins{0};       // num_doppler_bins_step2
+        float step{0.0f};        // doppler_step2
+        float pfa2{0.0f};
+        float threshold{0.0f};   // calculate_threshold with d_step_two
+        float2* d_wipe{nullptr}; // max_prns x nbins rows of N
+        float* d_freq{nullptr};
+        bool active{false};      // set while the per-PRN step-two launches are issued
+        float center{0.0f}, ip{0.0f};
+    } st2;
     std::mutex mu;
 };
 
@@ -895,6 +924,15 @@ AcqParams params_of(const gsdr_acq* a)
     ap.cfar = a->conf.pfa > 0.0f ? 1 : 0;
     ap.eff = a->eff;
     ap.out_off = a->N - a->eff;
+    if (a->st2.active)
+        {
+            ap.step_two = 1;
+            ap.center2 = a->st2.center;
+            ap.step2 = a->st2.step;
+            ap.half2 = (float)std::floor((double)a->st2.nbins / 2.0);
+            ap.ip2 = a->st2.ip;
+            ap.threshold = a->st2.threshold;
+        }
     return ap;
 }
 
@@ -902,7 +940,7 @@ int rebuild_wipeoffs(gsdr_acq* a)
 {
     hipLaunchKernelGGL(acq_wipeoff_kernel, dim3(a->D), dim3(256), 0, a->stream, a->d_wipe, a->N,
         (float)a->conf.fs_in, a->conf.doppler_max, a->conf.doppler_center, (int32_t)a->conf.doppler_step,
-        a->conf.doppler_bias);
+        a->conf.doppler_bias, (const float*)nullptr);
     GSDR_HIP(hipGetLastError());
     GSDR_HIP(hipStreamSynchronize(a->stream));
     return GSDR_OK;
@@ -918,6 +956,17 @@ void compute_threshold(gsdr_acq* a)
     const int num_bins = (int)(a->eff * a->D);
     const double p = std::pow(1.0 - (double)pfa, 1.0 / (double)(float)num_bins);
     a->threshold = (float)(2.0 * gsdr::gamma_p_inv_int(2 * (int)a->conf.max_dwells, p));
+}
+
+// calculate_threshold with d_step_two (:894-909): pfa2 and the narrow bin count;
+// with pfa2 <= 0 the reference returns early and keeps the first-step threshold.
+float step_two_threshold(const gsdr_acq* a)
+{
+    const float pfa = a->st2.pfa2;
+    if (pfa <= 0.0f) return a->threshold;
+    const int num_bins = (int)(a->eff * a->st2.nbins);
+    const double p = std::pow(1.0 - (double)pfa, 1.0 / (double)(float)num_bins);
+    return (float)(2.0 * gsdr::gamma_p_inv_int(2 * (int)a->conf.max_dwells, p));
 }
 
 // Event bracket around one stage launch when profiling is on.

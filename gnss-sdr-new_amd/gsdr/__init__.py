@@ -37,6 +37,7 @@ EXPORTED = [
     "gsdr_trk_conf_default", "gsdr_trk_create", "gsdr_trk_destroy", "gsdr_trk_start", "gsdr_trk_stop",
     "gsdr_trk_run_device", "gsdr_trk_run", "gsdr_trk_get_channel", "gsdr_trk_save_state", "gsdr_trk_restore_state",
     "gsdr_trk_set_profiling", "gsdr_trk_read_profile", "gsdr_acq_set_cu_mask", "gsdr_trk_set_cu_mask",
+    "gsdr_acq_set_step_two", "gsdr_acq_get_step_two_threshold", "gsdr_acq_run_step_two",
     "gsdr_trk_set_data_code",
 ]
 
@@ -203,6 +204,9 @@ def load():
     L.gsdr_trk_set_profiling.argtypes = [P, I]
     L.gsdr_trk_read_profile.argtypes = [P, P, P]
     L.gsdr_acq_set_cu_mask.argtypes = [P, P, I]
+    L.gsdr_acq_set_step_two.argtypes = [P, U32, F, F]
+    L.gsdr_acq_get_step_two_threshold.argtypes = [P, P]
+    L.gsdr_acq_run_step_two.argtypes = [P, P, U32, P, P, P, U64, P]
     L.gsdr_trk_set_cu_mask.argtypes = [P, P, I]
     _lib = L
     return L
@@ -304,6 +308,31 @@ class Acquisition:
         out = np.zeros(nblocks * self.nprn, ACQ_RESULT_DTYPE)
         _check(load().gsdr_acq_run(self._h, _ptr(iq), int(nblocks), int(stamp0), _ptr(out)))
         return out.reshape(nblocks, self.nprn)
+
+    def set_step_two(self, num_doppler_bins_step2=4, doppler_step2=125.0, pfa2=0.0):
+        """make_two_steps narrow grid (Acq_Conf second_nbins / second_doppler_step /
+        pfa_second_step; pcps_acquisition.cc:298-314, :717-773)."""
+        _check(load().gsdr_acq_set_step_two(self._h, int(num_doppler_bins_step2), float(doppler_step2),
+                                            float(pfa2)))
+
+    @property
+    def step_two_threshold(self):
+        t = ctypes.c_float()
+        _check(load().gsdr_acq_get_step_two_threshold(self._h, ctypes.byref(t)))
+        return t.value
+
+    def run_step_two(self, iq, prn_slots, doppler_centers_hz, coarse_input_power, stamp=0):
+        """Second step for the given PRN slots on one attempt of host IQ, centred on
+        each slot's coarse Acq_doppler_hz -> structured array [len(prn_slots)]."""
+        iq = self._items(iq)
+        slots = np.ascontiguousarray(prn_slots, np.uint32)
+        cen = np.ascontiguousarray(doppler_centers_hz, np.float32)
+        ip = np.ascontiguousarray(coarse_input_power, np.float32)
+        assert len(slots) == len(cen) == len(ip)
+        out = np.zeros(len(slots), ACQ_RESULT_DTYPE)
+        _check(load().gsdr_acq_run_step_two(self._h, _ptr(iq), len(slots), _ptr(slots), _ptr(cen), _ptr(ip),
+                                            int(stamp), _ptr(out)))
+        return out
 
     def run_device(self, iq_dev_ptr, nblocks, stride_items, stamp0, out_dev_ptr, stream_ptr=0):
         _check(load().gsdr_acq_run_device(self._h, ctypes.c_void_p(iq_dev_ptr), int(nblocks), int(stride_items),

@@ -150,6 +150,25 @@ int gsdr_acq_run_device(gsdr_acq* acq, const void* iq_dev, uint32_t nblocks, uin
  * (D rows of fft_size floats, Doppler-major).  Synchronous. */
 int gsdr_acq_dump_grid(gsdr_acq* acq, const void* iq_host, uint32_t prn_slot, float* grid_host);
 
+/* make_two_steps (pcps_acquisition.cc:298-314, :717-773, :781-800, :894-909;
+ * Acq_Conf second_nbins / second_doppler_step / pfa_second_step, acq_conf.cc:63-76).
+ * After a positive first step the reference searches the NEXT block on a narrow
+ * grid of num_doppler_bins_step2 bins spaced doppler_step2 Hz around the coarse
+ * Acq_doppler_hz (float arithmetic, no doppler_bias), with its own threshold
+ * (pfa2 and the narrow bin count; pfa2 outside (0,1] means pfa as in Acq_Conf)
+ * and, for CFAR, the first step's input power (d_input_power is not recomputed
+ * in step two, :530-540).  set_step_two configures the narrow grid for the
+ * handle; run_step_two runs it for nsel PRN slots of the current batch over one
+ * attempt (max_dwells blocks) of host IQ, prn_slots[i] with centre
+ * doppler_center_hz[i] (the coarse Acq_doppler_hz) and coarse_input_power[i]
+ * (the coarse result's input_power; ignored by the peak-ratio statistic).
+ * out[i]: the step-two Gnss_Synchro fields (doppler_hz from the narrow grid,
+ * :539) and the decision against the step-two threshold.  Synchronous. */
+int gsdr_acq_set_step_two(gsdr_acq* acq, uint32_t num_doppler_bins_step2, float doppler_step2, float pfa2);
+int gsdr_acq_get_step_two_threshold(const gsdr_acq* acq, float* threshold);
+int gsdr_acq_run_step_two(gsdr_acq* acq, const void* iq_host, uint32_t nsel, const uint32_t* prn_slots,
+    const float* doppler_center_hz, const float* coarse_input_power, uint64_t stamp, gsdr_acq_result* out);
+
 /* Stage profiling with HIP events recorded on the launch stream (observability,
  * the role of the reference's per-block timing prints).  When enabled, every
  * gsdr_acq_run / gsdr_acq_run_device call records device time per stage:

@@ -174,3 +174,61 @@ def acquire(x, code, fs, doppler_max, doppler_step, D=None, pfa=0.0, samples_per
     r.doppler_hz = doppler_hz(di, doppler_max, doppler_step, doppler_center)
     r.delay_samples = float(np.fmod(np.float32(ti), np.float32(samples_per_code)))
     return r
+
+
+# ---------------------------------------------------------------- make_two_steps
+def step_two_freqs(center2, doppler_step2, nbins2):
+    """update_grid_doppler_wipeoffs_step2 (:307-314): float32
+    (float(d) - float(floor(nbins2 / 2.0))) * step2, then + centre."""
+    f32 = np.float32
+    half = f32(math.floor(nbins2 / 2.0))
+    return [f32(f32(center2) + f32(f32(f32(d) - half) * f32(doppler_step2))) for d in range(nbins2)]
+
+
+def doppler_wipeoffs_step2(fs, N, center2, doppler_step2, nbins2):
+    """The narrow grid's carriers (update_local_carrier with float freq, :233-246)."""
+    f32 = np.float32
+    w = np.empty((nbins2, N), np.complex64)
+    for d, f in enumerate(step_two_freqs(center2, doppler_step2, nbins2)):
+        step = f32(TWO_PI) * f32(f) / f32(fs)
+        w[d] = volk.s32f_sincos_32fc(float(-step), N)
+    return w
+
+
+def step_two_doppler_hz(d, center2, doppler_step2, nbins2):
+    """:539 / :576 — static_cast<int32_t>(centre + (float(d) - float(floor(n/2.0))) * step2)."""
+    f32 = np.float32
+    v = f32(f32(center2) + f32(f32(f32(d) - f32(math.floor(nbins2 / 2.0))) * f32(doppler_step2)))
+    return int(np.trunc(v))
+
+
+def step_two_statistic(M, coarse_input_power, center2, doppler_step2, samples_per_chip=None, fft_size=None,
+                       cfar=True):
+    """The step-two branch of acquisition_core (:744-773): CFAR divides the narrow-grid
+    maximum by the FIRST step's d_input_power (the step-two branch of
+    max_to_input_power_statistic does not recompute it, :530-540); the peak ratio is
+    unchanged.  Returns (index_time, index_doppler, peak, second_peak, statistic, doppler_hz)."""
+    nb = M.shape[0]
+    if cfar:
+        D, _ = M.shape
+        gmax = np.float32(0.0)
+        di = ti = 0
+        for i in range(D):
+            t = volk.index_max_32u(M[i])
+            if M[i, t] > gmax:
+                gmax, di, ti = M[i, t], i, t
+        stat = np.float32(np.float32(gmax) / np.float32(coarse_input_power))
+        second = np.float32(0)
+    else:
+        ti, di, gmax, second, stat = first_vs_second_peak_statistic(M, samples_per_chip, fft_size)
+    return int(ti), int(di), np.float32(gmax), second, stat, step_two_doppler_hz(di, center2, doppler_step2, nb)
+
+
+def threshold_step_two(pfa, pfa2, fft_size, nbins2, max_dwells=1, bit_transition=False, first_threshold=None):
+    """calculate_threshold with d_step_two (:894-909); pfa2 outside (0,1] is pfa
+    (acq_conf.cc:72-76); pfa2 <= 0 keeps the first-step threshold."""
+    if pfa2 <= 0.0 or pfa2 > 1.0:
+        pfa2 = pfa
+    if pfa2 <= 0.0:
+        return first_threshold
+    return threshold(pfa2, fft_size, nbins2, max_dwells, bit_transition)

@@ -127,3 +127,17 @@ def test_synth_galileo_replicas_match_oracle():
                                               replica.galileo_e1_code_complex_sampled("1C", cboc, p, fs))
     for fs in (6000000, 25000000):
         np.testing.assert_array_equal(synth.bds_b1i_sampled(3, fs), replica.beidou_b1i_code_complex_sampled(3, fs))
+
+
+def test_step_two_grid_formulae():
+    """make_two_steps grid (pcps_acquisition.cc:307-314, :539): float arithmetic,
+    floor(n/2.0) centring, truncation toward zero of the reported Doppler."""
+    from oracle import pcps
+    assert pcps.step_two_freqs(1500.0, 125.0, 4) == [1250.0, 1375.0, 1500.0, 1625.0]
+    assert pcps.step_two_freqs(-750.0, 100.0, 5) == [-950.0, -850.0, -750.0, -650.0, -550.0]
+    assert pcps.step_two_doppler_hz(0, -750.0, 62.5, 4) == -875
+    assert pcps.step_two_doppler_hz(1, 1000.0, 62.5, 4) == 937   # 937.5 truncates
+    assert pcps.step_two_doppler_hz(0, -1000.0, 62.5, 3) == -1062  # -1062.5 truncates toward zero
+    # pfa2 outside (0,1] falls back to pfa (acq_conf.cc:72-76); peak ratio keeps the first threshold
+    assert pcps.threshold_step_two(0.01, 0.0, 4000, 4) == pcps.threshold(0.01, 4000, 4)
+    assert pcps.threshold_step_two(0.0, 0.0, 4000, 4, first_threshold=2.5) == 2.5

@@ -101,7 +101,8 @@ int gsdr_acq_create(int device, const gsdr_acq_conf* conf, gsdr_acq** out)
     *out = nullptr;
     GSDR_REQUIRE(conf->fs_in > 0 && conf->consumed_samples > 0, GSDR_E_ARG, "gsdr_acq_create: fs_in and consumed_samples must be > 0");
     GSDR_REQUIRE(conf->doppler_step > 0, GSDR_E_ARG, "gsdr_acq_create: doppler_step must be > 0");
-    GSDR_REQUIRE(conf->item_type == GSDR_ITEM_GR_COMPLEX || conf->item_type == GSDR_ITEM_CSHORT, GSDR_E_ARG,
+    GSDR_REQUIRE(conf->item_type == GSDR_ITEM_GR_COMPLEX || conf->item_type == GSDR_ITEM_CSHORT ||
+                     conf->item_type == GSDR_ITEM_IBYTE, GSDR_E_ARG,
         "gsdr_acq_create: unknown item type %d", conf->item_type);
     GSDR_REQUIRE(conf->max_prns > 0 && conf->max_blocks > 0, GSDR_E_ARG, "gsdr_acq_create: capacities must be > 0");
     GSDR_REQUIRE(conf->pfa >= 0.0f && conf->pfa <= 1.0f, GSDR_E_ARG, "gsdr_acq_create: pfa outside [0,1]");

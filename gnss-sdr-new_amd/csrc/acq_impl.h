@@ -90,9 +90,15 @@ __device__ __forceinline__ float2 load_item(const void* __restrict__ p, size_t i
         {
             return reinterpret_cast<const float2*>(p)[i];
         }
-    else
+    else if constexpr (IT == GSDR_ITEM_CSHORT)
         {
             short2 s = reinterpret_cast<const short2*>(p)[i];
+            return make_float2((float)s.x, (float)s.y);
+        }
+    else
+        {
+            // Ibyte_To_Complex: interleaved_char_to_complex, scale 1 (exact)
+            char2 s = reinterpret_cast<const char2*>(p)[i];
             return make_float2((float)s.x, (float)s.y);
         }
 }
@@ -863,7 +869,7 @@ using gsdr::fft::FourStepPlan;
 using gsdr::fft::RuntimePlan;
 using gsdr::fft::StaticPlan;
 
-size_t item_bytes(int it) { return it == GSDR_ITEM_CSHORT ? 4 : 8; }
+size_t item_bytes(int it) { return it == GSDR_ITEM_CSHORT ? 4 : (it == GSDR_ITEM_IBYTE ? 2 : 8); }
 
 // FFT variants (gsdr_acq::variant): 1-4 compile-time plans for the sample rates
 // GNSS front-ends use (2/4/8/16 Msps at 1 ms, acq_v_static.hip), 10-12 runtime
@@ -892,6 +898,8 @@ int set_lds_attrs(size_t bytes)
     GSDR_HIP(hipFuncSetAttribute((const void*)acq_forward_kernel<PT, GSDR_ITEM_GR_COMPLEX>,
         hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
     GSDR_HIP(hipFuncSetAttribute((const void*)acq_forward_kernel<PT, GSDR_ITEM_CSHORT>,
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+    GSDR_HIP(hipFuncSetAttribute((const void*)acq_forward_kernel<PT, GSDR_ITEM_IBYTE>,
         hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
     GSDR_HIP(hipFuncSetAttribute((const void*)acq_correlate_kernel<PT, false>,
         hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
@@ -1042,8 +1050,11 @@ void launch_forward(gsdr_acq* a, const void* iq, int item_type, uint32_t nblocks
     if (item_type == GSDR_ITEM_GR_COMPLEX)
         hipLaunchKernelGGL((acq_forward_kernel<PT, GSDR_ITEM_GR_COMPLEX>), dim3(nblocks, a->D), dim3(PT::NT),
             a->lds_bytes, s, iq, stride, a->d_wipe, a->d_X, a->d_tw, plan_of<PT>(a), a->consumed, a->D);
-    else
+    else if (item_type == GSDR_ITEM_CSHORT)
         hipLaunchKernelGGL((acq_forward_kernel<PT, GSDR_ITEM_CSHORT>), dim3(nblocks, a->D), dim3(PT::NT),
+            a->lds_bytes, s, iq, stride, a->d_wipe, a->d_X, a->d_tw, plan_of<PT>(a), a->consumed, a->D);
+    else
+        hipLaunchKernelGGL((acq_forward_kernel<PT, GSDR_ITEM_IBYTE>), dim3(nblocks, a->D), dim3(PT::NT),
             a->lds_bytes, s, iq, stride, a->d_wipe, a->d_X, a->d_tw, plan_of<PT>(a), a->consumed, a->D);
 }
 

@@ -36,8 +36,11 @@ int launch_forward_pk(gsdr_acq* a, const void* iq, int item_type, uint32_t nbloc
             if (item_type == GSDR_ITEM_GR_COMPLEX)                                                              \
                 hipLaunchKernelGGL((acq_forward_pk_kernel<M, GSDR_ITEM_GR_COMPLEX>), dim3(nblocks, a->D),       \
                     dim3(M::NT), M::lds_bytes(), s, iq, stride, a->d_wipe, a->d_X, a->d_tw, a->consumed, a->D); \
-            else                                                                                                \
+            else if (item_type == GSDR_ITEM_CSHORT)                                                             \
                 hipLaunchKernelGGL((acq_forward_pk_kernel<M, GSDR_ITEM_CSHORT>), dim3(nblocks, a->D),           \
+                    dim3(M::NT), M::lds_bytes(), s, iq, stride, a->d_wipe, a->d_X, a->d_tw, a->consumed, a->D); \
+            else                                                                                                \
+                hipLaunchKernelGGL((acq_forward_pk_kernel<M, GSDR_ITEM_IBYTE>), dim3(nblocks, a->D),            \
                     dim3(M::NT), M::lds_bytes(), s, iq, stride, a->d_wipe, a->d_X, a->d_tw, a->consumed, a->D); \
             GSDR_HIP(hipGetLastError());                                                                        \
             return GSDR_OK;                                                                                     \
@@ -71,6 +74,8 @@ int setup_corr_variant(gsdr_acq* a, int v)
             GSDR_HIP(hipFuncSetAttribute((const void*)acq_forward_pk_kernel<M, GSDR_ITEM_GR_COMPLEX>,          \
                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)M::lds_bytes()));                              \
             GSDR_HIP(hipFuncSetAttribute((const void*)acq_forward_pk_kernel<M, GSDR_ITEM_CSHORT>,              \
+                hipFuncAttributeMaxDynamicSharedMemorySize, (int)M::lds_bytes()));                              \
+            GSDR_HIP(hipFuncSetAttribute((const void*)acq_forward_pk_kernel<M, GSDR_ITEM_IBYTE>,               \
                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)M::lds_bytes()));                              \
             a->corr_variant = ID;                                                                               \
             return GSDR_OK;                                                                                     \

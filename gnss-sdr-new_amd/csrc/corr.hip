@@ -62,9 +62,15 @@ __device__ __forceinline__ float2 load_item(const void* __restrict__ p, int64_t 
         {
             return reinterpret_cast<const float2*>(p)[i];
         }
-    else
+    else if constexpr (IT == GSDR_ITEM_CSHORT)
         {
             short2 s = reinterpret_cast<const short2*>(p)[i];
+            return make_float2((float)s.x, (float)s.y);
+        }
+    else
+        {
+            // Ibyte_To_Complex: interleaved_char_to_complex, scale 1 (exact)
+            char2 s = reinterpret_cast<const char2*>(p)[i];
             return make_float2((float)s.x, (float)s.y);
         }
 }
@@ -476,7 +482,7 @@ struct gsdr_corr
 namespace
 {
 
-size_t item_bytes(int it) { return it == GSDR_ITEM_CSHORT ? 4 : 8; }
+size_t item_bytes(int it) { return it == GSDR_ITEM_CSHORT ? 4 : (it == GSDR_ITEM_IBYTE ? 2 : 8); }
 
 // The reference's host-side phasors, bit for bit (std::cos/std::sin/std::exp on
 // float, cpu_multicorrelator_real_codes.cc:114-123), reduced to their angles.
@@ -541,8 +547,11 @@ int launch(gsdr_corr* c, const gsdr_corr_job* d_jobs, const JobAux* d_aux, int n
     if (item_type == GSDR_ITEM_GR_COMPLEX)
         hipLaunchKernelGGL((corr_kernel<GSDR_ITEM_GR_COMPLEX>), grid, dim3(kCorrThreads), lds, s, d_jobs, d_aux,
             c->d_chans, iq, iq_items, (float2*)out, c->max_taps, c->assoc, c->d_partials, c->d_counters, c->max_chunks);
-    else
+    else if (item_type == GSDR_ITEM_CSHORT)
         hipLaunchKernelGGL((corr_kernel<GSDR_ITEM_CSHORT>), grid, dim3(kCorrThreads), lds, s, d_jobs, d_aux,
+            c->d_chans, iq, iq_items, (float2*)out, c->max_taps, c->assoc, c->d_partials, c->d_counters, c->max_chunks);
+    else
+        hipLaunchKernelGGL((corr_kernel<GSDR_ITEM_IBYTE>), grid, dim3(kCorrThreads), lds, s, d_jobs, d_aux,
             c->d_chans, iq, iq_items, (float2*)out, c->max_taps, c->assoc, c->d_partials, c->d_counters, c->max_chunks);
     GSDR_HIP(hipGetLastError());
     if (c->profiling)
@@ -628,6 +637,8 @@ int gsdr_corr_create(int device, int max_channels, int max_len, int max_taps, gs
         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     GSDR_HIP(hipFuncSetAttribute((const void*)corr_kernel<GSDR_ITEM_CSHORT>,
         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    GSDR_HIP(hipFuncSetAttribute((const void*)corr_kernel<GSDR_ITEM_IBYTE>,
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     if (ensure_jobs(c, 64) != GSDR_OK)
         {
             gsdr_corr_destroy(c);
@@ -692,7 +703,7 @@ int gsdr_corr_run_batch(gsdr_corr* c, const gsdr_corr_job* jobs, int njobs, cons
     int64_t iq_items, float* out_dev, void* stream)
 {
     GSDR_REQUIRE(c && (jobs || njobs == 0) && iq_dev && out_dev, GSDR_E_ARG, "gsdr_corr_run_batch: null argument");
-    GSDR_REQUIRE(item_type == GSDR_ITEM_GR_COMPLEX || item_type == GSDR_ITEM_CSHORT, GSDR_E_ARG,
+    GSDR_REQUIRE(item_type >= GSDR_ITEM_GR_COMPLEX && item_type <= GSDR_ITEM_IBYTE, GSDR_E_ARG,
         "gsdr_corr_run_batch: item type %d", item_type);
     std::lock_guard<std::mutex> lk(c->mu);
     gsdr::DeviceGuard g(c->device);
@@ -731,7 +742,7 @@ int gsdr_corr_run(gsdr_corr* c, int ch, const void* sig_in_host, int item_type, 
     GSDR_REQUIRE(n >= 0 && n <= c->max_len, GSDR_E_ARG, "gsdr_corr_run: length %d outside [0,%d]", n, c->max_len);
     GSDR_REQUIRE(ch >= 0 && ch < c->max_channels && c->chans[ch].ntaps > 0, GSDR_E_STATE,
         "gsdr_corr_run: channel %d has no local code", ch);
-    GSDR_REQUIRE(item_type == GSDR_ITEM_GR_COMPLEX || item_type == GSDR_ITEM_CSHORT, GSDR_E_ARG,
+    GSDR_REQUIRE(item_type >= GSDR_ITEM_GR_COMPLEX && item_type <= GSDR_ITEM_IBYTE, GSDR_E_ARG,
         "gsdr_corr_run: item type %d", item_type);
     gsdr_corr_job jb{};
     jb.channel = ch;
@@ -786,7 +797,7 @@ int gsdr_corr_run_epochs(gsdr_corr* c, const gsdr_corr_job* jobs_dev, int jobs_p
 {
     GSDR_REQUIRE(c && jobs_dev && iq_dev && out_dev, GSDR_E_ARG, "gsdr_corr_run_epochs: null argument");
     GSDR_REQUIRE(jobs_per_epoch >= 0 && n_epochs >= 0, GSDR_E_ARG, "gsdr_corr_run_epochs: negative count");
-    GSDR_REQUIRE(item_type == GSDR_ITEM_GR_COMPLEX || item_type == GSDR_ITEM_CSHORT, GSDR_E_ARG,
+    GSDR_REQUIRE(item_type >= GSDR_ITEM_GR_COMPLEX && item_type <= GSDR_ITEM_IBYTE, GSDR_E_ARG,
         "gsdr_corr_run_epochs: item type %d", item_type);
     std::lock_guard<std::mutex> lk(c->mu);
     gsdr::DeviceGuard g(c->device);

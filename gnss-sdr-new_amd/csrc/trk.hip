@@ -698,9 +698,15 @@ __device__ __forceinline__ float2 load_iq(const void* __restrict__ p, int64_t i)
 {
     if constexpr (IT == GSDR_ITEM_GR_COMPLEX)
         return reinterpret_cast<const float2*>(p)[i];
-    else
+    else if constexpr (IT == GSDR_ITEM_CSHORT)
         {
             const short2 s = reinterpret_cast<const short2*>(p)[i];
+            return make_float2((float)s.x, (float)s.y);
+        }
+    else
+        {
+            // Ibyte_To_Complex: interleaved_char_to_complex, scale 1 (exact)
+            const char2 s = reinterpret_cast<const char2*>(p)[i];
             return make_float2((float)s.x, (float)s.y);
         }
 }
@@ -1117,7 +1123,7 @@ struct gsdr_trk
 namespace
 {
 
-size_t trk_item_bytes(int it) { return it == GSDR_ITEM_CSHORT ? 4 : 8; }
+size_t trk_item_bytes(int it) { return it == GSDR_ITEM_CSHORT ? 4 : (it == GSDR_ITEM_IBYTE ? 2 : 8); }
 
 // constructor (dll_pll_veml_tracking.cc:85-560) for one channel slot, GPS L1 C/A
 // Tracking_FLL_PLL_filter::set_params (tracking_FLL_PLL_filter.cc:23-58)
@@ -1332,8 +1338,12 @@ int launch(gsdr_trk* k, const void* iq, uint64_t iq_first, uint64_t iq_items, ui
         hipLaunchKernelGGL((trk_kernel<GSDR_ITEM_GR_COMPLEX>), grid, dim3(kTrkThreads), k->lds_bytes, s, k->d_consts, k->d_chans,
             (const float* const*)k->d_codes, (const float* const*)k->d_data_codes, iq, iq_first, iq_items, max_epochs, out,
             nout, k->code_pad, k->data_pad, timing, k->timing_wall);
-    else
+    else if (k->conf.item_type == GSDR_ITEM_CSHORT)
         hipLaunchKernelGGL((trk_kernel<GSDR_ITEM_CSHORT>), grid, dim3(kTrkThreads), k->lds_bytes, s, k->d_consts, k->d_chans,
+            (const float* const*)k->d_codes, (const float* const*)k->d_data_codes, iq, iq_first, iq_items, max_epochs, out,
+            nout, k->code_pad, k->data_pad, timing, k->timing_wall);
+    else
+        hipLaunchKernelGGL((trk_kernel<GSDR_ITEM_IBYTE>), grid, dim3(kTrkThreads), k->lds_bytes, s, k->d_consts, k->d_chans,
             (const float* const*)k->d_codes, (const float* const*)k->d_data_codes, iq, iq_first, iq_items, max_epochs, out,
             nout, k->code_pad, k->data_pad, timing, k->timing_wall);
     GSDR_HIP(hipGetLastError());
@@ -1396,7 +1406,7 @@ int gsdr_trk_create(int device, const gsdr_trk_conf* conf, gsdr_trk** out)
     GSDR_REQUIRE(conf->max_channels > 0, GSDR_E_ARG, "gsdr_trk_create: max_channels must be > 0");
     GSDR_REQUIRE(conf->signal >= GSDR_SIGNAL_GPS_1C && conf->signal <= GSDR_SIGNAL_BDS_B1, GSDR_E_UNSUPPORTED,
         "gsdr_trk_create: signal %d not implemented", conf->signal);
-    GSDR_REQUIRE(conf->item_type == GSDR_ITEM_GR_COMPLEX || conf->item_type == GSDR_ITEM_CSHORT, GSDR_E_ARG,
+    GSDR_REQUIRE(conf->item_type >= GSDR_ITEM_GR_COMPLEX && conf->item_type <= GSDR_ITEM_IBYTE, GSDR_E_ARG,
         "gsdr_trk_create: unknown item type %d", conf->item_type);
     GSDR_REQUIRE(conf->extend_correlation_symbols >= 1, GSDR_E_ARG,
         "gsdr_trk_create: extend_correlation_symbols must be >= 1");
@@ -1459,6 +1469,9 @@ int gsdr_trk_create(int device, const gsdr_trk_conf* conf, gsdr_trk** out)
             (int)(kCuLds - kStaticLdsMargin));
     if (e == hipSuccess)
         e = hipFuncSetAttribute((const void*)trk_kernel<GSDR_ITEM_CSHORT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+            (int)(kCuLds - kStaticLdsMargin));
+    if (e == hipSuccess)
+        e = hipFuncSetAttribute((const void*)trk_kernel<GSDR_ITEM_IBYTE>, hipFuncAttributeMaxDynamicSharedMemorySize,
             (int)(kCuLds - kStaticLdsMargin));
     if (e != hipSuccess)
         {

@@ -20,6 +20,8 @@ GSDR_E_UNSUPPORTED = -5
 
 ITEM_GR_COMPLEX = 0
 ITEM_CSHORT = 1
+ITEM_IBYTE = 2  # interleaved int8 I,Q (Ibyte_To_Complex)
+_ITEM_NP = {0: np.complex64, 1: np.int16, 2: np.int8}
 ASSOC_GENERIC = 0
 ASSOC_AVX = 1
 
@@ -297,9 +299,7 @@ class Acquisition:
         return t.value
 
     def _items(self, iq):
-        if self.item_type == ITEM_CSHORT:
-            return np.ascontiguousarray(iq, np.int16)
-        return np.ascontiguousarray(iq, np.complex64)
+        return np.ascontiguousarray(iq, _ITEM_NP[int(self.item_type)])
 
     def run(self, iq, nblocks=1, stamp0=0):
         """Synchronous drop-in: host IQ of nblocks*max_dwells*consumed items (nblocks
@@ -408,7 +408,7 @@ class Correlator:
     def run(self, channel, sig, rem_carr, carr_step, rem_code, code_step, n, carr_rate=0.0, code_rate=0.0,
             item_type=ITEM_GR_COMPLEX):
         """Carrier_wipeoff_multicorrelator_resampler (7-argument form), synchronous."""
-        sig = np.ascontiguousarray(sig, np.int16 if item_type == ITEM_CSHORT else np.complex64)
+        sig = np.ascontiguousarray(sig, _ITEM_NP[int(item_type)])
         out = np.zeros(self.ntaps[channel], np.complex64)
         _check(load().gsdr_corr_run(self._h, channel, _ptr(sig), item_type, rem_carr, carr_step, carr_rate, rem_code,
                                     code_step, code_rate, int(n), _ptr(out)))
@@ -492,8 +492,8 @@ class Tracking:
     def run(self, iq, iq_first_sample, max_epochs):
         """Synchronous: host IQ -> (records [max_channels, max_epochs], counts [max_channels])."""
         item = int(self.conf["item_type"][0])
-        iq = np.ascontiguousarray(iq, np.int16 if item == ITEM_CSHORT else np.complex64)
-        n_items = len(iq) // 2 if item == ITEM_CSHORT else len(iq)
+        iq = np.ascontiguousarray(iq, _ITEM_NP[item])
+        n_items = len(iq) if item == ITEM_GR_COMPLEX else len(iq) // 2
         out = np.zeros(self.max_channels * max_epochs, TRK_EPOCH_DTYPE)
         n = np.zeros(self.max_channels, np.uint32)
         _check(load().gsdr_trk_run(self._h, _ptr(iq), int(iq_first_sample), int(n_items), int(max_epochs), _ptr(out),

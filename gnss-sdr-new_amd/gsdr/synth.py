@@ -125,6 +125,20 @@ def to_cshort(iq, scale=1000.0):
     return np.clip(np.rint(a), -32768, 32767).astype(np.int16)
 
 
+def to_ibyte(iq, scale=20.0):
+    """complex -> interleaved int8 I,Q (SignalSource.item_type=byte), saturating."""
+    a = np.empty(2 * len(iq), np.float64)
+    a[0::2] = iq.real * scale
+    a[1::2] = iq.imag * scale
+    return np.clip(np.rint(a), -128, 127).astype(np.int8)
+
+
+def ibyte_to_complex(b):
+    """Ibyte_To_Complex (gr::blocks::interleaved_char_to_complex, scale 1)."""
+    b = np.asarray(b, np.int8).astype(np.float32)
+    return (b[0::2] + 1j * b[1::2]).astype(np.complex64)
+
+
 # ---------------------------------------------------------------- Galileo E1, BeiDou B1I
 # Code tables: Galileo OS SIS ICD memory codes (data/galileo_e1_codes.bin, see
 # tools/extract_galileo_e1_codes.py); BeiDou B1I Gold codes from the ICD's G1/G2

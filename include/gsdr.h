@@ -48,7 +48,11 @@ extern "C" {
 
 /* Sample item types (Acq_Conf::item_type, acq_conf.h:42; item_type_size). */
 #define GSDR_ITEM_GR_COMPLEX 0 /* complex<float>, 8 bytes */
-#define GSDR_ITEM_CSHORT 1     /* complex<int16>, 4 bytes */
+#define GSDR_ITEM_CSHORT 1     /* complex<int16>, 4 bytes (also ishort: Ishort_To_Complex reads the same pairs) */
+/* interleaved int8 I,Q, 2 bytes: SignalSource.item_type=byte through Ibyte_To_Complex
+ * (data_type_adapter/adapters/ibyte_to_complex.cc:39, gr::blocks::interleaved_char_to_complex
+ * with scale 1): converted exactly to complex<float> inside the kernels' loads. */
+#define GSDR_ITEM_IBYTE 2
 
 /* Float association used for the resampler code-phase index:
  * GSDR_ASSOC_GENERIC: floor((step*n + shift) - rem)   KERN/32f_xn_resampler_32f_xn.h:73

@@ -177,6 +177,29 @@ def test_cshort_input():
         _check_result(res[p], grids[p], 0.01, 4, fs, dmax, dstep, 4000.0)
 
 
+def test_ibyte_input():
+    """SignalSource.item_type=byte through Ibyte_To_Complex: the engine reads the
+    interleaved int8 pairs directly (exact conversion), identical to gr_complex input
+    of the converted samples."""
+    fs, N, dmax, dstep = 4000000, 4000, 10000, 250
+    sats = synth.random_constellation(8, seed_offset=17, cn0_dbhz=50.0)
+    x = synth.gps_l1_iq(fs, N, sats, seed_offset=17)
+    xb = synth.to_ibyte(x, 24.0)
+    xf = synth.ibyte_to_complex(xb)
+    prns = np.array([s.prn for s in sats[:4]])
+    codes = _codes(prns, fs, N)
+    acq = gsdr.Acquisition(fs, N, dmax, dstep, pfa=0.01, max_prns=4, item_type=gsdr.ITEM_IBYTE)
+    acq.set_local_codes(codes, prns)
+    res = acq.run(xb)[0]
+    ref = gsdr.Acquisition(fs, N, dmax, dstep, pfa=0.01, max_prns=4)
+    ref.set_local_codes(codes, prns)
+    res_f = ref.run(xf)[0]
+    assert res.tobytes() == res_f.tobytes()
+    grids = _oracle_grids(xf, codes, fs, dmax, dstep, 80)
+    for p in range(4):
+        _check_result(res[p], grids[p], 0.01, 4, fs, dmax, dstep, 4000.0)
+
+
 def test_bad_configuration_errors():
     with pytest.raises(gsdr.GsdrError) as e:
         gsdr.Acquisition(4000000, 4000, 10000, 250, pfa=2.0)

@@ -134,7 +134,7 @@ def test_high_dynamics_resampler_and_rotator():
     assert ccompare(got, ref) <= 1e-4
 
 
-@pytest.mark.parametrize("item_type", [gsdr.ITEM_GR_COMPLEX, gsdr.ITEM_CSHORT])
+@pytest.mark.parametrize("item_type", [gsdr.ITEM_GR_COMPLEX, gsdr.ITEM_CSHORT, gsdr.ITEM_IBYTE])
 def test_batched_channels_from_device_buffer(item_type):
     """Config C3 shape: 12 channels x N=16000 x K=5 in one launch over a device IQ buffer."""
     fs, N, K = 16e6, 16000, 5
@@ -154,10 +154,13 @@ def test_batched_channels_from_device_buffer(item_type):
     if item_type == gsdr.ITEM_CSHORT:
         host = synth.to_cshort(x, 1000.0)
         xf = (host[0::2].astype(np.float32) + 1j * host[1::2].astype(np.float32)).astype(np.complex64)
+    elif item_type == gsdr.ITEM_IBYTE:
+        host = synth.to_ibyte(x, 20.0)
+        xf = synth.ibyte_to_complex(host)
     else:
         host = x
         xf = x
-    dev = torch.from_numpy(host.view(np.int16) if item_type == gsdr.ITEM_CSHORT else host.view(np.float32)).cuda()
+    dev = torch.from_numpy(host if item_type != gsdr.ITEM_GR_COMPLEX else host.view(np.float32)).cuda()
     out = torch.zeros(12 * K * 2, dtype=torch.float32, device="cuda")
     corr.run_batch(jobs, dev.data_ptr(), total, out.data_ptr(), item_type=item_type)
     torch.cuda.synchronize()

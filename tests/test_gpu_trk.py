@@ -129,7 +129,7 @@ def test_single_channel_matches_oracle_through_bit_sync():
     assert np.count_nonzero(g["flags"] & gsdr.TRK_F_VALID_OUTPUT) > 10
 
 
-@pytest.mark.parametrize("item", [gsdr.ITEM_GR_COMPLEX, gsdr.ITEM_CSHORT])
+@pytest.mark.parametrize("item", [gsdr.ITEM_GR_COMPLEX, gsdr.ITEM_CSHORT, gsdr.ITEM_IBYTE])
 def test_channel_pool_across_launches(item):
     """8 channels in one launch per chunk; the loop state persists on the device
     between launches (chunked input, like consecutive GNU Radio buffers)."""
@@ -142,6 +142,9 @@ def test_channel_pool_across_launches(item):
     if item == gsdr.ITEM_CSHORT:
         host = synth.to_cshort(iq, 800.0)
         iq_ref = (host[0::2].astype(np.float32) + 1j * host[1::2].astype(np.float32)).astype(np.complex64)
+    elif item == gsdr.ITEM_IBYTE:
+        host = synth.to_ibyte(iq, 16.0)
+        iq_ref = synth.ibyte_to_complex(host)
     else:
         host = iq
         iq_ref = iq
@@ -158,7 +161,7 @@ def test_channel_pool_across_launches(item):
     for k in range(4):
         lo = max(0, bounds[k] - 8000)
         hi = bounds[k + 1]
-        chunk = host[2 * lo:2 * hi] if item == gsdr.ITEM_CSHORT else host[lo:hi]
+        chunk = host[2 * lo:2 * hi] if item != gsdr.ITEM_GR_COMPLEX else host[lo:hi]
         rec, n = t.run(chunk, lo, 2000)
         for c in range(len(sats)):
             got[c].append(rec[c][:n[c]])

@@ -46,6 +46,11 @@ void pcps_acquisition_mi355x::ensure_engine()
         }
     d_engine_dmax = dmax;
     d_engine_step = d_doppler_step;
+    // make_two_steps narrow grid (Acq_Conf second_nbins / second_doppler_step / pfa2)
+    if (d_acq_parameters.make_2_steps &&
+        gsdr_acq_set_step_two(d_engine, d_acq_parameters.num_doppler_bins_step2, d_acq_parameters.doppler_step2,
+            d_acq_parameters.pfa2) != GSDR_OK)
+        throw std::runtime_error(std::string("pcps_acquisition_mi355x: ") + gsdr_last_error());
     uint32_t D = 0, N = 0;
     gsdr_acq_get_dims(d_engine, &D, &N);
     d_num_doppler_bins = D;
@@ -137,12 +142,17 @@ bool pcps_acquisition_mi355x::start()
     return true;
 }
 
-// calculate_threshold (:894-909): computed by the engine from pfa.
+// calculate_threshold (:894-909): computed by the engine from pfa, or from pfa2
+// and the narrow bin count while d_step_two.
 void pcps_acquisition_mi355x::calculate_threshold()
 {
-    if (d_acq_parameters.pfa <= 0.0F) return;
+    const float pfa = d_step_two ? d_acq_parameters.pfa2 : d_acq_parameters.pfa;
+    if (pfa <= 0.0F) return;
     ensure_engine();
-    gsdr_acq_get_threshold(d_engine, &d_threshold);
+    if (d_step_two)
+        gsdr_acq_get_step_two_threshold(d_engine, &d_threshold);
+    else
+        gsdr_acq_get_threshold(d_engine, &d_threshold);
 }
 
 void pcps_acquisition_mi355x::send_positive_acquisition()
@@ -157,14 +167,28 @@ void pcps_acquisition_mi355x::send_negative_acquisition()
     if (d_events) d_events(2);
 }
 
-// acquisition_core (:615-882) for the single-dwell, single-step configuration.
+// acquisition_core (:615-882) for the single-dwell configuration, with the
+// make_two_steps narrow grid (:717-773) when d_step_two.
 void pcps_acquisition_mi355x::acquisition_core(uint64_t samp_count)
 {
     d_mag = 0.0F;
     d_num_noncoherent_integrations_counter++;
-    gsdr_acq_set_threshold(d_engine, d_threshold);
+    // the engine keeps the first-step threshold (calculate_threshold reads it back
+    // after step two); the step-two decision below uses d_threshold
+    if (!d_step_two) gsdr_acq_set_threshold(d_engine, d_threshold);
     gsdr_acq_result r{};
-    if (gsdr_acq_run(d_engine, d_data_buffer.data(), 1, samp_count, &r) != GSDR_OK)
+    int rc;
+    if (d_step_two)
+        {
+            const uint32_t slot = 0;
+            rc = gsdr_acq_run_step_two(d_engine, d_data_buffer.data(), 1, &slot, &d_doppler_center_step_two,
+                &d_input_power, samp_count, &r);
+        }
+    else
+        {
+            rc = gsdr_acq_run(d_engine, d_data_buffer.data(), 1, samp_count, &r);
+        }
+    if (rc != GSDR_OK)
         {
             // device error -> negative acquisition, the reference's failure convention
             std::cerr << "pcps_acquisition_mi355x: " << gsdr_last_error() << '\n';
@@ -192,13 +216,35 @@ void pcps_acquisition_mi355x::acquisition_core(uint64_t samp_count)
                     d_gnss_synchro->Acq_samplestamp_samples = samp_count;
                 }
             d_gnss_synchro->Acq_doppler_hz = static_cast<double>(r.doppler_hz);
+            if (d_step_two) d_gnss_synchro->Acq_doppler_step = static_cast<uint32_t>(d_acq_parameters.doppler_step2);
         }
-    // decision and dwell FSM (:781-829, non-bit-transition branch, one step)
+    // decision and dwell FSM (:781-829, non-bit-transition branch)
     if (d_test_statistics > d_threshold)
         {
             d_active = false;
-            send_positive_acquisition();
-            d_state = 0;
+            if (d_acq_parameters.make_2_steps)
+                {
+                    if (d_step_two)
+                        {
+                            send_positive_acquisition();
+                            d_step_two = false;
+                            d_state = 0;
+                        }
+                    else
+                        {
+                            // clear the buffer and search the narrow grid on the next block
+                            d_step_two = true;
+                            d_num_noncoherent_integrations_counter = 0;
+                            d_positive_acq = 0;
+                            d_state = 0;
+                        }
+                    calculate_threshold();
+                }
+            else
+                {
+                    send_positive_acquisition();
+                    d_state = 0;
+                }
         }
     else
         {
@@ -210,6 +256,9 @@ void pcps_acquisition_mi355x::acquisition_core(uint64_t samp_count)
             if (d_state != 0) send_negative_acquisition();
             d_state = 0;
             d_active = false;
+            const bool was_step_two = d_step_two;
+            d_step_two = false;
+            if (was_step_two) calculate_threshold();
         }
     if (d_num_noncoherent_integrations_counter == d_acq_parameters.max_dwells || d_positive_acq == 1)
         {
@@ -224,12 +273,20 @@ int pcps_acquisition_mi355x::work(const void* in, int ninput_items)
     std::unique_lock<std::mutex> lk(d_setlock);
     if (!d_active)
         {
+            int consumed = 0;
             if (!d_acq_parameters.blocking_on_standby)
                 {
                     d_sample_counter += static_cast<uint64_t>(ninput_items);
-                    return ninput_items;
+                    consumed = ninput_items;
                 }
-            return 0;
+            // make_two_steps: centre the narrow grid on the coarse Doppler (:937-943)
+            if (d_step_two)
+                {
+                    d_doppler_center_step_two = d_gnss_synchro ? static_cast<float>(d_gnss_synchro->Acq_doppler_hz) : 0.0F;
+                    d_state = 0;
+                    d_active = true;
+                }
+            return consumed;
         }
     switch (d_state)
         {

@@ -51,6 +51,7 @@ public:
     float test_statistics() const { return d_test_statistics; }
     float input_power() const { return d_input_power; }
     uint32_t num_doppler_bins() const { return d_num_doppler_bins; }
+    bool step_two() const { return d_step_two; }
 
 private:
     void acquisition_core(uint64_t samp_count);
@@ -83,6 +84,8 @@ private:
     uint32_t d_num_doppler_bins{0};
     uint32_t d_buffer_count{0};
     bool d_active{false};
+    bool d_step_two{false};                // make_2_steps: the next core call is the narrow grid
+    float d_doppler_center_step_two{0.0F};
     std::mutex d_setlock;
 };
 

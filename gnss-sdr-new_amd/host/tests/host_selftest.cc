@@ -125,6 +125,72 @@ void test_acquisition_validation(const std::vector<std::complex<float>>& capture
         static_cast<unsigned long long>(gnss_synchro.Acq_samplestamp_samples));
 }
 
+// make_two_steps on the same capture: coarse 500 Hz grid on the first millisecond,
+// then a 5-bin 100 Hz narrow grid around it on the second (blocking_on_standby so
+// the 2 ms capture holds both blocks).
+void test_acquisition_two_steps(const std::vector<std::complex<float>>& capture)
+{
+    InMemoryConfiguration config;
+    config.set_property("GNSS-SDR.internal_fs_sps", "4000000");
+    config.set_property("Acquisition_1C.implementation", "GPS_L1_CA_PCPS_Acquisition_MI355X");
+    config.set_property("Acquisition_1C.item_type", "gr_complex");
+    config.set_property("Acquisition_1C.coherent_integration_time_ms", "1");
+    config.set_property("Acquisition_1C.pfa", "0.01");
+    config.set_property("Acquisition_1C.doppler_max", "5000");
+    config.set_property("Acquisition_1C.doppler_step", "500");
+    config.set_property("Acquisition_1C.make_two_steps", "true");
+    config.set_property("Acquisition_1C.second_nbins", "5");
+    config.set_property("Acquisition_1C.second_doppler_step", "100");
+    config.set_property("Acquisition_1C.blocking_on_standby", "true");
+
+    Gnss_Synchro gnss_synchro{};
+    gnss_synchro.System = 'G';
+    gnss_synchro.Signal[0] = '1';
+    gnss_synchro.Signal[1] = 'C';
+    gnss_synchro.PRN = 1;
+    GpsL1CaPcpsAcquisitionMI355X acquisition(&config, "Acquisition_1C", 1, 0);
+    int rx_message = 0;
+    acquisition.get_block()->set_event_handler([&](int ev) { rx_message = ev; });
+    acquisition.set_gnss_synchro(&gnss_synchro);
+    acquisition.set_doppler_max(5000);
+    acquisition.set_doppler_step(500);
+    acquisition.set_local_code();
+    acquisition.set_state(1);
+    acquisition.init();
+    acquisition.get_block()->start();
+    const float thr1 = acquisition.get_block()->threshold();
+    size_t pos = 0;
+    int guard = 0;
+    bool saw_step_two = false;
+    double coarse = 0.0;
+    float thr2 = thr1;
+    // at the end of the capture keep calling with no new items: the state machine
+    // still has to run the core on its full buffer
+    while (rx_message == 0 && guard++ < 100)
+        {
+            const int n = static_cast<int>(std::min<size_t>(1000, capture.size() - pos));
+            const bool before = acquisition.get_block()->step_two();
+            pos += static_cast<size_t>(acquisition.get_block()->work(capture.data() + pos, n));
+            if (!before && acquisition.get_block()->step_two())
+                {
+                    saw_step_two = true;
+                    coarse = gnss_synchro.Acq_doppler_hz;
+                    thr2 = acquisition.get_block()->threshold();
+                }
+        }
+    EXPECT(saw_step_two, "first step positive -> step two");
+    EXPECT(rx_message == 1, "two-step acquisition positive");
+    EXPECT(gnss_synchro.Acq_doppler_step == 100U, "Acq_doppler_step = second_doppler_step");
+    EXPECT(std::abs(gnss_synchro.Acq_doppler_hz - coarse) <= 200.0, "narrow grid within +-2 bins of the coarse Doppler");
+    EXPECT(std::abs(gnss_synchro.Acq_doppler_hz - 1680.0) < std::abs(coarse - 1680.0) + 1e-9,
+        "refinement does not move away from the capture's Doppler");
+    EXPECT(gnss_synchro.Acq_samplestamp_samples == 8000ULL, "step two on the second block");
+    EXPECT(thr2 < thr1, "step-two threshold from the narrow bin count");
+    EXPECT(acquisition.get_block()->threshold() == thr1, "first-step threshold restored after step two");
+    std::printf("two steps: coarse %.0f Hz -> fine %.0f Hz, delay %.1f samples, stat %.3f\n", coarse,
+        gnss_synchro.Acq_doppler_hz, gnss_synchro.Acq_delay_samples, acquisition.get_block()->test_statistics());
+}
+
 void test_multicorrelator(const std::vector<std::complex<float>>& capture)
 {
     const int n = 4000;
@@ -183,6 +249,7 @@ int main(int argc, char** argv)
             return 2;
         }
     test_acquisition_validation(capture);
+    test_acquisition_two_steps(capture);
     test_multicorrelator(capture);
     if (failures == 0) std::printf("host_selftest: PASS\n");
     return failures == 0 ? 0 : 1;

@@ -47,6 +47,7 @@ constexpr int kMaxCn0 = 64;         // cn0_samples capacity
 constexpr int kMaxTrkTaps = 5;
 constexpr int kMaxCodeFloats = 16384;
 constexpr int kPreambleLen = 160;   // GPS_CA_PREAMBLE_LENGTH_SYMBOLS (GPS_L1_CA.h:61)
+constexpr int kMaxSmoother = 32;             // Dll_Pll_Conf::smoother_length cap (high_dyn histories)
 constexpr int kSpl = 8;                       // samples per lane per correlation chunk
 constexpr int kWinCore = kSpl * kTrkThreads;  // 4096: the next call's window staged in LDS
 constexpr int kHalo = 16;                     // slack around the predicted next start
@@ -194,6 +195,7 @@ struct TrkConst
     CfConst cf;
     SmConst sm[2];  // 0: CN0, 1: carrier lock test
     CfConst cf_narrow;
+    int32_t high_dyn, smoother_length;  // Dll_Pll_Conf::high_dyn / smoother_length (dll_pll_conf.h:62,80)
 };
 
 // Mutable scalar loop state (dll_pll_veml_tracking.h:117-209 minus the
@@ -217,6 +219,7 @@ struct TrkHot
     int32_t pull_in_transitory, cloop, acc_carrier_phase_initialized, flag_pll_180;
     double corr_time;            // d_current_correlation_time_s
     int32_t narrow, extend_count;  // after the switch to the extended correlator
+    int32_t hist_n, hist_head;     // high_dyn: d_carr_ph_history / d_code_ph_history fill and oldest slot
 };
 
 // Device-memory image of the mutable part of one channel.
@@ -225,6 +228,9 @@ struct TrkChan
     TrkHot h;
     LoopFilter code_filter;
     float2 prompt_buffer[kMaxCn0];
+    // high_dyn: the two boost::circular_buffer<pair<double,double>> of capacity
+    // 2*smoother_length (:554-563), pushed together (same sample count)
+    double hist_carr[2 * kMaxSmoother], hist_code[2 * kMaxSmoother], hist_samples[2 * kMaxSmoother];
 };
 
 struct Prep  // lane-0 -> workgroup broadcast of one call's NCO
@@ -237,6 +243,12 @@ struct Prep  // lane-0 -> workgroup broadcast of one call's NCO
     int32_t woff;  // >= 0: this call's samples are in the LDS window at that offset
     int32_t fast;  // every code index of the call lies in [-L, 2L): branch-free wrap
     int32_t narrow;  // the call uses the narrow tap shifts
+    // high_dyn: rotator rate term and resampler rate (do_correlation_step, :1069-1075),
+    // taps 1..K-1 as sample-shifted copies of tap 0 (32f_xn_high_dynamics_resampler_32f_xn.h:84-91)
+    int32_t hd;
+    double theta_rate;
+    float code_rate;
+    int32_t hdshift[kMaxTrkTaps];
 };
 
 // ------------------------------------------------------------------ wave-0 loop body
@@ -349,6 +361,8 @@ __device__ inline void clear_tracking_vars(TrkHot& t)  // :1192-1213
     for (int w = 0; w < 5; ++w) t.circ[w] = 0u;
     t.carrier_phase_rate_step_rad = 0.0;
     t.code_phase_rate_step_chips = 0.0;
+    t.hist_n = 0;  // d_carr_ph_history.clear(), d_code_ph_history.clear()
+    t.hist_head = 0;
 }
 
 // cn0_and_tracking_lock_status (:970-1056) with cn0_m2m4_estimator and
@@ -459,7 +473,29 @@ __device__ inline void run_dll_pll(const TrkConst& c, TrkHot& t, LoopFilter& lf)
     if (c.carrier_aiding) t.code_freq_chips += t.carrier_doppler_hz * c.code_chip_rate / c.signal_carrier_freq;
 }
 
-__device__ inline void update_tracking_vars(const TrkConst& c, TrkHot& t)  // :1216-1287 (high_dyn = false)
+// high_dyn rate estimate (:1232-1251, :1265-1284): mean of the newest
+// smoother_length steps minus mean of the oldest, over the newest sample counts,
+// summed in the reference's order ([k] counts from the oldest element).  The
+// element just pushed (slot) comes from registers, not read back.
+__device__ inline double hist_rate(const double* v, const double* s, int head, int cap, int L, int slot, double vnew,
+    double snew)
+{
+    double cp1 = 0.0, cp2 = 0.0, samples = 0.0;
+    for (int k = 0; k < L; ++k)
+        {
+            const int a = (head + k) % cap, b = (head + 2 * L - k - 1) % cap;
+            cp1 += a == slot ? vnew : v[a];
+            cp2 += b == slot ? vnew : v[b];
+            samples += b == slot ? snew : s[b];
+        }
+    cp1 /= (double)L;
+    cp2 /= (double)L;
+    return (cp2 - cp1) / samples;
+}
+
+// Every lane of wave 0 runs this with uniform values; the history stores write
+// the same value from every lane.
+__device__ inline void update_tracking_vars(const TrkConst& c, TrkHot& t, TrkChan* gc)  // :1216-1287
 {
     const double T_chip = 1.0 / t.code_freq_chips;
     const double T_prn = T_chip * (double)c.code_length_chips;
@@ -467,11 +503,40 @@ __device__ inline void update_tracking_vars(const TrkConst& c, TrkHot& t)  // :1
     const double K_blk = T_prn_samples + t.rem_code_phase_samples;
     t.current_prn_length_samples = (int32_t)floor(K_blk);
     t.carrier_phase_step_rad = kTwoPi * t.carrier_doppler_hz / c.fs_in;
+    int slot = 0;
+    const int cap = 2 * c.smoother_length;
+    const double ns = (double)t.current_prn_length_samples;
+    if (c.high_dyn)
+        {
+            // push_back on a full circular buffer overwrites the oldest element
+            if (t.hist_n < cap)
+                {
+                    slot = (t.hist_head + t.hist_n) % cap;
+                    t.hist_n++;
+                }
+            else
+                {
+                    slot = t.hist_head;
+                    t.hist_head = (t.hist_head + 1) % cap;
+                }
+            if (t.hist_n == cap)
+                t.carrier_phase_rate_step_rad = hist_rate(gc->hist_carr, gc->hist_samples, t.hist_head, cap,
+                    c.smoother_length, slot, t.carrier_phase_step_rad, ns);
+            gc->hist_carr[slot] = t.carrier_phase_step_rad;
+        }
     const double len = (double)t.current_prn_length_samples;
     t.rem_carr_phase_rad += (float)(t.carrier_phase_step_rad * len + 0.5 * t.carrier_phase_rate_step_rad * len * len);
     t.rem_carr_phase_rad = (float)fmod((double)t.rem_carr_phase_rad, kTwoPi);
     t.acc_carrier_phase_rad -= (t.carrier_phase_step_rad * len + 0.5 * t.carrier_phase_rate_step_rad * len * len);
     t.code_phase_step_chips = t.code_freq_chips / c.fs_in;
+    if (c.high_dyn)
+        {
+            if (t.hist_n == cap)
+                t.code_phase_rate_step_chips = hist_rate(gc->hist_code, gc->hist_samples, t.hist_head, cap,
+                    c.smoother_length, slot, t.code_phase_step_chips, ns);
+            gc->hist_code[slot] = t.code_phase_step_chips;
+            gc->hist_samples[slot] = ns;
+        }
     t.rem_code_phase_samples = K_blk - len;
     t.rem_code_phase_chips = t.code_freq_chips * t.rem_code_phase_samples / c.fs_in;
 }
@@ -575,7 +640,7 @@ __device__ inline void save_correlation_results(const TrkConst& c, TrkHot& t, co
 
 // One general_work call after the correlation (taps given; slot kMaxTrkTaps is
 // the pilot-tracking data prompt): states 2 and 4.
-__device__ inline void after_correlation(const TrkConst& c, TrkHot& t, LoopFilter& lf, float2* pbuf,
+__device__ inline void after_correlation(const TrkConst& c, TrkHot& t, TrkChan* gc, LoopFilter& lf, float2* pbuf,
     const float2 (&taps)[kMaxTrkTaps + 1], uint64_t nitems_read, int lane, EpochOut& o)
 {
     o.flags = 0;
@@ -605,7 +670,7 @@ __device__ inline void after_correlation(const TrkConst& c, TrkHot& t, LoopFilte
                 {
                     int next_state = 0;
                     run_dll_pll(c, t, lf);
-                    update_tracking_vars(c, t);
+                    update_tracking_vars(c, t, gc);
                     if (!t.pull_in_transitory)
                         {
                             if (c.secondary || c.symbols_per_bit > 1)
@@ -645,7 +710,7 @@ __device__ inline void after_correlation(const TrkConst& c, TrkHot& t, LoopFilte
     else if (t.state == 3)  // coherent integration (:1989-2026)
         {
             save_correlation_results(c, t, taps);
-            update_tracking_vars(c, t);
+            update_tracking_vars(c, t, gc);
             if (t.current_data_symbol == 0)
                 {
                     o.prompt_i = (double)t.P_data_accu.x;
@@ -673,7 +738,7 @@ __device__ inline void after_correlation(const TrkConst& c, TrkHot& t, LoopFilte
             else
                 {
                     run_dll_pll(c, t, lf);
-                    update_tracking_vars(c, t);
+                    update_tracking_vars(c, t, gc);
                     if (!t.acc_carrier_phase_initialized)
                         {
                             t.acc_carrier_phase_rad = -(double)t.rem_carr_phase_rad;
@@ -773,6 +838,57 @@ __device__ __forceinline__ void correlate_chunk(const void* __restrict__ iq, con
                         }
                 }
             ph = make_float2(ph.x * p.wstep.x - ph.y * p.wstep.y, ph.x * p.wstep.y + ph.y * p.wstep.x);
+        }
+}
+
+// high_dyn correlation (do_correlation_step with set_high_dynamics_resampler(true)):
+// VOLK-GNSSSDR 32f_xn_high_dynamics_resampler_32f_xn generic (:67-96: tap 0 index
+// floor(step*m + rate*(m*m) + shift0 - rem) with the unsigned m*m, taps 1..K-1 the
+// sample-shifted copies of tap 0) and 32fc_32f_high_dynamic_rotator_dot_prod_32fc_xn
+// (:68-112: sample n rotated by the phase of n*theta + (n-1)^2*theta_rate, from the
+// fp64 model as in corr.hip).  Lane-strided samples; the window or HBM as the fast path.
+template <int IT>
+__device__ void correlate_call_hd(const void* __restrict__ iq, const float2* s_win, const float* s_code,
+    const float* s_data, const Prep& p, int vl, int L, int K, bool data, float shift0, float shiftP,
+    float2 (&acc)[kMaxTrkTaps + 1])
+{
+    constexpr double kInvTwoPi = 0.15915494309189533576888376337251;
+    auto index = [&](float shift, uint32_t m) {
+        const float a = gsdr::mul_rn(p.code_step, (float)m);
+        const float b = gsdr::mul_rn(p.code_rate, (float)(m * m));
+        int raw = (int)floorf(gsdr::sub_rn(gsdr::add_rn(gsdr::add_rn(a, b), shift), p.rem_code));
+        raw %= L;
+        return raw < 0 ? raw + L : raw;
+    };
+    for (int n = (int)threadIdx.x; n < vl; n += kTrkThreads)
+        {
+            const float2 x = p.woff >= 0 ? s_win[p.woff + n] : load_iq<IT>(iq, p.off + n);
+            double phi = p.psi0 + (double)n * p.theta;
+            if (n > 0)
+                {
+                    const double m1 = (double)(n - 1);
+                    phi += m1 * m1 * p.theta_rate;
+                }
+            const float ang = (float)fma(-rint(phi * kInvTwoPi), kTwoPi, phi);
+            float sn, cs;
+            sincosf(ang, &sn, &cs);
+            const float2 tt = make_float2(x.x * cs - x.y * sn, x.x * sn + x.y * cs);
+#pragma unroll
+            for (int k = 0; k < kMaxTrkTaps; ++k)
+                {
+                    if (k < K)
+                        {
+                            const float cv = s_code[index(shift0, (uint32_t)((n + p.hdshift[k]) % vl))];
+                            acc[k].x += tt.x * cv;
+                            acc[k].y += tt.y * cv;
+                        }
+                }
+            if (data)
+                {
+                    const float dv = s_data[index(shiftP, (uint32_t)n)];
+                    acc[kMaxTrkTaps].x += tt.x * dv;
+                    acc[kMaxTrkTaps].y += tt.y * dv;
+                }
         }
 }
 
@@ -898,6 +1014,20 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                             const float hi = floorf(gsdr::add_rn(gsdr::mul_rn(p.code_step, (float)(vl - 1)), smax));
                             const float Lf = (float)L;
                             p.fast = p.code_step >= 0.0f && lo >= -Lf && hi < 2.0f * Lf;
+                            if (c.high_dyn)
+                                {
+                                    p.hd = 1;
+                                    p.theta_rate = -(double)(float)t.carrier_phase_rate_step_rad;
+                                    p.code_rate = (float)t.code_phase_rate_step_chips * (float)c.code_samples_per_chip;
+                                    unsigned int shs = 0;
+                                    p.hdshift[0] = 0;
+                                    for (int k = 1; k < K; ++k)
+                                        {
+                                            const float* sk = t.narrow ? c.shifts_narrow : c.shifts;
+                                            shs += (int)roundf((sk[k] - sk[k - 1]) / p.code_step);
+                                            p.hdshift[k] = (int)shs;
+                                        }
+                                }
                             const double w = p.theta * (double)kTrkThreads;
                             float sn, cs;
                             sincosf((float)fma(-rint(w * 0.15915494309189533576888376337251), 6.283185307179586476925286766559, w),
@@ -926,7 +1056,12 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
 #pragma unroll
             for (int k = 0; k < kMaxTrkTaps; ++k)
                 sh_rem[k] = gsdr::sub_rn(p.narrow ? c.shifts_narrow[k] : c.shifts[k], p.rem_code);
-            if (K <= 3)
+            if (p.hd)
+                {
+                    const float* sk = p.narrow ? c.shifts_narrow : c.shifts;
+                    correlate_call_hd<IT>(iq, s_win, s_code, s_data, p, vl, L, K, data, sk[0], sk[c.iP], acc);
+                }
+            else if (K <= 3)
                 correlate_call<IT, 3, false>(iq, s_win, s_code, s_data, p, vl, L, sh_rem, ph, acc);
             else if (!data)
                 correlate_call<IT, kMaxTrkTaps, false>(iq, s_win, s_code, s_data, p, vl, L, sh_rem, ph, acc);
@@ -1000,7 +1135,7 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                             t.code_lock_fail_counter = 0;
                         }
                     EpochOut o;
-                    after_correlation(c, t, s_lf, s_pbuf, taps, n_read, lane, o);
+                    after_correlation(c, t, gc, s_lf, s_pbuf, taps, n_read, lane, o);
                     if (lane == 0)
                         {
                             gsdr_trk_epoch r;
@@ -1026,7 +1161,8 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                             r.evm = t.evm;
                             r.data_prompt[0] = data ? taps[kMaxTrkTaps].x : 0.0F;
                             r.data_prompt[1] = data ? taps[kMaxTrkTaps].y : 0.0F;
-                            r.reserved[0] = r.reserved[1] = 0;
+                            r.carrier_rate = (float)t.carrier_phase_rate_step_rad;
+                            r.code_rate = (float)t.code_phase_rate_step_chips;
                             out[(size_t)ch * max_epochs + e] = r;
                             if (timing)
                                 {
@@ -1261,6 +1397,9 @@ void init_channel(const gsdr_trk_conf& cf, TrkConst& c, TrkChan& ch)
     c.early_late_space_narrow_chips = cf.early_late_space_narrow_chips;
     c.dll_bw_narrow_hz = cf.dll_bw_narrow_hz;
     c.enable_ext = cf.extend_correlation_symbols > 1 ? 1 : 0;
+    c.high_dyn = cf.high_dyn ? 1 : 0;
+    // dll_pll_conf.cc:118-123: smoother_length < 1 is set to 1
+    c.smoother_length = cf.smoother_length < 1 ? 1 : (int32_t)cf.smoother_length;
     // Exponential_Smoother defaults (exponential_smoother.h:58-63) + dll_pll_veml_tracking.cc:540-552
     sm_set(c.sm[0], cf.cn0_smoother_alpha, 25.0F, 12.0F, cf.cn0_smoother_samples / (int)(c.code_period * 1000.0));
     sm_set(c.sm[1], cf.carrier_lock_test_smoother_alpha, -1.0F, 0.0F, cf.carrier_lock_test_smoother_samples);
@@ -1389,6 +1528,7 @@ void gsdr_trk_conf_default(gsdr_trk_conf* c)
     c->pll_filter_order = 3;
     c->dll_filter_order = 2;
     c->extend_correlation_symbols = 1;
+    c->smoother_length = 10;
     c->cn0_samples = 20;
     c->cn0_smoother_samples = 200;
     c->carrier_lock_test_smoother_samples = 25;
@@ -1410,7 +1550,8 @@ int gsdr_trk_create(int device, const gsdr_trk_conf* conf, gsdr_trk** out)
         "gsdr_trk_create: unknown item type %d", conf->item_type);
     GSDR_REQUIRE(conf->extend_correlation_symbols >= 1, GSDR_E_ARG,
         "gsdr_trk_create: extend_correlation_symbols must be >= 1");
-    GSDR_REQUIRE(conf->high_dyn == 0, GSDR_E_UNSUPPORTED, "gsdr_trk_create: high_dyn not implemented in the loop");
+    GSDR_REQUIRE(!conf->high_dyn || conf->smoother_length <= (uint32_t)kMaxSmoother, GSDR_E_UNSUPPORTED,
+        "gsdr_trk_create: smoother_length %u > %d", conf->smoother_length, kMaxSmoother);
     GSDR_REQUIRE(conf->cn0_samples >= 1 && conf->cn0_samples <= kMaxCn0, GSDR_E_UNSUPPORTED,
         "gsdr_trk_create: cn0_samples %d outside [1,%d]", conf->cn0_samples, kMaxCn0);
     GSDR_REQUIRE(conf->pll_filter_order == 2 || conf->pll_filter_order == 3, GSDR_E_ARG,
@@ -1586,6 +1727,8 @@ int gsdr_trk_start(gsdr_trk* k, int ch, uint32_t prn, const float* code, int cod
     t.carrier_doppler_hz = acq_doppler_hz;
     t.carrier_phase_step_rad = kTwoPi * t.carrier_doppler_hz / c.fs_in;
     t.carrier_phase_rate_step_rad = 0.0;
+    t.hist_n = 0;  // d_carr_ph_history.clear(), d_code_ph_history.clear() (:651-652)
+    t.hist_head = 0;
     t.carrier_lock_fail_counter = 0;
     t.code_lock_fail_counter = 0;
     t.rem_code_phase_samples = 0.0;

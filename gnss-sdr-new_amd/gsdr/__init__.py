@@ -59,7 +59,7 @@ TRK_CONF_DTYPE = np.dtype([
     ("extend_correlation_symbols", "i4"), ("cn0_samples", "i4"), ("cn0_smoother_samples", "i4"),
     ("carrier_lock_test_smoother_samples", "i4"), ("cn0_min", "i4"), ("max_code_lock_fail", "i4"),
     ("max_carrier_lock_fail", "i4"), ("enable_fll_pull_in", "i4"), ("enable_fll_steady_state", "i4"),
-    ("carrier_aiding", "i4"), ("high_dyn", "i4"), ("track_pilot", "i4")], align=True)
+    ("carrier_aiding", "i4"), ("high_dyn", "i4"), ("track_pilot", "i4"), ("smoother_length", "u4")], align=True)
 assert TRK_CONF_DTYPE.itemsize == 144
 
 TRK_EPOCH_DTYPE = np.dtype([
@@ -67,7 +67,7 @@ TRK_EPOCH_DTYPE = np.dtype([
     ("rem_carr_phase_rad", "f4"), ("flags", "i4"), ("carrier_doppler_hz", "f8"), ("code_freq_chips", "f8"),
     ("rem_code_phase_samples", "f8"), ("acc_carrier_phase_rad", "f8"), ("cn0_db_hz", "f8"),
     ("carrier_lock_test", "f8"), ("prompt_i", "f8"), ("prompt_q", "f8"), ("evm", "f8"), ("data_prompt", "f4", (2,)),
-    ("reserved", "i4", (2,))], align=True)
+    ("carrier_rate", "f4"), ("code_rate", "f4")], align=True)
 assert TRK_EPOCH_DTYPE.itemsize == 152
 
 

@@ -65,8 +65,9 @@ class Satellite:
     code_doppler: the code rate follows the carrier Doppler (1 + f_d / f_L1)."""
 
     def __init__(self, prn, doppler_hz, code_delay_chips, cn0_dbhz=45.0, phase=0.0, bit_period_ms=20,
-                 preamble_every_bits=None, code_doppler=False):
+                 preamble_every_bits=None, code_doppler=False, doppler_rate_hz_s=0.0):
         self.prn = prn
+        self.doppler_rate_hz_s = doppler_rate_hz_s  # linear Doppler ramp (high-dynamics tests)
         self.doppler_hz = doppler_hz
         self.code_delay_chips = code_delay_chips
         self.cn0_dbhz = cn0_dbhz
@@ -105,13 +106,22 @@ def gps_l1_iq(fs, n_samples, sats, seed_offset=0, t0_samples=0, noise=True, dtyp
         chips = gps_ca_chips(s.prn)
         amp = np.sqrt(10.0 ** (s.cn0_dbhz / 10.0) / fs)
         rate = 1.023e6 * (1.0 + s.doppler_hz / GPS_L1_HZ) if s.code_doppler else 1.023e6
-        code_phase = t * rate - s.code_delay_chips
+        ramp = getattr(s, "doppler_rate_hz_s", 0.0)
+        if ramp:
+            cycles = s.doppler_hz * t + 0.5 * ramp * t * t
+            code_phase = t * 1.023e6 + (1.023e6 / GPS_L1_HZ * cycles if s.code_doppler else 0.0) - s.code_delay_chips
+        else:
+            cycles = None
+            code_phase = t * rate - s.code_delay_chips
         c = chips[np.floor(code_phase).astype(np.int64) % 1023]
         nbits = int(np.ceil((t[-1] + 1) * 1000 / s.bit_period_ms)) + 2
         bits = s.nav_bits(nbits)
         # bit edges follow the code epochs (20 code periods per bit)
         b = bits[np.floor(code_phase / 1023.0 / s.bit_period_ms).astype(np.int64) % nbits]
-        out += amp * c * b * np.exp(1j * (2 * np.pi * s.doppler_hz * t + s.phase))
+        if cycles is not None:
+            out += amp * c * b * np.exp(1j * (2 * np.pi * cycles + s.phase))
+        else:
+            out += amp * c * b * np.exp(1j * (2 * np.pi * s.doppler_hz * t + s.phase))
     if noise:
         out += (rng.standard_normal(n_samples) + 1j * rng.standard_normal(n_samples)) * np.sqrt(0.5)
     return out.astype(dtype)

@@ -319,8 +319,10 @@ typedef struct gsdr_trk_conf
     int32_t enable_fll_pull_in;
     int32_t enable_fll_steady_state;
     int32_t carrier_aiding;
-    int32_t high_dyn; /* only 0 in this version */
+    int32_t high_dyn;    /* Dll_Pll_Conf::high_dyn: high-dynamics resampler/rotator + carrier/code rate
+                            estimates from the step histories (dll_pll_veml_tracking.cc:1232-1284) */
     int32_t track_pilot; /* Dll_Pll_Conf::track_pilot (default 1); forced 0 for GPS L1 C/A and BeiDou B1I */
+    uint32_t smoother_length; /* Dll_Pll_Conf::smoother_length (default 10, at most 32): histories of 2x that */
 } gsdr_trk_conf;
 
 /* One general_work call of one channel (written for every call that ran a
@@ -344,7 +346,8 @@ typedef struct gsdr_trk_epoch
     double prompt_q;               /* Prompt_Q (valid output only) */
     double evm;                    /* EVM (fork indicator, :1027-1053) */
     float data_prompt[2];          /* pilot tracking: the data-component prompt of the call (d_Prompt_Data[0]) */
-    int32_t reserved[2];
+    float carrier_rate;            /* high_dyn: (float)d_carrier_phase_rate_step_rad after the call [rad/sample^2] */
+    float code_rate;               /* high_dyn: (float)d_code_phase_rate_step_chips after the call [chips/sample^2] */
 } gsdr_trk_epoch;
 
 #define GSDR_TRK_F_VALID_OUTPUT 1 /* Flag_valid_symbol_output: a Gnss_Synchro was emitted */

@@ -494,6 +494,10 @@ typedef struct orc_trk
     int32_t carrier_lock_fail_counter, code_lock_fail_counter;
     int pull_in_transitory, cloop, acc_carrier_phase_initialized, flag_pll_180;
     int assoc;
+    /* high_dyn: d_carr_ph_history / d_code_ph_history, boost::circular_buffer of
+       capacity 2*smoother_length (:554-563), element [k] counted from the oldest */
+    double hc_step[64], hc_samples[64], hk_step[64], hk_samples[64];
+    int hc_n, hc_head, hk_n, hk_head;
 } orc_trk;
 
 /* Dll_Pll_Conf defaults (dll_pll_conf.h:38-84, dll_pll_conf.cc:25-35 with the
@@ -534,13 +538,14 @@ void orc_trk_conf_default(gsdr_trk_conf* c)
     c->carrier_aiding = 1;
     c->high_dyn = 0;
     c->track_pilot = 1;
+    c->smoother_length = 10;
 }
 
 /* constructor (dll_pll_veml_tracking.cc:85-560) and the signal table (:170-430) */
 orc_trk* orc_trk_create(const gsdr_trk_conf* conf)
 {
     if (conf->signal < GSDR_SIGNAL_GPS_1C || conf->signal > GSDR_SIGNAL_BDS_B1 || conf->extend_correlation_symbols < 1 ||
-        conf->high_dyn || conf->cn0_samples > MAX_CN0_SAMPLES || conf->cn0_samples < 1)
+        (conf->high_dyn && conf->smoother_length > 32) || conf->cn0_samples > MAX_CN0_SAMPLES || conf->cn0_samples < 1)
         return NULL;
     orc_trk* t = (orc_trk*)calloc(1, sizeof(orc_trk));
     if (!t) return NULL;
@@ -658,6 +663,7 @@ static void clear_tracking_vars(orc_trk* t)
     t->circ_head = 0;
     t->carrier_phase_rate_step_rad = 0.0;
     t->code_phase_rate_step_chips = 0.0;
+    t->hc_n = t->hc_head = t->hk_n = t->hk_head = 0;
 }
 
 /* start_tracking (:640-882) + the state-1 pull-in call (:1813-1844) at nitems_read */
@@ -700,6 +706,7 @@ int orc_trk_start(orc_trk* t, uint32_t prn, const float* code, int code_samples,
     t->carrier_doppler_hz = t->acq_carrier_doppler_hz;
     t->carrier_phase_step_rad = TWO_PI_REF * t->carrier_doppler_hz / t->p.fs_in;
     t->carrier_phase_rate_step_rad = 0.0;
+    t->hc_n = t->hc_head = t->hk_n = t->hk_head = 0; /* :651-652 */
     for (int k = 0; k < t->n_taps; ++k) t->taps[k] = (tcf){0.0F, 0.0F};
     t->carrier_lock_fail_counter = 0;
     t->code_lock_fail_counter = 0;
@@ -771,7 +778,7 @@ static void do_correlation_step(orc_trk* t, const float* in)
         t->rem_carr_phase_rad, (float)t->carrier_phase_step_rad, (float)t->carrier_phase_rate_step_rad,
         (float)t->rem_code_phase_chips * (float)t->code_samples_per_chip,
         (float)t->code_phase_step_chips * (float)t->code_samples_per_chip,
-        (float)t->code_phase_rate_step_chips * (float)t->code_samples_per_chip, t->p.vector_length, 0, t->assoc);
+        (float)t->code_phase_rate_step_chips * (float)t->code_samples_per_chip, t->p.vector_length, t->p.high_dyn, t->assoc);
     for (int k = 0; k < t->n_taps; ++k) t->taps[k] = (tcf){out[2 * k], out[2 * k + 1]};
     if (t->track_pilot)
         {
@@ -781,7 +788,7 @@ static void do_correlation_step(orc_trk* t, const float* in)
                 t->rem_carr_phase_rad, (float)t->carrier_phase_step_rad, (float)t->carrier_phase_rate_step_rad,
                 (float)t->rem_code_phase_chips * (float)t->code_samples_per_chip,
                 (float)t->code_phase_step_chips * (float)t->code_samples_per_chip,
-                (float)t->code_phase_rate_step_chips * (float)t->code_samples_per_chip, t->p.vector_length, 0, t->assoc);
+                (float)t->code_phase_rate_step_chips * (float)t->code_samples_per_chip, t->p.vector_length, t->p.high_dyn, t->assoc);
             t->prompt_data = (tcf){dout[0], dout[1]};
         }
 }
@@ -870,20 +877,67 @@ static void run_dll_pll(orc_trk* t)
     if (t->p.carrier_aiding) t->code_freq_chips += t->carrier_doppler_hz * t->code_chip_rate / t->signal_carrier_freq;
 }
 
-/* update_tracking_vars (:1216-1287), high_dyn = false */
+/* boost::circular_buffer::push_back (overwrites the oldest element when full) */
+static void hist_push(double* v, double* s, int* n, int* head, int cap, double a, double b)
+{
+    int slot;
+    if (*n < cap)
+        {
+            slot = (*head + *n) % cap;
+            (*n)++;
+        }
+    else
+        {
+            slot = *head;
+            *head = (*head + 1) % cap;
+        }
+    v[slot] = a;
+    s[slot] = b;
+}
+
+/* the rate estimate of :1238-1250 / :1271-1283 */
+static double hist_rate(const double* v, const double* s, int head, int cap, int L)
+{
+    double tmp_cp1 = 0.0, tmp_cp2 = 0.0, tmp_samples = 0.0;
+    for (int k = 0; k < L; k++)
+        {
+            tmp_cp1 += v[(head + k) % cap];
+            tmp_cp2 += v[(head + L * 2 - k - 1) % cap];
+            tmp_samples += s[(head + L * 2 - k - 1) % cap];
+        }
+    tmp_cp1 /= (double)L;
+    tmp_cp2 /= (double)L;
+    return (tmp_cp2 - tmp_cp1) / tmp_samples;
+}
+
+/* update_tracking_vars (:1216-1287) */
 static void update_tracking_vars(orc_trk* t)
 {
+    const int L = t->p.smoother_length < 1 ? 1 : (int)t->p.smoother_length; /* dll_pll_conf.cc:119-123 */
+    const int cap = 2 * L;
     t->T_chip_seconds = 1.0 / t->code_freq_chips;
     t->T_prn_seconds = t->T_chip_seconds * (double)t->code_length_chips;
     t->T_prn_samples = t->T_prn_seconds * t->p.fs_in;
     t->K_blk_samples = t->T_prn_samples + t->rem_code_phase_samples;
     t->current_prn_length_samples = (int32_t)floor(t->K_blk_samples);
     t->carrier_phase_step_rad = TWO_PI_REF * t->carrier_doppler_hz / t->p.fs_in;
+    if (t->p.high_dyn)
+        {
+            hist_push(t->hc_step, t->hc_samples, &t->hc_n, &t->hc_head, cap, t->carrier_phase_step_rad,
+                (double)t->current_prn_length_samples);
+            if (t->hc_n == cap) t->carrier_phase_rate_step_rad = hist_rate(t->hc_step, t->hc_samples, t->hc_head, cap, L);
+        }
     const double len = (double)t->current_prn_length_samples;
     t->rem_carr_phase_rad += (float)(t->carrier_phase_step_rad * len + 0.5 * t->carrier_phase_rate_step_rad * len * len);
     t->rem_carr_phase_rad = (float)fmod((double)t->rem_carr_phase_rad, TWO_PI_REF);
     t->acc_carrier_phase_rad -= (t->carrier_phase_step_rad * len + 0.5 * t->carrier_phase_rate_step_rad * len * len);
     t->code_phase_step_chips = t->code_freq_chips / t->p.fs_in;
+    if (t->p.high_dyn)
+        {
+            hist_push(t->hk_step, t->hk_samples, &t->hk_n, &t->hk_head, cap, t->code_phase_step_chips,
+                (double)t->current_prn_length_samples);
+            if (t->hk_n == cap) t->code_phase_rate_step_chips = hist_rate(t->hk_step, t->hk_samples, t->hk_head, cap, L);
+        }
     t->rem_code_phase_samples = t->K_blk_samples - len;
     t->rem_code_phase_chips = t->code_freq_chips * t->rem_code_phase_samples / t->p.fs_in;
 }
@@ -1162,6 +1216,8 @@ static int trk_call(orc_trk* t, const float* in, const float* taps_in, uint64_t 
         }
     r->data_prompt[0] = t->prompt_data.re;
     r->data_prompt[1] = t->prompt_data.im;
+    r->carrier_rate = (float)t->carrier_phase_rate_step_rad;
+    r->code_rate = (float)t->code_phase_rate_step_chips;
     if (loss_of_lock) r->flags |= GSDR_TRK_F_LOSS_OF_LOCK;
     if (t->flag_pll_180) r->flags |= GSDR_TRK_F_PLL_180;
     r->consumed = t->current_prn_length_samples;

@@ -77,6 +77,8 @@ def _replay_check(g, oracle_channel, tag):
         np.testing.assert_array_equal(g[f], o[f], err_msg="%s %s" % (tag, f))
     np.testing.assert_array_equal(g["prompt_i"], o["prompt_i"], err_msg=tag)
     np.testing.assert_array_equal(g["prompt_q"], o["prompt_q"], err_msg=tag)
+    np.testing.assert_array_equal(g["carrier_rate"], o["carrier_rate"], err_msg=tag)
+    np.testing.assert_array_equal(g["code_rate"], o["code_rate"], err_msg=tag)
     for f, tol in (("carrier_doppler_hz", 1e-2), ("code_freq_chips", 1e-4), ("rem_code_phase_samples", 1e-4),
                    ("acc_carrier_phase_rad", 1e-2), ("cn0_db_hz", 1e-3), ("carrier_lock_test", 1e-4),
                    ("evm", 1e-4)):
@@ -103,8 +105,8 @@ def _free_check(g, o, tag):
     assert np.median(dc) <= 0.02 and dc.max() <= 1.0, (tag, np.percentile(dc, [50, 95, 100]))
 
 
-def _oracle_channel(fs, code, delay, dop, nitems):
-    ch = trk.Channel(_conf(fs)[0:1].view(trk.TRK_CONF_DTYPE))
+def _oracle_channel(fs, code, delay, dop, nitems, conf=None):
+    ch = trk.Channel((_conf(fs) if conf is None else conf)[0:1].view(trk.TRK_CONF_DTYPE))
     first = ch.start(code, delay, dop, 0, nitems)
     return ch, first
 
@@ -348,3 +350,48 @@ def test_extended_integration_matches_oracle(sig):
     _free_check(g, orc, sig)
     st = set(np.unique(g["state"]).tolist())
     assert {2, 3, 4} <= st
+
+
+@pytest.mark.parametrize("smoother", [10, 3])
+def test_high_dynamics_loop_matches_oracle(smoother):
+    """high_dyn = true (dll_pll_veml_tracking.cc:527-533, :1232-1284): carrier and code
+    rate estimates from the step histories drive the high-dynamics resampler/rotator.
+    A 60 Hz/s Doppler ramp; replay (the oracle loop on the GPU's taps: histories and
+    rates bit-identical) and free-running agreement with the oracle's generic VOLK
+    high-dynamics kernels."""
+    fs = 2.0e6
+    sat = synth.Satellite(9, -1500.0, 512.2, 46.0, 0.3, preamble_every_bits=25, code_doppler=True,
+                          doppler_rate_hz_s=60.0)
+    iq = synth.gps_l1_iq(fs, int(1.6 * fs), [sat], seed_offset=8)
+    delay, dop = _acq(sat, fs)
+    code = synth.gps_ca_chips(9)
+    conf = _conf(fs)
+    conf["high_dyn"] = 1
+    conf["smoother_length"] = smoother
+    t = gsdr.Tracking(conf)
+    first_g = t.start(0, 9, code, delay, dop, 0, 2000)
+    rec, n = t.run(iq, 0, 2000)
+    g = rec[0][:n[0]]
+    free, first_o = _oracle_channel(fs, code, delay, dop, 2000, conf)
+    assert first_g == first_o
+    _replay_check(g, _oracle_channel(fs, code, delay, dop, 2000, conf)[0], "hd%d" % smoother)
+    orc, _ = free.run(iq, 0, first_o, 2000)
+    _free_check(g, orc, "hd%d" % smoother)
+    # the loop follows the ramp: final Doppler near -1500 + 60 * t
+    t_end = float(g["sample_counter"][-1]) / fs
+    assert abs(float(g["carrier_doppler_hz"][-1]) - (-1500.0 + 60.0 * t_end)) < 10.0
+    assert g["state"][-1] == 4
+    # the rate estimates are live once the histories are full (2 * smoother_length calls)
+    assert np.all(g["carrier_rate"][:2 * smoother - 1] == 0.0)
+    assert np.count_nonzero(g["carrier_rate"]) > len(g) // 2 and np.count_nonzero(g["code_rate"]) > len(g) // 2
+    # mean carrier rate ~ the ramp: 2*pi*60/fs^2 rad/sample^2 (noisy per call)
+    want = 2 * np.pi * 60.0 / fs ** 2
+    assert abs(np.mean(g["carrier_rate"][len(g) // 2:]) - want) < 0.5 * want
+
+
+def test_high_dynamics_conf_limits():
+    conf = _conf(2.0e6)
+    conf["high_dyn"] = 1
+    conf["smoother_length"] = 33
+    with pytest.raises(gsdr.GsdrError):
+        gsdr.Tracking(conf)

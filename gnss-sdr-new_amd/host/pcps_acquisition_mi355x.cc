@@ -79,6 +79,7 @@ void pcps_acquisition_mi355x::init()
         }
     d_mag = 0.0F;
     d_input_power = 0.0F;
+    d_step_repeat = false;  // :262
     ensure_engine();
     gsdr_acq_set_doppler(d_engine, d_acq_parameters.doppler_max, d_doppler_step, d_doppler_center);
 }
@@ -118,7 +119,7 @@ void pcps_acquisition_mi355x::set_state(int32_t state)
     d_state = state;
     if (d_state == 1)
         {
-            if (d_gnss_synchro)
+            if (d_gnss_synchro && !d_step_repeat)  // :324
                 {
                     d_gnss_synchro->Acq_delay_samples = 0.0;
                     d_gnss_synchro->Acq_doppler_hz = 0.0;
@@ -155,9 +156,11 @@ void pcps_acquisition_mi355x::calculate_threshold()
         gsdr_acq_get_threshold(d_engine, &d_threshold);
 }
 
+// send_positive_acquisition (:344-386) with the fork's repeat steps (:360-368)
 void pcps_acquisition_mi355x::send_positive_acquisition()
 {
-    d_positive_acq = 1;
+    if (!d_step_repeat) d_positive_acq = 1;
+    if (d_acq_parameters.make_repeat_steps) d_step_repeat = true;
     if (d_events) d_events(1);
 }
 
@@ -201,7 +204,8 @@ void pcps_acquisition_mi355x::acquisition_core(uint64_t samp_count)
     d_mag = r.peak;
     d_input_power = r.input_power;
     d_test_statistics = r.test_statistic;
-    if (d_gnss_synchro)
+    // with make_2_steps and repeat steps only the narrow grid updates Gnss_Synchro (:697)
+    if (d_gnss_synchro && (d_step_two || !(d_acq_parameters.make_2_steps && d_step_repeat)))
         {
             if (d_acq_parameters.use_automatic_resampler)
                 {
@@ -286,13 +290,14 @@ int pcps_acquisition_mi355x::work(const void* in, int ninput_items)
                     d_state = 0;
                     d_active = true;
                 }
+            if (d_step_repeat) d_active = true;  // :944-947
             return consumed;
         }
     switch (d_state)
         {
         case 0:
             {
-                if (d_gnss_synchro)
+                if (d_gnss_synchro && !d_step_repeat)  // :956-963
                     {
                         d_gnss_synchro->Acq_delay_samples = 0.0;
                         d_gnss_synchro->Acq_doppler_hz = 0.0;

@@ -52,6 +52,7 @@ public:
     float input_power() const { return d_input_power; }
     uint32_t num_doppler_bins() const { return d_num_doppler_bins; }
     bool step_two() const { return d_step_two; }
+    bool step_repeat() const { return d_step_repeat; }
 
 private:
     void acquisition_core(uint64_t samp_count);
@@ -86,6 +87,7 @@ private:
     bool d_active{false};
     bool d_step_two{false};                // make_2_steps: the next core call is the narrow grid
     float d_doppler_center_step_two{0.0F};
+    bool d_step_repeat{false};  // fork's make_repeat_steps: keep re-acquiring after a positive
     std::mutex d_setlock;
 };
 

@@ -191,6 +191,55 @@ void test_acquisition_two_steps(const std::vector<std::complex<float>>& capture)
         gnss_synchro.Acq_doppler_hz, gnss_synchro.Acq_delay_samples, acquisition.get_block()->test_statistics());
 }
 
+// The fork's make_repeat_steps: after a positive the block re-arms itself and
+// acquires again on the next block without a new set_state(1).
+void test_acquisition_repeat_steps(const std::vector<std::complex<float>>& capture)
+{
+    InMemoryConfiguration config;
+    config.set_property("GNSS-SDR.internal_fs_sps", "4000000");
+    config.set_property("Acquisition_1C.implementation", "GPS_L1_CA_PCPS_Acquisition_MI355X");
+    config.set_property("Acquisition_1C.item_type", "gr_complex");
+    config.set_property("Acquisition_1C.coherent_integration_time_ms", "1");
+    config.set_property("Acquisition_1C.pfa", "0.01");
+    config.set_property("Acquisition_1C.doppler_max", "5000");
+    config.set_property("Acquisition_1C.doppler_step", "250");
+    config.set_property("Acquisition_1C.make_repeat_steps", "true");
+    config.set_property("Acquisition_1C.blocking_on_standby", "true");
+    Gnss_Synchro gnss_synchro{};
+    gnss_synchro.System = 'G';
+    gnss_synchro.Signal[0] = '1';
+    gnss_synchro.Signal[1] = 'C';
+    gnss_synchro.PRN = 1;
+    GpsL1CaPcpsAcquisitionMI355X acquisition(&config, "Acquisition_1C", 1, 0);
+    int positives = 0;
+    std::vector<uint64_t> stamps;
+    acquisition.get_block()->set_event_handler([&](int ev) {
+        if (ev == 1)
+            {
+                ++positives;
+                stamps.push_back(gnss_synchro.Acq_samplestamp_samples);
+            }
+    });
+    acquisition.set_gnss_synchro(&gnss_synchro);
+    acquisition.set_local_code();
+    acquisition.set_state(1);
+    acquisition.init();
+    acquisition.get_block()->start();
+    size_t pos = 0;
+    for (int guard = 0; guard < 100 && positives < 2; ++guard)
+        {
+            const int n = static_cast<int>(std::min<size_t>(1000, capture.size() - pos));
+            pos += static_cast<size_t>(acquisition.get_block()->work(capture.data() + pos, n));
+        }
+    EXPECT(positives == 2, "repeat steps: a second positive without set_state(1)");
+    EXPECT(acquisition.get_block()->step_repeat(), "d_step_repeat latched");
+    EXPECT(stamps.size() == 2 && stamps[0] == 4000ULL && stamps[1] == 8000ULL, "one positive per block");
+    EXPECT(std::abs(gnss_synchro.Acq_delay_samples - 524.0) < 1.0, "repeated acquisition keeps the code phase");
+    std::printf("repeat steps: %d positives, stamps %llu %llu\n", positives,
+        stamps.size() > 0 ? static_cast<unsigned long long>(stamps[0]) : 0ULL,
+        stamps.size() > 1 ? static_cast<unsigned long long>(stamps[1]) : 0ULL);
+}
+
 void test_multicorrelator(const std::vector<std::complex<float>>& capture)
 {
     const int n = 4000;
@@ -250,6 +299,7 @@ int main(int argc, char** argv)
         }
     test_acquisition_validation(capture);
     test_acquisition_two_steps(capture);
+    test_acquisition_repeat_steps(capture);
     test_multicorrelator(capture);
     if (failures == 0) std::printf("host_selftest: PASS\n");
     return failures == 0 ? 0 : 1;

@@ -8,12 +8,14 @@
 #include <algorithm>
 #include <cmath>
 #include <complex>
+#include <cstring>
 #include <cstdio>
 #include <fstream>
 #include <iostream>
 #include <string>
 #include <vector>
 
+#include "acquisition_service.h"
 #include "gnss_replicas.h"
 #include "gps_l1_ca_pcps_acquisition_mi355x.h"
 #include "hip_multicorrelator_real_codes.h"
@@ -240,6 +242,78 @@ void test_acquisition_repeat_steps(const std::vector<std::complex<float>>& captu
         stamps.size() > 1 ? static_cast<unsigned long long>(stamps[1]) : 0ULL);
 }
 
+// Batched acquisition service: 4 channels' requests answered by one grid per
+// block, each answer bit-identical to a one-PRN engine on the same block.
+void test_acquisition_service(const std::vector<std::complex<float>>& capture)
+{
+    InMemoryConfiguration config;
+    config.set_property("GNSS-SDR.internal_fs_sps", "4000000");
+    config.set_property("Acquisition_1C.item_type", "gr_complex");
+    config.set_property("Acquisition_1C.coherent_integration_time_ms", "1");
+    config.set_property("Acquisition_1C.pfa", "0.01");
+    config.set_property("Acquisition_1C.doppler_max", "5000");
+    config.set_property("Acquisition_1C.doppler_step", "250");
+    Acq_Conf conf;
+    conf.ms_per_code = 1;
+    conf.SetFromConfiguration(&config, "Acquisition_1C", 1023000.0, 4000000.0);
+    AcquisitionService svc(conf, 8, 0);
+    const uint32_t prns[4] = {1, 2, 11, 20};
+    std::vector<std::vector<std::complex<float>>> codes;
+    struct Answer
+    {
+        uint32_t channel;
+        gsdr_acq_result r;
+        bool positive;
+    };
+    std::vector<Answer> answers;
+    for (uint32_t ch = 0; ch < 4; ++ch)
+        {
+            codes.push_back(gps_l1_ca_code_gen_complex_sampled(prns[ch], 4000000));
+            svc.request(ch, prns[ch], codes.back().data(),
+                [&](uint32_t c, const gsdr_acq_result& r, bool pos) { answers.push_back({c, r, pos}); });
+        }
+    EXPECT(svc.pending() == 4, "four pending requests");
+    svc.work(capture.data(), 4000);
+    EXPECT(svc.grids_run() == 1 && answers.size() == 4 && svc.pending() == 0, "one grid answers every request");
+    // channel 0 re-arms, the others stay idle: the second block runs a 1-PRN grid
+    svc.request(0, 1, codes[0].data(), [&](uint32_t c, const gsdr_acq_result& r, bool pos) { answers.push_back({c, r, pos}); });
+    svc.work(capture.data() + 4000, 4000);
+    EXPECT(svc.grids_run() == 2 && answers.size() == 5, "second grid for the re-armed channel");
+    // reference: one engine per channel (the reference's one-PRN-per-block layout)
+    for (size_t i = 0; i < answers.size(); ++i)
+        {
+            const uint32_t ch = answers[i].channel;
+            const size_t blk = i < 4 ? 0 : 1;
+            gsdr_acq_conf c{};
+            c.fs_in = 4000000;
+            c.consumed_samples = 4000;
+            c.samples_per_code = conf.samples_per_code;
+            c.samples_per_chip = conf.samples_per_chip;
+            c.doppler_max = 5000;
+            c.doppler_step = 250;
+            c.pfa = 0.01F;
+            c.max_dwells = 1;
+            c.item_type = GSDR_ITEM_GR_COMPLEX;
+            c.max_prns = 1;
+            c.max_blocks = 1;
+            c.sampled_ms = 1;
+            c.ms_per_code = 1;
+            gsdr_acq* one = nullptr;
+            EXPECT(gsdr_acq_create(0, &c, &one) == GSDR_OK, "single engine");
+            gsdr_acq_set_local_codes(one, reinterpret_cast<const float*>(codes[ch].data()), &prns[ch], 1);
+            gsdr_acq_result r{};
+            gsdr_acq_run(one, capture.data() + 4000 * blk, 1, 4000 * (blk + 1), &r);
+            gsdr_acq_destroy(one);
+            EXPECT(std::memcmp(&r, &answers[i].r, sizeof(r)) == 0, "batched answer == one-PRN engine");
+        }
+    EXPECT(answers[0].channel == 0 && answers[0].positive && std::abs(answers[0].r.acq_delay_samples - 524.0) < 1.0,
+        "PRN 1 acquired at 524 samples");
+    std::printf("acquisition service: %zu answers from %llu grids; PRN 1 stat %.2f (thr %.2f), positives:", answers.size(),
+        static_cast<unsigned long long>(svc.grids_run()), answers[0].r.test_statistic, svc.threshold());
+    for (const auto& a : answers) std::printf(" %u:%d", a.r.prn, a.positive ? 1 : 0);
+    std::printf("\n");
+}
+
 void test_multicorrelator(const std::vector<std::complex<float>>& capture)
 {
     const int n = 4000;
@@ -300,6 +374,7 @@ int main(int argc, char** argv)
     test_acquisition_validation(capture);
     test_acquisition_two_steps(capture);
     test_acquisition_repeat_steps(capture);
+    test_acquisition_service(capture);
     test_multicorrelator(capture);
     if (failures == 0) std::printf("host_selftest: PASS\n");
     return failures == 0 ? 0 : 1;

@@ -10,7 +10,9 @@ One step = one batch of B consecutive 1 ms blocks of synthetic GPS L1 C/A IQ at
     4000 samples + discriminators + loop filters + NCO update + lock detectors),
     device-resident (gsdr_trk_run_device), the channel state restored to the same
     start each step so every step re-tracks the same 64 ms.
-Acquisition and tracking run on two HIP streams (they are independent work).
+Acquisition and tracking run on separate HIP streams (they are independent work):
+the acquisition blocks of a step are split over two handles (--acq-chains 2), so one
+chain's forward-spectra kernel overlaps the other's correlate grid.
 Whole-job throughput = blocks * 4000 samples * ranks / max-over-ranks wall time.
 
 Multi-GPU: one process per GPU (torch.distributed.run); every rank processes its
@@ -157,6 +159,12 @@ def main():
     ap.add_argument("--no-profile-events", action="store_true")
     ap.add_argument("--cu-partition", action="store_true",
                     help="give the tracking stream CHANNELS CUs of its own and acquisition the rest")
+    ap.add_argument("--trk-cus", type=int, default=0,
+                    help="with --cu-partition: CUs reserved for tracking (default: one per channel)")
+    ap.add_argument("--acq-chains", type=int, default=2,
+                    help="split the step's blocks over this many acquisition handles, each on its own stream "
+                         "(2: one chain's forward spectra overlap the other's correlate grid; at most 3 with the "
+                         "tracking stream, GPU_MAX_HW_QUEUES = 4)")
     ap.add_argument("--only", choices=["acq", "trk"], default=None,
                     help="diagnostic: run only one of the two stages (the line is then not the metric)")
     args = ap.parse_args()
@@ -183,8 +191,16 @@ def main():
     trk_out = torch.zeros(CHANNELS * B * gsdr.TRK_EPOCH_DTYPE.itemsize, dtype=torch.uint8, device=dev)
     trk_n = torch.zeros(CHANNELS, dtype=torch.int32, device=dev)
 
-    acq = gsdr.Acquisition(FS, N, DMAX, DSTEP, pfa=PFA, max_prns=P, max_blocks=B, num_doppler_bins=D, device=local)
-    acq.set_local_codes(codes, np.arange(1, P + 1))
+    nch = max(1, args.acq_chains)
+    assert B % nch == 0, "--blocks must be a multiple of --acq-chains"
+    Bc = B // nch
+    acqs = []
+    for _ in range(nch):
+        a = gsdr.Acquisition(FS, N, DMAX, DSTEP, pfa=PFA, max_prns=P, max_blocks=Bc, num_doppler_bins=D,
+                             device=local)
+        a.set_local_codes(codes, np.arange(1, P + 1))
+        acqs.append(a)
+    acq = acqs[0]
     trk = gsdr.Tracking(trk_conf(CHANNELS), device=local)
     from gsdr import synth
     for c, s in enumerate(sats):
@@ -195,9 +211,10 @@ def main():
     # whole CU; give it CHANNELS CUs (one per XCD for 8) and the acquisition grid
     # the other 248, so neither waits for the other's workgroups to drain.
     if args.cu_partition:
-        trk_mask, acq_mask = gsdr.cu_partition(CHANNELS)
+        trk_mask, acq_mask = gsdr.cu_partition(args.trk_cus or CHANNELS)
         trk.set_cu_mask(trk_mask)
-        acq.set_cu_mask(acq_mask)
+        for a in acqs:
+            a.set_cu_mask(acq_mask)
     trk.save_state(0)
 
     def step():
@@ -205,7 +222,9 @@ def main():
             trk.restore_state(0)
             trk.run_device(iq_dev.data_ptr(), 0, B * N, B, trk_out.data_ptr(), trk_n.data_ptr())
         if args.only != "trk":
-            acq.run_device(iq_dev.data_ptr(), B, N, 0, res_dev.data_ptr())
+            for i, a in enumerate(acqs):
+                a.run_device(iq_dev.data_ptr() + i * Bc * N * 8, Bc, N, i * Bc * N,
+                             res_dev.data_ptr() + i * Bc * P * gsdr.ACQ_RESULT_DTYPE.itemsize)
 
     for _ in range(args.warmup):
         step()
@@ -225,9 +244,10 @@ def main():
                         for c in range(CHANNELS)]) if nrec.min() > 0 else None
 
     if not args.no_profile_events:
-        acq.set_profiling(True)
+        for a in acqs:
+            a.set_profiling(True)
+            a.read_profile()
         trk.set_profiling(True)
-        acq.read_profile()
         trk.read_profile()
     if dist is not None:
         dist.barrier()
@@ -247,7 +267,10 @@ def main():
     stage_ms, stage_n = (np.zeros(4), np.zeros(4, np.uint32))
     trk_ms, trk_launches = 0.0, 0
     if not args.no_profile_events:
-        stage_ms, stage_n = acq.read_profile()
+        for a in acqs:
+            ms_a, n_a = a.read_profile()
+            stage_ms = stage_ms + ms_a
+            stage_n = stage_n + n_a
         trk_ms, trk_launches = trk.read_profile()
 
     samples = world * args.steps * B * N
@@ -273,7 +296,9 @@ def main():
                         "over the same span",
             "blocks_per_step": B, "fs_sps": FS, "fft_size": N, "prns": P, "doppler_bins": D, "channels": CHANNELS,
             "taps": TAPS, "item_type": "gr_complex", "parallelism": "blocks sharded per rank (dp%d)" % world,
-            "cu_partition": {"tracking": CHANNELS, "acquisition": 256 - CHANNELS} if args.cu_partition else None,
+            "cu_partition": ({"tracking": args.trk_cus or CHANNELS, "acquisition": 256 - (args.trk_cus or CHANNELS)}
+                             if args.cu_partition else None),
+            "acq_chains": nch,
         },
         "real_time_factor": round(value * 1e6 / FS, 2),
     }
@@ -313,7 +338,8 @@ def main():
     if rank == 0:
         print(json.dumps(line), flush=True)
     trk.close()
-    acq.close()
+    for a in acqs:
+        a.close()
     if dist is not None:
         dist.destroy_process_group()
 

@@ -309,16 +309,19 @@ def main():
         # stage_n / steps launches of each stage, each over B * steps / stage_n blocks
         corr_launch_s = stage_ms[1] / stage_n[1] / 1e3
         blocks_per_launch = B * args.steps / stage_n[1]
-        achieved = correlate_kernel_bytes_per_block() * blocks_per_launch / corr_launch_s
+        # the nch chains' correlate launches run concurrently (one per stream, same
+        # duration): the chip's correlate throughput is nch launches per launch time
+        achieved = correlate_kernel_bytes_per_block() * blocks_per_launch * nch / corr_launch_s
         pmc = load_pmc_traffic()
         traffic = None
-        if pmc and pmc.get("kernel") == "acq_correlate_kernel" and pmc.get("blocks") == blocks_per_launch:
-            traffic = pmc.get("hbm_bytes_per_launch")
+        if pmc and pmc.get("kernel") == "acq_correlate_kernel" and pmc.get("blocks"):
+            # PMC HBM bytes of one launch over pmc["blocks"] blocks, per block x this launch's blocks
+            traffic = pmc.get("hbm_bytes_per_launch") / pmc["blocks"] * blocks_per_launch
         line["roofline"] = {
             "bound": "hbm", "achieved": round(achieved / 1e9, 2), "peak": HBM_PEAK / 1e9, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK, 4), "traffic": traffic,
             "kernel": "acq_correlate_kernel", "avg_launch_us": round(corr_launch_s * 1e6, 2),
-            "blocks_per_launch": blocks_per_launch,
+            "blocks_per_launch": blocks_per_launch, "concurrent_launches": nch,
             "algorithmic_bytes_per_launch": int(correlate_kernel_bytes_per_block() * blocks_per_launch),
         }
         line["stages_us_per_launch"] = {

@@ -1437,7 +1437,12 @@ constexpr size_t kStaticLdsMargin = 4 * 1024;  // the kernel's static __shared__
 size_t lds_for(int code_pad, int data_pad)
 {
     const size_t need = (size_t)(code_pad + data_pad) * sizeof(float) + (size_t)(kWinCore + kHalo) * sizeof(float2);
-    return std::max(need, kCuLds - kStaticLdsMargin);
+    // LDS reserved per channel workgroup: by default the whole CU, so no acquisition
+    // workgroup shares its issue slots once it runs; GSDR_TRK_LDS_KB trades that for
+    // an earlier start on a busy chip (a full-CU workgroup waits for an empty CU).
+    size_t reserve = kCuLds - kStaticLdsMargin;
+    if (const char* e = std::getenv("GSDR_TRK_LDS_KB")) reserve = std::min(reserve, (size_t)std::atoi(e) * 1024);
+    return std::max(need, reserve);
 }
 
 int launch(gsdr_trk* k, const void* iq, uint64_t iq_first, uint64_t iq_items, uint32_t max_epochs, gsdr_trk_epoch* out,

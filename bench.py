@@ -79,9 +79,15 @@ def trk_conf(nch):
     return c
 
 
-def make_workload(blocks, rank):
+def make_workload(blocks, rank, periodic=False):
     from gsdr import synth
     sats = synth.random_constellation(CHANNELS, seed_offset=100 + rank)
+    if periodic:
+        # a whole number of carrier cycles per batch: the batch repeated end to end
+        # is a continuous signal (the code has 1 ms period and no code Doppler here)
+        span = blocks * N / FS
+        for s in sats:
+            s.doppler_hz = round(s.doppler_hz * span) / span
     iq = synth.gps_l1_iq(FS, blocks * N, sats, seed_offset=100 + rank)
     codes = np.stack([synth.gps_ca_sampled(p, FS) for p in range(1, P + 1)])
     return sats, iq, codes
@@ -165,6 +171,9 @@ def main():
                     help="split the step's blocks over this many acquisition handles, each on its own stream "
                          "(2: one chain's forward spectra overlap the other's correlate grid; at most 3 with the "
                          "tracking stream, GPU_MAX_HW_QUEUES = 4)")
+    ap.add_argument("--trk-stream", action="store_true",
+                    help="tracking follows one continuous stream (the batch repeated, Dopplers on whole cycles per "
+                         "batch): one tracking launch covers all timed steps instead of one launch per step")
     ap.add_argument("--only", choices=["acq", "trk"], default=None,
                     help="diagnostic: run only one of the two stages (the line is then not the metric)")
     args = ap.parse_args()
@@ -185,10 +194,18 @@ def main():
     dev = torch.device("cuda", local)
     B = args.blocks
 
-    sats, iq, codes = make_workload(B, rank)
+    sats, iq, codes = make_workload(B, rank, periodic=args.trk_stream)
     iq_dev = torch.from_numpy(iq.view(np.float32).copy()).to(dev)
     res_dev = torch.zeros(B * P * gsdr.ACQ_RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
-    trk_out = torch.zeros(CHANNELS * B * gsdr.TRK_EPOCH_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    W, K = args.warmup, args.steps
+    if args.trk_stream:
+        # the tracking stream: warmup + timed batches end to end
+        iq_long = iq_dev.repeat(W + K + 1)  # + one batch of slack for the last calls
+        trk_epochs = max(W, K) * B
+    else:
+        iq_long = iq_dev
+        trk_epochs = B
+    trk_out = torch.zeros(CHANNELS * trk_epochs * gsdr.TRK_EPOCH_DTYPE.itemsize, dtype=torch.uint8, device=dev)
     trk_n = torch.zeros(CHANNELS, dtype=torch.int32, device=dev)
 
     nch = max(1, args.acq_chains)
@@ -217,8 +234,13 @@ def main():
             a.set_cu_mask(acq_mask)
     trk.save_state(0)
 
+    def trk_stream_launch(nsteps):
+        # one launch: nsteps * B general_work calls per channel, continuing the stream
+        if args.only != "acq" and nsteps > 0:
+            trk.run_device(iq_long.data_ptr(), 0, (W + K + 1) * B * N, nsteps * B, trk_out.data_ptr(), trk_n.data_ptr())
+
     def step():
-        if args.only != "acq":
+        if args.only != "acq" and not args.trk_stream:
             trk.restore_state(0)
             trk.run_device(iq_dev.data_ptr(), 0, B * N, B, trk_out.data_ptr(), trk_n.data_ptr())
         if args.only != "trk":
@@ -226,6 +248,8 @@ def main():
                 a.run_device(iq_dev.data_ptr() + i * Bc * N * 8, Bc, N, i * Bc * N,
                              res_dev.data_ptr() + i * Bc * P * gsdr.ACQ_RESULT_DTYPE.itemsize)
 
+    if args.trk_stream:
+        trk_stream_launch(W)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
@@ -233,7 +257,8 @@ def main():
     res = res_dev.cpu().numpy().view(gsdr.ACQ_RESULT_DTYPE).reshape(B, P)
     det = {int(r["prn"]) for r in res[0] if r["positive"]}
     vis = {s.prn for s in sats}
-    recs = trk_out.cpu().numpy().view(gsdr.TRK_EPOCH_DTYPE).reshape(CHANNELS, B)
+    ep_warm = max(W * B, 1) if args.trk_stream else B  # the warmup launch's max_epochs (record layout)
+    recs = trk_out.cpu().numpy().view(gsdr.TRK_EPOCH_DTYPE)[:CHANNELS * ep_warm].reshape(CHANNELS, ep_warm)
     nrec = trk_n.cpu().numpy()
     taps = np.stack([recs[c][nrec[c] - 1]["taps"][:6].view(np.complex64) for c in range(CHANNELS)])
     prompt_ratio = float(np.median(np.abs(taps[:, 1]) / np.maximum(np.abs(taps[:, 0]), 1e-9)))
@@ -253,6 +278,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    if args.trk_stream:
+        trk_stream_launch(K)
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize(dev)
@@ -264,6 +291,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    trk_calls_timed = int(trk_n.cpu().numpy().min())
     stage_ms, stage_n = (np.zeros(4), np.zeros(4, np.uint32))
     trk_ms, trk_launches = 0.0, 0
     if not args.no_profile_events:
@@ -296,6 +324,8 @@ def main():
                         "over the same span",
             "blocks_per_step": B, "fs_sps": FS, "fft_size": N, "prns": P, "doppler_bins": D, "channels": CHANNELS,
             "taps": TAPS, "item_type": "gr_complex", "parallelism": "blocks sharded per rank (dp%d)" % world,
+            "tracking": ("one continuous stream, one launch per timed region" if args.trk_stream
+                         else "64 ms re-tracked per step from a saved state, one launch per step"),
             "cu_partition": ({"tracking": args.trk_cus or CHANNELS, "acquisition": 256 - (args.trk_cus or CHANNELS)}
                              if args.cu_partition else None),
             "acq_chains": nch,
@@ -329,11 +359,13 @@ def main():
             "acq_correlate": round(stage_ms[1] / max(stage_n[1], 1) * 1e3, 2),
             "acq_reduce": round(stage_ms[2] / max(stage_n[2], 1) * 1e3, 2),
             "trk_loop_all_epochs": round(trk_ms / max(trk_launches, 1) * 1e3, 2),
+            "trk_launch_covers_steps": K if args.trk_stream else 1,
             "acq_launches_per_step": round(stage_n[1] / args.steps, 2),
         }
     line["acq_roof_frac_whole_step"] = round(acq_bytes_per_block() * B / (ms_per_step / 1e3) / HBM_PEAK, 4)
     line["check"] = {"visible": len(vis), "acquired_block0": len(vis & det),
                      "median_prompt_over_early": round(prompt_ratio, 2), "trk_calls_per_channel": int(nrec.min()),
+                     "trk_calls_per_channel_timed": trk_calls_timed,
                      "median_mean16_doppler_err_hz": None if dop_err is None else round(float(np.median(dop_err)), 2),
                      "channels_within_25hz": None if dop_err is None else int(np.sum(dop_err < 25.0))}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

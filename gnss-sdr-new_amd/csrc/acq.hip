@@ -269,7 +269,7 @@ void gsdr_acq_destroy(gsdr_acq* a)
         }
     for (hipEvent_t e : a->prof_pool) (void)hipEventDestroy(e);
     void* bufs[] = {a->st2.d_wipe, a->st2.d_freq, a->d_tw, a->d_wipe, a->d_code_fft, a->d_code_stage, a->d_prn, a->d_X, a->d_stats, a->d_res,
-        a->d_iq, a->d_grid, a->d_tw_sub, a->d_scratch, a->d_slots, a->d_resk, a->d_acc, a->d_acc_slots};
+        a->d_iq, a->d_grid, a->d_dgrid, a->d_tw_sub, a->d_scratch, a->d_slots, a->d_resk, a->d_acc, a->d_acc_slots};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     if (a->stream) (void)hipStreamDestroy(a->stream);
@@ -360,6 +360,27 @@ int gsdr_acq_run(gsdr_acq* a, const void* iq_host, uint32_t nblocks, uint64_t st
     int rc = dispatch(a, 0, a->d_iq, nblocks, a->consumed, stamp0, a->d_res, a->stream, 0);
     if (rc != GSDR_OK) return rc;
     GSDR_HIP(hipMemcpyAsync(out, a->d_res, (size_t)nblocks * a->nprn * sizeof(gsdr_acq_result), hipMemcpyDeviceToHost,
+        a->stream));
+    GSDR_HIP(hipStreamSynchronize(a->stream));
+    return GSDR_OK;
+}
+
+int gsdr_acq_run_dwell(gsdr_acq* a, const void* iq_host, uint32_t dwell, uint64_t stamp, gsdr_acq_result* out)
+{
+    GSDR_REQUIRE(a && iq_host && out, GSDR_E_ARG, "gsdr_acq_run_dwell: null argument");
+    GSDR_REQUIRE(a->nprn > 0, GSDR_E_STATE, "gsdr_acq_run_dwell: set_local_codes first");
+    GSDR_REQUIRE(dwell < a->conf.max_dwells, GSDR_E_ARG, "gsdr_acq_run_dwell: dwell %u outside [0,%u)", dwell,
+        a->conf.max_dwells);
+    GSDR_REQUIRE(!a->st2.active, GSDR_E_STATE, "gsdr_acq_run_dwell: step two in progress");
+    std::lock_guard<std::mutex> lk(a->mu);
+    gsdr::DeviceGuard g(a->device);
+    if (!a->d_dgrid)
+        GSDR_HIP(hipMalloc(&a->d_dgrid, (size_t)a->conf.max_prns * a->D * a->eff * sizeof(float)));
+    GSDR_HIP(hipMemcpyAsync(a->d_iq, iq_host, (size_t)a->consumed * item_bytes(a->conf.item_type),
+        hipMemcpyHostToDevice, a->stream));
+    int rc = dispatch(a, 5, nullptr, 1, a->consumed, stamp, a->d_res, a->stream, dwell);
+    if (rc != GSDR_OK) return rc;
+    GSDR_HIP(hipMemcpyAsync(out, a->d_res, (size_t)a->nprn * sizeof(gsdr_acq_result), hipMemcpyDeviceToHost,
         a->stream));
     GSDR_HIP(hipStreamSynchronize(a->stream));
     return GSDR_OK;

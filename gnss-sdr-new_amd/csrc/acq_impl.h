@@ -73,6 +73,7 @@ struct AcqParams
     float step2;          // Acq_Conf::doppler_step2
     float half2;          // static_cast<float>(floor(num_doppler_bins_step2 / 2.0))
     float ip2;            // d_input_power of the coarse step (not recomputed in step two, :530-540)
+    uint32_t counter;     // d_num_noncoherent_integrations_counter of the statistic (CFAR divisor, :534)
 };
 
 // Acq_doppler_hz of Doppler row d: first step int32 arithmetic (:537); step two
@@ -300,7 +301,14 @@ __global__ void __launch_bounds__(PT::NT) acq_correlate_kernel(const float2* __r
 // values are fetched by the hook while the current transform runs.  The last
 // stage visits each lane's outputs in increasing index order, so a strict '>'
 // keeps the lane's first maximum (the reference's index_max semantics).
-template <class MP, int PG, int WPE>
+//
+// STAT 0: row (max, first argmax, sum) with the slot-keyed maximum below.
+// STAT 1: row (exact max, sum) only -- an order-free reduction, 2.5 VALU per output
+//         instead of 7 -- and acq_argmax_pk_kernel recomputes the one row per
+//         (b, p) that the grid maximum selects to find its first maximum; the
+//         reported peak is then the exact |R|^2, with the reference's first-index
+//         rule (32f_index_max_32u) among exact ties.
+template <class MP, int PG, int WPE, int STAT>
 __global__ void __launch_bounds__(MP::NT) __attribute__((amdgpu_waves_per_eu(WPE))) acq_correlate_pk_kernel(const float2* __restrict__ X,
     const float2* __restrict__ code_fft, RowStat* __restrict__ stats, const float2* __restrict__ tw, uint32_t D,
     uint32_t P, uint32_t nblocks)
@@ -354,6 +362,55 @@ __global__ void __launch_bounds__(MP::NT) __attribute__((amdgpu_waves_per_eu(WPE
     }
     for (int q = 0; q < np; ++q)
         {
+            if constexpr (STAT == 1)
+                {
+                    float rmax = 0.0f, sum = 0.0f;
+                    auto load = [&](int bb, int r, int) -> c2 { return gsdr::pk::conj_mul(xr[bb][r], cr[bb][r]); };
+                    auto hook = [&]() {
+                        if (q + 1 < np)
+                            {
+                                const c2* c = reinterpret_cast<const c2*>(code_fft) + (size_t)(p0 + q + 1) * N;
+#pragma unroll
+                                for (int bb = 0; bb < BPT1; ++bb)
+                                    {
+                                        const int j = (int)threadIdx.x + bb * NT;
+                                        if (NB1 % NT == 0 || j < NB1)
+                                            {
+#pragma unroll
+                                                for (int r = 0; r < R1; ++r) cr[bb][r] = c[j + r * NB1];
+                                            }
+                                    }
+                            }
+                    };
+                    auto store = [&](int, c2 v, int) {
+                        const float m = __builtin_fmaf(v.x, v.x, v.y * v.y);
+                        rmax = __builtin_fmaxf(rmax, m);
+                        sum += m;
+                    };
+                    MP::template run<false>(lds, tw, load, store, hook);
+#pragma unroll
+                    for (int off = 32; off > 0; off >>= 1)
+                        {
+                            rmax = __builtin_fmaxf(rmax, __shfl_xor(rmax, off));
+                            sum += __shfl_xor(sum, off);
+                        }
+                    RowStat* sc = scratch + (q & 1) * NW;
+                    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+                    if (lane == 0) sc[wave] = RowStat{rmax, 0u, sum, 0};
+                    __syncthreads();
+                    if (threadIdx.x == 0)
+                        {
+                            RowStat best = sc[0];
+#pragma unroll
+                            for (int w = 1; w < NW; ++w)
+                                {
+                                    best.max = __builtin_fmaxf(best.max, sc[w].max);
+                                    best.sum += sc[w].sum;
+                                }
+                            stats[((size_t)b * P + p0 + q) * D + d] = best;
+                        }
+                    continue;
+                }
             // Row statistics with a slot-keyed maximum: key = bits(|R|^2) with its 5
             // low mantissa bits replaced by (31 - slot).  Non-negative floats order
             // like their bit patterns, so one integer max per output keeps the
@@ -414,6 +471,57 @@ __global__ void __launch_bounds__(MP::NT) __attribute__((amdgpu_waves_per_eu(WPE
                         }
                     stats[((size_t)b * P + p0 + q) * D + d] = RowStat{best.max, best.idx, best.sum, 0};
                 }
+        }
+}
+
+// ---------------------------------------------------------------- K_argmax (packed f32)
+// After acq_reduce_kernel chose the grid maximum's Doppler row d* of (b, p) from
+// STAT-1 row maxima: recompute that row with the same packed plan and load
+// functor (bit-identical values) and find its first maximum with a 64-bit key
+// (|R|^2 bits, ~index) -- volk_gnsssdr_32f_index_max_32u's strict '>' scan
+// (KERN/32f_index_max_32u.h:446-467) -- then write code_phase and
+// Acq_delay_samples = fmod(indext, samples_per_code) (pcps_acquisition.cc:709).
+template <class MP>
+__global__ void __launch_bounds__(MP::NT) acq_argmax_pk_kernel(const float2* __restrict__ X,
+    const float2* __restrict__ code_fft, gsdr_acq_result* __restrict__ res, const float2* __restrict__ tw, uint32_t D,
+    uint32_t P, float samples_per_code)
+{
+    using gsdr::pk::c2;
+    constexpr int NT = MP::NT;
+    constexpr int NW = NT / 64;
+    constexpr uint32_t N = MP::N;
+    extern __shared__ float2 lds_raw[];
+    c2* lds = reinterpret_cast<c2*>(lds_raw);
+    unsigned long long* scratch = reinterpret_cast<unsigned long long*>(lds_raw + N);
+    const uint32_t bp = blockIdx.x;
+    const uint32_t b = bp / P, p = bp - b * P;
+    const uint32_t d = res[bp].doppler_index;
+    if (d >= D) return;  // uniform: no maximum found (an all-NaN grid)
+    const c2* x = reinterpret_cast<const c2*>(X) + ((size_t)b * D + d) * N;
+    const c2* c = reinterpret_cast<const c2*>(code_fft) + (size_t)p * N;
+    unsigned long long key = 0ull;
+    auto load = [&](int, int, int i) -> c2 { return gsdr::pk::conj_mul(x[i], c[i]); };
+    auto store = [&](int i, c2 v, int) {
+        const float m = __builtin_fmaf(v.x, v.x, v.y * v.y);
+        const unsigned long long k = ((unsigned long long)__float_as_uint(m) << 32) | (0xffffffffu - (uint32_t)i);
+        key = k > key ? k : key;
+    };
+    MP::template run<false>(lds, tw, load, store, [] {});
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1)
+        {
+            const unsigned long long o = __shfl_xor(key, off);
+            key = o > key ? o : key;
+        }
+    if ((threadIdx.x & 63) == 0) scratch[threadIdx.x >> 6] = key;
+    __syncthreads();
+    if (threadIdx.x == 0)
+        {
+#pragma unroll
+            for (int w = 1; w < NW; ++w) key = scratch[w] > key ? scratch[w] : key;
+            const uint32_t idx = 0xffffffffu - (uint32_t)(key & 0xffffffffu);
+            res[bp].code_phase = idx;
+            res[bp].acq_delay_samples = (double)fmodf((float)idx, samples_per_code);
         }
 }
 
@@ -664,6 +772,91 @@ __global__ void acq_decide_kernel(const gsdr_acq_result* __restrict__ resk, gsdr
     res[bp] = resk[(size_t)bp * K + k];
 }
 
+// ---------------------------------------------------------------- dwell per call (gsdr_acq_run_dwell)
+// acquisition_core's own dwell loop: one call per general_work block, the |R|^2
+// grid kept across calls (pcps_acquisition.cc:637-680: the first dwell writes
+// d_magnitude_grid, later dwells add into it with volk_32f_x2_add_32f) in a
+// device-resident grid[p][d][eff]; the statistic of the accumulated grid after
+// every call (:689-696) with the dwell counter as the CFAR divisor (:534).
+// One workgroup per (d, p) of one block.
+template <class PT>
+__global__ void __launch_bounds__(PT::NT) acq_dwell_grid_kernel(const float2* __restrict__ X,
+    const float2* __restrict__ code_fft, RowStat* __restrict__ stats, const float2* __restrict__ tw,
+    typename PT::PlanT plan, AcqParams ap, float* __restrict__ grid, uint32_t dwell)
+{
+    extern __shared__ float2 lds[];
+    RowStat* scratch = reinterpret_cast<RowStat*>(lds + gsdr::fft::lds_elems_dev(plan));
+    const uint32_t N = plan.n;
+    const uint32_t d = blockIdx.x / ap.P, p = blockIdx.x - d * ap.P;
+    float* row = grid + ((size_t)p * ap.D + d) * ap.eff;
+    const float2* x = X + (size_t)d * N;
+    const float2* c = code_fft + (size_t)p * N;
+    float best = -1.0f, sum = 0.0f;
+    uint32_t bidx = 0xffffffffu;
+    auto load = [&](int i) -> float2 {
+        float2 a = x[i], q = c[i];
+        return make_float2(a.x * q.x + a.y * q.y, a.x * q.y - a.y * q.x);
+    };
+    auto store = [&](int i, float2 v) {
+        const int j = i - (int)ap.out_off;
+        if (j < 0) return;
+        float m = v.x * v.x + v.y * v.y;
+        if (dwell > 0) m = row[j] + m;
+        row[j] = m;
+        if (stat_better(m, (uint32_t)j, best, bidx))
+            {
+                best = m;
+                bidx = (uint32_t)j;
+            }
+        sum += m;
+    };
+    PT::run(plan, lds, tw, load, store);
+    block_reduce_stat<PT::NT>(best, bidx, sum, scratch);
+    if (threadIdx.x == 0) stats[(size_t)p * ap.D + d] = RowStat{best, bidx, sum, 0};
+}
+
+// first_vs_second_peak_statistic (:546-612) on the accumulated grid: row d* with
+// the +-samples_per_chip window zeroed (wrap at d_fft_size, :580-590), first
+// maximum of the rest.  One workgroup per PRN.
+__global__ void __launch_bounds__(256) acq_grid_second_peak_kernel(const float* __restrict__ grid,
+    gsdr_acq_result* __restrict__ res, AcqParams ap)
+{
+    __shared__ RowStat scratch[4];
+    const uint32_t p = blockIdx.x;
+    const uint32_t d = res[p].doppler_index;
+    const int32_t ti = (int32_t)res[p].code_phase;
+    const int32_t E = (int32_t)ap.N;
+    int32_t e1 = ti - (int32_t)ap.samples_per_chip;
+    int32_t e2 = ti + (int32_t)ap.samples_per_chip;
+    if (e1 < 0)
+        e1 = E + e1;
+    else if (e2 >= E)
+        e2 = e2 - E;
+    const float* row = grid + ((size_t)p * ap.D + d) * ap.eff;
+    float best = 0.0f, sum = 0.0f;
+    uint32_t bidx = 0;
+    for (uint32_t j = threadIdx.x; j < ap.eff; j += 256)
+        {
+            const int32_t jj = (int32_t)j;
+            const bool excluded = (e1 < e2) ? (jj >= e1 && jj < e2) : (jj >= e1 || jj < e2);
+            const float m = excluded ? 0.0f : row[j];
+            if (stat_better(m, j, best, bidx))
+                {
+                    best = m;
+                    bidx = j;
+                }
+        }
+    block_reduce_stat<256>(best, bidx, sum, scratch);
+    if (threadIdx.x == 0)
+        {
+            gsdr_acq_result r = res[p];
+            r.second_peak = best;
+            r.test_statistic = r.peak / best;
+            r.positive = r.test_statistic > ap.threshold ? 1 : 0;
+            res[p] = r;
+        }
+}
+
 // ---------------------------------------------------------------- K_forward (packed f32)
 // X_{b,d} = FFT(x_b .* w_d) on the packed plan (the N = 4000 path, with the packed
 // correlate variants).  Grid (B, D) with the block index fastest, as
@@ -736,13 +929,14 @@ __global__ void __launch_bounds__(64) acq_reduce_kernel(const RowStat* __restric
     r.acq_delay_samples = (double)fmodf((float)tsel, ap.samples_per_code);
     r.samplestamp = stamp0 + (uint64_t)b * block_stride;
     r.positive = 0;
-    r.num_dwells = 1;
+    r.num_dwells = (int32_t)ap.counter;
     if (ap.cfar)
         {
             const uint32_t opp = (dsel + ap.D / 2) % ap.D;
             const float acc = s[opp].sum;
             // float(accumulate) / int32 in float, then / 2.0 / counter in double (pcps_acquisition.cc:533)
-            const float ip = ap.step_two ? ap.ip2 : (float)((double)(acc / (float)(int32_t)ap.N) / 2.0 / (double)ap.dwells);
+            const float ip =
+                ap.step_two ? ap.ip2 : (float)((double)(acc / (float)(int32_t)ap.eff) / 2.0 / (double)ap.counter);
             r.input_power = ip;
             r.test_statistic = m / ip;
             r.positive = r.test_statistic > ap.threshold ? 1 : 0;
@@ -819,6 +1013,7 @@ struct gsdr_acq
     int nt{256};
     int variant{0};
     int corr_variant{0};      // 0: the generic LDS kernels; >0: a GSDR_PK_VARIANTS id (packed forward + correlate)
+    int corr_stat{0};         // the variant's row statistic (1: argmax recomputed by acq_argmax_pk_kernel)
     size_t corr_lds_bytes{0};
     Plan plan{};
     gsdr::fft::Plan4 plan4{};  // four-step plan (variants 20-22, N beyond one workgroup's LDS)
@@ -835,6 +1030,7 @@ struct gsdr_acq
     gsdr_acq_result* d_res{nullptr};
     void* d_iq{nullptr};
     float* d_grid{nullptr};
+    float* d_dgrid{nullptr};     // gsdr_acq_run_dwell: the |R|^2 grid kept across calls (max_prns x D x eff)
     float2* d_tw_sub{nullptr};   // four-step: W_N2 table
     float2* d_scratch{nullptr};  // four-step: slot rows of N complex
     uint32_t* d_slots{nullptr};  // four-step: slot occupancy bitmap
@@ -882,13 +1078,21 @@ size_t item_bytes(int it) { return it == GSDR_ITEM_CSHORT ? 4 : (it == GSDR_ITEM
 // Packed-f32 correlate (and forward) variants: (id, plan, PRNs per workgroup,
 // waves-per-EU hint).  30/35/37 are N = 4000 plans (30 the default); 60-62 the
 // other compile-time sizes (1 ms at 16 / 8 / 2 Msps).
+// Columns: (id, plan, PRNs per workgroup, waves-per-EU hint, row statistic: 0 max +
+// first argmax in the kernel, 1 max + sum with the argmax recomputed for the
+// selected row, see acq_correlate_pk_kernel).
 #define GSDR_PK_VARIANTS(X)                                              \
-    X(30, (gsdr::pk::PkPlan<256, true, 25, 16, 10>), 1, 1)              \
-    X(35, (gsdr::pk::PkPlan<256, true, 20, 20, 10>), 1, 1)              \
-    X(37, (gsdr::pk::PkPlan<512, true, 25, 16, 10>), 2, 1)              \
-    X(60, (gsdr::pk::PkPlan<1024, true, 16, 10, 10, 10>), 1, 1)         \
-    X(61, (gsdr::pk::PkPlan<512, true, 20, 20, 20>), 1, 1)              \
-    X(62, (gsdr::pk::PkPlan<256, true, 20, 10, 10>), 1, 1)
+    X(30, (gsdr::pk::PkPlan<256, true, 25, 16, 10>), 1, 1, 0)           \
+    X(31, (gsdr::pk::PkPlan<256, true, 25, 16, 10>), 1, 1, 1)           \
+    X(32, (gsdr::pk::PkPlan<256, false, 25, 16, 10>), 1, 1, 1)          \
+    X(35, (gsdr::pk::PkPlan<256, true, 20, 20, 10>), 1, 1, 0)           \
+    X(36, (gsdr::pk::PkPlan<256, true, 20, 20, 10>), 1, 1, 1)           \
+    X(37, (gsdr::pk::PkPlan<512, true, 25, 16, 10>), 2, 1, 0)           \
+    X(38, (gsdr::pk::PkPlan<256, false, 20, 20, 10>), 1, 1, 1)          \
+    X(39, (gsdr::pk::PkPlan<256, true, 25, 16, 10>), 1, 5, 1)           \
+    X(60, (gsdr::pk::PkPlan<1024, true, 16, 10, 10, 10>), 1, 1, 1)      \
+    X(61, (gsdr::pk::PkPlan<512, true, 20, 20, 20>), 1, 1, 1)           \
+    X(62, (gsdr::pk::PkPlan<256, true, 20, 10, 10>), 1, 1, 1)
 
 template <class PT>
 int set_lds_attrs(size_t bytes)
@@ -911,6 +1115,8 @@ int set_lds_attrs(size_t bytes)
         hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
     GSDR_HIP(hipFuncSetAttribute((const void*)acq_second_peak_dwell_kernel<PT>,
         hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+    GSDR_HIP(hipFuncSetAttribute((const void*)acq_dwell_grid_kernel<PT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (int)bytes));
     return GSDR_OK;
 }
 
@@ -932,6 +1138,7 @@ AcqParams params_of(const gsdr_acq* a)
     ap.cfar = a->conf.pfa > 0.0f ? 1 : 0;
     ap.eff = a->eff;
     ap.out_off = a->N - a->eff;
+    ap.counter = a->K;
     if (a->st2.active)
         {
             ap.step_two = 1;
@@ -1020,6 +1227,7 @@ struct StageTimer
 namespace gsdr_acq_impl
 {
 int launch_corr_variant(gsdr_acq* a, uint32_t nblocks, hipStream_t s);
+int launch_argmax_variant(gsdr_acq* a, uint32_t nblocks, gsdr_acq_result* res, hipStream_t s);
 int launch_forward_pk(gsdr_acq* a, const void* iq, int item_type, uint32_t nblocks, uint64_t stride, hipStream_t s);
 int setup_corr_variant(gsdr_acq* a, int v);
 int dispatch_static(gsdr_acq* a, int op, const void* iq, uint32_t nblocks, uint64_t stride, uint64_t stamp0,
@@ -1131,6 +1339,11 @@ int launch_all(gsdr_acq* a, const void* iq, int item_type, uint32_t nblocks, uin
     hipLaunchKernelGGL(acq_reduce_kernel, dim3(nblocks * a->nprn), dim3(64), 0, s, a->d_stats, res, a->d_prn, ap,
         stamp0, stride);
     GSDR_HIP(hipGetLastError());
+    if (a->corr_variant > 0 && a->corr_stat == 1)
+        {
+            int rc = gsdr_acq_impl::launch_argmax_variant(a, nblocks, res, s);
+            if (rc != GSDR_OK) return rc;
+        }
     t.end(2);
     if (!ap.cfar)
         {
@@ -1139,6 +1352,30 @@ int launch_all(gsdr_acq* a, const void* iq, int item_type, uint32_t nblocks, uin
                 a->d_code_fft, res, a->d_tw, plan_of<PT>(a), ap);
             GSDR_HIP(hipGetLastError());
             t.end(3);
+        }
+    return GSDR_OK;
+}
+
+// gsdr_acq_run_dwell: forward spectra of the block at a->d_iq, the accumulating
+// grid kernel, the statistic with counter dwell+1 and (peak ratio) the second
+// peak on the accumulated row.
+template <class PT>
+int launch_dwell(gsdr_acq* a, uint32_t dwell, uint64_t stamp, gsdr_acq_result* res, hipStream_t s)
+{
+    launch_forward<PT>(a, a->d_iq, a->conf.item_type, 1, a->consumed, s);
+    GSDR_HIP(hipGetLastError());
+    AcqParams ap = params_of(a);
+    ap.counter = dwell + 1;
+    hipLaunchKernelGGL((acq_dwell_grid_kernel<PT>), dim3(a->D * a->nprn), dim3(PT::NT), a->lds_bytes, s, a->d_X,
+        a->d_code_fft, a->d_stats, a->d_tw, plan_of<PT>(a), ap, a->d_dgrid, dwell);
+    GSDR_HIP(hipGetLastError());
+    hipLaunchKernelGGL(acq_reduce_kernel, dim3(a->nprn), dim3(64), 0, s, a->d_stats, res, a->d_prn, ap, stamp,
+        (uint64_t)a->consumed);
+    GSDR_HIP(hipGetLastError());
+    if (!ap.cfar)
+        {
+            hipLaunchKernelGGL(acq_grid_second_peak_kernel, dim3(a->nprn), dim3(256), 0, s, a->d_dgrid, res, ap);
+            GSDR_HIP(hipGetLastError());
         }
     return GSDR_OK;
 }

@@ -7,13 +7,14 @@ namespace gsdr_acq_impl
 
 int launch_corr_variant(gsdr_acq* a, uint32_t nblocks, hipStream_t s)
 {
-#define GSDR_PK_CASE(ID, MP, PG, WPE)                                                                                \
+#define GSDR_PK_CASE(ID, MP, PG, WPE, ST)                                                                       \
     case ID:                                                                                                    \
         {                                                                                                       \
             using M = GSDR_UNPAREN MP;                                                                          \
             const uint32_t groups = (a->nprn + (PG)-1) / (PG);                                                  \
-            hipLaunchKernelGGL((acq_correlate_pk_kernel<M, PG, WPE>), dim3(nblocks * a->D * groups), dim3(M::NT),   \
-                a->corr_lds_bytes, s, a->d_X, a->d_code_fft, a->d_stats, a->d_tw, a->D, a->nprn, nblocks);      \
+            hipLaunchKernelGGL((acq_correlate_pk_kernel<M, PG, WPE, ST>), dim3(nblocks * a->D * groups),         \
+                dim3(M::NT), a->corr_lds_bytes, s, a->d_X, a->d_code_fft, a->d_stats, a->d_tw, a->D, a->nprn,   \
+                nblocks);                                                                                       \
             return GSDR_OK;                                                                                     \
         }
 #define GSDR_UNPAREN(...) __VA_ARGS__
@@ -26,10 +27,33 @@ int launch_corr_variant(gsdr_acq* a, uint32_t nblocks, hipStream_t s)
 #undef GSDR_UNPAREN
 }
 
+// The STAT-1 variants' first-maximum pass over the selected rows.
+int launch_argmax_variant(gsdr_acq* a, uint32_t nblocks, gsdr_acq_result* res, hipStream_t s)
+{
+#define GSDR_PKA_CASE(ID, MP, PG, WPE, ST)                                                                      \
+    case ID:                                                                                                    \
+        {                                                                                                       \
+            using M = GSDR_UNPAREN MP;                                                                          \
+            hipLaunchKernelGGL((acq_argmax_pk_kernel<M>), dim3(nblocks * a->nprn), dim3(M::NT),                 \
+                a->corr_lds_bytes, s, a->d_X, a->d_code_fft, res, a->d_tw, a->D, a->nprn,                       \
+                a->conf.samples_per_code);                                                                      \
+            GSDR_HIP(hipGetLastError());                                                                        \
+            return GSDR_OK;                                                                                     \
+        }
+#define GSDR_UNPAREN(...) __VA_ARGS__
+    switch (a->corr_variant)
+        {
+            GSDR_PK_VARIANTS(GSDR_PKA_CASE)
+        default: gsdr::set_error("internal: bad argmax variant %d", a->corr_variant); return GSDR_E_STATE;
+        }
+#undef GSDR_PKA_CASE
+#undef GSDR_UNPAREN
+}
+
 // Forward spectra on the packed plan of the selected variant.
 int launch_forward_pk(gsdr_acq* a, const void* iq, int item_type, uint32_t nblocks, uint64_t stride, hipStream_t s)
 {
-#define GSDR_PKF_CASE(ID, MP, PG, WPE)                                                                          \
+#define GSDR_PKF_CASE(ID, MP, PG, WPE, ST)                                                                          \
     case ID:                                                                                                    \
         {                                                                                                       \
             using M = GSDR_UNPAREN MP;                                                                          \
@@ -59,12 +83,14 @@ int launch_forward_pk(gsdr_acq* a, const void* iq, int item_type, uint32_t nbloc
 int setup_corr_variant(gsdr_acq* a, int v)
 {
 
-#define GSDR_PK_SETUP(ID, MP, PG, WPE)                                                                               \
+#define GSDR_PK_SETUP(ID, MP, PG, WPE, ST)                                                                      \
     case ID:                                                                                                    \
         {                                                                                                       \
             using M = GSDR_UNPAREN MP;                                                                          \
             a->corr_lds_bytes = M::lds_bytes() + (size_t)2 * (M::NT / 64) * sizeof(RowStat);                   \
-            GSDR_HIP(hipFuncSetAttribute((const void*)acq_correlate_pk_kernel<M, PG, WPE>,                          \
+            GSDR_HIP(hipFuncSetAttribute((const void*)acq_correlate_pk_kernel<M, PG, WPE, ST>,                  \
+                hipFuncAttributeMaxDynamicSharedMemorySize, (int)a->corr_lds_bytes));                           \
+            GSDR_HIP(hipFuncSetAttribute((const void*)acq_argmax_pk_kernel<M>,                                  \
                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)a->corr_lds_bytes));                           \
             if (M::N != (int)a->N)                                                                              \
                 {                                                                                               \
@@ -78,6 +104,7 @@ int setup_corr_variant(gsdr_acq* a, int v)
             GSDR_HIP(hipFuncSetAttribute((const void*)acq_forward_pk_kernel<M, GSDR_ITEM_IBYTE>,               \
                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)M::lds_bytes()));                              \
             a->corr_variant = ID;                                                                               \
+            a->corr_stat = ST;                                                                                  \
             return GSDR_OK;                                                                                     \
         }
 #define GSDR_UNPAREN(...) __VA_ARGS__

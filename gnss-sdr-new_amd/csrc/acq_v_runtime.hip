@@ -15,6 +15,7 @@ int dispatch_runtime(gsdr_acq* a, int op, const void* iq, uint32_t nblocks, uint
             case 1: return launch_code_fft<GSDR_UNPAREN PT>(a, aux);                                     \
             case 2: return launch_dump<GSDR_UNPAREN PT>(a, false, 0);                                    \
             case 3: return launch_dump<GSDR_UNPAREN PT>(a, true, aux);                                   \
+            case 5: return launch_dwell<GSDR_UNPAREN PT>(a, aux, stamp0, res, s);                         \
             default: return set_lds_attrs<GSDR_UNPAREN PT>(a->lds_bytes);                                \
             }
 #define GSDR_UNPAREN(...) __VA_ARGS__

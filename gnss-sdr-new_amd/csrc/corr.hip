@@ -246,7 +246,7 @@ template <int IT>
 __global__ void __launch_bounds__(kCorrThreads) corr_kernel(const gsdr_corr_job* __restrict__ jobs,
     const JobAux* __restrict__ aux, const ChanDev* __restrict__ chans, const void* __restrict__ iq, int64_t iq_items,
     float2* __restrict__ out, int max_taps, int assoc, float2* __restrict__ partials, unsigned int* __restrict__ counters,
-    int max_chunks)
+    int max_chunks, int nchan)
 {
     extern __shared__ float s_code[];
     __shared__ double s_model[3];
@@ -257,6 +257,17 @@ __global__ void __launch_bounds__(kCorrThreads) corr_kernel(const gsdr_corr_job*
 
     const int jb = blockIdx.y, chunk = blockIdx.x;
     const gsdr_corr_job job = jobs[jb];
+    // device-resident job tables are not validated by the host: a job whose channel
+    // is out of range or whose length exceeds the handle's max_len (more chunks than
+    // the grid holds) gets NaN outputs from chunk 0 and never touches the arrival
+    // counter, so later launches' last-arriver detection stays intact
+    if (job.channel < 0 || job.channel >= nchan || job.n_samples < 0 ||
+        (job.n_samples + kChunk - 1) / kChunk > max_chunks)
+        {
+            if (chunk == 0 && (int)threadIdx.x < max_taps)
+                out[(size_t)jb * max_taps + threadIdx.x] = make_float2(__builtin_nanf(""), __builtin_nanf(""));
+            return;
+        }
     const ChanDev ch = chans[job.channel];
     const int K = ch.ntaps;
     const int N = job.n_samples;
@@ -546,13 +557,13 @@ int launch(gsdr_corr* c, const gsdr_corr_job* d_jobs, const JobAux* d_aux, int n
     const dim3 grid(c->max_chunks, njobs);
     if (item_type == GSDR_ITEM_GR_COMPLEX)
         hipLaunchKernelGGL((corr_kernel<GSDR_ITEM_GR_COMPLEX>), grid, dim3(kCorrThreads), lds, s, d_jobs, d_aux,
-            c->d_chans, iq, iq_items, (float2*)out, c->max_taps, c->assoc, c->d_partials, c->d_counters, c->max_chunks);
+            c->d_chans, iq, iq_items, (float2*)out, c->max_taps, c->assoc, c->d_partials, c->d_counters, c->max_chunks, c->max_channels);
     else if (item_type == GSDR_ITEM_CSHORT)
         hipLaunchKernelGGL((corr_kernel<GSDR_ITEM_CSHORT>), grid, dim3(kCorrThreads), lds, s, d_jobs, d_aux,
-            c->d_chans, iq, iq_items, (float2*)out, c->max_taps, c->assoc, c->d_partials, c->d_counters, c->max_chunks);
+            c->d_chans, iq, iq_items, (float2*)out, c->max_taps, c->assoc, c->d_partials, c->d_counters, c->max_chunks, c->max_channels);
     else
         hipLaunchKernelGGL((corr_kernel<GSDR_ITEM_IBYTE>), grid, dim3(kCorrThreads), lds, s, d_jobs, d_aux,
-            c->d_chans, iq, iq_items, (float2*)out, c->max_taps, c->assoc, c->d_partials, c->d_counters, c->max_chunks);
+            c->d_chans, iq, iq_items, (float2*)out, c->max_taps, c->assoc, c->d_partials, c->d_counters, c->max_chunks, c->max_channels);
     GSDR_HIP(hipGetLastError());
     if (c->profiling)
         {

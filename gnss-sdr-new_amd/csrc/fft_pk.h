@@ -243,7 +243,11 @@ struct Dft<25> : DftCT<5, 5>
 // One Stockham stage over an N-point LDS buffer of c2.
 //   TWP: inter-stage twiddles as powers of one table root (1 VMEM load per
 //        butterfly, R-2 extra complex multiplies); else R-1 table loads.
-template <int R, int NT, int N, int Ns, bool TWP, bool FIRST, bool LAST, class Load, class Store, class Hook>
+//   ORD: the last stage hands each lane its outputs in increasing index order (a
+//        first-maximum scan needs it); without ORD it visits butterfly by
+//        butterfly, so a partially filled pass is skipped as a whole instead of
+//        predicating every output (order-free reductions: max, sum).
+template <int R, int NT, int N, int Ns, bool TWP, bool FIRST, bool LAST, bool ORD, class Load, class Store, class Hook>
 __device__ __forceinline__ void stage(c2* lds, const float2* __restrict__ tw, Load& load, Store& store, Hook& hook)
 {
     constexpr int BPT = fft::bpt_for(R);
@@ -307,7 +311,7 @@ __device__ __forceinline__ void stage(c2* lds, const float2* __restrict__ tw, Lo
                         }
                 }
         }
-    if constexpr (LAST)
+    if constexpr (LAST && ORD)
         {
             // last stage: Ns = N/R and k = j, so output j + r*Ns; r outer, b inner
             // visits this lane's outputs in increasing index order, and the
@@ -324,16 +328,30 @@ __device__ __forceinline__ void stage(c2* lds, const float2* __restrict__ tw, Lo
                         }
                 }
         }
+    else if constexpr (LAST)
+        {
+            static_assert(!LAST || Ns * R == N, "last stage");
+#pragma unroll
+            for (int b = 0; b < BPT; ++b)
+                {
+                    const int j = (int)threadIdx.x + b * NT;
+                    if (NB % NT == 0 || j < NB)
+                        {
+#pragma unroll
+                            for (int r = 0; r < R; ++r) store(j + r * Ns, v[b][r], r * BPT + b);
+                        }
+                }
+        }
     else
         __syncthreads();
 }
 
-template <int NT, int N, int Ns, bool TWP, bool FIRST, int R, int... Rest, class Load, class Store, class Hook>
+template <int NT, int N, int Ns, bool TWP, bool FIRST, bool ORD, int R, int... Rest, class Load, class Store, class Hook>
 __device__ __forceinline__ void stages(c2* lds, const float2* __restrict__ tw, Load& load, Store& store, Hook& hook)
 {
     constexpr bool LAST = sizeof...(Rest) == 0;
-    stage<R, NT, N, Ns, TWP, FIRST, LAST>(lds, tw, load, store, hook);
-    if constexpr (!LAST) stages<NT, N, Ns * R, TWP, false, Rest...>(lds, tw, load, store, hook);
+    stage<R, NT, N, Ns, TWP, FIRST, LAST, ORD>(lds, tw, load, store, hook);
+    if constexpr (!LAST) stages<NT, N, Ns * R, TWP, false, ORD, Rest...>(lds, tw, load, store, hook);
 }
 
 // Compile-time packed plan.  load(b, r, i) -> c2 returns input element i
@@ -361,10 +379,10 @@ struct PkPlan
     {
         return (int)threadIdx.x + (slot % BPTL) * NT + (slot / BPTL) * NSL;
     }
-    template <class Load, class Store, class Hook>
+    template <bool ORD = true, class Load, class Store, class Hook>
     __device__ __forceinline__ static void run(c2* lds, const float2* __restrict__ tw, Load load, Store store, Hook hook)
     {
-        stages<NT, N, 1, TWP, true, Rs...>(lds, tw, load, store, hook);
+        stages<NT, N, 1, TWP, true, ORD, Rs...>(lds, tw, load, store, hook);
     }
 };
 

@@ -1253,6 +1253,10 @@ struct gsdr_trk
     bool profiling{false};
     std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_recs;
     std::vector<hipEvent_t> prof_pool;
+    // recorded after every launch on the stream it used: host read-modify-writes of
+    // d_chans (start / stop / get_channel) wait for it, so a launch in flight on a
+    // caller stream cannot write a stale channel back over them
+    hipEvent_t last_launch{nullptr};
     std::mutex mu;
 };
 
@@ -1491,6 +1495,7 @@ int launch(gsdr_trk* k, const void* iq, uint64_t iq_first, uint64_t iq_items, ui
             (const float* const*)k->d_codes, (const float* const*)k->d_data_codes, iq, iq_first, iq_items, max_epochs, out,
             nout, k->code_pad, k->data_pad, timing, k->timing_wall);
     GSDR_HIP(hipGetLastError());
+    GSDR_HIP(hipEventRecord(k->last_launch, s));
     if (k->profiling)
         {
             GSDR_HIP(hipEventRecord(e1, s));
@@ -1595,6 +1600,7 @@ int gsdr_trk_create(int device, const gsdr_trk_conf* conf, gsdr_trk** out)
             k->timing_wall = std::atoi(tv) == 2;
         }
     hipError_t e = hipStreamCreateWithFlags(&k->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&k->last_launch, hipEventDisableTiming);
     if (e == hipSuccess) e = hipMalloc(&k->d_consts, nch * sizeof(TrkConst));
     if (e == hipSuccess) e = hipMalloc(&k->d_chans, nch * sizeof(TrkChan));
     if (e == hipSuccess) e = hipMalloc(&k->d_snap[0], nch * sizeof(TrkChan));
@@ -1670,6 +1676,11 @@ void gsdr_trk_destroy(gsdr_trk* k)
             (void)hipEventDestroy(r.second);
         }
     for (hipEvent_t e : k->prof_pool) (void)hipEventDestroy(e);
+    if (k->last_launch)
+        {
+            (void)hipEventSynchronize(k->last_launch);
+            (void)hipEventDestroy(k->last_launch);
+        }
     for (float* p : k->code_bufs)
         if (p) (void)hipFree(p);
     for (float* p : k->data_code_bufs)
@@ -1696,6 +1707,7 @@ int gsdr_trk_start(gsdr_trk* k, int ch, uint32_t prn, const float* code, int cod
     std::lock_guard<std::mutex> lk(k->mu);
     gsdr::DeviceGuard g(k->device);
     // the device copy is authoritative between launches (the loop runs there)
+    GSDR_HIP(hipStreamWaitEvent(k->stream, k->last_launch, 0));
     GSDR_HIP(hipMemcpyAsync(&k->h_chans[ch], k->d_chans + ch, sizeof(TrkChan), hipMemcpyDeviceToHost, k->stream));
     GSDR_HIP(hipStreamSynchronize(k->stream));
     TrkConst& c = k->h_consts[ch];
@@ -1833,6 +1845,7 @@ int gsdr_trk_stop(gsdr_trk* k, int ch)
     std::lock_guard<std::mutex> lk(k->mu);
     gsdr::DeviceGuard g(k->device);
     const int32_t zero = 0;
+    GSDR_HIP(hipStreamWaitEvent(k->stream, k->last_launch, 0));
     GSDR_HIP(hipMemcpyAsync(reinterpret_cast<char*>(k->d_chans + ch) + offsetof(TrkChan, h) + offsetof(TrkHot, state),
         &zero, sizeof(zero),
         hipMemcpyHostToDevice, k->stream));
@@ -1884,6 +1897,7 @@ int gsdr_trk_get_channel(gsdr_trk* k, int ch, int32_t* state, uint64_t* next_sam
     GSDR_REQUIRE(ch >= 0 && ch < (int)k->conf.max_channels, GSDR_E_ARG, "gsdr_trk_get_channel: channel %d", ch);
     std::lock_guard<std::mutex> lk(k->mu);
     gsdr::DeviceGuard g(k->device);
+    GSDR_HIP(hipStreamWaitEvent(k->stream, k->last_launch, 0));
     GSDR_HIP(hipMemcpyAsync(&k->h_chans[ch], k->d_chans + ch, sizeof(TrkChan), hipMemcpyDeviceToHost, k->stream));
     GSDR_HIP(hipStreamSynchronize(k->stream));
     const TrkHot& t = k->h_chans[ch].h;

@@ -6,15 +6,21 @@
 
 namespace
 {
+// item_type_helpers.cc:22-58
 bool item_type_valid(const std::string& t)
 {
-    return t == "gr_complex" || t == "cshort" || t == "cbyte";
+    return t == "byte" || t == "cbyte" || t == "ibyte" || t == "short" || t == "cshort" || t == "ishort" ||
+           t == "float" || t == "gr_complex";
 }
 size_t item_type_size(const std::string& t)
 {
-    if (t == "gr_complex") return 8;
+    if (t == "byte" || t == "ibyte") return 1;
+    if (t == "cbyte") return 2;
+    if (t == "short" || t == "ishort") return 2;
     if (t == "cshort") return 4;
-    return 2;
+    if (t == "float") return 4;
+    if (t == "gr_complex") return 8;
+    return 0;
 }
 }  // namespace
 

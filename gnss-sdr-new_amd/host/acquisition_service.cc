@@ -1,5 +1,7 @@
 #include "acquisition_service.h"
 
+#include "pcps_acquisition_mi355x.h"
+
 #include <algorithm>
 #include <cstring>
 #include <stdexcept>
@@ -21,7 +23,7 @@ AcquisitionService::AcquisitionService(const Acq_Conf& conf, uint32_t max_reques
     c.doppler_step = static_cast<uint32_t>(conf.doppler_step);
     c.pfa = conf.use_CFAR_algorithm_flag ? conf.pfa : 0.0F;
     c.max_dwells = 1;
-    c.item_type = conf.item_type == "cshort" ? GSDR_ITEM_CSHORT : GSDR_ITEM_GR_COMPLEX;
+    c.item_type = pcps_acquisition_mi355x::engine_item_type(conf.item_type);
     c.max_prns = max_requests;
     c.max_blocks = 1;
     c.sampled_ms = conf.sampled_ms;

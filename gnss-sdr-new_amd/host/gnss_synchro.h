@@ -29,11 +29,13 @@ public:
     double Code_phase_samples{};
     uint64_t Tracking_sample_counter{};
     int32_t correlation_length_ms{};
+    double EVM{};  // the fork's error-vector-magnitude lock indicator (gnss_synchro.h:84)
 
     bool Flag_valid_acquisition{};
     bool Flag_valid_symbol_output{};
     bool Flag_valid_word{};
     bool Flag_valid_pseudorange{};
+    bool Flag_PLL_180_deg_phase_locked{};
 };
 
 #endif

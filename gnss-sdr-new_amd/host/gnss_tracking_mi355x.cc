@@ -1,0 +1,80 @@
+#include "gnss_tracking_mi355x.h"
+
+#include <cmath>
+#include <iostream>
+
+namespace
+{
+constexpr double GPS_L1_CA_CODE_RATE_CPS = 1.023e6;  // GPS_L1_CA.h
+constexpr double GPS_L1_CA_CODE_LENGTH_CHIPS = 1023.0;
+constexpr double GALILEO_E1_CODE_CHIP_RATE_CPS = 1.023e6;  // Galileo_E1.h
+constexpr double GALILEO_E1_B_CODE_LENGTH_CHIPS = 4092.0;
+constexpr double BEIDOU_B1I_CODE_RATE_CPS = 2.046e6;  // Beidou_B1I.h
+constexpr double BEIDOU_B1I_CODE_LENGTH_CHIPS = 2046.0;
+}  // namespace
+
+void DllPllTrackingAdapterMI355X::make_block(int32_t signal, int device)
+{
+    item_size_ = trk_params_.item_type == "cshort" ? 4 : (trk_params_.item_type == "cbyte" ? 2 : 8);
+    tracking_ = std::make_unique<dll_pll_veml_tracking_mi355x>(trk_params_, signal, device);
+}
+
+// gps_l1_ca_dll_pll_tracking.cc:34-91
+GpsL1CaDllPllTrackingMI355X::GpsL1CaDllPllTrackingMI355X(const ConfigurationInterface* configuration,
+    const std::string& role, unsigned int in_streams, unsigned int out_streams, int device)
+    : DllPllTrackingAdapterMI355X(role, "GPS_L1_CA_DLL_PLL_Tracking_MI355X")
+{
+    (void)in_streams;
+    (void)out_streams;
+    trk_params_.SetFromConfiguration(configuration, role);
+    trk_params_.vector_length = static_cast<uint32_t>(
+        std::round(trk_params_.fs_in / (GPS_L1_CA_CODE_RATE_CPS / GPS_L1_CA_CODE_LENGTH_CHIPS)));
+    if (trk_params_.extend_correlation_symbols < 1) trk_params_.extend_correlation_symbols = 1;
+    if (trk_params_.extend_correlation_symbols > 20) trk_params_.extend_correlation_symbols = 20;
+    // GPS L1 C/A has no pilot: data tracking (:52-57)
+    trk_params_.track_pilot = false;
+    trk_params_.system = 'G';
+    trk_params_.signal[0] = '1';
+    trk_params_.signal[1] = 'C';
+    make_block(GSDR_SIGNAL_GPS_1C, device);
+}
+
+// galileo_e1_dll_pll_veml_tracking.cc:34-75: extended integration only when
+// tracking the pilot
+GalileoE1DllPllVemlTrackingMI355X::GalileoE1DllPllVemlTrackingMI355X(const ConfigurationInterface* configuration,
+    const std::string& role, unsigned int in_streams, unsigned int out_streams, int device)
+    : DllPllTrackingAdapterMI355X(role, "Galileo_E1_DLL_PLL_VEML_Tracking_MI355X")
+{
+    (void)in_streams;
+    (void)out_streams;
+    trk_params_.SetFromConfiguration(configuration, role);
+    if (trk_params_.extend_correlation_symbols < 1)
+        trk_params_.extend_correlation_symbols = 1;
+    else if (!trk_params_.track_pilot && trk_params_.extend_correlation_symbols > 1)
+        trk_params_.extend_correlation_symbols = 1;
+    trk_params_.vector_length = static_cast<uint32_t>(
+        std::round(trk_params_.fs_in / (GALILEO_E1_CODE_CHIP_RATE_CPS / GALILEO_E1_B_CODE_LENGTH_CHIPS)));
+    trk_params_.system = 'E';
+    trk_params_.signal[0] = '1';
+    trk_params_.signal[1] = 'B';
+    make_block(GSDR_SIGNAL_GAL_1B, device);
+}
+
+// beidou_b1i_dll_pll_tracking.cc:34-90
+BeidouB1iDllPllTrackingMI355X::BeidouB1iDllPllTrackingMI355X(const ConfigurationInterface* configuration,
+    const std::string& role, unsigned int in_streams, unsigned int out_streams, int device)
+    : DllPllTrackingAdapterMI355X(role, "BEIDOU_B1I_DLL_PLL_Tracking_MI355X")
+{
+    (void)in_streams;
+    (void)out_streams;
+    trk_params_.SetFromConfiguration(configuration, role);
+    trk_params_.vector_length = static_cast<uint32_t>(
+        std::round(trk_params_.fs_in / (BEIDOU_B1I_CODE_RATE_CPS / BEIDOU_B1I_CODE_LENGTH_CHIPS)));
+    if (trk_params_.extend_correlation_symbols < 1) trk_params_.extend_correlation_symbols = 1;
+    if (trk_params_.extend_correlation_symbols > 20) trk_params_.extend_correlation_symbols = 20;
+    trk_params_.track_pilot = false;
+    trk_params_.system = 'C';
+    trk_params_.signal[0] = 'B';
+    trk_params_.signal[1] = '1';
+    make_block(GSDR_SIGNAL_BDS_B1, device);
+}

@@ -11,7 +11,26 @@ pcps_acquisition_mi355x::pcps_acquisition_mi355x(const Acq_Conf& conf, int devic
       d_doppler_step(static_cast<uint32_t>(conf.doppler_step)),
       d_consumed_samples(static_cast<uint32_t>(conf.sampled_ms * conf.samples_per_ms * (conf.bit_transition_flag ? 2.0 : 1.0)))
 {
+    // item types the block accepts (Acq_Conf item_type_valid: gr_complex, cshort,
+    // cbyte); anything else is the reference's std::invalid_argument (acq_conf.cc:28-31)
+    d_item_type = engine_item_type(conf.item_type);
+    // make_two_steps with non-coherent dwells would need a step-two dwell grid;
+    // the engine's narrow grid runs one block per call
+    if (conf.make_2_steps && conf.max_dwells > 1 && !conf.bit_transition_flag)
+        throw std::invalid_argument("pcps_acquisition_mi355x: make_two_steps with max_dwells > 1 is not supported");
     d_data_buffer.resize(static_cast<size_t>(d_consumed_samples) * conf.it_size);
+}
+
+// Acq_Conf::item_type -> engine item type.  cbyte (lv_8sc_t, it_size 2) is what
+// the reference adapter turns into gr_complex with complex_byte_to_float_x2 +
+// float_to_complex (gps_l1_ca_pcps_acquisition.cc:76-80, :191-196): interleaved
+// int8 I/Q at scale 1, GSDR_ITEM_IBYTE converts it exactly in the kernels' loads.
+int pcps_acquisition_mi355x::engine_item_type(const std::string& item_type)
+{
+    if (item_type == "gr_complex") return GSDR_ITEM_GR_COMPLEX;
+    if (item_type == "cshort") return GSDR_ITEM_CSHORT;
+    if (item_type == "cbyte") return GSDR_ITEM_IBYTE;
+    throw std::invalid_argument("Unknown item type: " + item_type);
 }
 
 pcps_acquisition_mi355x::~pcps_acquisition_mi355x() { gsdr_acq_destroy(d_engine); }
@@ -34,7 +53,7 @@ void pcps_acquisition_mi355x::ensure_engine()
     c.pfa = d_acq_parameters.use_CFAR_algorithm_flag ? d_acq_parameters.pfa : 0.0F;
     c.max_dwells = d_acq_parameters.max_dwells;
     c.bit_transition_flag = d_acq_parameters.bit_transition_flag ? 1 : 0;
-    c.item_type = d_acq_parameters.item_type == "cshort" ? GSDR_ITEM_CSHORT : GSDR_ITEM_GR_COMPLEX;
+    c.item_type = d_item_type;
     c.max_prns = 1;
     c.max_blocks = 1;
     c.sampled_ms = d_acq_parameters.sampled_ms;
@@ -170,8 +189,12 @@ void pcps_acquisition_mi355x::send_negative_acquisition()
     if (d_events) d_events(2);
 }
 
-// acquisition_core (:615-882) for the single-dwell configuration, with the
-// make_two_steps narrow grid (:717-773) when d_step_two.
+// acquisition_core (:615-882).  One call integrates the block in d_data_buffer:
+// a single-dwell configuration runs the whole grid per call (gsdr_acq_run); with
+// max_dwells > 1 the engine keeps the |R|^2 grid of the attempt on the device
+// and this call adds its dwell (gsdr_acq_run_dwell, the counter as in :638);
+// with bit_transition_flag the engine's N/2-output grid decides every call
+// (:831-869); make_two_steps searches the narrow grid (:717-773).
 void pcps_acquisition_mi355x::acquisition_core(uint64_t samp_count)
 {
     d_mag = 0.0F;
@@ -186,6 +209,11 @@ void pcps_acquisition_mi355x::acquisition_core(uint64_t samp_count)
             const uint32_t slot = 0;
             rc = gsdr_acq_run_step_two(d_engine, d_data_buffer.data(), 1, &slot, &d_doppler_center_step_two,
                 &d_input_power, samp_count, &r);
+        }
+    else if (d_acq_parameters.max_dwells > 1 && !d_acq_parameters.bit_transition_flag)
+        {
+            rc = gsdr_acq_run_dwell(d_engine, d_data_buffer.data(), d_num_noncoherent_integrations_counter - 1U, samp_count,
+                &r);
         }
     else
         {
@@ -202,7 +230,8 @@ void pcps_acquisition_mi355x::acquisition_core(uint64_t samp_count)
             return;
         }
     d_mag = r.peak;
-    d_input_power = r.input_power;
+    // CFAR input power (:534) -- kept from the coarse step during step two (:531)
+    if (!d_step_two) d_input_power = r.input_power;
     d_test_statistics = r.test_statistic;
     // with make_2_steps and repeat steps only the narrow grid updates Gnss_Synchro (:697)
     if (d_gnss_synchro && (d_step_two || !(d_acq_parameters.make_2_steps && d_step_repeat)))
@@ -222,49 +251,90 @@ void pcps_acquisition_mi355x::acquisition_core(uint64_t samp_count)
             d_gnss_synchro->Acq_doppler_hz = static_cast<double>(r.doppler_hz);
             if (d_step_two) d_gnss_synchro->Acq_doppler_step = static_cast<uint32_t>(d_acq_parameters.doppler_step2);
         }
-    // decision and dwell FSM (:781-829, non-bit-transition branch)
-    if (d_test_statistics > d_threshold)
+    if (!d_acq_parameters.bit_transition_flag)
         {
-            d_active = false;
-            if (d_acq_parameters.make_2_steps)
+            // decision and dwell FSM (:781-829)
+            if (d_test_statistics > d_threshold)
                 {
-                    if (d_step_two)
+                    d_active = false;
+                    if (d_acq_parameters.make_2_steps)
                         {
-                            send_positive_acquisition();
-                            d_step_two = false;
-                            d_state = 0;
+                            if (d_step_two)
+                                {
+                                    send_positive_acquisition();
+                                    d_step_two = false;
+                                    d_state = 0;
+                                }
+                            else
+                                {
+                                    // clear the buffer and search the narrow grid on the next block
+                                    d_step_two = true;
+                                    d_num_noncoherent_integrations_counter = 0;
+                                    d_positive_acq = 0;
+                                    d_state = 0;
+                                }
+                            calculate_threshold();
                         }
                     else
                         {
-                            // clear the buffer and search the narrow grid on the next block
-                            d_step_two = true;
-                            d_num_noncoherent_integrations_counter = 0;
-                            d_positive_acq = 0;
+                            send_positive_acquisition();
                             d_state = 0;
                         }
-                    calculate_threshold();
                 }
             else
                 {
-                    send_positive_acquisition();
+                    d_buffer_count = 0;
+                    d_state = 1;
+                }
+            if (d_num_noncoherent_integrations_counter == d_acq_parameters.max_dwells)
+                {
+                    if (d_state != 0) send_negative_acquisition();
                     d_state = 0;
+                    d_active = false;
+                    const bool was_step_two = d_step_two;
+                    d_step_two = false;
+                    if (was_step_two) calculate_threshold();
                 }
         }
     else
         {
-            d_buffer_count = 0;
-            d_state = 1;
-        }
-    if (d_num_noncoherent_integrations_counter == d_acq_parameters.max_dwells)
-        {
-            if (d_state != 0) send_negative_acquisition();
-            d_state = 0;
+            // bit transition: every call decides on its own (:831-869)
             d_active = false;
-            const bool was_step_two = d_step_two;
-            d_step_two = false;
-            if (was_step_two) calculate_threshold();
+            if (d_test_statistics > d_threshold)
+                {
+                    if (d_acq_parameters.make_2_steps)
+                        {
+                            if (d_step_two)
+                                {
+                                    send_positive_acquisition();
+                                    d_step_two = false;
+                                    d_state = 0;
+                                }
+                            else
+                                {
+                                    d_step_two = true;
+                                    d_num_noncoherent_integrations_counter = 0U;
+                                    d_state = 0;
+                                }
+                            calculate_threshold();
+                        }
+                    else
+                        {
+                            send_positive_acquisition();
+                            d_state = 0;
+                        }
+                }
+            else
+                {
+                    d_state = 0;
+                    const bool was_step_two = d_step_two;
+                    d_step_two = false;
+                    if (was_step_two) calculate_threshold();
+                    send_negative_acquisition();
+                }
         }
-    if (d_num_noncoherent_integrations_counter == d_acq_parameters.max_dwells || d_positive_acq == 1)
+    if (d_num_noncoherent_integrations_counter == d_acq_parameters.max_dwells || d_positive_acq == 1 ||
+        d_acq_parameters.bit_transition_flag)
         {
             d_num_noncoherent_integrations_counter = 0U;
             d_positive_acq = 0;

@@ -12,6 +12,7 @@
 #include <functional>
 #include <memory>
 #include <mutex>
+#include <string>
 #include <vector>
 
 #include "acq_conf.h"
@@ -54,6 +55,9 @@ public:
     bool step_two() const { return d_step_two; }
     bool step_repeat() const { return d_step_repeat; }
 
+    uint32_t num_noncoherent_integrations() const { return d_num_noncoherent_integrations_counter; }
+    static int engine_item_type(const std::string& item_type);
+
 private:
     void acquisition_core(uint64_t samp_count);
     void ensure_engine();
@@ -62,6 +66,7 @@ private:
 
     Acq_Conf d_acq_parameters;
     int d_device;
+    int d_item_type{GSDR_ITEM_GR_COMPLEX};
     gsdr_acq* d_engine{nullptr};
     int32_t d_engine_dmax{0};
     uint32_t d_engine_step{0};

@@ -4,7 +4,16 @@
 //     on the reference capture, through the adapter + block mirror + GPU engine.
 //  2. Hip_Multicorrelator_Real_Codes / Hip_Multicorrelator on the acquired signal,
 //     checked against an fp64 evaluation of the reference's phasor model.
-// Usage: host_selftest <GPS_L1_CA_ID_1_Fs_4Msps_2ms.dat>
+//  3. The dwell FSM across calls (max_dwells = 2) against the one-shot dwell
+//     engine, the bit-transition branch, cbyte input.
+//  4. GalileoE1PcpsAmbiguousAcquisitionTest.ValidationOfResults
+//     (galileo_e1_pcps_ambiguous_acquisition_test.cc:289-371) through the Galileo
+//     adapter on Galileo_E1_ID_1_Fs_4Msps_8ms.dat, and the BeiDou adapter on a
+//     synthetic B1I signal (the reference's B1I capture is not in the tree).
+//  5. Acquisition -> tracking hand-off through the factory-built adapters
+//     (TrackingInterface::start_tracking from the acquisition's Gnss_Synchro,
+//     Gnss_Synchro records out) on synthetic GPS L1 C/A and Galileo E1 streams.
+// Usage: host_selftest <GPS_L1_CA_ID_1_Fs_4Msps_2ms.dat> [Galileo_E1_ID_1_Fs_4Msps_8ms.dat]
 #include <algorithm>
 #include <cmath>
 #include <complex>
@@ -15,8 +24,14 @@
 #include <string>
 #include <vector>
 
+#include <random>
+
 #include "acquisition_service.h"
+#include "beidou_b1i_pcps_acquisition_mi355x.h"
+#include "galileo_e1_pcps_ambiguous_acquisition_mi355x.h"
+#include "gnss_block_factory_mi355x.h"
 #include "gnss_replicas.h"
+#include "gnss_tracking_mi355x.h"
 #include "gps_l1_ca_pcps_acquisition_mi355x.h"
 #include "hip_multicorrelator_real_codes.h"
 
@@ -314,6 +329,464 @@ void test_acquisition_service(const std::vector<std::complex<float>>& capture)
     std::printf("\n");
 }
 
+
+// Feed an acquisition block like a GNU Radio source until it sends an event;
+// returns the event (0: none before the data ran out).
+template <class T>
+int run_acquisition(pcps_acquisition_mi355x* blk, const T* data, size_t n, int chunk, int* last_event)
+{
+    size_t pos = 0;
+    *last_event = 0;
+    for (int guard = 0; guard < 100000 && *last_event == 0; ++guard)
+        {
+            const int m = static_cast<int>(std::min<size_t>(static_cast<size_t>(chunk), n - pos));
+            const int used = blk->work(data + pos, m);
+            pos += static_cast<size_t>(used);
+            if (m == 0 && used == 0 && guard > 16) break;
+        }
+    return *last_event;
+}
+
+InMemoryConfiguration gps_acq_config(const std::string& extra_key = "", const std::string& extra_value = "")
+{
+    InMemoryConfiguration config;
+    config.set_property("GNSS-SDR.internal_fs_sps", "4000000");
+    config.set_property("Acquisition_1C.implementation", "GPS_L1_CA_PCPS_Acquisition_MI355X");
+    config.set_property("Acquisition_1C.item_type", "gr_complex");
+    config.set_property("Acquisition_1C.coherent_integration_time_ms", "1");
+    config.set_property("Acquisition_1C.doppler_max", "5000");
+    config.set_property("Acquisition_1C.doppler_step", "250");
+    config.set_property("Acquisition_1C.blocking_on_standby", "true");
+    if (!extra_key.empty()) config.set_property(extra_key, extra_value);
+    return config;
+}
+
+// max_dwells = 2 across two general_work calls (pcps_acquisition.cc:672-680,
+// :815-829): with an unreachable threshold the block integrates both blocks and
+// reports negative after the second; its statistic equals the one-shot dwell
+// engine's (gsdr_acq_run over the two-block attempt); with threshold 0 the first
+// dwell is positive and the counter resets.
+void test_acquisition_dwells(const std::vector<std::complex<float>>& capture)
+{
+    for (const char* pfa : {"0", "0.01"})
+        {
+            InMemoryConfiguration config = gps_acq_config("Acquisition_1C.max_dwells", "2");
+            config.set_property("Acquisition_1C.pfa", pfa);
+            Gnss_Synchro gs{};
+            gs.System = 'G';
+            gs.Signal[0] = '1';
+            gs.Signal[1] = 'C';
+            gs.PRN = 1;
+            GpsL1CaPcpsAcquisitionMI355X acq(&config, "Acquisition_1C", 1, 0);
+            int ev = 0;
+            int events = 0;
+            acq.get_block()->set_event_handler([&](int e) {
+                ev = e;
+                ++events;
+            });
+            acq.set_gnss_synchro(&gs);
+            acq.set_local_code();
+            acq.set_state(1);
+            acq.init();
+            acq.get_block()->start();
+            const bool cfar = std::string(pfa) != "0";
+            if (!cfar) acq.get_block()->set_threshold(1e30F);
+            // the CFAR threshold comes from pfa with 2 dwells; make it unreachable too
+            if (cfar) acq.get_block()->set_threshold(1e30F);
+            run_acquisition(acq.get_block(), capture.data(), capture.size(), 1000, &ev);
+            EXPECT(ev == 2 && events == 1, "max_dwells=2, unreachable threshold: one negative after the second dwell");
+            EXPECT(gs.Acq_samplestamp_samples == 8000ULL, "decision on the second block");
+            const float stat_block = acq.get_block()->test_statistics();
+            // one-shot: both dwells of the attempt in one engine call
+            gsdr_acq_conf c{};
+            c.fs_in = 4000000;
+            c.consumed_samples = 4000;
+            c.samples_per_code = 4000.0F;
+            c.samples_per_chip = 4;
+            c.doppler_max = 5000;
+            c.doppler_step = 250;
+            c.pfa = cfar ? 0.01F : 0.0F;
+            c.max_dwells = 2;
+            c.item_type = GSDR_ITEM_GR_COMPLEX;
+            c.max_prns = 1;
+            c.max_blocks = 1;
+            c.sampled_ms = 1;
+            c.ms_per_code = 1;
+            gsdr_acq* one = nullptr;
+            EXPECT(gsdr_acq_create(0, &c, &one) == GSDR_OK, "dwell engine");
+            const auto code = gps_l1_ca_code_gen_complex_sampled(1, 4000000);
+            const uint32_t prn = 1;
+            gsdr_acq_set_local_codes(one, reinterpret_cast<const float*>(code.data()), &prn, 1);
+            gsdr_acq_set_threshold(one, 1e30F);
+            gsdr_acq_result r{};
+            EXPECT(gsdr_acq_run(one, capture.data(), 1, 4000, &r) == GSDR_OK, "dwell engine run");
+            gsdr_acq_destroy(one);
+            EXPECT(r.num_dwells == 2, "one-shot attempt reports its last dwell");
+            EXPECT(std::abs(r.test_statistic - stat_block) <= 1e-5F * std::abs(r.test_statistic),
+                "per-call dwell statistic == one-shot dwell statistic");
+            EXPECT(std::abs(gs.Acq_delay_samples - r.acq_delay_samples) < 0.5 &&
+                       std::abs(gs.Acq_doppler_hz - r.doppler_hz) < 0.5,
+                "per-call dwell cell == one-shot dwell cell");
+            std::printf("dwells (pfa %s): per-call stat %.5f, one-shot %.5f, delay %.0f doppler %.0f\n", pfa, stat_block,
+                r.test_statistic, gs.Acq_delay_samples, gs.Acq_doppler_hz);
+            // threshold 0: positive on the first dwell, counter reset
+            acq.get_block()->set_threshold(0.0F);
+            acq.set_state(1);
+            ev = 0;
+            events = 0;
+            run_acquisition(acq.get_block(), capture.data(), capture.size(), 1000, &ev);
+            EXPECT(ev == 1 && acq.get_block()->num_noncoherent_integrations() == 0, "positive first dwell resets the counter");
+            EXPECT(std::abs(gs.Acq_delay_samples - 524.0) < 1.0, "PRN 1 at 524 samples");
+        }
+}
+
+// bit_transition_flag (pcps_acquisition.cc:71, :85-92, :831-869): a 2 ms buffer,
+// the code in the second half of the 8000-point FFT, every call decides.
+void test_acquisition_bit_transition(const std::vector<std::complex<float>>& capture)
+{
+    InMemoryConfiguration config = gps_acq_config("Acquisition_1C.bit_transition_flag", "true");
+    config.set_property("Acquisition_1C.pfa", "0.01");
+    Gnss_Synchro gs{};
+    gs.System = 'G';
+    gs.Signal[0] = '1';
+    gs.Signal[1] = 'C';
+    gs.PRN = 1;
+    GpsL1CaPcpsAcquisitionMI355X acq(&config, "Acquisition_1C", 1, 0);
+    int ev = 0;
+    acq.get_block()->set_event_handler([&](int e) { ev = e; });
+    acq.set_gnss_synchro(&gs);
+    acq.set_local_code();
+    acq.set_state(1);
+    acq.init();
+    acq.get_block()->start();
+    run_acquisition(acq.get_block(), capture.data(), capture.size(), 1000, &ev);
+    EXPECT(ev == 1, "bit transition: positive");
+    EXPECT(std::abs(gs.Acq_delay_samples - 524.0) < 1.0 && std::abs(gs.Acq_doppler_hz - 1680.0) <= 666.0,
+        "bit transition: 524 samples / 1680 Hz");
+    EXPECT(gs.Acq_samplestamp_samples == 8000ULL, "bit transition: one 8000-sample buffer");
+    // a negative bit-transition call: unreachable threshold, no re-arm (:858-868)
+    acq.get_block()->set_threshold(1e30F);
+    acq.set_state(1);
+    ev = 0;
+    run_acquisition(acq.get_block(), capture.data(), capture.size(), 1000, &ev);
+    EXPECT(ev == 2, "bit transition: immediate negative");
+    std::printf("bit transition: delay %.0f doppler %.0f stat %.2f\n", gs.Acq_delay_samples, gs.Acq_doppler_hz,
+        acq.get_block()->test_statistics());
+}
+
+// item_type=cbyte: interleaved int8 I/Q (complex_byte_to_float_x2 + float_to_complex)
+void test_acquisition_cbyte(const std::vector<std::complex<float>>& capture)
+{
+    std::vector<int8_t> bytes(2 * capture.size());
+    for (size_t i = 0; i < capture.size(); ++i)
+        {
+            bytes[2 * i] = static_cast<int8_t>(std::lrint(std::max(-127.0F, std::min(127.0F, 1000.0F * capture[i].real()))));
+            bytes[2 * i + 1] = static_cast<int8_t>(std::lrint(std::max(-127.0F, std::min(127.0F, 1000.0F * capture[i].imag()))));
+        }
+    InMemoryConfiguration config = gps_acq_config("Acquisition_1C.item_type", "cbyte");
+    config.set_property("Acquisition_1C.pfa", "0.01");
+    Gnss_Synchro gs{};
+    gs.System = 'G';
+    gs.Signal[0] = '1';
+    gs.Signal[1] = 'C';
+    gs.PRN = 1;
+    GpsL1CaPcpsAcquisitionMI355X acq(&config, "Acquisition_1C", 1, 0);
+    EXPECT(acq.item_size() == 2, "cbyte item size");
+    int ev = 0;
+    acq.get_block()->set_event_handler([&](int e) { ev = e; });
+    acq.set_gnss_synchro(&gs);
+    acq.set_local_code();
+    acq.set_state(1);
+    acq.init();
+    acq.get_block()->start();
+    size_t pos = 0;
+    for (int guard = 0; guard < 100 && ev == 0; ++guard)
+        {
+            const int m = static_cast<int>(std::min<size_t>(1000, capture.size() - pos));
+            pos += static_cast<size_t>(acq.get_block()->work(bytes.data() + 2 * pos, m));
+        }
+    EXPECT(ev == 1 && std::abs(gs.Acq_delay_samples - 524.0) < 1.0, "cbyte: PRN 1 acquired at 524 samples");
+    bool threw = false;
+    try
+        {
+            InMemoryConfiguration bad = gps_acq_config("Acquisition_1C.item_type", "ishort");
+            GpsL1CaPcpsAcquisitionMI355X b(&bad, "Acquisition_1C", 1, 0);
+        }
+    catch (const std::invalid_argument&)
+        {
+            threw = true;
+        }
+    EXPECT(threw, "unknown item type -> std::invalid_argument");
+    std::printf("cbyte: delay %.0f doppler %.0f\n", gs.Acq_delay_samples, gs.Acq_doppler_hz);
+}
+
+void test_galileo_acquisition(const std::vector<std::complex<float>>& capture)
+{
+    InMemoryConfiguration config;
+    config.set_property("Acquisition_1B.implementation", "Galileo_E1_PCPS_Ambiguous_Acquisition_MI355X");
+    config.set_property("GNSS-SDR.internal_fs_sps", "4000000");
+    config.set_property("Acquisition_1B.item_type", "gr_complex");
+    config.set_property("Acquisition_1B.coherent_integration_time_ms", "4");
+    config.set_property("Acquisition_1B.dump", "false");
+    config.set_property("Acquisition_1B.pfa", "0.001");
+    config.set_property("Acquisition_1B.doppler_max", "10000");
+    config.set_property("Acquisition_1B.doppler_step", "250");
+    config.set_property("Acquisition_1B.repeat_satellite", "false");
+    config.set_property("Acquisition_1B.cboc", "true");
+    Gnss_Synchro gs{};
+    gs.Channel_ID = 0;
+    gs.System = 'E';
+    gs.Signal[0] = '1';
+    gs.Signal[1] = 'B';
+    gs.PRN = 1;
+    auto acq_ = gsdr_factory::GetAcqBlock(&config, "Acquisition_1B", 1, 0, 0);
+    auto* acquisition = dynamic_cast<GalileoE1PcpsAmbiguousAcquisitionMI355X*>(acq_.get());
+    EXPECT(acquisition != nullptr, "factory builds the Galileo adapter");
+    if (!acquisition) return;
+    int ev = 0;
+    acquisition->get_block()->set_event_handler([&](int e) { ev = e; });
+    acquisition->set_channel(gs.Channel_ID);
+    acquisition->set_gnss_synchro(&gs);
+    acquisition->set_threshold(config.property("Acquisition_1B.threshold", 1e-9F));
+    acquisition->set_doppler_max(10000);
+    acquisition->set_doppler_step(250);
+    acquisition->set_local_code();
+    acquisition->init();
+    acquisition->reset();
+    acquisition->set_state(1);
+    acquisition->get_block()->start();
+    run_acquisition(acquisition->get_block(), capture.data(), capture.size(), 4096, &ev);
+    EXPECT(ev == 1, "Galileo: Acquisition failure. Expected message: 1=ACQ SUCCESS.");
+    const double delay_error_samples = std::abs(2920.0 - gs.Acq_delay_samples);
+    const auto delay_error_chips = static_cast<float>(delay_error_samples * 1023 / 4000000);
+    const double doppler_error_hz = std::abs(-632.0 - gs.Acq_doppler_hz);
+    EXPECT(doppler_error_hz <= 166, "Galileo: Doppler error exceeds 166 Hz");
+    EXPECT(delay_error_chips < 0.175, "Galileo: Delay error exceeds 0.175 chips");
+    std::printf("galileo acquisition: message %d delay %.1f samples doppler %.0f Hz stat %.2f (thr %.2f)\n", ev,
+        gs.Acq_delay_samples, gs.Acq_doppler_hz, acquisition->get_block()->test_statistics(),
+        acquisition->get_block()->threshold());
+}
+
+// ---- synthetic streams: code x carrier (+ data bits) + AWGN, code Doppler included
+struct SynthSat
+{
+    std::vector<float> chips;  // one sample per chip (or sub-chip replica)
+    double chip_rate;          // replica samples per second (chips/s x samples per chip)
+    double carrier_hz;         // L1 / E1 / B1I carrier [Hz]
+    double delay_samples;      // code start sample
+    double doppler_hz;
+    double amplitude;
+    std::vector<float> secondary;  // per code period (empty: none)
+};
+
+std::vector<std::complex<float>> synth_stream(const std::vector<SynthSat>& sats, double fs, size_t n, uint32_t seed,
+    double noise_sigma)
+{
+    std::vector<std::complex<float>> x(n);
+    std::mt19937 gen(seed);
+    std::normal_distribution<double> nd(0.0, noise_sigma);
+    for (size_t i = 0; i < n; ++i) x[i] = std::complex<float>(static_cast<float>(nd(gen)), static_cast<float>(nd(gen)));
+    for (const auto& s : sats)
+        {
+            const double L = static_cast<double>(s.chips.size());
+            const double rate = s.chip_rate * (1.0 + s.doppler_hz / s.carrier_hz);
+            for (size_t i = 0; i < n; ++i)
+                {
+                    const double t = (static_cast<double>(i) - s.delay_samples) / fs;
+                    const double c = t * rate;                   // replica samples since the code start
+                    const double period = std::floor(c / L);
+                    double k = c - period * L;
+                    const auto idx = static_cast<size_t>(std::min(L - 1.0, std::max(0.0, std::floor(k))));
+                    double v = s.chips[idx];
+                    if (!s.secondary.empty())
+                        {
+                            const auto p = static_cast<long long>(period);
+                            const long long ns = static_cast<long long>(s.secondary.size());
+                            v *= s.secondary[static_cast<size_t>(((p % ns) + ns) % ns)];
+                        }
+                    const double ph = 2.0 * M_PI * s.doppler_hz * static_cast<double>(i) / fs + 0.3;
+                    x[i] += std::complex<float>(static_cast<float>(s.amplitude * v * std::cos(ph)),
+                        static_cast<float>(s.amplitude * v * std::sin(ph)));
+                }
+        }
+    return x;
+}
+
+void test_beidou_acquisition()
+{
+    const double fs = 4000000.0;
+    SynthSat s{beidou_b1i_code_gen_float(6), 2.046e6, 1561.098e6, 1234.0, 2000.0, 0.05, {}};
+    const auto x = synth_stream({s}, fs, 8000, 7, 1.0);
+    InMemoryConfiguration config;
+    config.set_property("GNSS-SDR.internal_fs_sps", "4000000");
+    config.set_property("Acquisition_B1.implementation", "BEIDOU_B1I_PCPS_Acquisition_MI355X");
+    config.set_property("Acquisition_B1.item_type", "gr_complex");
+    config.set_property("Acquisition_B1.coherent_integration_time_ms", "1");
+    config.set_property("Acquisition_B1.pfa", "0.01");
+    config.set_property("Acquisition_B1.doppler_max", "5000");
+    config.set_property("Acquisition_B1.doppler_step", "250");
+    config.set_property("Acquisition_B1.blocking_on_standby", "true");
+    Gnss_Synchro gs{};
+    gs.System = 'C';
+    gs.Signal[0] = 'B';
+    gs.Signal[1] = '1';
+    gs.PRN = 6;
+    auto acq_ = gsdr_factory::GetAcqBlock(&config, "Acquisition_B1", 1, 0, 0);
+    auto* acq = dynamic_cast<BeidouB1iPcpsAcquisitionMI355X*>(acq_.get());
+    EXPECT(acq != nullptr, "factory builds the BeiDou adapter");
+    if (!acq) return;
+    int ev = 0;
+    acq->get_block()->set_event_handler([&](int e) { ev = e; });
+    acq->set_gnss_synchro(&gs);
+    acq->init();  // loads the replica (beidou_b1i_pcps_acquisition.cc:135-139)
+    acq->set_state(1);
+    acq->get_block()->start();
+    run_acquisition(acq->get_block(), x.data(), x.size(), 1000, &ev);
+    // code start 1234 samples after the block start; the grid is 250 Hz
+    EXPECT(ev == 1 && std::abs(gs.Acq_delay_samples - 1234.0) <= 1.0 && std::abs(gs.Acq_doppler_hz - 2000.0) <= 125.0,
+        "BeiDou B1I synthetic: PRN 6 at 1234 samples / 2000 Hz");
+    std::printf("beidou acquisition: message %d delay %.1f doppler %.0f stat %.2f\n", ev, gs.Acq_delay_samples,
+        gs.Acq_doppler_hz, acq->get_block()->test_statistics());
+}
+
+// Channel-level hand-off: acquisition adapter -> Gnss_Synchro -> tracking adapter
+// start_tracking (ChannelFsm::start_tracking, channel_fsm.cc:204-208), then the
+// tracking block's general_work over the rest of the stream in GNU-Radio-sized
+// chunks; Gnss_Synchro records out.
+struct HandOff
+{
+    int outputs{0};
+    int loss{0};
+    double doppler{0.0};
+    double cn0{0.0};
+    double prompt_i{0.0}, prompt_q{0.0};
+    bool pll_locked{false};
+};
+
+HandOff run_handoff(AcquisitionInterface* acq, pcps_acquisition_mi355x* ablk, TrackingInterface* trk,
+    dll_pll_veml_tracking_mi355x* tblk, Gnss_Synchro* gs, const std::vector<std::complex<float>>& x)
+{
+    HandOff h;
+    int ev = 0;
+    ablk->set_event_handler([&](int e) { ev = e; });
+    acq->set_gnss_synchro(gs);
+    acq->set_local_code();
+    acq->init();
+    acq->set_state(1);
+    ablk->start();
+    size_t pos = 0;
+    for (int guard = 0; guard < 1000 && ev == 0 && pos < x.size(); ++guard)
+        pos += static_cast<size_t>(ablk->work(x.data() + pos, static_cast<int>(std::min<size_t>(4096, x.size() - pos))));
+    EXPECT(ev == 1, "hand-off: acquisition positive");
+    if (ev != 1) return h;
+    trk->set_gnss_synchro(gs);
+    trk->start_tracking();
+    tblk->set_event_handler([&](int e) {
+        if (e == 3) ++h.loss;
+    });
+    // the tracking block sees the stream from the acquisition stamp on
+    uint64_t nread = gs->Acq_samplestamp_samples;
+    std::vector<double> dop;
+    while (nread + static_cast<uint64_t>(tblk->forecast()) <= x.size())
+        {
+            Gnss_Synchro out{};
+            int nout = 0;
+            const int avail = static_cast<int>(std::min<uint64_t>(8192, x.size() - nread));
+            const int used = tblk->work(x.data() + nread, avail, nread, &out, &nout);
+            if (nout == 1 && out.Flag_valid_symbol_output)
+                {
+                    ++h.outputs;
+                    dop.push_back(out.Carrier_Doppler_hz);
+                    h.cn0 = out.CN0_dB_hz;
+                    h.prompt_i = out.Prompt_I;
+                    h.prompt_q = out.Prompt_Q;
+                }
+            if (used <= 0) break;
+            nread += static_cast<uint64_t>(used);
+        }
+    const size_t k = std::min<size_t>(dop.size(), 20);
+    for (size_t i = dop.size() - k; i < dop.size(); ++i) h.doppler += dop[i] / static_cast<double>(k);
+    return h;
+}
+
+void test_tracking_handoff()
+{
+    const double fs = 4000000.0;
+    // GPS L1 C/A, PRN 1: code start 524.3 samples, 1680 Hz, 50 dB-Hz (A^2/(2 sigma^2) fs)
+    const double sigma = 1.0;
+    const double amp_gps = std::sqrt(2.0 * std::pow(10.0, 5.0) / fs) * sigma;
+    SynthSat g{gps_l1_ca_code_gen_float(1), 1.023e6, 1575.42e6, 524.3, 1680.0, amp_gps, {}};
+    const auto x = synth_stream({g}, fs, static_cast<size_t>(fs * 0.4), 11, sigma);
+    InMemoryConfiguration config = gps_acq_config();
+    config.set_property("Acquisition_1C.pfa", "0.01");
+    config.set_property("Tracking_1C.implementation", "GPS_L1_CA_DLL_PLL_Tracking_MI355X");
+    config.set_property("Tracking_1C.item_type", "gr_complex");
+    config.set_property("Tracking_1C.pll_bw_hz", "40.0");  // conf/gnss-sdr_GPS_L1_gr_complex.conf:66-67
+    config.set_property("Tracking_1C.dll_bw_hz", "4.0");
+    Gnss_Synchro gs{};
+    gs.System = 'G';
+    gs.Signal[0] = '1';
+    gs.Signal[1] = 'C';
+    gs.PRN = 1;
+    auto acq = gsdr_factory::GetAcqBlock(&config, "Acquisition_1C", 1, 0, 0);
+    auto trk = gsdr_factory::GetTrkBlock(&config, "Tracking_1C", 1, 1, 0);
+    auto* gacq = dynamic_cast<GpsL1CaPcpsAcquisitionMI355X*>(acq.get());
+    auto* gtrk = dynamic_cast<GpsL1CaDllPllTrackingMI355X*>(trk.get());
+    EXPECT(gacq && gtrk, "factory builds the GPS acquisition and tracking adapters");
+    if (!gacq || !gtrk) return;
+    EXPECT(gtrk->conf().vector_length == 4000U && gtrk->item_size() == 8, "GPS tracking: vector_length 4000");
+    const HandOff h = run_handoff(gacq, gacq->get_block(), gtrk, gtrk->get_block(), &gs, x);
+    EXPECT(h.outputs > 350 && h.loss == 0, "GPS hand-off: one Gnss_Synchro per ms, no loss of lock");
+    EXPECT(std::abs(h.doppler - 1680.0) < 3.0, "GPS hand-off: carrier Doppler converged to 1680 Hz");
+    EXPECT(h.cn0 > 44.0 && h.cn0 < 56.0, "GPS hand-off: CN0 estimate near 50 dB-Hz");
+    EXPECT(std::abs(h.prompt_i) > 4.0 * std::abs(h.prompt_q), "GPS hand-off: carrier phase locked (|I| >> |Q|)");
+    std::printf("gps hand-off: %d outputs, doppler %.2f Hz, CN0 %.1f dB-Hz, prompt (%.1f, %.1f), losses %d\n",
+        h.outputs, h.doppler, h.cn0, h.prompt_i, h.prompt_q, h.loss);
+
+    // Galileo E1: E1-B data + E1-C pilot with its secondary code, sinBOC(1,1)
+    // replicas at 2 samples per chip, 4 ms code, pilot tracking (track_pilot)
+    const double amp_gal = std::sqrt(2.0 * std::pow(10.0, 5.0) / fs) * sigma / std::sqrt(2.0);
+    std::vector<float> sec(25);
+    const char* sec_str = "0011100000001010110110010";
+    for (int i = 0; i < 25; ++i) sec[i] = sec_str[i] == '0' ? 1.0F : -1.0F;
+    auto e1c = galileo_e1_code_gen_sinboc11_float("1C", 11);
+    for (auto& v : e1c) v = -v;  // E1-C enters the composite signal with a minus sign
+    SynthSat gb{galileo_e1_code_gen_sinboc11_float("1B", 11), 2.046e6, 1575.42e6, 2920.0, -632.0, amp_gal, {}};
+    SynthSat gc{e1c, 2.046e6, 1575.42e6, 2920.0, -632.0, amp_gal, sec};
+    const auto y = synth_stream({gb, gc}, fs, static_cast<size_t>(fs * 0.6), 13, sigma);
+    InMemoryConfiguration gcfg;
+    gcfg.set_property("GNSS-SDR.internal_fs_sps", "4000000");
+    gcfg.set_property("Acquisition_1B.implementation", "Galileo_E1_PCPS_Ambiguous_Acquisition_MI355X");
+    gcfg.set_property("Acquisition_1B.item_type", "gr_complex");
+    gcfg.set_property("Acquisition_1B.coherent_integration_time_ms", "4");
+    gcfg.set_property("Acquisition_1B.pfa", "0.01");
+    gcfg.set_property("Acquisition_1B.doppler_max", "5000");
+    gcfg.set_property("Acquisition_1B.doppler_step", "125");
+    gcfg.set_property("Acquisition_1B.blocking_on_standby", "true");
+    gcfg.set_property("Tracking_1B.implementation", "Galileo_E1_DLL_PLL_VEML_Tracking_MI355X");
+    gcfg.set_property("Tracking_1B.item_type", "gr_complex");
+    gcfg.set_property("Tracking_1B.pll_bw_hz", "15.0");
+    gcfg.set_property("Tracking_1B.dll_bw_hz", "2.0");
+    Gnss_Synchro es{};
+    es.System = 'E';
+    es.Signal[0] = '1';
+    es.Signal[1] = 'B';
+    es.PRN = 11;
+    auto eacq_ = gsdr_factory::GetAcqBlock(&gcfg, "Acquisition_1B", 1, 0, 0);
+    auto etrk_ = gsdr_factory::GetTrkBlock(&gcfg, "Tracking_1B", 1, 1, 0);
+    auto* eacq = dynamic_cast<GalileoE1PcpsAmbiguousAcquisitionMI355X*>(eacq_.get());
+    auto* etrk = dynamic_cast<GalileoE1DllPllVemlTrackingMI355X*>(etrk_.get());
+    EXPECT(eacq && etrk, "factory builds the Galileo acquisition and tracking adapters");
+    if (!eacq || !etrk) return;
+    EXPECT(etrk->conf().vector_length == 16000U && etrk->conf().track_pilot, "Galileo tracking: 16000 samples, pilot");
+    const HandOff e = run_handoff(eacq, eacq->get_block(), etrk, etrk->get_block(), &es, y);
+    EXPECT(e.outputs > 100 && e.loss == 0, "Galileo hand-off: one Gnss_Synchro per 4 ms, no loss of lock");
+    EXPECT(std::abs(e.doppler + 632.0) < 3.0, "Galileo hand-off: carrier Doppler converged to -632 Hz");
+    EXPECT(e.cn0 > 44.0 && e.cn0 < 56.0, "Galileo hand-off: CN0 estimate near 50 dB-Hz");
+    std::printf("galileo hand-off: %d outputs, doppler %.2f Hz, CN0 %.1f dB-Hz, prompt (%.1f, %.1f), losses %d\n",
+        e.outputs, e.doppler, e.cn0, e.prompt_i, e.prompt_q, e.loss);
+}
+
 void test_multicorrelator(const std::vector<std::complex<float>>& capture)
 {
     const int n = 4000;
@@ -375,7 +848,22 @@ int main(int argc, char** argv)
     test_acquisition_two_steps(capture);
     test_acquisition_repeat_steps(capture);
     test_acquisition_service(capture);
+    test_acquisition_dwells(capture);
+    test_acquisition_bit_transition(capture);
+    test_acquisition_cbyte(capture);
     test_multicorrelator(capture);
+    if (argc > 2)
+        {
+            const auto gal = read_capture(argv[2]);
+            if (gal.size() < 32000)
+                {
+                    std::cerr << "cannot read capture " << argv[2] << '\n';
+                    return 2;
+                }
+            test_galileo_acquisition(gal);
+        }
+    test_beidou_acquisition();
+    test_tracking_handoff();
     if (failures == 0) std::printf("host_selftest: PASS\n");
     return failures == 0 ? 0 : 1;
 }

@@ -143,6 +143,17 @@ int gsdr_acq_get_threshold(const gsdr_acq* acq, float* threshold);
  * out: nblocks*nprn results, attempt-major (host). */
 int gsdr_acq_run(gsdr_acq* acq, const void* iq_host, uint32_t nblocks, uint64_t stamp0, gsdr_acq_result* out);
 
+/* acquisition_core's dwell loop one block per call, as the reference block runs
+ * it (pcps_acquisition.cc:637-680, :781-829): dwell = the call's
+ * d_num_noncoherent_integrations_counter - 1 (0 <= dwell < max_dwells).  Dwell 0
+ * starts a device-resident |R|^2 grid per PRN, later dwells add this block's
+ * |R|^2 into it (volk_32f_x2_add_32f); the statistic is evaluated on the
+ * accumulated grid with the counter as the CFAR divisor (:534), against the
+ * max_dwells threshold (:908).  iq_host: one block (consumed_samples items);
+ * out: nprn results (num_dwells = dwell + 1).  Synchronous.  The caller keeps
+ * the dwell FSM (positive / next dwell / negative after max_dwells). */
+int gsdr_acq_run_dwell(gsdr_acq* acq, const void* iq_host, uint32_t dwell, uint64_t stamp, gsdr_acq_result* out);
+
 /* Device-resident form: iq_dev holds nblocks*max_dwells blocks, block j starting
  * at item j*block_stride_items.  Results are written to out_dev (device memory,
  * nblocks*nprn).  Asynchronous on stream; no host synchronisation. */
@@ -309,7 +320,7 @@ typedef struct gsdr_trk_conf
     uint32_t bit_synchronization_time_limit_s;
     int32_t pll_filter_order;
     int32_t dll_filter_order;
-    int32_t extend_correlation_symbols; /* only 1 in this version */
+    int32_t extend_correlation_symbols; /* coherent symbols per correlation after bit sync (state 3, :1989-2026) */
     int32_t cn0_samples;
     int32_t cn0_smoother_samples;
     int32_t carrier_lock_test_smoother_samples;

@@ -58,6 +58,16 @@ def correlate_kernel_bytes_per_block():
     return 8 * N * P * D + 16 * P * D
 
 
+def correlate_kernel_flops_per_block():
+    """Nominal FP32 work of the dominant kernel per block (SURVEY §8(d) F_acq's P*D
+    term): per (d, p) the code product, the N-point FFT, |.|^2 and the row
+    reductions, 5 N log2 N + 11 N."""
+    return P * D * (5 * N * math.log2(N) + 11 * N)
+
+
+FP32_PEAK = 157.3e12   # MI355X FP32 vector (= f32 MFMA) peak, MI355X_MICROARCH.md
+
+
 def trk_bytes_per_epoch():
     """B_trk = 8N + 8K per channel-epoch."""
     return 8 * N + 8 * TAPS
@@ -93,49 +103,114 @@ def make_workload(blocks, rank, periodic=False):
     return sats, iq, codes
 
 
+def rank_plan(world, rank, blocks_per_rank, channels):
+    """The job's shard map (gsdr.shard): one stream of
+    world * blocks_per_rank blocks per step; this rank's acquisition block span
+    and its tracking channels (c % world)."""
+    from gsdr import shard
+    total = world * blocks_per_rank
+    return {"total_blocks": total, "blocks": shard.block_range(total, world, rank),
+            "channels": [int(c) for c in shard.channels_of(channels, world, rank)]}
+
+
+def host_cpu_info():
+    """Threads the CPU baseline may use and what they are: the affinity set,
+    capped by OMP_NUM_THREADS (the GPU box sets it to the job's CPU share; nproc
+    there shows the whole machine)."""
+    aff = len(os.sched_getaffinity(0))
+    cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = min(aff, cap) if cap > 0 else aff
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"nproc": os.cpu_count(), "affinity": aff, "threads": threads, "cpu_model": model}
+
+
 def cpu_baseline(iq, codes, sats, budget_s=12.0):
-    """Oracle restatement on this host's CPU (1 thread): numpy pocketfft complex64
-    PCPS (acquisition_core + CFAR statistic) for all 32 PRNs x 81 bins of a block,
-    plus the C restatement of dll_pll_veml_tracking (generic VOLK correlator + loop)
-    for every channel's general_work call in the block."""
-    from oracle import pcps, trk
+    """The C++ CPU restatement (oracle/cpu_baseline.cc) on this host's cores: per
+    1 ms block the 32 PRN x 81 Doppler CFAR PCPS grid (own batched AVX2
+    mixed-radix FFT -- no FFTW3f / pocketfft on the image -- std::thread over
+    (Doppler bin, PRN group) tasks) plus one dll_pll_veml_tracking call per
+    channel (fused AVX2 resampler + rotator correlator feeding the oracle's
+    DLL/PLL restatement), on a bounded sample of blocks.  Also the per-core
+    correlator rate (N=4000, K=3) for the fairness check against the reference's
+    VOLK a_avx probe, 187 M channel-samples/s/core."""
+    import ctypes
+    from oracle import trk
+
+    info = host_cpu_info()
+    nt = info["threads"]
+    L = ctypes.CDLL(os.path.join(ROOT, "oracle", "build", "libcpubase.so"))
+    L.cpub_acq_create.restype = ctypes.c_void_p
+    L.cpub_acq_create.argtypes = [ctypes.c_int] * 3 + [ctypes.c_double, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    L.cpub_acq_run.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+    L.cpub_acq_destroy.argtypes = [ctypes.c_void_p]
+    L.cpub_trk_calls.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                 ctypes.c_int, ctypes.c_void_p]
+    L.cpub_corr.argtypes = ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                             ctypes.c_int] + [ctypes.c_float] * 4 + [ctypes.c_int])
     from gsdr import synth
-    wipe = pcps.doppler_wipeoffs(FS, N, DMAX, DSTEP, D)
-    cconj = np.conj(np.fft.fft(codes.astype(np.complex64), axis=1)).astype(np.complex64)
-    chans = []
+    codes_c = np.ascontiguousarray(codes, np.complex64)
+    h = L.cpub_acq_create(N, D, P, float(FS), DMAX, DSTEP, codes_c.ctypes.data)
+    nblk_data = len(iq) // N
+    # the workload is periodic over its blocks (bench --trk-stream construction),
+    # so channels read a doubled copy at their position modulo the period
+    iq2 = np.ascontiguousarray(np.concatenate([iq, iq]), np.complex64)
+    period = nblk_data * N
+    chans, firsts = [], []
     for s in sats:
         o = trk.Channel(trk_conf(1).view(trk.TRK_CONF_DTYPE))
         delay, dop = acq_result_for(s)
-        first = o.start(synth.gps_ca_chips(s.prn), delay, dop, 0, 0)
-        chans.append([o, first])
-    rec = np.zeros(1, trk.TRK_EPOCH_DTYPE)
-    L = trk._lib()
+        firsts.append(o.start(synth.gps_ca_chips(s.prn), delay, dop, 0, 0))
+        chans.append(o)
+    handles = (ctypes.c_void_p * len(chans))(*[o._h for o in chans])
+    recs = np.zeros(len(chans), trk.TRK_EPOCH_DTYPE)
+    out = np.zeros((P, 5), np.float32)
+    pos = np.array(firsts, np.int64)
 
     def one_block(b):
-        x = iq[b * N:(b + 1) * N]
-        X = np.fft.fft(x[None, :] * wipe, axis=1).astype(np.complex64)
-        for p in range(P):
-            R = np.fft.ifft(X * cconj[p][None, :], axis=1) * N
-            M = (R.real * R.real + R.imag * R.imag).astype(np.float32)
-            pcps.max_to_input_power_statistic(M)
-        for c in chans:
-            o, n = c
-            if n + N <= len(iq):
-                L.orc_trk_call(o._h, iq[n:].ctypes.data, n, rec.ctypes.data)
-                c[1] = n + int(rec["consumed"][0])
+        L.cpub_acq_run(h, iq[(b % nblk_data) * N:].ctypes.data, nt, out.ctypes.data)
+        rel = (pos % period).astype(np.uint64)
+        absn = pos.astype(np.uint64)
+        L.cpub_trk_calls(handles, len(chans), iq2.ctypes.data, rel.ctypes.data, absn.ctypes.data, nt, recs.ctypes.data)
+        pos[:] += recs["consumed"].astype(np.int64)
 
-    t0 = time.perf_counter()
     one_block(0)
-    t1 = time.perf_counter() - t0
-    nblk = int(max(1, min(len(iq) // N - 1, math.ceil(budget_s / max(t1, 1e-3)))))
     t0 = time.perf_counter()
-    for b in range(1, nblk + 1):
+    one_block(1)
+    t1 = time.perf_counter() - t0
+    nblk = int(max(2, min(4000, math.ceil(budget_s / max(t1, 1e-4)))))
+    t0 = time.perf_counter()
+    for b in range(2, nblk + 2):
         one_block(b)
     dt = time.perf_counter() - t0
-    return {"value": round(nblk * N / dt / 1e6, 5), "unit": "Msamples/s", "cores": 1, "kind": "port",
-            "sample": "%d blocks of 1 ms (4000 samples): 32 PRN x 81 Doppler CFAR PCPS (numpy pocketfft complex64) "
-                      "+ one dll_pll_veml_tracking call (C restatement: generic VOLK 3-tap correlator + DLL/PLL) "
-                      "for each of 8 channels; %.1f s on one host core" % (nblk, dt)}
+    detected = int(np.sum(out[:, 4] > 0))
+    L.cpub_acq_destroy(h)
+    # per-core correlator rate (1 thread, N = 4000, K = 3, L = 1023)
+    code = synth.gps_ca_chips(1).astype(np.float32)
+    shifts = np.array([-0.5, 0.0, 0.5], np.float32)
+    o6 = np.zeros(6, np.float32)
+    sig = np.ascontiguousarray(iq[:N], np.complex64)
+    reps = 2000
+    tc = time.perf_counter()
+    for _ in range(reps):
+        L.cpub_corr(o6.ctypes.data, sig.ctypes.data, code.ctypes.data, 1023, shifts.ctypes.data, 3, 0.3, 0.01, 0.1,
+                    float(np.float32(1.023e6 / FS)), N)
+    corr_rate = reps * N / (time.perf_counter() - tc) / 1e6
+    return {"value": round(nblk * N / dt / 1e6, 4), "unit": "Msamples/s", "cores": nt, "kind": "port",
+            "sample": "%d blocks of 1 ms (4000 samples) in %.1f s: 32 PRN x 81 Doppler CFAR PCPS per block "
+                      "(oracle/cpu_baseline.cc: own 8-lane AVX2 mixed-radix FFT, no FFTW3f/pocketfft on the image) "
+                      "+ one dll_pll_veml_tracking call for each of 8 channels (fused AVX2 correlator + DLL/PLL "
+                      "restatement), std::thread x %d" % (nblk, dt, nt),
+            "host": info, "stats_checked_prns": detected,
+            "per_core_correlator_Mchsps": round(corr_rate, 1),
+            "fairness": "per-core correlator %.0f M ch-samples/s (N=4000, K=3) vs the reference VOLK a_avx probe "
+                        "187 (BASELINE.md §2): %.2fx" % (corr_rate, corr_rate / 187.0)}
 
 
 def load_pmc_traffic():
@@ -149,6 +224,7 @@ def load_pmc_traffic():
         if f.startswith("pmc_") and f.endswith(".json"):
             try:
                 d = json.load(open(os.path.join(pdir, f)))
+                d["file"] = "profiles/" + f
                 best = d
             except Exception:
                 pass
@@ -172,11 +248,16 @@ def main():
                          "(2: one chain's forward spectra overlap the other's correlate grid; at most 3 with the "
                          "tracking stream, GPU_MAX_HW_QUEUES = 4)")
     ap.add_argument("--trk-stream", action="store_true",
-                    help="tracking follows one continuous stream (the batch repeated, Dopplers on whole cycles per "
-                         "batch): one tracking launch covers all timed steps instead of one launch per step")
+                    help="(default) tracking follows one continuous stream: the batch repeated end to end (Dopplers on "
+                         "whole cycles per batch, so the repetition is a continuous signal), one tracking launch "
+                         "covering all timed steps -- every channel converges as a receiver's would")
+    ap.add_argument("--trk-replay", action="store_true",
+                    help="re-track the same 64 ms from a saved start state every step (the pull-in transient each "
+                         "time; one tracking launch per step)")
     ap.add_argument("--only", choices=["acq", "trk"], default=None,
                     help="diagnostic: run only one of the two stages (the line is then not the metric)")
     args = ap.parse_args()
+    args.trk_stream = not args.trk_replay
 
     import torch
     import gsdr
@@ -193,20 +274,28 @@ def main():
         torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     B = args.blocks
-
-    sats, iq, codes = make_workload(B, rank, periodic=args.trk_stream)
+    W, K = args.warmup, args.steps
+    # One stream for the whole job: every rank ingests the full
+    # stream of world*B blocks per step; rank r acquires its block span
+    # (gsdr.shard.block_range) and tracks channels c % world == r over the whole
+    # span (gsdr.shard.channels_of).  No data-path collective.
+    plan = rank_plan(world, rank, B, CHANNELS)
+    total = plan["total_blocks"]
+    lo, hi = plan["blocks"]
+    my_ch = plan["channels"]
+    sats, iq, codes = make_workload(total, 0, periodic=True)
     iq_dev = torch.from_numpy(iq.view(np.float32).copy()).to(dev)
     res_dev = torch.zeros(B * P * gsdr.ACQ_RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
-    W, K = args.warmup, args.steps
+    nloc = max(1, len(my_ch))
     if args.trk_stream:
-        # the tracking stream: warmup + timed batches end to end
-        iq_long = iq_dev.repeat(W + K + 1)  # + one batch of slack for the last calls
-        trk_epochs = max(W, K) * B
+        # the tracking stream: warmup + timed steps end to end
+        iq_long = iq_dev.repeat(W + K + 1)  # + one step of slack for the last calls
+        trk_epochs = max(W, K) * total
     else:
         iq_long = iq_dev
-        trk_epochs = B
-    trk_out = torch.zeros(CHANNELS * trk_epochs * gsdr.TRK_EPOCH_DTYPE.itemsize, dtype=torch.uint8, device=dev)
-    trk_n = torch.zeros(CHANNELS, dtype=torch.int32, device=dev)
+        trk_epochs = total
+    trk_out = torch.zeros(nloc * trk_epochs * gsdr.TRK_EPOCH_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    trk_n = torch.zeros(nloc, dtype=torch.int32, device=dev)
 
     nch = max(1, args.acq_chains)
     assert B % nch == 0, "--blocks must be a multiple of --acq-chains"
@@ -217,35 +306,39 @@ def main():
                              device=local)
         a.set_local_codes(codes, np.arange(1, P + 1))
         acqs.append(a)
-    acq = acqs[0]
-    trk = gsdr.Tracking(trk_conf(CHANNELS), device=local)
+    trk = gsdr.Tracking(trk_conf(nloc), device=local) if len(my_ch) else None
     from gsdr import synth
-    for c, s in enumerate(sats):
+    for i, c in enumerate(my_ch):
+        s = sats[c]
         delay, dop = acq_result_for(s)
-        trk.start(c, s.prn, synth.gps_ca_chips(s.prn), delay, dop, 0, 0)
+        trk.start(i, s.prn, synth.gps_ca_chips(s.prn), delay, dop, 0, 0)
     # each handle launches on its own HIP stream (its own hardware queue).  The
     # tracking pool is a latency chain of one workgroup per channel that needs a
-    # whole CU; give it CHANNELS CUs (one per XCD for 8) and the acquisition grid
-    # the other 248, so neither waits for the other's workgroups to drain.
-    if args.cu_partition:
-        trk_mask, acq_mask = gsdr.cu_partition(args.trk_cus or CHANNELS)
+    # whole CU; --cu-partition gives it CUs of its own and the acquisition grid
+    # the rest, so neither waits for the other's workgroups to drain.
+    if args.cu_partition and trk is not None:
+        trk_mask, acq_mask = gsdr.cu_partition(args.trk_cus or nloc)
         trk.set_cu_mask(trk_mask)
         for a in acqs:
             a.set_cu_mask(acq_mask)
-    trk.save_state(0)
+    if trk is not None:
+        trk.save_state(0)
+    do_trk = args.only != "acq" and trk is not None
 
     def trk_stream_launch(nsteps):
-        # one launch: nsteps * B general_work calls per channel, continuing the stream
-        if args.only != "acq" and nsteps > 0:
-            trk.run_device(iq_long.data_ptr(), 0, (W + K + 1) * B * N, nsteps * B, trk_out.data_ptr(), trk_n.data_ptr())
+        # one launch: nsteps * total general_work calls per channel, continuing the stream
+        if do_trk and nsteps > 0:
+            trk.run_device(iq_long.data_ptr(), 0, (W + K + 1) * total * N, nsteps * total, trk_out.data_ptr(),
+                           trk_n.data_ptr())
 
     def step():
-        if args.only != "acq" and not args.trk_stream:
+        if do_trk and not args.trk_stream:
             trk.restore_state(0)
-            trk.run_device(iq_dev.data_ptr(), 0, B * N, B, trk_out.data_ptr(), trk_n.data_ptr())
+            trk.run_device(iq_dev.data_ptr(), 0, total * N, total, trk_out.data_ptr(), trk_n.data_ptr())
         if args.only != "trk":
             for i, a in enumerate(acqs):
-                a.run_device(iq_dev.data_ptr() + i * Bc * N * 8, Bc, N, i * Bc * N,
+                b0 = lo + i * Bc
+                a.run_device(iq_dev.data_ptr() + b0 * N * 8, Bc, N, b0 * N,
                              res_dev.data_ptr() + i * Bc * P * gsdr.ACQ_RESULT_DTYPE.itemsize)
 
     if args.trk_stream:
@@ -257,23 +350,26 @@ def main():
     res = res_dev.cpu().numpy().view(gsdr.ACQ_RESULT_DTYPE).reshape(B, P)
     det = {int(r["prn"]) for r in res[0] if r["positive"]}
     vis = {s.prn for s in sats}
-    ep_warm = max(W * B, 1) if args.trk_stream else B  # the warmup launch's max_epochs (record layout)
-    recs = trk_out.cpu().numpy().view(gsdr.TRK_EPOCH_DTYPE)[:CHANNELS * ep_warm].reshape(CHANNELS, ep_warm)
-    nrec = trk_n.cpu().numpy()
-    taps = np.stack([recs[c][nrec[c] - 1]["taps"][:6].view(np.complex64) for c in range(CHANNELS)])
-    prompt_ratio = float(np.median(np.abs(taps[:, 1]) / np.maximum(np.abs(taps[:, 0]), 1e-9)))
-    # carrier Doppler averaged over the last 16 calls (one call's value carries the
-    # PLL's per-epoch jitter at 40 Hz loop bandwidth); channels start from the
-    # 250 Hz acquisition grid, so some are still pulling in after 64 ms
-    dop_err = np.array([abs(np.mean(recs[c][max(nrec[c] - 16, 0):nrec[c]]["carrier_doppler_hz"]) - sats[c].doppler_hz)
-                        for c in range(CHANNELS)]) if nrec.min() > 0 else None
+    prompt_ratio, dop_err, nrec = None, None, np.zeros(1, np.int64)
+    if do_trk:
+        ep_warm = max(W * total, 1) if args.trk_stream else total  # the warmup launch's max_epochs (record layout)
+        recs = trk_out.cpu().numpy().view(gsdr.TRK_EPOCH_DTYPE)[:nloc * ep_warm].reshape(nloc, ep_warm)
+        nrec = trk_n.cpu().numpy()
+        taps = np.stack([recs[i][nrec[i] - 1]["taps"][:6].view(np.complex64) for i in range(nloc)])
+        prompt_ratio = float(np.median(np.abs(taps[:, 1]) / np.maximum(np.abs(taps[:, 0]), 1e-9)))
+        # carrier Doppler averaged over the last 16 calls (one call's value carries
+        # the PLL's per-epoch jitter at 40 Hz loop bandwidth)
+        if nrec.min() > 0:
+            dop_err = np.array([abs(np.mean(recs[i][max(nrec[i] - 16, 0):nrec[i]]["carrier_doppler_hz"]) -
+                                    sats[c].doppler_hz) for i, c in enumerate(my_ch)])
 
     if not args.no_profile_events:
         for a in acqs:
             a.set_profiling(True)
             a.read_profile()
-        trk.set_profiling(True)
-        trk.read_profile()
+        if trk is not None:
+            trk.set_profiling(True)
+            trk.read_profile()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -291,7 +387,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    trk_calls_timed = int(trk_n.cpu().numpy().min())
+    trk_calls_timed = int(trk_n.cpu().numpy().min()) if do_trk else 0
     stage_ms, stage_n = (np.zeros(4), np.zeros(4, np.uint32))
     trk_ms, trk_launches = 0.0, 0
     if not args.no_profile_events:
@@ -299,7 +395,8 @@ def main():
             ms_a, n_a = a.read_profile()
             stage_ms = stage_ms + ms_a
             stage_n = stage_n + n_a
-        trk_ms, trk_launches = trk.read_profile()
+        if trk is not None:
+            trk_ms, trk_launches = trk.read_profile()
 
     samples = world * args.steps * B * N
     value = samples / elapsed / 1e6
@@ -317,16 +414,18 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic (seeded GPS L1 C/A IQ, 8 visible PRNs at 45 dB-Hz + AWGN, per-rank shard)",
+        "data": "synthetic (seeded GPS L1 C/A IQ, 8 visible PRNs at 45 dB-Hz + AWGN; one stream per job)",
         "config": {
             "workload": "C2: GPS L1 C/A 4 Msps; per 1 ms block a 32 PRN x 81 Doppler (+-10 kHz, 250 Hz) CFAR PCPS "
                         "grid + closed-loop DLL/PLL tracking (3-tap E-P-L, dll_pll_veml_tracking) of 8 channels "
                         "over the same span",
             "blocks_per_step": B, "fs_sps": FS, "fft_size": N, "prns": P, "doppler_bins": D, "channels": CHANNELS,
-            "taps": TAPS, "item_type": "gr_complex", "parallelism": "blocks sharded per rank (dp%d)" % world,
+            "taps": TAPS, "item_type": "gr_complex",
+            "parallelism": "one stream of %d blocks per step: acquisition blocks [%d,%d) and channels %s on rank %d "
+                           "of %d (gsdr.shard), no data-path collective" % (total, lo, hi, my_ch, rank, world),
             "tracking": ("one continuous stream, one launch per timed region" if args.trk_stream
-                         else "64 ms re-tracked per step from a saved state, one launch per step"),
-            "cu_partition": ({"tracking": args.trk_cus or CHANNELS, "acquisition": 256 - (args.trk_cus or CHANNELS)}
+                         else "the step's span re-tracked from a saved state, one launch per step"),
+            "cu_partition": ({"tracking": args.trk_cus or nloc, "acquisition": 256 - (args.trk_cus or nloc)}
                              if args.cu_partition else None),
             "acq_chains": nch,
         },
@@ -344,16 +443,34 @@ def main():
         achieved = correlate_kernel_bytes_per_block() * blocks_per_launch * nch / corr_launch_s
         pmc = load_pmc_traffic()
         traffic = None
-        if pmc and pmc.get("kernel") == "acq_correlate_kernel" and pmc.get("blocks"):
+        if pmc and pmc.get("kernel") == "acq_correlate_kernel" and pmc.get("blocks") and pmc.get("hbm_bytes_per_launch"):
             # PMC HBM bytes of one launch over pmc["blocks"] blocks, per block x this launch's blocks
             traffic = pmc.get("hbm_bytes_per_launch") / pmc["blocks"] * blocks_per_launch
+        # The correlate kernel is VALU-issue bound, not HBM bound: its spectra are
+        # read from HBM once and re-served from L2 to the 32 PRN workgroups (PMC
+        # traffic below), and the packed-f32 FFT's issue slots set its time
+        # (DESIGN.md §5).  The roofline is therefore the FP32 vector peak, with the
+        # nominal FFT flops; the logical-byte HBM figure is kept alongside.
+        flops = correlate_kernel_flops_per_block() * blocks_per_launch * nch / corr_launch_s
         line["roofline"] = {
-            "bound": "hbm", "achieved": round(achieved / 1e9, 2), "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK, 4), "traffic": traffic,
-            "kernel": "acq_correlate_kernel", "avg_launch_us": round(corr_launch_s * 1e6, 2),
+            "bound": "valu", "achieved": round(flops / 1e12, 2), "peak": FP32_PEAK / 1e12, "unit": "TFLOP/s",
+            "frac": round(flops / FP32_PEAK, 4), "traffic": traffic,
+            "kernel": "acq_correlate_pk_kernel", "avg_launch_us": round(corr_launch_s * 1e6, 2),
             "blocks_per_launch": blocks_per_launch, "concurrent_launches": nch,
-            "algorithmic_bytes_per_launch": int(correlate_kernel_bytes_per_block() * blocks_per_launch),
+            "nominal_flops_per_launch": int(correlate_kernel_flops_per_block() * blocks_per_launch),
+            "hbm_logical": {"achieved": round(achieved / 1e9, 2), "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                            "frac": round(achieved / HBM_PEAK, 4),
+                            "algorithmic_bytes_per_launch": int(correlate_kernel_bytes_per_block() * blocks_per_launch)},
         }
+        if pmc:
+            kc = pmc.get("kernels", {}).get("acq_correlate_kernel", {}).get("counters", {})
+            if kc.get("SQ_INSTS_VALU") and pmc.get("blocks"):
+                line["roofline"]["pmc"] = {
+                    "source": pmc.get("file"),
+                    "valu_wave_instructions_per_block": round(kc["SQ_INSTS_VALU"] / pmc["blocks"]),
+                    "lds_bank_conflict_frac": round(kc.get("SQ_LDS_BANK_CONFLICT", 0) / max(kc.get("SQ_ACTIVE_INST_LDS", 1), 1), 3),
+                    "hbm_bytes_per_block": round(pmc["hbm_bytes_per_launch"] / pmc["blocks"]) if pmc.get("hbm_bytes_per_launch") else None,
+                }
         line["stages_us_per_launch"] = {
             "acq_forward": round(stage_ms[0] / max(stage_n[0], 1) * 1e3, 2),
             "acq_correlate": round(stage_ms[1] / max(stage_n[1], 1) * 1e3, 2),
@@ -364,7 +481,9 @@ def main():
         }
     line["acq_roof_frac_whole_step"] = round(acq_bytes_per_block() * B / (ms_per_step / 1e3) / HBM_PEAK, 4)
     line["check"] = {"visible": len(vis), "acquired_block0": len(vis & det),
-                     "median_prompt_over_early": round(prompt_ratio, 2), "trk_calls_per_channel": int(nrec.min()),
+                     "median_prompt_over_early": None if prompt_ratio is None else round(prompt_ratio, 2),
+                     "prompt_over_early_theory": round(1.0 / (1.0 - 0.25), 2),
+                     "trk_calls_per_channel": int(nrec.min()),
                      "trk_calls_per_channel_timed": trk_calls_timed,
                      "median_mean16_doppler_err_hz": None if dop_err is None else round(float(np.median(dop_err)), 2),
                      "channels_within_25hz": None if dop_err is None else int(np.sum(dop_err < 25.0))}
@@ -372,7 +491,8 @@ def main():
         line["cpu_baseline"] = cpu_baseline(iq, codes, sats)
     if rank == 0:
         print(json.dumps(line), flush=True)
-    trk.close()
+    if trk is not None:
+        trk.close()
     for a in acqs:
         a.close()
     if dist is not None:

@@ -16,6 +16,7 @@
 //   K_second          per (b,p), peak-ratio mode only: recompute row d*, second peak outside
 //                     the +-1 chip window with the reference's wrap      (:546-612)
 #include "acq_impl.h"
+#include "gsdr_stream_internal.h"
 
 namespace
 {
@@ -358,6 +359,33 @@ int gsdr_acq_run(gsdr_acq* a, const void* iq_host, uint32_t nblocks, uint64_t st
     const size_t bytes = (size_t)nblocks * a->K * a->consumed * item_bytes(a->conf.item_type);
     GSDR_HIP(hipMemcpyAsync(a->d_iq, iq_host, bytes, hipMemcpyHostToDevice, a->stream));
     int rc = dispatch(a, 0, a->d_iq, nblocks, a->consumed, stamp0, a->d_res, a->stream, 0);
+    if (rc != GSDR_OK) return rc;
+    GSDR_HIP(hipMemcpyAsync(out, a->d_res, (size_t)nblocks * a->nprn * sizeof(gsdr_acq_result), hipMemcpyDeviceToHost,
+        a->stream));
+    GSDR_HIP(hipStreamSynchronize(a->stream));
+    return GSDR_OK;
+}
+
+int gsdr_acq_run_stream(gsdr_acq* a, gsdr_stream* ring, uint64_t first_sample, uint32_t nblocks, uint64_t stamp0,
+    gsdr_acq_result* out)
+{
+    GSDR_REQUIRE(a && ring && out, GSDR_E_ARG, "gsdr_acq_run_stream: null argument");
+    GSDR_REQUIRE(a->nprn > 0, GSDR_E_STATE, "gsdr_acq_run_stream: set_local_codes first");
+    GSDR_REQUIRE(nblocks > 0 && nblocks <= a->conf.max_blocks, GSDR_E_ARG,
+        "gsdr_acq_run_stream: nblocks %u outside [1,%u]", nblocks, a->conf.max_blocks);
+    GSDR_REQUIRE(gsdr::stream_item_type(ring) == a->conf.item_type, GSDR_E_ARG,
+        "gsdr_acq_run_stream: ring item type %d != acquisition item type %d", gsdr::stream_item_type(ring),
+        a->conf.item_type);
+    std::lock_guard<std::mutex> lk(a->mu);
+    gsdr::DeviceGuard g(a->device);
+    const void* iq = nullptr;
+    int rc = gsdr::stream_view(ring, first_sample, (uint64_t)nblocks * a->K * a->consumed, &iq);
+    if (rc != GSDR_OK) return rc;
+    rc = gsdr::stream_acquire(ring, a->stream);
+    if (rc != GSDR_OK) return rc;
+    rc = dispatch(a, 0, iq, nblocks, a->consumed, stamp0, a->d_res, a->stream, 0);
+    if (rc != GSDR_OK) return rc;
+    rc = gsdr::stream_release(ring, a->stream);
     if (rc != GSDR_OK) return rc;
     GSDR_HIP(hipMemcpyAsync(out, a->d_res, (size_t)nblocks * a->nprn * sizeof(gsdr_acq_result), hipMemcpyDeviceToHost,
         a->stream));

@@ -27,7 +27,7 @@ namespace
 using gsdr::fft::Plan;
 
 // Default correlate variant at N = 4000 (see GSDR_PK_VARIANTS).
-constexpr int kDefaultCorrVariant4000 = 30;
+constexpr int kDefaultCorrVariant4000 = 31;
 
 // Default packed variant for an FFT size (0: none, the generic kernels).
 inline int default_pk_variant(uint32_t N)

@@ -1,0 +1,195 @@
+// Device IQ ring indexed by absolute sample count (SURVEY §8(b) gsdr_stream_push,
+// §8(f) rank 3, §7 H6): the input stream is uploaded once per GPU and every
+// consumer -- the acquisition grid, the tracking channel pool -- reads its window
+// in place by absolute sample index, the index dll_pll_veml_tracking itself uses
+// (nitems_read, dll_pll_veml_tracking.cc:1797,1818,2122) and pcps_acquisition's
+// sample stamp counts (pcps_acquisition.cc:968,1009).
+//
+// Layout: `cap` items at ring positions sample % cap, plus a mirror of the first
+// `window` positions after the end, so any window of up to `window` items is one
+// contiguous device span (no consumer handles the wrap).  Pushes run on the
+// ring's own copy stream; a consumer launch waits on the last push's event and
+// records a reader event that the next push waits on before it overwrites.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "gsdr_internal.h"
+#include "gsdr_stream_internal.h"
+
+struct gsdr_stream
+{
+    int device{0};
+    int item_type{GSDR_ITEM_GR_COMPLEX};
+    size_t item_bytes{8};
+    uint64_t cap{0};     // ring positions
+    uint64_t window{0};  // longest contiguous window (mirrored positions)
+    uint8_t* d_ring{nullptr};
+    bool started{false};
+    uint64_t base{0};  // absolute index of the first item pushed
+    uint64_t head{0};  // absolute index of the next item to push
+    hipStream_t copy{nullptr};
+    hipEvent_t pushed{nullptr};
+    hipEvent_t read{nullptr};  // the last consumer launch reading the ring
+    std::mutex mu;
+};
+
+namespace gsdr
+{
+int stream_item_type(const gsdr_stream* s) { return s->item_type; }
+
+int stream_view(gsdr_stream* s, uint64_t first, uint64_t n, const void** ptr)
+{
+    std::lock_guard<std::mutex> lk(s->mu);
+    GSDR_REQUIRE(s->started, GSDR_E_STATE, "gsdr_stream: nothing pushed yet");
+    const uint64_t oldest = s->head > s->cap ? std::max(s->base, s->head - s->cap) : s->base;
+    GSDR_REQUIRE(first >= oldest && first + n <= s->head, GSDR_E_ARG,
+        "gsdr_stream: window [%llu, %llu) outside the ring's [%llu, %llu)", (unsigned long long)first,
+        (unsigned long long)(first + n), (unsigned long long)oldest, (unsigned long long)s->head);
+    GSDR_REQUIRE(n <= s->window, GSDR_E_ARG, "gsdr_stream: window of %llu items exceeds the ring's %llu",
+        (unsigned long long)n, (unsigned long long)s->window);
+    *ptr = s->d_ring + (first % s->cap) * s->item_bytes;
+    return GSDR_OK;
+}
+
+int stream_span(gsdr_stream* s, uint64_t* first, uint64_t* n)
+{
+    std::lock_guard<std::mutex> lk(s->mu);
+    GSDR_REQUIRE(s->started, GSDR_E_STATE, "gsdr_stream: nothing pushed yet");
+    const uint64_t oldest = s->head > s->cap ? std::max(s->base, s->head - s->cap) : s->base;
+    const uint64_t lo = s->head > s->window ? std::max(oldest, s->head - s->window) : oldest;
+    *first = lo;
+    *n = s->head - lo;
+    return GSDR_OK;
+}
+
+int stream_acquire(gsdr_stream* s, hipStream_t consumer)
+{
+    GSDR_HIP(hipStreamWaitEvent(consumer, s->pushed, 0));
+    return GSDR_OK;
+}
+
+int stream_release(gsdr_stream* s, hipStream_t consumer)
+{
+    std::lock_guard<std::mutex> lk(s->mu);
+    // one reader event suffices: consumers of one ring are ordered by the caller
+    // (a later launch on another stream makes this event wait for the earlier one)
+    GSDR_HIP(hipStreamWaitEvent(consumer, s->read, 0));
+    GSDR_HIP(hipEventRecord(s->read, consumer));
+    return GSDR_OK;
+}
+}  // namespace gsdr
+
+namespace
+{
+size_t bytes_of(int it) { return it == GSDR_ITEM_CSHORT ? 4 : (it == GSDR_ITEM_IBYTE ? 2 : 8); }
+}  // namespace
+
+extern "C" {
+
+int gsdr_stream_create(int device, int item_type, uint64_t capacity_items, uint64_t max_window_items, gsdr_stream** out)
+{
+    GSDR_REQUIRE(out, GSDR_E_ARG, "gsdr_stream_create: null argument");
+    *out = nullptr;
+    GSDR_REQUIRE(item_type >= GSDR_ITEM_GR_COMPLEX && item_type <= GSDR_ITEM_IBYTE, GSDR_E_ARG,
+        "gsdr_stream_create: unknown item type %d", item_type);
+    GSDR_REQUIRE(capacity_items > 0 && max_window_items > 0 && max_window_items <= capacity_items, GSDR_E_ARG,
+        "gsdr_stream_create: need 0 < max_window_items <= capacity_items");
+    int ndev = 0;
+    GSDR_HIP(hipGetDeviceCount(&ndev));
+    GSDR_REQUIRE(device >= 0 && device < ndev, GSDR_E_ARG, "gsdr_stream_create: device %d of %d", device, ndev);
+    gsdr::DeviceGuard g(device);
+    auto* s = new (std::nothrow) gsdr_stream();
+    GSDR_REQUIRE(s, GSDR_E_ALLOC, "gsdr_stream_create: out of host memory");
+    s->device = device;
+    s->item_type = item_type;
+    s->item_bytes = bytes_of(item_type);
+    s->cap = capacity_items;
+    s->window = max_window_items;
+    hipError_t e = hipMalloc(&s->d_ring, (size_t)(s->cap + s->window) * s->item_bytes);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&s->copy, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&s->pushed, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&s->read, hipEventDisableTiming);
+    if (e != hipSuccess)
+        {
+            gsdr::set_error("gsdr_stream_create: %s", hipGetErrorString(e));
+            gsdr_stream_destroy(s);
+            return GSDR_E_ALLOC;
+        }
+    *out = s;
+    return GSDR_OK;
+}
+
+void gsdr_stream_destroy(gsdr_stream* s)
+{
+    if (!s) return;
+    gsdr::DeviceGuard g(s->device);
+    if (s->copy) (void)hipStreamSynchronize(s->copy);
+    if (s->read) (void)hipEventSynchronize(s->read);
+    if (s->pushed) (void)hipEventDestroy(s->pushed);
+    if (s->read) (void)hipEventDestroy(s->read);
+    if (s->copy) (void)hipStreamDestroy(s->copy);
+    if (s->d_ring) (void)hipFree(s->d_ring);
+    delete s;
+}
+
+int gsdr_stream_push(gsdr_stream* s, const void* iq_host, uint64_t first_sample, uint64_t n)
+{
+    GSDR_REQUIRE(s && (iq_host || n == 0), GSDR_E_ARG, "gsdr_stream_push: null argument");
+    std::lock_guard<std::mutex> lk(s->mu);
+    gsdr::DeviceGuard g(s->device);
+    if (!s->started)
+        {
+            s->started = true;
+            s->base = s->head = first_sample;
+        }
+    GSDR_REQUIRE(first_sample == s->head, GSDR_E_ARG,
+        "gsdr_stream_push: items must be contiguous (next is %llu, got %llu)", (unsigned long long)s->head,
+        (unsigned long long)first_sample);
+    GSDR_REQUIRE(n <= s->cap, GSDR_E_ARG, "gsdr_stream_push: %llu items exceed the ring capacity %llu",
+        (unsigned long long)n, (unsigned long long)s->cap);
+    if (n == 0) return GSDR_OK;
+    // overwrite only what no consumer launch still reads
+    GSDR_HIP(hipStreamWaitEvent(s->copy, s->read, 0));
+    const auto* src = static_cast<const uint8_t*>(iq_host);
+    uint64_t done = 0;
+    while (done < n)
+        {
+            const uint64_t pos = (s->head + done) % s->cap;
+            const uint64_t len = std::min<uint64_t>(n - done, s->cap - pos);
+            GSDR_HIP(hipMemcpyAsync(s->d_ring + pos * s->item_bytes, src + done * s->item_bytes, len * s->item_bytes,
+                hipMemcpyHostToDevice, s->copy));
+            if (pos < s->window)
+                {
+                    // mirror of the first `window` positions after the end
+                    const uint64_t mlen = std::min<uint64_t>(len, s->window - pos);
+                    GSDR_HIP(hipMemcpyAsync(s->d_ring + (s->cap + pos) * s->item_bytes, src + done * s->item_bytes,
+                        mlen * s->item_bytes, hipMemcpyHostToDevice, s->copy));
+                }
+            done += len;
+        }
+    GSDR_HIP(hipEventRecord(s->pushed, s->copy));
+    s->head += n;
+    return GSDR_OK;
+}
+
+int gsdr_stream_span(gsdr_stream* s, uint64_t* first_sample, uint64_t* n_items)
+{
+    GSDR_REQUIRE(s && first_sample && n_items, GSDR_E_ARG, "gsdr_stream_span: null argument");
+    return gsdr::stream_span(s, first_sample, n_items);
+}
+
+int gsdr_stream_window(gsdr_stream* s, uint64_t first_sample, uint64_t n_items, const void** iq_dev)
+{
+    GSDR_REQUIRE(s && iq_dev, GSDR_E_ARG, "gsdr_stream_window: null argument");
+    int rc = gsdr::stream_view(s, first_sample, n_items, iq_dev);
+    if (rc != GSDR_OK) return rc;
+    gsdr::DeviceGuard g(s->device);
+    GSDR_HIP(hipEventSynchronize(s->pushed));
+    return GSDR_OK;
+}
+
+}  // extern "C"

@@ -34,6 +34,7 @@
 #include <vector>
 
 #include "gsdr_internal.h"
+#include "gsdr_stream_internal.h"
 
 // The reference loop is compiled for x86-64 without FMA contraction; keep every
 // a*b+c of the restatement as two roundings.
@@ -1861,6 +1862,29 @@ int gsdr_trk_run_device(gsdr_trk* k, const void* iq_dev, uint64_t iq_first_sampl
     gsdr::DeviceGuard g(k->device);
     hipStream_t s = stream ? (hipStream_t)stream : k->stream;
     return launch(k, iq_dev, iq_first_sample, iq_items, max_epochs, out_dev, n_out_dev, s);
+}
+
+int gsdr_trk_run_stream(gsdr_trk* k, gsdr_stream* ring, uint32_t max_epochs, gsdr_trk_epoch* out_dev,
+    uint32_t* n_out_dev, void* stream)
+{
+    GSDR_REQUIRE(k && ring && out_dev && n_out_dev, GSDR_E_ARG, "gsdr_trk_run_stream: null argument");
+    GSDR_REQUIRE(gsdr::stream_item_type(ring) == k->conf.item_type, GSDR_E_ARG,
+        "gsdr_trk_run_stream: ring item type %d != tracking item type %d", gsdr::stream_item_type(ring),
+        k->conf.item_type);
+    std::lock_guard<std::mutex> lk(k->mu);
+    gsdr::DeviceGuard g(k->device);
+    hipStream_t s = stream ? (hipStream_t)stream : k->stream;
+    uint64_t first = 0, n = 0;
+    int rc = gsdr::stream_span(ring, &first, &n);
+    if (rc != GSDR_OK) return rc;
+    const void* iq = nullptr;
+    rc = gsdr::stream_view(ring, first, n, &iq);
+    if (rc != GSDR_OK) return rc;
+    rc = gsdr::stream_acquire(ring, s);
+    if (rc != GSDR_OK) return rc;
+    rc = launch(k, iq, first, n, max_epochs, out_dev, n_out_dev, s);
+    if (rc != GSDR_OK) return rc;
+    return gsdr::stream_release(ring, s);
 }
 
 int gsdr_trk_run(gsdr_trk* k, const void* iq_host, uint64_t iq_first_sample, uint64_t iq_items, uint32_t max_epochs,

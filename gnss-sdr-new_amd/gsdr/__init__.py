@@ -39,6 +39,8 @@ EXPORTED = [
     "gsdr_trk_conf_default", "gsdr_trk_create", "gsdr_trk_destroy", "gsdr_trk_start", "gsdr_trk_stop",
     "gsdr_trk_run_device", "gsdr_trk_run", "gsdr_trk_get_channel", "gsdr_trk_save_state", "gsdr_trk_restore_state",
     "gsdr_trk_set_profiling", "gsdr_trk_read_profile", "gsdr_acq_set_cu_mask", "gsdr_trk_set_cu_mask",
+    "gsdr_acq_run_dwell", "gsdr_acq_run_stream", "gsdr_trk_run_stream",
+    "gsdr_stream_create", "gsdr_stream_destroy", "gsdr_stream_push", "gsdr_stream_span", "gsdr_stream_window",
     "gsdr_acq_set_step_two", "gsdr_acq_get_step_two_threshold", "gsdr_acq_run_step_two",
     "gsdr_trk_set_data_code",
 ]
@@ -210,6 +212,15 @@ def load():
     L.gsdr_acq_get_step_two_threshold.argtypes = [P, P]
     L.gsdr_acq_run_step_two.argtypes = [P, P, U32, P, P, P, U64, P]
     L.gsdr_trk_set_cu_mask.argtypes = [P, P, I]
+    L.gsdr_acq_run_dwell.argtypes = [P, P, U32, U64, P]
+    L.gsdr_stream_create.argtypes = [I, I, U64, U64, P]
+    L.gsdr_stream_destroy.argtypes = [P]
+    L.gsdr_stream_destroy.restype = None
+    L.gsdr_stream_push.argtypes = [P, P, U64, U64]
+    L.gsdr_stream_span.argtypes = [P, P, P]
+    L.gsdr_stream_window.argtypes = [P, U64, U64, P]
+    L.gsdr_acq_run_stream.argtypes = [P, P, U64, U32, U64, P]
+    L.gsdr_trk_run_stream.argtypes = [P, P, U32, P, P, P]
     _lib = L
     return L
 
@@ -307,6 +318,22 @@ class Acquisition:
         iq = self._items(iq)
         out = np.zeros(nblocks * self.nprn, ACQ_RESULT_DTYPE)
         _check(load().gsdr_acq_run(self._h, _ptr(iq), int(nblocks), int(stamp0), _ptr(out)))
+        return out.reshape(nblocks, self.nprn)
+
+    def run_dwell(self, iq, dwell, stamp=0):
+        """acquisition_core's per-call dwell (gsdr_acq_run_dwell): one block of host
+        IQ added to the device grid of the attempt (dwell 0 starts it) ->
+        structured array [nprn]."""
+        iq = self._items(iq)
+        out = np.zeros(self.nprn, ACQ_RESULT_DTYPE)
+        _check(load().gsdr_acq_run_dwell(self._h, _ptr(iq), int(dwell), int(stamp), _ptr(out)))
+        return out
+
+    def run_stream(self, ring, first_sample, nblocks=1, stamp0=0):
+        """nblocks attempts read in place from a Stream (device IQ ring) from
+        absolute sample first_sample -> structured array [nblocks, nprn]."""
+        out = np.zeros(nblocks * self.nprn, ACQ_RESULT_DTYPE)
+        _check(load().gsdr_acq_run_stream(self._h, ring._h, int(first_sample), int(nblocks), int(stamp0), _ptr(out)))
         return out.reshape(nblocks, self.nprn)
 
     def set_step_two(self, num_doppler_bins_step2=4, doppler_step2=125.0, pfa2=0.0):
@@ -505,6 +532,12 @@ class Tracking:
                                           int(max_epochs), ctypes.c_void_p(out_dev_ptr), ctypes.c_void_p(nout_dev_ptr),
                                           ctypes.c_void_p(stream_ptr)))
 
+    def run_stream(self, ring, max_epochs, out_dev_ptr, nout_dev_ptr, stream_ptr=0):
+        """Advance the channels over a Stream's newest contiguous window
+        (gsdr_trk_run_stream); asynchronous."""
+        _check(load().gsdr_trk_run_stream(self._h, ring._h, int(max_epochs), ctypes.c_void_p(out_dev_ptr),
+                                          ctypes.c_void_p(nout_dev_ptr), ctypes.c_void_p(stream_ptr)))
+
     def channel(self, ch):
         st, nxt, dop, cn0 = ctypes.c_int32(), ctypes.c_uint64(), ctypes.c_double(), ctypes.c_double()
         _check(load().gsdr_trk_get_channel(self._h, int(ch), ctypes.byref(st), ctypes.byref(nxt), ctypes.byref(dop),
@@ -529,6 +562,45 @@ class Tracking:
         n = ctypes.c_uint32()
         _check(load().gsdr_trk_read_profile(self._h, ctypes.byref(ms), ctypes.byref(n)))
         return ms.value, n.value
+
+
+class Stream:
+    """Device IQ ring indexed by absolute sample count (gsdr_stream_*): push the
+    input stream once, read it in place from Acquisition.run_stream and
+    Tracking.run_stream."""
+
+    def __init__(self, item_type, capacity_items, max_window_items, device=0):
+        self._h = ctypes.c_void_p()
+        _check(load().gsdr_stream_create(int(device), int(item_type), int(capacity_items), int(max_window_items),
+                                         ctypes.byref(self._h)))
+        self.item_type = int(item_type)
+
+    def close(self):
+        if self._h:
+            load().gsdr_stream_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def push(self, iq, first_sample):
+        iq = np.ascontiguousarray(iq, _ITEM_NP[self.item_type])
+        n = len(iq) if self.item_type == ITEM_GR_COMPLEX else len(iq) // 2
+        _check(load().gsdr_stream_push(self._h, _ptr(iq), int(first_sample), int(n)))
+        return n
+
+    def span(self):
+        f, n = ctypes.c_uint64(), ctypes.c_uint64()
+        _check(load().gsdr_stream_span(self._h, ctypes.byref(f), ctypes.byref(n)))
+        return f.value, n.value
+
+    def window(self, first_sample, n_items):
+        p = ctypes.c_void_p()
+        _check(load().gsdr_stream_window(self._h, int(first_sample), int(n_items), ctypes.byref(p)))
+        return p.value
 
 
 def cu_partition(n_reserved, n_cus=256):

@@ -67,6 +67,41 @@ int gsdr_abi_version(void);
 int gsdr_device_count(int* count);
 
 /* ======================================================================== */
+/* Device IQ ring indexed by absolute sample count                           */
+/* ======================================================================== */
+/*
+ * The input stream uploaded once per GPU and read in place by every consumer --
+ * the acquisition grid and the tracking channel pool -- by absolute sample
+ * index: the nitems_read index dll_pll_veml_tracking consumes by
+ * (dll_pll_veml_tracking.cc:1797,1818,2122) and the sample counter
+ * pcps_acquisition stamps its results with (pcps_acquisition.cc:968,1009).  In a
+ * GNU Radio flowgraph one block pushes each general_work call's items; the
+ * acquisition and tracking blocks then launch on windows of the ring instead of
+ * copying their own host buffers.
+ *
+ * capacity_items ring positions (sample % capacity) plus a mirror of the first
+ * max_window_items positions, so every window of up to max_window_items items
+ * is one contiguous device span.  The ring keeps the last capacity_items items.
+ */
+typedef struct gsdr_stream gsdr_stream;
+
+int gsdr_stream_create(int device, int item_type, uint64_t capacity_items, uint64_t max_window_items, gsdr_stream** out);
+void gsdr_stream_destroy(gsdr_stream* stream);
+/* Append n items (item_type of the ring) whose first one is absolute input sample
+ * first_sample; pushes are contiguous (first_sample = the previous push's end;
+ * the first push sets the origin).  Asynchronous H2D on the ring's copy stream,
+ * ordered after every consumer launch issued so far (no overwrite of data in
+ * use); n <= capacity_items. */
+int gsdr_stream_push(gsdr_stream* stream, const void* iq_host, uint64_t first_sample, uint64_t n);
+/* The longest contiguous window ending at the newest item: [*first_sample,
+ * *first_sample + *n_items). */
+int gsdr_stream_span(gsdr_stream* stream, uint64_t* first_sample, uint64_t* n_items);
+/* Device pointer of items [first_sample, first_sample + n_items) after the pushes
+ * so far have landed (synchronises with the copy stream); GSDR_E_ARG if the window
+ * is not (or no longer) in the ring. */
+int gsdr_stream_window(gsdr_stream* stream, uint64_t first_sample, uint64_t n_items, const void** iq_dev);
+
+/* ======================================================================== */
 /* Acquisition — PCPS (pcps_acquisition)                                     */
 /* ======================================================================== */
 
@@ -159,6 +194,15 @@ int gsdr_acq_run_dwell(gsdr_acq* acq, const void* iq_host, uint32_t dwell, uint6
  * nblocks*nprn).  Asynchronous on stream; no host synchronisation. */
 int gsdr_acq_run_device(gsdr_acq* acq, const void* iq_dev, uint32_t nblocks, uint64_t block_stride_items,
     uint64_t stamp0, gsdr_acq_result* out_dev, void* stream);
+
+/* Ring form: nblocks attempts on the ring's items from absolute sample
+ * first_sample on (the nblocks*max_dwells consecutive blocks gsdr_acq_run would
+ * read from a contiguous host buffer), results to out_host (nblocks*nprn), sample
+ * stamps from stamp0 as in gsdr_acq_run.  The launch waits for the ring's
+ * pushes on the device (no host synchronisation before it) and is ordered before
+ * later pushes overwrite the window.  Synchronous (results on the host). */
+int gsdr_acq_run_stream(gsdr_acq* acq, gsdr_stream* stream, uint64_t first_sample, uint32_t nblocks, uint64_t stamp0,
+    gsdr_acq_result* out_host);
 
 /* The reference's acquisition grid dump (pcps_acquisition.cc:408-508): writes the
  * |R|^2 grid of PRN slot `prn_slot` for one host block into grid_host
@@ -395,6 +439,15 @@ int gsdr_trk_stop(gsdr_trk* trk, int ch);
  * count (device).  Asynchronous on stream (NULL = the handle's own stream). */
 int gsdr_trk_run_device(gsdr_trk* trk, const void* iq_dev, uint64_t iq_first_sample, uint64_t iq_items,
     uint32_t max_epochs, gsdr_trk_epoch* out_dev, uint32_t* n_out_dev, void* stream);
+
+/* Ring form: every active channel advances by up to max_epochs calls over the
+ * ring's newest contiguous window (gsdr_stream_span); a channel whose next call
+ * needs items not pushed yet stops and continues on a later call, so pushing the
+ * stream in any chunking gives the records of one contiguous run.  Asynchronous on
+ * stream (NULL = the handle's own), ordered after the ring's pushes and before the
+ * pushes that would overwrite the window. */
+int gsdr_trk_run_stream(gsdr_trk* trk, gsdr_stream* ring, uint32_t max_epochs, gsdr_trk_epoch* out_dev,
+    uint32_t* n_out_dev, void* stream);
 
 /* Host form of the same call (synchronous): copies the records back. */
 int gsdr_trk_run(gsdr_trk* trk, const void* iq_host, uint64_t iq_first_sample, uint64_t iq_items,

@@ -1000,6 +1000,29 @@ int orc_trk_call_taps(orc_trk* t, const float* taps, uint64_t nitems_read, gsdr_
     return trk_call(t, NULL, taps, nitems_read, r);
 }
 
+/* The inputs do_correlation_step passes to the multicorrelator for the channel's
+ * next call (:1064-1089), for an external correlator feeding orc_trk_call_taps
+ * (the CPU baseline's AVX2 correlator): p[0] rem_carr_phase_rad, p[1]
+ * carr_phase_step_rad, p[2] carr_phase_rate_step_rad, p[3] rem_code_phase x spc,
+ * p[4] code_phase_step x spc, p[5] code_phase_rate_step x spc; *n_samples =
+ * vector_length; *code / *code_samples / shifts[0..n_taps) the replica and taps;
+ * returns n_taps. */
+int orc_trk_corr_params(const orc_trk* t, float* p, int* n_samples, const float** code, int* code_samples,
+    float* shifts)
+{
+    p[0] = t->rem_carr_phase_rad;
+    p[1] = (float)t->carrier_phase_step_rad;
+    p[2] = (float)t->carrier_phase_rate_step_rad;
+    p[3] = (float)t->rem_code_phase_chips * (float)t->code_samples_per_chip;
+    p[4] = (float)t->code_phase_step_chips * (float)t->code_samples_per_chip;
+    p[5] = (float)t->code_phase_rate_step_chips * (float)t->code_samples_per_chip;
+    *n_samples = (int)t->p.vector_length;
+    *code = t->code;
+    *code_samples = t->code_samples;
+    for (int k = 0; k < t->n_taps; ++k) shifts[k] = t->shifts[k];
+    return t->n_taps;
+}
+
 /* taps_in: 12 floats -- five complex tap slots (n_taps used) + the data prompt */
 static void correlate_or_copy(orc_trk* t, const float* in, const float* taps_in)
 {

@@ -31,11 +31,13 @@ def summarise(root, match):
     return {c: sum(v) / len(v) for c, v in vals.items()}
 
 
-KERNELS = {"acq_correlate_kernel": "acq_correlate", "acq_forward_kernel": "acq_forward"}
+KERNELS = {"acq_correlate_kernel": "acq_correlate", "acq_forward_kernel": "acq_forward",
+           "acq_argmax_pk_kernel": "acq_argmax", "trk_kernel": "trk_kernel", "corr_kernel": "corr_kernel"}
 
 
 def as_json(root):
-    out = {"source": "rocprofv3 --kernel-trace --pmc, profiles/acq_driver.py --what acq (C2, 64 blocks)",
+    out = {"source": "rocprofv3 --kernel-trace --pmc: profiles/acq_driver.py --what acq / --what trk (C2, 64 "
+                     "blocks: acquisition; 8-channel tracking over 64 ms) and profiles/configs_bench.py --only C3 (corr_kernel)",
            "blocks": 64, "kernels": {}}
     for name, match in KERNELS.items():
         s = summarise(root, match)

@@ -1,0 +1,115 @@
+"""Device IQ ring indexed by absolute sample count (gsdr_stream_*, SURVEY §8(b)
+gsdr_stream_push / §8(f) rank 3): the stream pushed in GNU-Radio-sized chunks and
+read in place by the acquisition grid (gsdr_acq_run_stream) and the tracking pool
+(gsdr_trk_run_stream) gives results identical to the contiguous-buffer paths --
+acquisition byte-identical to gsdr_acq_run on the same blocks, tracking records
+identical to one contiguous gsdr_trk_run over the whole stream (the tracking
+block consumes by nitems_read, dll_pll_veml_tracking.cc:1797,1818,2122, so a
+call that needs items not pushed yet simply waits for the next push)."""
+import numpy as np
+import pytest
+import torch
+
+import gsdr
+from gsdr import synth
+
+pytestmark = pytest.mark.gpu
+
+FS, N = 4000000, 4000
+
+
+def _conf(nch, item=gsdr.ITEM_GR_COMPLEX):
+    c = gsdr.trk_conf_default()
+    c["fs_in"] = FS
+    c["pll_bw_hz"] = 40.0
+    c["dll_bw_hz"] = 4.0
+    c["max_channels"] = nch
+    c["item_type"] = item
+    return c
+
+
+def _acq_result(s):
+    tau = s.code_delay_chips / 1.023e6 * FS
+    return float(round(tau) % N), float(250 * round(s.doppler_hz / 250))
+
+
+@pytest.mark.parametrize("item", [gsdr.ITEM_GR_COMPLEX, gsdr.ITEM_CSHORT])
+def test_ring_matches_contiguous(item):
+    ms = 160
+    sats = synth.random_constellation(6, seed_offset=21)
+    x = synth.gps_l1_iq(FS, ms * N, sats, seed_offset=21)
+    if item == gsdr.ITEM_CSHORT:
+        q = np.clip(np.rint(x.view(np.float32) * 40.0), -32767, 32767).astype(np.int16)
+        items = q
+        per_item = 2
+    else:
+        items = x
+        per_item = 1
+    codes = np.stack([synth.gps_ca_sampled(s.prn, FS) for s in sats])
+    prns = np.array([s.prn for s in sats])
+    acq = gsdr.Acquisition(FS, N, 10000, 250, pfa=0.01, max_prns=len(prns), item_type=item)
+    acq.set_local_codes(codes, prns)
+    # reference tracking: one contiguous run over the whole stream
+    ref = gsdr.Tracking(_conf(len(sats), item))
+    ring_trk = gsdr.Tracking(_conf(len(sats), item))
+    for c, s in enumerate(sats):
+        d, f = _acq_result(s)
+        ref.start(c, s.prn, synth.gps_ca_chips(s.prn), d, f, 0, 0)
+        ring_trk.start(c, s.prn, synth.gps_ca_chips(s.prn), d, f, 0, 0)
+    ref_recs, ref_n = ref.run(items, 0, ms + 2)
+    ring = gsdr.Stream(item, capacity_items=64 * N, max_window_items=40 * N)
+    dev = torch.device("cuda", 0)
+    me = 64
+    out = torch.zeros(len(sats) * me * gsdr.TRK_EPOCH_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    nout = torch.zeros(len(sats), dtype=torch.int32, device=dev)
+    got = [[] for _ in sats]
+    acq_done = 0
+    chunk = 4096
+    pushed = 0
+    total = ms * N
+    while pushed < total:
+        n = min(chunk, total - pushed)
+        ring.push(items[pushed * per_item:(pushed + n) * per_item], pushed)
+        pushed += n
+        # acquisition of every block completed by this push, read in place
+        while (acq_done + 1) * N <= pushed:
+            b = acq_done
+            r_ring = acq.run_stream(ring, b * N, 1, stamp0=(b + 1) * N)
+            r_host = acq.run(items[b * N * per_item:(b + 1) * N * per_item], 1, stamp0=(b + 1) * N)
+            assert r_ring.tobytes() == r_host.tobytes(), b
+            acq_done += 1
+        ring_trk.run_stream(ring, me, out.data_ptr(), nout.data_ptr())
+        torch.cuda.synchronize(dev)
+        recs = out.cpu().numpy().view(gsdr.TRK_EPOCH_DTYPE).reshape(len(sats), me)
+        cnt = nout.cpu().numpy()
+        for c in range(len(sats)):
+            got[c].extend(recs[c, :cnt[c]].copy())
+    assert acq_done == ms
+    for c in range(len(sats)):
+        g = np.array(got[c], dtype=gsdr.TRK_EPOCH_DTYPE)
+        r = ref_recs[c, :ref_n[c]]
+        assert len(g) == len(r) and len(g) >= ms - 2, (c, len(g), len(r))
+        assert g.tobytes() == r.tobytes(), c
+    ring.close()
+
+
+def test_ring_errors():
+    ring = gsdr.Stream(gsdr.ITEM_GR_COMPLEX, capacity_items=8 * N, max_window_items=4 * N)
+    x = np.zeros(3 * N, np.complex64)
+    ring.push(x, 1000)
+    assert ring.span() == (1000, 3 * N)
+    with pytest.raises(gsdr.GsdrError):
+        ring.push(x, 5)  # not contiguous
+    ring.push(x, 1000 + 3 * N)
+    ring.push(x, 1000 + 6 * N)  # 9 N pushed, capacity 8 N: the oldest N dropped
+    assert ring.span() == (1000 + 5 * N, 4 * N)
+    with pytest.raises(gsdr.GsdrError):
+        ring.window(1000, N)  # overwritten
+    with pytest.raises(gsdr.GsdrError):
+        ring.window(1000 + 2 * N, 5 * N)  # longer than the mirrored window
+    assert ring.window(1000 + 4 * N, 4 * N)
+    acq = gsdr.Acquisition(FS, N, 5000, 500, pfa=0.01, max_prns=1, item_type=gsdr.ITEM_CSHORT)
+    acq.set_local_codes(synth.gps_ca_sampled(1, FS)[None], [1])
+    with pytest.raises(gsdr.GsdrError):
+        acq.run_stream(ring, 1000 + 5 * N, 1)  # item type mismatch
+    ring.close()

@@ -44,8 +44,10 @@ def test_cpp_replica_and_acq_conf_match_oracle(tmp_path):
     src = tmp_path / "probe.cc"
     src.write_text(PROBE)
     exe = tmp_path / "probe"
-    subprocess.check_call(["g++", "-std=c++17", "-O1", "-I", HOST, "-I", os.path.join(ROOT, "include"), str(src),
-                           os.path.join(HOST, "gnss_replicas.cc"), os.path.join(HOST, "acq_conf.cc"), "-o", str(exe)])
+    subprocess.check_call(["g++", "-std=c++17", "-O1", "-ffp-contract=off", "-I", HOST, "-I",
+                           os.path.join(ROOT, "include"), "-Wa,-I" + os.path.join(ROOT, "gnss-sdr-new_amd", "gsdr", "data"),
+                           str(src), os.path.join(HOST, "gnss_replicas.cc"), os.path.join(HOST, "galileo_e1_codes.cc"),
+                           os.path.join(HOST, "acq_conf.cc"), "-o", str(exe)])
     lines = subprocess.check_output([str(exe)], text=True).splitlines()
     for prn in range(1, 33):
         got = np.array(lines[prn - 1].split(), np.int32)
@@ -65,7 +67,8 @@ def test_host_selftest_on_gpu():
     if not os.path.exists(exe):
         subprocess.check_call(["make", "-C", HOST])
     cap = os.path.join(ROOT, "tests", "golden", "GPS_L1_CA_ID_1_Fs_4Msps_2ms.dat")
-    r = subprocess.run([exe, cap], capture_output=True, text=True, timeout=120)
+    gal = os.path.join(ROOT, "tests", "golden", "Galileo_E1_ID_1_Fs_4Msps_8ms.dat")
+    r = subprocess.run([exe, cap, gal], capture_output=True, text=True, timeout=120)
     print(r.stdout, r.stderr)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "host_selftest: PASS" in r.stdout

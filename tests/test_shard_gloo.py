@@ -1,7 +1,10 @@
 """Multi-process (world_size 2, gloo, CPU) coverage of the sharded path: block
-and channel partitions tile the work, per-rank acquisition of its block span
-(oracle restatement) merged on the host equals the single-process result, and
-the benchmark's barrier + max-over-ranks timing reduction."""
+and channel partitions tile the work, each rank runs the shard bench.rank_plan
+gives it (the map bench.py and the engine launches use: one stream, block span
+per rank, channels c % world) -- per-rank acquisition of its block span and
+per-rank tracking of its channels (oracle restatement) merged on the host equal
+the single-process results -- and the benchmark's barrier + max-over-ranks
+timing reduction."""
 import os
 import socket
 
@@ -16,7 +19,10 @@ from oracle import pcps
 
 FS, N, DMAX, DSTEP = 2000000, 2000, 5000, 500
 PRNS = (3, 7, 19)
-BLOCKS = 5
+BLOCKS_PER_RANK = 3
+BLOCKS = 2 * BLOCKS_PER_RANK
+TRK_CH = 3          # channels tracked (PRNS), sharded c % world
+TRK_EPOCHS = 4
 
 
 def _stream():
@@ -37,13 +43,45 @@ def _acq_blocks(x, lo, hi):
     return out
 
 
+def _track(x, channels):
+    """Oracle tracking of the given channels over the stream (the engine's
+    per-rank channel pool)."""
+    from oracle import trk
+    sats = synth.random_constellation(3, seed_offset=7, cn0_dbhz=55.0, max_doppler=4000.0, prns=PRNS)
+    out = []
+    for c in channels:
+        s = sats[c]
+        ch = trk.Channel(_trk_conf())
+        tau = s.code_delay_chips / 1.023e6 * FS
+        first = ch.start(synth.gps_ca_chips(s.prn), float(round(tau) % N), float(DSTEP * round(s.doppler_hz / DSTEP)),
+                         0, 0)
+        recs, _ = ch.run(x, 0, first, TRK_EPOCHS)
+        out.append(np.array(recs["taps"][:, :6]).copy())
+    return out
+
+
+def _trk_conf():
+    from oracle import trk
+    c = np.zeros(1, trk.TRK_CONF_DTYPE)
+    trk._lib().orc_trk_conf_default(c.ctypes.data)
+    c["fs_in"] = FS
+    c["max_channels"] = 1
+    return c
+
+
 def _worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
+        import bench
         x = _stream()
-        lo, hi = shard.block_range(BLOCKS, world, rank)
+        plan = bench.rank_plan(world, rank, BLOCKS_PER_RANK, TRK_CH)
+        assert plan["total_blocks"] == BLOCKS
+        lo, hi = plan["blocks"]
         mine = torch.from_numpy(_acq_blocks(x, lo, hi))
+        trk_mine = _track(x, plan["channels"])
+        trk_all = [None] * world
+        dist.all_gather_object(trk_all, trk_mine)
         # host-side result merge (object gather: spans differ in length)
         gathered = [None] * world
         dist.all_gather_object(gathered, mine.numpy())
@@ -55,7 +93,7 @@ def _worker(rank, world, port, q):
         t = torch.tensor([1.0 + rank], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         if rank == 0:
-            q.put((gathered, all_ch, float(t.item())))
+            q.put((gathered, all_ch, float(t.item()), trk_all))
     finally:
         dist.destroy_process_group()
 
@@ -92,7 +130,7 @@ def test_two_rank_gloo_matches_single_process():
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    gathered, all_ch, tmax = q.get(timeout=240)
+    gathered, all_ch, tmax, trk_all = q.get(timeout=240)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -104,3 +142,9 @@ def test_two_rank_gloo_matches_single_process():
     assert tmax == 2.0
     recs = shard.merge_channels([[("r0", c) for c in all_ch[0]], [("r1", c) for c in all_ch[1]]], 12, world)
     assert [r[1] for r in recs] == list(range(12))
+    # tracking: channel c on rank c % 2, merged == one process tracking every channel
+    merged_trk = shard.merge_channels(trk_all, TRK_CH, world)
+    single_trk = _track(_stream(), list(range(TRK_CH)))
+    for a, b in zip(merged_trk, single_trk):
+        assert a.shape == (TRK_EPOCHS, 6)
+        np.testing.assert_array_equal(a, b)

@@ -1887,6 +1887,28 @@ int gsdr_trk_run_stream(gsdr_trk* k, gsdr_stream* ring, uint32_t max_epochs, gsd
     return gsdr::stream_release(ring, s);
 }
 
+int gsdr_trk_run_stream_host(gsdr_trk* k, gsdr_stream* ring, uint32_t max_epochs, gsdr_trk_epoch* out_host,
+    uint32_t* n_out_host)
+{
+    GSDR_REQUIRE(k && ring && out_host && n_out_host, GSDR_E_ARG, "gsdr_trk_run_stream_host: null argument");
+    {
+        std::lock_guard<std::mutex> lk(k->mu);
+        gsdr::DeviceGuard g(k->device);
+        int rc = ensure_out(k, max_epochs);
+        if (rc != GSDR_OK) return rc;
+    }
+    int rc = gsdr_trk_run_stream(k, ring, max_epochs, k->d_out, k->d_nout, nullptr);
+    if (rc != GSDR_OK) return rc;
+    std::lock_guard<std::mutex> lk(k->mu);
+    gsdr::DeviceGuard g(k->device);
+    GSDR_HIP(hipMemcpyAsync(n_out_host, k->d_nout, k->conf.max_channels * sizeof(uint32_t), hipMemcpyDeviceToHost,
+        k->stream));
+    GSDR_HIP(hipMemcpyAsync(out_host, k->d_out, (size_t)k->conf.max_channels * max_epochs * sizeof(gsdr_trk_epoch),
+        hipMemcpyDeviceToHost, k->stream));
+    GSDR_HIP(hipStreamSynchronize(k->stream));
+    return GSDR_OK;
+}
+
 int gsdr_trk_run(gsdr_trk* k, const void* iq_host, uint64_t iq_first_sample, uint64_t iq_items, uint32_t max_epochs,
     gsdr_trk_epoch* out_host, uint32_t* n_out_host)
 {

@@ -39,7 +39,7 @@ EXPORTED = [
     "gsdr_trk_conf_default", "gsdr_trk_create", "gsdr_trk_destroy", "gsdr_trk_start", "gsdr_trk_stop",
     "gsdr_trk_run_device", "gsdr_trk_run", "gsdr_trk_get_channel", "gsdr_trk_save_state", "gsdr_trk_restore_state",
     "gsdr_trk_set_profiling", "gsdr_trk_read_profile", "gsdr_acq_set_cu_mask", "gsdr_trk_set_cu_mask",
-    "gsdr_acq_run_dwell", "gsdr_acq_run_stream", "gsdr_trk_run_stream",
+    "gsdr_acq_run_dwell", "gsdr_acq_run_stream", "gsdr_trk_run_stream", "gsdr_trk_run_stream_host",
     "gsdr_stream_create", "gsdr_stream_destroy", "gsdr_stream_push", "gsdr_stream_span", "gsdr_stream_window",
     "gsdr_acq_set_step_two", "gsdr_acq_get_step_two_threshold", "gsdr_acq_run_step_two",
     "gsdr_trk_set_data_code",
@@ -221,6 +221,7 @@ def load():
     L.gsdr_stream_window.argtypes = [P, U64, U64, P]
     L.gsdr_acq_run_stream.argtypes = [P, P, U64, U32, U64, P]
     L.gsdr_trk_run_stream.argtypes = [P, P, U32, P, P, P]
+    L.gsdr_trk_run_stream_host.argtypes = [P, P, U32, P, P]
     _lib = L
     return L
 

@@ -70,7 +70,7 @@ size_t AcquisitionService::pending() const
 // One batched acquisition_core over all pending requests; each request is
 // answered once (the channel re-arms it for another attempt, as the channel FSM
 // re-arms its acquisition block after a negative result).
-void AcquisitionService::run_grid()
+void AcquisitionService::run_grid(gsdr_stream* ring, uint64_t first_sample)
 {
     std::vector<Request> reqs;
     {
@@ -94,7 +94,9 @@ void AcquisitionService::run_grid()
         d_codes_dirty = true;
     }
     std::vector<gsdr_acq_result> res(reqs.size());
-    const int rc = gsdr_acq_run(d_engine, d_buffer.data(), 1, d_sample_counter, res.data());
+    // sample stamp: the counter after the block (pcps_acquisition.cc:1009, :1019)
+    const int rc = ring ? gsdr_acq_run_stream(d_engine, ring, first_sample, 1, first_sample + d_consumed, res.data())
+                        : gsdr_acq_run(d_engine, d_buffer.data(), 1, d_sample_counter, res.data());
     ++d_grids;
     for (size_t i = 0; i < reqs.size(); ++i)
         {
@@ -129,4 +131,23 @@ int AcquisitionService::work(const void* in, int ninput_items)
                 }
         }
     return used;
+}
+
+int AcquisitionService::work_ring(gsdr_stream* ring, uint64_t head)
+{
+    if (!d_ring_started)
+        {
+            d_ring_started = true;
+            d_ring_cursor = head;
+            return 0;
+        }
+    int blocks = 0;
+    while (d_ring_cursor + d_consumed <= head)
+        {
+            run_grid(ring, d_ring_cursor);
+            d_ring_cursor += d_consumed;
+            d_sample_counter = d_ring_cursor;
+            ++blocks;
+        }
+    return blocks;
 }

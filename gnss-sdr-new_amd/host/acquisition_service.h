@@ -47,6 +47,12 @@ public:
     // without any pending request are skipped without a launch.
     int work(const void* in, int ninput_items);
 
+    // Device-ring form (gsdr_stream): the stream is pushed into the
+    // GPU's IQ ring once (by whoever ingests it); the service runs its grids in
+    // place on the ring's blocks [cursor, head), block after block, with no host
+    // copy of its own.  The first call sets the block grid's origin at `head`.
+    int work_ring(gsdr_stream* ring, uint64_t head);
+
     float threshold() const { return d_threshold; }
     uint64_t sample_counter() const { return d_sample_counter; }
     uint64_t grids_run() const { return d_grids; }
@@ -59,7 +65,8 @@ private:
         std::vector<std::complex<float>> code;
         Callback done;
     };
-    void run_grid();
+    // grid over the pending requests on the current block: host buffer or ring
+    void run_grid(gsdr_stream* ring = nullptr, uint64_t first_sample = 0);
 
     Acq_Conf d_conf;
     uint32_t d_max;
@@ -73,6 +80,8 @@ private:
     uint32_t d_fill{0};
     uint64_t d_sample_counter{0};
     uint64_t d_grids{0};
+    bool d_ring_started{false};
+    uint64_t d_ring_cursor{0};  // absolute sample index of the next block on the ring
     mutable std::mutex d_mu;
 };
 

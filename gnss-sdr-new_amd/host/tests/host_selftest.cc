@@ -34,6 +34,7 @@
 #include "gnss_tracking_mi355x.h"
 #include "gps_l1_ca_pcps_acquisition_mi355x.h"
 #include "hip_multicorrelator_real_codes.h"
+#include "tracking_pool.h"
 
 namespace
 {
@@ -807,6 +808,102 @@ void test_tracking_handoff()
         e.outputs, e.doppler, e.cn0, e.prompt_i, e.prompt_q, e.loss);
 }
 
+// The receiver on the device IQ ring: the stream pushed once into
+// the GPU's ring in 4096-item chunks; the batched acquisition service runs its
+// grids in place on the ring (answers identical to the host-buffer service) and
+// the tracking pool, started from the positive answers' Gnss_Synchro, advances
+// over the ring after every push.
+void test_receiver_on_ring()
+{
+    const double fs = 4000000.0;
+    const double sigma = 1.0;
+    const double amp = std::sqrt(2.0 * std::pow(10.0, 5.0) / fs) * sigma;
+    const std::vector<float> bits = {1, -1, -1, -1, 1, -1, 1, 1};
+    SynthSat a{gps_l1_ca_code_gen_float(1), 1.023e6, 1575.42e6, 524.3, 1680.0, amp, {}, bits, 0.02};
+    SynthSat b{gps_l1_ca_code_gen_float(7), 1.023e6, 1575.42e6, 2100.8, -3250.0, amp, {}, bits, 0.02};
+    const auto x = synth_stream({a, b}, fs, static_cast<size_t>(fs * 1.6), 17, sigma);
+    InMemoryConfiguration config = gps_acq_config();
+    config.set_property("Acquisition_1C.pfa", "0.01");
+    config.set_property("Acquisition_1C.doppler_max", "5000");
+    config.set_property("Acquisition_1C.doppler_step", "250");
+    config.set_property("Tracking_1C.pll_bw_hz", "40.0");
+    config.set_property("Tracking_1C.dll_bw_hz", "4.0");
+    config.set_property("Tracking_1C.pull_in_time_s", "0");
+    Acq_Conf aconf;
+    aconf.ms_per_code = 1;
+    aconf.SetFromConfiguration(&config, "Acquisition_1C", 1023000.0, 2000000.0);
+    Dll_Pll_Conf tconf;
+    tconf.SetFromConfiguration(&config, "Tracking_1C");
+    tconf.vector_length = 4000;
+    tconf.track_pilot = false;
+    gsdr_stream* ring = nullptr;
+    EXPECT(gsdr_stream_create(0, GSDR_ITEM_GR_COMPLEX, 64 * 4000, 32 * 4000, &ring) == GSDR_OK, "ring");
+    if (!ring) return;
+    AcquisitionService svc_ring(aconf, 4, 0), svc_host(aconf, 4, 0);
+    TrackingPool pool(tconf, GSDR_SIGNAL_GPS_1C, 4, ring, 0);
+    const uint32_t prns[3] = {1, 7, 20};
+    std::vector<std::vector<std::complex<float>>> codes;
+    std::vector<Gnss_Synchro> gs(3);
+    struct Ans
+    {
+        gsdr_acq_result r;
+        bool pos;
+    };
+    std::vector<Ans> ans_ring(3), ans_host(3);
+    std::vector<int> answered(3, 0);
+    uint64_t head = 0;
+    for (uint32_t ch = 0; ch < 3; ++ch)
+        {
+            codes.push_back(gps_l1_ca_code_gen_complex_sampled(prns[ch], 4000000));
+            gs[ch].System = 'G';
+            gs[ch].Signal[0] = '1';
+            gs[ch].Signal[1] = 'C';
+            gs[ch].PRN = prns[ch];
+            gs[ch].Channel_ID = static_cast<int32_t>(ch);
+            svc_ring.request(ch, prns[ch], codes[ch].data(), [&](uint32_t c, const gsdr_acq_result& r, bool pos) {
+                ans_ring[c] = {r, pos};
+                answered[c] = 1;
+                if (pos)
+                    {
+                        gs[c].Acq_delay_samples = r.acq_delay_samples;
+                        gs[c].Acq_doppler_hz = r.doppler_hz;
+                        gs[c].Acq_samplestamp_samples = r.samplestamp;
+                        pool.start(c, &gs[c], head);
+                    }
+            });
+            svc_host.request(ch, prns[ch], codes[ch].data(),
+                [&](uint32_t c, const gsdr_acq_result& r, bool pos) { ans_host[c] = {r, pos}; });
+        }
+    std::vector<int> outputs(3, 0);
+    std::vector<double> last_dop(3, 0.0);
+    svc_ring.work_ring(ring, 0);  // origin of the ring's block grid
+    size_t pos = 0;
+    while (pos < x.size())
+        {
+            const size_t n = std::min<size_t>(4096, x.size() - pos);
+            if (gsdr_stream_push(ring, x.data() + pos, pos, n) != GSDR_OK) break;
+            pos += n;
+            head = pos;
+            svc_ring.work_ring(ring, head);
+            svc_host.work(x.data() + pos - n, static_cast<int>(n));
+            pool.advance([&](uint32_t slot, const Gnss_Synchro& o) {
+                if (o.Flag_valid_symbol_output) ++outputs[slot];
+                last_dop[slot] = o.Carrier_Doppler_hz;
+            });
+        }
+    for (int c = 0; c < 3; ++c)
+        EXPECT(answered[c] && std::memcmp(&ans_ring[c].r, &ans_host[c].r, sizeof(gsdr_acq_result)) == 0,
+            "ring acquisition answer == host-buffer answer");
+    EXPECT(ans_ring[0].pos && ans_ring[1].pos && !ans_ring[2].pos, "PRN 1 and 7 acquired, PRN 20 not");
+    EXPECT(outputs[0] > 8 && outputs[1] > 8, "tracking pool: bit-synchronised outputs on both channels");
+    EXPECT(std::abs(last_dop[0] - 1680.0) < 3.0 && std::abs(last_dop[1] + 3250.0) < 3.0,
+        "tracking pool: Doppler converged on both channels");
+    std::printf("receiver on ring: acq PRN1 %d PRN7 %d PRN20 %d; pool outputs %d / %d, doppler %.2f / %.2f Hz\n",
+        ans_ring[0].pos ? 1 : 0, ans_ring[1].pos ? 1 : 0, ans_ring[2].pos ? 1 : 0, outputs[0], outputs[1], last_dop[0],
+        last_dop[1]);
+    gsdr_stream_destroy(ring);
+}
+
 void test_multicorrelator(const std::vector<std::complex<float>>& capture)
 {
     const int n = 4000;
@@ -884,6 +981,7 @@ int main(int argc, char** argv)
         }
     test_beidou_acquisition();
     test_tracking_handoff();
+    test_receiver_on_ring();
     if (failures == 0) std::printf("host_selftest: PASS\n");
     return failures == 0 ? 0 : 1;
 }

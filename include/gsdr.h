@@ -449,6 +449,11 @@ int gsdr_trk_run_device(gsdr_trk* trk, const void* iq_dev, uint64_t iq_first_sam
 int gsdr_trk_run_stream(gsdr_trk* trk, gsdr_stream* ring, uint32_t max_epochs, gsdr_trk_epoch* out_dev,
     uint32_t* n_out_dev, void* stream);
 
+/* Ring form with the records copied back to the host (synchronous; the
+ * handle's own stream and record buffers): the tracking pool service's call. */
+int gsdr_trk_run_stream_host(gsdr_trk* trk, gsdr_stream* ring, uint32_t max_epochs, gsdr_trk_epoch* out_host,
+    uint32_t* n_out_host);
+
 /* Host form of the same call (synchronous): copies the records back. */
 int gsdr_trk_run(gsdr_trk* trk, const void* iq_host, uint64_t iq_first_sample, uint64_t iq_items,
     uint32_t max_epochs, gsdr_trk_epoch* out_host, uint32_t* n_out_host);

@@ -24,12 +24,10 @@ def _signal(fs, N, prn, doppler, delay_chips, cn0=55.0, seed=0, code=None):
     return synth.gps_l1_iq(fs, N, sats, seed_offset=seed)
 
 
-def _galileo_like_code(L=8184, seed=4):
-    """Stand-in +-1 replica with Galileo E1's 2-samples-per-chip length (the kernel is
-    code-agnostic; the real E1 memory codes are not needed for kernel parity)."""
-    rng = np.random.default_rng(seed)
-    chips = np.where(rng.random(L // 2) < 0.5, -1.0, 1.0).astype(np.float32)
-    return np.repeat(chips, 2)
+def _galileo_code(prn=11):
+    """Galileo E1-B tracking replica: the ICD memory code as sinBOC(1,1) at 2 samples
+    per chip (galileo_e1_code_gen_sinboc11_float, galileo_e1_signal_replica.cc:100-111)."""
+    return synth.gal_e1_sinboc11(prn).astype(np.float32)
 
 
 @pytest.mark.parametrize("assoc", [gsdr.ASSOC_GENERIC, gsdr.ASSOC_AVX])
@@ -59,7 +57,7 @@ CASES = [
 
 @pytest.mark.parametrize("name,fs,N,L,spc,shifts_chips", CASES)
 def test_taps_vs_generic_and_exact(name, fs, N, L, spc, shifts_chips):
-    code = synth.gps_ca_chips(5) if L == 1023 else _galileo_like_code(L)
+    code = synth.gps_ca_chips(5) if L == 1023 else _galileo_code()
     shifts = np.array(shifts_chips, np.float32) * spc
     corr = gsdr.Correlator(2, N, max_taps=8)
     corr.set_local_code_and_taps(0, code, shifts)

@@ -241,7 +241,14 @@ def _open_loop_sig(g, iq, code, data_code, fs, acq_dop, shifts_chips, spc, chip_
         x = iq[n0:n0 + vl]
         ref = volk.multicorrelator_real_codes(x, code, shifts, rem_carr, carr_step, rem_code, code_step, vl)
         got = g["taps"][e][:2 * len(shifts)].view(np.complex64)
-        worst = max(worst, vnorm_rel(got, ref))
+        # at large N (C3: 16000, C5: 25000/100000 samples) the generic rotator's own
+        # fp32 phase drift is of the order of the 1e-4 bar, so the
+        # distance to the oracle is taken beyond the oracle's own distance to the
+        # float64 evaluation of the same correlation, and the taps must also sit
+        # within 1e-4 of that float64 value
+        exact = volk.multicorrelator_real_codes_exact(x, code, shifts, rem_carr, carr_step, rem_code, code_step, vl)
+        assert vnorm_rel(got, exact) <= 1e-4, (e, vnorm_rel(got, exact))
+        worst = max(worst, vnorm_rel(got, ref) - (vnorm_rel(ref, exact) if vl > 8000 else 0.0))
         if data_code is not None:
             refd = volk.multicorrelator_real_codes(x, data_code, shifts[iP:iP + 1], rem_carr, carr_step, rem_code,
                                                    code_step, vl)

@@ -33,6 +33,7 @@
 #include <new>
 #include <vector>
 
+#include "fft_pk.h"
 #include "gsdr_internal.h"
 #include "gsdr_stream_internal.h"
 
@@ -52,6 +53,9 @@ constexpr int kMaxSmoother = 32;             // Dll_Pll_Conf::smoother_length ca
 constexpr int kSpl = 8;                       // samples per lane per correlation chunk
 constexpr int kWinCore = kSpl * kTrkThreads;  // 4096: the next call's window staged in LDS
 constexpr int kHalo = 16;                     // slack around the predicted next start
+constexpr int kStreamRow = 64 * 16;           // bytes one wave's global_load_lds_dwordx4 writes
+constexpr int kCodeMargin = 32;
+constexpr int kTimingSlots = 8;               // GSDR_TRK_TIMING record per call               // replica samples copied on each side of the LDS replica
 
 // MATH_CONSTANTS.h:47-50
 constexpr double kGnssPi = 3.1415926535898;
@@ -242,8 +246,9 @@ struct Prep  // lane-0 -> workgroup broadcast of one call's NCO
     int64_t off;
     int32_t go;
     int32_t woff;  // >= 0: this call's samples are in the LDS window at that offset
-    int32_t fast;  // every code index of the call lies in [-L, 2L): branch-free wrap
+    int32_t wrap;  // code index range of the call: 2 within the replica's margins, 1 within [-L, 2L), 0 general
     int32_t narrow;  // the call uses the narrow tap shifts
+    int32_t pf_ok;   // streamed call: chunk 0 is in the buffer prefetched during the previous update
     // high_dyn: rotator rate term and resampler rate (do_correlation_step, :1069-1075),
     // taps 1..K-1 as sample-shifted copies of tap 0 (32f_xn_high_dynamics_resampler_32f_xn.h:84-91)
     int32_t hd;
@@ -366,9 +371,39 @@ __device__ inline void clear_tracking_vars(TrkHot& t)  // :1192-1213
     t.hist_head = 0;
 }
 
+// Sequential float sums over the buffer elements (the estimators' loops, in the
+// reference's element order): every lane of wave 0 reads the per-element terms
+// back from LDS (same address on all lanes) and adds them in order.
+template <int NS>
+__device__ __forceinline__ void seq_sums(const float* terms, int stride, int n, float (&sum)[NS])
+{
+    __builtin_amdgcn_wave_barrier();
+    for (int q = 0; q < NS; ++q) sum[q] = 0.0F;
+    int i = 0;
+    for (; i + 4 <= n; i += 4)
+        {
+            float4 v[NS];
+#pragma unroll
+            for (int q = 0; q < NS; ++q) v[q] = *reinterpret_cast<const float4*>(terms + q * stride + i);
+#pragma unroll
+            for (int q = 0; q < NS; ++q) sum[q] += v[q].x;
+#pragma unroll
+            for (int q = 0; q < NS; ++q) sum[q] += v[q].y;
+#pragma unroll
+            for (int q = 0; q < NS; ++q) sum[q] += v[q].z;
+#pragma unroll
+            for (int q = 0; q < NS; ++q) sum[q] += v[q].w;
+        }
+    for (; i < n; ++i)
+#pragma unroll
+        for (int q = 0; q < NS; ++q) sum[q] += terms[q * stride + i];
+}
+
 // cn0_and_tracking_lock_status (:970-1056) with cn0_m2m4_estimator and
-// carrier_lock_detector (lock_detectors.cc:90-148); wave 0, lane = element.
-__device__ inline int cn0_and_lock(const TrkConst& c, TrkHot& t, float2* pbuf, double coh, int lane)
+// carrier_lock_detector (lock_detectors.cc:90-148); wave 0, lane = element,
+// sums in element order through `scratch` (4 x kMaxCn0 floats of LDS).
+__device__ inline int cn0_and_lock(const TrkConst& c, TrkHot& t, float2* pbuf, float (*scratch)[kMaxCn0], double coh,
+    int lane)
 {
     const int n = c.cn0_samples;
     if (t.cn0_estimation_counter < n)
@@ -386,13 +421,13 @@ __device__ inline int cn0_and_lock(const TrkConst& c, TrkHot& t, float2* pbuf, d
     const float a_i = fabsf(ei.x);
     const float aux_i = ei.y * ei.y + ei.x * ei.x;
     const float aux2_i = aux_i * aux_i;
-    float psig = 0.0F, m2 = 0.0F, m4 = 0.0F;
-    for (int i = 0; i < n; i++)
-        {
-            psig += lane_f(a_i, i);
-            m2 += lane_f(aux_i, i);
-            m4 += lane_f(aux2_i, i);
-        }
+    scratch[0][lane] = a_i;
+    scratch[1][lane] = aux_i;
+    scratch[2][lane] = aux2_i;
+    scratch[3][lane] = ei.x * ei.x;  // EVM: sum of squared in-phase prompts
+    float sums[4];
+    seq_sums<4>(&scratch[0][0], kMaxCn0, n, sums);
+    float psig = sums[0], m2 = sums[1], m4 = sums[2];
     const float fn = (float)n;
     psig /= fn;
     psig = psig * psig;
@@ -428,20 +463,19 @@ __device__ inline int cn0_and_lock(const TrkConst& c, TrkHot& t, float2* pbuf, d
             return 0;
         }
     // EVM (fork indicator, :1027-1053)
-    const float sq_i = ei.x * ei.x;
-    float s = 0;
-    for (int i = 0; i < n; i++) s = s + lane_f(sq_i, i);
+    float s = sums[3];
     float d = s / fn;
     d = sqrtf(d);
     const float ea = fabsf(ei.x / d) - 1.0F;
     const float eb = fabsf(ei.y / d) - 0.0F;
     const float aa_i = ea * ea, bb_i = eb * eb;
-    s = 0;
-    for (int i = 0; i < n; i++)
-        {
-            s = s + lane_f(aa_i, i);
-            s = s + lane_f(bb_i, i);
-        }
+    __builtin_amdgcn_wave_barrier();
+    float* flat = &scratch[0][0];  // 2 x kMaxCn0 floats, interleaved: s = s + aa_i; s = s + bb_i in element order
+    flat[2 * lane] = aa_i;
+    flat[2 * lane + 1] = bb_i;
+    float s2[1];
+    seq_sums<1>(flat, 0, 2 * n, s2);
+    s = s2[0];
     t.evm = sqrt((double)(s / fn / 1.0F));
     return 1;
 }
@@ -589,7 +623,10 @@ struct EpochOut
 
 // save_correlation_results (:1288-1400): secondary-code wipe-off of the tap
 // accumulators, data-symbol accumulation (NH wipe-off / pilot data prompt).
-__device__ inline void save_correlation_results(const TrkConst& c, TrkHot& t, const float2 (&taps)[kMaxTrkTaps + 1])
+// epl: the taps at c.iE / c.iP / c.iL (summed from LDS by run-time index, so no
+// private array is indexed at run time)
+__device__ inline void save_correlation_results(const TrkConst& c, TrkHot& t, const float2 (&taps)[kMaxTrkTaps + 1],
+    const float2 (&epl)[3])
 {
     float sg = 1.0F;
     if (c.secondary)
@@ -615,10 +652,10 @@ __device__ inline void save_correlation_results(const TrkConst& c, TrkHot& t, co
             acc(t.VE_accu, taps[0], sg);
             acc(t.VL_accu, taps[4], sg);
         }
-    acc(t.E_accu, taps[c.iE], sg);
-    acc(t.P_accu, taps[c.iP], sg);
-    acc(t.L_accu, taps[c.iL], sg);
-    const float2 pd = c.track_pilot ? taps[kMaxTrkTaps] : taps[c.iP];
+    acc(t.E_accu, epl[0], sg);
+    acc(t.P_accu, epl[1], sg);
+    acc(t.L_accu, epl[2], sg);
+    const float2 pd = c.track_pilot ? taps[kMaxTrkTaps] : epl[1];
     if (c.symbols_per_bit > 1)
         {
             if (c.data_sec_len > 0)
@@ -641,8 +678,16 @@ __device__ inline void save_correlation_results(const TrkConst& c, TrkHot& t, co
 
 // One general_work call after the correlation (taps given; slot kMaxTrkTaps is
 // the pilot-tracking data prompt): states 2 and 4.
+// GSDR_TRK_TIMING: wall-clock probes inside the loop update (slots 4-6 of the record)
+__device__ __forceinline__ void tprobe(uint64_t* pr, int i)
+{
+    if (pr) pr[i] = wall_clock64();
+}
+
 __device__ inline void after_correlation(const TrkConst& c, TrkHot& t, TrkChan* gc, LoopFilter& lf, float2* pbuf,
-    const float2 (&taps)[kMaxTrkTaps + 1], uint64_t nitems_read, int lane, EpochOut& o)
+    float (*scratch)[kMaxCn0], const float2 (&taps)[kMaxTrkTaps + 1], const float2 (&epl)[3], uint64_t nitems_read,
+    int lane, EpochOut& o,
+    uint64_t* pr = nullptr)
 {
     o.flags = 0;
     o.prompt_i = 0.0;
@@ -654,13 +699,15 @@ __device__ inline void after_correlation(const TrkConst& c, TrkHot& t, TrkChan* 
                     t.VE_accu = taps[0];
                     t.VL_accu = taps[4];
                 }
-            t.E_accu = taps[c.iE];
-            t.P_accu = taps[c.iP];
-            t.L_accu = taps[c.iL];
+            t.E_accu = epl[0];
+            t.P_accu = epl[1];
+            t.L_accu = epl[2];
             t.spc = c.early_late_space_chips;
             if (nitems_read < c.acq_sample_stamp || nitems_read - c.acq_sample_stamp >= c.bit_sync_span)
                 t.carrier_lock_fail_counter = 300000;
-            if (!cn0_and_lock(c, t, pbuf, c.code_period, lane))
+            const int locked = cn0_and_lock(c, t, pbuf, scratch, c.code_period, lane);
+            tprobe(pr, 0);
+            if (!locked)
                 {
                     clear_tracking_vars(t);
                     if (c.track_pilot) t.P_data_accu = make_float2(0.f, 0.f);
@@ -671,12 +718,14 @@ __device__ inline void after_correlation(const TrkConst& c, TrkHot& t, TrkChan* 
                 {
                     int next_state = 0;
                     run_dll_pll(c, t, lf);
+                    tprobe(pr, 1);
                     update_tracking_vars(c, t, gc);
+                    tprobe(pr, 2);
                     if (!t.pull_in_transitory)
                         {
                             if (c.secondary || c.symbols_per_bit > 1)
                                 {
-                                    circ_push(t, taps[c.iP]);
+                                    circ_push(t, epl[1]);
                                     if (t.circ_size >= c.sec_len) next_state = acquire_secondary(c, t);
                                 }
                             else
@@ -710,7 +759,7 @@ __device__ inline void after_correlation(const TrkConst& c, TrkHot& t, TrkChan* 
         }
     else if (t.state == 3)  // coherent integration (:1989-2026)
         {
-            save_correlation_results(c, t, taps);
+            save_correlation_results(c, t, taps, epl);
             update_tracking_vars(c, t, gc);
             if (t.current_data_symbol == 0)
                 {
@@ -728,8 +777,10 @@ __device__ inline void after_correlation(const TrkConst& c, TrkHot& t, TrkChan* 
         }
     else  // state 4
         {
-            save_correlation_results(c, t, taps);
-            if (!cn0_and_lock(c, t, pbuf, c.code_period * (double)c.extend_correlation_symbols, lane))
+            save_correlation_results(c, t, taps, epl);
+            const int locked = cn0_and_lock(c, t, pbuf, scratch, c.code_period * (double)c.extend_correlation_symbols, lane);
+            tprobe(pr, 0);
+            if (!locked)
                 {
                     clear_tracking_vars(t);
                     if (c.track_pilot) t.P_data_accu = make_float2(0.f, 0.f);
@@ -739,7 +790,9 @@ __device__ inline void after_correlation(const TrkConst& c, TrkHot& t, TrkChan* 
             else
                 {
                     run_dll_pll(c, t, lf);
+                    tprobe(pr, 1);
                     update_tracking_vars(c, t, gc);
+                    tprobe(pr, 2);
                     if (!t.acc_carrier_phase_initialized)
                         {
                             t.acc_carrier_phase_rad = -(double)t.rem_carr_phase_rad;
@@ -789,57 +842,151 @@ __device__ __forceinline__ int wrap_code(int raw, int L)
     return raw;
 }
 
+template <int IT>
+constexpr int item_bytes()
+{
+    return IT == GSDR_ITEM_GR_COMPLEX ? 8 : (IT == GSDR_ITEM_CSHORT ? 4 : 2);
+}
+
+// one stream item from an LDS byte image of the input (raw item format)
+template <int IT>
+__device__ __forceinline__ float2 lds_iq(const char* b, int byte)
+{
+    if constexpr (IT == GSDR_ITEM_GR_COMPLEX)
+        return *reinterpret_cast<const float2*>(b + byte);
+    else if constexpr (IT == GSDR_ITEM_CSHORT)
+        {
+            const short2 v = *reinterpret_cast<const short2*>(b + byte);
+            return make_float2((float)v.x, (float)v.y);
+        }
+    else
+        {
+            const char2 v = *reinterpret_cast<const char2*>(b + byte);
+            return make_float2((float)v.x, (float)v.y);
+        }
+}
+
+typedef __attribute__((address_space(1))) void gsdr_gvoid;
+typedef __attribute__((address_space(3))) void gsdr_lvoid;
+
+// Asynchronous copy of input bytes [first, first + nbytes) (relative to the
+// stream pointer) into an LDS buffer with global_load_lds_dwordx4: no VGPR
+// destinations, so a whole chunk is in flight at once.  The buffer starts at the
+// 16-byte block holding `first` (returned); every lane's source is clamped to a
+// 16-byte block holding at least one byte of the stream, i.e. inside the
+// stream's own pages.  Waves [w0, kTrkThreads/64) issue; the buffer is valid
+// after the issuing waves' vmcnt drains (any __syncthreads).
+__device__ __forceinline__ uintptr_t stream_fetch(const void* iq, uint64_t iq_bytes, int64_t first, int nbytes,
+    char* lds, int w0)
+{
+    const uintptr_t base = reinterpret_cast<uintptr_t>(iq);
+    const uintptr_t lo = base & ~(uintptr_t)15;
+    const uintptr_t hi = (base + iq_bytes - 1) & ~(uintptr_t)15;
+    const uintptr_t start = (uintptr_t)((int64_t)base + first) & ~(uintptr_t)15;
+    const int rows = (nbytes + 15 + kStreamRow - 1) / kStreamRow;  // first - start <= 15
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    for (int r = wave - w0; r < rows; r += kTrkThreads / 64 - w0)
+        {
+            if (r < 0) break;
+            uintptr_t a = start + (uintptr_t)r * kStreamRow + (uintptr_t)lane * 16;
+            a = a < lo ? lo : (a > hi ? hi : a);
+            __builtin_amdgcn_global_load_lds((gsdr_gvoid*)a, (gsdr_lvoid*)(lds + r * kStreamRow), 16, 0, 0);
+        }
+    return start;
+}
+
+// (int)floorf(x) in one instruction (v_cvt_flr_i32_f32: floor, then convert; exact)
+__device__ __forceinline__ int floor_i(float x)
+{
+    int r;
+    asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+
 // One correlation chunk of kSpl samples per lane (n = n0 + tid + j*kTrkThreads),
-// KT taps, no branches inside: samples past the end are zero and their index clamped.
+// KT taps, no branches inside.  FULL: every sample of the chunk lies inside the
+// call; otherwise samples past the end are zero and their index clamped.
+// WRAP: 2 = every code index of the call lies in [-kCodeMargin, L + kCodeMargin),
+// read straight from the margin-padded replica; 1 = in [-L, 2L), one conditional
+// add/sub; 0 = general modulo.  Complex products and the accumulations are
+// packed-f32 (v_pk_mul/v_pk_fma: one instruction per tap and sample).
 // DATA: one more accumulator, acc[kMaxTrkTaps], on the data-component replica
 // s_data at the prompt tap's index (the pilot-tracking data correlator of
 // do_correlation_step, whose only tap sits at the prompt shift).
-template <int IT, bool FROM_WIN, bool FAST, int KT, bool DATA>
+template <int IT, int SRC, int WRAP, bool FULL, int KT, bool DATA>
 __device__ __forceinline__ void correlate_chunk(const void* __restrict__ iq, const float2* s_win, const float* s_code,
     const float* s_data, const Prep& p, int n0, int vl, int L, const float (&sh_rem)[kMaxTrkTaps], float2& ph,
-    float2 (&acc)[kMaxTrkTaps + 1])
+    float2 (&acc)[kMaxTrkTaps + 1], const char* sbuf = nullptr, int sboff = 0)
 {
+    using gsdr::pk::c2;
     constexpr int IPK = KT / 2;  // prompt slot: 1 of E,P,L / 2 of VE,E,P,L,VL
-    float2 xs[kSpl];
+    c2 xs[kSpl];
 #pragma unroll
     for (int j = 0; j < kSpl; ++j)
         {
             const int n = n0 + (int)threadIdx.x + j * kTrkThreads;
-            const int nc = min(n, vl - 1);
-            const float2 v = FROM_WIN ? s_win[p.woff + nc] : load_iq<IT>(iq, p.off + nc);
-            xs[j] = n < vl ? v : make_float2(0.f, 0.f);
+            const int nc = FULL ? n : min(n, vl - 1);
+            float2 v;
+            if constexpr (SRC == 0)
+                v = s_win[p.woff + nc];
+            else if constexpr (SRC == 1)
+                v = load_iq<IT>(iq, p.off + nc);
+            else
+                v = lds_iq<IT>(sbuf, sboff + nc * item_bytes<IT>());
+            xs[j] = (FULL || n < vl) ? gsdr::pk::from(v) : c2{0.f, 0.f};
         }
+    c2 av[kMaxTrkTaps + 1];
+#pragma unroll
+    for (int k = 0; k <= kMaxTrkTaps; ++k) av[k] = gsdr::pk::from(acc[k]);
+    c2 phv = gsdr::pk::from(ph);
+    const c2 ws = gsdr::pk::from(p.wstep);
 #pragma unroll
     for (int j = 0; j < kSpl; ++j)
         {
-            const int n = min(n0 + (int)threadIdx.x + j * kTrkThreads, vl - 1);
-            const float2 x = xs[j];
-            const float2 tt = make_float2(x.x * ph.x - x.y * ph.y, x.x * ph.y + x.y * ph.x);
+            const int n0j = n0 + (int)threadIdx.x + j * kTrkThreads;
+            const int n = FULL ? n0j : min(n0j, vl - 1);
+            const c2 tt = gsdr::pk::mul(xs[j], phv);
             const float a = gsdr::mul_rn(p.code_step, (float)n);
 #pragma unroll
             for (int k = 0; k < KT; ++k)
                 {
                     // a_avx association: floor(step*n + (shift - rem))
-                    int raw = (int)floorf(gsdr::add_rn(a, sh_rem[k]));
-                    if (FAST)
+                    int raw = floor_i(gsdr::add_rn(a, sh_rem[k]));
+                    if (WRAP == 1)
                         {
                             raw += raw < 0 ? L : 0;
                             raw -= raw >= L ? L : 0;
                         }
-                    else
+                    else if (WRAP == 0)
                         raw = wrap_code(raw, L);
-                    const float cv = s_code[raw];
-                    acc[k].x += tt.x * cv;
-                    acc[k].y += tt.y * cv;
-                    if (DATA && k == IPK)
-                        {
-                            const float dv = s_data[raw];
-                            acc[kMaxTrkTaps].x += tt.x * dv;
-                            acc[kMaxTrkTaps].y += tt.y * dv;
-                        }
+                    av[k] = gsdr::pk::fmas(tt, s_code[raw], av[k]);
+                    if (DATA && k == IPK) av[kMaxTrkTaps] = gsdr::pk::fmas(tt, s_data[raw], av[kMaxTrkTaps]);
                 }
-            ph = make_float2(ph.x * p.wstep.x - ph.y * p.wstep.y, ph.x * p.wstep.y + ph.y * p.wstep.x);
+            phv = gsdr::pk::mul(phv, ws);
         }
+#pragma unroll
+    for (int k = 0; k <= kMaxTrkTaps; ++k) acc[k] = gsdr::pk::to(av[k]);
+    ph = gsdr::pk::to(phv);
+}
+
+// the chunk at n0 with the call's wrap mode; FULL when the whole chunk is inside the call
+template <int IT, int SRC, int KT, bool DATA>
+__device__ __forceinline__ void correlate_chunk_any(const void* __restrict__ iq, const float2* s_win, const float* s_code,
+    const float* s_data, const Prep& p, int n0, int vl, int L, const float (&sh_rem)[kMaxTrkTaps], float2& ph,
+    float2 (&acc)[kMaxTrkTaps + 1], const char* sbuf = nullptr, int sboff = 0)
+{
+    if (p.wrap == 2)
+        {
+            if (n0 + kWinCore <= vl)
+                correlate_chunk<IT, SRC, 2, true, KT, DATA>(iq, s_win, s_code, s_data, p, n0, vl, L, sh_rem, ph, acc, sbuf, sboff);
+            else
+                correlate_chunk<IT, SRC, 2, false, KT, DATA>(iq, s_win, s_code, s_data, p, n0, vl, L, sh_rem, ph, acc, sbuf, sboff);
+        }
+    else if (p.wrap == 1)
+        correlate_chunk<IT, SRC, 1, false, KT, DATA>(iq, s_win, s_code, s_data, p, n0, vl, L, sh_rem, ph, acc, sbuf, sboff);
+    else
+        correlate_chunk<IT, SRC, 0, false, KT, DATA>(iq, s_win, s_code, s_data, p, n0, vl, L, sh_rem, ph, acc, sbuf, sboff);
 }
 
 // high_dyn correlation (do_correlation_step with set_high_dynamics_resampler(true)):
@@ -901,19 +1048,41 @@ __device__ __forceinline__ void correlate_call(const void* __restrict__ iq, cons
     for (int n0 = 0; n0 < vl; n0 += kWinCore)
         {
             if (p.woff >= 0)
-                {
-                    if (p.fast)
-                        correlate_chunk<IT, true, true, KT, DATA>(iq, s_win, s_code, s_data, p, n0, vl, L, sh_rem, ph, acc);
-                    else
-                        correlate_chunk<IT, true, false, KT, DATA>(iq, s_win, s_code, s_data, p, n0, vl, L, sh_rem, ph, acc);
-                }
+                correlate_chunk_any<IT, 0, KT, DATA>(iq, s_win, s_code, s_data, p, n0, vl, L, sh_rem, ph, acc);
             else
-                {
-                    if (p.fast)
-                        correlate_chunk<IT, false, true, KT, DATA>(iq, s_win, s_code, s_data, p, n0, vl, L, sh_rem, ph, acc);
-                    else
-                        correlate_chunk<IT, false, false, KT, DATA>(iq, s_win, s_code, s_data, p, n0, vl, L, sh_rem, ph, acc);
-                }
+                correlate_chunk_any<IT, 1, KT, DATA>(iq, s_win, s_code, s_data, p, n0, vl, L, sh_rem, ph, acc);
+        }
+}
+
+// Streamed call (vector_length > kWinCore): the call's samples pass through two
+// LDS chunk buffers of `chunk` samples filled by global_load_lds.  Chunk j is
+// read from buffer j&1 while chunk j+1 lands in the other; chunk 0 was
+// prefetched during the previous call's loop update when `pf_ok` (else fetched
+// here).  The __syncthreads at the top of each chunk drains the DMA (vmcnt(0))
+// and orders the previous chunk's reads before its buffer is refilled.
+template <int IT, int KT, bool DATA>
+__device__ __forceinline__ void correlate_call_stream(const void* __restrict__ iq, uint64_t iq_items, char* sb,
+    int sbuf_bytes, int chunk, bool pf_ok, uintptr_t pf_start, const float* s_code, const float* s_data, const Prep& p,
+    int vl, int L, const float (&sh_rem)[kMaxTrkTaps], float2& ph, float2 (&acc)[kMaxTrkTaps + 1])
+{
+    constexpr int isz = item_bytes<IT>();
+    const uint64_t nbytes = iq_items * (uint64_t)isz;
+    const uintptr_t s0 = reinterpret_cast<uintptr_t>(iq) + (uintptr_t)p.off * isz;  // byte address of sample 0
+    uintptr_t bstart[2];
+    bstart[0] = pf_ok ? pf_start : stream_fetch(iq, nbytes, p.off * isz, chunk * isz, sb, 0);
+    bstart[1] = 0;
+    const int nch = (vl + chunk - 1) / chunk;
+    for (int j = 0; j < nch; ++j)
+        {
+            __syncthreads();
+            if (j + 1 < nch)
+                bstart[(j + 1) & 1] =
+                    stream_fetch(iq, nbytes, (p.off + (int64_t)(j + 1) * chunk) * isz, chunk * isz, sb + ((j + 1) & 1) * sbuf_bytes, 0);
+            const char* buf = sb + (j & 1) * sbuf_bytes;
+            const int boff = (int)((int64_t)s0 - (int64_t)bstart[j & 1]);
+            const int nend = min((j + 1) * chunk, vl);
+            for (int n0 = j * chunk; n0 < nend; n0 += kWinCore)
+                correlate_chunk_any<IT, 2, KT, DATA>(iq, nullptr, s_code, s_data, p, n0, vl, L, sh_rem, ph, acc, buf, boff);
         }
 }
 
@@ -928,18 +1097,27 @@ template <int IT>
 __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __restrict__ consts,
     TrkChan* __restrict__ chans, const float* const* __restrict__ codes, const float* const* __restrict__ data_codes,
     const void* __restrict__ iq, uint64_t iq_first, uint64_t iq_items, uint32_t max_epochs, gsdr_trk_epoch* __restrict__ out,
-    uint32_t* __restrict__ nout, int code_pad, int data_pad, uint64_t* __restrict__ timing, int timing_wall)
+    uint32_t* __restrict__ nout, int code_pad, int data_pad, uint64_t* __restrict__ timing, int timing_wall, int stream_chunk,
+    int sbuf_bytes)
 {
     // LDS: [replica | data replica (pilot tracking) | next call's input window]
     extern __shared__ float s_dyn[];
-    float* s_code = s_dyn;
-    float* s_data = s_dyn + code_pad;
+    // replicas with kCodeMargin wrapped samples on each side: s_code[-M .. L+M)
+    float* s_code = s_dyn + kCodeMargin;
+    float* s_data = s_dyn + code_pad + kCodeMargin;
     float2* s_win = reinterpret_cast<float2*>(s_dyn + code_pad + data_pad);
+    char* s_sb = reinterpret_cast<char*>(s_dyn + code_pad + data_pad);  // streamed calls: two chunk buffers
     __shared__ LoopFilter s_lf;
     __shared__ float2 s_pbuf[kMaxCn0];
+    __shared__ __attribute__((aligned(16))) float s_cn[4][kMaxCn0];  // cn0_and_lock's per-element terms
     __shared__ int s_state;
     __shared__ Prep prep;
     __shared__ float2 s_red[kTrkThreads / 64][kMaxTrkTaps + 1];
+    // the loop state lives in LDS between calls and in wave 0's registers only
+    // during the loop update, so the correlation keeps its registers for loads
+    // in flight (with the state resident for the whole launch the kernel sat at
+    // 256 VGPRs and the compiler serialised the sample loads)
+    __shared__ TrkHot s_t;
     const int ch = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const TrkConst& c = consts[ch];
@@ -947,12 +1125,11 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
     // The tracking loop is a latency chain that shares its CUs with the
     // acquisition grid running on another queue: raise the issue priority.
     __builtin_amdgcn_s_setprio(3);
-    TrkHot t;
-    if (wave == 0) t = gc->h;
     if (tid == 0)
         {
+            s_t = gc->h;
             s_lf = gc->code_filter;
-            s_state = t.state;
+            s_state = s_t.state;
         }
     if (tid < kMaxCn0) s_pbuf[tid] = gc->prompt_buffer[tid];
     __syncthreads();
@@ -965,24 +1142,28 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
     const int L = c.code_samples;
     const int vl = c.vector_length;
     const bool use_window = vl <= kWinCore;
+    const bool streamed = !use_window && stream_chunk > 0;
     const bool data = c.track_pilot != 0;
     {
         const float* cd = codes[ch];
-        for (int i = tid; i < L; i += kTrkThreads) s_code[i] = cd[i];
+        for (int i = tid - kCodeMargin; i < L + kCodeMargin; i += kTrkThreads) s_code[i] = cd[((i % L) + L) % L];
         if (data)
             {
                 const float* dd = data_codes[ch];
-                for (int i = tid; i < L; i += kTrkThreads) s_data[i] = dd[i];
+                for (int i = tid - kCodeMargin; i < L + kCodeMargin; i += kTrkThreads) s_data[i] = dd[((i % L) + L) % L];
             }
     }
     int64_t win_base = INT64_MIN;  // absolute-index base of the staged window (uniform)
+    int64_t pf_first = INT64_MIN;  // streamed calls: first sample of the prefetched chunk 0 (uniform)
+    uintptr_t pf_start = 0;        // and the byte address its LDS buffer starts at
     uint32_t e = 0;
     for (;; ++e)
         {
             uint64_t tm0 = 0, tm1 = 0, tm2 = 0;
-            if (timing && tid == 0) tm0 = timing_wall ? wall_clock64() : clock64();
+            if (timing && tid == 0) tm0 = wall_clock64();
             if (tid == 0)
                 {
+                    const TrkHot& t = s_t;
                     Prep p{};
                     const int64_t off = (int64_t)(t.next_sample - iq_first);
                     p.go = (e < max_epochs) && t.state >= 2 && t.state <= 4 && t.next_sample >= iq_first &&
@@ -992,6 +1173,8 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                     p.woff = -1;
                     if (use_window && win_base != INT64_MIN && off >= win_base && off - win_base + vl <= kWinCore + kHalo)
                         p.woff = (int32_t)(off - win_base);
+                    p.pf_ok = streamed && pf_first != INT64_MIN && off >= pf_first &&
+                              off + min(vl, stream_chunk) <= pf_first + stream_chunk + kHalo;
                     if (p.go)
                         {
                             // do_correlation_step's float arguments (:1069-1075); the
@@ -1014,7 +1197,10 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                             const float lo = floorf(smin);
                             const float hi = floorf(gsdr::add_rn(gsdr::mul_rn(p.code_step, (float)(vl - 1)), smax));
                             const float Lf = (float)L;
-                            p.fast = p.code_step >= 0.0f && lo >= -Lf && hi < 2.0f * Lf;
+                            const bool mono = p.code_step >= 0.0f;
+                            p.wrap = (mono && lo >= -(float)kCodeMargin && hi < Lf + (float)kCodeMargin)
+                                         ? 2
+                                         : ((mono && lo >= -Lf && hi < 2.0f * Lf) ? 1 : 0);
                             if (c.high_dyn)
                                 {
                                     p.hd = 1;
@@ -1039,7 +1225,7 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                 }
             __syncthreads();
             if (!prep.go) break;
-            if (timing && tid == 0) tm1 = timing_wall ? wall_clock64() : clock64();
+            if (timing && tid == 0) tm1 = wall_clock64();
             // ---- correlation: lane-interleaved samples, fp64 phasor anchor + fp32 steps
             const Prep p = prep;
             float2 acc[kMaxTrkTaps + 1];
@@ -1061,6 +1247,18 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                 {
                     const float* sk = p.narrow ? c.shifts_narrow : c.shifts;
                     correlate_call_hd<IT>(iq, s_win, s_code, s_data, p, vl, L, K, data, sk[0], sk[c.iP], acc);
+                }
+            else if (streamed)
+                {
+                    if (K <= 3)
+                        correlate_call_stream<IT, 3, false>(iq, iq_items, s_sb, sbuf_bytes, stream_chunk, p.pf_ok, pf_start,
+                            s_code, s_data, p, vl, L, sh_rem, ph, acc);
+                    else if (!data)
+                        correlate_call_stream<IT, kMaxTrkTaps, false>(iq, iq_items, s_sb, sbuf_bytes, stream_chunk, p.pf_ok,
+                            pf_start, s_code, s_data, p, vl, L, sh_rem, ph, acc);
+                    else
+                        correlate_call_stream<IT, kMaxTrkTaps, true>(iq, iq_items, s_sb, sbuf_bytes, stream_chunk, p.pf_ok,
+                            pf_start, s_code, s_data, p, vl, L, sh_rem, ph, acc);
                 }
             else if (K <= 3)
                 correlate_call<IT, 3, false>(iq, s_win, s_code, s_data, p, vl, L, sh_rem, ph, acc);
@@ -1087,7 +1285,7 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                     for (int k = 0; k <= kMaxTrkTaps; ++k) s_red[wave][k] = acc[k];
                 }
             __syncthreads();  // partials visible; every read of the LDS window done
-            if (timing && tid == 0) tm2 = timing_wall ? wall_clock64() : clock64();
+            if (timing && tid == 0) tm2 = wall_clock64();
             // ---- fetch the window the next call most likely reads: [off + vl - kHalo/2, +kWinCore+kHalo)
             float2 wv[kSpl];
             float2 wh = make_float2(0.f, 0.f);
@@ -1106,8 +1304,18 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                             wh = (i >= 0 && (uint64_t)i < iq_items) ? load_iq<IT>(iq, i) : make_float2(0.f, 0.f);
                         }
                 }
+            if (streamed)
+                {
+                    // chunk 0 of the call most likely next, fetched by waves 1.. while
+                    // wave 0 runs the loop update (its own memory waits stay unaffected)
+                    const int64_t nb = p.off + vl - kHalo / 2;
+                    pf_start = stream_fetch(iq, iq_items * (uint64_t)item_bytes<IT>(), nb * item_bytes<IT>(),
+                        (stream_chunk + kHalo) * item_bytes<IT>(), s_sb, 1);
+                    pf_first = nb;
+                }
             if (wave == 0)
                 {
+                    TrkHot t = s_t;
                     float2 taps[kMaxTrkTaps + 1];
 #pragma unroll
                     for (int k = 0; k <= kMaxTrkTaps; ++k)
@@ -1124,6 +1332,22 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                                 }
                             taps[k] = r;
                         }
+                    float2 epl[3];
+                    {
+                        const int ix[3] = {c.iE, c.iP, c.iL};
+#pragma unroll
+                        for (int q = 0; q < 3; ++q)
+                            {
+                                float2 r = make_float2(0.f, 0.f);
+#pragma unroll
+                                for (int w = 0; w < kTrkThreads / 64; ++w)
+                                    {
+                                        r.x += s_red[w][ix[q]].x;
+                                        r.y += s_red[w][ix[q]].y;
+                                    }
+                                epl[q] = r;
+                            }
+                    }
                     const uint64_t n_read = t.next_sample;
                     const int32_t state0 = t.state;
                     // pull-in transitory check at the top of general_work (:1794-1803):
@@ -1136,7 +1360,10 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                             t.code_lock_fail_counter = 0;
                         }
                     EpochOut o;
-                    after_correlation(c, t, gc, s_lf, s_pbuf, taps, n_read, lane, o);
+                    uint64_t pr[3] = {0, 0, 0};
+                    uint64_t tm3 = 0;
+                    if (timing) tm3 = wall_clock64();
+                    after_correlation(c, t, gc, s_lf, s_pbuf, s_cn, taps, epl, n_read, lane, o, timing ? pr : nullptr);
                     if (lane == 0)
                         {
                             gsdr_trk_epoch r;
@@ -1167,14 +1394,19 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                             out[(size_t)ch * max_epochs + e] = r;
                             if (timing)
                                 {
-                                    uint64_t* tr = timing + ((size_t)ch * max_epochs + e) * 4;
+                                    uint64_t* tr = timing + ((size_t)ch * max_epochs + e) * kTimingSlots;
                                     tr[0] = tm0;
                                     tr[1] = tm1;
                                     tr[2] = tm2;
-                                    tr[3] = timing_wall ? wall_clock64() : clock64();
+                                    tr[3] = tm3;
+                                    tr[4] = pr[0] ? pr[0] : tm3;
+                                    tr[5] = pr[1] ? pr[1] : tr[4];
+                                    tr[6] = pr[2] ? pr[2] : tr[5];
+                                    tr[7] = wall_clock64();
                                 }
                         }
                     t.next_sample = n_read + (uint64_t)(int64_t)t.current_prn_length_samples;
+                    if (lane == 0) s_t = t;
                 }
             if (use_window)
                 {
@@ -1188,7 +1420,7 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
     __syncthreads();
     if (tid == 0)
         {
-            gc->h = t;
+            gc->h = s_t;
             gc->code_filter = s_lf;
             nout[ch] = e;
         }
@@ -1240,14 +1472,14 @@ struct gsdr_trk
     void* d_iq{nullptr};
     uint64_t iq_cap{0};
     size_t lds_bytes{0};
-    int code_pad{1024};  // floats reserved for the replica ahead of the LDS window
+    int code_pad{1024 + 2 * kCodeMargin};  // floats reserved for the padded replica ahead of the LDS window
     int data_pad{0};     // floats reserved for the data replica (pilot tracking)
     // GSDR_TRK_TIMING=1: per-phase clock64 stamps of every call, summarised on destroy
     bool timing_on{false};
     int timing_wall{0};  // GSDR_TRK_TIMING=2: constant-rate wall clock instead of the shader clock
     uint64_t* d_timing{nullptr};
     size_t timing_cap{0};
-    double tsum[4]{};
+    double tsum[kTimingSlots]{};
     uint32_t timing_epochs{0};
     uint32_t* timing_nout{nullptr};
     uint64_t tcount{0};
@@ -1439,9 +1671,29 @@ int ensure_out(gsdr_trk* k, uint32_t max_epochs)
 // latency chain and co-resident FFT waves would slow every call down.
 constexpr size_t kCuLds = 160 * 1024;
 constexpr size_t kStaticLdsMargin = 4 * 1024;  // the kernel's static __shared__ arrays
+// Streamed calls (vector_length > kWinCore): two chunk buffers in the LDS left
+// after the replicas, each (chunk + kHalo) items + 16 alignment bytes rounded up
+// to whole glds rows; chunk a multiple of kWinCore.  chunk = 0: no room (the
+// calls then read HBM directly).
+int item_size(int item_type) { return item_type == GSDR_ITEM_GR_COMPLEX ? 8 : (item_type == GSDR_ITEM_CSHORT ? 4 : 2); }
+int stream_buffer_bytes(int chunk, int isz) { return (((chunk + kHalo) * isz + 16) / kStreamRow + 2) * kStreamRow; }
+void stream_plan(size_t lds_bytes, int code_pad, int data_pad, int isz, int& chunk, int& sbuf)
+{
+    const long avail = (long)lds_bytes - (long)(code_pad + data_pad) * (long)sizeof(float);
+    chunk = 0;
+    sbuf = 0;
+    for (int c = kWinCore; c <= 64 * kWinCore; c += kWinCore)
+        {
+            if (2L * stream_buffer_bytes(c, isz) > avail) break;
+            chunk = c;
+            sbuf = stream_buffer_bytes(c, isz);
+        }
+}
+
 size_t lds_for(int code_pad, int data_pad)
 {
-    const size_t need = (size_t)(code_pad + data_pad) * sizeof(float) + (size_t)(kWinCore + kHalo) * sizeof(float2);
+    const size_t need = (size_t)(code_pad + data_pad) * sizeof(float) +
+                        std::max((size_t)(kWinCore + kHalo) * sizeof(float2), (size_t)2 * stream_buffer_bytes(kWinCore, 8));
     // LDS reserved per channel workgroup: by default the whole CU, so no acquisition
     // workgroup shares its issue slots once it runs; GSDR_TRK_LDS_KB trades that for
     // an earlier start on a busy chip (a full-CU workgroup waits for an empty CU).
@@ -1456,7 +1708,7 @@ int launch(gsdr_trk* k, const void* iq, uint64_t iq_first, uint64_t iq_items, ui
     uint64_t* timing = nullptr;
     if (k->timing_on)
         {
-            const size_t need = (size_t)k->conf.max_channels * max_epochs * 4;
+            const size_t need = (size_t)k->conf.max_channels * max_epochs * kTimingSlots;
             if (need > k->timing_cap)
                 {
                     if (k->d_timing) GSDR_HIP(hipFree(k->d_timing));
@@ -1483,18 +1735,20 @@ int launch(gsdr_trk* k, const void* iq, uint64_t iq_first, uint64_t iq_items, ui
             GSDR_HIP(hipEventRecord(e0, s));
         }
     const dim3 grid(k->conf.max_channels);
+    int chunk = 0, sbuf = 0;
+    stream_plan(k->lds_bytes, k->code_pad, k->data_pad, item_size(k->conf.item_type), chunk, sbuf);
     if (k->conf.item_type == GSDR_ITEM_GR_COMPLEX)
         hipLaunchKernelGGL((trk_kernel<GSDR_ITEM_GR_COMPLEX>), grid, dim3(kTrkThreads), k->lds_bytes, s, k->d_consts, k->d_chans,
             (const float* const*)k->d_codes, (const float* const*)k->d_data_codes, iq, iq_first, iq_items, max_epochs, out,
-            nout, k->code_pad, k->data_pad, timing, k->timing_wall);
+            nout, k->code_pad, k->data_pad, timing, k->timing_wall, chunk, sbuf);
     else if (k->conf.item_type == GSDR_ITEM_CSHORT)
         hipLaunchKernelGGL((trk_kernel<GSDR_ITEM_CSHORT>), grid, dim3(kTrkThreads), k->lds_bytes, s, k->d_consts, k->d_chans,
             (const float* const*)k->d_codes, (const float* const*)k->d_data_codes, iq, iq_first, iq_items, max_epochs, out,
-            nout, k->code_pad, k->data_pad, timing, k->timing_wall);
+            nout, k->code_pad, k->data_pad, timing, k->timing_wall, chunk, sbuf);
     else
         hipLaunchKernelGGL((trk_kernel<GSDR_ITEM_IBYTE>), grid, dim3(kTrkThreads), k->lds_bytes, s, k->d_consts, k->d_chans,
             (const float* const*)k->d_codes, (const float* const*)k->d_data_codes, iq, iq_first, iq_items, max_epochs, out,
-            nout, k->code_pad, k->data_pad, timing, k->timing_wall);
+            nout, k->code_pad, k->data_pad, timing, k->timing_wall, chunk, sbuf);
     GSDR_HIP(hipGetLastError());
     GSDR_HIP(hipEventRecord(k->last_launch, s));
     if (k->profiling)
@@ -1592,7 +1846,7 @@ int gsdr_trk_create(int device, const gsdr_trk_conf* conf, gsdr_trk** out)
     k->code_bufs.assign(nch, nullptr);
     k->data_code_bufs.assign(nch, nullptr);
     k->data_code_len.assign(nch, 0);
-    k->code_pad = 1024;  // grows with the longest replica started (gsdr_trk_start)
+    k->code_pad = 1024 + 2 * kCodeMargin;  // grows with the longest replica started (gsdr_trk_start)
     k->data_pad = 0;
     k->lds_bytes = lds_for(k->code_pad, k->data_pad);
     if (const char* tv = std::getenv("GSDR_TRK_TIMING"))
@@ -1644,30 +1898,31 @@ void gsdr_trk_destroy(gsdr_trk* k)
     if (k->timing_on && k->d_timing && k->timing_epochs)
         {
             const uint32_t nch = k->conf.max_channels, me = k->timing_epochs;
-            std::vector<uint64_t> tm((size_t)nch * me * 4);
+            std::vector<uint64_t> tm((size_t)nch * me * kTimingSlots);
             std::vector<uint32_t> cnt(nch);
             if (hipMemcpy(tm.data(), k->d_timing, tm.size() * sizeof(uint64_t), hipMemcpyDeviceToHost) == hipSuccess &&
                 hipMemcpy(cnt.data(), k->timing_nout, nch * sizeof(uint32_t), hipMemcpyDeviceToHost) == hipSuccess)
                 for (uint32_t c = 0; c < nch; ++c)
                     for (uint32_t e = 0; e < cnt[c] && e < me; ++e)
                         {
-                            const uint64_t* r = &tm[((size_t)c * me + e) * 4];
-                            for (int q = 0; q < 3; ++q)
+                            const uint64_t* r = &tm[((size_t)c * me + e) * kTimingSlots];
+                            for (int q = 0; q + 1 < kTimingSlots; ++q)
                                 if (r[q + 1] >= r[q]) k->tsum[q] += (double)(r[q + 1] - r[q]);
                             if (e + 1 < cnt[c] && e + 1 < me)
                                 {
-                                    const uint64_t next0 = tm[((size_t)c * me + e + 1) * 4];
-                                    if (next0 >= r[3]) k->tsum[3] += (double)(next0 - r[3]);
+                                    const uint64_t next0 = tm[((size_t)c * me + e + 1) * kTimingSlots];
+                                    if (next0 >= r[kTimingSlots - 1]) k->tsum[kTimingSlots - 1] += (double)(next0 - r[kTimingSlots - 1]);
                                 }
                             k->tcount++;
                         }
         }
     if (k->timing_on && k->tcount)
         {
-            static const char* names[] = {"prep", "correlate", "update", "window-write"};
+            static const char* names[kTimingSlots] = {"prep", "correlate", "tap-sum", "cn0-lock", "dll-pll", "update-vars",
+                "rest", "window-write"};
             std::fprintf(stderr, "gsdr_trk timing: %llu calls, %s ticks per call:", (unsigned long long)k->tcount,
-                k->timing_wall ? "wall_clock64" : "clock64");
-            for (int q = 0; q < 4; ++q) std::fprintf(stderr, " %s %.0f", names[q], k->tsum[q] / k->tcount);
+                "wall_clock64 (100 MHz)");
+            for (int q = 0; q < kTimingSlots; ++q) std::fprintf(stderr, " %s %.0f", names[q], k->tsum[q] / k->tcount);
             std::fprintf(stderr, "\n");
         }
     if (k->d_timing) (void)hipFree(k->d_timing);
@@ -1807,7 +2062,7 @@ int gsdr_trk_start(gsdr_trk* k, int ch, uint32_t prn, const float* code, int cod
     t.next_sample = nitems_read + (uint64_t)(int64_t)offset;
     *first_sample = t.next_sample;
     {
-        const int cp = std::max(k->code_pad, (code_samples + 1) & ~1);
+        const int cp = std::max(k->code_pad, (code_samples + 2 * kCodeMargin + 1) & ~1);
         const int dp = k->conf.track_pilot ? cp : 0;
         GSDR_REQUIRE(lds_for(cp, dp) <= kCuLds - kStaticLdsMargin, GSDR_E_UNSUPPORTED,
             "gsdr_trk_start: replica of %d samples does not fit the LDS next to the input window", code_samples);

@@ -180,7 +180,8 @@ int gsdr_acq_create(int device, const gsdr_acq_conf* conf, gsdr_acq** out)
     const size_t nP = conf->max_prns, nB = conf->max_blocks;
     hipError_t e = hipStreamCreateWithFlags(&a->stream, hipStreamNonBlocking);
 
-    if (e == hipSuccess) e = hipMalloc(&a->d_tw, N * sizeof(float2));
+    const size_t tw_n = std::max<size_t>(N, a->tw_entries);
+    if (e == hipSuccess) e = hipMalloc(&a->d_tw, tw_n * sizeof(float2));
     if (e == hipSuccess) e = hipMalloc(&a->d_wipe, (size_t)a->D * N * sizeof(float2));
     if (e == hipSuccess) e = hipMalloc(&a->d_code_fft, nP * N * sizeof(float2));
     if (e == hipSuccess) e = hipMalloc(&a->d_code_stage, nP * a->consumed * sizeof(float2));
@@ -235,13 +236,14 @@ int gsdr_acq_create(int device, const gsdr_acq_conf* conf, gsdr_acq** out)
             return GSDR_E_ALLOC;
         }
     // twiddles W_N^m in double, rounded once
-    std::vector<float2> tw(N);
+    std::vector<float2> tw(tw_n);
     for (uint32_t m = 0; m < N; ++m)
         {
             const double ang = 2.0 * M_PI * (double)m / (double)N;
             tw[m] = make_float2((float)std::cos(ang), (float)(-std::sin(ang)));
         }
-    if ((e = hipMemcpy(a->d_tw, tw.data(), N * sizeof(float2), hipMemcpyHostToDevice)) != hipSuccess)
+    if (a->tw_fill && a->tw_entries > N) a->tw_fill(tw.data());  // packed variant's per-stage table
+    if ((e = hipMemcpy(a->d_tw, tw.data(), tw_n * sizeof(float2), hipMemcpyHostToDevice)) != hipSuccess)
         {
             gsdr::set_error("gsdr_acq_create: twiddle upload: %s", hipGetErrorString(e));
             gsdr_acq_destroy(a);

@@ -27,7 +27,7 @@ namespace
 using gsdr::fft::Plan;
 
 // Default correlate variant at N = 4000 (see GSDR_PK_VARIANTS).
-constexpr int kDefaultCorrVariant4000 = 31;
+constexpr int kDefaultCorrVariant4000 = 70;
 
 // Default packed variant for an FFT size (0: none, the generic kernels).
 inline int default_pk_variant(uint32_t N)
@@ -308,6 +308,11 @@ __global__ void __launch_bounds__(PT::NT) acq_correlate_kernel(const float2* __r
 //         (b, p) that the grid maximum selects to find its first maximum; the
 //         reported peak is then the exact |R|^2, with the reference's first-index
 //         rule (32f_index_max_32u) among exact ties.
+// STAT 2: row maximum only.  The CFAR statistic needs the sum of one row per
+//         (b, p), the row opposite the peak (pcps_acquisition.cc:531-533), so
+//         acq_argmax_pk_kernel forms it there by Parseval instead of every row
+//         summing its 4000 outputs: sum_n |R[n]|^2 = N sum_k |Y[k]|^2 for the
+//         unnormalised transform of Y = conj(X) C.
 template <class MP, int PG, int WPE, int STAT>
 __global__ void __launch_bounds__(MP::NT) __attribute__((amdgpu_waves_per_eu(WPE))) acq_correlate_pk_kernel(const float2* __restrict__ X,
     const float2* __restrict__ code_fft, RowStat* __restrict__ stats, const float2* __restrict__ tw, uint32_t D,
@@ -341,35 +346,46 @@ __global__ void __launch_bounds__(MP::NT) __attribute__((amdgpu_waves_per_eu(WPE
     const uint32_t b = row / D, d = row - (row / D) * D;
     const uint32_t p0 = g * PG;
     const int np = (int)min((uint32_t)PG, P - p0);
-    const c2* x = reinterpret_cast<const c2*>(X) + (size_t)row * N;
+    // the X row and the code spectra through buffer descriptors built from
+    // wave-uniform values: per-lane byte offset j*8 in voffset, r*NB1*8 as the
+    // scalar/immediate offset -- no 64-bit address arithmetic per load
+    const auto xrs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float2*>(X) + (size_t)row * N, 0, (int)(N * sizeof(c2)), 0x00020000);
+    const auto crs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float2*>(code_fft) + (size_t)p0 * N, 0, (int)((size_t)np * N * sizeof(c2)), 0x00020000);
+    auto bload = [](decltype(xrs) rs, int voff, int soff) -> c2 {
+        const auto u = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, 0);
+        return c2{__uint_as_float(u[0]), __uint_as_float(u[1])};
+    };
+    // a wave with any first-stage butterfly loads for all its lanes (the idle
+    // lanes' clamped, in-bounds copies keep every register defined, so no
+    // zero-fill code); a wave with none skips the loads
     c2 xr[BPT1][R1], cr[BPT1][R1];
-    {
-        const c2* c = reinterpret_cast<const c2*>(code_fft) + (size_t)p0 * N;
 #pragma unroll
-        for (int bb = 0; bb < BPT1; ++bb)
-            {
-                const int j = (int)threadIdx.x + bb * NT;
-                if (NB1 % NT == 0 || j < NB1)
-                    {
+    for (int bb = 0; bb < BPT1; ++bb)
+        {
+            const int j = (int)threadIdx.x + bb * NT;
+            const int j0 = (int)(threadIdx.x & ~63u) + bb * NT;
+            if (NB1 % NT == 0 || j0 < NB1)
+                {
+                    const int jj = min(j, NB1 - 1);
 #pragma unroll
-                        for (int r = 0; r < R1; ++r)
-                            {
-                                xr[bb][r] = x[j + r * NB1];
-                                cr[bb][r] = c[j + r * NB1];
-                            }
-                    }
-            }
-    }
+                    for (int r = 0; r < R1; ++r)
+                        {
+                            xr[bb][r] = bload(xrs, jj * 8, r * NB1 * 8);
+                            cr[bb][r] = bload(crs, jj * 8, r * NB1 * 8);
+                        }
+                }
+        }
     for (int q = 0; q < np; ++q)
         {
-            if constexpr (STAT == 1)
+            if constexpr (STAT >= 1)
                 {
                     float rmax = 0.0f, sum = 0.0f;
                     auto load = [&](int bb, int r, int) -> c2 { return gsdr::pk::conj_mul(xr[bb][r], cr[bb][r]); };
                     auto hook = [&]() {
                         if (q + 1 < np)
                             {
-                                const c2* c = reinterpret_cast<const c2*>(code_fft) + (size_t)(p0 + q + 1) * N;
 #pragma unroll
                                 for (int bb = 0; bb < BPT1; ++bb)
                                     {
@@ -377,7 +393,8 @@ __global__ void __launch_bounds__(MP::NT) __attribute__((amdgpu_waves_per_eu(WPE
                                         if (NB1 % NT == 0 || j < NB1)
                                             {
 #pragma unroll
-                                                for (int r = 0; r < R1; ++r) cr[bb][r] = c[j + r * NB1];
+                                                for (int r = 0; r < R1; ++r)
+                                                    cr[bb][r] = bload(crs, j * 8, (int)((q + 1) * N * 8) + r * NB1 * 8);
                                             }
                                     }
                             }
@@ -385,14 +402,14 @@ __global__ void __launch_bounds__(MP::NT) __attribute__((amdgpu_waves_per_eu(WPE
                     auto store = [&](int, c2 v, int) {
                         const float m = __builtin_fmaf(v.x, v.x, v.y * v.y);
                         rmax = __builtin_fmaxf(rmax, m);
-                        sum += m;
+                        if constexpr (STAT == 1) sum += m;
                     };
                     MP::template run<false>(lds, tw, load, store, hook);
-#pragma unroll
-                    for (int off = 32; off > 0; off >>= 1)
+                    rmax = gsdr::wave_max(rmax);
+                    if constexpr (STAT == 1)
                         {
-                            rmax = __builtin_fmaxf(rmax, __shfl_xor(rmax, off));
-                            sum += __shfl_xor(sum, off);
+#pragma unroll
+                            for (int off = 32; off > 0; off >>= 1) sum += __shfl_xor(sum, off);
                         }
                     RowStat* sc = scratch + (q & 1) * NW;
                     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -481,10 +498,10 @@ __global__ void __launch_bounds__(MP::NT) __attribute__((amdgpu_waves_per_eu(WPE
 // (|R|^2 bits, ~index) -- volk_gnsssdr_32f_index_max_32u's strict '>' scan
 // (KERN/32f_index_max_32u.h:446-467) -- then write code_phase and
 // Acq_delay_samples = fmod(indext, samples_per_code) (pcps_acquisition.cc:709).
-template <class MP>
+template <class MP, int STAT>
 __global__ void __launch_bounds__(MP::NT) acq_argmax_pk_kernel(const float2* __restrict__ X,
     const float2* __restrict__ code_fft, gsdr_acq_result* __restrict__ res, const float2* __restrict__ tw, uint32_t D,
-    uint32_t P, float samples_per_code)
+    uint32_t P, float samples_per_code, AcqParams ap)
 {
     using gsdr::pk::c2;
     constexpr int NT = MP::NT;
@@ -522,6 +539,39 @@ __global__ void __launch_bounds__(MP::NT) acq_argmax_pk_kernel(const float2* __r
             const uint32_t idx = 0xffffffffu - (uint32_t)(key & 0xffffffffu);
             res[bp].code_phase = idx;
             res[bp].acq_delay_samples = (double)fmodf((float)idx, samples_per_code);
+        }
+    if constexpr (STAT == 2)
+        {
+            // CFAR input power of the row opposite the peak (pcps_acquisition.cc:531-533)
+            // by Parseval: accumulate(|R|^2) / fft_size = sum_k |X_opp[k]|^2 |C[k]|^2
+            if (!ap.cfar || ap.step_two) return;
+            const uint32_t opp = (d + D / 2) % D;
+            const c2* xo = reinterpret_cast<const c2*>(X) + ((size_t)b * D + opp) * N;
+            float acc = 0.0f;
+            for (uint32_t i = threadIdx.x; i < N; i += NT)
+                {
+                    const c2 y = gsdr::pk::conj_mul(xo[i], c[i]);
+                    acc = __builtin_fmaf(y.x, y.x, __builtin_fmaf(y.y, y.y, acc));
+                }
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+            float* fs = reinterpret_cast<float*>(scratch + NW);
+            __syncthreads();
+            if ((threadIdx.x & 63) == 0) fs[threadIdx.x >> 6] = acc;
+            __syncthreads();
+            if (threadIdx.x == 0)
+                {
+                    float tot = 0.0f;
+#pragma unroll
+                    for (int w = 0; w < NW; ++w) tot += fs[w];
+                    // (float)((double)(acc / eff) / 2.0 / counter), acc / eff = tot
+                    const float ip = (float)((double)tot / 2.0 / (double)ap.counter);
+                    gsdr_acq_result r = res[bp];
+                    r.input_power = ip;
+                    r.test_statistic = r.peak / ip;
+                    r.positive = r.test_statistic > ap.threshold ? 1 : 0;
+                    res[bp] = r;
+                }
         }
 }
 
@@ -1013,7 +1063,9 @@ struct gsdr_acq
     int nt{256};
     int variant{0};
     int corr_variant{0};      // 0: the generic LDS kernels; >0: a GSDR_PK_VARIANTS id (packed forward + correlate)
-    int corr_stat{0};         // the variant's row statistic (1: argmax recomputed by acq_argmax_pk_kernel)
+    int corr_stat{0};         // the variant's row statistic (1/2: argmax recomputed by acq_argmax_pk_kernel)
+    size_t tw_entries{0};     // twiddle entries the packed variant reads (W_N + its per-stage table)
+    void (*tw_fill)(float2*){nullptr};  // fills the per-stage table after W_N
     size_t corr_lds_bytes{0};
     Plan plan{};
     gsdr::fft::Plan4 plan4{};  // four-step plan (variants 20-22, N beyond one workgroup's LDS)
@@ -1092,7 +1144,19 @@ size_t item_bytes(int it) { return it == GSDR_ITEM_CSHORT ? 4 : (it == GSDR_ITEM
     X(39, (gsdr::pk::PkPlan<256, true, 25, 16, 10>), 1, 5, 1)           \
     X(60, (gsdr::pk::PkPlan<1024, true, 16, 10, 10, 10>), 1, 1, 1)      \
     X(61, (gsdr::pk::PkPlan<512, true, 20, 20, 20>), 1, 1, 1)           \
-    X(62, (gsdr::pk::PkPlan<256, true, 20, 10, 10>), 1, 1, 1)
+    X(62, (gsdr::pk::PkPlan<256, true, 20, 10, 10>), 1, 1, 1)           \
+    X(63, (gsdr::pk::PkPlan<1024, 1, 16, 10, 10, 10>), 1, 1, 2)         \
+    X(64, (gsdr::pk::PkPlan<512, 1, 20, 20, 20>), 1, 1, 2)              \
+    X(65, (gsdr::pk::PkPlan<256, 1, 20, 10, 10>), 1, 1, 2)              \
+    X(70, (gsdr::pk::PkPlan<256, 1, 25, 16, 10>), 1, 1, 2)              \
+    X(71, (gsdr::pk::PkPlan<256, 2, 25, 16, 10>), 1, 1, 1)              \
+    X(72, (gsdr::pk::PkPlan<256, 2, 25, 16, 10>), 1, 1, 2)              \
+    X(73, (gsdr::pk::PkPlan<256, 2, 20, 20, 10>), 1, 1, 2)              \
+    X(74, (gsdr::pk::PkPlan<256, 2, 10, 16, 25>), 1, 1, 2)              \
+    X(75, (gsdr::pk::PkPlan<256, 1, 16, 25, 10>), 1, 1, 2)              \
+    X(76, (gsdr::pk::PkPlan<256, 1, 25, 10, 16>), 1, 1, 2)              \
+    X(77, (gsdr::pk::PkPlan<256, 1, 25, 16, 10>), 1, 5, 2)              \
+    X(78, (gsdr::pk::PkPlan<256, 1, 20, 20, 10>), 1, 1, 2)
 
 template <class PT>
 int set_lds_attrs(size_t bytes)
@@ -1339,7 +1403,7 @@ int launch_all(gsdr_acq* a, const void* iq, int item_type, uint32_t nblocks, uin
     hipLaunchKernelGGL(acq_reduce_kernel, dim3(nblocks * a->nprn), dim3(64), 0, s, a->d_stats, res, a->d_prn, ap,
         stamp0, stride);
     GSDR_HIP(hipGetLastError());
-    if (a->corr_variant > 0 && a->corr_stat == 1)
+    if (a->corr_variant > 0 && a->corr_stat >= 1)
         {
             int rc = gsdr_acq_impl::launch_argmax_variant(a, nblocks, res, s);
             if (rc != GSDR_OK) return rc;

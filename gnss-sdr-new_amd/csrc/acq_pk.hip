@@ -34,9 +34,9 @@ int launch_argmax_variant(gsdr_acq* a, uint32_t nblocks, gsdr_acq_result* res, h
     case ID:                                                                                                    \
         {                                                                                                       \
             using M = GSDR_UNPAREN MP;                                                                          \
-            hipLaunchKernelGGL((acq_argmax_pk_kernel<M>), dim3(nblocks * a->nprn), dim3(M::NT),                 \
+            hipLaunchKernelGGL((acq_argmax_pk_kernel<M, ST>), dim3(nblocks * a->nprn), dim3(M::NT),             \
                 a->corr_lds_bytes, s, a->d_X, a->d_code_fft, res, a->d_tw, a->D, a->nprn,                       \
-                a->conf.samples_per_code);                                                                      \
+                a->conf.samples_per_code, params_of(a));                                                        \
             GSDR_HIP(hipGetLastError());                                                                        \
             return GSDR_OK;                                                                                     \
         }
@@ -90,7 +90,7 @@ int setup_corr_variant(gsdr_acq* a, int v)
             a->corr_lds_bytes = M::lds_bytes() + (size_t)2 * (M::NT / 64) * sizeof(RowStat);                   \
             GSDR_HIP(hipFuncSetAttribute((const void*)acq_correlate_pk_kernel<M, PG, WPE, ST>,                  \
                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)a->corr_lds_bytes));                           \
-            GSDR_HIP(hipFuncSetAttribute((const void*)acq_argmax_pk_kernel<M>,                                  \
+            GSDR_HIP(hipFuncSetAttribute((const void*)acq_argmax_pk_kernel<M, ST>,                              \
                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)a->corr_lds_bytes));                           \
             if (M::N != (int)a->N)                                                                              \
                 {                                                                                               \
@@ -105,6 +105,8 @@ int setup_corr_variant(gsdr_acq* a, int v)
                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)M::lds_bytes()));                              \
             a->corr_variant = ID;                                                                               \
             a->corr_stat = ST;                                                                                  \
+            a->tw_entries = M::tw_entries();                                                                    \
+            a->tw_fill = &M::fill_stage_tw;                                                                     \
             return GSDR_OK;                                                                                     \
         }
 #define GSDR_UNPAREN(...) __VA_ARGS__

@@ -22,6 +22,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cmath>
+
 #include "fft_lds.h"
 #include "fft_multi.h"
 
@@ -240,6 +242,48 @@ struct Dft<25> : DftCT<5, 5>
 {
 };
 
+// ---- per-stage twiddle table (TWP == 2) ----
+// Row length for a radix-R stage: the R-1 roots, padded to an even count.
+constexpr int stage_tw_row(int R) { return (R - 1 + 1) & ~1; }
+
+template <int... Rs>
+constexpr size_t stage_tw_entries()
+{
+    constexpr int r[] = {Rs...};
+    size_t n = 0;
+    int ns = r[0];
+    for (size_t s = 1; s < sizeof...(Rs); ++s)
+        {
+            n += (size_t)ns * stage_tw_row(r[s]);
+            ns *= r[s];
+        }
+    return n;
+}
+
+// Host: entries N, N+1, ... of the table the kernels read: for every non-first
+// stage s (radix R, Ns-point sub-transforms, TSTRIDE = N/(Ns R)) and k < Ns the
+// row W_N^{r k TSTRIDE}, r = 1..R-1 (angles in double, rounded once).
+template <int... Rs>
+inline void stage_tw_fill(float2* tw, int N)
+{
+    constexpr int r[] = {Rs...};
+    size_t o = (size_t)N;
+    int ns = r[0];
+    for (size_t s = 1; s < sizeof...(Rs); ++s)
+        {
+            const int R = r[s], row = stage_tw_row(R), ts = N / (ns * R);
+            for (int k = 0; k < ns; ++k)
+                for (int q = 0; q < row; ++q)
+                    {
+                        const long m = q + 1 < R ? (long)(q + 1) * k * ts % N : 0;
+                        const double ang = 2.0 * 3.141592653589793238462643383279502884 * (double)m / (double)N;
+                        tw[o + (size_t)k * row + q] = make_float2((float)std::cos(ang), (float)(-std::sin(ang)));
+                    }
+            o += (size_t)ns * row;
+            ns *= R;
+        }
+}
+
 // One Stockham stage over an N-point LDS buffer of c2.
 //   TWP: inter-stage twiddles as powers of one table root (1 VMEM load per
 //        butterfly, R-2 extra complex multiplies); else R-1 table loads.
@@ -247,7 +291,8 @@ struct Dft<25> : DftCT<5, 5>
 //        first-maximum scan needs it); without ORD it visits butterfly by
 //        butterfly, so a partially filled pass is skipped as a whole instead of
 //        predicating every output (order-free reductions: max, sum).
-template <int R, int NT, int N, int Ns, bool TWP, bool FIRST, bool LAST, bool ORD, class Load, class Store, class Hook>
+template <int R, int NT, int N, int Ns, int TWP, int TOFF, bool FIRST, bool LAST, bool ORD, class Load, class Store,
+    class Hook>
 __device__ __forceinline__ void stage(c2* lds, const float2* __restrict__ tw, Load& load, Store& store, Hook& hook)
 {
     constexpr int BPT = fft::bpt_for(R);
@@ -257,8 +302,24 @@ __device__ __forceinline__ void stage(c2* lds, const float2* __restrict__ tw, Lo
 #pragma unroll
     for (int b = 0; b < BPT; ++b)
         {
+            // one pass per lane (BPT == 1): every lane loads, the idle ones from a
+            // clamped in-bounds index -- no branch around the loads, so no
+            // zero-filled registers for the idle lanes; their results are never
+            // stored.  Several passes: the per-lane guard.
             const int j = (int)threadIdx.x + b * NT;
-            if (NB % NT == 0 || j < NB)
+            if constexpr (BPT == 1 && NB % NT != 0)
+                {
+                    const int jj = min(j, NB - 1);
+#pragma unroll
+                    for (int r = 0; r < R; ++r)
+                        {
+                            if constexpr (FIRST)
+                                v[b][r] = load(b, r, jj + r * NB);
+                            else
+                                v[b][r] = lds[jj + r * NB];
+                        }
+                }
+            else if (NB % NT == 0 || j < NB)
                 {
 #pragma unroll
                     for (int r = 0; r < R; ++r)
@@ -285,7 +346,22 @@ __device__ __forceinline__ void stage(c2* lds, const float2* __restrict__ tw, Lo
                         {
                             k = j % Ns;
                             const int step = k * TSTRIDE;
-                            if constexpr (TWP)
+                            if constexpr (TWP == 2)
+                                {
+                                    // per-stage table (stage_tw_fill): row k holds W_N^{r k TSTRIDE},
+                                    // r = 1..R-1, padded to an even count -> 16-byte loads
+                                    constexpr int PR = stage_tw_row(R);
+                                    const float4* t4 = reinterpret_cast<const float4*>(tw + TOFF + k * PR);
+#pragma unroll
+                                    for (int h = 0; h < PR / 2; ++h)
+                                        {
+                                            const float4 q = t4[h];
+                                            const int r0 = 2 * h + 1;
+                                            v[b][r0] = mul(v[b][r0], c2{q.x, q.y});
+                                            if (r0 + 1 < R) v[b][r0 + 1] = mul(v[b][r0 + 1], c2{q.z, q.w});
+                                        }
+                                }
+                            else if constexpr (TWP == 1)
                                 {
                                     const c2 w1 = from(tw[step]);
                                     c2 w = w1;
@@ -346,23 +422,35 @@ __device__ __forceinline__ void stage(c2* lds, const float2* __restrict__ tw, Lo
         __syncthreads();
 }
 
-template <int NT, int N, int Ns, bool TWP, bool FIRST, bool ORD, int R, int... Rest, class Load, class Store, class Hook>
+// TOFF: the stage's first entry in the per-stage twiddle table (TWP == 2), which
+// follows the N-entry W_N table; a stage of radix R over Ns-point sub-transforms
+// holds Ns rows of stage_tw_row(R) entries.
+template <int NT, int N, int Ns, int TWP, int TOFF, bool FIRST, bool ORD, int R, int... Rest, class Load, class Store,
+    class Hook>
 __device__ __forceinline__ void stages(c2* lds, const float2* __restrict__ tw, Load& load, Store& store, Hook& hook)
 {
     constexpr bool LAST = sizeof...(Rest) == 0;
-    stage<R, NT, N, Ns, TWP, FIRST, LAST, ORD>(lds, tw, load, store, hook);
-    if constexpr (!LAST) stages<NT, N, Ns * R, TWP, false, ORD, Rest...>(lds, tw, load, store, hook);
+    stage<R, NT, N, Ns, TWP, TOFF, FIRST, LAST, ORD>(lds, tw, load, store, hook);
+    constexpr int NEXT = FIRST ? TOFF : TOFF + Ns * stage_tw_row(R);
+    if constexpr (!LAST) stages<NT, N, Ns * R, TWP, NEXT, false, ORD, Rest...>(lds, tw, load, store, hook);
 }
 
 // Compile-time packed plan.  load(b, r, i) -> c2 returns input element i
 // (= j + r*N/R1 of this lane's b-th first-stage butterfly j); store(i, c2)
 // consumes output element i, visited in increasing i per lane; hook() runs
 // once the first stage's inputs are in registers (before its butterflies).
-template <int NT_, bool TWP_, int... Rs>
+//   TWP: 0 inter-stage twiddles as R-1 loads from the W_N table, 1 as powers of one
+//        loaded root, 2 from the per-stage table (stage_tw_fill: R-1 consecutive
+//        roots per butterfly, 16-byte loads, no multiplies to form them).
+template <int NT_, int TWP_, int... Rs>
 struct PkPlan
 {
     static constexpr int NT = NT_;
-    static constexpr bool TWP = TWP_;
+    static constexpr int TWP = TWP_;
+    // entries of the twiddle table the kernels read: W_N (N) + the per-stage table
+    static constexpr size_t tw_entries() { return (size_t)N + (TWP == 2 ? stage_tw_entries<Rs...>() : 0); }
+    // host: fill tw[N ..) with the per-stage table (tw[0, N) = W_N^m is the caller's)
+    static void fill_stage_tw(float2* tw) { stage_tw_fill<Rs...>(tw, N); }
     static constexpr int N = (Rs * ...);
     static constexpr int nstages = sizeof...(Rs);
     static constexpr int R1 = fft::FirstRadix<Rs...>::value;
@@ -382,7 +470,7 @@ struct PkPlan
     template <bool ORD = true, class Load, class Store, class Hook>
     __device__ __forceinline__ static void run(c2* lds, const float2* __restrict__ tw, Load load, Store store, Hook hook)
     {
-        stages<NT, N, 1, TWP, true, ORD, Rs...>(lds, tw, load, store, hook);
+        stages<NT, N, 1, TWP, N, true, ORD, Rs...>(lds, tw, load, store, hook);
     }
 };
 

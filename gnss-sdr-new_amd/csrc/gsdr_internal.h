@@ -82,4 +82,27 @@ int replace_stream(hipStream_t* stream, const uint32_t* mask, int n_words);
 // returns x with P(a, x) = p.  (Boost gamma_p_inv, used by calculate_threshold.)
 double gamma_p_inv_int(int a, double p);
 
+// Wave64 maximum of a float by DPP lane moves (no LDS, no index arithmetic):
+// quad swaps, half-row and row mirrors give each 16-lane row its maximum, the
+// row broadcasts carry rows 0..2 into lane 63.  fmaxf keeps the float rule
+// (a NaN operand yields the other value).  The result is read from lane 63 and is
+// wave-uniform.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ float dpp_max_step(float x)
+{
+    const int o = __builtin_amdgcn_update_dpp(__float_as_int(x), __float_as_int(x), CTRL, ROW_MASK, 0xf, false);
+    return __builtin_fmaxf(x, __int_as_float(o));
+}
+
+__device__ __forceinline__ float wave_max(float v)
+{
+    v = dpp_max_step<0xb1, 0xf>(v);   // quad_perm [1,0,3,2]
+    v = dpp_max_step<0x4e, 0xf>(v);   // quad_perm [2,3,0,1]
+    v = dpp_max_step<0x141, 0xf>(v);  // row_half_mirror
+    v = dpp_max_step<0x140, 0xf>(v);  // row_mirror
+    v = dpp_max_step<0x142, 0xa>(v);  // row_bcast:15 into rows 1 and 3
+    v = dpp_max_step<0x143, 0xc>(v);  // row_bcast:31 into rows 2 and 3
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+
 }  // namespace gsdr

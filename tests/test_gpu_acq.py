@@ -211,3 +211,35 @@ def test_bad_configuration_errors():
     with pytest.raises(gsdr.GsdrError) as e:
         acq.run(np.zeros(4000, np.complex64))
     assert e.value.code == gsdr.GSDR_E_STATE
+
+
+# Packed correlate variants (acq_impl.h GSDR_PK_VARIANTS): id -> sample rate of its
+# FFT size.  Row statistic 1 (max + sum, argmax recomputed) and 2 (max only, the CFAR
+# row sum by Parseval in acq_argmax_pk_kernel) must both match the oracle.
+PK_VARIANTS = [(30, 4000000), (31, 4000000), (70, 4000000), (75, 4000000), (76, 4000000), (78, 4000000),
+               (60, 16000000), (63, 16000000), (61, 8000000), (64, 8000000), (62, 2000000), (65, 2000000)]
+
+
+@pytest.mark.parametrize("pfa", [0.01, 0.0])
+@pytest.mark.parametrize("variant,fs", PK_VARIANTS)
+def test_packed_variants_match_oracle(monkeypatch, variant, fs, pfa):
+    monkeypatch.setenv("GSDR_ACQ_CORR_VARIANT", str(variant))
+    N = fs // 1000
+    dmax, dstep = 10000, 250
+    sats = synth.random_constellation(6, seed_offset=21 + variant)
+    x = synth.gps_l1_iq(fs, N, sats, seed_offset=21 + variant)
+    prns = np.array([s.prn for s in sats[:4]] + [33 - s.prn for s in sats[:2]])
+    codes = _codes(prns, fs, N)
+    spc = int(np.ceil(fs / 1023000.0))
+    acq = gsdr.Acquisition(fs, N, dmax, dstep, pfa=pfa, max_prns=len(prns), num_doppler_bins=81)
+    acq.set_local_codes(codes, prns)
+    res = acq.run(x)[0]
+    grids = _oracle_grids(x, codes, fs, dmax, dstep, 81)
+    exact = sum(_check_result(res[p], grids[p], pfa, spc, fs, dmax, dstep, float(np.float32(fs) * np.float32(0.001)))
+                for p in range(len(prns)))
+    assert exact >= len(prns) - 1
+    if pfa > 0:
+        for p in range(len(prns)):
+            ti, di, gmax, ip, stat = pcps.max_to_input_power_statistic(grids[p])
+            if abs(stat - acq.threshold) > 1e-3 * acq.threshold:
+                assert bool(res[p]["positive"]) == bool(stat > acq.threshold)

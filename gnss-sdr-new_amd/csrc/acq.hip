@@ -66,6 +66,31 @@ bool choose_variant(gsdr_acq* a)
                 a->nt = nts[i];
                 return true;
             }
+    // packed four-step (FourStepPkPlan) for the sizes of the GNSS configurations
+    // beyond one workgroup's LDS: Galileo E1 4 / 8 ms at 8 Msps, 4 ms at 25 Msps,
+    // 1 ms at 25 Msps (GSDR_ACQ_FOUR_GENERIC=1 keeps the generic four-step)
+    {
+        struct F
+        {
+            int id, n, r, n2;
+        };
+        const F fours[] = {{24, 32000, 8, 4000}, {25, 64000, 16, 4000}, {26, 100000, 25, 4000}, {27, 25000, 5, 5000}};
+        const char* g = std::getenv("GSDR_ACQ_FOUR_GENERIC");
+        for (const F& f : fours)
+            if (f.n == N && !(g && std::atoi(g) != 0))
+                {
+                    a->variant = f.id;
+                    if (const char* e = std::getenv("GSDR_ACQ_FOUR_VARIANT")) a->variant = std::atoi(e);  // experiments
+                    a->nt = 256;
+                    a->plan4 = gsdr::fft::Plan4{};
+                    a->plan4.n = N;
+                    a->plan4.r1 = f.r;
+                    a->plan4.sub.n = f.n2;
+                    a->plan4.sub.nstages = 0;  // compile-time sub-plan
+                    a->plan.n = N;
+                    return true;
+                }
+    }
     // four-step (fft_4step.h): N = R * N2, the largest register radix R whose N2
     // has an LDS plan
     const int radices[] = {25, 20, 16, 12, 10, 8};

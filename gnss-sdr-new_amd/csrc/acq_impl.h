@@ -35,7 +35,7 @@ inline int default_pk_variant(uint32_t N)
     switch (N)
         {
         case 4000: return kDefaultCorrVariant4000;
-        case 16000: return 60;
+        case 16000: return 90;
         case 8000: return 61;
         case 2000: return 62;
         default: return 0;
@@ -313,11 +313,20 @@ __global__ void __launch_bounds__(PT::NT) acq_correlate_kernel(const float2* __r
 //         acq_argmax_pk_kernel forms it there by Parseval instead of every row
 //         summing its 4000 outputs: sum_n |R[n]|^2 = N sum_k |Y[k]|^2 for the
 //         unnormalised transform of Y = conj(X) C.
-template <class MP, int PG, int WPE, int STAT>
+//
+// PG < 0: groups of -PG PRNs without the next-code prefetch (the code values are
+// loaded by the first stage itself) -- for plans whose registers cannot hold
+// both first-stage operand sets through a transform (N = 16000 on 1024 lanes).
+constexpr int pg_count(int pg) { return pg < 0 ? -pg : pg; }
+
+template <class MP, int PG_, int WPE, int STAT>
 __global__ void __launch_bounds__(MP::NT) __attribute__((amdgpu_waves_per_eu(WPE))) acq_correlate_pk_kernel(const float2* __restrict__ X,
     const float2* __restrict__ code_fft, RowStat* __restrict__ stats, const float2* __restrict__ tw, uint32_t D,
     uint32_t P, uint32_t nblocks)
 {
+    constexpr int PG = pg_count(PG_);
+    constexpr bool PREFETCH = PG_ > 0;
+    static_assert(PREFETCH || STAT >= 1, "the slot-keyed statistic path prefetches");
     using gsdr::pk::c2;
     constexpr int NT = MP::NT;
     constexpr int NW = NT / 64;
@@ -373,7 +382,7 @@ __global__ void __launch_bounds__(MP::NT) __attribute__((amdgpu_waves_per_eu(WPE
                     for (int r = 0; r < R1; ++r)
                         {
                             xr[bb][r] = bload(xrs, jj * 8, r * NB1 * 8);
-                            cr[bb][r] = bload(crs, jj * 8, r * NB1 * 8);
+                            if constexpr (PREFETCH) cr[bb][r] = bload(crs, jj * 8, r * NB1 * 8);
                         }
                 }
         }
@@ -382,9 +391,14 @@ __global__ void __launch_bounds__(MP::NT) __attribute__((amdgpu_waves_per_eu(WPE
             if constexpr (STAT >= 1)
                 {
                     float rmax = 0.0f, sum = 0.0f;
-                    auto load = [&](int bb, int r, int) -> c2 { return gsdr::pk::conj_mul(xr[bb][r], cr[bb][r]); };
+                    auto load = [&](int bb, int r, int i) -> c2 {
+                        if constexpr (PREFETCH)
+                            return gsdr::pk::conj_mul(xr[bb][r], cr[bb][r]);
+                        else
+                            return gsdr::pk::conj_mul(xr[bb][r], bload(crs, i * 8, (int)(q * N * 8)));
+                    };
                     auto hook = [&]() {
-                        if (q + 1 < np)
+                        if (PREFETCH && q + 1 < np)
                             {
 #pragma unroll
                                 for (int bb = 0; bb < BPT1; ++bb)
@@ -488,6 +502,204 @@ __global__ void __launch_bounds__(MP::NT) __attribute__((amdgpu_waves_per_eu(WPE
                         }
                     stats[((size_t)b * P + p0 + q) * D + d] = RowStat{best.max, best.idx, best.sum, 0};
                 }
+        }
+}
+
+// ---------------------------------------------------------------- K_correlate, register four-step
+// For transforms whose full LDS image allows only one workgroup per CU (N = 16000
+// at 16 Msps: 128 KB, so the workgroup's barriers and first-stage loads cannot
+// overlap another's work).  N = R * L, decimation in frequency as in fft_4step.h:
+//   phase 1: every lane takes CPL columns n2 of the R x L view, loads the R products
+//            conj(X[n1 L + n2]) C[n1 L + n2] (coalesced), runs the packed DFT_R and
+//            scales row k1 by W_N^{n2 k1} -- the whole transform now sits in VGPRs
+//            (R * CPL complex per lane);
+//   phase 2: R/H rounds: H rows go to LDS (H * L complex -- 64 KB for H = 8, L =
+//            1000, so two workgroups share a CU), H batched L-point Stockham
+//            transforms run there, the last stage's |.|^2 feeds the row maximum.
+// Only the row maximum is kept (STAT 2): the outputs arrive in no particular order
+// and duplicated (clamped) lanes only repeat values, which a maximum ignores.
+// acq_argmax_pk_kernel recomputes the selected row on the full-LDS plan for the
+// first-maximum index and the exact peak.
+template <int R, int NT, int L, int H, int Ns, bool LAST, class Out>
+__device__ __forceinline__ void rows_stage(gsdr::pk::c2* lds, const float2* __restrict__ tw, Out& out)
+{
+    using gsdr::pk::c2;
+    constexpr int NB = L / R;       // butterflies per row
+    constexpr int TOT = H * NB;     // butterflies of the stage
+    constexpr int BPT = (TOT + NT - 1) / NT;
+    constexpr int TSTRIDE = L / (Ns * R);
+    const int wbase = (int)(threadIdx.x & ~63u);
+    c2 v[BPT][R];
+    int jb[BPT], rw[BPT];
+#pragma unroll
+    for (int b = 0; b < BPT; ++b)
+        {
+            const int jj = min((int)threadIdx.x + b * NT, TOT - 1);
+            rw[b] = jj / NB;
+            jb[b] = jj - rw[b] * NB;
+            if (TOT % NT == 0 || wbase + b * NT < TOT)
+                {
+#pragma unroll
+                    for (int r = 0; r < R; ++r) v[b][r] = lds[rw[b] * L + jb[b] + r * NB];
+                }
+        }
+    __syncthreads();
+#pragma unroll
+    for (int b = 0; b < BPT; ++b)
+        {
+            if (TOT % NT == 0 || wbase + b * NT < TOT)
+                {
+                    int k = 0;
+                    if constexpr (Ns > 1)
+                        {
+                            k = jb[b] % Ns;
+                            const c2 w1 = gsdr::pk::from(out.twiddle(k * TSTRIDE));
+                            c2 w = w1;
+#pragma unroll
+                            for (int r = 1; r < R; ++r)
+                                {
+                                    if (r > 1) w = gsdr::pk::mul(w, w1);
+                                    v[b][r] = gsdr::pk::mul(v[b][r], w);
+                                }
+                        }
+                    gsdr::pk::Dft<R>::run(v[b]);
+                    if constexpr (LAST)
+                        {
+#pragma unroll
+                            for (int r = 0; r < R; ++r) out.value(v[b][r]);
+                        }
+                    else
+                        {
+                            const int base = rw[b] * L + (jb[b] - k) * R + k;
+#pragma unroll
+                            for (int r = 0; r < R; ++r) lds[base + r * Ns] = v[b][r];
+                        }
+                }
+        }
+    if constexpr (!LAST) __syncthreads();
+}
+
+template <int NT, int L, int H, int Ns, int R, int... Rest, class Out>
+__device__ __forceinline__ void rows_stages(gsdr::pk::c2* lds, const float2* __restrict__ tw, Out& out)
+{
+    constexpr bool LAST = sizeof...(Rest) == 0;
+    rows_stage<R, NT, L, H, Ns, LAST>(lds, tw, out);
+    if constexpr (!LAST) rows_stages<NT, L, H, Ns * R, Rest...>(lds, tw, out);
+}
+
+template <int R_, int NT_, int H_, int WPE_, int... Rs>
+struct RegFourStep
+{
+    static constexpr int R = R_, NT = NT_, H = H_, WPE = WPE_;
+    static constexpr int L = (Rs * ...);
+    static constexpr int N = R * L;
+    static constexpr int CPL = (L + NT - 1) / NT;
+    static constexpr size_t lds_bytes() { return (size_t)H * L * sizeof(float2) + (NT / 64) * sizeof(float); }
+    static_assert(R % H == 0, "rows go through LDS in groups of H");
+    template <class Out>
+    __device__ __forceinline__ static void row_transforms(gsdr::pk::c2* lds, const float2* __restrict__ tw, Out& out)
+    {
+        rows_stages<NT, L, H, 1, Rs...>(lds, tw, out);
+    }
+};
+
+template <class RP>
+__global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(RP::WPE))) acq_correlate_reg_kernel(const float2* __restrict__ X,
+    const float2* __restrict__ code_fft, RowStat* __restrict__ stats, const float2* __restrict__ tw, uint32_t D,
+    uint32_t P, uint32_t nblocks)
+{
+    using gsdr::pk::c2;
+    constexpr int R = RP::R, NT = RP::NT, H = RP::H, L = RP::L, CPL = RP::CPL;
+    constexpr uint32_t N = RP::N;
+    constexpr int NW = NT / 64;
+    extern __shared__ float2 lds_raw[];
+    c2* lds = reinterpret_cast<c2*>(lds_raw);
+    float* red = reinterpret_cast<float*>(lds_raw + H * L);
+    // (row = b*D + d, PRN p), XCD-aware: the P workgroups of one row on one XCD
+    const uint32_t nrows = nblocks * D;
+    const uint32_t id = blockIdx.x;
+    const uint32_t full = nrows >> 3;
+    uint32_t row, p;
+    if (id < full * 8u * P)
+        {
+            const uint32_t xcd = id & 7u, slot = id >> 3;
+            row = (slot / P) * 8u + xcd;
+            p = slot - (slot / P) * P;
+        }
+    else
+        {
+            const uint32_t t = id - full * 8u * P;
+            row = full * 8u + t / P;
+            p = t - (t / P) * P;
+        }
+    const uint32_t b = row / D, d = row - (row / D) * D;
+    const auto xrs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float2*>(X) + (size_t)row * N, 0, (int)(N * sizeof(c2)), 0x00020000);
+    const auto crs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float2*>(code_fft) + (size_t)p * N, 0, (int)(N * sizeof(c2)), 0x00020000);
+    auto bload = [](decltype(xrs) rs, int voff, int soff) -> c2 {
+        const auto u = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, 0);
+        return c2{__uint_as_float(u[0]), __uint_as_float(u[1])};
+    };
+    const int wbase = (int)(threadIdx.x & ~63u);
+    // phase 1: columns (clamped: a lane past L repeats column L-1, whose values
+    // are written to the same LDS words and only repeat outputs)
+    c2 v[CPL][R];
+#pragma unroll
+    for (int c = 0; c < CPL; ++c)
+        {
+            if (L % NT == 0 || wbase + c * NT < L)
+                {
+                    const int n2 = min((int)threadIdx.x + c * NT, L - 1);
+#pragma unroll
+                    for (int n1 = 0; n1 < R; ++n1)
+                        v[c][n1] = gsdr::pk::conj_mul(bload(xrs, n2 * 8, n1 * L * 8), bload(crs, n2 * 8, n1 * L * 8));
+                    gsdr::pk::Dft<R>::run(v[c]);
+                    const c2 w1 = gsdr::pk::from(tw[n2]);
+                    c2 w = w1;
+#pragma unroll
+                    for (int k1 = 1; k1 < R; ++k1)
+                        {
+                            if (k1 > 1) w = gsdr::pk::mul(w, w1);
+                            v[c][k1] = gsdr::pk::mul(v[c][k1], w);
+                        }
+                }
+        }
+    struct Out
+    {
+        const float2* tw;
+        float m;
+        __device__ __forceinline__ float2 twiddle(int m_) const { return tw[m_ * R]; }  // W_L^m = W_N^{m R}
+        __device__ __forceinline__ void value(c2 x) { m = __builtin_fmaxf(m, __builtin_fmaf(x.x, x.x, x.y * x.y)); }
+    } out{tw, 0.0f};
+    // phase 2: rows k1 = h*H .. h*H+H-1 through LDS
+#pragma unroll
+    for (int h = 0; h < R / H; ++h)
+        {
+            if (h > 0) __syncthreads();  // the previous group's last-stage reads are done
+#pragma unroll
+            for (int c = 0; c < CPL; ++c)
+                {
+                    if (L % NT == 0 || wbase + c * NT < L)
+                        {
+                            const int n2 = min((int)threadIdx.x + c * NT, L - 1);
+#pragma unroll
+                            for (int i = 0; i < H; ++i) lds[i * L + n2] = v[c][h * H + i];
+                        }
+                }
+            __syncthreads();
+            RP::row_transforms(lds, tw, out);
+        }
+    float rmax = gsdr::wave_max(out.m);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) red[wave] = rmax;
+    __syncthreads();
+    if (threadIdx.x == 0)
+        {
+            float best = red[0];
+#pragma unroll
+            for (int w2 = 1; w2 < NW; ++w2) best = __builtin_fmaxf(best, red[w2]);
+            stats[((size_t)b * P + p) * D + d] = RowStat{best, 0u, 0.0f, 0};
         }
 }
 
@@ -1128,8 +1340,10 @@ size_t item_bytes(int it) { return it == GSDR_ITEM_CSHORT ? 4 : (it == GSDR_ITEM
 // Correlate-kernel variants for N = 4000 (env GSDR_ACQ_CORR_VARIANT selects one;
 // 0 = the single-transform kernel of the plan variant).
 // Packed-f32 correlate (and forward) variants: (id, plan, PRNs per workgroup,
-// waves-per-EU hint).  30/35/37 are N = 4000 plans (30 the default); 60-62 the
-// other compile-time sizes (1 ms at 16 / 8 / 2 Msps).
+// waves-per-EU hint).  30-39, 70-78 are N = 4000 plans (70 the default); 60-69 the
+// other compile-time sizes (1 ms at 16 / 8 / 2 Msps); 90-92 run the correlate on
+// the register four-step (acq_correlate_reg_kernel, N = 16000, 90 the default) and
+// the forward / argmax passes on the listed plan.
 // Columns: (id, plan, PRNs per workgroup, waves-per-EU hint, row statistic: 0 max +
 // first argmax in the kernel, 1 max + sum with the argmax recomputed for the
 // selected row, see acq_correlate_pk_kernel).
@@ -1148,6 +1362,13 @@ size_t item_bytes(int it) { return it == GSDR_ITEM_CSHORT ? 4 : (it == GSDR_ITEM
     X(63, (gsdr::pk::PkPlan<1024, 1, 16, 10, 10, 10>), 1, 1, 2)         \
     X(64, (gsdr::pk::PkPlan<512, 1, 20, 20, 20>), 1, 1, 2)              \
     X(65, (gsdr::pk::PkPlan<256, 1, 20, 10, 10>), 1, 1, 2)              \
+    X(66, (gsdr::pk::PkPlan<1024, 1, 16, 10, 10, 10>), 4, 1, 2)         \
+    X(67, (gsdr::pk::PkPlan<1024, 1, 16, 10, 10, 10>), -4, 1, 2)        \
+    X(68, (gsdr::pk::PkPlan<1024, 1, 16, 10, 10, 10>), -8, 1, 2)        \
+    X(69, (gsdr::pk::PkPlan<1024, 1, 16, 10, 10, 10>), -32, 1, 2)       \
+    X(90, (gsdr::pk::PkPlan<1024, 1, 16, 10, 10, 10>), 1, 1, 2)         \
+    X(91, (gsdr::pk::PkPlan<1024, 1, 16, 10, 10, 10>), 1, 1, 2)         \
+    X(92, (gsdr::pk::PkPlan<1024, 1, 16, 10, 10, 10>), 1, 1, 2)         \
     X(70, (gsdr::pk::PkPlan<256, 1, 25, 16, 10>), 1, 1, 2)              \
     X(71, (gsdr::pk::PkPlan<256, 2, 25, 16, 10>), 1, 1, 1)              \
     X(72, (gsdr::pk::PkPlan<256, 2, 25, 16, 10>), 1, 1, 2)              \

@@ -5,13 +5,43 @@
 namespace gsdr_acq_impl
 {
 
+// Variants whose correlate kernel is not acq_correlate_pk_kernel (their forward
+// and argmax passes use the variant's PkPlan): 90 = N 16000 on the register
+// four-step 16 x (10 x 10 x 10), 512 lanes, 8 rows per LDS round.
+using RegPlan90 = RegFourStep<16, 512, 8, 1, 10, 10, 10>;
+using RegPlan91 = RegFourStep<16, 512, 4, 6, 10, 10, 10>;
+using RegPlan92 = RegFourStep<16, 512, 4, 1, 10, 10, 10>;
+
+template <class RP>
+int launch_reg(gsdr_acq* a, uint32_t nblocks, hipStream_t s)
+{
+    hipLaunchKernelGGL((acq_correlate_reg_kernel<RP>), dim3(nblocks * a->D * a->nprn), dim3(RP::NT), RP::lds_bytes(),
+        s, a->d_X, a->d_code_fft, a->d_stats, a->d_tw, a->D, a->nprn, nblocks);
+    return GSDR_OK;
+}
+
+template <class RP>
+int setup_reg()
+{
+    GSDR_HIP(hipFuncSetAttribute((const void*)acq_correlate_reg_kernel<RP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (int)RP::lds_bytes()));
+    return GSDR_OK;
+}
+
 int launch_corr_variant(gsdr_acq* a, uint32_t nblocks, hipStream_t s)
 {
+    switch (a->corr_variant)
+        {
+        case 90: return launch_reg<RegPlan90>(a, nblocks, s);
+        case 91: return launch_reg<RegPlan91>(a, nblocks, s);
+        case 92: return launch_reg<RegPlan92>(a, nblocks, s);
+        default: break;
+        }
 #define GSDR_PK_CASE(ID, MP, PG, WPE, ST)                                                                       \
     case ID:                                                                                                    \
         {                                                                                                       \
             using M = GSDR_UNPAREN MP;                                                                          \
-            const uint32_t groups = (a->nprn + (PG)-1) / (PG);                                                  \
+            const uint32_t groups = (a->nprn + pg_count(PG) - 1) / pg_count(PG);                                                  \
             hipLaunchKernelGGL((acq_correlate_pk_kernel<M, PG, WPE, ST>), dim3(nblocks * a->D * groups),         \
                 dim3(M::NT), a->corr_lds_bytes, s, a->d_X, a->d_code_fft, a->d_stats, a->d_tw, a->D, a->nprn,   \
                 nblocks);                                                                                       \
@@ -103,6 +133,9 @@ int setup_corr_variant(gsdr_acq* a, int v)
                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)M::lds_bytes()));                              \
             GSDR_HIP(hipFuncSetAttribute((const void*)acq_forward_pk_kernel<M, GSDR_ITEM_IBYTE>,               \
                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)M::lds_bytes()));                              \
+            if (ID == 90 && setup_reg<RegPlan90>() != GSDR_OK) return GSDR_E_DEVICE;                           \
+            if (ID == 91 && setup_reg<RegPlan91>() != GSDR_OK) return GSDR_E_DEVICE;                           \
+            if (ID == 92 && setup_reg<RegPlan92>() != GSDR_OK) return GSDR_E_DEVICE;                           \
             a->corr_variant = ID;                                                                               \
             a->corr_stat = ST;                                                                                  \
             a->tw_entries = M::tw_entries();                                                                    \

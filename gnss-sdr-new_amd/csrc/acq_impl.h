@@ -520,14 +520,37 @@ __global__ void __launch_bounds__(MP::NT) __attribute__((amdgpu_waves_per_eu(WPE
 // and duplicated (clamped) lanes only repeat values, which a maximum ignores.
 // acq_argmax_pk_kernel recomputes the selected row on the full-LDS plan for the
 // first-maximum index and the exact peak.
-template <int R, int NT, int L, int H, int Ns, bool LAST, class Out>
-__device__ __forceinline__ void rows_stage(gsdr::pk::c2* lds, const float2* __restrict__ tw, Out& out)
+// Row layouts in LDS: row rw at rw * stride, element e at e + (e / S) * P -- one
+// pad of P elements every S, so the strided Stockham writes spread over the banks.
+// The stage functions need S | Ns (writes) and S | L/R (reads) so every address
+// is a per-butterfly base plus a compile-time offset.  Pads chosen with an LDS
+// bank model (ds_write_b64: 4 x 16 lanes, ds_read_b64: 2 x 32 lanes; see
+// MI355X_MICROARCH.md LDS): for L = 1000, radix 10, the buffers written by the
+// first and second row stages pad (S, P) = (10, 1) and (50, 3) -- 25 % fewer LDS
+// cycles than the plain layout.
+template <int L, int S, int P>
+struct RowPad
+{
+    static constexpr int stride = L + (S ? (L / S) * P : 0);
+    static constexpr int pad_every = S;
+    __device__ __forceinline__ static int pad(int e) { return S ? e + (e / S) * P : e; }
+    static constexpr int cpad(int e) { return S ? e + (e / S) * P : e; }
+};
+
+template <int R, int NT, int L, int H, int Ns, bool LAST, class In, class OutL, class Out>
+__device__ __forceinline__ void rows_stage(gsdr::pk::c2* lds, Out& out)
 {
     using gsdr::pk::c2;
     constexpr int NB = L / R;       // butterflies per row
     constexpr int TOT = H * NB;     // butterflies of the stage
     constexpr int BPT = (TOT + NT - 1) / NT;
     constexpr int TSTRIDE = L / (Ns * R);
+    // reads: element jb + r NB, pad(jb) + cpad(r NB) needs S | NB
+    static_assert(In::pad_every == 0 || NB % In::pad_every == 0, "read layout: S must divide L/R");
+    // writes: element (jb - k) R + k + r Ns (k < Ns), pad((jb - k) R) + k + cpad(r Ns)
+    // needs S | Ns R and Ns | S
+    static_assert(LAST || OutL::pad_every == 0 || ((Ns * R) % OutL::pad_every == 0 && OutL::pad_every % Ns == 0),
+        "write layout: S must divide Ns R and be a multiple of Ns");
     const int wbase = (int)(threadIdx.x & ~63u);
     c2 v[BPT][R];
     int jb[BPT], rw[BPT];
@@ -539,8 +562,10 @@ __device__ __forceinline__ void rows_stage(gsdr::pk::c2* lds, const float2* __re
             jb[b] = jj - rw[b] * NB;
             if (TOT % NT == 0 || wbase + b * NT < TOT)
                 {
+                    // element jb + r NB: the pad of r NB is compile-time (S | NB)
+                    const int base = rw[b] * In::stride + In::pad(jb[b]);
 #pragma unroll
-                    for (int r = 0; r < R; ++r) v[b][r] = lds[rw[b] * L + jb[b] + r * NB];
+                    for (int r = 0; r < R; ++r) v[b][r] = lds[base + In::cpad(r * NB)];
                 }
         }
     __syncthreads();
@@ -570,36 +595,65 @@ __device__ __forceinline__ void rows_stage(gsdr::pk::c2* lds, const float2* __re
                         }
                     else
                         {
-                            const int base = rw[b] * L + (jb[b] - k) * R + k;
+                            // element (jb - k) R + k + r Ns: with S | Ns and S | Ns R the
+                            // pad splits into the butterfly's part and a compile-time r part
+                            const int base = rw[b] * OutL::stride + OutL::pad((jb[b] - k) * R) + k;
 #pragma unroll
-                            for (int r = 0; r < R; ++r) lds[base + r * Ns] = v[b][r];
+                            for (int r = 0; r < R; ++r) lds[base + OutL::cpad(r * Ns)] = v[b][r];
                         }
                 }
         }
     if constexpr (!LAST) __syncthreads();
 }
 
-template <int NT, int L, int H, int Ns, int R, int... Rest, class Out>
-__device__ __forceinline__ void rows_stages(gsdr::pk::c2* lds, const float2* __restrict__ tw, Out& out)
+template <int NT, int L, int H, int Ns, class Pads, int Si, int R, int... Rest, class Out>
+__device__ __forceinline__ void rows_stages(gsdr::pk::c2* lds, Out& out)
 {
     constexpr bool LAST = sizeof...(Rest) == 0;
-    rows_stage<R, NT, L, H, Ns, LAST>(lds, tw, out);
-    if constexpr (!LAST) rows_stages<NT, L, H, Ns * R, Rest...>(lds, tw, out);
+    using In = typename Pads::template layout<Si>;
+    using OutL = typename Pads::template layout<LAST ? Si : Si + 1>;
+    rows_stage<R, NT, L, H, Ns, LAST, In, OutL>(lds, out);
+    if constexpr (!LAST) rows_stages<NT, L, H, Ns * R, Pads, Si + 1, Rest...>(lds, out);
 }
 
-template <int R_, int NT_, int H_, int WPE_, int... Rs>
+// Pads for the buffers between the row stages (buffer 0 = phase 1's rows).
+template <int L>
+struct NoPads
+{
+    template <int I>
+    using layout = RowPad<L, 0, 0>;
+};
+struct Pads1000x10
+{
+    template <int I>
+    using layout = std::conditional_t<I == 1, RowPad<1000, 10, 1>,
+        std::conditional_t<I == 2, RowPad<1000, 50, 3>, RowPad<1000, 0, 0>>>;
+};
+
+template <int R_, int NT_, int H_, int WPE_, class Pads_, int... Rs>
 struct RegFourStep
 {
     static constexpr int R = R_, NT = NT_, H = H_, WPE = WPE_;
     static constexpr int L = (Rs * ...);
     static constexpr int N = R * L;
     static constexpr int CPL = (L + NT - 1) / NT;
-    static constexpr size_t lds_bytes() { return (size_t)H * L * sizeof(float2) + (NT / 64) * sizeof(float); }
+    using Pads = Pads_;
+    static constexpr int max_stride()
+    {
+        int m = L;
+        constexpr int ns = sizeof...(Rs);
+        if (ns > 1 && Pads::template layout<1>::stride > m) m = Pads::template layout<1>::stride;
+        if (ns > 2 && Pads::template layout<2>::stride > m) m = Pads::template layout<2>::stride;
+        if (ns > 3 && Pads::template layout<3>::stride > m) m = Pads::template layout<3>::stride;
+        return m;
+    }
+    static constexpr int lds_elems = H * max_stride();
+    static constexpr size_t lds_bytes() { return (size_t)lds_elems * sizeof(float2) + (NT / 64) * sizeof(float); }
     static_assert(R % H == 0, "rows go through LDS in groups of H");
     template <class Out>
-    __device__ __forceinline__ static void row_transforms(gsdr::pk::c2* lds, const float2* __restrict__ tw, Out& out)
+    __device__ __forceinline__ static void row_transforms(gsdr::pk::c2* lds, Out& out)
     {
-        rows_stages<NT, L, H, 1, Rs...>(lds, tw, out);
+        rows_stages<NT, L, H, 1, Pads, 0, Rs...>(lds, out);
     }
 };
 
@@ -614,7 +668,7 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(RP:
     constexpr int NW = NT / 64;
     extern __shared__ float2 lds_raw[];
     c2* lds = reinterpret_cast<c2*>(lds_raw);
-    float* red = reinterpret_cast<float*>(lds_raw + H * L);
+    float* red = reinterpret_cast<float*>(lds_raw + RP::lds_elems);
     // (row = b*D + d, PRN p), XCD-aware: the P workgroups of one row on one XCD
     const uint32_t nrows = nblocks * D;
     const uint32_t id = blockIdx.x;
@@ -688,7 +742,7 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(RP:
                         }
                 }
             __syncthreads();
-            RP::row_transforms(lds, tw, out);
+            RP::row_transforms(lds, out);
         }
     float rmax = gsdr::wave_max(out.m);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;

@@ -8,9 +8,9 @@ namespace gsdr_acq_impl
 // Variants whose correlate kernel is not acq_correlate_pk_kernel (their forward
 // and argmax passes use the variant's PkPlan): 90 = N 16000 on the register
 // four-step 16 x (10 x 10 x 10), 512 lanes, 8 rows per LDS round.
-using RegPlan90 = RegFourStep<16, 512, 8, 1, 10, 10, 10>;
-using RegPlan91 = RegFourStep<16, 512, 4, 6, 10, 10, 10>;
-using RegPlan92 = RegFourStep<16, 512, 4, 1, 10, 10, 10>;
+using RegPlan90 = RegFourStep<16, 512, 8, 1, NoPads<1000>, 10, 10, 10>;
+using RegPlan91 = RegFourStep<16, 512, 8, 1, Pads1000x10, 10, 10, 10>;
+using RegPlan92 = RegFourStep<16, 512, 4, 1, Pads1000x10, 10, 10, 10>;
 
 template <class RP>
 int launch_reg(gsdr_acq* a, uint32_t nblocks, hipStream_t s)

@@ -44,7 +44,10 @@
 namespace
 {
 
-constexpr int kTrkThreads = 512;
+#ifndef GSDR_TRK_THREADS
+#define GSDR_TRK_THREADS 512
+#endif
+constexpr int kTrkThreads = GSDR_TRK_THREADS;
 constexpr int kMaxCn0 = 64;         // cn0_samples capacity
 constexpr int kMaxTrkTaps = 5;
 constexpr int kMaxCodeFloats = 16384;

@@ -46,6 +46,21 @@ def emit(cfg, stage, fs, samples, sec, extra=None):
     print(json.dumps(d), flush=True)
 
 
+FP32_PEAK_TFLOPS = 157.3  # MI355X dense FP32 (vector), MI355X_MICROARCH.md
+
+
+def acq_roofline(N, P, D, blocks, sec):
+    """Nominal FFT flops of the PCPS grid: D forward transforms
+    (5 N log2 N + 6 N: wipe-off product + FFT) and P*D correlate transforms
+    (5 N log2 N + 11 N: product, FFT, |.|^2 and the row statistic) per block,
+    against the FP32 peak -- the acquisition kernels are VALU-bound."""
+    import math
+    f = D * (5 * N * math.log2(N) + 6 * N) + P * D * (5 * N * math.log2(N) + 11 * N)
+    tf = f * blocks / sec / 1e12
+    return {"roofline": {"bound": "valu", "achieved": round(tf, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(tf / FP32_PEAK_TFLOPS, 4), "nominal_flops_per_block": round(f)}}
+
+
 def trk_conf(gsdr, fs, sig, nch, **kw):
     c = gsdr.trk_conf_default()
     c["fs_in"] = fs
@@ -122,7 +137,7 @@ def main():
         acq.set_local_codes(np.stack([synth.gps_ca_sampled(p, fs) for p in range(1, 33)]), np.arange(1, 33))
         res = torch.zeros(B * 32 * gsdr.ACQ_RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
         sec = timed(lambda: acq.run_device(iq_dev.data_ptr(), B, N, 0, res.data_ptr()), a.reps, 3, torch)
-        emit("C3", "acquisition 32 PRN x 81 Doppler, N=16000", fs, B * N, sec)
+        emit("C3", "acquisition 32 PRN x 81 Doppler, N=16000", fs, B * N, sec, acq_roofline(N, 32, 81, B, sec))
         acq.close()
         del iq_dev
 
@@ -162,7 +177,7 @@ def main():
         res = torch.zeros(B * 36 * gsdr.ACQ_RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
         sec = timed(lambda: acq.run_device(iq_dev.data_ptr(), B, 2 * N, 0, res.data_ptr()), max(2, a.reps // 3), 1, torch)
         emit("C4", "acquisition 36 PRN x %d Doppler, bit transition, FFT %d" % (acq.num_doppler_bins, acq.fft_size),
-             fs, B * 2 * N, sec)
+             fs, B * 2 * N, sec, acq_roofline(2 * N, 36, acq.num_doppler_bins, B, sec))
         acq.close()
         del iq_dev
 

@@ -334,7 +334,7 @@ __global__ void __launch_bounds__(MP::NT) __attribute__((amdgpu_waves_per_eu(WPE
     constexpr uint32_t N = MP::N;
     extern __shared__ float2 lds_raw[];
     c2* lds = reinterpret_cast<c2*>(lds_raw);
-    RowStat* scratch = reinterpret_cast<RowStat*>(lds_raw + N);
+    RowStat* scratch = reinterpret_cast<RowStat*>(lds_raw + MP::lds_bytes() / sizeof(float2));
     const uint32_t G = (P + PG - 1) / PG;
     const uint32_t nrows = nblocks * D;
     const uint32_t id = blockIdx.x;
@@ -775,7 +775,7 @@ __global__ void __launch_bounds__(MP::NT) acq_argmax_pk_kernel(const float2* __r
     constexpr uint32_t N = MP::N;
     extern __shared__ float2 lds_raw[];
     c2* lds = reinterpret_cast<c2*>(lds_raw);
-    unsigned long long* scratch = reinterpret_cast<unsigned long long*>(lds_raw + N);
+    unsigned long long* scratch = reinterpret_cast<unsigned long long*>(lds_raw + MP::lds_bytes() / sizeof(float2));
     const uint32_t bp = blockIdx.x;
     const uint32_t b = bp / P, p = bp - b * P;
     const uint32_t d = res[bp].doppler_index;
@@ -888,6 +888,40 @@ __device__ __forceinline__ void pool_release(uint32_t* slots, int slot)
         __hip_atomic_fetch_and(&slots[slot >> 5], ~(1u << (slot & 31)), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Cell (b, d, p) of a 1-D correlate grid over nrows = nblocks * D rows x P PRNs,
+// XCD-aware for code reuse: workgroup ids go to the XCDs round-robin, so XCD x
+// takes rows x, x + 8, ... and walks them PRN-group-major -- for each group of PG
+// PRNs (PG | P) every one of its rows, the group's PG transforms of a row
+// consecutively.  An XCD's L2 then holds PG code spectra while the X rows stream
+// (at C4, N = 64000: 4 x 512 KB of codes instead of cycling through all 36) and
+// each X row is fetched once per group.  Rows beyond the last multiple of 8 are
+// mapped row-major.
+__device__ __forceinline__ void dwell_cell(uint32_t D, uint32_t P, uint32_t nrows, uint32_t& b, uint32_t& d,
+    uint32_t& p)
+{
+    const uint32_t id = blockIdx.x;
+    const uint32_t full = nrows >> 3;
+    const uint32_t PG = (P % 4u == 0u) ? 4u : ((P % 2u == 0u) ? 2u : 1u);
+    uint32_t row;
+    if (id < full * 8u * P)
+        {
+            const uint32_t xcd = id & 7u, slot = id >> 3;
+            const uint32_t per_group = full * PG;
+            const uint32_t pg = slot / per_group, rem = slot - pg * per_group;
+            const uint32_t ri = rem / PG;
+            row = ri * 8u + xcd;
+            p = pg * PG + (rem - ri * PG);
+        }
+    else
+        {
+            const uint32_t t = id - full * 8u * P;
+            row = full * 8u + t / P;
+            p = t - (t / P) * P;
+        }
+    b = row / D;
+    d = row - b * D;
+}
+
 template <class PT>
 __global__ void __launch_bounds__(PT::NT) acq_correlate_dwell_kernel(const float2* __restrict__ X,
     const float2* __restrict__ code_fft, RowStat* __restrict__ stats, const float2* __restrict__ tw,
@@ -897,7 +931,8 @@ __global__ void __launch_bounds__(PT::NT) acq_correlate_dwell_kernel(const float
     extern __shared__ float2 lds[];
     RowStat* scratch = reinterpret_cast<RowStat*>(lds + gsdr::fft::lds_elems_dev(plan));
     const uint32_t N = plan.n;
-    const uint32_t d = blockIdx.x / ap.P, p = blockIdx.x - d * ap.P, b = blockIdx.y;
+    uint32_t b, d, p;
+    dwell_cell(ap.D, ap.P, gridDim.x / ap.P, b, d, p);
     const uint32_t K = ap.dwells;
     const int slot = K > 1 ? pool_acquire(acc_slots, acc_words) : 0;
     float* acc = acc_pool + (size_t)slot * ap.eff;
@@ -1431,7 +1466,9 @@ size_t item_bytes(int it) { return it == GSDR_ITEM_CSHORT ? 4 : (it == GSDR_ITEM
     X(75, (gsdr::pk::PkPlan<256, 1, 16, 25, 10>), 1, 1, 2)              \
     X(76, (gsdr::pk::PkPlan<256, 1, 25, 10, 16>), 1, 1, 2)              \
     X(77, (gsdr::pk::PkPlan<256, 1, 25, 16, 10>), 1, 5, 2)              \
-    X(78, (gsdr::pk::PkPlan<256, 1, 20, 20, 10>), 1, 1, 2)
+    X(78, (gsdr::pk::PkPlan<256, 1, 20, 20, 10>), 1, 1, 2)              \
+    X(79, (gsdr::pk::PkPlan<256, 3, 25, 16, 10>), 1, 1, 2)              \
+    X(80, (gsdr::pk::PkPlan<256, 3, 20, 20, 10>), 1, 1, 2)
 
 template <class PT>
 int set_lds_attrs(size_t bytes)
@@ -1620,7 +1657,7 @@ int launch_general(gsdr_acq* a, const void* iq, int item_type, uint32_t nblocks,
     t.end(0);
     AcqParams ap = params_of(a);
     t.begin();
-    hipLaunchKernelGGL((acq_correlate_dwell_kernel<PT>), dim3(a->D * a->nprn, nblocks), dim3(PT::NT), lds, s, a->d_X,
+    hipLaunchKernelGGL((acq_correlate_dwell_kernel<PT>), dim3(a->D * a->nprn * nblocks), dim3(PT::NT), lds, s, a->d_X,
         a->d_code_fft, a->d_stats, a->d_tw, plan_of<PT>(a), ap, a->d_acc, a->d_acc_slots, a->acc_words);
     GSDR_HIP(hipGetLastError());
     t.end(1);

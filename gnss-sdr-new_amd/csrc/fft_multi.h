@@ -135,6 +135,18 @@ struct FirstRadix
     static constexpr int value = R;
 };
 
+// second radix of a plan (0 for a one-stage plan)
+template <int... Rs>
+struct SecondRadix
+{
+    static constexpr int value = 0;
+};
+template <int R1, int R2, int... Rest>
+struct SecondRadix<R1, R2, Rest...>
+{
+    static constexpr int value = R2;
+};
+
 // Compile-time multi-transform plan.  load(b, r, i, float2 (&)[PB]) fills element
 // i (= j + r*N/R1 of this lane's b-th first-stage butterfly j) of the PB inputs;
 // store(i, const float2 (&)[PB]) consumes output element i; hook() runs once the

@@ -245,6 +245,10 @@ struct Dft<25> : DftCT<5, 5>
 // ---- per-stage twiddle table (TWP == 2) ----
 // Row length for a radix-R stage: the R-1 roots, padded to an even count.
 constexpr int stage_tw_row(int R) { return (R - 1 + 1) & ~1; }
+// LDS copy of the middle stage's table (TWP == 3): rows of stage_tw_row(R) + 2
+// entries, so 16 lanes reading 16 different rows with ds_read_b128 hit 16
+// different bank quads (row stride 36 dwords for R = 16).
+constexpr int lds_tw_row(int R) { return stage_tw_row(R) + 2; }
 
 template <int... Rs>
 constexpr size_t stage_tw_entries()
@@ -346,7 +350,17 @@ __device__ __forceinline__ void stage(c2* lds, const float2* __restrict__ tw, Lo
                         {
                             k = j % Ns;
                             const int step = k * TSTRIDE;
-                            if constexpr (TWP == 2)
+                            // TWP 3: the middle stage reads its roots from the LDS copy
+                            // of the per-stage table (PkPlan::run fills it), the last
+                            // stage forms powers as TWP 1
+                            constexpr int MODE = TWP == 3 ? (LAST ? 1 : 3) : TWP;
+                            if constexpr (MODE == 3)
+                                {
+                                    const c2* lt = lds + N + k * lds_tw_row(R);
+#pragma unroll
+                                    for (int r = 1; r < R; ++r) v[b][r] = mul(v[b][r], lt[r - 1]);
+                                }
+                            else if constexpr (MODE == 2)
                                 {
                                     // per-stage table (stage_tw_fill): row k holds W_N^{r k TSTRIDE},
                                     // r = 1..R-1, padded to an even count -> 16-byte loads
@@ -361,7 +375,7 @@ __device__ __forceinline__ void stage(c2* lds, const float2* __restrict__ tw, Lo
                                             if (r0 + 1 < R) v[b][r0 + 1] = mul(v[b][r0 + 1], c2{q.z, q.w});
                                         }
                                 }
-                            else if constexpr (TWP == 1)
+                            else if constexpr (MODE == 1)
                                 {
                                     const c2 w1 = from(tw[step]);
                                     c2 w = w1;
@@ -448,7 +462,7 @@ struct PkPlan
     static constexpr int NT = NT_;
     static constexpr int TWP = TWP_;
     // entries of the twiddle table the kernels read: W_N (N) + the per-stage table
-    static constexpr size_t tw_entries() { return (size_t)N + (TWP == 2 ? stage_tw_entries<Rs...>() : 0); }
+    static constexpr size_t tw_entries() { return (size_t)N + (TWP >= 2 ? stage_tw_entries<Rs...>() : 0); }
     // host: fill tw[N ..) with the per-stage table (tw[0, N) = W_N^m is the caller's)
     static void fill_stage_tw(float2* tw) { stage_tw_fill<Rs...>(tw, N); }
     static constexpr int N = (Rs * ...);
@@ -456,7 +470,11 @@ struct PkPlan
     static constexpr int R1 = fft::FirstRadix<Rs...>::value;
     static constexpr int BPT1 = fft::bpt_for(R1);
     static constexpr int NB1 = N / R1;
-    static constexpr size_t lds_bytes() { return (size_t)N * sizeof(c2); }
+    static constexpr int R2 = fft::SecondRadix<Rs...>::value;
+    static_assert(TWP != 3 || sizeof...(Rs) == 3, "TWP 3: one middle stage");
+    // TWP 3: the middle stage's table (R1 rows of its R2 - 1 roots) after the data
+    static constexpr int LTW = TWP == 3 ? R1 * lds_tw_row(R2) : 0;
+    static constexpr size_t lds_bytes() { return (size_t)(N + LTW) * sizeof(c2); }
     // last stage: radix, butterflies per thread, output stride; store(i, v, slot)
     // receives slot = r*BPTL + b in [0, RL*BPTL), this lane's output order
     static constexpr int RL = (0, ..., Rs);
@@ -470,6 +488,19 @@ struct PkPlan
     template <bool ORD = true, class Load, class Store, class Hook>
     __device__ __forceinline__ static void run(c2* lds, const float2* __restrict__ tw, Load load, Store store, Hook hook)
     {
+        if constexpr (TWP == 3)
+            {
+                // copy the middle stage's rows (global per-stage table at tw[N]) to
+                // LDS; the first stage's barrier orders these writes before the
+                // middle stage's reads, and a rewrite (next transform) stores the
+                // same values
+                constexpr int RW = stage_tw_row(R2);
+                for (int i = (int)threadIdx.x; i < R1 * RW; i += NT)
+                    {
+                        const int row = i / RW, q = i - row * RW;
+                        lds[N + row * lds_tw_row(R2) + q] = from(tw[N + i]);
+                    }
+            }
         stages<NT, N, 1, TWP, N, true, ORD, Rs...>(lds, tw, load, store, hook);
     }
 };

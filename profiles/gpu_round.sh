@@ -19,5 +19,9 @@ echo "== rocprof" &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
     python3 bench.py --no-cpu-baseline --steps 20 > "$OUT/bench_prof.json" 2> "$OUT/prof.err" &&
 find "$OUT/prof" -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats.csv" \; &&
-cat "$OUT/kernel_stats.csv"
+cat "$OUT/kernel_stats.csv" &&
+echo "== torchrun (world size 1, RCCL init + barrier + max-reduce path of bench.py)" &&
+timeout -k 10 200 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
+    --master-port 29517 bench.py --gpus 1 --steps 10 --warmup 5 --no-cpu-baseline > "$OUT/bench_torchrun.json" 2> "$OUT/bench_torchrun.err" &&
+cat "$OUT/bench_torchrun.json"
 echo "exit $?"

@@ -468,7 +468,10 @@ def main():
                 line["roofline"]["pmc"] = {
                     "source": pmc.get("file"),
                     "valu_wave_instructions_per_block": round(kc["SQ_INSTS_VALU"] / pmc["blocks"]),
-                    "lds_bank_conflict_frac": round(kc.get("SQ_LDS_BANK_CONFLICT", 0) / max(kc.get("SQ_ACTIVE_INST_LDS", 1), 1), 3),
+                    # bank-conflict cycles over all LDS-array cycles (SQ_LDS_IDX_ACTIVE,
+                    # MI355X_MICROARCH.md LDS); older summaries lack that counter
+                    "lds_bank_conflict_frac": (round(kc["SQ_LDS_BANK_CONFLICT"] / kc["SQ_LDS_IDX_ACTIVE"], 3)
+                                               if kc.get("SQ_LDS_IDX_ACTIVE") and "SQ_LDS_BANK_CONFLICT" in kc else None),
                     "hbm_bytes_per_block": round(pmc["hbm_bytes_per_launch"] / pmc["blocks"]) if pmc.get("hbm_bytes_per_launch") else None,
                 }
         line["stages_us_per_launch"] = {

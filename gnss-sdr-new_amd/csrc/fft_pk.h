@@ -295,10 +295,19 @@ inline void stage_tw_fill(float2* tw, int N)
 //        first-maximum scan needs it); without ORD it visits butterfly by
 //        butterfly, so a partially filled pass is skipped as a whole instead of
 //        predicating every output (order-free reductions: max, sum).
-template <int R, int NT, int N, int Ns, int TWP, int TOFF, bool FIRST, bool LAST, bool ORD, class Load, class Store,
-    class Hook>
+//   PADL (TWP_ >> 4): the buffer the last stage reads holds its N/RL-element
+//        blocks at a stride of N/RL + PADL, so the penultimate stage's strided
+//        writes spread over the LDS banks (bank model of MI355X_MICROARCH.md LDS:
+//        PADL = 9 makes the 25 x 16 x 10 plan's transposes conflict-free).
+template <int R, int NT, int N, int Ns, int TWP_, int TOFF, bool FIRST, bool LAST, bool PEN, bool ORD, class Load,
+    class Store, class Hook>
 __device__ __forceinline__ void stage(c2* lds, const float2* __restrict__ tw, Load& load, Store& store, Hook& hook)
 {
+    constexpr int TWP = TWP_ & 15;
+    constexpr int PADL = TWP_ >> 4;
+    // elements before the TWP 3 table: N plus the last-stage pads (this stage is
+    // the penultimate one whenever it reads the table)
+    constexpr int DATA = N + (N / (Ns * R) - 1) * PADL;
     constexpr int BPT = fft::bpt_for(R);
     constexpr int NB = N / R;
     constexpr int TSTRIDE = N / (Ns * R);
@@ -320,7 +329,7 @@ __device__ __forceinline__ void stage(c2* lds, const float2* __restrict__ tw, Lo
                             if constexpr (FIRST)
                                 v[b][r] = load(b, r, jj + r * NB);
                             else
-                                v[b][r] = lds[jj + r * NB];
+                                v[b][r] = lds[jj + r * NB + (LAST ? r * PADL : 0)];
                         }
                 }
             else if (NB % NT == 0 || j < NB)
@@ -331,7 +340,7 @@ __device__ __forceinline__ void stage(c2* lds, const float2* __restrict__ tw, Lo
                             if constexpr (FIRST)
                                 v[b][r] = load(b, r, j + r * NB);
                             else
-                                v[b][r] = lds[j + r * NB];
+                                v[b][r] = lds[j + r * NB + (LAST ? r * PADL : 0)];
                         }
                 }
         }
@@ -356,7 +365,7 @@ __device__ __forceinline__ void stage(c2* lds, const float2* __restrict__ tw, Lo
                             constexpr int MODE = TWP == 3 ? (LAST ? 1 : 3) : TWP;
                             if constexpr (MODE == 3)
                                 {
-                                    const c2* lt = lds + N + k * lds_tw_row(R);
+                                    const c2* lt = lds + DATA + k * lds_tw_row(R);
 #pragma unroll
                                     for (int r = 1; r < R; ++r) v[b][r] = mul(v[b][r], lt[r - 1]);
                                 }
@@ -395,7 +404,8 @@ __device__ __forceinline__ void stage(c2* lds, const float2* __restrict__ tw, Lo
                     Dft<R>::run(v[b]);
                     if constexpr (!LAST)
                         {
-                            const int base = (j - k) * R + k;
+                            // block (j - k) R / (Ns R) = j / Ns of the last stage's input
+                            const int base = (j - k) * R + k + (PEN ? (j / Ns) * PADL : 0);
 #pragma unroll
                             for (int r = 0; r < R; ++r) lds[base + r * Ns] = v[b][r];
                         }
@@ -444,7 +454,8 @@ template <int NT, int N, int Ns, int TWP, int TOFF, bool FIRST, bool ORD, int R,
 __device__ __forceinline__ void stages(c2* lds, const float2* __restrict__ tw, Load& load, Store& store, Hook& hook)
 {
     constexpr bool LAST = sizeof...(Rest) == 0;
-    stage<R, NT, N, Ns, TWP, TOFF, FIRST, LAST, ORD>(lds, tw, load, store, hook);
+    constexpr bool PEN = sizeof...(Rest) == 1;
+    stage<R, NT, N, Ns, TWP, TOFF, FIRST, LAST, PEN, ORD>(lds, tw, load, store, hook);
     constexpr int NEXT = FIRST ? TOFF : TOFF + Ns * stage_tw_row(R);
     if constexpr (!LAST) stages<NT, N, Ns * R, TWP, NEXT, false, ORD, Rest...>(lds, tw, load, store, hook);
 }
@@ -460,7 +471,8 @@ template <int NT_, int TWP_, int... Rs>
 struct PkPlan
 {
     static constexpr int NT = NT_;
-    static constexpr int TWP = TWP_;
+    static constexpr int TWP = TWP_ & 15;   // TWP_ >> 4: PADL (stage())
+    static constexpr int PADL = TWP_ >> 4;
     // entries of the twiddle table the kernels read: W_N (N) + the per-stage table
     static constexpr size_t tw_entries() { return (size_t)N + (TWP >= 2 ? stage_tw_entries<Rs...>() : 0); }
     // host: fill tw[N ..) with the per-stage table (tw[0, N) = W_N^m is the caller's)
@@ -474,7 +486,8 @@ struct PkPlan
     static_assert(TWP != 3 || sizeof...(Rs) == 3, "TWP 3: one middle stage");
     // TWP 3: the middle stage's table (R1 rows of its R2 - 1 roots) after the data
     static constexpr int LTW = TWP == 3 ? R1 * lds_tw_row(R2) : 0;
-    static constexpr size_t lds_bytes() { return (size_t)(N + LTW) * sizeof(c2); }
+    static constexpr int DATA = N + ((0, ..., Rs) - 1) * PADL;  // N + (RL - 1) PADL
+    static constexpr size_t lds_bytes() { return (size_t)(DATA + LTW) * sizeof(c2); }
     // last stage: radix, butterflies per thread, output stride; store(i, v, slot)
     // receives slot = r*BPTL + b in [0, RL*BPTL), this lane's output order
     static constexpr int RL = (0, ..., Rs);
@@ -498,10 +511,10 @@ struct PkPlan
                 for (int i = (int)threadIdx.x; i < R1 * RW; i += NT)
                     {
                         const int row = i / RW, q = i - row * RW;
-                        lds[N + row * lds_tw_row(R2) + q] = from(tw[N + i]);
+                        lds[DATA + row * lds_tw_row(R2) + q] = from(tw[N + i]);
                     }
             }
-        stages<NT, N, 1, TWP, N, true, ORD, Rs...>(lds, tw, load, store, hook);
+        stages<NT, N, 1, TWP_, N, true, ORD, Rs...>(lds, tw, load, store, hook);
     }
 };
 

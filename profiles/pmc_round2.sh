@@ -23,7 +23,7 @@ run() {
 run fetch FETCH_SIZE &&
 run write WRITE_SIZE &&
 run sqa SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES &&
-run sqb SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE &&
+run sqb SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE &&
 run l2 TCC_HIT_sum TCC_MISS_sum &&
 python3 profiles/pmc_summary.py --json "$OUT" > "$OUT/pmc.json" && cat "$OUT/pmc.json"
 echo "pmc exit $?"

@@ -213,6 +213,28 @@ def cpu_baseline(iq, codes, sats, budget_s=12.0):
                         "187 (BASELINE.md §2): %.2fx" % (corr_rate, corr_rate / 187.0)}
 
 
+def achievable_hbm_gbps(torch, dev, mib=1024):
+    """Achievable HBM bandwidth on this box ('also measure achievable BW
+    with a copy kernel'): device-to-device copy of a `mib` MiB buffer, read + write
+    bytes over the HIP-event time of the copy (median of 5)."""
+    n = mib * (1 << 20) // 4
+    a = torch.empty(n, dtype=torch.float32, device=dev)
+    b = torch.empty_like(a)
+    a.fill_(1.0)
+    b.copy_(a)
+    ts = []
+    for _ in range(5):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        b.copy_(a)
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1) / 1e3)
+    del a, b
+    return 2.0 * n * 4 / sorted(ts)[2] / 1e9
+
+
 def load_pmc_traffic():
     """HBM bytes per launch of the dominant kernel, from the committed rocprofv3 PMC
     summary (profiles/pmc_*.json, written by profiles/collect_pmc.py), if present."""
@@ -446,11 +468,12 @@ def main():
         if pmc and pmc.get("kernel") == "acq_correlate_kernel" and pmc.get("blocks") and pmc.get("hbm_bytes_per_launch"):
             # PMC HBM bytes of one launch over pmc["blocks"] blocks, per block x this launch's blocks
             traffic = pmc.get("hbm_bytes_per_launch") / pmc["blocks"] * blocks_per_launch
-        # The correlate kernel is VALU-issue bound, not HBM bound: its spectra are
-        # read from HBM once and re-served from L2 to the 32 PRN workgroups (PMC
-        # traffic below), and the packed-f32 FFT's issue slots set its time
-        # (DESIGN.md §5).  The roofline is therefore the FP32 vector peak, with the
-        # nominal FFT flops; the logical-byte HBM figure is kept alongside.
+        # The correlate kernel is not HBM bound: its spectra come from HBM once and
+        # are re-served from L2 / the Infinity Cache to the 32 PRN workgroups (PMC
+        # traffic below); its time is VALU issue (packed-f32 butterflies) plus the
+        # LDS round trips and barriers between stages.  The roofline
+        # is therefore the FP32 vector peak with the nominal FFT flops; the
+        # logical-byte HBM figure and this box's achievable copy rate are kept alongside.
         flops = correlate_kernel_flops_per_block() * blocks_per_launch * nch / corr_launch_s
         line["roofline"] = {
             "bound": "valu", "achieved": round(flops / 1e12, 2), "peak": FP32_PEAK / 1e12, "unit": "TFLOP/s",
@@ -459,6 +482,7 @@ def main():
             "blocks_per_launch": blocks_per_launch, "concurrent_launches": nch,
             "nominal_flops_per_launch": int(correlate_kernel_flops_per_block() * blocks_per_launch),
             "hbm_logical": {"achieved": round(achieved / 1e9, 2), "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                            "achievable_copy": round(achievable_hbm_gbps(torch, dev), 1),
                             "frac": round(achieved / HBM_PEAK, 4),
                             "algorithmic_bytes_per_launch": int(correlate_kernel_bytes_per_block() * blocks_per_launch)},
         }

@@ -580,6 +580,19 @@ int gsdr_acq_set_profiling(gsdr_acq* a, int enable)
     GSDR_REQUIRE(a, GSDR_E_ARG, "gsdr_acq_set_profiling: null handle");
     std::lock_guard<std::mutex> lk(a->mu);
     a->profiling = enable != 0;
+    if (a->profiling)
+        {
+            // pre-create the stage events, so a profiled run records pooled events
+            // instead of calling hipEventCreate inside the caller's timed loop (8 per
+            // call: four stages bracketed; read_profile returns them to the pool)
+            gsdr::DeviceGuard g(a->device);
+            while (a->prof_pool.size() + 2 * a->prof_recs.size() < 1024)
+                {
+                    hipEvent_t e = nullptr;
+                    if (hipEventCreate(&e) != hipSuccess) break;
+                    a->prof_pool.push_back(e);
+                }
+        }
     return GSDR_OK;
 }
 

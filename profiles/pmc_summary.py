@@ -18,9 +18,17 @@ import sys
 from collections import defaultdict
 
 
-def summarise(root, match):
+def summarise(root, match, passes=None):
+    """passes: which pass directories to read -- "acq" (the C2 acquisition driver:
+    directories without a trk_/c3_ prefix), "trk", "c3", or None for all.  The C3
+    pass also runs an acquisition (N = 16000), whose correlate kernel must not be
+    averaged into the C2 one's counters."""
     vals = defaultdict(list)
     for f in sorted(glob.glob(os.path.join(root, "*", "**", "*counter_collection.csv"), recursive=True)):
+        top = os.path.relpath(f, root).split(os.sep)[0]
+        kind = "trk" if top.startswith("trk_") else ("c3" if top.startswith("c3_") else "acq")
+        if passes is not None and kind != passes:
+            continue
         per = defaultdict(float)
         for r in csv.DictReader(open(f)):
             if match not in r["Kernel_Name"]:
@@ -31,16 +39,17 @@ def summarise(root, match):
     return {c: sum(v) / len(v) for c, v in vals.items()}
 
 
-KERNELS = {"acq_correlate_kernel": "acq_correlate", "acq_forward_kernel": "acq_forward",
-           "acq_argmax_pk_kernel": "acq_argmax", "trk_kernel": "trk_kernel", "corr_kernel": "corr_kernel"}
+KERNELS = {"acq_correlate_kernel": ("acq_correlate", "acq"), "acq_forward_kernel": ("acq_forward", "acq"),
+           "acq_argmax_pk_kernel": ("acq_argmax", "acq"), "trk_kernel": ("trk_kernel", "trk"),
+           "corr_kernel": ("corr_kernel", "c3")}
 
 
 def as_json(root):
     out = {"source": "rocprofv3 --kernel-trace --pmc: profiles/acq_driver.py --what acq / --what trk (C2, 64 "
                      "blocks: acquisition; 8-channel tracking over 64 ms) and profiles/configs_bench.py --only C3 (corr_kernel)",
            "blocks": 64, "kernels": {}}
-    for name, match in KERNELS.items():
-        s = summarise(root, match)
+    for name, (match, passes) in KERNELS.items():
+        s = summarise(root, match, passes)
         if not s:
             continue
         k = {"counters": {c: round(v, 1) for c, v in sorted(s.items())}}

@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--blocks", type=int, default=16)
     ap.add_argument("--variants", default="60,63")
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--prns", type=int, default=32)
     a = ap.parse_args()
     import torch
     import gsdr
@@ -31,16 +32,17 @@ def main():
     N = fs // 1000
     sats = synth.random_constellation(8, seed_offset=3, prns=list(range(1, 9)))
     iq = synth.gps_l1_iq(fs, B * N, sats, seed_offset=3)
-    codes = np.stack([synth.gps_ca_sampled(p, fs) for p in range(1, 33)])
+    NP = a.prns
+    codes = np.stack([synth.gps_ca_sampled(p, fs) for p in range(1, NP + 1)])
     dev = torch.device("cuda", 0)
     iq_dev = torch.from_numpy(iq.view(np.float32).copy()).to(dev)
     sptr = torch.cuda.current_stream(dev).cuda_stream
     ref = None
     for v in [int(x) for x in a.variants.split(",")]:
         os.environ["GSDR_ACQ_CORR_VARIANT"] = str(v)
-        acq = gsdr.Acquisition(fs, N, 10000, 250, pfa=0.01, max_prns=32, max_blocks=B, num_doppler_bins=81)
-        acq.set_local_codes(codes, np.arange(1, 33))
-        res_dev = torch.zeros(B * 32 * gsdr.ACQ_RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+        acq = gsdr.Acquisition(fs, N, 10000, 250, pfa=0.01, max_prns=NP, max_blocks=B, num_doppler_bins=81)
+        acq.set_local_codes(codes, np.arange(1, NP + 1))
+        res_dev = torch.zeros(B * NP * gsdr.ACQ_RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
         for _ in range(5):
             acq.run_device(iq_dev.data_ptr(), B, N, 0, res_dev.data_ptr(), sptr)
         torch.cuda.synchronize()
@@ -59,7 +61,7 @@ def main():
         t1.record()
         torch.cuda.synchronize()
         wall = t0.elapsed_time(t1) / a.reps
-        res = res_dev.cpu().numpy().view(gsdr.ACQ_RESULT_DTYPE).reshape(B, 32)
+        res = res_dev.cpu().numpy().view(gsdr.ACQ_RESULT_DTYPE).reshape(B, NP)
         if ref is None:
             ref = res
         same = float(np.mean((res["doppler_index"] == ref["doppler_index"]) & (res["code_phase"] == ref["code_phase"])))

@@ -1470,7 +1470,10 @@ size_t item_bytes(int it) { return it == GSDR_ITEM_CSHORT ? 4 : (it == GSDR_ITEM
     X(79, (gsdr::pk::PkPlan<256, 3, 25, 16, 10>), 1, 1, 2)              \
     X(80, (gsdr::pk::PkPlan<256, 3, 20, 20, 10>), 1, 1, 2)              \
     X(81, (gsdr::pk::PkPlan<256, 1 | (9 << 4), 25, 16, 10>), 1, 1, 2)   \
-    X(82, (gsdr::pk::PkPlan<256, 3 | (9 << 4), 25, 16, 10>), 1, 1, 2)
+    X(82, (gsdr::pk::PkPlan<256, 3 | (9 << 4), 25, 16, 10>), 1, 1, 2)   \
+    X(83, (gsdr::pk::PkPlan<256, 1 | 256, 25, 16, 10>), 1, 1, 2)        \
+    X(84, (gsdr::pk::PkPlan<256, 1 | (9 << 4) | 256, 25, 16, 10>), 1, 1, 2) \
+    X(85, (gsdr::pk::PkPlan<1024, 1 | 256, 16, 10, 10, 10>), 1, 1, 2)
 
 template <class PT>
 int set_lds_attrs(size_t bytes)

@@ -304,7 +304,14 @@ template <int R, int NT, int N, int Ns, int TWP_, int TOFF, bool FIRST, bool LAS
 __device__ __forceinline__ void stage(c2* lds, const float2* __restrict__ tw, Load& load, Store& store, Hook& hook)
 {
     constexpr int TWP = TWP_ & 15;
-    constexpr int PADL = TWP_ >> 4;
+    constexpr int PADL = (TWP_ >> 4) & 15;
+    // LATE (TWP_ bit 8): the barrier that keeps the in-place Stockham exchange
+    // safe (every wave's reads done before any wave's writes) moves from between
+    // this stage's LDS reads and its butterflies to between the butterflies and its
+    // writes, so the read latency overlaps the twiddles and the DFT; the last
+    // stage needs none (its caller separates the next LDS writes with a barrier)
+    constexpr bool LATE = ((TWP_ >> 8) & 1) != 0;
+    constexpr bool DEFER = LATE && !FIRST && !LAST;
     // elements before the TWP 3 table: N plus the last-stage pads (this stage is
     // the penultimate one whenever it reads the table)
     constexpr int DATA = N + (N / (Ns * R) - 1) * PADL;
@@ -346,12 +353,14 @@ __device__ __forceinline__ void stage(c2* lds, const float2* __restrict__ tw, Lo
         }
     if constexpr (FIRST)
         hook();
-    else
+    else if constexpr (!LATE)
         __syncthreads();
+    int kk[BPT];
 #pragma unroll
     for (int b = 0; b < BPT; ++b)
         {
             const int j = (int)threadIdx.x + b * NT;
+            kk[b] = 0;
             if (NB % NT == 0 || j < NB)
                 {
                     int k = 0;
@@ -402,9 +411,26 @@ __device__ __forceinline__ void stage(c2* lds, const float2* __restrict__ tw, Lo
                                 }
                         }
                     Dft<R>::run(v[b]);
-                    if constexpr (!LAST)
+                    kk[b] = k;
+                    if constexpr (!LAST && !DEFER)
                         {
                             // block (j - k) R / (Ns R) = j / Ns of the last stage's input
+                            const int base = (j - k) * R + k + (PEN ? (j / Ns) * PADL : 0);
+#pragma unroll
+                            for (int r = 0; r < R; ++r) lds[base + r * Ns] = v[b][r];
+                        }
+                }
+        }
+    if constexpr (DEFER)
+        {
+            __syncthreads();
+#pragma unroll
+            for (int b = 0; b < BPT; ++b)
+                {
+                    const int j = (int)threadIdx.x + b * NT;
+                    if (NB % NT == 0 || j < NB)
+                        {
+                            const int k = kk[b];
                             const int base = (j - k) * R + k + (PEN ? (j / Ns) * PADL : 0);
 #pragma unroll
                             for (int r = 0; r < R; ++r) lds[base + r * Ns] = v[b][r];
@@ -472,7 +498,7 @@ struct PkPlan
 {
     static constexpr int NT = NT_;
     static constexpr int TWP = TWP_ & 15;   // TWP_ >> 4: PADL (stage())
-    static constexpr int PADL = TWP_ >> 4;
+    static constexpr int PADL = (TWP_ >> 4) & 15;
     // entries of the twiddle table the kernels read: W_N (N) + the per-stage table
     static constexpr size_t tw_entries() { return (size_t)N + (TWP >= 2 ? stage_tw_entries<Rs...>() : 0); }
     // host: fill tw[N ..) with the per-stage table (tw[0, N) = W_N^m is the caller's)

@@ -1429,10 +1429,14 @@ size_t item_bytes(int it) { return it == GSDR_ITEM_CSHORT ? 4 : (it == GSDR_ITEM
 // Correlate-kernel variants for N = 4000 (env GSDR_ACQ_CORR_VARIANT selects one;
 // 0 = the single-transform kernel of the plan variant).
 // Packed-f32 correlate (and forward) variants: (id, plan, PRNs per workgroup,
-// waves-per-EU hint).  30-39, 70-78 are N = 4000 plans (70 the default); 60-69 the
+// waves-per-EU hint).  30-39, 70-85 are N = 4000 plans (70 the default); 60-69 the
 // other compile-time sizes (1 ms at 16 / 8 / 2 Msps); 90-92 run the correlate on
 // the register four-step (acq_correlate_reg_kernel, N = 16000, 90 the default) and
-// the forward / argmax passes on the listed plan.
+// the forward / argmax passes on the listed plan.  The plan's second argument packs
+// the twiddle mode (bits 0-3, fft_pk.h TWP), the last-stage block pad PADL (bits
+// 4-7) and the LATE barrier flag (bit 8).  The non-default ids are the measured
+// alternatives DESIGN.md 5 / 10 reports (all within noise of or slower than the
+// defaults); every one is in tests/test_gpu_acq.py's parity list.
 // Columns: (id, plan, PRNs per workgroup, waves-per-EU hint, row statistic: 0 max +
 // first argmax in the kernel, 1 max + sum with the argmax recomputed for the
 // selected row, see acq_correlate_pk_kernel).

@@ -517,6 +517,42 @@ def main():
                      "trk_calls_per_channel_timed": trk_calls_timed,
                      "median_mean16_doppler_err_hz": None if dop_err is None else round(float(np.median(dop_err)), 2),
                      "channels_within_25hz": None if dop_err is None else int(np.sum(dop_err < 25.0))}
+    # Acquisition-only and tracking-only rates, each timed over K steps
+    # after the headline's timed region with the same handles: the acquisition
+    # chains without the tracking launch, and the tracking launch alone (restarted
+    # from the saved start state, K steps of the continuous stream).
+    if args.only is None and do_trk and args.trk_stream:
+        if not args.no_profile_events:
+            for a in acqs:
+                a.set_profiling(False)
+            trk.set_profiling(False)
+
+        def timed_part(fn):
+            torch.cuda.synchronize(dev)
+            t = time.perf_counter()
+            fn()
+            torch.cuda.synchronize(dev)
+            return time.perf_counter() - t
+
+        def acq_only():
+            for _ in range(K):
+                for i, a in enumerate(acqs):
+                    b0 = lo + i * Bc
+                    a.run_device(iq_dev.data_ptr() + b0 * N * 8, Bc, N, b0 * N,
+                                 res_dev.data_ptr() + i * Bc * P * gsdr.ACQ_RESULT_DTYPE.itemsize)
+
+        def trk_only():
+            trk.restore_state(0)
+            trk.run_device(iq_long.data_ptr(), 0, (W + K + 1) * total * N, K * total, trk_out.data_ptr(),
+                           trk_n.data_ptr())
+        ta = timed_part(acq_only)
+        tt = timed_part(trk_only)
+        line["components"] = {
+            "acq_only_msps": round(B * N * K / ta / 1e6, 2),
+            "trk_only_msps": round(total * N * K / tt / 1e6, 2),
+            "trk_only_channels": nloc,
+            "note": "each over K steps after the timed region; trk_only = the stream's IQ rate through the tracking "
+                    "pool (every channel processes every sample)"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(iq, codes, sats)
     if rank == 0:

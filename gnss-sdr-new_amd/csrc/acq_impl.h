@@ -35,7 +35,7 @@ inline int default_pk_variant(uint32_t N)
     switch (N)
         {
         case 4000: return kDefaultCorrVariant4000;
-        case 16000: return 90;
+        case 16000: return 93;
         case 8000: return 61;
         case 2000: return 62;
         default: return 0;
@@ -630,10 +630,13 @@ struct Pads1000x10
         std::conditional_t<I == 2, RowPad<1000, 50, 3>, RowPad<1000, 0, 0>>>;
 };
 
+// WPE_ packs the waves-per-EU hint (bits 0-3) and PGS (bits 4+): with PGS > 0 an
+// XCD walks its rows PRN-group-major (groups of PGS PRNs, PGS | P), so its L2 holds
+// PGS code spectra (PGS x 128 KB at N = 16000) instead of cycling through all P.
 template <int R_, int NT_, int H_, int WPE_, class Pads_, int... Rs>
 struct RegFourStep
 {
-    static constexpr int R = R_, NT = NT_, H = H_, WPE = WPE_;
+    static constexpr int R = R_, NT = NT_, H = H_, WPE = WPE_ & 15, PGS = WPE_ >> 4;
     static constexpr int L = (Rs * ...);
     static constexpr int N = R * L;
     static constexpr int CPL = (L + NT - 1) / NT;
@@ -677,8 +680,19 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(RP:
     if (id < full * 8u * P)
         {
             const uint32_t xcd = id & 7u, slot = id >> 3;
-            row = (slot / P) * 8u + xcd;
-            p = slot - (slot / P) * P;
+            if (RP::PGS > 0 && P % (uint32_t)RP::PGS == 0)
+                {
+                    const uint32_t per_group = full * (uint32_t)RP::PGS;
+                    const uint32_t pg = slot / per_group, rem = slot - pg * per_group;
+                    const uint32_t ri = rem / (uint32_t)RP::PGS;
+                    row = ri * 8u + xcd;
+                    p = pg * (uint32_t)RP::PGS + (rem - ri * (uint32_t)RP::PGS);
+                }
+            else
+                {
+                    row = (slot / P) * 8u + xcd;
+                    p = slot - (slot / P) * P;
+                }
         }
     else
         {
@@ -1431,7 +1445,8 @@ size_t item_bytes(int it) { return it == GSDR_ITEM_CSHORT ? 4 : (it == GSDR_ITEM
 // Packed-f32 correlate (and forward) variants: (id, plan, PRNs per workgroup,
 // waves-per-EU hint).  30-39, 70-85 are N = 4000 plans (70 the default); 60-69 the
 // other compile-time sizes (1 ms at 16 / 8 / 2 Msps); 90-92 run the correlate on
-// the register four-step (acq_correlate_reg_kernel, N = 16000, 90 the default) and
+// the register four-step (acq_correlate_reg_kernel, N = 16000; 93 the default: 90
+// with the PRN-group-major XCD walk, 16 code spectra per L2) and
 // the forward / argmax passes on the listed plan.  The plan's second argument packs
 // the twiddle mode (bits 0-3, fft_pk.h TWP), the last-stage block pad PADL (bits
 // 4-7) and the LATE barrier flag (bit 8).  The non-default ids are the measured
@@ -1462,6 +1477,8 @@ size_t item_bytes(int it) { return it == GSDR_ITEM_CSHORT ? 4 : (it == GSDR_ITEM
     X(90, (gsdr::pk::PkPlan<1024, 1, 16, 10, 10, 10>), 1, 1, 2)         \
     X(91, (gsdr::pk::PkPlan<1024, 1, 16, 10, 10, 10>), 1, 1, 2)         \
     X(92, (gsdr::pk::PkPlan<1024, 1, 16, 10, 10, 10>), 1, 1, 2)         \
+    X(93, (gsdr::pk::PkPlan<1024, 1, 16, 10, 10, 10>), 1, 1, 2)         \
+    X(94, (gsdr::pk::PkPlan<1024, 1, 16, 10, 10, 10>), 1, 1, 2)         \
     X(70, (gsdr::pk::PkPlan<256, 1, 25, 16, 10>), 1, 1, 2)              \
     X(71, (gsdr::pk::PkPlan<256, 2, 25, 16, 10>), 1, 1, 1)              \
     X(72, (gsdr::pk::PkPlan<256, 2, 25, 16, 10>), 1, 1, 2)              \

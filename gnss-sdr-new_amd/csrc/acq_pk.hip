@@ -11,6 +11,8 @@ namespace gsdr_acq_impl
 using RegPlan90 = RegFourStep<16, 512, 8, 1, NoPads<1000>, 10, 10, 10>;
 using RegPlan91 = RegFourStep<16, 512, 8, 1, Pads1000x10, 10, 10, 10>;
 using RegPlan92 = RegFourStep<16, 512, 4, 1, Pads1000x10, 10, 10, 10>;
+using RegPlan93 = RegFourStep<16, 512, 8, 1 | (16 << 4), NoPads<1000>, 10, 10, 10>;
+using RegPlan94 = RegFourStep<16, 512, 8, 1 | (8 << 4), NoPads<1000>, 10, 10, 10>;
 
 template <class RP>
 int launch_reg(gsdr_acq* a, uint32_t nblocks, hipStream_t s)
@@ -35,6 +37,8 @@ int launch_corr_variant(gsdr_acq* a, uint32_t nblocks, hipStream_t s)
         case 90: return launch_reg<RegPlan90>(a, nblocks, s);
         case 91: return launch_reg<RegPlan91>(a, nblocks, s);
         case 92: return launch_reg<RegPlan92>(a, nblocks, s);
+        case 93: return launch_reg<RegPlan93>(a, nblocks, s);
+        case 94: return launch_reg<RegPlan94>(a, nblocks, s);
         default: break;
         }
 #define GSDR_PK_CASE(ID, MP, PG, WPE, ST)                                                                       \
@@ -136,6 +140,8 @@ int setup_corr_variant(gsdr_acq* a, int v)
             if (ID == 90 && setup_reg<RegPlan90>() != GSDR_OK) return GSDR_E_DEVICE;                           \
             if (ID == 91 && setup_reg<RegPlan91>() != GSDR_OK) return GSDR_E_DEVICE;                           \
             if (ID == 92 && setup_reg<RegPlan92>() != GSDR_OK) return GSDR_E_DEVICE;                           \
+            if (ID == 93 && setup_reg<RegPlan93>() != GSDR_OK) return GSDR_E_DEVICE;                           \
+            if (ID == 94 && setup_reg<RegPlan94>() != GSDR_OK) return GSDR_E_DEVICE;                           \
             a->corr_variant = ID;                                                                               \
             a->corr_stat = ST;                                                                                  \
             a->tw_entries = M::tw_entries();                                                                    \

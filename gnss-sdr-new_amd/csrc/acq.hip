@@ -403,17 +403,22 @@ int gsdr_acq_run_stream(gsdr_acq* a, gsdr_stream* ring, uint64_t first_sample, u
     GSDR_REQUIRE(gsdr::stream_item_type(ring) == a->conf.item_type, GSDR_E_ARG,
         "gsdr_acq_run_stream: ring item type %d != acquisition item type %d", gsdr::stream_item_type(ring),
         a->conf.item_type);
+    GSDR_REQUIRE(gsdr::stream_device(ring) == a->device, GSDR_E_ARG,
+        "gsdr_acq_run_stream: ring on device %d, acquisition handle on device %d", gsdr::stream_device(ring), a->device);
     std::lock_guard<std::mutex> lk(a->mu);
     gsdr::DeviceGuard g(a->device);
-    const void* iq = nullptr;
-    int rc = gsdr::stream_view(ring, first_sample, (uint64_t)nblocks * a->K * a->consumed, &iq);
-    if (rc != GSDR_OK) return rc;
-    rc = gsdr::stream_acquire(ring, a->stream);
-    if (rc != GSDR_OK) return rc;
-    rc = dispatch(a, 0, iq, nblocks, a->consumed, stamp0, a->d_res, a->stream, 0);
-    if (rc != GSDR_OK) return rc;
-    rc = gsdr::stream_release(ring, a->stream);
-    if (rc != GSDR_OK) return rc;
+    {
+        gsdr::StreamReader rd(ring);  // ring lock from view to reader-event record
+        const void* iq = nullptr;
+        int rc = rd.view(first_sample, (uint64_t)nblocks * a->K * a->consumed, &iq);
+        if (rc != GSDR_OK) return rc;
+        rc = rd.acquire(a->stream);
+        if (rc != GSDR_OK) return rc;
+        rc = dispatch(a, 0, iq, nblocks, a->consumed, stamp0, a->d_res, a->stream, 0);
+        if (rc != GSDR_OK) return rc;
+        rc = rd.release(a->stream);
+        if (rc != GSDR_OK) return rc;
+    }
     GSDR_HIP(hipMemcpyAsync(out, a->d_res, (size_t)nblocks * a->nprn * sizeof(gsdr_acq_result), hipMemcpyDeviceToHost,
         a->stream));
     GSDR_HIP(hipStreamSynchronize(a->stream));

@@ -40,12 +40,17 @@ struct gsdr_stream
 namespace gsdr
 {
 int stream_item_type(const gsdr_stream* s) { return s->item_type; }
+int stream_device(const gsdr_stream* s) { return s->device; }
 
-int stream_view(gsdr_stream* s, uint64_t first, uint64_t n, const void** ptr)
+namespace
 {
-    std::lock_guard<std::mutex> lk(s->mu);
+uint64_t oldest_of(const gsdr_stream* s) { return s->head > s->cap ? std::max(s->base, s->head - s->cap) : s->base; }
+
+// (ring lock held)
+int view_locked(gsdr_stream* s, uint64_t first, uint64_t n, const void** ptr)
+{
     GSDR_REQUIRE(s->started, GSDR_E_STATE, "gsdr_stream: nothing pushed yet");
-    const uint64_t oldest = s->head > s->cap ? std::max(s->base, s->head - s->cap) : s->base;
+    const uint64_t oldest = oldest_of(s);
     GSDR_REQUIRE(first >= oldest && first + n <= s->head, GSDR_E_ARG,
         "gsdr_stream: window [%llu, %llu) outside the ring's [%llu, %llu)", (unsigned long long)first,
         (unsigned long long)(first + n), (unsigned long long)oldest, (unsigned long long)s->head);
@@ -55,32 +60,35 @@ int stream_view(gsdr_stream* s, uint64_t first, uint64_t n, const void** ptr)
     return GSDR_OK;
 }
 
-int stream_span(gsdr_stream* s, uint64_t* first, uint64_t* n)
+int span_locked(gsdr_stream* s, uint64_t* first, uint64_t* n)
 {
-    std::lock_guard<std::mutex> lk(s->mu);
     GSDR_REQUIRE(s->started, GSDR_E_STATE, "gsdr_stream: nothing pushed yet");
-    const uint64_t oldest = s->head > s->cap ? std::max(s->base, s->head - s->cap) : s->base;
+    const uint64_t oldest = oldest_of(s);
     const uint64_t lo = s->head > s->window ? std::max(oldest, s->head - s->window) : oldest;
     *first = lo;
     *n = s->head - lo;
     return GSDR_OK;
 }
 
-int stream_acquire(gsdr_stream* s, hipStream_t consumer)
+int release_locked(gsdr_stream* s, hipStream_t consumer)
 {
-    GSDR_HIP(hipStreamWaitEvent(consumer, s->pushed, 0));
-    return GSDR_OK;
-}
-
-int stream_release(gsdr_stream* s, hipStream_t consumer)
-{
-    std::lock_guard<std::mutex> lk(s->mu);
-    // one reader event suffices: consumers of one ring are ordered by the caller
-    // (a later launch on another stream makes this event wait for the earlier one)
+    // one reader event suffices: the consumer first waits for the previous reader,
+    // so the event recorded here completes only after every earlier read
     GSDR_HIP(hipStreamWaitEvent(consumer, s->read, 0));
     GSDR_HIP(hipEventRecord(s->read, consumer));
     return GSDR_OK;
 }
+}  // namespace
+
+StreamReader::StreamReader(gsdr_stream* s) : s_(s), lk_(s->mu) {}
+int StreamReader::view(uint64_t first, uint64_t n, const void** ptr) { return view_locked(s_, first, n, ptr); }
+int StreamReader::span(uint64_t* first, uint64_t* n) { return span_locked(s_, first, n); }
+int StreamReader::acquire(hipStream_t consumer)
+{
+    GSDR_HIP(hipStreamWaitEvent(consumer, s_->pushed, 0));
+    return GSDR_OK;
+}
+int StreamReader::release(hipStream_t consumer) { return release_locked(s_, consumer); }
 }  // namespace gsdr
 
 namespace
@@ -179,16 +187,45 @@ int gsdr_stream_push(gsdr_stream* s, const void* iq_host, uint64_t first_sample,
 int gsdr_stream_span(gsdr_stream* s, uint64_t* first_sample, uint64_t* n_items)
 {
     GSDR_REQUIRE(s && first_sample && n_items, GSDR_E_ARG, "gsdr_stream_span: null argument");
-    return gsdr::stream_span(s, first_sample, n_items);
+    std::lock_guard<std::mutex> lk(s->mu);
+    return gsdr::span_locked(s, first_sample, n_items);
 }
 
 int gsdr_stream_window(gsdr_stream* s, uint64_t first_sample, uint64_t n_items, const void** iq_dev)
 {
     GSDR_REQUIRE(s && iq_dev, GSDR_E_ARG, "gsdr_stream_window: null argument");
-    int rc = gsdr::stream_view(s, first_sample, n_items, iq_dev);
+    std::lock_guard<std::mutex> lk(s->mu);
+    int rc = gsdr::view_locked(s, first_sample, n_items, iq_dev);
     if (rc != GSDR_OK) return rc;
     gsdr::DeviceGuard g(s->device);
     GSDR_HIP(hipEventSynchronize(s->pushed));
+    return GSDR_OK;
+}
+
+int gsdr_stream_window_async(gsdr_stream* s, uint64_t first_sample, uint64_t n_items, void* consumer_stream,
+    const void** iq_dev)
+{
+    GSDR_REQUIRE(s && consumer_stream && iq_dev, GSDR_E_ARG, "gsdr_stream_window_async: null argument");
+    std::lock_guard<std::mutex> lk(s->mu);
+    int rc = gsdr::view_locked(s, first_sample, n_items, iq_dev);
+    if (rc != GSDR_OK) return rc;
+    gsdr::DeviceGuard g(s->device);
+    GSDR_HIP(hipStreamWaitEvent((hipStream_t)consumer_stream, s->pushed, 0));
+    return GSDR_OK;
+}
+
+int gsdr_stream_release(gsdr_stream* s, void* consumer_stream)
+{
+    GSDR_REQUIRE(s && consumer_stream, GSDR_E_ARG, "gsdr_stream_release: null argument");
+    std::lock_guard<std::mutex> lk(s->mu);
+    gsdr::DeviceGuard g(s->device);
+    return gsdr::release_locked(s, (hipStream_t)consumer_stream);
+}
+
+int gsdr_stream_device(const gsdr_stream* s, int* device)
+{
+    GSDR_REQUIRE(s && device, GSDR_E_ARG, "gsdr_stream_device: null argument");
+    *device = s->device;
     return GSDR_OK;
 }
 

@@ -878,7 +878,8 @@ typedef __attribute__((address_space(3))) void gsdr_lvoid;
 // 16-byte block holding `first` (returned); every lane's source is clamped to a
 // 16-byte block holding at least one byte of the stream, i.e. inside the
 // stream's own pages.  Waves [w0, kTrkThreads/64) issue; the buffer is valid
-// after the issuing waves' vmcnt drains (any __syncthreads).
+// after the issuing waves' vmcnt drains: each issuing wave runs s_waitcnt
+// vmcnt(0) before the barrier that hands the buffer over (correlate_call_stream).
 __device__ __forceinline__ uintptr_t stream_fetch(const void* iq, uint64_t iq_bytes, int64_t first, int nbytes,
     char* lds, int w0)
 {
@@ -1077,6 +1078,11 @@ __device__ __forceinline__ void correlate_call_stream(const void* __restrict__ i
     const int nch = (vl + chunk - 1) / chunk;
     for (int j = 0; j < nch; ++j)
         {
+            // a workgroup barrier waits only on lgkmcnt and LDS DMA is tracked per
+            // wave in vmcnt: every issuing wave drains its own DMA (chunk j, and for
+            // j == 0 the prefetch waves 1.. issued during the previous loop update)
+            // before the barrier hands the buffer to the other waves
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             if (j + 1 < nch)
                 bstart[(j + 1) & 1] =
@@ -1121,6 +1127,7 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
     // in flight (with the state resident for the whole launch the kernel sat at
     // 256 VGPRs and the compiler serialised the sample loads)
     __shared__ TrkHot s_t;
+    __shared__ int s_overrun;  // the channel fell behind the input (one loss-of-lock record)
     const int ch = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const TrkConst& c = consts[ch];
@@ -1133,6 +1140,7 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
             s_t = gc->h;
             s_lf = gc->code_filter;
             s_state = s_t.state;
+            s_overrun = 0;
         }
     if (tid < kMaxCn0) s_pbuf[tid] = gc->prompt_buffer[tid];
     __syncthreads();
@@ -1168,6 +1176,24 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                 {
                     const TrkHot& t = s_t;
                     Prep p{};
+                    if (e == 0 && t.state >= 2 && t.state <= 4 && t.next_sample < iq_first && max_epochs > 0)
+                        {
+                            // the channel's next call starts before the oldest item the
+                            // caller provides (a ring that moved past a stalled channel):
+                            // it can never continue, so report it as a loss of lock
+                            // (event 3, the Channel FSM re-acquires) instead of stalling
+                            gsdr_trk_epoch r{};
+                            r.sample_counter = t.next_sample;
+                            r.state = t.state;
+                            r.flags = GSDR_TRK_F_LOSS_OF_LOCK | GSDR_TRK_F_OVERRUN;
+                            r.carrier_doppler_hz = t.carrier_doppler_hz;
+                            r.code_freq_chips = t.code_freq_chips;
+                            r.cn0_db_hz = t.cn0_db_hz;
+                            out[(size_t)ch * max_epochs] = r;
+                            clear_tracking_vars(s_t);
+                            s_t.state = 0;
+                            s_overrun = 1;
+                        }
                     const int64_t off = (int64_t)(t.next_sample - iq_first);
                     p.go = (e < max_epochs) && t.state >= 2 && t.state <= 4 && t.next_sample >= iq_first &&
                            (uint64_t)off + (uint64_t)vl <= iq_items;
@@ -1425,7 +1451,7 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
         {
             gc->h = s_t;
             gc->code_filter = s_lf;
-            nout[ch] = e;
+            nout[ch] = e + (uint32_t)s_overrun;
         }
     if (tid < kMaxCn0) gc->prompt_buffer[tid] = s_pbuf[tid];
 }
@@ -2129,20 +2155,23 @@ int gsdr_trk_run_stream(gsdr_trk* k, gsdr_stream* ring, uint32_t max_epochs, gsd
     GSDR_REQUIRE(gsdr::stream_item_type(ring) == k->conf.item_type, GSDR_E_ARG,
         "gsdr_trk_run_stream: ring item type %d != tracking item type %d", gsdr::stream_item_type(ring),
         k->conf.item_type);
+    GSDR_REQUIRE(gsdr::stream_device(ring) == k->device, GSDR_E_ARG,
+        "gsdr_trk_run_stream: ring on device %d, tracking handle on device %d", gsdr::stream_device(ring), k->device);
     std::lock_guard<std::mutex> lk(k->mu);
     gsdr::DeviceGuard g(k->device);
     hipStream_t s = stream ? (hipStream_t)stream : k->stream;
+    gsdr::StreamReader rd(ring);  // ring lock from window choice to reader-event record
     uint64_t first = 0, n = 0;
-    int rc = gsdr::stream_span(ring, &first, &n);
+    int rc = rd.span(&first, &n);
     if (rc != GSDR_OK) return rc;
     const void* iq = nullptr;
-    rc = gsdr::stream_view(ring, first, n, &iq);
+    rc = rd.view(first, n, &iq);
     if (rc != GSDR_OK) return rc;
-    rc = gsdr::stream_acquire(ring, s);
+    rc = rd.acquire(s);
     if (rc != GSDR_OK) return rc;
     rc = launch(k, iq, first, n, max_epochs, out_dev, n_out_dev, s);
     if (rc != GSDR_OK) return rc;
-    return gsdr::stream_release(ring, s);
+    return rd.release(s);
 }
 
 int gsdr_trk_run_stream_host(gsdr_trk* k, gsdr_stream* ring, uint32_t max_epochs, gsdr_trk_epoch* out_host,

@@ -42,13 +42,13 @@ EXPORTED = [
     "gsdr_acq_run_dwell", "gsdr_acq_run_stream", "gsdr_trk_run_stream", "gsdr_trk_run_stream_host",
     "gsdr_stream_create", "gsdr_stream_destroy", "gsdr_stream_push", "gsdr_stream_span", "gsdr_stream_window",
     "gsdr_acq_set_step_two", "gsdr_acq_get_step_two_threshold", "gsdr_acq_run_step_two",
-    "gsdr_trk_set_data_code",
+    "gsdr_trk_set_data_code", "gsdr_stream_window_async", "gsdr_stream_release", "gsdr_stream_device",
 ]
 
 SIGNAL_GPS_1C = 0
 SIGNAL_GAL_1B = 1
 SIGNAL_BDS_B1 = 2
-TRK_F_VALID_OUTPUT, TRK_F_LOSS_OF_LOCK, TRK_F_PLL_180, TRK_F_BIT_SYNC = 1, 2, 4, 8
+TRK_F_VALID_OUTPUT, TRK_F_LOSS_OF_LOCK, TRK_F_PLL_180, TRK_F_BIT_SYNC, TRK_F_OVERRUN = 1, 2, 4, 8, 16
 
 # include/gsdr.h gsdr_trk_conf / gsdr_trk_epoch (C layout)
 TRK_CONF_DTYPE = np.dtype([
@@ -219,6 +219,9 @@ def load():
     L.gsdr_stream_push.argtypes = [P, P, U64, U64]
     L.gsdr_stream_span.argtypes = [P, P, P]
     L.gsdr_stream_window.argtypes = [P, U64, U64, P]
+    L.gsdr_stream_window_async.argtypes = [P, U64, U64, P, P]
+    L.gsdr_stream_release.argtypes = [P, P]
+    L.gsdr_stream_device.argtypes = [P, P]
     L.gsdr_acq_run_stream.argtypes = [P, P, U64, U32, U64, P]
     L.gsdr_trk_run_stream.argtypes = [P, P, U32, P, P, P]
     L.gsdr_trk_run_stream_host.argtypes = [P, P, U32, P, P]
@@ -602,6 +605,23 @@ class Stream:
         p = ctypes.c_void_p()
         _check(load().gsdr_stream_window(self._h, int(first_sample), int(n_items), ctypes.byref(p)))
         return p.value
+
+    def window_async(self, first_sample, n_items, consumer_stream):
+        """Window for reads enqueued on consumer_stream (a hipStream_t handle, e.g.
+        torch.cuda.Stream.cuda_stream); call release(consumer_stream) after them."""
+        p = ctypes.c_void_p()
+        _check(load().gsdr_stream_window_async(self._h, int(first_sample), int(n_items),
+                                               ctypes.c_void_p(consumer_stream), ctypes.byref(p)))
+        return p.value
+
+    def release(self, consumer_stream):
+        _check(load().gsdr_stream_release(self._h, ctypes.c_void_p(consumer_stream)))
+
+    @property
+    def device(self):
+        d = ctypes.c_int()
+        _check(load().gsdr_stream_device(self._h, ctypes.byref(d)))
+        return d.value
 
 
 def cu_partition(n_reserved, n_cus=256):

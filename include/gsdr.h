@@ -98,8 +98,22 @@ int gsdr_stream_push(gsdr_stream* stream, const void* iq_host, uint64_t first_sa
 int gsdr_stream_span(gsdr_stream* stream, uint64_t* first_sample, uint64_t* n_items);
 /* Device pointer of items [first_sample, first_sample + n_items) after the pushes
  * so far have landed (synchronises with the copy stream); GSDR_E_ARG if the window
- * is not (or no longer) in the ring. */
+ * is not (or no longer) in the ring.  For host-synchronous readers: the pointer
+ * stays valid until the next push.  A reader whose kernels run on a stream uses
+ * the pair below instead. */
 int gsdr_stream_window(gsdr_stream* stream, uint64_t first_sample, uint64_t n_items, const void** iq_dev);
+/* Asynchronous reader: the same window, with consumer_stream (a hipStream_t)
+ * made to wait for the pushes so far; after enqueuing its reads the caller calls
+ * gsdr_stream_release(stream, consumer_stream), and every later push waits for
+ * those reads before it overwrites ring positions.  With pushes from another
+ * thread, the caller keeps the two calls and its launches between them free of
+ * any wait on that thread.  The library's own consumers (gsdr_acq_run_stream,
+ * gsdr_trk_run_stream) hold the ring lock from window to release. */
+int gsdr_stream_window_async(gsdr_stream* stream, uint64_t first_sample, uint64_t n_items, void* consumer_stream,
+    const void** iq_dev);
+int gsdr_stream_release(gsdr_stream* stream, void* consumer_stream);
+/* The device the ring lives on (a consumer handle must be on the same device). */
+int gsdr_stream_device(const gsdr_stream* stream, int* device);
 
 /* ======================================================================== */
 /* Acquisition — PCPS (pcps_acquisition)                                     */
@@ -409,6 +423,9 @@ typedef struct gsdr_trk_epoch
 #define GSDR_TRK_F_LOSS_OF_LOCK 2 /* event 3 (loss of lock), channel back to state 0 */
 #define GSDR_TRK_F_PLL_180 4      /* Flag_PLL_180_deg_phase_locked */
 #define GSDR_TRK_F_BIT_SYNC 8     /* preamble / bit synchronisation locked in this call (2 -> 4) */
+#define GSDR_TRK_F_OVERRUN 16     /* with LOSS_OF_LOCK: the channel's next call starts before the oldest
+                                     input item given (the ring moved past a stalled channel); the
+                                     record carries the channel's position, the channel is in state 0 */
 
 void gsdr_trk_conf_default(gsdr_trk_conf* conf);
 int gsdr_trk_create(int device, const gsdr_trk_conf* conf, gsdr_trk** out);

@@ -15,10 +15,10 @@ RTOL = 1e-4
 FS, C = 4000000, 4000
 
 
-def _oracle_attempt(chunks, codes, pfa, D, dmax, dstep, bit_transition, spc, threshold):
+def _oracle_attempt(chunks, codes, pfa, D, dmax, dstep, bit_transition, spc, threshold, fs=FS):
     """Per PRN: (dwell index, ti, di, peak, input_power/second, stat) of the decision."""
     N = len(chunks[0])
-    wipe = pcps.doppler_wipeoffs(FS, N, dmax, dstep, D)
+    wipe = pcps.doppler_wipeoffs(fs, N, dmax, dstep, D)
     out = []
     for code in codes:
         cf = pcps.fft_code(code, N, N, bit_transition=bit_transition)
@@ -108,3 +108,68 @@ def test_bit_transition(pfa):
         for i in range(len(prns)):
             _check(res[b, i], orc[i], pfa)
             assert res[b, i]["samplestamp"] == b * 2 * C
+
+
+@pytest.mark.parametrize("pfa", [0.01, 0.0])
+def test_bit_transition_c4_four_step(pfa):
+    """Config C4's acquisition as the bench times it (pcps_acquisition.cc:85-92,
+    :188-193, :671): Galileo E1 at 8 Msps, 4 ms code, bit_transition_flag -> FFT
+    64000 with the code in the second half and outputs [32000, 64000), +-10 kHz /
+    250 Hz (80 bins), on the general (dwell) path over the packed four-step."""
+    fs, C, dmax, dstep = 8000000, 32000, 10000, 250
+    rng = np.random.default_rng(64)
+    vis = [4, 19]
+    sats = [synth.GalileoSatellite(p, float(rng.uniform(-8000, 8000)), float(rng.uniform(0, 4092)), 47.0,
+                                   float(rng.uniform(0, 6.28))) for p in vis]
+    x = synth.gal_e1_iq(fs, 2 * C, sats, seed_offset=64)
+    prns = np.array([4, 7, 19, 30])
+    codes = np.stack([np.resize(synth.gal_e1_sampled(int(p), fs), 2 * C) for p in prns])
+    acq = gsdr.Acquisition(fs, 2 * C, dmax, dstep, pfa=pfa, max_prns=len(prns), bit_transition=True, sampled_ms=4,
+                           ms_per_code=4, samples_per_code=float(C))
+    assert acq.fft_size == 2 * C and acq.num_doppler_bins == 80
+    acq.set_local_codes(codes, prns)
+    D = acq.num_doppler_bins
+    spc = int(np.ceil(fs / 1023000.0))
+    thr = pcps.threshold(pfa, 2 * C, D, 1, bit_transition=True) if pfa > 0 else 2.0
+    if pfa > 0:
+        assert abs(acq.threshold - thr) <= 1e-6 * thr
+    else:
+        acq.set_threshold(thr)
+    res = acq.run(x)
+    orc = _oracle_attempt([x], codes, pfa, D, dmax, dstep, True, spc, thr, fs=fs)
+    for i in range(len(prns)):
+        _check(res[0, i], orc[i], pfa)
+        assert res[0, i]["positive"] == int(orc[i][5] > thr)
+    if pfa > 0:  # detection (not parity)
+        assert {int(r["prn"]) for r in res[0] if r["positive"]} >= set(vis)
+
+
+@pytest.mark.parametrize("pfa", [0.01, 0.0])
+def test_noncoherent_dwells_four_step(pfa):
+    """max_dwells > 1 at a four-step size (Galileo E1, 8 Msps, 4 ms: N = 32000):
+    the dwell accumulator rows of the general path on the packed four-step."""
+    fs, C, K, dmax, dstep = 8000000, 32000, 2, 3000, 500
+    rng = np.random.default_rng(32)
+    sats = [synth.GalileoSatellite(p, float(rng.uniform(-2500, 2500)), float(rng.uniform(0, 4092)), 43.0,
+                                   float(rng.uniform(0, 6.28))) for p in (4, 19)]
+    x = synth.gal_e1_iq(fs, K * C, sats, seed_offset=32)
+    prns = np.array([4, 7, 19])
+    codes = np.stack([synth.gal_e1_sampled(int(p), fs) for p in prns])
+    acq = gsdr.Acquisition(fs, C, dmax, dstep, pfa=pfa, max_prns=len(prns), max_dwells=K, sampled_ms=4,
+                           ms_per_code=4, samples_per_code=float(C))
+    assert acq.fft_size == C
+    acq.set_local_codes(codes, prns)
+    D = acq.num_doppler_bins
+    spc = int(np.ceil(fs / 1023000.0))
+    thr = pcps.threshold(pfa, C, D, K) if pfa > 0 else 3.0
+    if pfa > 0:
+        assert abs(acq.threshold - thr) <= 1e-6 * thr
+    else:
+        acq.set_threshold(thr)
+    res = acq.run(x, stamp0=7)
+    chunks = [x[k * C:(k + 1) * C] for k in range(K)]
+    orc = _oracle_attempt(chunks, codes, pfa, D, dmax, dstep, False, spc, thr, fs=fs)
+    for i in range(len(prns)):
+        _check(res[0, i], orc[i], pfa)
+        assert res[0, i]["samplestamp"] == 7 + orc[i][0] * C
+        assert res[0, i]["positive"] == int(orc[i][5] > thr)

@@ -14,6 +14,9 @@ I/Q, free-running agreement):
          12 Galileo E1 (N = 100000), 8 BeiDou B1I (N = 25000) on three handles over
          one IQ stream carrying all 32 satellites
 """
+import json
+import os
+
 import numpy as np
 import pytest
 
@@ -45,6 +48,7 @@ def _pool_check(conf, sats, iq_host, iq_ref, fs, codes, data_codes, acq, max_epo
                 narrow=None, open_loop=None, tag="", free=True):
     """One pool launch of all channels, then per channel: open-loop taps, replay and
     free-running checks against an oracle channel with the same configuration."""
+    spread = {}
     t = gsdr.Tracking(conf)
     starts = []
     for c, s in enumerate(sats):
@@ -61,7 +65,8 @@ def _pool_check(conf, sats, iq_host, iq_ref, fs, codes, data_codes, acq, max_epo
         assert len(g) >= max_epochs // 2, (tag, c, len(g))
         dc = None if data_codes is None else data_codes[c]
         if open_loop is None or c in open_loop:
-            worst = _open_loop_sig(g, iq_ref, codes[c], dc, fs, f, tap_chips, spc, chip_rate, vl, iP, narrow)
+            worst = _open_loop_sig(g, iq_ref, codes[c], dc, fs, f, tap_chips, spc, chip_rate, vl, iP, narrow,
+                                   spread=spread)
             assert worst <= 1e-4, (tag, c, worst)
         rep = trk.Channel(oc)
         assert rep.start(codes[c], d, f, 0, 0, prn=s.prn, data_code=dc) == fg
@@ -71,7 +76,19 @@ def _pool_check(conf, sats, iq_host, iq_ref, fs, codes, data_codes, acq, max_epo
             fo = fr.start(codes[c], d, f, 0, 0, prn=s.prn, data_code=dc)
             orc, _ = fr.run(iq_ref, 0, fo, max_epochs)
             _free_check(g, orc, "%s ch%d" % (tag, c))
+    _log_spread(tag, len(sats), spread)
     return rec, n
+
+
+def _log_spread(tag, nch, spread):
+    """Print (and with GSDR_PARITY_LOG append as JSON) the worst per-call distances
+    of the GPU taps and of the generic VOLK correlator to the fp64 evaluation."""
+    line = dict(tag=tag, channels=nch, **{k: (float(v) if isinstance(v, float) else v) for k, v in spread.items()})
+    print("parity spread", json.dumps(line))
+    path = os.environ.get("GSDR_PARITY_LOG")
+    if path:
+        with open(path, "a") as f:
+            f.write(json.dumps(line) + "\n")
 
 
 def test_c1_c2_gps_4msps_through_bit_sync():
@@ -100,10 +117,10 @@ def test_c1_c2_gps_4msps_through_bit_sync():
 
 def test_c3_gps_16msps_12_channel_pool():
     fs = 16.0e6
-    # 52 dB-Hz: the 1e-4 open-loop bar is relative to the taps, and at 16 Msps the
-    # reference rotator's own fp32 error grows with N while a
-    # 46 dB-Hz prompt is only ~7 % of the summed |x|
-    sats = synth.random_constellation(12, seed_offset=33, cn0_dbhz=52.0)
+    # SURVEY §8(d)'s 45 dB-Hz.  Every call's taps are held to 1e-4 of the fp64
+    # evaluation of the reference's correlation model (_open_loop_sig); the generic
+    # VOLK rotator's own distance to that value is reported beside it
+    sats = synth.random_constellation(12, seed_offset=33, cn0_dbhz=45.0)
     for s in sats:
         s.code_doppler = True
     iq = synth.gps_l1_iq(fs, int(0.2 * fs), sats, seed_offset=33)
@@ -156,12 +173,11 @@ def test_c5_hybrid_25msps_pool_share():
           synth.bds_b1i_iq(fs, ns, bds, seed_offset=37, noise=True, dtype=np.complex128)).astype(np.complex64)
     # GPS L1 C/A, N = 25000
     _pool_check(_conf(fs, 12), gps, iq, iq, fs, [synth.gps_ca_chips(s.prn) for s in gps], None, _gps_acq, 215,
-                [-0.25, 0.0, 0.25], 1, 1.023e6, 25000, 1, open_loop={0, 5, 11}, tag="c5gps", free=False)
+                [-0.25, 0.0, 0.25], 1, 1.023e6, 25000, 1, tag="c5gps")
     # Galileo E1 pilot tracking, N = 100000
     _pool_check(_conf_sig(fs, gsdr.SIGNAL_GAL_1B, 12, 1), gal, iq, iq, fs,
                 [synth.gal_e1_sinboc11(s.prn, pilot=True) for s in gal], [synth.gal_e1_sinboc11(s.prn) for s in gal],
-                _gal_acq, 53, [-0.5, -0.25, 0.0, 0.25, 0.5], 2, 1.023e6, 100000, 2, open_loop={0, 7}, tag="c5gal",
-                free=False)
+                _gal_acq, 53, [-0.5, -0.25, 0.0, 0.25, 0.5], 2, 1.023e6, 100000, 2, tag="c5gal")
     # BeiDou B1I (D1 and D2 GEO), N = 25000
     _pool_check(_conf_sig(fs, gsdr.SIGNAL_BDS_B1, 8), bds, iq, iq, fs, [synth.bds_b1i_chips(s.prn) for s in bds], None,
-                _bds_acq, 215, [-0.25, 0.0, 0.25], 1, 2.046e6, 25000, 1, open_loop={0, 7}, tag="c5bds", free=False)
+                _bds_acq, 215, [-0.25, 0.0, 0.25], 1, 2.046e6, 25000, 1, tag="c5bds")

@@ -219,10 +219,12 @@ def _conf_sig(fs, sig, nch=1, pilot=1):
     return c
 
 
-def _open_loop_sig(g, iq, code, data_code, fs, acq_dop, shifts_chips, spc, chip_rate, vl, iP, narrow_chips=None):
+def _open_loop_sig(g, iq, code, data_code, fs, acq_dop, shifts_chips, spc, chip_rate, vl, iP, narrow_chips=None,
+                   spread=None):
     """Check 1 for any signal: every call's taps (and the data prompt) against the
     oracle correlator fed with the GPU's own incoming NCO state (narrow tap shifts
-    in states 3/4 of the extended correlator)."""
+    in states 3/4 of the extended correlator).  spread (a dict) receives the worst
+    GPU-vs-fp64 and generic-VOLK-vs-fp64 distances over the calls."""
     wide = (np.asarray(shifts_chips, np.float32) * np.float32(spc)).astype(np.float32)
     narrow = None if narrow_chips is None else (np.asarray(narrow_chips, np.float32) * np.float32(spc)).astype(np.float32)
     worst = 0.0
@@ -247,8 +249,13 @@ def _open_loop_sig(g, iq, code, data_code, fs, acq_dop, shifts_chips, spc, chip_
         # float64 evaluation of the same correlation, and the taps must also sit
         # within 1e-4 of that float64 value
         exact = volk.multicorrelator_real_codes_exact(x, code, shifts, rem_carr, carr_step, rem_code, code_step, vl)
-        assert vnorm_rel(got, exact) <= 1e-4, (e, vnorm_rel(got, exact))
-        worst = max(worst, vnorm_rel(got, ref) - (vnorm_rel(ref, exact) if vl > 8000 else 0.0))
+        ge, re = vnorm_rel(got, exact), vnorm_rel(ref, exact)
+        assert ge <= 1e-4, (e, ge)
+        if spread is not None:
+            spread["gpu_vs_fp64"] = max(spread.get("gpu_vs_fp64", 0.0), ge)
+            spread["volk_generic_vs_fp64"] = max(spread.get("volk_generic_vs_fp64", 0.0), re)
+            spread["calls"] = spread.get("calls", 0) + 1
+        worst = max(worst, vnorm_rel(got, ref) - (re if vl > 8000 else 0.0))
         if data_code is not None:
             refd = volk.multicorrelator_real_codes(x, data_code, shifts[iP:iP + 1], rem_carr, carr_step, rem_code,
                                                    code_step, vl)

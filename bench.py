@@ -113,6 +113,46 @@ def rank_plan(world, rank, blocks_per_rank, channels):
             "channels": [int(c) for c in shard.channels_of(channels, world, rank)]}
 
 
+# ---------------------------------------------------------------- C5 workload
+C5_FS = 25000000
+C5_N = 25000            # samples per 1 ms block at 25 Msps
+C5_CHANNELS = 256       # BASELINE C5: 256 channels sharded across the node's GPUs
+C5_SHARE = (12, 12, 8)  # one 32-channel share: GPS L1 C/A, Galileo E1, BeiDou B1I
+C5_COUNTS = tuple(x * C5_CHANNELS // 32 for x in C5_SHARE)  # Channels_1C / _1B / _B1 .count: 96, 96, 64
+
+
+def c5_channel_signal(c):
+    """Signal (0 GPS, 1 Galileo, 2 BeiDou) and satellite slot of global channel c,
+    numbered as GNSS-SDR numbers a .conf's channels: the Channels_1C.count GPS
+    channels first, then Galileo, then BeiDou -- so the map c % world hands every
+    GPU of an 8-GPU node the 12 + 12 + 8 share of SURVEY 8(d)."""
+    c = int(c)
+    if c < C5_COUNTS[0]:
+        return 0, c % C5_SHARE[0]
+    if c < C5_COUNTS[0] + C5_COUNTS[1]:
+        return 1, (c - C5_COUNTS[0]) % C5_SHARE[1]
+    return 2, (c - C5_COUNTS[0] - C5_COUNTS[1]) % C5_SHARE[2]
+
+
+def c5_rank_plan(world, rank, blocks_per_rank, channels=C5_CHANNELS):
+    """The C5 job's shard map (SURVEY 8e, weak scaling): one 25 Msps stream of
+    world * blocks_per_rank 1 ms blocks per step; rank r acquires its block span
+    (every 4 ms group: GPS L1 C/A grids on its even milliseconds, BeiDou B1I grids on
+    the odd ones, one Galileo E1 4 ms grid) and tracks channels c % world of the 256
+    over the whole span -- per-rank work stays constant as the world grows, and the
+    channel -> GPU map replaces cuda_multicorrelator.cu:135-155's rand() % num_devices."""
+    from gsdr import shard
+    if blocks_per_rank % 4:
+        raise ValueError("C5 blocks per rank must be a multiple of 4 (the Galileo 4 ms grid)")
+    total = world * blocks_per_rank
+    lo, hi = shard.block_range(total, world, rank)
+    chans = [int(c) for c in shard.channels_of(channels, world, rank)]
+    pools = {sig: [c for c in chans if c5_channel_signal(c)[0] == sig] for sig in (0, 1, 2)}
+    return {"total_blocks": total, "blocks": (lo, hi), "channels": chans, "pools": pools,
+            "acq": {"gps_blocks": list(range(lo, hi, 2)), "bds_blocks": list(range(lo + 1, hi, 2)),
+                    "gal_groups": list(range(lo, hi, 4))}}
+
+
 def host_cpu_info():
     """Threads the CPU baseline may use and what they are: the affinity set,
     capped by OMP_NUM_THREADS (the GPU box sets it to the job's CPU share; nproc
@@ -253,6 +293,180 @@ def load_pmc_traffic():
     return best
 
 
+def run_c5(args):
+    """bench.py --workload c5: one step = a 25 Msps stream span of world x B 1 ms
+    blocks; rank r runs the acquisition of its block span (c5_rank_plan: GPS L1 C/A
+    and BeiDou B1I 32 PRN x 81 Doppler grids, N = 25000, on alternate milliseconds,
+    one Galileo E1 36 PRN x 41 Doppler 4 ms grid, N = 100000, per 4 ms group) and
+    re-tracks its channels of the 256 (three signal pools, device-resident
+    dll_pll_veml_tracking) over the whole span from their saved start states.
+    Inputs resident in HBM; value = world x B x 25000 samples per step / max-over-
+    ranks time (weak scaling)."""
+    import torch
+    import gsdr
+    from gsdr import synth
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    torch.cuda.set_device(local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    B = args.blocks if args.blocks % 4 == 0 and args.blocks != 64 else 8
+    W, K = args.warmup, args.steps
+    plan = c5_rank_plan(world, rank, B)
+    total = plan["total_blocks"]
+    lo, hi = plan["blocks"]
+    fs, n = C5_FS, C5_N
+    # the stream: 12 GPS + 12 Galileo + 8 BeiDou satellites at 45 dB-Hz, + one
+    # Galileo code period of slack for the last tracking calls
+    rng = np.random.default_rng(500)
+    gps = synth.random_constellation(12, seed_offset=500, cn0_dbhz=45.0, prns=list(range(1, 13)), max_doppler=4000.0)
+    gal = [synth.GalileoSatellite(p, float(rng.uniform(-4000, 4000)), float(rng.uniform(0, 4092)), 45.0,
+                                  float(rng.uniform(0, 6.28))) for p in range(1, 13)]
+    bds = [synth.Satellite(p, float(rng.uniform(-4000, 4000)), float(rng.uniform(0, 2046)), 45.0,
+                           float(rng.uniform(0, 6.28))) for p in (6, 7, 8, 9, 10, 11, 12, 13)]
+    ns = total * n + 4 * n
+    iq = (synth.gps_l1_iq(fs, ns, gps, seed_offset=500, noise=False, dtype=np.complex128) +
+          synth.gal_e1_iq(fs, ns, gal, seed_offset=500, noise=False, dtype=np.complex128) +
+          synth.bds_b1i_iq(fs, ns, bds, seed_offset=500, noise=True, dtype=np.complex128)).astype(np.complex64)
+    iq_dev = torch.from_numpy(iq.view(np.float32).copy()).to(dev)
+    base = iq_dev.data_ptr()
+    # acquisition handles of this rank's span
+    acq_specs = (
+        ("gps", n, 32, 10000, 250, 1, lambda: np.stack([synth.gps_ca_sampled(p, fs) for p in range(1, 33)]),
+         plan["acq"]["gps_blocks"], 2),
+        ("bds", n, 32, 10000, 250, 1, lambda: np.stack([synth.bds_b1i_sampled(p, fs)[:n] for p in range(1, 33)]),
+         plan["acq"]["bds_blocks"], 2),
+        ("gal", 4 * n, 36, 5000, 250, 4,
+         lambda: np.stack([synth.gal_e1_sampled(p, fs, pilot=True)[:4 * n] for p in range(1, 37)]),
+         plan["acq"]["gal_groups"], 4))
+    acqs = []
+    for name, N5, P5, dmax, dstep, ms, codes, blocks, stride_ms in acq_specs:
+        if not blocks:
+            continue
+        a = gsdr.Acquisition(fs, N5, dmax, dstep, pfa=0.01, max_prns=P5, max_blocks=len(blocks), sampled_ms=ms,
+                             ms_per_code=ms, chip_rate=2046000.0 if name == "bds" else 1023000.0, device=local)
+        a.set_local_codes(codes(), np.arange(1, P5 + 1))
+        res = torch.zeros(len(blocks) * P5 * gsdr.ACQ_RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+        acqs.append((name, a, blocks[0], len(blocks), stride_ms * n, res, P5, N5))
+    # tracking pools: channel c tracks satellite slot i of its signal
+    sats_of = (gps, gal, bds)
+    pools = []
+    for sig, chans in plan["pools"].items():
+        if not chans:
+            continue
+        sigc = (gsdr.SIGNAL_GPS_1C, gsdr.SIGNAL_GAL_1B, gsdr.SIGNAL_BDS_B1)[sig]
+        c = gsdr.trk_conf_default()
+        c["fs_in"] = fs
+        c["signal"] = sigc
+        c["max_channels"] = len(chans)
+        c["pll_bw_hz"], c["dll_bw_hz"] = (40.0, 4.0) if sig == 0 else (15.0, 1.0)
+        if sig == 1:
+            c["track_pilot"] = 1
+        t = gsdr.Tracking(c, device=local)
+        chip, per = ((1.023e6, n), (1.023e6, 4 * n), (2.046e6, n))[sig]
+        for i, gc in enumerate(chans):
+            s = sats_of[sig][c5_channel_signal(gc)[1]]
+            tau = s.code_delay_chips / (chip * (1 + s.doppler_hz / 1.57542e9)) * fs
+            dop = 250.0 * round(s.doppler_hz / 250.0)
+            if sig == 0:
+                t.start(i, s.prn, synth.gps_ca_chips(s.prn), float(round(tau) % per), dop, 0, 0)
+            elif sig == 1:
+                t.start(i, s.prn, synth.gal_e1_sinboc11(s.prn, pilot=True), float(round(tau) % per), dop, 0, 0,
+                        data_code=synth.gal_e1_sinboc11(s.prn))
+            else:
+                t.start(i, s.prn, synth.bds_b1i_chips(s.prn), float(round(tau) % per), dop, 0, 0)
+        t.save_state(0)
+        epochs = total * n // per + 1
+        out = torch.zeros(len(chans) * epochs * gsdr.TRK_EPOCH_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+        cnt = torch.zeros(len(chans), dtype=torch.int32, device=dev)
+        pools.append((sig, t, epochs, out, cnt, len(chans)))
+    n_items = len(iq)
+
+    def step():
+        for sig, t, epochs, out, cnt, _ in pools:
+            t.restore_state(0)
+            t.run_device(base, 0, n_items, epochs, out.data_ptr(), cnt.data_ptr())
+        for name, a, b0, nb, stride, res, P5, N5 in acqs:
+            a.run_device(base + b0 * n * 8, nb, stride, b0 * n, res.data_ptr())
+
+    for _ in range(W):
+        step()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(K):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    # sanity on the timed region's outputs: acquisitions of the visible satellites,
+    # tracking records per channel
+    det = {}
+    for name, a, b0, nb, stride, res, P5, N5 in acqs:
+        r = res.cpu().numpy().view(gsdr.ACQ_RESULT_DTYPE).reshape(nb, P5)
+        det[name] = sorted({int(x["prn"]) for x in r[0] if x["positive"]})
+    calls = {("gps", "gal", "bds")[sig]: int(cnt.cpu().numpy().min()) for sig, _, _, _, cnt, _ in pools}
+    import math
+    flops = 0.0
+    for name, a, b0, nb, stride, res, P5, N5 in acqs:
+        Dn = a.num_doppler_bins
+        flops += nb * (Dn * (5 * N5 * math.log2(N5) + 6 * N5) + P5 * Dn * (5 * N5 * math.log2(N5) + 11 * N5))
+    samples = world * K * B * n
+    value = samples / elapsed / 1e6
+    line = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "Msamples/s",
+        "n_gpus": world,
+        "steps": K,
+        "warmup": W,
+        "ms_per_step": round(elapsed / K * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (seeded 25 Msps IQ: 12 GPS L1 C/A + 12 Galileo E1 + 8 BeiDou B1I at 45 dB-Hz + AWGN; "
+                "one stream per job)",
+        "config": {
+            "workload": "C5: hybrid GPS L1 C/A + Galileo E1 + BeiDou B1I, 25 Msps, %d channels sharded c %% world "
+                        "(12/12/8 per 32-channel share); per 4 ms of the rank's span 2 GPS + 2 BeiDou 32 PRN x 81 "
+                        "Doppler grids (N 25000) and 1 Galileo 36 PRN x 41 Doppler grid (N 100000)" % C5_CHANNELS,
+            "blocks_per_step": total, "blocks_per_rank": B, "fs_sps": fs,
+            "parallelism": "one stream of %d ms per step: acquisition blocks [%d,%d) and %d channels (GPS %d, "
+                           "Galileo %d, BeiDou %d) on rank %d of %d, no data-path collective"
+                           % (total, lo, hi, len(plan["channels"]), len(plan["pools"][0]), len(plan["pools"][1]),
+                              len(plan["pools"][2]), rank, world),
+            "tracking": "each step re-tracks the span from the channels' saved start states (three pools, one "
+                        "launch each)"},
+        "real_time_factor": round(value * 1e6 / fs, 2),
+        "roofline": {"bound": "valu", "achieved": round(flops * K / elapsed / 1e12, 2), "peak": FP32_PEAK / 1e12,
+                     "unit": "TFLOP/s", "frac": round(flops * K / elapsed / FP32_PEAK, 4), "traffic": None,
+                     "note": "nominal FFT flops of the rank's acquisition grids over the whole step (tracking and "
+                             "acquisition share the GPU)"},
+        "check": {"acquired_block0": det, "trk_calls_min_per_pool": calls},
+        "cpu_baseline": None,
+    }
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    for _, t, _, _, _, _ in pools:
+        t.close()
+    for _, a, *_ in acqs:
+        a.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -278,8 +492,13 @@ def main():
                          "time; one tracking launch per step)")
     ap.add_argument("--only", choices=["acq", "trk"], default=None,
                     help="diagnostic: run only one of the two stages (the line is then not the metric)")
+    ap.add_argument("--workload", choices=["c2", "c5"], default="c2",
+                    help="c2 (default, the metric's configuration) or c5: the 25 Msps hybrid GPS/Galileo/BeiDou "
+                         "job, 256 channels sharded c %% world, acquisition block spans per rank")
     args = ap.parse_args()
     args.trk_stream = not args.trk_replay
+    if args.workload == "c5":
+        return run_c5(args)
 
     import torch
     import gsdr

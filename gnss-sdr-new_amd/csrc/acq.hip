@@ -80,7 +80,6 @@ bool choose_variant(gsdr_acq* a)
             if (f.n == N && !(g && std::atoi(g) != 0))
                 {
                     a->variant = f.id;
-                    if (const char* e = std::getenv("GSDR_ACQ_FOUR_VARIANT")) a->variant = std::atoi(e);  // experiments
                     a->nt = 256;
                     a->plan4 = gsdr::fft::Plan4{};
                     a->plan4.n = N;
@@ -191,6 +190,7 @@ int gsdr_acq_create(int device, const gsdr_acq_conf* conf, gsdr_acq** out)
             return GSDR_E_UNSUPPORTED;
         }
     int rc = dispatch(a, 4, nullptr, 0, 0, 0, nullptr, nullptr, 0);
+    if (rc == GSDR_OK && four) rc = gsdr_acq_impl::setup_split(a);
     if (rc == GSDR_OK && !a->general && default_pk_variant(N) > 0)
         {
             int v = default_pk_variant(N);

@@ -302,7 +302,6 @@ __global__ void __launch_bounds__(PT::NT) acq_correlate_kernel(const float2* __r
 // stage visits each lane's outputs in increasing index order, so a strict '>'
 // keeps the lane's first maximum (the reference's index_max semantics).
 //
-// STAT 0: row (max, first argmax, sum) with the slot-keyed maximum below.
 // STAT 1: row (exact max, sum) only -- an order-free reduction, 2.5 VALU per output
 //         instead of 7 -- and acq_argmax_pk_kernel recomputes the one row per
 //         (b, p) that the grid maximum selects to find its first maximum; the
@@ -326,7 +325,7 @@ __global__ void __launch_bounds__(MP::NT) __attribute__((amdgpu_waves_per_eu(WPE
 {
     constexpr int PG = pg_count(PG_);
     constexpr bool PREFETCH = PG_ > 0;
-    static_assert(PREFETCH || STAT >= 1, "the slot-keyed statistic path prefetches");
+    static_assert(STAT == 1 || STAT == 2, "row statistic 1 (max + sum) or 2 (max)");
     using gsdr::pk::c2;
     constexpr int NT = MP::NT;
     constexpr int NW = NT / 64;
@@ -388,8 +387,7 @@ __global__ void __launch_bounds__(MP::NT) __attribute__((amdgpu_waves_per_eu(WPE
         }
     for (int q = 0; q < np; ++q)
         {
-            if constexpr (STAT >= 1)
-                {
+            {
                     float rmax = 0.0f, sum = 0.0f;
                     auto load = [&](int bb, int r, int i) -> c2 {
                         if constexpr (PREFETCH)
@@ -440,68 +438,7 @@ __global__ void __launch_bounds__(MP::NT) __attribute__((amdgpu_waves_per_eu(WPE
                                 }
                             stats[((size_t)b * P + p0 + q) * D + d] = best;
                         }
-                    continue;
-                }
-            // Row statistics with a slot-keyed maximum: key = bits(|R|^2) with its 5
-            // low mantissa bits replaced by (31 - slot).  Non-negative floats order
-            // like their bit patterns, so one integer max per output keeps the
-            // lane's largest value and, among equal (truncated) values, the
-            // earliest output -- the reference's first-maximum rule up to 2^-18
-            // relative (the SURVEY H3 near-tie bound is 1e-4).  The truncated value
-            // is the reported peak.
-            static_assert(MP::NSLOTS <= 32, "slot key holds 5 bits");
-            uint32_t key = 0u;
-            float sum = 0.0f;
-            // conj(X . conj(C)) = conj(X) . C ; |IFFT(Y)| = |FFT(conj(Y))|
-            auto load = [&](int bb, int r, int) -> c2 { return gsdr::pk::conj_mul(xr[bb][r], cr[bb][r]); };
-            auto hook = [&]() {
-                if (q + 1 < np)
-                    {
-                        const c2* c = reinterpret_cast<const c2*>(code_fft) + (size_t)(p0 + q + 1) * N;
-#pragma unroll
-                        for (int bb = 0; bb < BPT1; ++bb)
-                            {
-                                const int j = (int)threadIdx.x + bb * NT;
-                                if (NB1 % NT == 0 || j < NB1)
-                                    {
-#pragma unroll
-                                        for (int r = 0; r < R1; ++r) cr[bb][r] = c[j + r * NB1];
-                                    }
-                            }
-                    }
-            };
-            auto store = [&](int, c2 v, int slot) {
-                const float m = __builtin_fmaf(v.x, v.x, v.y * v.y);
-                key = max(key, (__float_as_uint(m) & ~31u) | (uint32_t)(31 - slot));
-                sum += m;
-            };
-            MP::run(lds, tw, load, store, hook);
-            // wave: max key, then the lowest lane holding it; workgroup: LDS pass
-            uint32_t wkey = key;
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) wkey = max(wkey, (uint32_t)__shfl_xor((int)wkey, off));
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) sum += __shfl_xor(sum, off);
-            const uint64_t holders = __ballot(key == wkey);
-            const int first = __ffsll((unsigned long long)holders) - 1;
-            const int my_idx = MP::index_of_slot(31 - (int)(key & 31u));
-            const uint32_t widx = (uint32_t)__shfl(my_idx, first);
-            RowStat* sc = scratch + (q & 1) * NW;
-            const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-            if (lane == 0) sc[wave] = RowStat{__uint_as_float(wkey & ~31u), widx, sum, 0};
-            __syncthreads();
-            if (threadIdx.x == 0)
-                {
-                    RowStat best = sc[0];
-#pragma unroll
-                    for (int w = 1; w < NW; ++w)
-                        {
-                            const RowStat o = sc[w];
-                            if (stat_better(o.max, o.idx, best.max, best.idx)) best = RowStat{o.max, o.idx, best.sum, 0};
-                            best.sum += o.sum;
-                        }
-                    stats[((size_t)b * P + p0 + q) * D + d] = RowStat{best.max, best.idx, best.sum, 0};
-                }
+            }
         }
 }
 
@@ -591,7 +528,7 @@ __device__ __forceinline__ void rows_stage(gsdr::pk::c2* lds, Out& out)
                     if constexpr (LAST)
                         {
 #pragma unroll
-                            for (int r = 0; r < R; ++r) out.value(v[b][r]);
+                            for (int r = 0; r < R; ++r) out.value(v[b][r], jb[b] + r * Ns);  // row output jb + r Ns
                         }
                     else
                         {
@@ -616,18 +553,13 @@ __device__ __forceinline__ void rows_stages(gsdr::pk::c2* lds, Out& out)
     if constexpr (!LAST) rows_stages<NT, L, H, Ns * R, Pads, Si + 1, Rest...>(lds, out);
 }
 
-// Pads for the buffers between the row stages (buffer 0 = phase 1's rows).
+// Pads for the buffers between the row stages (buffer 0 = phase 1's rows); a
+// bank-model padding of the 1000-point rows measured within noise.
 template <int L>
 struct NoPads
 {
     template <int I>
     using layout = RowPad<L, 0, 0>;
-};
-struct Pads1000x10
-{
-    template <int I>
-    using layout = std::conditional_t<I == 1, RowPad<1000, 10, 1>,
-        std::conditional_t<I == 2, RowPad<1000, 50, 3>, RowPad<1000, 0, 0>>>;
 };
 
 // WPE_ packs the waves-per-EU hint (bits 0-3) and PGS (bits 4+): with PGS > 0 an
@@ -738,7 +670,7 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(RP:
         const float2* tw;
         float m;
         __device__ __forceinline__ float2 twiddle(int m_) const { return tw[m_ * R]; }  // W_L^m = W_N^{m R}
-        __device__ __forceinline__ void value(c2 x) { m = __builtin_fmaxf(m, __builtin_fmaf(x.x, x.x, x.y * x.y)); }
+        __device__ __forceinline__ void value(c2 x, int) { m = __builtin_fmaxf(m, __builtin_fmaf(x.x, x.x, x.y * x.y)); }
     } out{tw, 0.0f};
     // phase 2: rows k1 = h*H .. h*H+H-1 through LDS
 #pragma unroll
@@ -768,6 +700,273 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(RP:
 #pragma unroll
             for (int w2 = 1; w2 < NW; ++w2) best = __builtin_fmaxf(best, red[w2]);
             stats[((size_t)b * P + p) * D + d] = RowStat{best, 0u, 0.0f, 0};
+        }
+}
+
+// ---------------------------------------------------------------- K_correlate, split register four-step (large N)
+// Transforms too large for one workgroup's registers (N = 64000: 512 KB, the whole
+// register file of a CU; N = 100000) and the register-resident ones beyond the
+// LDS engine (N = 25000, 32000).  Outer decimation in frequency by ROUT:
+//   X[q + ROUT k'] = sum_m W_M^{m k'} z_q[m],   m < M = N / ROUT,
+//   z_q[m] = W_N^{m q} sum_{r < ROUT} Y[r M + m] W_ROUT^{r q},
+// so the ROUT sub-transforms own disjoint output sets and each one is a workgroup
+// of its own: an M-point register four-step (phase 1 columns in VGPRs, phase 2
+// rows through LDS, RegFourStep RP) whose loads form z_q from the ROUT products
+// Y = conj(X) C of its input positions.  Nothing round-trips through a global
+// scratch row (the packed four-step's phase-1 rows did, 2 x 8 N bytes per
+// transform); a sub-transform re-reads the whole X and code rows instead, which
+// the XCD-aware walk below keeps in L2.  Only the row maximum is kept (STAT 2,
+// atomically merged over the ROUT sub-transforms); acq_argmax_four_kernel
+// recomputes the selected row for the first-maximum index and the CFAR power.
+// HALF (bit_transition_flag): only outputs k >= N / 2 are the reference's
+// effective window (pcps_acquisition.cc:671); with k = q + ROUT (k1 + R k2),
+// k >= N / 2 exactly when the row output k2 >= L / 2.
+// Grid: one workgroup per (row = b*D + d, PRN p, sub-transform q), the ROUT*P
+// workgroups of one row on one XCD, each XCD walking its rows in groups of pgs
+// PRNs so its L2 holds pgs code rows while the X rows stream.
+template <int ROUT, class RP, bool HALF>
+__global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(RP::WPE))) acq_correlate_split_kernel(
+    const float2* __restrict__ X, const float2* __restrict__ code_fft, RowStat* __restrict__ stats,
+    const float2* __restrict__ tw, uint32_t D, uint32_t P, uint32_t nblocks, uint32_t pgs)
+{
+    using gsdr::pk::c2;
+    constexpr int R = RP::R, NT = RP::NT, H = RP::H, L = RP::L, CPL = RP::CPL;
+    constexpr uint32_t M = RP::N;
+    constexpr uint32_t N = M * ROUT;
+    constexpr int NW = NT / 64;
+    extern __shared__ float2 lds_raw[];
+    c2* lds = reinterpret_cast<c2*>(lds_raw);
+    float* red = reinterpret_cast<float*>(lds_raw + RP::lds_elems);
+    const uint32_t PV = P * ROUT;  // virtual PRNs: pv = p * ROUT + q
+    const uint32_t nrows = nblocks * D;
+    const uint32_t id = blockIdx.x;
+    const uint32_t full = nrows >> 3;
+    uint32_t row, pv;
+    if (id < full * 8u * PV)
+        {
+            const uint32_t xcd = id & 7u, slot = id >> 3;
+            const uint32_t G = pgs * ROUT;  // PV % G == 0 (host)
+            const uint32_t per_group = full * G;
+            const uint32_t pg = slot / per_group, rem = slot - pg * per_group;
+            const uint32_t ri = rem / G;
+            row = ri * 8u + xcd;
+            pv = pg * G + (rem - ri * G);
+        }
+    else
+        {
+            const uint32_t t = id - full * 8u * PV;
+            row = full * 8u + t / PV;
+            pv = t - (t / PV) * PV;
+        }
+    const uint32_t p = pv / ROUT, q = pv - p * ROUT;
+    const uint32_t b = row / D, d = row - (row / D) * D;
+    const auto xrs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float2*>(X) + (size_t)row * N, 0, (int)(N * sizeof(c2)), 0x00020000);
+    const auto crs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float2*>(code_fft) + (size_t)p * N, 0, (int)(N * sizeof(c2)), 0x00020000);
+    auto bload = [](decltype(xrs) rs, int voff, int soff) -> c2 {
+        const auto u = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, 0);
+        return c2{__uint_as_float(u[0]), __uint_as_float(u[1])};
+    };
+    // W_ROUT^{r q}: exact (+-1, +-i) for ROUT <= 4
+    static_assert(ROUT == 1 || ROUT == 2 || ROUT == 4, "outer radix 1, 2 or 4");
+    c2 wq[ROUT];
+#pragma unroll
+    for (int r = 0; r < ROUT; ++r)
+        {
+            const int e4 = (int)(((uint32_t)r * q) % ROUT) * (4 / ROUT);  // W_ROUT^{rq} = W_4^{e4}
+            wq[r] = e4 == 0 ? c2{1.f, 0.f} : (e4 == 1 ? c2{0.f, -1.f} : (e4 == 2 ? c2{-1.f, 0.f} : c2{0.f, 1.f}));
+        }
+    const int wbase = (int)(threadIdx.x & ~63u);
+    // phase 1: columns (clamped lanes repeat column L-1)
+    c2 v[CPL][R];
+#pragma unroll
+    for (int c = 0; c < CPL; ++c)
+        {
+            if (L % NT == 0 || wbase + c * NT < L)
+                {
+                    const int n2 = min((int)threadIdx.x + c * NT, L - 1);
+#pragma unroll
+                    for (int n1 = 0; n1 < R; ++n1)
+                        {
+                            const int m = n1 * L + n2;
+                            c2 z = gsdr::pk::conj_mul(bload(xrs, n2 * 8, n1 * L * 8), bload(crs, n2 * 8, n1 * L * 8));
+#pragma unroll
+                            for (int r = 1; r < ROUT; ++r)
+                                {
+                                    const int so = (int)((r * M + n1 * L) * 8);
+                                    const c2 y = gsdr::pk::conj_mul(bload(xrs, n2 * 8, so), bload(crs, n2 * 8, so));
+                                    z = z + gsdr::pk::mul(y, wq[r]);
+                                }
+                            if (ROUT > 1 && q > 0)
+                                {
+                                    // W_N^{m q} = (W_N^m)^q
+                                    const c2 w1 = gsdr::pk::from(tw[m]);
+                                    c2 w = w1;
+                                    for (uint32_t e = 1; e < q; ++e) w = gsdr::pk::mul(w, w1);
+                                    z = gsdr::pk::mul(z, w);
+                                }
+                            v[c][n1] = z;
+                        }
+                    gsdr::pk::Dft<R>::run(v[c]);
+                    // W_M^{n2 k1} = W_N^{ROUT n2 k1}
+                    const c2 w1 = gsdr::pk::from(tw[ROUT * n2]);
+                    c2 w = w1;
+#pragma unroll
+                    for (int k1 = 1; k1 < R; ++k1)
+                        {
+                            if (k1 > 1) w = gsdr::pk::mul(w, w1);
+                            v[c][k1] = gsdr::pk::mul(v[c][k1], w);
+                        }
+                }
+        }
+    struct Out
+    {
+        const float2* tw;
+        float m;
+        // W_L^m = W_N^{m R ROUT}
+        __device__ __forceinline__ float2 twiddle(int m_) const { return tw[m_ * R * ROUT]; }
+        __device__ __forceinline__ void value(c2 x, int k2)
+        {
+            const float a = __builtin_fmaf(x.x, x.x, x.y * x.y);
+            if (!HALF || k2 >= L / 2) m = __builtin_fmaxf(m, a);
+        }
+    } out{tw, 0.0f};
+#pragma unroll
+    for (int h = 0; h < R / H; ++h)
+        {
+            if (h > 0) __syncthreads();
+#pragma unroll
+            for (int c = 0; c < CPL; ++c)
+                {
+                    if (L % NT == 0 || wbase + c * NT < L)
+                        {
+                            const int n2 = min((int)threadIdx.x + c * NT, L - 1);
+#pragma unroll
+                            for (int i = 0; i < H; ++i) lds[i * L + n2] = v[c][h * H + i];
+                        }
+                }
+            __syncthreads();
+            RP::row_transforms(lds, out);
+        }
+    float rmax = gsdr::wave_max(out.m);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) red[wave] = rmax;
+    __syncthreads();
+    if (threadIdx.x == 0)
+        {
+            float best = red[0];
+#pragma unroll
+            for (int w2 = 1; w2 < NW; ++w2) best = __builtin_fmaxf(best, red[w2]);
+            RowStat* st = stats + ((size_t)b * P + p) * D + d;
+            if constexpr (ROUT == 1)
+                *st = RowStat{best, 0u, 0.0f, 0};
+            else  // non-negative floats order as their bit patterns (row zeroed by the host)
+                __hip_atomic_fetch_max(reinterpret_cast<uint32_t*>(&st->max), __float_as_uint(best), __ATOMIC_RELAXED,
+                    __HIP_MEMORY_SCOPE_AGENT);
+        }
+}
+
+// After acq_reduce_kernel chose the Doppler row d* of (b, p) from the split
+// kernel's row maxima: recompute row d* on the plan PT (FourStepPkPlan) -- its
+// first maximum over the effective window [N - eff, N) with the reference's
+// index_max rule (KERN/32f_index_max_32u.h:446-467), code_phase and
+// Acq_delay_samples (pcps_acquisition.cc:709), the peak as recomputed -- and the
+// CFAR power of the row opposite the peak (:531-533): by Parseval over the whole
+// row, or, for the half window of bit transition, by recomputing that row too.
+template <class PT>
+__global__ void __launch_bounds__(PT::NT) acq_argmax_four_kernel(const float2* __restrict__ X,
+    const float2* __restrict__ code_fft, gsdr_acq_result* __restrict__ res, const float2* __restrict__ tw,
+    typename PT::PlanT plan, AcqParams ap)
+{
+    constexpr int NT = PT::NT;
+    constexpr int NW = NT / 64;
+    extern __shared__ float2 lds[];
+    __shared__ unsigned long long s_key[NW];
+    __shared__ float s_sum[NW];
+    const uint32_t bp = blockIdx.x;
+    const uint32_t b = bp / ap.P, p = bp - b * ap.P;
+    const uint32_t N = ap.N;
+    const uint32_t d = res[bp].doppler_index;
+    if (d >= ap.D) return;  // uniform: no maximum found (an all-NaN grid)
+    const float2* c = code_fft + (size_t)p * N;
+    const int off = (int)ap.out_off;
+    auto row_load = [&](const float2* x) {
+        return [x, c](int i) -> float2 {
+            const float2 a = x[i], k = c[i];
+            return make_float2(a.x * k.x + a.y * k.y, a.x * k.y - a.y * k.x);
+        };
+    };
+    unsigned long long key = 0ull;
+    auto store = [&](int i, float2 v) {
+        const int j = i - off;
+        if (j < 0) return;
+        const float m = __builtin_fmaf(v.x, v.x, v.y * v.y);
+        const unsigned long long k = ((unsigned long long)__float_as_uint(m) << 32) | (0xffffffffu - (uint32_t)j);
+        key = k > key ? k : key;
+    };
+    PT::run(plan, lds, tw, row_load(X + ((size_t)b * ap.D + d) * N), store);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+        {
+            const unsigned long long t = __shfl_xor(key, o);
+            key = t > key ? t : key;
+        }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) s_key[wave] = key;
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < NW; ++w) key = s_key[w] > key ? s_key[w] : key;
+    const uint32_t idx = 0xffffffffu - (uint32_t)(key & 0xffffffffu);
+    const float peak = __uint_as_float((uint32_t)(key >> 32));
+    float ip = 0.0f;
+    if (ap.cfar && !ap.step_two)
+        {
+            const uint32_t opp = (d + ap.D / 2) % ap.D;
+            const float2* xo = X + ((size_t)b * ap.D + opp) * N;
+            float acc = 0.0f;
+            if (off == 0)
+                {
+                    // accumulate(|R|^2) / fft_size = sum_k |Y_opp[k]|^2 (unnormalised R = FFT(conj Y))
+                    for (uint32_t i = threadIdx.x; i < N; i += NT)
+                        {
+                            const float2 a = xo[i], k = c[i];
+                            const float yr = a.x * k.x + a.y * k.y, yi = a.x * k.y - a.y * k.x;
+                            acc = __builtin_fmaf(yr, yr, __builtin_fmaf(yi, yi, acc));
+                        }
+                }
+            else
+                {
+                    auto sum_store = [&](int i, float2 v) {
+                        if (i >= off) acc += __builtin_fmaf(v.x, v.x, v.y * v.y);
+                    };
+                    __syncthreads();  // LDS reuse by the second transform
+                    PT::run(plan, lds, tw, row_load(xo), sum_store);
+                }
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+            if (lane == 0) s_sum[wave] = acc;
+            __syncthreads();
+            float tot = 0.0f;
+#pragma unroll
+            for (int w = 0; w < NW; ++w) tot += s_sum[w];
+            // float(accumulate) / eff, then / 2.0 / counter in double (pcps_acquisition.cc:533)
+            ip = off == 0 ? (float)((double)tot / 2.0 / (double)ap.counter)
+                          : (float)((double)(tot / (float)(int32_t)ap.eff) / 2.0 / (double)ap.counter);
+        }
+    if (threadIdx.x == 0)
+        {
+            gsdr_acq_result r = res[bp];
+            r.code_phase = idx;
+            r.acq_delay_samples = (double)fmodf((float)idx, ap.samples_per_code);
+            r.peak = peak;
+            if (ap.cfar)
+                {
+                    if (!ap.step_two) r.input_power = ip;
+                    r.test_statistic = r.peak / r.input_power;
+                    r.positive = r.test_statistic > ap.threshold ? 1 : 0;
+                }
+            res[bp] = r;
         }
 }
 
@@ -1324,6 +1523,8 @@ __global__ void __launch_bounds__(PT::NT) acq_second_peak_kernel(const float2* _
     const uint32_t N = plan.n;
     const uint32_t d = res[bp].doppler_index;
     const int32_t ti = (int32_t)res[bp].code_phase;
+    // the window over the effective outputs j = i - out_off (bit transition: the
+    // second half); the reference wraps it at d_fft_size all the same (:580-590)
     int32_t e1 = ti - (int32_t)ap.samples_per_chip;
     int32_t e2 = ti + (int32_t)ap.samples_per_chip;
     if (e1 < 0)
@@ -1339,12 +1540,14 @@ __global__ void __launch_bounds__(PT::NT) acq_second_peak_kernel(const float2* _
         return make_float2(a.x * k.x + a.y * k.y, a.x * k.y - a.y * k.x);
     };
     auto store = [&](int i, float2 v) {
-        const bool excluded = (e1 < e2) ? (i >= e1 && i < e2) : (i >= e1 || i < e2);
+        const int j = i - (int)ap.out_off;
+        if (j < 0) return;
+        const bool excluded = (e1 < e2) ? (j >= e1 && j < e2) : (j >= e1 || j < e2);
         const float m = excluded ? 0.0f : v.x * v.x + v.y * v.y;
-        if (stat_better(m, (uint32_t)i, best, bidx))
+        if (stat_better(m, (uint32_t)j, best, bidx))
             {
                 best = m;
-                bidx = (uint32_t)i;
+                bidx = (uint32_t)j;
             }
     };
     PT::run(plan, lds, tw, load, store);
@@ -1378,6 +1581,8 @@ struct gsdr_acq
     int nt{256};
     int variant{0};
     int corr_variant{0};      // 0: the generic LDS kernels; >0: a GSDR_PK_VARIANTS id (packed forward + correlate)
+    int split{0};             // >0: the single-dwell split register four-step correlate (acq_split.hip)
+    uint32_t split_pgs{1};    // its PRN group per XCD pass
     int corr_stat{0};         // the variant's row statistic (1/2: argmax recomputed by acq_argmax_pk_kernel)
     size_t tw_entries{0};     // twiddle entries the packed variant reads (W_N + its per-stage table)
     void (*tw_fill)(float2*){nullptr};  // fills the per-stage table after W_N
@@ -1440,61 +1645,21 @@ size_t item_bytes(int it) { return it == GSDR_ITEM_CSHORT ? 4 : (it == GSDR_ITEM
 // four-step FFT beyond one workgroup's LDS (acq_v_four.hip).
 
 
-// Correlate-kernel variants for N = 4000 (env GSDR_ACQ_CORR_VARIANT selects one;
-// 0 = the single-transform kernel of the plan variant).
-// Packed-f32 correlate (and forward) variants: (id, plan, PRNs per workgroup,
-// waves-per-EU hint).  30-39, 70-85 are N = 4000 plans (70 the default); 60-69 the
-// other compile-time sizes (1 ms at 16 / 8 / 2 Msps); 90-92 run the correlate on
-// the register four-step (acq_correlate_reg_kernel, N = 16000; 93 the default: 90
-// with the PRN-group-major XCD walk, 16 code spectra per L2) and
-// the forward / argmax passes on the listed plan.  The plan's second argument packs
-// the twiddle mode (bits 0-3, fft_pk.h TWP), the last-stage block pad PADL (bits
-// 4-7) and the LATE barrier flag (bit 8).  The non-default ids are the measured
-// alternatives DESIGN.md 5 / 10 reports (all within noise of or slower than the
-// defaults); every one is in tests/test_gpu_acq.py's parity list.
-// Columns: (id, plan, PRNs per workgroup, waves-per-EU hint, row statistic: 0 max +
-// first argmax in the kernel, 1 max + sum with the argmax recomputed for the
-// selected row, see acq_correlate_pk_kernel).
+// Packed-f32 correlate (and forward / argmax) variants, one per compile-time FFT
+// size (default_pk_variant; GSDR_ACQ_CORR_VARIANT selects one for tests):
+// (id, plan, PRNs per workgroup, waves-per-EU hint, row statistic: 1 max + sum
+// with the argmax recomputed for the selected row, 2 max only with the CFAR row
+// sum by Parseval -- see acq_correlate_pk_kernel).  93 runs the correlate on the
+// register four-step (acq_correlate_reg_kernel, N = 16000, PRN-group-major XCD
+// walk) and its forward / argmax passes on the listed plan.  The alternatives
+// measured in rounds 1-2 (other radix orders, per-stage twiddle tables, LDS root
+// copies, padded layouts, late barriers, 5 waves, PRN groups)
+// were within noise of or slower than these and are no longer built.
 #define GSDR_PK_VARIANTS(X)                                              \
-    X(30, (gsdr::pk::PkPlan<256, true, 25, 16, 10>), 1, 1, 0)           \
-    X(31, (gsdr::pk::PkPlan<256, true, 25, 16, 10>), 1, 1, 1)           \
-    X(32, (gsdr::pk::PkPlan<256, false, 25, 16, 10>), 1, 1, 1)          \
-    X(35, (gsdr::pk::PkPlan<256, true, 20, 20, 10>), 1, 1, 0)           \
-    X(36, (gsdr::pk::PkPlan<256, true, 20, 20, 10>), 1, 1, 1)           \
-    X(37, (gsdr::pk::PkPlan<512, true, 25, 16, 10>), 2, 1, 0)           \
-    X(38, (gsdr::pk::PkPlan<256, false, 20, 20, 10>), 1, 1, 1)          \
-    X(39, (gsdr::pk::PkPlan<256, true, 25, 16, 10>), 1, 5, 1)           \
-    X(60, (gsdr::pk::PkPlan<1024, true, 16, 10, 10, 10>), 1, 1, 1)      \
     X(61, (gsdr::pk::PkPlan<512, true, 20, 20, 20>), 1, 1, 1)           \
     X(62, (gsdr::pk::PkPlan<256, true, 20, 10, 10>), 1, 1, 1)           \
-    X(63, (gsdr::pk::PkPlan<1024, 1, 16, 10, 10, 10>), 1, 1, 2)         \
-    X(64, (gsdr::pk::PkPlan<512, 1, 20, 20, 20>), 1, 1, 2)              \
-    X(65, (gsdr::pk::PkPlan<256, 1, 20, 10, 10>), 1, 1, 2)              \
-    X(66, (gsdr::pk::PkPlan<1024, 1, 16, 10, 10, 10>), 4, 1, 2)         \
-    X(67, (gsdr::pk::PkPlan<1024, 1, 16, 10, 10, 10>), -4, 1, 2)        \
-    X(68, (gsdr::pk::PkPlan<1024, 1, 16, 10, 10, 10>), -8, 1, 2)        \
-    X(69, (gsdr::pk::PkPlan<1024, 1, 16, 10, 10, 10>), -32, 1, 2)       \
-    X(90, (gsdr::pk::PkPlan<1024, 1, 16, 10, 10, 10>), 1, 1, 2)         \
-    X(91, (gsdr::pk::PkPlan<1024, 1, 16, 10, 10, 10>), 1, 1, 2)         \
-    X(92, (gsdr::pk::PkPlan<1024, 1, 16, 10, 10, 10>), 1, 1, 2)         \
     X(93, (gsdr::pk::PkPlan<1024, 1, 16, 10, 10, 10>), 1, 1, 2)         \
-    X(94, (gsdr::pk::PkPlan<1024, 1, 16, 10, 10, 10>), 1, 1, 2)         \
-    X(70, (gsdr::pk::PkPlan<256, 1, 25, 16, 10>), 1, 1, 2)              \
-    X(71, (gsdr::pk::PkPlan<256, 2, 25, 16, 10>), 1, 1, 1)              \
-    X(72, (gsdr::pk::PkPlan<256, 2, 25, 16, 10>), 1, 1, 2)              \
-    X(73, (gsdr::pk::PkPlan<256, 2, 20, 20, 10>), 1, 1, 2)              \
-    X(74, (gsdr::pk::PkPlan<256, 2, 10, 16, 25>), 1, 1, 2)              \
-    X(75, (gsdr::pk::PkPlan<256, 1, 16, 25, 10>), 1, 1, 2)              \
-    X(76, (gsdr::pk::PkPlan<256, 1, 25, 10, 16>), 1, 1, 2)              \
-    X(77, (gsdr::pk::PkPlan<256, 1, 25, 16, 10>), 1, 5, 2)              \
-    X(78, (gsdr::pk::PkPlan<256, 1, 20, 20, 10>), 1, 1, 2)              \
-    X(79, (gsdr::pk::PkPlan<256, 3, 25, 16, 10>), 1, 1, 2)              \
-    X(80, (gsdr::pk::PkPlan<256, 3, 20, 20, 10>), 1, 1, 2)              \
-    X(81, (gsdr::pk::PkPlan<256, 1 | (9 << 4), 25, 16, 10>), 1, 1, 2)   \
-    X(82, (gsdr::pk::PkPlan<256, 3 | (9 << 4), 25, 16, 10>), 1, 1, 2)   \
-    X(83, (gsdr::pk::PkPlan<256, 1 | 256, 25, 16, 10>), 1, 1, 2)        \
-    X(84, (gsdr::pk::PkPlan<256, 1 | (9 << 4) | 256, 25, 16, 10>), 1, 1, 2) \
-    X(85, (gsdr::pk::PkPlan<1024, 1 | 256, 16, 10, 10, 10>), 1, 1, 2)
+    X(70, (gsdr::pk::PkPlan<256, 1, 25, 16, 10>), 1, 1, 2)
 
 template <class PT>
 int set_lds_attrs(size_t bytes)
@@ -1519,6 +1684,9 @@ int set_lds_attrs(size_t bytes)
         hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
     GSDR_HIP(hipFuncSetAttribute((const void*)acq_dwell_grid_kernel<PT>, hipFuncAttributeMaxDynamicSharedMemorySize,
         (int)bytes));
+    if constexpr (std::is_same<typename PT::PlanT, gsdr::fft::Plan4>::value)
+        GSDR_HIP(hipFuncSetAttribute((const void*)acq_argmax_four_kernel<PT>,
+            hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
     return GSDR_OK;
 }
 
@@ -1632,6 +1800,8 @@ int launch_corr_variant(gsdr_acq* a, uint32_t nblocks, hipStream_t s);
 int launch_argmax_variant(gsdr_acq* a, uint32_t nblocks, gsdr_acq_result* res, hipStream_t s);
 int launch_forward_pk(gsdr_acq* a, const void* iq, int item_type, uint32_t nblocks, uint64_t stride, hipStream_t s);
 int setup_corr_variant(gsdr_acq* a, int v);
+int setup_split(gsdr_acq* a);
+int launch_split(gsdr_acq* a, uint32_t nblocks, hipStream_t s);
 int dispatch_static(gsdr_acq* a, int op, const void* iq, uint32_t nblocks, uint64_t stride, uint64_t stamp0,
     gsdr_acq_result* res, hipStream_t s, uint32_t aux);
 int dispatch_runtime(gsdr_acq* a, int op, const void* iq, uint32_t nblocks, uint64_t stride, uint64_t stamp0,
@@ -1706,12 +1876,54 @@ int launch_general(gsdr_acq* a, const void* iq, int item_type, uint32_t nblocks,
     return GSDR_OK;
 }
 
+// Split register four-step path (single dwell, with or without bit transition):
+// forward spectra on PT, the split correlate's row maxima, the grid maximum, the
+// selected row recomputed on PT for the first-maximum index / exact peak / CFAR
+// power, and (peak ratio) the second peak on the same row.
+template <class PT>
+int launch_split_all(gsdr_acq* a, const void* iq, int item_type, uint32_t nblocks, uint64_t stride, uint64_t stamp0,
+    gsdr_acq_result* res, hipStream_t s, StageTimer& t)
+{
+    const size_t lds = a->lds_bytes;
+    t.begin();
+    launch_forward<PT>(a, iq, item_type, nblocks, stride, s);
+    GSDR_HIP(hipGetLastError());
+    t.end(0);
+    AcqParams ap = params_of(a);
+    t.begin();
+    int rc = gsdr_acq_impl::launch_split(a, nblocks, s);
+    if (rc != GSDR_OK) return rc;
+    GSDR_HIP(hipGetLastError());
+    t.end(1);
+    t.begin();
+    hipLaunchKernelGGL(acq_reduce_kernel, dim3(nblocks * a->nprn), dim3(64), 0, s, a->d_stats, res, a->d_prn, ap,
+        stamp0, stride);
+    GSDR_HIP(hipGetLastError());
+    hipLaunchKernelGGL((acq_argmax_four_kernel<PT>), dim3(nblocks * a->nprn), dim3(PT::NT), lds, s, a->d_X,
+        a->d_code_fft, res, a->d_tw, plan_of<PT>(a), ap);
+    GSDR_HIP(hipGetLastError());
+    t.end(2);
+    if (!ap.cfar)
+        {
+            t.begin();
+            hipLaunchKernelGGL((acq_second_peak_kernel<PT>), dim3(nblocks * a->nprn), dim3(PT::NT), lds, s, a->d_X,
+                a->d_code_fft, res, a->d_tw, plan_of<PT>(a), ap);
+            GSDR_HIP(hipGetLastError());
+            t.end(3);
+        }
+    return GSDR_OK;
+}
+
 template <class PT>
 int launch_all(gsdr_acq* a, const void* iq, int item_type, uint32_t nblocks, uint64_t stride, uint64_t stamp0,
     gsdr_acq_result* res, hipStream_t s)
 {
     const size_t lds = a->lds_bytes;
     StageTimer t(a, s);
+    if constexpr (std::is_same<typename PT::PlanT, gsdr::fft::Plan4>::value)
+        {
+            if (a->split > 0) return launch_split_all<PT>(a, iq, item_type, nblocks, stride, stamp0, res, s, t);
+        }
     if (a->general) return launch_general<PT>(a, iq, item_type, nblocks, stride, stamp0, res, s, t);
     t.begin();
     if (a->corr_variant > 0)

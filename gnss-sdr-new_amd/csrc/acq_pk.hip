@@ -5,14 +5,11 @@
 namespace gsdr_acq_impl
 {
 
-// Variants whose correlate kernel is not acq_correlate_pk_kernel (their forward
-// and argmax passes use the variant's PkPlan): 90 = N 16000 on the register
-// four-step 16 x (10 x 10 x 10), 512 lanes, 8 rows per LDS round.
-using RegPlan90 = RegFourStep<16, 512, 8, 1, NoPads<1000>, 10, 10, 10>;
-using RegPlan91 = RegFourStep<16, 512, 8, 1, Pads1000x10, 10, 10, 10>;
-using RegPlan92 = RegFourStep<16, 512, 4, 1, Pads1000x10, 10, 10, 10>;
+// The variant whose correlate kernel is not acq_correlate_pk_kernel (its forward
+// and argmax passes use the variant's PkPlan): 93 = N 16000 on the register
+// four-step 16 x (10 x 10 x 10), 512 lanes, 8 rows per LDS round, each XCD's
+// rows walked in groups of 16 PRNs.
 using RegPlan93 = RegFourStep<16, 512, 8, 1 | (16 << 4), NoPads<1000>, 10, 10, 10>;
-using RegPlan94 = RegFourStep<16, 512, 8, 1 | (8 << 4), NoPads<1000>, 10, 10, 10>;
 
 template <class RP>
 int launch_reg(gsdr_acq* a, uint32_t nblocks, hipStream_t s)
@@ -34,11 +31,7 @@ int launch_corr_variant(gsdr_acq* a, uint32_t nblocks, hipStream_t s)
 {
     switch (a->corr_variant)
         {
-        case 90: return launch_reg<RegPlan90>(a, nblocks, s);
-        case 91: return launch_reg<RegPlan91>(a, nblocks, s);
-        case 92: return launch_reg<RegPlan92>(a, nblocks, s);
         case 93: return launch_reg<RegPlan93>(a, nblocks, s);
-        case 94: return launch_reg<RegPlan94>(a, nblocks, s);
         default: break;
         }
 #define GSDR_PK_CASE(ID, MP, PG, WPE, ST)                                                                       \
@@ -137,11 +130,7 @@ int setup_corr_variant(gsdr_acq* a, int v)
                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)M::lds_bytes()));                              \
             GSDR_HIP(hipFuncSetAttribute((const void*)acq_forward_pk_kernel<M, GSDR_ITEM_IBYTE>,               \
                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)M::lds_bytes()));                              \
-            if (ID == 90 && setup_reg<RegPlan90>() != GSDR_OK) return GSDR_E_DEVICE;                           \
-            if (ID == 91 && setup_reg<RegPlan91>() != GSDR_OK) return GSDR_E_DEVICE;                           \
-            if (ID == 92 && setup_reg<RegPlan92>() != GSDR_OK) return GSDR_E_DEVICE;                           \
             if (ID == 93 && setup_reg<RegPlan93>() != GSDR_OK) return GSDR_E_DEVICE;                           \
-            if (ID == 94 && setup_reg<RegPlan94>() != GSDR_OK) return GSDR_E_DEVICE;                           \
             a->corr_variant = ID;                                                                               \
             a->corr_stat = ST;                                                                                  \
             a->tw_entries = M::tw_entries();                                                                    \

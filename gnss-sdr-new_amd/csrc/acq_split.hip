@@ -1,0 +1,112 @@
+// Split register four-step correlate (acq_correlate_split_kernel, acq_impl.h) for
+// the FFT sizes of configs C4 / C5 beyond the LDS engine: plan choice, launch and
+// one-time setup, selected by gsdr_acq::split.
+#include "acq_impl.h"
+
+namespace gsdr_acq_impl
+{
+
+// Inner M-point register four-step plans (RegFourStep<R, NT, H, WPE, pads, row radices>):
+//   25000 = 25 x (10 x 10 x 10): 512 lanes, two columns per lane (50 complex in
+//           VGPRs), 5 rows of 1000 per LDS round (40 KB)
+//   32000 = 32 x (10 x 10 x 10): 1024 lanes, one column per lane (32 complex),
+//           8 rows per LDS round (64 KB)
+using Reg25k = RegFourStep<25, 512, 5, 1, NoPads<1000>, 10, 10, 10>;
+using Reg32k = RegFourStep<32, 1024, 8, 1, NoPads<1000>, 10, 10, 10>;
+
+// split ids: (N, outer radix ROUT, inner plan)
+//   1: 25000 = 1 x 25000 (C5 GPS L1 / BeiDou B1I at 25 Msps, 1 ms)
+//   2: 32000 = 1 x 32000 (Galileo E1 at 8 Msps, 4 ms)
+//   3: 64000 = 2 x 32000 (C4: Galileo E1 at 8 Msps with bit transition)
+//   4: 100000 = 4 x 25000 (C5 Galileo E1 at 25 Msps, 4 ms)
+namespace
+{
+struct SplitId
+{
+    int id;
+    uint32_t n;
+};
+constexpr SplitId kSplits[] = {{1, 25000}, {2, 32000}, {3, 64000}, {4, 100000}};
+
+// PRN group of an XCD pass: the largest divisor of P whose code rows fit in ~2 MB
+// (half an XCD's L2), so the rows of the group's codes stay resident while the X
+// rows stream past
+uint32_t prn_group(uint32_t P, uint32_t N)
+{
+    const size_t row = (size_t)N * sizeof(float2);
+    uint32_t best = 1;
+    for (uint32_t g = 1; g <= P; ++g)
+        if (P % g == 0 && (size_t)g * row <= (2u << 20)) best = g;
+    return best;
+}
+
+template <int ROUT, class RP, bool HALF>
+int launch_one(gsdr_acq* a, uint32_t nblocks, hipStream_t s)
+{
+    static_assert(RP::N * ROUT > 0, "plan");
+    if (RP::N * ROUT != (int)a->N)
+        {
+            gsdr::set_error("internal: split plan for N = %d, handle N = %u", RP::N * ROUT, a->N);
+            return GSDR_E_STATE;
+        }
+    if (ROUT > 1)
+        GSDR_HIP(hipMemsetAsync(a->d_stats, 0, (size_t)nblocks * a->nprn * a->D * sizeof(RowStat), s));
+    const uint32_t grid = nblocks * a->D * a->nprn * ROUT;
+    hipLaunchKernelGGL((acq_correlate_split_kernel<ROUT, RP, HALF>), dim3(grid), dim3(RP::NT), RP::lds_bytes(), s,
+        a->d_X, a->d_code_fft, a->d_stats, a->d_tw, a->D, a->nprn, nblocks, prn_group(a->nprn, a->N));
+    GSDR_HIP(hipGetLastError());
+    return GSDR_OK;
+}
+
+template <int ROUT, class RP, bool HALF>
+int attrs_one()
+{
+    GSDR_HIP(hipFuncSetAttribute((const void*)acq_correlate_split_kernel<ROUT, RP, HALF>,
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)RP::lds_bytes()));
+    return GSDR_OK;
+}
+}  // namespace
+
+int launch_split(gsdr_acq* a, uint32_t nblocks, hipStream_t s)
+{
+    const bool half = a->eff != a->N;
+    switch (a->split)
+        {
+        case 1: return half ? launch_one<1, Reg25k, true>(a, nblocks, s) : launch_one<1, Reg25k, false>(a, nblocks, s);
+        case 2: return half ? launch_one<1, Reg32k, true>(a, nblocks, s) : launch_one<1, Reg32k, false>(a, nblocks, s);
+        case 3: return half ? launch_one<2, Reg32k, true>(a, nblocks, s) : launch_one<2, Reg32k, false>(a, nblocks, s);
+        case 4: return half ? launch_one<4, Reg25k, true>(a, nblocks, s) : launch_one<4, Reg25k, false>(a, nblocks, s);
+        default: gsdr::set_error("internal: bad split variant %d", a->split); return GSDR_E_STATE;
+        }
+}
+
+// Select the split correlate for a single-dwell four-step handle (K = 1, with or
+// without bit transition).  Default: the ROUT = 1 splits (N = 25000 / 32000); the
+// ROUT > 1 ones (64000, 100000) measured slower than the packed four-step -- every
+// sub-transform re-reads the whole X and code rows -- and run only
+// with GSDR_ACQ_SPLIT=2.  GSDR_ACQ_SPLIT=0 keeps the packed four-step everywhere.
+int setup_split(gsdr_acq* a)
+{
+    a->split = 0;
+    if (a->K != 1) return GSDR_OK;  // non-coherent dwells: the accumulating general path
+    int mode = 1;
+    if (const char* e = std::getenv("GSDR_ACQ_SPLIT")) mode = std::atoi(e);
+    if (mode == 0) return GSDR_OK;
+    for (const SplitId& sp : kSplits)
+        if (sp.n == a->N) a->split = sp.id;
+    if (a->split >= 3 && mode < 2) a->split = 0;
+    if (!a->split) return GSDR_OK;
+    int rc = GSDR_OK;
+    switch (a->split)
+        {
+        case 1: rc = attrs_one<1, Reg25k, true>() | attrs_one<1, Reg25k, false>(); break;
+        case 2: rc = attrs_one<1, Reg32k, true>() | attrs_one<1, Reg32k, false>(); break;
+        case 3: rc = attrs_one<2, Reg32k, true>() | attrs_one<2, Reg32k, false>(); break;
+        case 4: rc = attrs_one<4, Reg25k, true>() | attrs_one<4, Reg25k, false>(); break;
+        default: break;
+        }
+    if (rc != GSDR_OK) a->split = 0;
+    return rc;
+}
+
+}  // namespace gsdr_acq_impl

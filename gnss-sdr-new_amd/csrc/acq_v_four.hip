@@ -27,7 +27,6 @@ int dispatch_four(gsdr_acq* a, int op, const void* iq, uint32_t nblocks, uint64_
             GSDR_CASE(25, (gsdr::fft::FourStepPkPlan<16, gsdr::pk::PkPlan<256, 1, 25, 16, 10>>))
             GSDR_CASE(26, (gsdr::fft::FourStepPkPlan<25, gsdr::pk::PkPlan<256, 1, 25, 16, 10>>))
             GSDR_CASE(27, (gsdr::fft::FourStepPkPlan<5, gsdr::pk::PkPlan<256, 1, 25, 20, 10>>))
-            GSDR_CASE(28, (gsdr::fft::FourStepPkPlan<16, gsdr::pk::PkPlan<256, 1, 25, 16, 10>, false>))
         default: gsdr::set_error("internal: bad FFT variant %d", a->variant); return GSDR_E_STATE;
         }
 #undef GSDR_CASE

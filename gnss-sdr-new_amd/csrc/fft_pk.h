@@ -241,6 +241,10 @@ template <>
 struct Dft<25> : DftCT<5, 5>
 {
 };
+template <>
+struct Dft<32> : DftCT<4, 8>
+{
+};
 
 // ---- per-stage twiddle table (TWP == 2) ----
 // Row length for a radix-R stage: the R-1 roots, padded to an even count.

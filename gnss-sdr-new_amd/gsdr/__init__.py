@@ -542,6 +542,13 @@ class Tracking:
         _check(load().gsdr_trk_run_stream(self._h, ring._h, int(max_epochs), ctypes.c_void_p(out_dev_ptr),
                                           ctypes.c_void_p(nout_dev_ptr), ctypes.c_void_p(stream_ptr)))
 
+    def run_stream_host(self, ring, max_epochs):
+        """gsdr_trk_run_stream_host: synchronous ring form -> (records, counts) on the host."""
+        out = np.zeros(self.max_channels * max_epochs, TRK_EPOCH_DTYPE)
+        n = np.zeros(self.max_channels, np.uint32)
+        _check(load().gsdr_trk_run_stream_host(self._h, ring._h, int(max_epochs), _ptr(out), _ptr(n)))
+        return out.reshape(self.max_channels, max_epochs), n
+
     def channel(self, ch):
         st, nxt, dop, cn0 = ctypes.c_int32(), ctypes.c_uint64(), ctypes.c_double(), ctypes.c_double()
         _check(load().gsdr_trk_get_channel(self._h, int(ch), ctypes.byref(st), ctypes.byref(nxt), ctypes.byref(dop),

@@ -179,6 +179,14 @@ def main():
         emit("C4", "acquisition 36 PRN x %d Doppler, bit transition, FFT %d" % (acq.num_doppler_bins, acq.fft_size),
              fs, B * 2 * N, sec, acq_roofline(2 * N, 36, acq.num_doppler_bins, B, sec))
         acq.close()
+        # the same grid without bit transition: one 4 ms code period, FFT 32000
+        acq = gsdr.Acquisition(fs, N, 5000, 125, pfa=0.0, max_prns=36, max_blocks=B, sampled_ms=4, ms_per_code=4)
+        acq.set_local_codes(codes[:, :N], np.arange(1, 37))
+        acq.set_threshold(2.5)
+        sec = timed(lambda: acq.run_device(iq_dev.data_ptr(), B, N, 0, res.data_ptr()), max(2, a.reps // 3), 1, torch)
+        emit("C4", "acquisition 36 PRN x %d Doppler, 4 ms, FFT %d" % (acq.num_doppler_bins, acq.fft_size),
+             fs, B * N, sec, acq_roofline(N, 36, acq.num_doppler_bins, B, sec))
+        acq.close()
         del iq_dev
 
     if "C5" in todo:

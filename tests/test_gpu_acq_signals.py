@@ -82,12 +82,17 @@ def test_beidou_b1i_synthetic_batch(fs):
     assert set(vis) <= det
 
 
+@pytest.mark.parametrize("split", ["1", "0", "2"])
 @pytest.mark.parametrize("fs,N,pfa", [(8000000, 32000, 0.01), (25000000, 25000, 0.0), (8000000, 64000, 0.01),
-                                      (25000000, 100000, 0.01)])
-def test_large_fft_four_step(fs, N, pfa):
-    """N beyond one workgroup's LDS (four-step FFT, fft_4step.h): Galileo E1 at 8 Msps
-    (4 ms: 32000; 8 ms: 64000), BeiDou B1I at 25 Msps (1 ms: 25000), Galileo at
-    25 Msps (100000) -- configs C4/C5.  Parity with the oracle grid statistics."""
+                                      (25000000, 100000, 0.01), (25000000, 25000, 0.01), (25000000, 100000, 0.0)])
+def test_large_fft_four_step(monkeypatch, fs, N, pfa, split):
+    """N beyond one workgroup's LDS: Galileo E1 at 8 Msps (4 ms: 32000; 8 ms:
+    64000), BeiDou B1I at 25 Msps (1 ms: 25000), Galileo at 25 Msps (100000) --
+    configs C4/C5 -- on every correlate path: GSDR_ACQ_SPLIT=1 (default: the split
+    register four-step for 25000 / 32000, the packed four-step for 64000 / 100000),
+    0 (the packed four-step everywhere), 2 (the split also with ROUT = 2 / 4).
+    Parity with the oracle grid statistics."""
+    monkeypatch.setenv("GSDR_ACQ_SPLIT", split)
     dmax, dstep = 2000, 500
     rng = np.random.default_rng(N)
     if N == 25000:

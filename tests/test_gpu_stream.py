@@ -113,3 +113,80 @@ def test_ring_errors():
     with pytest.raises(gsdr.GsdrError):
         acq.run_stream(ring, 1000 + 5 * N, 1)  # item type mismatch
     ring.close()
+
+
+def test_stalled_channel_reports_overrun():
+    """A channel whose next call starts before the oldest item the ring still
+    holds cannot continue: one record with LOSS_OF_LOCK | OVERRUN (event 3, the
+    channel FSM re-acquires) and the channel in state 0, instead of a silent stall."""
+    sats = synth.random_constellation(2, seed_offset=23)
+    x = synth.gps_l1_iq(FS, 40 * N, sats, seed_offset=23)
+    t = gsdr.Tracking(_conf(2))
+    for c, s in enumerate(sats):
+        d, f = _acq_result(s)
+        t.start(c, s.prn, synth.gps_ca_chips(s.prn), d, f, 0, 0)
+    ring = gsdr.Stream(gsdr.ITEM_GR_COMPLEX, capacity_items=8 * N, max_window_items=4 * N)
+    pushed = 0
+    while pushed < 40 * N:  # channels never run: the ring moves 32 ms past them
+        ring.push(x[pushed:pushed + 2 * N], pushed)
+        pushed += 2 * N
+    rec, n = t.run_stream_host(ring, 16)
+    for c in range(2):
+        assert n[c] == 1, (c, n[c])
+        assert rec[c, 0]["flags"] == gsdr.TRK_F_LOSS_OF_LOCK | gsdr.TRK_F_OVERRUN
+        assert t.channel(c)["state"] == 0
+    rec, n = t.run_stream_host(ring, 16)
+    assert list(n) == [0, 0]
+    ring.close()
+
+
+def test_two_thread_push_and_consume():
+    """GNU Radio deployment shape: a producer thread pushes while the consumer
+    thread runs ring acquisitions and tracking; the ring lock held from window
+    to reader event keeps every read identical to the contiguous-buffer result."""
+    import threading
+    ms = 96
+    sats = synth.random_constellation(4, seed_offset=29)
+    x = synth.gps_l1_iq(FS, ms * N, sats, seed_offset=29)
+    codes = np.stack([synth.gps_ca_sampled(s.prn, FS) for s in sats])
+    prns = np.array([s.prn for s in sats])
+    acq = gsdr.Acquisition(FS, N, 10000, 250, pfa=0.01, max_prns=len(prns))
+    acq.set_local_codes(codes, prns)
+    ref_acq = acq.run(x, 1, stamp0=0)  # warm
+    ring = gsdr.Stream(gsdr.ITEM_GR_COMPLEX, capacity_items=12 * N, max_window_items=4 * N)
+    pushed = [0]
+    cv = threading.Condition()
+    stop = [False]
+
+    def producer():
+        while pushed[0] < ms * N:
+            n = 1000
+            with cv:
+                # bounded lead over the consumer so the blocks it asks for are still held
+                while pushed[0] - done[0] * N > 6 * N and not stop[0]:
+                    cv.wait(0.05)
+            ring.push(x[pushed[0]:pushed[0] + n], pushed[0])
+            with cv:
+                pushed[0] += n
+                cv.notify_all()
+
+    done = [0]
+    th = threading.Thread(target=producer)
+    th.start()
+    try:
+        while done[0] < ms:
+            b = done[0]
+            with cv:
+                while pushed[0] < (b + 1) * N:
+                    cv.wait(0.05)
+            r_ring = acq.run_stream(ring, b * N, 1, stamp0=b * N)
+            r_host = acq.run(x[b * N:(b + 1) * N], 1, stamp0=b * N)
+            assert r_ring.tobytes() == r_host.tobytes(), b
+            with cv:
+                done[0] += 1
+                cv.notify_all()
+    finally:
+        stop[0] = True
+        th.join()
+    assert ref_acq.shape == (1, len(prns))
+    ring.close()

@@ -148,3 +148,72 @@ def test_two_rank_gloo_matches_single_process():
     for a, b in zip(merged_trk, single_trk):
         assert a.shape == (TRK_EPOCHS, 6)
         np.testing.assert_array_equal(a, b)
+
+
+def _c5_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import bench
+        plan = bench.c5_rank_plan(world, rank, 8)
+        plans = [None] * world
+        dist.all_gather_object(plans, plan)
+        dist.barrier()
+        t = torch.tensor([0.5 + rank], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        if rank == 0:
+            q.put((plans, float(t.item())))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_c5_plan_tiles_the_job():
+    """bench.py --workload c5 (BASELINE C5: 256 hybrid channels over the node's
+    GPUs): at every world size the ranks' block spans tile the stream, the 256
+    channels land once each on rank c % world in three signal pools, each rank's
+    acquisition grids cover its span (GPS / BeiDou on alternate ms, Galileo per
+    4 ms group), and the per-rank work stays constant (weak scaling)."""
+    import bench
+    work = set()
+    for world in (1, 2, 4, 8):
+        plans = [bench.c5_rank_plan(world, r, 8) for r in range(world)]
+        spans = [p["blocks"] for p in plans]
+        assert spans[0][0] == 0 and spans[-1][1] == 8 * world
+        assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
+        chans = sorted(sum((p["channels"] for p in plans), []))
+        assert chans == list(range(256))
+        for r, p in enumerate(plans):
+            assert all(c % world == r for c in p["channels"])
+            assert sorted(sum(p["pools"].values(), [])) == p["channels"]
+            lo, hi = p["blocks"]
+            a = p["acq"]
+            assert sorted(a["gps_blocks"] + a["bds_blocks"]) == list(range(lo, hi))
+            assert [g for g in a["gal_groups"]] == list(range(lo, hi, 4))
+            # per-rank work: grids, channel-milliseconds of tracking
+            work.add((len(a["gps_blocks"]), len(a["bds_blocks"]), len(a["gal_groups"]),
+                      len(p["channels"]) * p["total_blocks"]))
+        if world == 8:
+            assert all([len(p["pools"][s]) for s in (0, 1, 2)] == [12, 12, 8] for p in plans)
+    assert len(work) == 1
+    with pytest.raises(ValueError):
+        bench.c5_rank_plan(2, 0, 6)
+
+
+def test_c5_plan_two_rank_gloo():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    os.environ["PYTHONPATH"] = os.pathsep.join([here, root, os.path.join(root, "gnss-sdr-new_amd"),
+                                                os.environ.get("PYTHONPATH", "")])
+    port = _free_port()
+    procs = [ctx.Process(target=_c5_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    plans, tmax = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert tmax == 1.5
+    assert sorted(plans[0]["channels"] + plans[1]["channels"]) == list(range(256))
+    assert plans[0]["blocks"] == (0, 8) and plans[1]["blocks"] == (8, 16)

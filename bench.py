@@ -11,8 +11,8 @@ One step = one batch of B consecutive 1 ms blocks of synthetic GPS L1 C/A IQ at
     device-resident (gsdr_trk_run_device), the channel state restored to the same
     start each step so every step re-tracks the same 64 ms.
 Acquisition and tracking run on separate HIP streams (they are independent work):
-the acquisition blocks of a step are split over two handles (--acq-chains 2), so one
-chain's forward-spectra kernel overlaps the other's correlate grid.
+the acquisition blocks of a step are split over two handles (--acq-chains 2), each
+on its own stream.
 Whole-job throughput = blocks * 4000 samples * ranks / max-over-ranks wall time.
 
 Multi-GPU: one process per GPU (torch.distributed.run); every rank processes its
@@ -160,15 +160,17 @@ def host_cpu_info():
     aff = len(os.sched_getaffinity(0))
     cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
     threads = min(aff, cap) if cap > 0 else aff
-    model = "unknown"
+    model, cores = "unknown", None
     try:
         for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
+            if line.startswith("model name") and model == "unknown":
                 model = line.split(":", 1)[1].strip()
-                break
-    except OSError:
+            if line.startswith("cpu cores") and cores is None:
+                cores = int(line.split(":", 1)[1])
+    except (OSError, ValueError):
         pass
-    return {"nproc": os.cpu_count(), "affinity": aff, "threads": threads, "cpu_model": model}
+    return {"nproc": os.cpu_count(), "affinity": aff, "threads": threads, "cpu_model": model,
+            "cores_per_socket": cores}
 
 
 def cpu_baseline(iq, codes, sats, budget_s=12.0):
@@ -220,7 +222,12 @@ def cpu_baseline(iq, codes, sats, budget_s=12.0):
         L.cpub_trk_calls(handles, len(chans), iq2.ctypes.data, rel.ctypes.data, absn.ctypes.data, nt, recs.ctypes.data)
         pos[:] += recs["consumed"].astype(np.int64)
 
-    one_block(0)
+    # warm-up (thread pool, first touch, clocks), then size the sample from one block
+    tw = time.perf_counter()
+    nw = 0
+    while time.perf_counter() - tw < 1.0 or nw < 2:
+        one_block(nw)
+        nw += 1
     t0 = time.perf_counter()
     one_block(1)
     t1 = time.perf_counter() - t0
@@ -229,6 +236,19 @@ def cpu_baseline(iq, codes, sats, budget_s=12.0):
     for b in range(2, nblk + 2):
         one_block(b)
     dt = time.perf_counter() - t0
+    # thread scaling inside the job's CPU share (short samples): how far the
+    # measured figure is from a whole socket
+    scaling = {}
+    for tt in sorted({1, max(1, nt // 4), max(1, nt // 2), nt}):
+        nt_saved = nt
+        nt = tt
+        tb = time.perf_counter()
+        nb = 0
+        while time.perf_counter() - tb < 1.5 or nb < 2:
+            one_block(nblk + 2 + nb)
+            nb += 1
+        scaling[tt] = round(nb * N / (time.perf_counter() - tb) / 1e6, 4)
+        nt = nt_saved
     detected = int(np.sum(out[:, 4] > 0))
     L.cpub_acq_destroy(h)
     # per-core correlator rate (1 thread, N = 4000, K = 3, L = 1023)
@@ -242,7 +262,14 @@ def cpu_baseline(iq, codes, sats, budget_s=12.0):
         L.cpub_corr(o6.ctypes.data, sig.ctypes.data, code.ctypes.data, 1023, shifts.ctypes.data, 3, 0.3, 0.01, 0.1,
                     float(np.float32(1.023e6 / FS)), N)
     corr_rate = reps * N / (time.perf_counter() - tc) / 1e6
-    return {"value": round(nblk * N / dt / 1e6, 4), "unit": "Msamples/s", "cores": nt, "kind": "port",
+    value = nblk * N / dt / 1e6
+    socket_cores = info.get("cores_per_socket") or nt
+    return {"value": round(value, 4), "unit": "Msamples/s", "cores": nt, "kind": "port",
+            "thread_scaling_msps": scaling,
+            "full_socket_estimate": {"value": round(value * socket_cores / nt, 3), "cores": socket_cores,
+                                     "basis": "the measured rate per thread x the socket's cores (linear; the job's "
+                                              "CPU share is %d threads, thread_scaling_msps shows the scaling inside "
+                                              "it); an estimate, not a measurement" % nt},
             "sample": "%d blocks of 1 ms (4000 samples) in %.1f s: 32 PRN x 81 Doppler CFAR PCPS per block "
                       "(oracle/cpu_baseline.cc: own 8-lane AVX2 mixed-radix FFT, no FFTW3f/pocketfft on the image) "
                       "+ one dll_pll_veml_tracking call for each of 8 channels (fused AVX2 correlator + DLL/PLL "
@@ -632,13 +659,14 @@ def main():
         if nrec.min() > 0:
             dop_err = np.array([abs(np.mean(recs[i][max(nrec[i] - 16, 0):nrec[i]]["carrier_doppler_hz"]) -
                                     sats[c].doppler_hz) for i, c in enumerate(my_ch)])
-    stage_ms, stage_n = (np.zeros(4), np.zeros(4, np.uint32))
+    stage_ms, stage_n, stage_busy = (np.zeros(4), np.zeros(4, np.uint32), np.zeros(4))
     trk_ms, trk_launches = 0.0, 0
     if not args.no_profile_events:
         for a in acqs:
-            ms_a, n_a = a.read_profile()
+            ms_a, n_a, busy_a = a.read_profile_ex()
             stage_ms = stage_ms + ms_a
             stage_n = stage_n + n_a
+            stage_busy = stage_busy + busy_a
         if trk is not None:
             trk_ms, trk_launches = trk.read_profile()
 
@@ -678,36 +706,51 @@ def main():
     if args.only:
         line["diagnostic_only_stage"] = args.only
     if not args.no_profile_events and stage_n[1] > 0:
-        # the batch runs as interleaved chains (gsdr_acq split), so a step holds
-        # stage_n / steps launches of each stage, each over B * steps / stage_n blocks
+        # a step holds stage_n / steps correlate launches (one per chain), each over
+        # B * steps / stage_n blocks.  The chains' launches run concurrently on
+        # their streams and share the chip, so a launch's duration counts the time
+        # it shares with the other chain; the kernel's wall time is the union of the
+        # launch intervals (busy time; per handle from gsdr_acq_read_profile_ex, and
+        # for nch lock-stepped chains the launch time x launches / nch).
         corr_launch_s = stage_ms[1] / stage_n[1] / 1e3
         blocks_per_launch = B * args.steps / stage_n[1]
-        # the nch chains' correlate launches run concurrently (one per stream, same
-        # duration): the chip's correlate throughput is nch launches per launch time
-        achieved = correlate_kernel_bytes_per_block() * blocks_per_launch * nch / corr_launch_s
+        corr_busy_s = stage_busy[1] / 1e3 if nch == 1 else corr_launch_s * stage_n[1] / nch
+        blocks_timed = B * args.steps
+        achieved = correlate_kernel_bytes_per_block() * blocks_timed / corr_busy_s
         pmc = load_pmc_traffic()
         traffic = None
-        if pmc and pmc.get("kernel") == "acq_correlate_kernel" and pmc.get("blocks") and pmc.get("hbm_bytes_per_launch"):
-            # PMC HBM bytes of one launch over pmc["blocks"] blocks, per block x this launch's blocks
-            traffic = pmc.get("hbm_bytes_per_launch") / pmc["blocks"] * blocks_per_launch
+        kc_pmc = (pmc or {}).get("kernels", {}).get("acq_correlate_kernel", {})
+        if pmc and pmc.get("blocks") and kc_pmc.get("hbm_bytes_per_launch"):
+            # PMC HBM bytes per block (FETCH_SIZE x 2 + WRITE_SIZE, gfx950 correction) x this launch's blocks
+            traffic = kc_pmc["hbm_bytes_per_launch"] / pmc["blocks"] * blocks_per_launch
         # The correlate kernel is not HBM bound: its spectra come from HBM once and
         # are re-served from L2 / the Infinity Cache to the 32 PRN workgroups (PMC
         # traffic below); its time is VALU issue (packed-f32 butterflies) plus the
         # LDS round trips and barriers between stages.  The roofline
         # is therefore the FP32 vector peak with the nominal FFT flops; the
         # logical-byte HBM figure and this box's achievable copy rate are kept alongside.
-        flops = correlate_kernel_flops_per_block() * blocks_per_launch * nch / corr_launch_s
+        flops = correlate_kernel_flops_per_block() * blocks_timed / corr_busy_s
         line["roofline"] = {
             "bound": "valu", "achieved": round(flops / 1e12, 2), "peak": FP32_PEAK / 1e12, "unit": "TFLOP/s",
             "frac": round(flops / FP32_PEAK, 4), "traffic": traffic,
+            "traffic_source": (pmc or {}).get("file"),
             "kernel": "acq_correlate_pk_kernel", "avg_launch_us": round(corr_launch_s * 1e6, 2),
-            "blocks_per_launch": blocks_per_launch, "concurrent_launches": nch,
+            "busy_us_per_step": round(corr_busy_s / args.steps * 1e6, 2),
+            "blocks_per_launch": blocks_per_launch,
+            "launch_overlap": round(corr_launch_s * stage_n[1] / corr_busy_s, 3),
             "nominal_flops_per_launch": int(correlate_kernel_flops_per_block() * blocks_per_launch),
             "hbm_logical": {"achieved": round(achieved / 1e9, 2), "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                             "achievable_copy": round(achievable_hbm_gbps(torch, dev), 1),
                             "frac": round(achieved / HBM_PEAK, 4),
                             "algorithmic_bytes_per_launch": int(correlate_kernel_bytes_per_block() * blocks_per_launch)},
         }
+        if traffic:
+            # the metric's "% HBM roofline" as measured: the PMC's HBM bytes of the
+            # correlate grid over its busy time, against the 8 TB/s peak
+            meas = traffic * stage_n[1] / corr_busy_s
+            line["roofline"]["hbm_measured"] = {"achieved": round(meas / 1e9, 2), "peak": HBM_PEAK / 1e9,
+                                                "unit": "GB/s", "frac": round(meas / HBM_PEAK, 4),
+                                                "bytes_per_launch": round(traffic)}
         if pmc:
             kc = pmc.get("kernels", {}).get("acq_correlate_kernel", {}).get("counters", {})
             if kc.get("SQ_INSTS_VALU") and pmc.get("blocks"):

@@ -16,6 +16,9 @@
 //   K_second          per (b,p), peak-ratio mode only: recompute row d*, second peak outside
 //                     the +-1 chip window with the reference's wrap      (:546-612)
 #include "acq_impl.h"
+
+#include <algorithm>
+#include <utility>
 #include "gsdr_stream_internal.h"
 
 namespace
@@ -370,6 +373,7 @@ int gsdr_acq_run_device(gsdr_acq* a, const void* iq_dev, uint32_t nblocks, uint6
         nblocks, a->conf.max_blocks);
     GSDR_REQUIRE(stride >= a->consumed || nblocks == 1, GSDR_E_ARG, "gsdr_acq_run_device: block stride %llu < consumed %u",
         (unsigned long long)stride, a->consumed);
+    std::lock_guard<std::mutex> lk(a->mu);
     gsdr::DeviceGuard g(a->device);
     hipStream_t s = stream ? (hipStream_t)stream : a->stream;
     return dispatch(a, 0, iq_dev, nblocks, stride, stamp0, out_dev, s, 0);
@@ -601,7 +605,7 @@ int gsdr_acq_set_profiling(gsdr_acq* a, int enable)
     return GSDR_OK;
 }
 
-int gsdr_acq_read_profile(gsdr_acq* a, double* stage_ms, uint32_t* launches)
+int gsdr_acq_read_profile_ex(gsdr_acq* a, double* stage_ms, uint32_t* launches, double* stage_busy_ms)
 {
     GSDR_REQUIRE(a && stage_ms && launches, GSDR_E_ARG, "gsdr_acq_read_profile: null argument");
     std::lock_guard<std::mutex> lk(a->mu);
@@ -610,19 +614,55 @@ int gsdr_acq_read_profile(gsdr_acq* a, double* stage_ms, uint32_t* launches)
         {
             stage_ms[i] = 0.0;
             launches[i] = 0;
+            if (stage_busy_ms) stage_busy_ms[i] = 0.0;
         }
+    // per launch: duration, and [start, end) against the first record's start event
+    std::vector<std::pair<double, double>> iv[4];
+    hipEvent_t ref = a->prof_recs.empty() ? nullptr : a->prof_recs.front().a;
     for (auto& r : a->prof_recs)
         {
             GSDR_HIP(hipEventSynchronize(r.b));
-            float ms = 0.0f;
+            float ms = 0.0f, t0 = 0.0f, t1 = 0.0f;
             GSDR_HIP(hipEventElapsedTime(&ms, r.a, r.b));
+            GSDR_HIP(hipEventElapsedTime(&t0, ref, r.a));
+            GSDR_HIP(hipEventElapsedTime(&t1, ref, r.b));
             stage_ms[r.stage] += ms;
             launches[r.stage] += 1;
+            iv[r.stage].emplace_back(t0, t1);
+        }
+    // busy time of a stage: the union of its launch intervals (launches of one stage
+    // overlap when runs of the handle are issued on several streams)
+    if (stage_busy_ms)
+        for (int i = 0; i < 4; ++i)
+            {
+                std::sort(iv[i].begin(), iv[i].end());
+                double busy = 0.0, lo = 0.0, hi = -1e300;
+                for (const auto& x : iv[i])
+                    {
+                        if (x.first > hi)
+                            {
+                                if (hi > lo) busy += hi - lo;
+                                lo = x.first;
+                                hi = x.second;
+                            }
+                        else if (x.second > hi)
+                            hi = x.second;
+                    }
+                if (hi > lo) busy += hi - lo;
+                stage_busy_ms[i] = busy;
+            }
+    for (auto& r : a->prof_recs)
+        {
             a->prof_pool.push_back(r.a);
             a->prof_pool.push_back(r.b);
         }
     a->prof_recs.clear();
     return GSDR_OK;
+}
+
+int gsdr_acq_read_profile(gsdr_acq* a, double* stage_ms, uint32_t* launches)
+{
+    return gsdr_acq_read_profile_ex(a, stage_ms, launches, nullptr);
 }
 
 }  // extern "C"

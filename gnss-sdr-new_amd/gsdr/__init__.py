@@ -42,7 +42,7 @@ EXPORTED = [
     "gsdr_acq_run_dwell", "gsdr_acq_run_stream", "gsdr_trk_run_stream", "gsdr_trk_run_stream_host",
     "gsdr_stream_create", "gsdr_stream_destroy", "gsdr_stream_push", "gsdr_stream_span", "gsdr_stream_window",
     "gsdr_acq_set_step_two", "gsdr_acq_get_step_two_threshold", "gsdr_acq_run_step_two",
-    "gsdr_trk_set_data_code", "gsdr_stream_window_async", "gsdr_stream_release", "gsdr_stream_device",
+    "gsdr_trk_set_data_code", "gsdr_acq_read_profile_ex", "gsdr_stream_window_async", "gsdr_stream_release", "gsdr_stream_device",
 ]
 
 SIGNAL_GPS_1C = 0
@@ -219,6 +219,7 @@ def load():
     L.gsdr_stream_push.argtypes = [P, P, U64, U64]
     L.gsdr_stream_span.argtypes = [P, P, P]
     L.gsdr_stream_window.argtypes = [P, U64, U64, P]
+    L.gsdr_acq_read_profile_ex.argtypes = [P, P, P, P]
     L.gsdr_stream_window_async.argtypes = [P, U64, U64, P, P]
     L.gsdr_stream_release.argtypes = [P, P]
     L.gsdr_stream_device.argtypes = [P, P]
@@ -382,6 +383,14 @@ class Acquisition:
         n = np.zeros(4, np.uint32)
         _check(load().gsdr_acq_read_profile(self._h, _ptr(ms), _ptr(n)))
         return ms, n
+
+    def read_profile_ex(self):
+        """(stage_ms[4], launches[4], busy_ms[4]): busy = union of the stage's launch intervals."""
+        ms = np.zeros(4, np.float64)
+        n = np.zeros(4, np.uint32)
+        busy = np.zeros(4, np.float64)
+        _check(load().gsdr_acq_read_profile_ex(self._h, _ptr(ms), _ptr(n), _ptr(busy)))
+        return ms, n, busy
 
     def dump_grid(self, iq, prn_slot):
         iq = self._items(iq)

@@ -2,7 +2,15 @@
 
 #include <iostream>
 
+#include "gnss_sdr_flags.h"
+
+// dll_pll_conf.cc:24-28: the lock-detector defaults come from the gflags
 Dll_Pll_Conf::Dll_Pll_Conf()
+    : carrier_lock_th(FLAGS_carrier_lock_th),
+      cn0_samples(FLAGS_cn0_samples),
+      cn0_min(FLAGS_cn0_min),
+      max_code_lock_fail(FLAGS_max_lock_fail),
+      max_carrier_lock_fail(FLAGS_max_carrier_lock_fail)
 {
     signal[0] = '1';
     signal[1] = 'C';
@@ -22,9 +30,11 @@ void Dll_Pll_Conf::SetFromConfiguration(const ConfigurationInterface* configurat
     high_dyn = configuration->property(role + ".high_dyn", high_dyn);
     dump = configuration->property(role + ".dump", dump);
     pll_bw_hz = configuration->property(role + ".pll_bw_hz", pll_bw_hz);
+    if (FLAGS_pll_bw_hz != 0.0) pll_bw_hz = static_cast<float>(FLAGS_pll_bw_hz);  // :53-56
     pll_bw_narrow_hz = configuration->property(role + ".pll_bw_narrow_hz", pll_bw_narrow_hz);
     dll_bw_narrow_hz = configuration->property(role + ".dll_bw_narrow_hz", dll_bw_narrow_hz);
     dll_bw_hz = configuration->property(role + ".dll_bw_hz", dll_bw_hz);
+    if (FLAGS_dll_bw_hz != 0.0) dll_bw_hz = static_cast<float>(FLAGS_dll_bw_hz);  // :60-63
     dll_filter_order = configuration->property(role + ".dll_filter_order", dll_filter_order);
     pll_filter_order = configuration->property(role + ".pll_filter_order", pll_filter_order);
     if (dll_filter_order < 1) dll_filter_order = 1;

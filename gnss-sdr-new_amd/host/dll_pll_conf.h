@@ -1,8 +1,9 @@
 // Dll_Pll_Conf mirror (src/algorithms/tracking/libs/dll_pll_conf.h:30-84,
 // dll_pll_conf.cc:20-126): the Tracking_XX.* keys that drive dll_pll_veml_tracking,
-// with the reference defaults (incl. the gflags defaults gnss_sdr_flags.cc:45-54
-// for cn0_samples, cn0_min, max_lock_fail, max_carrier_lock_fail, carrier_lock_th),
-// and the mapping onto the engine's gsdr_trk_conf.
+// with the reference defaults: cn0_samples, cn0_min, max_lock_fail,
+// max_carrier_lock_fail and carrier_lock_th taken from the gflags at construction
+// (dll_pll_conf.cc:24-28, gnss_sdr_flags.h), --pll_bw_hz / --dll_bw_hz overriding
+// the .conf (:53-63); and the mapping onto the engine's gsdr_trk_conf.
 #ifndef GSDR_HOST_DLL_PLL_CONF_H
 #define GSDR_HOST_DLL_PLL_CONF_H
 

@@ -15,35 +15,36 @@
 #include "dll_pll_conf.h"
 #include "gnss_synchro.h"
 #include "gsdr.h"
+#include "tracking_block_mi355x.h"
 
-class dll_pll_veml_tracking_mi355x
+class dll_pll_veml_tracking_mi355x : public TrackingBlockMI355X
 {
 public:
     // signal: GSDR_SIGNAL_GPS_1C / GSDR_SIGNAL_GAL_1B / GSDR_SIGNAL_BDS_B1
     dll_pll_veml_tracking_mi355x(const Dll_Pll_Conf& conf, int32_t signal, int device = 0);
-    ~dll_pll_veml_tracking_mi355x();
+    ~dll_pll_veml_tracking_mi355x() override;
     dll_pll_veml_tracking_mi355x(const dll_pll_veml_tracking_mi355x&) = delete;
     dll_pll_veml_tracking_mi355x& operator=(const dll_pll_veml_tracking_mi355x&) = delete;
 
-    void set_gnss_synchro(Gnss_Synchro* p_gnss_synchro);
-    void set_channel(uint32_t channel);
+    void set_gnss_synchro(Gnss_Synchro* p_gnss_synchro) override;
+    void set_channel(uint32_t channel) override;
     // start_tracking (:640-882): takes Acq_delay_samples / Acq_doppler_hz /
     // Acq_samplestamp_samples from the channel's Gnss_Synchro and the PRN's
     // replica; the pull-in (state 1) runs on the next work() call
-    void start_tracking();
-    void stop_tracking();
-    void set_event_handler(std::function<void(int)> h) { d_events = std::move(h); }
+    void start_tracking() override;
+    void stop_tracking() override;
+    void set_event_handler(std::function<void(int)> h) override { d_events = std::move(h); }
 
     // forecast (:604-611): items general_work needs
-    int forecast() const { return 2 * static_cast<int>(d_vector_length); }
+    int forecast() const override { return 2 * static_cast<int>(d_vector_length); }
     // general_work: `in` holds ninput_items items of the configured item type, the
     // first one being input sample nitems_read.  Returns the items consumed
     // (consume_each); *noutput = 1 with *out filled when a Gnss_Synchro is
     // emitted (valid symbol output or loss of lock), else 0.
-    int work(const void* in, int ninput_items, uint64_t nitems_read, Gnss_Synchro* out, int* noutput);
+    int work(const void* in, int ninput_items, uint64_t nitems_read, Gnss_Synchro* out, int* noutput) override;
 
-    int32_t state() const { return d_state; }
-    const gsdr_trk_epoch& last_record() const { return d_last; }
+    int32_t state() const override { return d_state; }
+    const gsdr_trk_epoch& last_record() const override { return d_last; }
 
 private:
     void load_codes(uint32_t prn, std::vector<float>& code);

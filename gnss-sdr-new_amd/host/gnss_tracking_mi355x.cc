@@ -13,10 +13,21 @@ constexpr double BEIDOU_B1I_CODE_RATE_CPS = 2.046e6;  // Beidou_B1I.h
 constexpr double BEIDOU_B1I_CODE_LENGTH_CHIPS = 2046.0;
 }  // namespace
 
-void DllPllTrackingAdapterMI355X::make_block(int32_t signal, int device)
+void DllPllTrackingAdapterMI355X::make_block(const ConfigurationInterface* configuration, int32_t signal, int device)
 {
     item_size_ = trk_params_.item_type == "cshort" ? 4 : (trk_params_.item_type == "cbyte" ? 2 : 8);
-    tracking_ = std::make_unique<dll_pll_veml_tracking_mi355x>(trk_params_, signal, device);
+    pooled_ = configuration->property(role_ + ".mi355x_pool", false);
+    if (!pooled_)
+        {
+            tracking_ = std::make_unique<dll_pll_veml_tracking_mi355x>(trk_params_, signal, device);
+            return;
+        }
+    // the role's suffix names the signal's channel count key (Tracking_1C -> Channels_1C.count)
+    const std::string sig = role_.size() >= 2 ? role_.substr(role_.size() - 2) : std::string("1C");
+    const int count = configuration->property("Channels_" + sig + ".count", 32);
+    const int slots = configuration->property(role_ + ".mi355x_pool_channels", count > 0 ? count : 32);
+    tracking_ = std::make_unique<dll_pll_veml_tracking_pool_mi355x>(trk_params_, signal,
+        static_cast<uint32_t>(slots > 0 ? slots : 32), device, role_);
 }
 
 // gps_l1_ca_dll_pll_tracking.cc:34-91
@@ -36,7 +47,7 @@ GpsL1CaDllPllTrackingMI355X::GpsL1CaDllPllTrackingMI355X(const ConfigurationInte
     trk_params_.system = 'G';
     trk_params_.signal[0] = '1';
     trk_params_.signal[1] = 'C';
-    make_block(GSDR_SIGNAL_GPS_1C, device);
+    make_block(configuration, GSDR_SIGNAL_GPS_1C, device);
 }
 
 // galileo_e1_dll_pll_veml_tracking.cc:34-75: extended integration only when
@@ -57,7 +68,7 @@ GalileoE1DllPllVemlTrackingMI355X::GalileoE1DllPllVemlTrackingMI355X(const Confi
     trk_params_.system = 'E';
     trk_params_.signal[0] = '1';
     trk_params_.signal[1] = 'B';
-    make_block(GSDR_SIGNAL_GAL_1B, device);
+    make_block(configuration, GSDR_SIGNAL_GAL_1B, device);
 }
 
 // beidou_b1i_dll_pll_tracking.cc:34-90
@@ -76,5 +87,5 @@ BeidouB1iDllPllTrackingMI355X::BeidouB1iDllPllTrackingMI355X(const Configuration
     trk_params_.system = 'C';
     trk_params_.signal[0] = 'B';
     trk_params_.signal[1] = '1';
-    make_block(GSDR_SIGNAL_BDS_B1, device);
+    make_block(configuration, GSDR_SIGNAL_BDS_B1, device);
 }

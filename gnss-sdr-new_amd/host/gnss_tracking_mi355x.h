@@ -6,7 +6,11 @@
 // Galileo_E1_DLL_PLL_VEML_Tracking_MI355X, BEIDOU_B1I_DLL_PLL_Tracking_MI355X.
 // Each builds Dll_Pll_Conf from the role, sets vector_length =
 // round(fs_in / (chip rate / code length)) and the signal's extend / pilot rules,
-// and owns a dll_pll_veml_tracking_mi355x block.
+// and owns a tracking block: dll_pll_veml_tracking_mi355x (one engine handle per
+// channel), or with <role>.mi355x_pool=true a dll_pll_veml_tracking_pool_mi355x
+// slot in the GPU's shared pool of that role (every channel of the signal on the
+// GPU in one engine handle over the device IQ ring; <role>.mi355x_pool_channels
+// slots, default Channels_<signal>.count).
 #ifndef GSDR_HOST_GNSS_TRACKING_MI355X_H
 #define GSDR_HOST_GNSS_TRACKING_MI355X_H
 
@@ -16,6 +20,8 @@
 #include "configuration.h"
 #include "dll_pll_conf.h"
 #include "dll_pll_veml_tracking_mi355x.h"
+#include "dll_pll_veml_tracking_pool_mi355x.h"
+#include "tracking_block_mi355x.h"
 #include "tracking_interface.h"
 
 class DllPllTrackingAdapterMI355X : public TrackingInterface
@@ -33,7 +39,8 @@ public:
         tracking_->set_channel(channel);
     }
     // the gr::block the reference connects (get_left_block / get_right_block)
-    dll_pll_veml_tracking_mi355x* get_block() { return tracking_.get(); }
+    TrackingBlockMI355X* get_block() { return tracking_.get(); }
+    bool pooled() const { return pooled_; }
     const Dll_Pll_Conf& conf() const { return trk_params_; }
 
 protected:
@@ -41,10 +48,11 @@ protected:
         : role_(role), implementation_(std::move(implementation))
     {
     }
-    void make_block(int32_t signal, int device);
+    void make_block(const ConfigurationInterface* configuration, int32_t signal, int device);
 
     Dll_Pll_Conf trk_params_;
-    std::unique_ptr<dll_pll_veml_tracking_mi355x> tracking_;
+    std::unique_ptr<TrackingBlockMI355X> tracking_;
+    bool pooled_{false};
     std::string role_;
     std::string implementation_;
     size_t item_size_{8};

@@ -3,12 +3,17 @@
 #include <algorithm>
 #include <cmath>
 
+#include "gnss_sdr_flags.h"
+
 PcpsAcquisitionAdapterMI355X::PcpsAcquisitionAdapterMI355X(const ConfigurationInterface* configuration,
     const std::string& role, uint32_t ms_per_code, double chip_rate, double code_length_chips, double opt_freq, int device)
     : configuration_(configuration), role_(role)
 {
     acq_parameters_.ms_per_code = ms_per_code;
     acq_parameters_.SetFromConfiguration(configuration, role, chip_rate, opt_freq);
+    // --doppler_max overrides the .conf (gps_l1_ca_pcps_acquisition.cc:57-60 and the
+    // Galileo / BeiDou adapters alike)
+    if (FLAGS_doppler_max != 0) acq_parameters_.doppler_max = FLAGS_doppler_max;
     doppler_max_ = static_cast<unsigned int>(acq_parameters_.doppler_max);
     doppler_step_ = static_cast<unsigned int>(acq_parameters_.doppler_step);
     code_length_ = static_cast<unsigned int>(
@@ -56,6 +61,14 @@ void PcpsAcquisitionAdapterMI355X::set_channel(unsigned int channel)
 {
     channel_ = channel;
     acquisition_->set_channel(channel_);
+}
+
+// set_channel_fsm (gps_l1_ca_pcps_acquisition.h:102-106 and the Galileo / BeiDou
+// adapters alike): stored, and forwarded to the block
+void PcpsAcquisitionAdapterMI355X::set_channel_fsm(std::weak_ptr<ChannelFsm> channel_fsm)
+{
+    channel_fsm_ = channel_fsm;
+    acquisition_->set_channel_fsm(std::move(channel_fsm));
 }
 
 signed int PcpsAcquisitionAdapterMI355X::mag() { return static_cast<signed int>(acquisition_->mag()); }

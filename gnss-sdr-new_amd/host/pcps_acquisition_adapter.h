@@ -28,6 +28,7 @@ public:
 
     void set_gnss_synchro(Gnss_Synchro* gnss_synchro) override;
     void set_channel(unsigned int channel) override;
+    void set_channel_fsm(std::weak_ptr<ChannelFsm> channel_fsm) override;
     void set_threshold(float threshold) override;
     void set_doppler_max(unsigned int doppler_max) override;
     void set_doppler_step(unsigned int doppler_step) override;
@@ -61,6 +62,7 @@ protected:
     std::unique_ptr<pcps_acquisition_mi355x> acquisition_;
     std::vector<std::complex<float>> code_;
     Gnss_Synchro* gnss_synchro_{nullptr};
+    std::weak_ptr<ChannelFsm> channel_fsm_;
     std::string role_;
     float threshold_{0.0};
     unsigned int doppler_max_{0};

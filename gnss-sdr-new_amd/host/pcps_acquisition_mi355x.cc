@@ -175,12 +175,16 @@ void pcps_acquisition_mi355x::calculate_threshold()
         gsdr_acq_get_threshold(d_engine, &d_threshold);
 }
 
-// send_positive_acquisition (:344-386) with the fork's repeat steps (:360-368)
+// send_positive_acquisition (:344-386) with the fork's repeat steps (:360-368):
+// the channel FSM directly when one is set (:370-373), else event 1 (:374-377)
 void pcps_acquisition_mi355x::send_positive_acquisition()
 {
     if (!d_step_repeat) d_positive_acq = 1;
     if (d_acq_parameters.make_repeat_steps) d_step_repeat = true;
-    if (d_events) d_events(1);
+    if (auto fsm = d_channel_fsm.lock())
+        fsm->Event_valid_acquisition();
+    else if (d_events)
+        d_events(1);
 }
 
 void pcps_acquisition_mi355x::send_negative_acquisition()

@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "acq_conf.h"
+#include "channel_fsm.h"
 #include "gnss_synchro.h"
 #include "gsdr.h"
 
@@ -40,6 +41,8 @@ public:
     void set_doppler_center(int32_t doppler_center);
     void set_resampler_latency(uint32_t latency_samples) { d_acq_parameters.resampler_latency_samples = latency_samples; }
     void set_event_handler(std::function<void(int)> h) { d_events = std::move(h); }
+    // the channel FSM notified directly of a positive acquisition (pcps_acquisition.h:159-161)
+    void set_channel_fsm(std::weak_ptr<ChannelFsm> channel_fsm) { d_channel_fsm = std::move(channel_fsm); }
     // start(): sample counter reset and threshold from pfa (pcps_acquisition.cc:885-891)
     bool start();
     void calculate_threshold();
@@ -72,6 +75,7 @@ private:
     uint32_t d_engine_step{0};
     Gnss_Synchro* d_gnss_synchro{nullptr};
     std::function<void(int)> d_events;
+    std::weak_ptr<ChannelFsm> d_channel_fsm;
     std::vector<uint8_t> d_data_buffer;
     std::vector<std::complex<float>> d_code;
     bool d_code_set{false};

@@ -13,8 +13,15 @@
 //  5. Acquisition -> tracking hand-off through the factory-built adapters
 //     (TrackingInterface::start_tracking from the acquisition's Gnss_Synchro,
 //     Gnss_Synchro records out) on synthetic GPS L1 C/A and Galileo E1 streams.
+//  6. AcquisitionInterface::set_channel_fsm: a positive acquisition reaches the
+//     channel FSM's Event_valid_acquisition directly (pcps_acquisition.cc:370-373).
+//  7. The pooled tracking block (<role>.mi355x_pool=true): factory-built channels
+//     sharing one engine handle over the device ring, fed GNU-Radio style, give the
+//     per-channel blocks' records bit for bit; the rates of both are printed.
+//  8. The gflags overrides (--pll_bw_hz, --dll_bw_hz, --doppler_max) and defaults.
 // Usage: host_selftest <GPS_L1_CA_ID_1_Fs_4Msps_2ms.dat> [Galileo_E1_ID_1_Fs_4Msps_8ms.dat]
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <complex>
 #include <cstring>
@@ -29,8 +36,10 @@
 #include "acquisition_service.h"
 #include "beidou_b1i_pcps_acquisition_mi355x.h"
 #include "galileo_e1_pcps_ambiguous_acquisition_mi355x.h"
+#include "channel_fsm.h"
 #include "gnss_block_factory_mi355x.h"
 #include "gnss_replicas.h"
+#include "gnss_sdr_flags.h"
 #include "gnss_tracking_mi355x.h"
 #include "gps_l1_ca_pcps_acquisition_mi355x.h"
 #include "hip_multicorrelator_real_codes.h"
@@ -669,7 +678,7 @@ struct HandOff
 };
 
 HandOff run_handoff(AcquisitionInterface* acq, pcps_acquisition_mi355x* ablk, TrackingInterface* trk,
-    dll_pll_veml_tracking_mi355x* tblk, Gnss_Synchro* gs, const std::vector<std::complex<float>>& x)
+    TrackingBlockMI355X* tblk, Gnss_Synchro* gs, const std::vector<std::complex<float>>& x)
 {
     HandOff h;
     int ev = 0;
@@ -904,6 +913,221 @@ void test_receiver_on_ring()
     gsdr_stream_destroy(ring);
 }
 
+
+// A channel FSM that counts the events the acquisition block fires at it.
+class CountingFsm : public ChannelFsm
+{
+public:
+    int valid{0};
+    bool Event_valid_acquisition() override
+    {
+        ++valid;
+        return true;
+    }
+};
+
+// Channel's constructor hands the acquisition adapter its FSM (channel.cc:50);
+// the block then reports a positive acquisition through it instead of event 1
+// (pcps_acquisition.cc:370-377), and a negative one still as event 2.
+void test_channel_fsm_handoff(const std::vector<std::complex<float>>& capture)
+{
+    InMemoryConfiguration config = gps_acq_config();
+    config.set_property("Acquisition_1C.pfa", "0.01");
+    auto acq_ = gsdr_factory::GetAcqBlock(&config, "Acquisition_1C", 1, 0, 0);
+    auto* acq = dynamic_cast<GpsL1CaPcpsAcquisitionMI355X*>(acq_.get());
+    EXPECT(acq != nullptr, "factory builds the GPS acquisition adapter");
+    if (!acq) return;
+    auto fsm = std::make_shared<CountingFsm>();
+    acq->set_channel_fsm(fsm);
+    Gnss_Synchro gs{};
+    gs.System = 'G';
+    gs.Signal[0] = '1';
+    gs.Signal[1] = 'C';
+    gs.PRN = 1;
+    int ev = 0, last = 0;
+    acq->get_block()->set_event_handler([&](int e) {
+        ++ev;
+        last = e;
+    });
+    acq->set_gnss_synchro(&gs);
+    acq->set_local_code();
+    acq->init();
+    acq->set_state(1);
+    acq->get_block()->start();
+    for (size_t pos = 0; pos < 8000 && fsm->valid == 0;)
+        pos += static_cast<size_t>(acq->get_block()->work(capture.data() + pos, static_cast<int>(std::min<size_t>(1000, 8000 - pos))));
+    EXPECT(fsm->valid == 1 && ev == 0, "set_channel_fsm: positive -> ChannelFsm::Event_valid_acquisition, no event 1");
+    EXPECT(std::abs(gs.Acq_delay_samples - 524.0) < 1.0, "set_channel_fsm: PRN 1 at 524 samples");
+    // PRN 20 is absent: the negative result still goes out as event 2
+    gs.PRN = 20;
+    acq->set_local_code();
+    acq->init();
+    acq->set_state(1);
+    acq->get_block()->start();
+    for (size_t pos = 0; pos < 8000 && ev == 0;)
+        pos += static_cast<size_t>(acq->get_block()->work(capture.data() + pos, static_cast<int>(std::min<size_t>(1000, 8000 - pos))));
+    EXPECT(fsm->valid == 1 && ev == 1 && last == 2, "set_channel_fsm: negative -> event 2");
+    // an expired FSM falls back to the message port (event 1)
+    fsm.reset();
+    gs.PRN = 1;
+    ev = 0;
+    acq->set_local_code();
+    acq->init();
+    acq->set_state(1);
+    acq->get_block()->start();
+    for (size_t pos = 0; pos < 8000 && ev == 0;)
+        pos += static_cast<size_t>(acq->get_block()->work(capture.data() + pos, static_cast<int>(std::min<size_t>(1000, 8000 - pos))));
+    EXPECT(ev == 1 && last == 1, "expired channel FSM: positive -> event 1");
+    std::printf("channel fsm hand-off: Event_valid_acquisition, negative event 2, expired FSM event 1\n");
+}
+
+// gnss_sdr_flags.cc:41-58 defaults into Dll_Pll_Conf, and the command-line
+// overrides of the .conf (dll_pll_conf.cc:24-28, :53-63; the acquisition
+// adapters' --doppler_max, gps_l1_ca_pcps_acquisition.cc:57-60).
+void test_flag_overrides()
+{
+    InMemoryConfiguration config = gps_acq_config();
+    config.set_property("Tracking_1C.pll_bw_hz", "40.0");
+    config.set_property("Tracking_1C.dll_bw_hz", "4.0");
+    Dll_Pll_Conf a;
+    a.SetFromConfiguration(&config, "Tracking_1C");
+    EXPECT(a.pll_bw_hz == 40.0F && a.dll_bw_hz == 4.0F, ".conf bandwidths without flags");
+    EXPECT(a.cn0_samples == 20 && a.cn0_min == 25 && a.max_code_lock_fail == 50 && a.max_carrier_lock_fail == 5000 &&
+               a.carrier_lock_th == 0.7,
+        "lock-detector defaults from the gflags");
+    FLAGS_pll_bw_hz = 25.0;
+    FLAGS_dll_bw_hz = 1.5;
+    FLAGS_cn0_min = 30;
+    FLAGS_doppler_max = 7000;
+    Dll_Pll_Conf b;
+    b.SetFromConfiguration(&config, "Tracking_1C");
+    EXPECT(b.pll_bw_hz == 25.0F && b.dll_bw_hz == 1.5F, "--pll_bw_hz / --dll_bw_hz override the .conf");
+    EXPECT(b.cn0_min == 30, "--cn0_min sets the default");
+    auto acq_ = gsdr_factory::GetAcqBlock(&config, "Acquisition_1C", 1, 0, 0);
+    auto* acq = dynamic_cast<GpsL1CaPcpsAcquisitionMI355X*>(acq_.get());
+    EXPECT(acq && acq->conf().doppler_max == 7000, "--doppler_max overrides Acquisition_1C.doppler_max");
+    FLAGS_pll_bw_hz = 0.0;
+    FLAGS_dll_bw_hz = 0.0;
+    FLAGS_cn0_min = 25;
+    FLAGS_doppler_max = 0;
+}
+
+// Several GPS channels tracked by factory-built blocks in GNU Radio fashion: every
+// block's work() is called in turn on the shared input from its own nitems_read.
+// pooled = false: one engine handle per channel (a synchronous H2D + launch + D2H
+// per general_work call); true: one shared pool per GPU over the device ring.
+struct PoolRun
+{
+    std::vector<std::vector<gsdr_trk_epoch>> recs;
+    std::vector<int> outputs;
+    double seconds{0.0};
+    uint64_t calls{0};
+};
+
+PoolRun run_tracking_blocks(bool pooled, const std::vector<std::complex<float>>& x, const std::vector<Gnss_Synchro>& acq)
+{
+    InMemoryConfiguration config;
+    config.set_property("GNSS-SDR.internal_fs_sps", "4000000");
+    config.set_property("Tracking_1C.implementation", "GPS_L1_CA_DLL_PLL_Tracking_MI355X");
+    config.set_property("Tracking_1C.item_type", "gr_complex");
+    config.set_property("Tracking_1C.pll_bw_hz", "40.0");
+    config.set_property("Tracking_1C.dll_bw_hz", "4.0");
+    config.set_property("Tracking_1C.pull_in_time_s", "0");
+    config.set_property("Channels_1C.count", std::to_string(acq.size()));
+    if (pooled) config.set_property("Tracking_1C.mi355x_pool", "true");
+    const size_t n = acq.size();
+    std::vector<std::unique_ptr<TrackingInterface>> trk;
+    std::vector<Gnss_Synchro> gs(acq);
+    PoolRun r;
+    r.recs.resize(n);
+    r.outputs.assign(n, 0);
+    std::vector<uint64_t> nread(n);
+    for (size_t c = 0; c < n; ++c)
+        {
+            trk.push_back(gsdr_factory::GetTrkBlock(&config, "Tracking_1C", 1, 1, 0));
+            trk[c]->set_channel(static_cast<unsigned int>(c));
+            trk[c]->set_gnss_synchro(&gs[c]);
+            trk[c]->start_tracking();
+            nread[c] = gs[c].Acq_samplestamp_samples;
+        }
+    auto* a0 = dynamic_cast<DllPllTrackingAdapterMI355X*>(trk[0].get());
+    EXPECT(a0 && a0->pooled() == pooled, "factory: pooled block iff Tracking_1C.mi355x_pool");
+    const auto t0 = std::chrono::steady_clock::now();
+    bool progress = true;
+    while (progress)
+        {
+            progress = false;
+            for (size_t c = 0; c < n; ++c)
+                {
+                    auto* blk = dynamic_cast<DllPllTrackingAdapterMI355X*>(trk[c].get())->get_block();
+                    if (nread[c] + static_cast<uint64_t>(blk->forecast()) > x.size()) continue;
+                    // the scheduler hands each block what the upstream buffer holds (>= forecast)
+                    const int avail = static_cast<int>(std::min<uint64_t>(16384, x.size() - nread[c]));
+                    Gnss_Synchro out{};
+                    int nout = 0;
+                    const int used = blk->work(x.data() + nread[c], avail, nread[c], &out, &nout);
+                    if (used <= 0) continue;
+                    progress = true;
+                    if (blk->state() >= 2 && blk->last_record().sample_counter == nread[c])
+                        {
+                            r.recs[c].push_back(blk->last_record());
+                            ++r.calls;
+                        }
+                    if (nout == 1 && out.Flag_valid_symbol_output) ++r.outputs[c];
+                    nread[c] += static_cast<uint64_t>(used);
+                }
+        }
+    r.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return r;
+}
+
+void test_pooled_tracking()
+{
+    const double fs = 4000000.0;
+    const double sigma = 1.0;
+    const double amp = std::sqrt(2.0 * std::pow(10.0, 4.8) / fs) * sigma;
+    const std::vector<float> bits = {1, -1, -1, -1, 1, -1, 1, 1};
+    const uint32_t prns[6] = {1, 7, 13, 19, 22, 30};
+    const double dly[6] = {524.3, 2100.8, 77.1, 3333.3, 1500.5, 999.9};
+    const double dop[6] = {1680.0, -3250.0, 500.0, 2750.0, -1250.0, 4000.0};
+    std::vector<SynthSat> sats;
+    std::vector<Gnss_Synchro> acq(6);
+    for (int i = 0; i < 6; ++i)
+        {
+            sats.push_back({gps_l1_ca_code_gen_float(prns[i]), 1.023e6, 1575.42e6, dly[i], dop[i], amp, {}, bits, 0.02});
+            acq[i].System = 'G';
+            acq[i].Signal[0] = '1';
+            acq[i].Signal[1] = 'C';
+            acq[i].PRN = prns[i];
+            acq[i].Channel_ID = i;
+            acq[i].Acq_delay_samples = std::fmod(std::round(dly[i]), 4000.0);
+            acq[i].Acq_doppler_hz = 250.0 * std::round(dop[i] / 250.0);
+            acq[i].Acq_samplestamp_samples = 0;
+        }
+    // pull_in_time_s = 0 ends the pull-in transitory after 1 s, then bit sync and outputs
+    const auto x = synth_stream(sats, fs, static_cast<size_t>(fs * 1.7), 23, sigma);
+    const PoolRun one = run_tracking_blocks(false, x, acq);
+    const PoolRun pool = run_tracking_blocks(true, x, acq);
+    bool same = true;
+    for (int c = 0; c < 6; ++c)
+        {
+            same = same && one.recs[c].size() == pool.recs[c].size() && one.recs[c].size() > 1000;
+            for (size_t e = 0; same && e < one.recs[c].size(); ++e)
+                same = std::memcmp(&one.recs[c][e], &pool.recs[c][e], sizeof(gsdr_trk_epoch)) == 0;
+        }
+    EXPECT(same, "pooled tracking blocks: every call's record identical to the per-channel blocks'");
+    EXPECT(pool.outputs[0] > 8 && pool.outputs == one.outputs, "pooled tracking: same Gnss_Synchro outputs");
+    if (pool.outputs != one.outputs || pool.outputs[0] <= 8)
+        std::fprintf(stderr, "outputs per channel: per-channel %d %d %d, pooled %d %d %d\n", one.outputs[0], one.outputs[1],
+            one.outputs[2], pool.outputs[0], pool.outputs[1], pool.outputs[2]);
+    const double msps_one = static_cast<double>(one.calls) * 4000.0 / one.seconds / 1e6;
+    const double msps_pool = static_cast<double>(pool.calls) * 4000.0 / pool.seconds / 1e6;
+    std::printf("tracking blocks, 6 GPS channels x %zu calls: per-channel adapters %.1f M ch-samples/s (%.1f us per "
+                "general_work call), pooled %.1f M ch-samples/s (%.1f us per call)\n",
+        one.recs[0].size(), msps_one, one.seconds / static_cast<double>(one.calls) * 1e6, msps_pool,
+        pool.seconds / static_cast<double>(pool.calls) * 1e6);
+}
+
 void test_multicorrelator(const std::vector<std::complex<float>>& capture)
 {
     const int n = 4000;
@@ -982,6 +1206,9 @@ int main(int argc, char** argv)
     test_beidou_acquisition();
     test_tracking_handoff();
     test_receiver_on_ring();
+    test_channel_fsm_handoff(capture);
+    test_flag_overrides();
+    test_pooled_tracking();
     if (failures == 0) std::printf("host_selftest: PASS\n");
     return failures == 0 ? 0 : 1;
 }

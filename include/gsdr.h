@@ -251,6 +251,11 @@ int gsdr_acq_run_step_two(gsdr_acq* acq, const void* iq_host, uint32_t nsel, con
  * (milliseconds) and the number of launches per stage, and resets them. */
 int gsdr_acq_set_profiling(gsdr_acq* acq, int enable);
 int gsdr_acq_read_profile(gsdr_acq* acq, double* stage_ms, uint32_t* launches);
+/* The same, plus per stage the busy time: the union of its launches' [start, end)
+ * intervals (stage_busy_ms may be NULL) -- the stage's wall time when launches of
+ * the handle overlap (runs issued on several streams); stage_ms / launches then
+ * over-counts it. */
+int gsdr_acq_read_profile_ex(gsdr_acq* acq, double* stage_ms, uint32_t* launches, double* stage_busy_ms);
 
 /* Debug/verification: device forward spectrum for one host block,
  * D rows x fft_size complex<float> (= FFT(x .* w_d)). */

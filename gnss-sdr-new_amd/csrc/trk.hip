@@ -53,12 +53,15 @@ constexpr int kMaxTrkTaps = 5;
 constexpr int kMaxCodeFloats = 16384;
 constexpr int kPreambleLen = 160;   // GPS_CA_PREAMBLE_LENGTH_SYMBOLS (GPS_L1_CA.h:61)
 constexpr int kMaxSmoother = 32;             // Dll_Pll_Conf::smoother_length cap (high_dyn histories)
-constexpr int kSpl = 8;                       // samples per lane per correlation chunk
+#ifndef GSDR_TRK_SPL
+#define GSDR_TRK_SPL 8
+#endif
+constexpr int kSpl = GSDR_TRK_SPL;            // samples per lane per correlation chunk
 constexpr int kWinCore = kSpl * kTrkThreads;  // 4096: the next call's window staged in LDS
 constexpr int kHalo = 16;                     // slack around the predicted next start
 constexpr int kStreamRow = 64 * 16;           // bytes one wave's global_load_lds_dwordx4 writes
-constexpr int kCodeMargin = 32;
-constexpr int kTimingSlots = 8;               // GSDR_TRK_TIMING record per call               // replica samples copied on each side of the LDS replica
+constexpr int kCodeMargin = 32;              // replica samples copied on each side of the LDS replica
+constexpr int kTimingSlots = 8;              // GSDR_TRK_TIMING record per call
 
 // MATH_CONSTANTS.h:47-50
 constexpr double kGnssPi = 3.1415926535898;
@@ -682,15 +685,14 @@ __device__ inline void save_correlation_results(const TrkConst& c, TrkHot& t, co
 // One general_work call after the correlation (taps given; slot kMaxTrkTaps is
 // the pilot-tracking data prompt): states 2 and 4.
 // GSDR_TRK_TIMING: wall-clock probes inside the loop update (slots 4-6 of the record)
-__device__ __forceinline__ void tprobe(uint64_t* pr, int i)
+__device__ __forceinline__ void tprobe(bool on, uint64_t (&pr)[3], int i)
 {
-    if (pr) pr[i] = wall_clock64();
+    if (on) pr[i] = wall_clock64();
 }
 
 __device__ inline void after_correlation(const TrkConst& c, TrkHot& t, TrkChan* gc, LoopFilter& lf, float2* pbuf,
     float (*scratch)[kMaxCn0], const float2 (&taps)[kMaxTrkTaps + 1], const float2 (&epl)[3], uint64_t nitems_read,
-    int lane, EpochOut& o,
-    uint64_t* pr = nullptr)
+    int lane, EpochOut& o, bool tm, uint64_t (&pr)[3])
 {
     o.flags = 0;
     o.prompt_i = 0.0;
@@ -709,7 +711,7 @@ __device__ inline void after_correlation(const TrkConst& c, TrkHot& t, TrkChan* 
             if (nitems_read < c.acq_sample_stamp || nitems_read - c.acq_sample_stamp >= c.bit_sync_span)
                 t.carrier_lock_fail_counter = 300000;
             const int locked = cn0_and_lock(c, t, pbuf, scratch, c.code_period, lane);
-            tprobe(pr, 0);
+            tprobe(tm, pr, 0);
             if (!locked)
                 {
                     clear_tracking_vars(t);
@@ -721,9 +723,9 @@ __device__ inline void after_correlation(const TrkConst& c, TrkHot& t, TrkChan* 
                 {
                     int next_state = 0;
                     run_dll_pll(c, t, lf);
-                    tprobe(pr, 1);
+                    tprobe(tm, pr, 1);
                     update_tracking_vars(c, t, gc);
-                    tprobe(pr, 2);
+                    tprobe(tm, pr, 2);
                     if (!t.pull_in_transitory)
                         {
                             if (c.secondary || c.symbols_per_bit > 1)
@@ -782,7 +784,7 @@ __device__ inline void after_correlation(const TrkConst& c, TrkHot& t, TrkChan* 
         {
             save_correlation_results(c, t, taps, epl);
             const int locked = cn0_and_lock(c, t, pbuf, scratch, c.code_period * (double)c.extend_correlation_symbols, lane);
-            tprobe(pr, 0);
+            tprobe(tm, pr, 0);
             if (!locked)
                 {
                     clear_tracking_vars(t);
@@ -793,9 +795,9 @@ __device__ inline void after_correlation(const TrkConst& c, TrkHot& t, TrkChan* 
             else
                 {
                     run_dll_pll(c, t, lf);
-                    tprobe(pr, 1);
+                    tprobe(tm, pr, 1);
                     update_tracking_vars(c, t, gc);
-                    tprobe(pr, 2);
+                    tprobe(tm, pr, 2);
                     if (!t.acc_carrier_phase_initialized)
                         {
                             t.acc_carrier_phase_rad = -(double)t.rem_carr_phase_rad;
@@ -940,17 +942,17 @@ __device__ __forceinline__ void correlate_chunk(const void* __restrict__ iq, con
                 v = lds_iq<IT>(sbuf, sboff + nc * item_bytes<IT>());
             xs[j] = (FULL || n < vl) ? gsdr::pk::from(v) : c2{0.f, 0.f};
         }
-    c2 av[kMaxTrkTaps + 1];
-#pragma unroll
-    for (int k = 0; k <= kMaxTrkTaps; ++k) av[k] = gsdr::pk::from(acc[k]);
-    c2 phv = gsdr::pk::from(ph);
-    const c2 ws = gsdr::pk::from(p.wstep);
+    // Three phases -- every replica index, then every replica gather, then the
+    // FMAs -- so the chunk's kSpl*KT LDS gathers are in flight together; written
+    // as one loop the scheduler issued them one at a time, each behind its own
+    // lgkmcnt(0) wait.  The FMA order per accumulator is unchanged.
+    float cv[kSpl][KT];
+    float dv[kSpl];
 #pragma unroll
     for (int j = 0; j < kSpl; ++j)
         {
             const int n0j = n0 + (int)threadIdx.x + j * kTrkThreads;
             const int n = FULL ? n0j : min(n0j, vl - 1);
-            const c2 tt = gsdr::pk::mul(xs[j], phv);
             const float a = gsdr::mul_rn(p.code_step, (float)n);
 #pragma unroll
             for (int k = 0; k < KT; ++k)
@@ -964,8 +966,30 @@ __device__ __forceinline__ void correlate_chunk(const void* __restrict__ iq, con
                         }
                     else if (WRAP == 0)
                         raw = wrap_code(raw, L);
-                    av[k] = gsdr::pk::fmas(tt, s_code[raw], av[k]);
-                    if (DATA && k == IPK) av[kMaxTrkTaps] = gsdr::pk::fmas(tt, s_data[raw], av[kMaxTrkTaps]);
+                    cv[j][k] = __int_as_float(raw);
+                }
+        }
+#pragma unroll
+    for (int j = 0; j < kSpl; ++j)
+        {
+            if (DATA) dv[j] = s_data[__float_as_int(cv[j][IPK])];
+#pragma unroll
+            for (int k = 0; k < KT; ++k) cv[j][k] = s_code[__float_as_int(cv[j][k])];
+        }
+    c2 av[kMaxTrkTaps + 1];
+#pragma unroll
+    for (int k = 0; k <= kMaxTrkTaps; ++k) av[k] = gsdr::pk::from(acc[k]);
+    c2 phv = gsdr::pk::from(ph);
+    const c2 ws = gsdr::pk::from(p.wstep);
+#pragma unroll
+    for (int j = 0; j < kSpl; ++j)
+        {
+            const c2 tt = gsdr::pk::mul(xs[j], phv);
+#pragma unroll
+            for (int k = 0; k < KT; ++k)
+                {
+                    av[k] = gsdr::pk::fmas(tt, cv[j][k], av[k]);
+                    if (DATA && k == IPK) av[kMaxTrkTaps] = gsdr::pk::fmas(tt, dv[j], av[kMaxTrkTaps]);
                 }
             phv = gsdr::pk::mul(phv, ws);
         }
@@ -1095,6 +1119,84 @@ __device__ __forceinline__ void correlate_call_stream(const void* __restrict__ i
         }
 }
 
+// One call's NCO and read plan from the loop state (lane-uniform): computed by
+// wave 0 at the end of the previous call's update, where the state is still in
+// registers (launch start: by lane 0 from the LDS copy).
+__device__ __forceinline__ Prep make_prep(const TrkConst& c, const TrkHot& t, bool go_epoch, uint64_t iq_first,
+    uint64_t iq_items, int vl, int K, int L, bool use_window, bool streamed, int stream_chunk, int64_t win_base,
+    int64_t pf_first)
+{
+    Prep p{};
+    const int64_t off = (int64_t)(t.next_sample - iq_first);
+    p.go = go_epoch && t.state >= 2 && t.state <= 4 && t.next_sample >= iq_first &&
+           (uint64_t)off + (uint64_t)vl <= iq_items;
+    p.off = off;
+    p.narrow = t.narrow;
+    p.woff = -1;
+    if (use_window && win_base != INT64_MIN && off >= win_base && off - win_base + vl <= kWinCore + kHalo)
+        p.woff = (int32_t)(off - win_base);
+    p.pf_ok = streamed && pf_first != INT64_MIN && off >= pf_first &&
+              off + min(vl, stream_chunk) <= pf_first + stream_chunk + kHalo;
+    if (p.go)
+        {
+            // do_correlation_step's float arguments (:1069-1075); the
+            // reference's phasors (cos r, -sin r) and exp(-j step)
+            // (cpu_multicorrelator_real_codes.cc:114-123) as angles
+            const float rem_carr = t.rem_carr_phase_rad;
+            const float carr_step = (float)t.carrier_phase_step_rad;
+            p.rem_code = (float)t.rem_code_phase_chips * (float)c.code_samples_per_chip;
+            p.code_step = (float)t.code_phase_step_chips * (float)c.code_samples_per_chip;
+            p.psi0 = -(double)rem_carr;
+            p.theta = -(double)carr_step;
+            // index range of the call (monotone in n for step > 0)
+            // static tap indices throughout: a run-time index into p
+            // (hdshift) sent the whole Prep through scratch
+            float smin = 1e30f, smax = -1e30f;
+#pragma unroll
+            for (int k = 0; k < kMaxTrkTaps; ++k)
+                {
+                    if (k < K)
+                        {
+                            const float sr =
+                                gsdr::sub_rn(t.narrow ? c.shifts_narrow[k] : c.shifts[k], p.rem_code);
+                            smin = fminf(smin, sr);
+                            smax = fmaxf(smax, sr);
+                        }
+                }
+            const float lo = floorf(smin);
+            const float hi = floorf(gsdr::add_rn(gsdr::mul_rn(p.code_step, (float)(vl - 1)), smax));
+            const float Lf = (float)L;
+            const bool mono = p.code_step >= 0.0f;
+            p.wrap = (mono && lo >= -(float)kCodeMargin && hi < Lf + (float)kCodeMargin)
+                         ? 2
+                         : ((mono && lo >= -Lf && hi < 2.0f * Lf) ? 1 : 0);
+            if (c.high_dyn)
+                {
+                    p.hd = 1;
+                    p.theta_rate = -(double)(float)t.carrier_phase_rate_step_rad;
+                    p.code_rate = (float)t.code_phase_rate_step_chips * (float)c.code_samples_per_chip;
+                    unsigned int shs = 0;
+                    p.hdshift[0] = 0;
+#pragma unroll
+                    for (int k = 1; k < kMaxTrkTaps; ++k)
+                        {
+                            if (k < K)
+                                {
+                                    const float* sk = t.narrow ? c.shifts_narrow : c.shifts;
+                                    shs += (int)roundf((sk[k] - sk[k - 1]) / p.code_step);
+                                    p.hdshift[k] = (int)shs;
+                                }
+                        }
+                }
+            const double w = p.theta * (double)kTrkThreads;
+            float sn, cs;
+            sincosf((float)fma(-rint(w * 0.15915494309189533576888376337251), 6.283185307179586476925286766559, w),
+                &sn, &cs);
+            p.wstep = make_float2(cs, sn);
+        }
+    return p;
+}
+
 // grid = channels; one kTrkThreads-lane workgroup per channel.  Wave 0 holds the
 // mutable loop state in registers for the whole launch (uniform across its
 // lanes); the configuration comes through scalar loads; the histories indexed at
@@ -1172,10 +1274,9 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
         {
             uint64_t tm0 = 0, tm1 = 0, tm2 = 0;
             if (timing && tid == 0) tm0 = wall_clock64();
-            if (tid == 0)
+            if (tid == 0 && e == 0)
                 {
                     const TrkHot& t = s_t;
-                    Prep p{};
                     if (e == 0 && t.state >= 2 && t.state <= 4 && t.next_sample < iq_first && max_epochs > 0)
                         {
                             // the channel's next call starts before the oldest item the
@@ -1194,63 +1295,8 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                             s_t.state = 0;
                             s_overrun = 1;
                         }
-                    const int64_t off = (int64_t)(t.next_sample - iq_first);
-                    p.go = (e < max_epochs) && t.state >= 2 && t.state <= 4 && t.next_sample >= iq_first &&
-                           (uint64_t)off + (uint64_t)vl <= iq_items;
-                    p.off = off;
-                    p.narrow = t.narrow;
-                    p.woff = -1;
-                    if (use_window && win_base != INT64_MIN && off >= win_base && off - win_base + vl <= kWinCore + kHalo)
-                        p.woff = (int32_t)(off - win_base);
-                    p.pf_ok = streamed && pf_first != INT64_MIN && off >= pf_first &&
-                              off + min(vl, stream_chunk) <= pf_first + stream_chunk + kHalo;
-                    if (p.go)
-                        {
-                            // do_correlation_step's float arguments (:1069-1075); the
-                            // reference's phasors (cos r, -sin r) and exp(-j step)
-                            // (cpu_multicorrelator_real_codes.cc:114-123) as angles
-                            const float rem_carr = t.rem_carr_phase_rad;
-                            const float carr_step = (float)t.carrier_phase_step_rad;
-                            p.rem_code = (float)t.rem_code_phase_chips * (float)c.code_samples_per_chip;
-                            p.code_step = (float)t.code_phase_step_chips * (float)c.code_samples_per_chip;
-                            p.psi0 = -(double)rem_carr;
-                            p.theta = -(double)carr_step;
-                            // index range of the call (monotone in n for step > 0)
-                            float smin = 1e30f, smax = -1e30f;
-                            for (int k = 0; k < K; ++k)
-                                {
-                                    const float sr = gsdr::sub_rn(t.narrow ? c.shifts_narrow[k] : c.shifts[k], p.rem_code);
-                                    smin = fminf(smin, sr);
-                                    smax = fmaxf(smax, sr);
-                                }
-                            const float lo = floorf(smin);
-                            const float hi = floorf(gsdr::add_rn(gsdr::mul_rn(p.code_step, (float)(vl - 1)), smax));
-                            const float Lf = (float)L;
-                            const bool mono = p.code_step >= 0.0f;
-                            p.wrap = (mono && lo >= -(float)kCodeMargin && hi < Lf + (float)kCodeMargin)
-                                         ? 2
-                                         : ((mono && lo >= -Lf && hi < 2.0f * Lf) ? 1 : 0);
-                            if (c.high_dyn)
-                                {
-                                    p.hd = 1;
-                                    p.theta_rate = -(double)(float)t.carrier_phase_rate_step_rad;
-                                    p.code_rate = (float)t.code_phase_rate_step_chips * (float)c.code_samples_per_chip;
-                                    unsigned int shs = 0;
-                                    p.hdshift[0] = 0;
-                                    for (int k = 1; k < K; ++k)
-                                        {
-                                            const float* sk = t.narrow ? c.shifts_narrow : c.shifts;
-                                            shs += (int)roundf((sk[k] - sk[k - 1]) / p.code_step);
-                                            p.hdshift[k] = (int)shs;
-                                        }
-                                }
-                            const double w = p.theta * (double)kTrkThreads;
-                            float sn, cs;
-                            sincosf((float)fma(-rint(w * 0.15915494309189533576888376337251), 6.283185307179586476925286766559, w),
-                                &sn, &cs);
-                            p.wstep = make_float2(cs, sn);
-                        }
-                    prep = p;
+                    prep = make_prep(c, t, e < max_epochs, iq_first, iq_items, vl, K, L, use_window, streamed,
+                        stream_chunk, win_base, pf_first);
                 }
             __syncthreads();
             if (!prep.go) break;
@@ -1345,37 +1391,32 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
             if (wave == 0)
                 {
                     TrkHot t = s_t;
+                    // lane k sums tap k over the waves in wave order (one batch of
+                    // LDS reads instead of a serial read per partial), then every
+                    // lane takes the totals by readlane; E/P/L are the same sums
+                    float2 mine = make_float2(0.f, 0.f);
+                    if (lane <= kMaxTrkTaps)
+                        {
+                            float2 v[kTrkThreads / 64];
+#pragma unroll
+                            for (int w = 0; w < kTrkThreads / 64; ++w) v[w] = s_red[w][lane];
+#pragma unroll
+                            for (int w = 0; w < kTrkThreads / 64; ++w)
+                                {
+                                    mine.x += v[w].x;
+                                    mine.y += v[w].y;
+                                }
+                        }
                     float2 taps[kMaxTrkTaps + 1];
 #pragma unroll
                     for (int k = 0; k <= kMaxTrkTaps; ++k)
-                        {
-                            float2 r = make_float2(0.f, 0.f);
-                            if (k < K || (k == kMaxTrkTaps && data))
-                                {
-#pragma unroll
-                                    for (int w = 0; w < kTrkThreads / 64; ++w)
-                                        {
-                                            r.x += s_red[w][k].x;
-                                            r.y += s_red[w][k].y;
-                                        }
-                                }
-                            taps[k] = r;
-                        }
+                        taps[k] = (k < K || (k == kMaxTrkTaps && data)) ? make_float2(lane_f(mine.x, k), lane_f(mine.y, k))
+                                                                       : make_float2(0.f, 0.f);
                     float2 epl[3];
                     {
                         const int ix[3] = {c.iE, c.iP, c.iL};
 #pragma unroll
-                        for (int q = 0; q < 3; ++q)
-                            {
-                                float2 r = make_float2(0.f, 0.f);
-#pragma unroll
-                                for (int w = 0; w < kTrkThreads / 64; ++w)
-                                    {
-                                        r.x += s_red[w][ix[q]].x;
-                                        r.y += s_red[w][ix[q]].y;
-                                    }
-                                epl[q] = r;
-                            }
+                        for (int q = 0; q < 3; ++q) epl[q] = make_float2(lane_f(mine.x, ix[q]), lane_f(mine.y, ix[q]));
                     }
                     const uint64_t n_read = t.next_sample;
                     const int32_t state0 = t.state;
@@ -1392,7 +1433,7 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                     uint64_t pr[3] = {0, 0, 0};
                     uint64_t tm3 = 0;
                     if (timing) tm3 = wall_clock64();
-                    after_correlation(c, t, gc, s_lf, s_pbuf, s_cn, taps, epl, n_read, lane, o, timing ? pr : nullptr);
+                    after_correlation(c, t, gc, s_lf, s_pbuf, s_cn, taps, epl, n_read, lane, o, timing != nullptr, pr);
                     if (lane == 0)
                         {
                             gsdr_trk_epoch r;
@@ -1436,6 +1477,11 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                         }
                     t.next_sample = n_read + (uint64_t)(int64_t)t.current_prn_length_samples;
                     if (lane == 0) s_t = t;
+                    // the next call's plan from the registers (the window / chunk-0
+                    // prefetch of this iteration starts at nb)
+                    const Prep pn = make_prep(c, t, e + 1 < max_epochs, iq_first, iq_items, vl, K, L, use_window, streamed,
+                        stream_chunk, use_window ? nb : win_base, streamed ? nb : pf_first);
+                    if (lane == 0) prep = pn;
                 }
             if (use_window)
                 {
@@ -1711,7 +1757,9 @@ void stream_plan(size_t lds_bytes, int code_pad, int data_pad, int isz, int& chu
     const long avail = (long)lds_bytes - (long)(code_pad + data_pad) * (long)sizeof(float);
     chunk = 0;
     sbuf = 0;
-    for (int c = kWinCore; c <= 64 * kWinCore; c += kWinCore)
+    int cap = 64 * kWinCore;
+    if (const char* e = std::getenv("GSDR_TRK_STREAM_CHUNK")) cap = std::max(kWinCore, std::atoi(e) / kWinCore * kWinCore);
+    for (int c = kWinCore; c <= cap; c += kWinCore)
         {
             if (2L * stream_buffer_bytes(c, isz) > avail) break;
             chunk = c;

@@ -768,56 +768,75 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(RP:
         const auto u = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, 0);
         return c2{__uint_as_float(u[0]), __uint_as_float(u[1])};
     };
-    // W_ROUT^{r q}: exact (+-1, +-i) for ROUT <= 4
     static_assert(ROUT == 1 || ROUT == 2 || ROUT == 4, "outer radix 1, 2 or 4");
-    c2 wq[ROUT];
-#pragma unroll
-    for (int r = 0; r < ROUT; ++r)
-        {
-            const int e4 = (int)(((uint32_t)r * q) % ROUT) * (4 / ROUT);  // W_ROUT^{rq} = W_4^{e4}
-            wq[r] = e4 == 0 ? c2{1.f, 0.f} : (e4 == 1 ? c2{0.f, -1.f} : (e4 == 2 ? c2{-1.f, 0.f} : c2{0.f, 1.f}));
-        }
     const int wbase = (int)(threadIdx.x & ~63u);
-    // phase 1: columns (clamped lanes repeat column L-1)
+    // phase 1: columns (clamped lanes repeat column L-1), with the sub-transform
+    // index q a compile-time constant: the outer factors W_ROUT^{rq} are exact
+    // (+-1, +-i: an add/sub with swapped operands) and W_N^{mq} one table read
+    // (m q < N)
     c2 v[CPL][R];
+    auto phase1 = [&](auto qc) {
+        constexpr int Q = decltype(qc)::value;
 #pragma unroll
-    for (int c = 0; c < CPL; ++c)
+        for (int c = 0; c < CPL; ++c)
+            {
+                if (L % NT == 0 || wbase + c * NT < L)
+                    {
+                        const int n2 = min((int)threadIdx.x + c * NT, L - 1);
+#pragma unroll
+                        for (int n1 = 0; n1 < R; ++n1)
+                            {
+                                const int m = n1 * L + n2;
+                                c2 z = gsdr::pk::conj_mul(bload(xrs, n2 * 8, n1 * L * 8), bload(crs, n2 * 8, n1 * L * 8));
+#pragma unroll
+                                for (int r = 1; r < ROUT; ++r)
+                                    {
+                                        const int so = (int)((r * M + n1 * L) * 8);
+                                        const c2 y = gsdr::pk::conj_mul(bload(xrs, n2 * 8, so), bload(crs, n2 * 8, so));
+                                        // W_ROUT^{r Q} = W_4^{e}, e = (r Q mod ROUT) * 4 / ROUT
+                                        const int e = ((r * Q) % ROUT) * (4 / ROUT);
+                                        if (e == 0)
+                                            z = z + y;
+                                        else if (e == 1)
+                                            z = gsdr::pk::add_mi(z, y);  // z + (-i) y
+                                        else if (e == 2)
+                                            z = z - y;
+                                        else
+                                            z = gsdr::pk::sub_mi(z, y);  // z + i y
+                                    }
+                                if constexpr (Q > 0) z = gsdr::pk::mul(z, gsdr::pk::from(tw[m * Q]));
+                                v[c][n1] = z;
+                            }
+                        gsdr::pk::Dft<R>::run(v[c]);
+                        // W_M^{n2 k1} = W_N^{ROUT n2 k1}
+                        const c2 w1 = gsdr::pk::from(tw[ROUT * n2]);
+                        c2 w = w1;
+#pragma unroll
+                        for (int k1 = 1; k1 < R; ++k1)
+                            {
+                                if (k1 > 1) w = gsdr::pk::mul(w, w1);
+                                v[c][k1] = gsdr::pk::mul(v[c][k1], w);
+                            }
+                    }
+            }
+    };
+    if constexpr (ROUT == 1)
+        phase1(std::integral_constant<int, 0>{});
+    else if constexpr (ROUT == 2)
         {
-            if (L % NT == 0 || wbase + c * NT < L)
+            if (q == 0)
+                phase1(std::integral_constant<int, 0>{});
+            else
+                phase1(std::integral_constant<int, 1>{});
+        }
+    else
+        {
+            switch (q)
                 {
-                    const int n2 = min((int)threadIdx.x + c * NT, L - 1);
-#pragma unroll
-                    for (int n1 = 0; n1 < R; ++n1)
-                        {
-                            const int m = n1 * L + n2;
-                            c2 z = gsdr::pk::conj_mul(bload(xrs, n2 * 8, n1 * L * 8), bload(crs, n2 * 8, n1 * L * 8));
-#pragma unroll
-                            for (int r = 1; r < ROUT; ++r)
-                                {
-                                    const int so = (int)((r * M + n1 * L) * 8);
-                                    const c2 y = gsdr::pk::conj_mul(bload(xrs, n2 * 8, so), bload(crs, n2 * 8, so));
-                                    z = z + gsdr::pk::mul(y, wq[r]);
-                                }
-                            if (ROUT > 1 && q > 0)
-                                {
-                                    // W_N^{m q} = (W_N^m)^q
-                                    const c2 w1 = gsdr::pk::from(tw[m]);
-                                    c2 w = w1;
-                                    for (uint32_t e = 1; e < q; ++e) w = gsdr::pk::mul(w, w1);
-                                    z = gsdr::pk::mul(z, w);
-                                }
-                            v[c][n1] = z;
-                        }
-                    gsdr::pk::Dft<R>::run(v[c]);
-                    // W_M^{n2 k1} = W_N^{ROUT n2 k1}
-                    const c2 w1 = gsdr::pk::from(tw[ROUT * n2]);
-                    c2 w = w1;
-#pragma unroll
-                    for (int k1 = 1; k1 < R; ++k1)
-                        {
-                            if (k1 > 1) w = gsdr::pk::mul(w, w1);
-                            v[c][k1] = gsdr::pk::mul(v[c][k1], w);
-                        }
+                case 0: phase1(std::integral_constant<int, 0>{}); break;
+                case 1: phase1(std::integral_constant<int, 1>{}); break;
+                case 2: phase1(std::integral_constant<int, 2>{}); break;
+                default: phase1(std::integral_constant<int, 3>{}); break;
                 }
         }
     struct Out
@@ -1659,7 +1678,8 @@ size_t item_bytes(int it) { return it == GSDR_ITEM_CSHORT ? 4 : (it == GSDR_ITEM
     X(61, (gsdr::pk::PkPlan<512, true, 20, 20, 20>), 1, 1, 1)           \
     X(62, (gsdr::pk::PkPlan<256, true, 20, 10, 10>), 1, 1, 1)           \
     X(93, (gsdr::pk::PkPlan<1024, 1, 16, 10, 10, 10>), 1, 1, 2)         \
-    X(70, (gsdr::pk::PkPlan<256, 1, 25, 16, 10>), 1, 1, 2)
+    X(70, (gsdr::pk::PkPlan<256, 1, 25, 16, 10>), 1, 1, 2)           \
+    X(71, (gsdr::pk::PkPlan<256, 1, 25, 16, 10>), 1, 5, 2)
 
 template <class PT>
 int set_lds_attrs(size_t bytes)

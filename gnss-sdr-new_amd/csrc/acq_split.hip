@@ -13,12 +13,17 @@ namespace gsdr_acq_impl
 //           8 rows per LDS round (64 KB)
 using Reg25k = RegFourStep<25, 512, 5, 1, NoPads<1000>, 10, 10, 10>;
 using Reg32k = RegFourStep<32, 1024, 8, 1, NoPads<1000>, 10, 10, 10>;
+//   16000 = 16 x (10 x 10 x 10): the C3 plan (variant 93's register four-step), 512
+//           lanes, two columns per lane, 8 rows per LDS round (64 KB)
+using Reg16k = RegFourStep<16, 512, 8, 1, NoPads<1000>, 10, 10, 10>;
 
 // split ids: (N, outer radix ROUT, inner plan)
 //   1: 25000 = 1 x 25000 (C5 GPS L1 / BeiDou B1I at 25 Msps, 1 ms)
 //   2: 32000 = 1 x 32000 (Galileo E1 at 8 Msps, 4 ms)
 //   3: 64000 = 2 x 32000 (C4: Galileo E1 at 8 Msps with bit transition)
 //   4: 100000 = 4 x 25000 (C5 Galileo E1 at 25 Msps, 4 ms)
+//   5: 32000 = 2 x 16000
+//   6: 64000 = 4 x 16000
 namespace
 {
 struct SplitId
@@ -26,7 +31,7 @@ struct SplitId
     int id;
     uint32_t n;
 };
-constexpr SplitId kSplits[] = {{1, 25000}, {2, 32000}, {3, 64000}, {4, 100000}};
+constexpr SplitId kSplits[] = {{1, 25000}, {2, 32000}, {3, 64000}, {4, 100000}, {5, 32000}, {6, 64000}};
 
 // PRN group of an XCD pass: the largest divisor of P whose code rows fit in ~2 MB
 // (half an XCD's L2), so the rows of the group's codes stay resident while the X
@@ -76,15 +81,19 @@ int launch_split(gsdr_acq* a, uint32_t nblocks, hipStream_t s)
         case 2: return half ? launch_one<1, Reg32k, true>(a, nblocks, s) : launch_one<1, Reg32k, false>(a, nblocks, s);
         case 3: return half ? launch_one<2, Reg32k, true>(a, nblocks, s) : launch_one<2, Reg32k, false>(a, nblocks, s);
         case 4: return half ? launch_one<4, Reg25k, true>(a, nblocks, s) : launch_one<4, Reg25k, false>(a, nblocks, s);
+        case 5: return half ? launch_one<2, Reg16k, true>(a, nblocks, s) : launch_one<2, Reg16k, false>(a, nblocks, s);
+        case 6: return half ? launch_one<4, Reg16k, true>(a, nblocks, s) : launch_one<4, Reg16k, false>(a, nblocks, s);
         default: gsdr::set_error("internal: bad split variant %d", a->split); return GSDR_E_STATE;
         }
 }
 
 // Select the split correlate for a single-dwell four-step handle (K = 1, with or
-// without bit transition).  Default: the ROUT = 1 splits (N = 25000 / 32000); the
-// ROUT > 1 ones (64000, 100000) measured slower than the packed four-step -- every
-// sub-transform re-reads the whole X and code rows -- and run only
-// with GSDR_ACQ_SPLIT=2.  GSDR_ACQ_SPLIT=0 keeps the packed four-step everywhere.
+// without bit transition).  Default: 25000 / 32000 (ROUT = 1) and 64000 = 2 x 32000
+// (C4 bit transition: 52 -> 61 Msps, profiles/r03q); 100000 = 4 x 25000 measured
+// slower than the packed four-step (87 vs 100 Msps: every sub-transform re-reads the
+// whole X and code rows, 64 B per point from L2) and runs only with GSDR_ACQ_SPLIT=2,
+// as do the 16000-based splits 5 / 6 (GSDR_ACQ_SPLIT_ID).  GSDR_ACQ_SPLIT=0 keeps
+// the packed four-step everywhere.
 int setup_split(gsdr_acq* a)
 {
     a->split = 0;
@@ -93,8 +102,15 @@ int setup_split(gsdr_acq* a)
     if (const char* e = std::getenv("GSDR_ACQ_SPLIT")) mode = std::atoi(e);
     if (mode == 0) return GSDR_OK;
     for (const SplitId& sp : kSplits)
-        if (sp.n == a->N) a->split = sp.id;
-    if (a->split >= 3 && mode < 2) a->split = 0;
+        if (sp.n == a->N && !a->split) a->split = sp.id;
+    if (a->split == 4 && mode < 2) a->split = 0;
+    // experiments: GSDR_ACQ_SPLIT_ID forces a split of the handle's N
+    if (const char* e = std::getenv("GSDR_ACQ_SPLIT_ID"))
+        {
+            const int want = std::atoi(e);
+            for (const SplitId& sp : kSplits)
+                if (sp.id == want && sp.n == a->N) a->split = want;
+        }
     if (!a->split) return GSDR_OK;
     int rc = GSDR_OK;
     switch (a->split)
@@ -103,6 +119,8 @@ int setup_split(gsdr_acq* a)
         case 2: rc = attrs_one<1, Reg32k, true>() | attrs_one<1, Reg32k, false>(); break;
         case 3: rc = attrs_one<2, Reg32k, true>() | attrs_one<2, Reg32k, false>(); break;
         case 4: rc = attrs_one<4, Reg25k, true>() | attrs_one<4, Reg25k, false>(); break;
+        case 5: rc = attrs_one<2, Reg16k, true>() | attrs_one<2, Reg16k, false>(); break;
+        case 6: rc = attrs_one<4, Reg16k, true>() | attrs_one<4, Reg16k, false>(); break;
         default: break;
         }
     if (rc != GSDR_OK) a->split = 0;

@@ -231,6 +231,9 @@ struct TrkHot
     double corr_time;            // d_current_correlation_time_s
     int32_t narrow, extend_count;  // after the switch to the extended correlator
     int32_t hist_n, hist_head;     // high_dyn: d_carr_ph_history / d_code_ph_history fill and oldest slot
+    // run_dll_pll's d_carr_phase_error_hz, d_carr_error_filt_hz, d_code_error_chips,
+    // d_code_error_filt_chips as log_data writes them (float of the double members)
+    float log_err[4];
 };
 
 // Device-memory image of the mutable part of one channel.
@@ -375,6 +378,7 @@ __device__ inline void clear_tracking_vars(TrkHot& t)  // :1192-1213
     t.code_phase_rate_step_chips = 0.0;
     t.hist_n = 0;  // d_carr_ph_history.clear(), d_code_ph_history.clear()
     t.hist_head = 0;
+    for (int i = 0; i < 4; ++i) t.log_err[i] = 0.0F;
 }
 
 // Sequential float sums over the buffer elements (the estimators' loops, in the
@@ -511,6 +515,10 @@ __device__ inline void run_dll_pll(const TrkConst& c, TrkHot& t, LoopFilter& lf)
         c.veml ? dll_nc_vemlp(t.VE_accu, t.E_accu, t.L_accu, t.VL_accu) : dll_nc_e_minus_l(t.E_accu, t.L_accu, t.spc, 1.0F, 1.0F);
     const double code_error_filt_chips = (double)lf_apply(lf, (float)code_error_chips);
     t.code_freq_chips = c.code_chip_rate - code_error_filt_chips;
+    t.log_err[0] = (float)carr_phase_error_hz;
+    t.log_err[1] = (float)carr_error_filt_hz;
+    t.log_err[2] = (float)code_error_chips;
+    t.log_err[3] = (float)code_error_filt_chips;
     if (c.carrier_aiding) t.code_freq_chips += t.carrier_doppler_hz * c.code_chip_rate / c.signal_carrier_freq;
 }
 
@@ -625,7 +633,20 @@ struct EpochOut
 {
     int32_t flags;
     double prompt_i, prompt_q;
+    float log_accu[5];  // log_data's |VE|, |E|, |P|, |L|, |VL| accumulators (GSDR_TRK_F_LOGGED)
 };
+
+// log_data (:1403-1500): the accumulator magnitudes at the reference's log point
+// (std::abs<float> of the complex accumulators; VE/VL written as 0 without VEML)
+__device__ inline void log_point(const TrkConst& c, const TrkHot& t, EpochOut& o)
+{
+    o.flags |= GSDR_TRK_F_LOGGED;
+    o.log_accu[0] = c.veml ? hypotf(t.VE_accu.x, t.VE_accu.y) : 0.0F;
+    o.log_accu[1] = hypotf(t.E_accu.x, t.E_accu.y);
+    o.log_accu[2] = hypotf(t.P_accu.x, t.P_accu.y);
+    o.log_accu[3] = hypotf(t.L_accu.x, t.L_accu.y);
+    o.log_accu[4] = c.veml ? hypotf(t.VL_accu.x, t.VL_accu.y) : 0.0F;
+}
 
 // save_correlation_results (:1288-1400): secondary-code wipe-off of the tap
 // accumulators, data-symbol accumulation (NH wipe-off / pilot data prompt).
@@ -697,6 +718,7 @@ __device__ inline void after_correlation(const TrkConst& c, TrkHot& t, TrkChan* 
     o.flags = 0;
     o.prompt_i = 0.0;
     o.prompt_q = 0.0;
+    for (int i = 0; i < 5; ++i) o.log_accu[i] = 0.0F;
     if (t.state == 2)
         {
             if (c.veml)
@@ -726,6 +748,7 @@ __device__ inline void after_correlation(const TrkConst& c, TrkHot& t, TrkChan* 
                     tprobe(tm, pr, 1);
                     update_tracking_vars(c, t, gc);
                     tprobe(tm, pr, 2);
+                    log_point(c, t, o);
                     if (!t.pull_in_transitory)
                         {
                             if (c.secondary || c.symbols_per_bit > 1)
@@ -768,6 +791,7 @@ __device__ inline void after_correlation(const TrkConst& c, TrkHot& t, TrkChan* 
             update_tracking_vars(c, t, gc);
             if (t.current_data_symbol == 0)
                 {
+                    log_point(c, t, o);
                     o.prompt_i = (double)t.P_data_accu.x;
                     o.prompt_q = (double)t.P_data_accu.y;
                     o.flags |= GSDR_TRK_F_VALID_OUTPUT;
@@ -805,6 +829,7 @@ __device__ inline void after_correlation(const TrkConst& c, TrkHot& t, TrkChan* 
                         }
                     if (t.current_data_symbol == 0)
                         {
+                            log_point(c, t, o);
                             o.prompt_i = (double)t.P_data_accu.x;
                             o.prompt_q = (double)t.P_data_accu.y;
                             o.flags |= GSDR_TRK_F_VALID_OUTPUT;
@@ -1461,6 +1486,13 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                             r.data_prompt[1] = data ? taps[kMaxTrkTaps].y : 0.0F;
                             r.carrier_rate = (float)t.carrier_phase_rate_step_rad;
                             r.code_rate = (float)t.code_phase_rate_step_chips;
+#pragma unroll
+                            for (int i = 0; i < 5; ++i) r.log_accu[i] = o.log_accu[i];
+                            r.carr_phase_error_hz = t.log_err[0];
+                            r.carr_error_filt_hz = t.log_err[1];
+                            r.code_error_chips = t.log_err[2];
+                            r.code_error_filt_chips = t.log_err[3];
+                            r.reserved = 0;
                             out[(size_t)ch * max_epochs + e] = r;
                             if (timing)
                                 {

@@ -48,7 +48,7 @@ EXPORTED = [
 SIGNAL_GPS_1C = 0
 SIGNAL_GAL_1B = 1
 SIGNAL_BDS_B1 = 2
-TRK_F_VALID_OUTPUT, TRK_F_LOSS_OF_LOCK, TRK_F_PLL_180, TRK_F_BIT_SYNC, TRK_F_OVERRUN = 1, 2, 4, 8, 16
+TRK_F_VALID_OUTPUT, TRK_F_LOSS_OF_LOCK, TRK_F_PLL_180, TRK_F_BIT_SYNC, TRK_F_OVERRUN, TRK_F_LOGGED = 1, 2, 4, 8, 16, 32
 
 # include/gsdr.h gsdr_trk_conf / gsdr_trk_epoch (C layout)
 TRK_CONF_DTYPE = np.dtype([
@@ -69,8 +69,64 @@ TRK_EPOCH_DTYPE = np.dtype([
     ("rem_carr_phase_rad", "f4"), ("flags", "i4"), ("carrier_doppler_hz", "f8"), ("code_freq_chips", "f8"),
     ("rem_code_phase_samples", "f8"), ("acc_carrier_phase_rad", "f8"), ("cn0_db_hz", "f8"),
     ("carrier_lock_test", "f8"), ("prompt_i", "f8"), ("prompt_q", "f8"), ("evm", "f8"), ("data_prompt", "f4", (2,)),
-    ("carrier_rate", "f4"), ("code_rate", "f4")], align=True)
-assert TRK_EPOCH_DTYPE.itemsize == 152
+    ("carrier_rate", "f4"), ("code_rate", "f4"), ("log_accu", "f4", (5,)), ("carr_phase_error_hz", "f4"),
+    ("carr_error_filt_hz", "f4"), ("code_error_chips", "f4"), ("code_error_filt_chips", "f4"), ("reserved", "i4")], align=True)
+assert TRK_EPOCH_DTYPE.itemsize == 192
+
+
+# The tracking block's dump record (dll_pll_veml_tracking.cc:1403-1500, log_data):
+# 108 packed bytes per logged call, in the reference's write order.
+TRK_DUMP_DTYPE = np.dtype([
+    ("abs_VE", "<f4"), ("abs_E", "<f4"), ("abs_P", "<f4"), ("abs_L", "<f4"), ("abs_VL", "<f4"),
+    ("Prompt_I", "<f4"), ("Prompt_Q", "<f4"), ("PRN_start_sample_count", "<u8"), ("acc_carrier_phase_rad", "<f4"),
+    ("carrier_doppler_hz", "<f4"), ("carrier_doppler_rate_hz", "<f4"), ("code_freq_chips", "<f4"),
+    ("code_freq_rate_chips", "<f4"), ("carr_error_hz", "<f4"), ("carr_error_filt_hz", "<f4"),
+    ("code_error_chips", "<f4"), ("code_error_filt_chips", "<f4"), ("CN0_SNV_dB_Hz", "<f4"),
+    ("carrier_lock_test", "<f4"), ("aux1", "<f4"), ("aux2", "<f8"), ("PRN", "<u4"),
+    ("acq_code_phase_samples", "<f4"), ("acq_carrier_doppler_hz", "<f4"), ("EVM", "<f4")])
+assert TRK_DUMP_DTYPE.itemsize == 108
+
+
+def trk_dump_records(recs, fs_in, prn, acq_code_phase_samples, acq_carrier_doppler_hz, veml=False,
+                     track_pilot=False):
+    """The dump records the reference writes for a channel's calls: one per record
+    flagged TRK_F_LOGGED (host/tracking_dump.cc is the C++ writer of the same bytes).
+    acq_code_phase_samples is d_acq_code_phase_samples after the pull-in (:1817-1828)."""
+    r = recs[(recs["flags"] & TRK_F_LOGGED) != 0]
+    out = np.zeros(len(r), TRK_DUMP_DTYPE)
+    ip = 2 if veml else 1
+    acc = r["log_accu"]
+    out["abs_VE"] = acc[:, 0] if veml else 0.0
+    out["abs_E"], out["abs_P"], out["abs_L"] = acc[:, 1], acc[:, 2], acc[:, 3]
+    out["abs_VL"] = acc[:, 4] if veml else 0.0
+    out["Prompt_I"] = r["data_prompt"][:, 0] if track_pilot else r["taps"][:, 2 * ip]
+    out["Prompt_Q"] = r["data_prompt"][:, 1] if track_pilot else r["taps"][:, 2 * ip + 1]
+    stamp = r["sample_counter"] + r["consumed"].astype(np.uint64)
+    out["PRN_start_sample_count"] = stamp
+    out["acc_carrier_phase_rad"] = r["acc_carrier_phase_rad"].astype(np.float32)
+    out["carrier_doppler_hz"] = r["carrier_doppler_hz"].astype(np.float32)
+    two_pi = 2.0 * 3.1415926535897932384626433832795
+    out["carrier_doppler_rate_hz"] = (r["carrier_rate"].astype(np.float64) * fs_in * fs_in / two_pi).astype(np.float32)
+    out["code_freq_chips"] = r["code_freq_chips"].astype(np.float32)
+    out["code_freq_rate_chips"] = (r["code_rate"].astype(np.float64) * fs_in * fs_in).astype(np.float32)
+    out["carr_error_hz"] = r["carr_phase_error_hz"]
+    out["carr_error_filt_hz"] = r["carr_error_filt_hz"]
+    out["code_error_chips"] = r["code_error_chips"]
+    out["code_error_filt_chips"] = r["code_error_filt_chips"]
+    out["CN0_SNV_dB_Hz"] = r["cn0_db_hz"].astype(np.float32)
+    out["carrier_lock_test"] = r["carrier_lock_test"].astype(np.float32)
+    out["aux1"] = r["rem_code_phase_samples"].astype(np.float32)
+    out["aux2"] = stamp.astype(np.float64)
+    out["PRN"] = prn
+    out["acq_code_phase_samples"] = np.float32(acq_code_phase_samples)
+    out["acq_carrier_doppler_hz"] = np.float32(acq_carrier_doppler_hz)
+    out["EVM"] = r["evm"].astype(np.float32)
+    return out
+
+
+def read_trk_dump(path):
+    """A tracking dump file (the reference's trk_channel_<n>.dat layout) as records."""
+    return np.fromfile(path, dtype=TRK_DUMP_DTYPE)
 
 
 class GsdrError(RuntimeError):

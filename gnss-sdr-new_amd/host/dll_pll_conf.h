@@ -25,6 +25,7 @@ public:
     gsdr_trk_conf to_engine(int32_t signal, uint32_t max_channels) const;
 
     std::string item_type{"gr_complex"};
+    std::string dump_filename{"./dll_pll_dump.dat"};
     double fs_in{2000000.0};
     double carrier_lock_th{0.7};
     float fll_bw_hz{35.0};
@@ -60,6 +61,7 @@ public:
     bool carrier_aiding{true};
     bool high_dyn{false};
     bool dump{false};
+    bool dump_mat{true};  // read for parity; the .mat conversion is not reproduced (tracking_dump.h)
 };
 
 #endif

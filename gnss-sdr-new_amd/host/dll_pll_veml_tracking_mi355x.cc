@@ -14,6 +14,7 @@ dll_pll_veml_tracking_mi355x::dll_pll_veml_tracking_mi355x(const Dll_Pll_Conf& c
     if (gsdr_trk_create(device, &c, &d_engine) != GSDR_OK)
         throw std::runtime_error(std::string("dll_pll_veml_tracking_mi355x: ") + gsdr_last_error());
     d_vector_length = d_conf.vector_length;
+    if (d_conf.dump) d_dump.configure(d_conf.dump_filename);
     d_item_bytes = c.item_type == GSDR_ITEM_CSHORT ? 4 : (c.item_type == GSDR_ITEM_IBYTE ? 2 : 8);
 }
 
@@ -29,6 +30,7 @@ void dll_pll_veml_tracking_mi355x::set_channel(uint32_t channel)
 {
     std::lock_guard<std::mutex> l(d_setlock);
     d_channel = channel;
+    if (d_conf.dump) d_dump.open(channel);
 }
 
 void dll_pll_veml_tracking_mi355x::start_tracking()
@@ -94,6 +96,12 @@ int dll_pll_veml_tracking_mi355x::work(const void* in, int ninput_items, uint64_
                         if (d_events) d_events(3);
                         return 0;
                     }
+                if (d_conf.dump)
+                    d_dump.set_acquisition(d_acquisition_gnss_synchro->PRN,
+                        TrackingDump::pull_in_code_phase(d_signal, d_conf.fs_in, nitems_read,
+                            d_acquisition_gnss_synchro->Acq_samplestamp_samples,
+                            d_acquisition_gnss_synchro->Acq_delay_samples),
+                        d_acquisition_gnss_synchro->Acq_doppler_hz);
                 d_state = 2;
                 return static_cast<int>(first - nitems_read);
             }
@@ -112,6 +120,7 @@ int dll_pll_veml_tracking_mi355x::work(const void* in, int ninput_items, uint64_
             return 0;
         }
     if (nrec == 0) return 0;  // not enough input for the call: wait for more items
+    if (d_conf.dump) d_dump.write(d_last, d_conf.fs_in, d_signal == GSDR_SIGNAL_GAL_1B, d_conf.track_pilot);
     const bool loss_of_lock = (d_last.flags & GSDR_TRK_F_LOSS_OF_LOCK) != 0;
     if ((d_last.flags & GSDR_TRK_F_VALID_OUTPUT) || loss_of_lock)
         {

@@ -16,6 +16,7 @@
 #include "gnss_synchro.h"
 #include "gsdr.h"
 #include "tracking_block_mi355x.h"
+#include "tracking_dump.h"
 
 class dll_pll_veml_tracking_mi355x : public TrackingBlockMI355X
 {
@@ -61,6 +62,7 @@ private:
     gsdr_trk_epoch d_last{};
     std::function<void(int)> d_events;
     std::mutex d_setlock;
+    TrackingDump d_dump;  // <role>.dump: the reference's per-channel .dat (log_data)
 };
 
 #endif

@@ -177,8 +177,9 @@ void SharedTrackingPool::drop(int slot)
 
 dll_pll_veml_tracking_pool_mi355x::dll_pll_veml_tracking_pool_mi355x(const Dll_Pll_Conf& conf, int32_t signal,
     uint32_t pool_channels, int device, const std::string& pool_key)
-    : d_conf(conf)
+    : d_conf(conf), d_signal(signal)
 {
+    if (d_conf.dump) d_dump.configure(d_conf.dump_filename);
     d_pool = SharedTrackingPool::get(pool_key, conf, signal, pool_channels, device);
     d_slot = d_pool->acquire_slot();
     if (d_slot < 0)
@@ -197,6 +198,7 @@ void dll_pll_veml_tracking_pool_mi355x::set_channel(uint32_t channel)
 {
     std::lock_guard<std::mutex> l(d_setlock);
     d_channel = channel;
+    if (d_conf.dump) d_dump.open(channel);
 }
 
 void dll_pll_veml_tracking_pool_mi355x::start_tracking()
@@ -233,6 +235,11 @@ int dll_pll_veml_tracking_pool_mi355x::work(const void* in, int ninput_items, ui
                         d_pool->feed(in, nitems_read, ninput_items, false);
                         const uint64_t first = d_pool->start(d_slot, g->PRN, g->Signal, g->Acq_delay_samples,
                             g->Acq_doppler_hz, g->Acq_samplestamp_samples, nitems_read);
+                        if (d_conf.dump)
+                            d_dump.set_acquisition(g->PRN,
+                                TrackingDump::pull_in_code_phase(d_signal, d_conf.fs_in, nitems_read,
+                                    g->Acq_samplestamp_samples, g->Acq_delay_samples),
+                                g->Acq_doppler_hz);
                         d_state = 2;
                         return static_cast<int>(first - nitems_read);
                     }
@@ -270,6 +277,7 @@ int dll_pll_veml_tracking_pool_mi355x::work(const void* in, int ninput_items, ui
             if (d_events) d_events(3);
             return 0;
         }
+    if (d_conf.dump) d_dump.write(d_last, d_conf.fs_in, d_signal == GSDR_SIGNAL_GAL_1B, d_conf.track_pilot);
     const bool loss_of_lock = (d_last.flags & GSDR_TRK_F_LOSS_OF_LOCK) != 0;
     if ((d_last.flags & GSDR_TRK_F_VALID_OUTPUT) || loss_of_lock)
         {

@@ -28,6 +28,7 @@
 #include "gnss_synchro.h"
 #include "gsdr.h"
 #include "tracking_block_mi355x.h"
+#include "tracking_dump.h"
 
 class SharedTrackingPool
 {
@@ -104,6 +105,7 @@ public:
 
 private:
     Dll_Pll_Conf d_conf;
+    int32_t d_signal;
     std::shared_ptr<SharedTrackingPool> d_pool;
     int d_slot{-1};
     Gnss_Synchro* d_acquisition_gnss_synchro{nullptr};
@@ -112,6 +114,7 @@ private:
     gsdr_trk_epoch d_last{};
     std::function<void(int)> d_events;
     std::mutex d_setlock;
+    TrackingDump d_dump;  // <role>.dump: the reference's per-channel .dat (log_data)
 };
 
 #endif

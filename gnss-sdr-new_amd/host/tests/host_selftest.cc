@@ -26,6 +26,7 @@
 #include <complex>
 #include <cstring>
 #include <cstdio>
+#include <filesystem>
 #include <fstream>
 #include <iostream>
 #include <string>
@@ -43,7 +44,9 @@
 #include "gnss_tracking_mi355x.h"
 #include "gps_l1_ca_pcps_acquisition_mi355x.h"
 #include "hip_multicorrelator_real_codes.h"
+#include "tracking_dump.h"
 #include "tracking_pool.h"
+#include <unistd.h>
 
 namespace
 {
@@ -1024,7 +1027,8 @@ struct PoolRun
     uint64_t calls{0};
 };
 
-PoolRun run_tracking_blocks(bool pooled, const std::vector<std::complex<float>>& x, const std::vector<Gnss_Synchro>& acq)
+PoolRun run_tracking_blocks(bool pooled, const std::vector<std::complex<float>>& x, const std::vector<Gnss_Synchro>& acq,
+    const std::string& dump_filename)
 {
     InMemoryConfiguration config;
     config.set_property("GNSS-SDR.internal_fs_sps", "4000000");
@@ -1035,6 +1039,11 @@ PoolRun run_tracking_blocks(bool pooled, const std::vector<std::complex<float>>&
     config.set_property("Tracking_1C.pull_in_time_s", "0");
     config.set_property("Channels_1C.count", std::to_string(acq.size()));
     if (pooled) config.set_property("Tracking_1C.mi355x_pool", "true");
+    if (!dump_filename.empty())
+        {
+            config.set_property("Tracking_1C.dump", "true");
+            config.set_property("Tracking_1C.dump_filename", dump_filename);
+        }
     const size_t n = acq.size();
     std::vector<std::unique_ptr<TrackingInterface>> trk;
     std::vector<Gnss_Synchro> gs(acq);
@@ -1078,7 +1087,60 @@ PoolRun run_tracking_blocks(bool pooled, const std::vector<std::complex<float>>&
                 }
         }
     r.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    trk.clear();  // closes the dump files
     return r;
+}
+
+std::vector<char> read_file(const std::string& path)
+{
+    std::ifstream f(path, std::ios::binary);
+    return std::vector<char>((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+}
+
+// The reference's tracking dump (log_data, dll_pll_veml_tracking.cc:1403-1500) as the
+// adapters write it: one 108-byte record per logged call, decoded against the
+// engine's records, and the pooled blocks' files byte-identical to the per-channel ones.
+void check_tracking_dump(const PoolRun& one, const std::string& stem_one, const std::string& stem_pool,
+    const std::vector<Gnss_Synchro>& acq)
+{
+    bool sizes = true, fields = true, same = true;
+    size_t logged_total = 0;
+    for (size_t c = 0; c < acq.size(); ++c)
+        {
+            const auto a = read_file(stem_one + std::to_string(c) + ".dat");
+            const auto b = read_file(stem_pool + std::to_string(c) + ".dat");
+            std::vector<const gsdr_trk_epoch*> logged;
+            for (const auto& r : one.recs[c])
+                if (r.flags & GSDR_TRK_F_LOGGED) logged.push_back(&r);
+            logged_total += logged.size();
+            sizes = sizes && a.size() == logged.size() * TrackingDump::kRecordBytes && !logged.empty();
+            same = same && a == b;
+            for (size_t i = 0; fields && i < logged.size() && (i + 1) * TrackingDump::kRecordBytes <= a.size(); ++i)
+                {
+                    const char* p = a.data() + i * TrackingDump::kRecordBytes;
+                    float f[7];
+                    uint64_t stamp;
+                    uint32_t prn;
+                    float pll_err, cn0, evm;
+                    std::memcpy(f, p, sizeof(f));
+                    std::memcpy(&stamp, p + 28, 8);
+                    std::memcpy(&pll_err, p + 36 + 5 * 4, 4);
+                    std::memcpy(&cn0, p + 36 + 9 * 4, 4);
+                    std::memcpy(&prn, p + 36 + 12 * 4 + 8, 4);
+                    std::memcpy(&evm, p + 104, 4);
+                    const gsdr_trk_epoch& r = *logged[i];
+                    fields = fields && f[0] == 0.0F && f[4] == 0.0F && f[2] == r.log_accu[2] && f[1] == r.log_accu[1] &&
+                             f[5] == r.taps[2] && f[6] == r.taps[3] &&
+                             stamp == r.sample_counter + static_cast<uint64_t>(r.consumed) &&
+                             pll_err == r.carr_phase_error_hz && cn0 == static_cast<float>(r.cn0_db_hz) &&
+                             prn == acq[c].PRN && evm == static_cast<float>(r.evm) && r.log_accu[2] > 0.0F;
+                }
+        }
+    EXPECT(sizes, "tracking dump: one 108-byte record per logged call in <dump_filename stem><channel>.dat");
+    EXPECT(fields, "tracking dump: records decode to the engine's log_data fields");
+    EXPECT(same, "tracking dump: pooled blocks write the per-channel blocks' bytes");
+    std::printf("tracking dump: %zu logged calls over %zu channels (%s<ch>.dat)\n", logged_total, acq.size(),
+        stem_one.c_str());
 }
 
 void test_pooled_tracking()
@@ -1106,8 +1168,12 @@ void test_pooled_tracking()
         }
     // pull_in_time_s = 0 ends the pull-in transitory after 1 s, then bit sync and outputs
     const auto x = synth_stream(sats, fs, static_cast<size_t>(fs * 1.7), 23, sigma);
-    const PoolRun one = run_tracking_blocks(false, x, acq);
-    const PoolRun pool = run_tracking_blocks(true, x, acq);
+    const std::string dir = (std::filesystem::temp_directory_path() / ("gsdr_selftest_" + std::to_string(getpid()))).string();
+    const PoolRun one = run_tracking_blocks(false, x, acq, dir + "/one/trk_dump.dat");
+    const PoolRun pool = run_tracking_blocks(true, x, acq, dir + "/pool/trk_dump.dat");
+    check_tracking_dump(one, dir + "/one/trk_dump", dir + "/pool/trk_dump", acq);
+    std::error_code ec;
+    std::filesystem::remove_all(dir, ec);
     bool same = true;
     for (int c = 0; c < 6; ++c)
         {

@@ -422,6 +422,12 @@ typedef struct gsdr_trk_epoch
     float data_prompt[2];          /* pilot tracking: the data-component prompt of the call (d_Prompt_Data[0]) */
     float carrier_rate;            /* high_dyn: (float)d_carrier_phase_rate_step_rad after the call [rad/sample^2] */
     float code_rate;               /* high_dyn: (float)d_code_phase_rate_step_chips after the call [chips/sample^2] */
+    /* log_data (dll_pll_veml_tracking.cc:1403-1500), valid when flags has GSDR_TRK_F_LOGGED: the
+     * accumulator magnitudes |VE|, |E|, |P|, |L|, |VL| (VE/VL 0 without VEML) and the loop
+     * errors as the dump writes them (static_cast<float> of the double members) */
+    float log_accu[5];
+    float carr_phase_error_hz, carr_error_filt_hz, code_error_chips, code_error_filt_chips;
+    int32_t reserved;              /* 0 (keeps the record free of padding bytes) */
 } gsdr_trk_epoch;
 
 #define GSDR_TRK_F_VALID_OUTPUT 1 /* Flag_valid_symbol_output: a Gnss_Synchro was emitted */
@@ -431,6 +437,8 @@ typedef struct gsdr_trk_epoch
 #define GSDR_TRK_F_OVERRUN 16     /* with LOSS_OF_LOCK: the channel's next call starts before the oldest
                                      input item given (the ring moved past a stalled channel); the
                                      record carries the channel's position, the channel is in state 0 */
+#define GSDR_TRK_F_LOGGED 32      /* the reference calls log_data() for this call (state 2 locked; states
+                                     3/4 with a completed data symbol): the record's log_* fields are set */
 
 void gsdr_trk_conf_default(gsdr_trk_conf* conf);
 int gsdr_trk_create(int device, const gsdr_trk_conf* conf, gsdr_trk** out);

@@ -32,10 +32,11 @@ TRK_EPOCH_DTYPE = np.dtype([
     ("rem_carr_phase_rad", "f4"), ("flags", "i4"), ("carrier_doppler_hz", "f8"), ("code_freq_chips", "f8"),
     ("rem_code_phase_samples", "f8"), ("acc_carrier_phase_rad", "f8"), ("cn0_db_hz", "f8"),
     ("carrier_lock_test", "f8"), ("prompt_i", "f8"), ("prompt_q", "f8"), ("evm", "f8"), ("data_prompt", "f4", (2,)),
-    ("carrier_rate", "f4"), ("code_rate", "f4")], align=True)
-assert TRK_EPOCH_DTYPE.itemsize == 152
+    ("carrier_rate", "f4"), ("code_rate", "f4"), ("log_accu", "f4", (5,)), ("carr_phase_error_hz", "f4"),
+    ("carr_error_filt_hz", "f4"), ("code_error_chips", "f4"), ("code_error_filt_chips", "f4"), ("reserved", "i4")], align=True)
+assert TRK_EPOCH_DTYPE.itemsize == 192
 
-F_VALID_OUTPUT, F_LOSS_OF_LOCK, F_PLL_180, F_BIT_SYNC = 1, 2, 4, 8
+F_VALID_OUTPUT, F_LOSS_OF_LOCK, F_PLL_180, F_BIT_SYNC, F_LOGGED = 1, 2, 4, 8, 32
 
 _init = False
 

@@ -1088,6 +1088,18 @@ static void save_correlation_results(orc_trk* t)
     t->cloop = t->track_pilot ? 0 : 1;
 }
 
+/* log_data (:1403-1500): the dump's accumulator magnitudes, std::abs<float> of the
+ * complex accumulators (VE/VL written as 0 without VEML) */
+static void log_data(const orc_trk* t, gsdr_trk_epoch* r)
+{
+    r->flags |= GSDR_TRK_F_LOGGED;
+    r->log_accu[0] = t->veml ? hypotf(t->VE_accu.re, t->VE_accu.im) : 0.0F;
+    r->log_accu[1] = hypotf(t->E_accu.re, t->E_accu.im);
+    r->log_accu[2] = hypotf(t->P_accu.re, t->P_accu.im);
+    r->log_accu[3] = hypotf(t->L_accu.re, t->L_accu.im);
+    r->log_accu[4] = t->veml ? hypotf(t->VL_accu.re, t->VL_accu.im) : 0.0F;
+}
+
 static int trk_call(orc_trk* t, const float* in, const float* taps_in, uint64_t nitems_read, gsdr_trk_epoch* r)
 {
     memset(r, 0, sizeof(*r));
@@ -1130,6 +1142,7 @@ static int trk_call(orc_trk* t, const float* in, const float* taps_in, uint64_t 
                         int next_state = 0;
                         run_dll_pll(t);
                         update_tracking_vars(t);
+                        log_data(t, r);
                         if (!t->pull_in_transitory)
                             {
                                 if (t->secondary || t->symbols_per_bit > 1)
@@ -1189,6 +1202,7 @@ static int trk_call(orc_trk* t, const float* in, const float* taps_in, uint64_t 
                 update_tracking_vars(t);
                 if (t->current_data_symbol == 0)
                     {
+                        log_data(t, r);
                         fill_output(t, r);
                         t->P_data_accu = (tcf){0.0F, 0.0F};
                     }
@@ -1221,6 +1235,7 @@ static int trk_call(orc_trk* t, const float* in, const float* taps_in, uint64_t 
                             }
                         if (t->current_data_symbol == 0)
                             {
+                                log_data(t, r);
                                 fill_output(t, r);
                                 t->P_data_accu = (tcf){0.0F, 0.0F};
                             }
@@ -1241,6 +1256,10 @@ static int trk_call(orc_trk* t, const float* in, const float* taps_in, uint64_t 
     r->data_prompt[1] = t->prompt_data.im;
     r->carrier_rate = (float)t->carrier_phase_rate_step_rad;
     r->code_rate = (float)t->code_phase_rate_step_chips;
+    r->carr_phase_error_hz = (float)t->carr_phase_error_hz;
+    r->carr_error_filt_hz = (float)t->carr_error_filt_hz;
+    r->code_error_chips = (float)t->code_error_chips;
+    r->code_error_filt_chips = (float)t->code_error_filt_chips;
     if (loss_of_lock) r->flags |= GSDR_TRK_F_LOSS_OF_LOCK;
     if (t->flag_pll_180) r->flags |= GSDR_TRK_F_PLL_180;
     r->consumed = t->current_prn_length_samples;

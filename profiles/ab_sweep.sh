@@ -15,7 +15,7 @@ i=0
 for SETTING in "$@"; do
   echo "== [$i] $SETTING :: $CMD"
   timeout -k 10 300 env $SETTING $CMD > "$OUT/ab_$i.json" 2> "$OUT/ab_$i.err" || { tail -5 "$OUT/ab_$i.err"; exit 1; }
-  python3 - "$OUT/ab_$i.json" "$SETTING" <<'PY'
+  PYTHONIOENCODING=utf-8 python3 - "$OUT/ab_$i.json" "$SETTING" <<'PY'
 import json, sys
 for line in open(sys.argv[1]):
     line = line.strip()
@@ -24,7 +24,7 @@ for line in open(sys.argv[1]):
     d = json.loads(line)
     r = d.get("roofline", {})
     print(sys.argv[2], "|", d.get("stage", d.get("metric", ""))[:60], "|", d.get("value", d.get("msps")),
-          "| frac", r.get("frac"))
+          "| frac", r.get("frac"), "| launch us", r.get("avg_launch_us"))
 PY
   i=$((i + 1))
 done

@@ -82,16 +82,23 @@ def test_beidou_b1i_synthetic_batch(fs):
     assert set(vis) <= det
 
 
-@pytest.mark.parametrize("split", ["1", "0", "2"])
+@pytest.mark.parametrize("split", ["1", "0", "2", "id5", "id6"])
 @pytest.mark.parametrize("fs,N,pfa", [(8000000, 32000, 0.01), (25000000, 25000, 0.0), (8000000, 64000, 0.01),
                                       (25000000, 100000, 0.01), (25000000, 25000, 0.01), (25000000, 100000, 0.0)])
 def test_large_fft_four_step(monkeypatch, fs, N, pfa, split):
     """N beyond one workgroup's LDS: Galileo E1 at 8 Msps (4 ms: 32000; 8 ms:
     64000), BeiDou B1I at 25 Msps (1 ms: 25000), Galileo at 25 Msps (100000) --
     configs C4/C5 -- on every correlate path: GSDR_ACQ_SPLIT=1 (default: the split
-    register four-step for 25000 / 32000, the packed four-step for 64000 / 100000),
-    0 (the packed four-step everywhere), 2 (the split also with ROUT = 2 / 4).
+    register four-step for 25000 / 32000 / 64000, the packed four-step for 100000),
+    0 (the packed four-step everywhere), 2 (the split also for 100000 = 4 x 25000),
+    id5 / id6 (32000 = 2 x 16000, 64000 = 4 x 16000).
     Parity with the oracle grid statistics."""
+    if split.startswith("id"):
+        # a forced split of this N (acq_split.hip: 5 = 2 x 16000, 6 = 4 x 16000)
+        if {"id5": 32000, "id6": 64000}[split] != N:
+            pytest.skip("split id for another FFT size")
+        monkeypatch.setenv("GSDR_ACQ_SPLIT_ID", split[2:])
+        split = "2"
     monkeypatch.setenv("GSDR_ACQ_SPLIT", split)
     dmax, dstep = 2000, 500
     rng = np.random.default_rng(N)

@@ -86,6 +86,12 @@ def _replay_check(g, oracle_channel, tag):
         assert d <= tol, (tag, f, d)
     dr = np.abs(np.angle(np.exp(1j * (g["rem_carr_phase_rad"].astype(np.float64) - o["rem_carr_phase_rad"]))))
     assert dr.max() <= 5e-2, (tag, dr.max())  # integrates the float Doppler drift above
+    # log_data's fields (the tracking dump): accumulator magnitudes and loop errors
+    np.testing.assert_allclose(g["log_accu"], o["log_accu"], rtol=1e-5, atol=1e-3, err_msg=tag)
+    for f, tol in (("carr_phase_error_hz", 1e-3), ("carr_error_filt_hz", 1e-2), ("code_error_chips", 1e-4),
+                   ("code_error_filt_chips", 1e-3)):
+        d = np.max(np.abs(g[f].astype(np.float64) - o[f]))
+        assert d <= tol, (tag, f, d)
 
 
 def _free_check(g, o, tag):

@@ -183,3 +183,55 @@ def test_extended_integration_cycle():
     assert np.all((recs["flags"][sync + 1:] & trk.F_VALID_OUTPUT) != 0)  # one 4 ms symbol per call
     assert abs(np.mean(recs[-60:]["carrier_doppler_hz"]) - sat.doppler_hz) < 2.0
     assert not np.any(recs["flags"] & trk.F_LOSS_OF_LOCK)
+
+
+def test_log_data_points_and_dump(tmp_path):
+    """log_data (dll_pll_veml_tracking.cc:1403-1500) is called in state 2 after every
+    locked loop update and in states 3/4 when a data symbol completes; the engine
+    flags those calls (TRK_F_LOGGED) and the dump file holds one 108-byte record for
+    each.  Galileo E1 pilot with 4-symbol extended integration covers all three states."""
+    import gsdr
+    fs = 4.0e6
+    c = _conf_sig(fs, 1, 1)
+    c["extend_correlation_symbols"] = 4
+    c["pll_bw_narrow_hz"] = 5.0
+    c["dll_bw_narrow_hz"] = 0.25
+    c["early_late_space_narrow_chips"] = 0.06
+    c["very_early_late_space_narrow_chips"] = 0.25
+    sat = synth.GalileoSatellite(11, 1234.5, 1000.3, 50.0, 0.7)
+    iq = synth.gal_e1_iq(fs, int(1.2 * fs), [sat], seed_offset=5)
+    ch = trk.Channel(c)
+    tau = sat.code_delay_chips / (1.023e6 * (1 + sat.doppler_hz / 1.57542e9)) * fs
+    first = ch.start(synth.gal_e1_sinboc11(11, pilot=True), float(round(tau) % 16000), 1250.0, 0, 0, prn=11,
+                     data_code=synth.gal_e1_sinboc11(11))
+    recs, _ = ch.run(iq, 0, first, 1000)
+    logged = (recs["flags"] & trk.F_LOGGED) != 0
+    lost = (recs["flags"] & trk.F_LOSS_OF_LOCK) != 0
+    valid = (recs["flags"] & trk.F_VALID_OUTPUT) != 0
+    want = ((recs["state"] == 2) & ~lost) | (np.isin(recs["state"], (3, 4)) & valid)
+    np.testing.assert_array_equal(logged, want)
+    assert np.count_nonzero(logged & (recs["state"] == 3)) > 10
+    # state 2: the accumulators are the call's taps (VE, E, P, L, VL)
+    s2 = recs[(recs["state"] == 2) & logged]
+    taps = s2["taps"].reshape(-1, 5, 2)
+    np.testing.assert_allclose(s2["log_accu"], np.hypot(taps[..., 0], taps[..., 1]), rtol=1e-6)
+    # state 3 runs no loop update: its errors are the previous update's
+    i3 = np.nonzero(recs["state"] == 3)[0]
+    i3 = i3[i3 > 0]
+    for f in ("carr_phase_error_hz", "code_error_chips", "code_error_filt_chips"):
+        np.testing.assert_array_equal(recs[f][i3], recs[f][i3 - 1])
+    assert np.all(recs["code_error_filt_chips"][recs["state"] == 4] != 0.0)
+    # the dump records and their file round trip
+    d = gsdr.trk_dump_records(recs, fs, 11, 123.25, 1250.0, veml=True, track_pilot=True)
+    assert len(d) == np.count_nonzero(logged)
+    path = tmp_path / "trk_dump11.dat"
+    d.tofile(path)
+    assert path.stat().st_size == 108 * len(d)
+    back = gsdr.read_trk_dump(path)
+    np.testing.assert_array_equal(back, d)
+    r = recs[logged]
+    np.testing.assert_array_equal(back["PRN_start_sample_count"], r["sample_counter"] + r["consumed"].astype(np.uint64))
+    np.testing.assert_array_equal(back["Prompt_I"], r["data_prompt"][:, 0])
+    np.testing.assert_array_equal(back["abs_P"], r["log_accu"][:, 2])
+    np.testing.assert_array_equal(back["carr_error_hz"], r["carr_phase_error_hz"])
+    assert np.all(back["PRN"] == 11) and np.all(back["acq_code_phase_samples"] == np.float32(123.25))

@@ -67,8 +67,42 @@ def as_json(root):
     return out
 
 
+def kernel_durations(root):
+    """Average duration (us) per kernel from the passes' --stats summaries."""
+    acc = defaultdict(list)
+    for f in glob.glob(os.path.join(root, "*", "**", "*kernel_stats.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            acc[r["Name"]].append(float(r["AverageNs"]) / 1e3)
+    return {k: sum(v) / len(v) for k, v in acc.items()}
+
+
+def cfg_json(root):
+    """Every kernel of a configuration driver's passes: average duration, counters,
+    HBM bytes per launch (FETCH_SIZE doubled, both KiB)."""
+    names = set()
+    for f in glob.glob(os.path.join(root, "*", "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            names.add(r["Kernel_Name"])
+    dur = kernel_durations(root)
+    out = {}
+    for full in sorted(names):
+        short = full.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
+        s = summarise(root, full)
+        k = {"counters": {c: round(v, 1) for c, v in sorted(s.items())}}
+        if full in dur:
+            k["avg_us"] = round(dur[full], 1)
+        if "FETCH_SIZE" in s and "WRITE_SIZE" in s:
+            k["hbm_read_bytes_per_launch"] = 2.0 * s["FETCH_SIZE"] * 1024.0
+            k["hbm_write_bytes_per_launch"] = s["WRITE_SIZE"] * 1024.0
+            k["hbm_bytes_per_launch"] = k["hbm_read_bytes_per_launch"] + k["hbm_write_bytes_per_launch"]
+        out[short[:140]] = k
+    return out
+
+
 if __name__ == "__main__":
-    if sys.argv[1] == "--json":
+    if sys.argv[1] == "--cfg-json":
+        print(json.dumps(cfg_json(sys.argv[2]), indent=1))
+    elif sys.argv[1] == "--json":
         print(json.dumps(as_json(sys.argv[2]), indent=1))
     else:
         root, match = sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "correlate"

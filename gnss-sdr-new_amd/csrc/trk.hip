@@ -61,7 +61,8 @@ constexpr int kWinCore = kSpl * kTrkThreads;  // 4096: the next call's window st
 constexpr int kHalo = 16;                     // slack around the predicted next start
 constexpr int kStreamRow = 64 * 16;           // bytes one wave's global_load_lds_dwordx4 writes
 constexpr int kCodeMargin = 32;              // replica samples copied on each side of the LDS replica
-constexpr int kTimingSlots = 8;              // GSDR_TRK_TIMING record per call
+constexpr int kTimingSlots = 9;              // GSDR_TRK_TIMING record per call: 8 stamps + stream-wait ticks
+constexpr int kStampSlots = 8;
 
 // MATH_CONSTANTS.h:47-50
 constexpr double kGnssPi = 3.1415926535898;
@@ -1116,7 +1117,7 @@ __device__ __forceinline__ void correlate_call(const void* __restrict__ iq, cons
 template <int IT, int KT, bool DATA>
 __device__ __forceinline__ void correlate_call_stream(const void* __restrict__ iq, uint64_t iq_items, char* sb,
     int sbuf_bytes, int chunk, bool pf_ok, uintptr_t pf_start, const float* s_code, const float* s_data, const Prep& p,
-    int vl, int L, const float (&sh_rem)[kMaxTrkTaps], float2& ph, float2 (&acc)[kMaxTrkTaps + 1])
+    int vl, int L, const float (&sh_rem)[kMaxTrkTaps], float2& ph, float2 (&acc)[kMaxTrkTaps + 1], bool probe, uint64_t& swait)
 {
     constexpr int isz = item_bytes<IT>();
     const uint64_t nbytes = iq_items * (uint64_t)isz;
@@ -1131,8 +1132,10 @@ __device__ __forceinline__ void correlate_call_stream(const void* __restrict__ i
             // wave in vmcnt: every issuing wave drains its own DMA (chunk j, and for
             // j == 0 the prefetch waves 1.. issued during the previous loop update)
             // before the barrier hands the buffer to the other waves
+            const uint64_t w0 = probe ? wall_clock64() : 0;
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
+            if (probe) swait += wall_clock64() - w0;
             if (j + 1 < nch)
                 bstart[(j + 1) & 1] =
                     stream_fetch(iq, nbytes, (p.off + (int64_t)(j + 1) * chunk) * isz, chunk * isz, sb + ((j + 1) & 1) * sbuf_bytes, 0);
@@ -1297,7 +1300,7 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
     uint32_t e = 0;
     for (;; ++e)
         {
-            uint64_t tm0 = 0, tm1 = 0, tm2 = 0;
+            uint64_t tm0 = 0, tm1 = 0, tm2 = 0, swait = 0;
             if (timing && tid == 0) tm0 = wall_clock64();
             if (tid == 0 && e == 0)
                 {
@@ -1350,15 +1353,16 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                 }
             else if (streamed)
                 {
+                    const bool sw = timing && tid == 0;
                     if (K <= 3)
                         correlate_call_stream<IT, 3, false>(iq, iq_items, s_sb, sbuf_bytes, stream_chunk, p.pf_ok, pf_start,
-                            s_code, s_data, p, vl, L, sh_rem, ph, acc);
+                            s_code, s_data, p, vl, L, sh_rem, ph, acc, sw, swait);
                     else if (!data)
                         correlate_call_stream<IT, kMaxTrkTaps, false>(iq, iq_items, s_sb, sbuf_bytes, stream_chunk, p.pf_ok,
-                            pf_start, s_code, s_data, p, vl, L, sh_rem, ph, acc);
+                            pf_start, s_code, s_data, p, vl, L, sh_rem, ph, acc, sw, swait);
                     else
                         correlate_call_stream<IT, kMaxTrkTaps, true>(iq, iq_items, s_sb, sbuf_bytes, stream_chunk, p.pf_ok,
-                            pf_start, s_code, s_data, p, vl, L, sh_rem, ph, acc);
+                            pf_start, s_code, s_data, p, vl, L, sh_rem, ph, acc, sw, swait);
                 }
             else if (K <= 3)
                 correlate_call<IT, 3, false>(iq, s_win, s_code, s_data, p, vl, L, sh_rem, ph, acc);
@@ -1505,6 +1509,7 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                                     tr[5] = pr[1] ? pr[1] : tr[4];
                                     tr[6] = pr[2] ? pr[2] : tr[5];
                                     tr[7] = wall_clock64();
+                                    tr[8] = swait;
                                 }
                         }
                     t.next_sample = n_read + (uint64_t)(int64_t)t.current_prn_length_samples;
@@ -2015,20 +2020,21 @@ void gsdr_trk_destroy(gsdr_trk* k)
                     for (uint32_t e = 0; e < cnt[c] && e < me; ++e)
                         {
                             const uint64_t* r = &tm[((size_t)c * me + e) * kTimingSlots];
-                            for (int q = 0; q + 1 < kTimingSlots; ++q)
+                            for (int q = 0; q + 1 < kStampSlots; ++q)
                                 if (r[q + 1] >= r[q]) k->tsum[q] += (double)(r[q + 1] - r[q]);
                             if (e + 1 < cnt[c] && e + 1 < me)
                                 {
                                     const uint64_t next0 = tm[((size_t)c * me + e + 1) * kTimingSlots];
-                                    if (next0 >= r[kTimingSlots - 1]) k->tsum[kTimingSlots - 1] += (double)(next0 - r[kTimingSlots - 1]);
+                                    if (next0 >= r[kStampSlots - 1]) k->tsum[kStampSlots - 1] += (double)(next0 - r[kStampSlots - 1]);
                                 }
+                            k->tsum[kStampSlots] += (double)r[kStampSlots];  // stream-wait: a duration
                             k->tcount++;
                         }
         }
     if (k->timing_on && k->tcount)
         {
             static const char* names[kTimingSlots] = {"prep", "correlate", "tap-sum", "cn0-lock", "dll-pll", "update-vars",
-                "rest", "window-write"};
+                "rest", "window-write", "(correlate's stream-wait)"};
             std::fprintf(stderr, "gsdr_trk timing: %llu calls, %s ticks per call:", (unsigned long long)k->tcount,
                 "wall_clock64 (100 MHz)");
             for (int q = 0; q < kTimingSlots; ++q) std::fprintf(stderr, " %s %.0f", names[q], k->tsum[q] / k->tcount);

@@ -105,4 +105,25 @@ __device__ __forceinline__ float wave_max(float v)
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
 
+// Wave64 sum by the same DPP lane moves (no LDS round trips, unlike __shfl_xor's
+// ds_bpermute): the disabled rows of the two row broadcasts read 0, so they keep
+// their value.  The total is valid in lane 63 only (rows 0..2 hold partial sums).
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ float dpp_add_step(float x)
+{
+    const int o = __builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, ROW_MASK, 0xf, false);
+    return x + __int_as_float(o);
+}
+
+__device__ __forceinline__ float wave_sum_lane63(float v)
+{
+    v = dpp_add_step<0xb1, 0xf>(v);   // quad_perm [1,0,3,2]
+    v = dpp_add_step<0x4e, 0xf>(v);   // quad_perm [2,3,0,1]
+    v = dpp_add_step<0x141, 0xf>(v);  // row_half_mirror
+    v = dpp_add_step<0x140, 0xf>(v);  // row_mirror
+    v = dpp_add_step<0x142, 0xa>(v);  // row_bcast:15 into rows 1 and 3
+    v = dpp_add_step<0x143, 0xc>(v);  // row_bcast:31 into rows 2 and 3
+    return v;
+}
+
 }  // namespace gsdr

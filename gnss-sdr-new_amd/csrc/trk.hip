@@ -1375,15 +1375,12 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                 {
                     if (k < K || (k == kMaxTrkTaps && data))
                         {
-#pragma unroll
-                            for (int off = 32; off > 0; off >>= 1)
-                                {
-                                    acc[k].x += __shfl_xor(acc[k].x, off);
-                                    acc[k].y += __shfl_xor(acc[k].y, off);
-                                }
+                            // wave sums by DPP (the total in lane 63)
+                            acc[k].x = gsdr::wave_sum_lane63(acc[k].x);
+                            acc[k].y = gsdr::wave_sum_lane63(acc[k].y);
                         }
                 }
-            if (lane == 0)
+            if (lane == 63)
                 {
 #pragma unroll
                     for (int k = 0; k <= kMaxTrkTaps; ++k) s_red[wave][k] = acc[k];

@@ -221,18 +221,14 @@ __device__ __forceinline__ void chunk_accumulate(const gsdr_corr_job& job, const
                 }
             if (!HD) ph = make_float2(ph.x * wstep.x - ph.y * wstep.y, ph.x * wstep.y + ph.y * wstep.x);
         }
-    // wave64 reduction into s_red[wave]
+    // wave64 reduction into s_red[wave]: DPP sums, the total in lane 63
 #pragma unroll
     for (int k = 0; k < kMaxTaps; ++k)
         {
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1)
-                {
-                    acc[k].x += __shfl_xor(acc[k].x, off);
-                    acc[k].y += __shfl_xor(acc[k].y, off);
-                }
+            acc[k].x = gsdr::wave_sum_lane63(acc[k].x);
+            acc[k].y = gsdr::wave_sum_lane63(acc[k].y);
         }
-    if ((threadIdx.x & 63) == 0)
+    if ((threadIdx.x & 63) == 63)
         {
 #pragma unroll
             for (int k = 0; k < kMaxTaps; ++k) s_red[threadIdx.x >> 6][k] = acc[k];

@@ -1387,22 +1387,36 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                 }
             __syncthreads();  // partials visible; every read of the LDS window done
             if (timing && tid == 0) tm2 = wall_clock64();
-            // ---- fetch the window the next call most likely reads: [off + vl - kHalo/2, +kWinCore+kHalo)
-            float2 wv[kSpl];
-            float2 wh = make_float2(0.f, 0.f);
+            // ---- stage the window the next call most likely reads, [off + vl - kHalo/2,
+            // +kWinCore+kHalo), into LDS: waves 1.. only, while wave 0 runs the loop
+            // update (every read of the current window is done), so wave 0 issues no
+            // global loads that a vmcnt wait inside its update would wait for
             const int64_t nb = p.off + vl - kHalo / 2;
-            if (use_window)
+            if (use_window && wave != 0)
                 {
+                    // two batches of loads in flight (the update hides their latency)
+                    constexpr int kW = kTrkThreads - 64;
+                    constexpr int kIt = (kWinCore + kHalo + kW - 1) / kW;
+                    constexpr int kB = (kIt + 1) / 2;
 #pragma unroll
-                    for (int j = 0; j < kSpl; ++j)
+                    for (int j0 = 0; j0 < kIt; j0 += kB)
                         {
-                            const int64_t i = nb + tid + j * kTrkThreads;
-                            wv[j] = (i >= 0 && (uint64_t)i < iq_items) ? load_iq<IT>(iq, i) : make_float2(0.f, 0.f);
-                        }
-                    if (tid < kHalo)
-                        {
-                            const int64_t i = nb + kWinCore + tid;
-                            wh = (i >= 0 && (uint64_t)i < iq_items) ? load_iq<IT>(iq, i) : make_float2(0.f, 0.f);
+                            float2 wv[kB];
+#pragma unroll
+                            for (int j = 0; j < kB; ++j)
+                                {
+                                    const int i = tid - 64 + (j0 + j) * kW;
+                                    const int64_t g = nb + i;
+                                    wv[j] = (j0 + j < kIt && i < kWinCore + kHalo && g >= 0 && (uint64_t)g < iq_items)
+                                                ? load_iq<IT>(iq, g)
+                                                : make_float2(0.f, 0.f);
+                                }
+#pragma unroll
+                            for (int j = 0; j < kB; ++j)
+                                {
+                                    const int i = tid - 64 + (j0 + j) * kW;
+                                    if (j0 + j < kIt && i < kWinCore + kHalo) s_win[i] = wv[j];
+                                }
                         }
                 }
             if (streamed)
@@ -1517,13 +1531,7 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                         stream_chunk, use_window ? nb : win_base, streamed ? nb : pf_first);
                     if (lane == 0) prep = pn;
                 }
-            if (use_window)
-                {
-#pragma unroll
-                    for (int j = 0; j < kSpl; ++j) s_win[tid + j * kTrkThreads] = wv[j];
-                    if (tid < kHalo) s_win[kWinCore + tid] = wh;
-                    win_base = nb;
-                }
+            if (use_window) win_base = nb;
             // the next iteration's prep barrier orders the window writes and s_red reuse
         }
     __syncthreads();

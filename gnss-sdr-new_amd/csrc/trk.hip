@@ -712,7 +712,46 @@ __device__ __forceinline__ void tprobe(bool on, uint64_t (&pr)[3], int i)
     if (on) pr[i] = wall_clock64();
 }
 
-__device__ inline void after_correlation(const TrkConst& c, TrkHot& t, TrkChan* gc, LoopFilter& lf, float2* pbuf,
+// run_dll_pll of a call computed speculatively by wave 1 (states 2 and 4): the
+// discriminators and loop filters read nothing the CN0 estimator and lock detector
+// write, so wave 1 runs them on its own copy of the state -- into the code loop
+// filter slot that is not current -- while wave 0 evaluates the lock; wave 0 takes
+// the results when the call stays locked (and drops them on a loss of lock).
+// Same operations on the same values: the loop is bit-identical to run_dll_pll on
+// wave 0.
+struct DllPllSpec
+{
+    double carrier_doppler_hz, code_freq_chips;
+    float2 P_accu_old;
+    float cf_w, cf_x;
+    float log_err[4];
+};
+
+struct SpecLink
+{
+    DllPllSpec* res;   // LDS
+    int* ready;        // LDS: the call index whose results res holds
+    LoopFilter* lfs;   // LDS: the code loop filter's two slots
+    int* lfi_lds;      // LDS: the current slot (read by wave 1 at the start of a call)
+    int lfi;           // wave 0: the current slot
+    int e;             // wave 0: this call's index
+};
+
+__device__ inline void take_dll_pll(TrkHot& t, SpecLink& sl)
+{
+    while (__hip_atomic_load(sl.ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != sl.e)
+        __builtin_amdgcn_s_sleep(1);
+    const DllPllSpec r = *sl.res;
+    t.carrier_doppler_hz = r.carrier_doppler_hz;
+    t.code_freq_chips = r.code_freq_chips;
+    t.P_accu_old = r.P_accu_old;
+    t.cf_w = r.cf_w;
+    t.cf_x = r.cf_x;
+    for (int i = 0; i < 4; ++i) t.log_err[i] = r.log_err[i];
+    sl.lfi ^= 1;  // wave 1 filtered into the other slot
+}
+
+__device__ inline void after_correlation(const TrkConst& c, TrkHot& t, TrkChan* gc, SpecLink& sl, float2* pbuf,
     float (*scratch)[kMaxCn0], const float2 (&taps)[kMaxTrkTaps + 1], const float2 (&epl)[3], uint64_t nitems_read,
     int lane, EpochOut& o, bool tm, uint64_t (&pr)[3])
 {
@@ -745,7 +784,7 @@ __device__ inline void after_correlation(const TrkConst& c, TrkHot& t, TrkChan* 
             else
                 {
                     int next_state = 0;
-                    run_dll_pll(c, t, lf);
+                    take_dll_pll(t, sl);
                     tprobe(tm, pr, 1);
                     update_tracking_vars(c, t, gc);
                     tprobe(tm, pr, 2);
@@ -774,6 +813,7 @@ __device__ inline void after_correlation(const TrkConst& c, TrkHot& t, TrkChan* 
                                     t.extend_count = 0;
                                     t.corr_time = c.corr_time_ext;
                                     t.state = 3;
+                                    LoopFilter& lf = sl.lfs[sl.lfi];
                                     lf.T = (float)t.corr_time;
                                     lf_update(lf);
                                     lf.bw = c.dll_bw_narrow_hz;
@@ -819,7 +859,7 @@ __device__ inline void after_correlation(const TrkConst& c, TrkHot& t, TrkChan* 
                 }
             else
                 {
-                    run_dll_pll(c, t, lf);
+                    take_dll_pll(t, sl);
                     tprobe(tm, pr, 1);
                     update_tracking_vars(c, t, gc);
                     tprobe(tm, pr, 2);
@@ -1246,7 +1286,10 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
     float* s_data = s_dyn + code_pad + kCodeMargin;
     float2* s_win = reinterpret_cast<float2*>(s_dyn + code_pad + data_pad);
     char* s_sb = reinterpret_cast<char*>(s_dyn + code_pad + data_pad);  // streamed calls: two chunk buffers
-    __shared__ LoopFilter s_lf;
+    __shared__ LoopFilter s_lfs[2];  // code loop filter: current slot and wave 1's speculative one
+    __shared__ int s_lfi;
+    __shared__ DllPllSpec s_spec;
+    __shared__ int s_spec_e;
     __shared__ float2 s_pbuf[kMaxCn0];
     __shared__ __attribute__((aligned(16))) float s_cn[4][kMaxCn0];  // cn0_and_lock's per-element terms
     __shared__ int s_state;
@@ -1268,7 +1311,9 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
     if (tid == 0)
         {
             s_t = gc->h;
-            s_lf = gc->code_filter;
+            s_lfs[0] = gc->code_filter;
+            s_lfi = 0;
+            s_spec_e = -1;
             s_state = s_t.state;
             s_overrun = 0;
         }
@@ -1295,6 +1340,7 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
             }
     }
     int64_t win_base = INT64_MIN;  // absolute-index base of the staged window (uniform)
+    int lfi0 = 0;                  // wave 0: the current code loop filter slot (s_lfi)
     int64_t pf_first = INT64_MIN;  // streamed calls: first sample of the prefetched chunk 0 (uniform)
     uintptr_t pf_start = 0;        // and the byte address its LDS buffer starts at
     uint32_t e = 0;
@@ -1388,14 +1434,15 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
             __syncthreads();  // partials visible; every read of the LDS window done
             if (timing && tid == 0) tm2 = wall_clock64();
             // ---- stage the window the next call most likely reads, [off + vl - kHalo/2,
-            // +kWinCore+kHalo), into LDS: waves 1.. only, while wave 0 runs the loop
-            // update (every read of the current window is done), so wave 0 issues no
-            // global loads that a vmcnt wait inside its update would wait for
+            // +kWinCore+kHalo), into LDS: waves 2.. only, while wave 0 runs the loop
+            // update and wave 1 the speculative DLL/PLL (every read of the current window
+            // is done), so wave 0 issues no global loads that a vmcnt wait inside its
+            // update would wait for
             const int64_t nb = p.off + vl - kHalo / 2;
-            if (use_window && wave != 0)
+            if (use_window && wave >= 2)
                 {
                     // two batches of loads in flight (the update hides their latency)
-                    constexpr int kW = kTrkThreads - 64;
+                    constexpr int kW = kTrkThreads - 128;
                     constexpr int kIt = (kWinCore + kHalo + kW - 1) / kW;
                     constexpr int kB = (kIt + 1) / 2;
 #pragma unroll
@@ -1405,7 +1452,7 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
 #pragma unroll
                             for (int j = 0; j < kB; ++j)
                                 {
-                                    const int i = tid - 64 + (j0 + j) * kW;
+                                    const int i = tid - 128 + (j0 + j) * kW;
                                     const int64_t g = nb + i;
                                     wv[j] = (j0 + j < kIt && i < kWinCore + kHalo && g >= 0 && (uint64_t)g < iq_items)
                                                 ? load_iq<IT>(iq, g)
@@ -1414,7 +1461,7 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
 #pragma unroll
                             for (int j = 0; j < kB; ++j)
                                 {
-                                    const int i = tid - 64 + (j0 + j) * kW;
+                                    const int i = tid - 128 + (j0 + j) * kW;
                                     if (j0 + j < kIt && i < kWinCore + kHalo) s_win[i] = wv[j];
                                 }
                         }
@@ -1428,36 +1475,81 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                         (stream_chunk + kHalo) * item_bytes<IT>(), s_sb, 1);
                     pf_first = nb;
                 }
+            // lane k sums tap k over the waves in wave order (one batch of LDS reads
+            // instead of a serial read per partial), then every lane takes the totals
+            // by readlane; E/P/L are the same sums
+            auto tap_totals = [&](float2 (&taps)[kMaxTrkTaps + 1], float2 (&epl)[3]) {
+                float2 mine = make_float2(0.f, 0.f);
+                if (lane <= kMaxTrkTaps)
+                    {
+                        float2 v[kTrkThreads / 64];
+#pragma unroll
+                        for (int w = 0; w < kTrkThreads / 64; ++w) v[w] = s_red[w][lane];
+#pragma unroll
+                        for (int w = 0; w < kTrkThreads / 64; ++w)
+                            {
+                                mine.x += v[w].x;
+                                mine.y += v[w].y;
+                            }
+                    }
+#pragma unroll
+                for (int k = 0; k <= kMaxTrkTaps; ++k)
+                    taps[k] = (k < K || (k == kMaxTrkTaps && data)) ? make_float2(lane_f(mine.x, k), lane_f(mine.y, k))
+                                                                   : make_float2(0.f, 0.f);
+                const int ix[3] = {c.iE, c.iP, c.iL};
+#pragma unroll
+                for (int q = 0; q < 3; ++q) epl[q] = make_float2(lane_f(mine.x, ix[q]), lane_f(mine.y, ix[q]));
+            };
+            if (wave == 1)
+                {
+                    // this call's DLL/PLL on a copy of the state, into the code loop
+                    // filter slot that is not current (take_dll_pll)
+                    TrkHot t1 = s_t;
+                    if (t1.state == 2 || t1.state == 4)
+                        {
+                            float2 taps[kMaxTrkTaps + 1], epl[3];
+                            tap_totals(taps, epl);
+                            const uint64_t n_read = t1.next_sample;
+                            if (t1.pull_in_transitory &&
+                                (n_read < c.acq_sample_stamp || n_read - c.acq_sample_stamp >= c.pull_in_span))
+                                t1.pull_in_transitory = 0;
+                            if (t1.state == 2)
+                                {
+                                    if (c.veml)
+                                        {
+                                            t1.VE_accu = taps[0];
+                                            t1.VL_accu = taps[4];
+                                        }
+                                    t1.E_accu = epl[0];
+                                    t1.P_accu = epl[1];
+                                    t1.L_accu = epl[2];
+                                    t1.spc = c.early_late_space_chips;
+                                }
+                            else
+                                save_correlation_results(c, t1, taps, epl);
+                            const int cur = s_lfi;
+                            LoopFilter& lf1 = s_lfs[cur ^ 1];
+                            lf1 = s_lfs[cur];
+                            run_dll_pll(c, t1, lf1);
+                            if (lane == 0)
+                                {
+                                    DllPllSpec r;
+                                    r.carrier_doppler_hz = t1.carrier_doppler_hz;
+                                    r.code_freq_chips = t1.code_freq_chips;
+                                    r.P_accu_old = t1.P_accu_old;
+                                    r.cf_w = t1.cf_w;
+                                    r.cf_x = t1.cf_x;
+                                    for (int i = 0; i < 4; ++i) r.log_err[i] = t1.log_err[i];
+                                    s_spec = r;
+                                    __hip_atomic_store(&s_spec_e, (int)e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                                }
+                        }
+                }
             if (wave == 0)
                 {
                     TrkHot t = s_t;
-                    // lane k sums tap k over the waves in wave order (one batch of
-                    // LDS reads instead of a serial read per partial), then every
-                    // lane takes the totals by readlane; E/P/L are the same sums
-                    float2 mine = make_float2(0.f, 0.f);
-                    if (lane <= kMaxTrkTaps)
-                        {
-                            float2 v[kTrkThreads / 64];
-#pragma unroll
-                            for (int w = 0; w < kTrkThreads / 64; ++w) v[w] = s_red[w][lane];
-#pragma unroll
-                            for (int w = 0; w < kTrkThreads / 64; ++w)
-                                {
-                                    mine.x += v[w].x;
-                                    mine.y += v[w].y;
-                                }
-                        }
-                    float2 taps[kMaxTrkTaps + 1];
-#pragma unroll
-                    for (int k = 0; k <= kMaxTrkTaps; ++k)
-                        taps[k] = (k < K || (k == kMaxTrkTaps && data)) ? make_float2(lane_f(mine.x, k), lane_f(mine.y, k))
-                                                                       : make_float2(0.f, 0.f);
-                    float2 epl[3];
-                    {
-                        const int ix[3] = {c.iE, c.iP, c.iL};
-#pragma unroll
-                        for (int q = 0; q < 3; ++q) epl[q] = make_float2(lane_f(mine.x, ix[q]), lane_f(mine.y, ix[q]));
-                    }
+                    float2 taps[kMaxTrkTaps + 1], epl[3];
+                    tap_totals(taps, epl);
                     const uint64_t n_read = t.next_sample;
                     const int32_t state0 = t.state;
                     // pull-in transitory check at the top of general_work (:1794-1803):
@@ -1473,7 +1565,13 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                     uint64_t pr[3] = {0, 0, 0};
                     uint64_t tm3 = 0;
                     if (timing) tm3 = wall_clock64();
-                    after_correlation(c, t, gc, s_lf, s_pbuf, s_cn, taps, epl, n_read, lane, o, timing != nullptr, pr);
+                    SpecLink sl{&s_spec, &s_spec_e, s_lfs, &s_lfi, lfi0, (int)e};
+                    after_correlation(c, t, gc, sl, s_pbuf, s_cn, taps, epl, n_read, lane, o, timing != nullptr, pr);
+                    if (sl.lfi != lfi0)
+                        {
+                            lfi0 = sl.lfi;
+                            if (lane == 0) s_lfi = lfi0;
+                        }
                     if (lane == 0)
                         {
                             gsdr_trk_epoch r;
@@ -1538,7 +1636,7 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
     if (tid == 0)
         {
             gc->h = s_t;
-            gc->code_filter = s_lf;
+            gc->code_filter = s_lfs[s_lfi];
             nout[ch] = e + (uint32_t)s_overrun;
         }
     if (tid < kMaxCn0) gc->prompt_buffer[tid] = s_pbuf[tid];

@@ -412,7 +412,9 @@ __device__ __forceinline__ void seq_sums(const float* terms, int stride, int n, 
 
 // cn0_and_tracking_lock_status (:970-1056) with cn0_m2m4_estimator and
 // carrier_lock_detector (lock_detectors.cc:90-148); wave 0, lane = element,
-// sums in element order through `scratch` (4 x kMaxCn0 floats of LDS).
+// sums in element order through `scratch` (3 x kMaxCn0 floats of LDS).  Returns 0 on a
+// loss of lock, 1 while the prompt buffer fills, 2 with a full buffer: then the EVM
+// (:1027-1053, an output only) is the one wave 1 computed (evm_of).
 __device__ inline int cn0_and_lock(const TrkConst& c, TrkHot& t, float2* pbuf, float (*scratch)[kMaxCn0], double coh,
     int lane)
 {
@@ -435,9 +437,8 @@ __device__ inline int cn0_and_lock(const TrkConst& c, TrkHot& t, float2* pbuf, f
     scratch[0][lane] = a_i;
     scratch[1][lane] = aux_i;
     scratch[2][lane] = aux2_i;
-    scratch[3][lane] = ei.x * ei.x;  // EVM: sum of squared in-phase prompts
-    float sums[4];
-    seq_sums<4>(&scratch[0][0], kMaxCn0, n, sums);
+    float sums[3];
+    seq_sums<3>(&scratch[0][0], kMaxCn0, n, sums);
     float psig = sums[0], m2 = sums[1], m4 = sums[2];
     const float fn = (float)n;
     psig /= fn;
@@ -473,22 +474,34 @@ __device__ inline int cn0_and_lock(const TrkConst& c, TrkHot& t, float2* pbuf, f
             t.code_lock_fail_counter = 0;
             return 0;
         }
-    // EVM (fork indicator, :1027-1053)
-    float s = sums[3];
-    float d = s / fn;
+    return 2;
+}
+
+// The fork indicator EVM of cn0_and_tracking_lock_status (:1027-1053) on wave 1, from
+// the prompt buffer with this call's prompt (a full buffer: cn0_estimation_counter >=
+// cn0_samples before the call): the same float sums in element order as the oracle,
+// through `scratch` (2 x kMaxCn0 floats of LDS).
+__device__ inline double evm_of(const TrkConst& c, const TrkHot& t, const float2* pbuf, float* scratch, int lane)
+{
+    const int n = c.cn0_samples;
+    const int widx = t.cn0_estimation_counter % n;
+    float2 ei = make_float2(0.f, 0.f);
+    if (lane < n) ei = lane == widx ? t.P_accu : pbuf[lane];
+    scratch[lane] = ei.x * ei.x;  // sum of squared in-phase prompts
+    float s1[1];
+    seq_sums<1>(scratch, 0, n, s1);
+    const float fn = (float)n;
+    float d = s1[0] / fn;
     d = sqrtf(d);
     const float ea = fabsf(ei.x / d) - 1.0F;
     const float eb = fabsf(ei.y / d) - 0.0F;
     const float aa_i = ea * ea, bb_i = eb * eb;
     __builtin_amdgcn_wave_barrier();
-    float* flat = &scratch[0][0];  // 2 x kMaxCn0 floats, interleaved: s = s + aa_i; s = s + bb_i in element order
-    flat[2 * lane] = aa_i;
-    flat[2 * lane + 1] = bb_i;
+    scratch[2 * lane] = aa_i;  // interleaved: s = s + aa_i; s = s + bb_i in element order
+    scratch[2 * lane + 1] = bb_i;
     float s2[1];
-    seq_sums<1>(flat, 0, 2 * n, s2);
-    s = s2[0];
-    t.evm = sqrt((double)(s / fn / 1.0F));
-    return 1;
+    seq_sums<1>(scratch, 0, 2 * n, s2);
+    return sqrt((double)(s2[0] / fn / 1.0F));
 }
 
 __device__ inline void run_dll_pll(const TrkConst& c, TrkHot& t, LoopFilter& lf)  // :1092-1179 (no Doppler correction)
@@ -635,6 +648,7 @@ struct EpochOut
     int32_t flags;
     double prompt_i, prompt_q;
     float log_accu[5];  // log_data's |VE|, |E|, |P|, |L|, |VL| accumulators (GSDR_TRK_F_LOGGED)
+    bool evm;           // locked with a full prompt buffer: t.evm is wave 1's evm_of
 };
 
 // log_data (:1403-1500): the accumulator magnitudes at the reference's log point
@@ -756,6 +770,7 @@ __device__ inline void after_correlation(const TrkConst& c, TrkHot& t, TrkChan* 
     int lane, EpochOut& o, bool tm, uint64_t (&pr)[3])
 {
     o.flags = 0;
+    o.evm = false;
     o.prompt_i = 0.0;
     o.prompt_q = 0.0;
     for (int i = 0; i < 5; ++i) o.log_accu[i] = 0.0F;
@@ -784,6 +799,7 @@ __device__ inline void after_correlation(const TrkConst& c, TrkHot& t, TrkChan* 
             else
                 {
                     int next_state = 0;
+                    o.evm = locked == 2;
                     take_dll_pll(t, sl);
                     tprobe(tm, pr, 1);
                     update_tracking_vars(c, t, gc);
@@ -859,6 +875,7 @@ __device__ inline void after_correlation(const TrkConst& c, TrkHot& t, TrkChan* 
                 }
             else
                 {
+                    o.evm = locked == 2;
                     take_dll_pll(t, sl);
                     tprobe(tm, pr, 1);
                     update_tracking_vars(c, t, gc);
@@ -1089,8 +1106,10 @@ __device__ __forceinline__ void correlate_chunk_any(const void* __restrict__ iq,
 // sample-shifted copies of tap 0) and 32fc_32f_high_dynamic_rotator_dot_prod_32fc_xn
 // (:68-112: sample n rotated by the phase of n*theta + (n-1)^2*theta_rate, from the
 // fp64 model as in corr.hip).  Lane-strided samples; the window or HBM as the fast path.
+// (always inlined: as a call it took the address of the kernel's accumulators,
+// which then lived in scratch for every correlation path)
 template <int IT>
-__device__ void correlate_call_hd(const void* __restrict__ iq, const float2* s_win, const float* s_code,
+__device__ __forceinline__ void correlate_call_hd(const void* __restrict__ iq, const float2* s_win, const float* s_code,
     const float* s_data, const Prep& p, int vl, int L, int K, bool data, float shift0, float shiftP,
     float2 (&acc)[kMaxTrkTaps + 1])
 {
@@ -1291,7 +1310,10 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
     __shared__ DllPllSpec s_spec;
     __shared__ int s_spec_e;
     __shared__ float2 s_pbuf[kMaxCn0];
-    __shared__ __attribute__((aligned(16))) float s_cn[4][kMaxCn0];  // cn0_and_lock's per-element terms
+    __shared__ __attribute__((aligned(16))) float s_cn[3][kMaxCn0];  // cn0_and_lock's per-element terms
+    __shared__ __attribute__((aligned(16))) float s_evm_buf[2 * kMaxCn0];  // evm_of's (wave 1)
+    __shared__ double s_evm;
+    __shared__ int s_evm_e;
     __shared__ int s_state;
     __shared__ Prep prep;
     __shared__ float2 s_red[kTrkThreads / 64][kMaxTrkTaps + 1];
@@ -1314,6 +1336,7 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
             s_lfs[0] = gc->code_filter;
             s_lfi = 0;
             s_spec_e = -1;
+            s_evm_e = -1;
             s_state = s_t.state;
             s_overrun = 0;
         }
@@ -1376,7 +1399,11 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
             if (!prep.go) break;
             if (timing && tid == 0) tm1 = wall_clock64();
             // ---- correlation: lane-interleaved samples, fp64 phasor anchor + fp32 steps
-            const Prep p = prep;
+            // the plan read from LDS where it is used (a register copy lived across the
+            // whole correlation and the allocator spilled it); the offset is read once,
+            // before wave 0 can write the next plan
+            const Prep& p = prep;
+            const int64_t p_off = p.off;
             float2 acc[kMaxTrkTaps + 1];
 #pragma unroll
             for (int k = 0; k <= kMaxTrkTaps; ++k) acc[k] = make_float2(0.f, 0.f);
@@ -1434,17 +1461,21 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
             __syncthreads();  // partials visible; every read of the LDS window done
             if (timing && tid == 0) tm2 = wall_clock64();
             // ---- stage the window the next call most likely reads, [off + vl - kHalo/2,
-            // +kWinCore+kHalo), into LDS: waves 2.. only, while wave 0 runs the loop
-            // update and wave 1 the speculative DLL/PLL (every read of the current window
-            // is done), so wave 0 issues no global loads that a vmcnt wait inside its
-            // update would wait for
-            const int64_t nb = p.off + vl - kHalo / 2;
-            if (use_window && wave >= 2)
+            // +kWinCore+kHalo), into LDS: waves 3.. only, while wave 0 runs the loop
+            // update, wave 1 the speculative DLL/PLL and wave 2 the EVM (every read of the
+            // current window is done), so wave 0 issues no global loads that a vmcnt wait
+            // inside its update would wait for
+            const int64_t nb = p_off + vl - kHalo / 2;
+            if (use_window && wave >= 3)
                 {
                     // two batches of loads in flight (the update hides their latency)
-                    constexpr int kW = kTrkThreads - 128;
+                    constexpr int kW = kTrkThreads - 192;
                     constexpr int kIt = (kWinCore + kHalo + kW - 1) / kW;
                     constexpr int kB = (kIt + 1) / 2;
+                    // one 64-bit base per call and constant steps (per-item 64-bit
+                    // offsets were hoisted out of the call loop and held 26 VGPRs)
+                    const int i0 = tid - 192;
+                    const int64_t g0 = nb + i0;
 #pragma unroll
                     for (int j0 = 0; j0 < kIt; j0 += kB)
                         {
@@ -1452,16 +1483,15 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
 #pragma unroll
                             for (int j = 0; j < kB; ++j)
                                 {
-                                    const int i = tid - 128 + (j0 + j) * kW;
-                                    const int64_t g = nb + i;
-                                    wv[j] = (j0 + j < kIt && i < kWinCore + kHalo && g >= 0 && (uint64_t)g < iq_items)
+                                    const int64_t g = g0 + (int64_t)((j0 + j) * kW);
+                                    wv[j] = (j0 + j < kIt && i0 + (j0 + j) * kW < kWinCore + kHalo && (uint64_t)g < iq_items)
                                                 ? load_iq<IT>(iq, g)
                                                 : make_float2(0.f, 0.f);
                                 }
 #pragma unroll
                             for (int j = 0; j < kB; ++j)
                                 {
-                                    const int i = tid - 128 + (j0 + j) * kW;
+                                    const int i = i0 + (j0 + j) * kW;
                                     if (j0 + j < kIt && i < kWinCore + kHalo) s_win[i] = wv[j];
                                 }
                         }
@@ -1470,7 +1500,7 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                 {
                     // chunk 0 of the call most likely next, fetched by waves 1.. while
                     // wave 0 runs the loop update (its own memory waits stay unaffected)
-                    const int64_t nb = p.off + vl - kHalo / 2;
+                    const int64_t nb = p_off + vl - kHalo / 2;
                     pf_start = stream_fetch(iq, iq_items * (uint64_t)item_bytes<IT>(), nb * item_bytes<IT>(),
                         (stream_chunk + kHalo) * item_bytes<IT>(), s_sb, 1);
                     pf_first = nb;
@@ -1545,6 +1575,27 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                                 }
                         }
                 }
+            if (wave == 2)
+                {
+                    // this call's EVM (an output only) with a full prompt buffer; wave 0
+                    // takes it for the record when the call stays locked
+                    TrkHot t2 = s_t;
+                    if ((t2.state == 2 || t2.state == 4) && t2.cn0_estimation_counter >= c.cn0_samples)
+                        {
+                            float2 taps[kMaxTrkTaps + 1], epl[3];
+                            tap_totals(taps, epl);
+                            if (t2.state == 2)
+                                t2.P_accu = epl[1];
+                            else
+                                save_correlation_results(c, t2, taps, epl);
+                            const double evm = evm_of(c, t2, s_pbuf, s_evm_buf, lane);
+                            if (lane == 0)
+                                {
+                                    s_evm = evm;
+                                    __hip_atomic_store(&s_evm_e, (int)e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                                }
+                        }
+                }
             if (wave == 0)
                 {
                     TrkHot t = s_t;
@@ -1571,6 +1622,12 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                         {
                             lfi0 = sl.lfi;
                             if (lane == 0) s_lfi = lfi0;
+                        }
+                    if (o.evm)
+                        {
+                            while (__hip_atomic_load(&s_evm_e, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != (int)e)
+                                __builtin_amdgcn_s_sleep(1);
+                            t.evm = s_evm;
                         }
                     if (lane == 0)
                         {

@@ -156,15 +156,50 @@ __host__ __device__ inline void lf_initialize(LoopFilter& f, float y0)  // :258-
     f.idx = 3;
 }
 
-__device__ inline float lf_apply(LoopFilter& f, float in)  // :58-93
+// Tracking_loop_filter::apply on a filter held in registers (wave 1's speculative
+// DLL/PLL): the ring elements are separate scalars picked by selects -- with arrays
+// the compiler turned the selects back into a run-time index, i.e. a scratch access
+// (and the LDS form was a chain of dependent LDS round trips).  The reference's
+// products and sums in its order.
+struct LfReg
+{
+    float i0, i1, i2, i3, o0, o1, o2, o3, c0, c1, c2, c3, d0, d1, d2;
+    int nin, nout, idx;
+};
+
+__device__ __forceinline__ LfReg lf_load(const LoopFilter& f)
+{
+    return LfReg{f.inputs[0], f.inputs[1], f.inputs[2], f.inputs[3], f.outputs[0], f.outputs[1], f.outputs[2],
+        f.outputs[3], f.icoef[0], f.icoef[1], f.icoef[2], f.icoef[3], f.ocoef[0], f.ocoef[1], f.ocoef[2], f.nin, f.nout,
+        f.idx};
+}
+
+__device__ __forceinline__ float lf_pick(float a0, float a1, float a2, float a3, int i)
+{
+    return i == 0 ? a0 : (i == 1 ? a1 : (i == 2 ? a2 : a3));
+}
+
+__device__ __forceinline__ float lf_apply(LfReg& f, float in)  // :58-93
 {
     float r = 0.0F;
-    for (int ii = 0; ii < f.nout; ++ii) r += f.ocoef[ii] * f.outputs[(f.idx + ii) % 4];
+    const float oc[3] = {f.d0, f.d1, f.d2};
+    const float ic[4] = {f.c0, f.c1, f.c2, f.c3};
+#pragma unroll
+    for (int ii = 0; ii < 3; ++ii)
+        if (ii < f.nout) r += oc[ii] * lf_pick(f.o0, f.o1, f.o2, f.o3, (f.idx + ii) & 3);
     f.idx--;
     if (f.idx < 0) f.idx += 4;
-    f.inputs[f.idx] = in;
-    for (int ii = 0; ii < f.nin; ++ii) r += f.icoef[ii] * f.inputs[(f.idx + ii) % 4];
-    f.outputs[f.idx] = r;
+    f.i0 = f.idx == 0 ? in : f.i0;
+    f.i1 = f.idx == 1 ? in : f.i1;
+    f.i2 = f.idx == 2 ? in : f.i2;
+    f.i3 = f.idx == 3 ? in : f.i3;
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii)
+        if (ii < f.nin) r += ic[ii] * lf_pick(f.i0, f.i1, f.i2, f.i3, (f.idx + ii) & 3);
+    f.o0 = f.idx == 0 ? r : f.o0;
+    f.o1 = f.idx == 1 ? r : f.o1;
+    f.o2 = f.idx == 2 ? r : f.o2;
+    f.o3 = f.idx == 3 ? r : f.o3;
     return r;
 }
 
@@ -504,7 +539,7 @@ __device__ inline double evm_of(const TrkConst& c, const TrkHot& t, const float2
     return sqrt((double)(s2[0] / fn / 1.0F));
 }
 
-__device__ inline void run_dll_pll(const TrkConst& c, TrkHot& t, LoopFilter& lf)  // :1092-1179 (no Doppler correction)
+__device__ inline void run_dll_pll(const TrkConst& c, TrkHot& t, LfReg& lf)  // :1092-1179 (no Doppler correction)
 {
     const double carr_phase_error_hz =
         (t.cloop ? pll_cloop_two_quadrant_atan(t.P_accu) : pll_four_quadrant_atan(t.P_accu)) / kTwoPi;
@@ -1557,10 +1592,24 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                                 }
                             else
                                 save_correlation_results(c, t1, taps, epl);
+                            // the filter in registers, written to the other slot after
                             const int cur = s_lfi;
-                            LoopFilter& lf1 = s_lfs[cur ^ 1];
-                            lf1 = s_lfs[cur];
+                            LfReg lf1 = lf_load(s_lfs[cur]);
                             run_dll_pll(c, t1, lf1);
+                            if (lane == 0)
+                                {
+                                    LoopFilter& d = s_lfs[cur ^ 1];
+                                    d = s_lfs[cur];
+                                    d.inputs[0] = lf1.i0;
+                                    d.inputs[1] = lf1.i1;
+                                    d.inputs[2] = lf1.i2;
+                                    d.inputs[3] = lf1.i3;
+                                    d.outputs[0] = lf1.o0;
+                                    d.outputs[1] = lf1.o1;
+                                    d.outputs[2] = lf1.o2;
+                                    d.outputs[3] = lf1.o3;
+                                    d.idx = lf1.idx;
+                                }
                             if (lane == 0)
                                 {
                                     DllPllSpec r;

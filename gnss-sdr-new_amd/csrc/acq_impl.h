@@ -562,13 +562,101 @@ struct NoPads
     using layout = RowPad<L, 0, 0>;
 };
 
+// The bank-model pads of the 10 x 10 x 10 row plan: the buffers the
+// first and second row stages write hold one pad element every 10 / 3 every 50,
+// so stage 1's stride-10 writes (22-dword lane stride) and stage 2's writes
+// spread over the LDS banks.
+struct Pads1000
+{
+    template <int I>
+    using layout = std::conditional_t<I == 1, RowPad<1000, 10, 1>,
+        std::conditional_t<I == 2, RowPad<1000, 50, 3>, RowPad<1000, 0, 0>>>;
+};
+
+// ---- wave-local row transforms
+// One wave transforms one L-point row in place in its own LDS row buffer: the
+// Stockham exchange between the row stages needs no workgroup barrier, because
+// a wave's LDS instructions execute in issue order -- every lane's reads of a
+// stage are issued before any of its writes, and the next stage's reads after
+// them.  The empty asm statements (memory clobber) keep the compiler from moving
+// a write above a read whose address it believes distinct (other lanes' data is
+// involved, which per-thread alias analysis cannot see).  Lanes past the stage's
+// butterfly count repeat the last butterfly (same values to the same addresses,
+// repeated outputs for an order-free maximum), so no lane is predicated off.
+template <int R, int L, int Ns, bool LAST, class In, class OutL, class Out>
+__device__ __forceinline__ void wl_stage(gsdr::pk::c2* row, Out& out, int lane)
+{
+    using gsdr::pk::c2;
+    constexpr int NB = L / R;
+    constexpr int BPT = (NB + 63) / 64;
+    constexpr int TSTRIDE = L / (Ns * R);
+    static_assert(In::pad_every == 0 || NB % In::pad_every == 0, "read layout: S must divide L/R");
+    static_assert(LAST || OutL::pad_every == 0 || ((Ns * R) % OutL::pad_every == 0 && OutL::pad_every % Ns == 0),
+        "write layout: S must divide Ns R and be a multiple of Ns");
+    c2 v[BPT][R];
+    int jb[BPT];
+#pragma unroll
+    for (int b = 0; b < BPT; ++b)
+        {
+            jb[b] = NB % 64 == 0 ? lane + 64 * b : min(lane + 64 * b, NB - 1);
+            const int base = In::pad(jb[b]);
+#pragma unroll
+            for (int r = 0; r < R; ++r) v[b][r] = row[base + In::cpad(r * NB)];
+        }
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int b = 0; b < BPT; ++b)
+        {
+            int k = 0;
+            if constexpr (Ns > 1)
+                {
+                    k = jb[b] % Ns;
+                    const c2 w1 = gsdr::pk::from(out.twiddle(k * TSTRIDE));
+                    c2 w = w1;
+#pragma unroll
+                    for (int r = 1; r < R; ++r)
+                        {
+                            if (r > 1) w = gsdr::pk::mul(w, w1);
+                            v[b][r] = gsdr::pk::mul(v[b][r], w);
+                        }
+                }
+            gsdr::pk::Dft<R>::run(v[b]);
+            if constexpr (LAST)
+                {
+#pragma unroll
+                    for (int r = 0; r < R; ++r) out.value(v[b][r], jb[b] + r * Ns);
+                }
+            else
+                {
+                    const int base = OutL::pad((jb[b] - k) * R) + k;
+#pragma unroll
+                    for (int r = 0; r < R; ++r) row[base + OutL::cpad(r * Ns)] = v[b][r];
+                }
+        }
+    if constexpr (!LAST) asm volatile("" ::: "memory");
+}
+
+template <int L, int Ns, class Pads, int Si, int R, int... Rest, class Out>
+__device__ __forceinline__ void wl_stages(gsdr::pk::c2* row, Out& out, int lane)
+{
+    constexpr bool LAST = sizeof...(Rest) == 0;
+    using In = typename Pads::template layout<Si>;
+    using OutL = typename Pads::template layout<LAST ? Si : Si + 1>;
+    wl_stage<R, L, Ns, LAST, In, OutL>(row, out, lane);
+    if constexpr (!LAST) wl_stages<L, Ns * R, Pads, Si + 1, Rest...>(row, out, lane);
+}
+
 // WPE_ packs the waves-per-EU hint (bits 0-3) and PGS (bits 4+): with PGS > 0 an
 // XCD walks its rows PRN-group-major (groups of PGS PRNs, PGS | P), so its L2 holds
 // PGS code spectra (PGS x 128 KB at N = 16000) instead of cycling through all P.
+// H_ = 0: wave-local rows (WL): each round puts one row per wave in LDS and every
+// wave transforms its own row without workgroup barriers (wl_stages); H = NT / 64
+// rows per round, the last round partial when NT / 64 does not divide R.
 template <int R_, int NT_, int H_, int WPE_, class Pads_, int... Rs>
 struct RegFourStep
 {
-    static constexpr int R = R_, NT = NT_, H = H_, WPE = WPE_ & 15, PGS = WPE_ >> 4;
+    static constexpr bool WL = H_ == 0;
+    static constexpr int R = R_, NT = NT_, H = WL ? NT_ / 64 : H_, WPE = WPE_ & 15, PGS = WPE_ >> 4;
     static constexpr int L = (Rs * ...);
     static constexpr int N = R * L;
     static constexpr int CPL = (L + NT - 1) / NT;
@@ -584,11 +672,69 @@ struct RegFourStep
     }
     static constexpr int lds_elems = H * max_stride();
     static constexpr size_t lds_bytes() { return (size_t)lds_elems * sizeof(float2) + (NT / 64) * sizeof(float); }
-    static_assert(R % H == 0, "rows go through LDS in groups of H");
+    static_assert(WL || R % H == 0, "rows go through LDS in groups of H");
     template <class Out>
     __device__ __forceinline__ static void row_transforms(gsdr::pk::c2* lds, Out& out)
     {
         rows_stages<NT, L, H, 1, Pads, 0, Rs...>(lds, out);
+    }
+    // WL: one row (at lds, max_stride() elements) by the calling wave
+    template <class Out>
+    __device__ __forceinline__ static void wl_row(gsdr::pk::c2* row, Out& out, int lane)
+    {
+        wl_stages<L, 1, Pads, 0, Rs...>(row, out, lane);
+    }
+
+    // Phase 2 of a register four-step: the R rows (phase 1's v[c][k1], lane column
+    // n2 = threadIdx.x + c NT, clamped) through LDS and the L-point row transforms.
+    template <int CPL, class Out>
+    __device__ __forceinline__ static void phase2(gsdr::pk::c2* lds, gsdr::pk::c2 (&v)[CPL][R], Out& out)
+    {
+        const int wbase = (int)(threadIdx.x & ~63u);
+        if constexpr (!WL)
+            {
+#pragma unroll
+                for (int h = 0; h < R / H; ++h)
+                    {
+                        if (h > 0) __syncthreads();  // the previous group's last-stage reads are done
+#pragma unroll
+                        for (int c = 0; c < CPL; ++c)
+                            {
+                                if (L % NT == 0 || wbase + c * NT < L)
+                                    {
+                                        const int n2 = min((int)threadIdx.x + c * NT, L - 1);
+#pragma unroll
+                                        for (int i = 0; i < H; ++i) lds[i * L + n2] = v[c][h * H + i];
+                                    }
+                            }
+                        __syncthreads();
+                        row_transforms(lds, out);
+                    }
+            }
+        else
+            {
+                using L0 = typename Pads::template layout<0>;
+                constexpr int STR = max_stride();
+                const int wave = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
+#pragma unroll
+                for (int h = 0; h < (R + H - 1) / H; ++h)
+                    {
+                        if (h > 0) __syncthreads();  // every wave's row of the previous round is done
+#pragma unroll
+                        for (int c = 0; c < CPL; ++c)
+                            {
+                                if (L % NT == 0 || wbase + c * NT < L)
+                                    {
+                                        const int n2 = min((int)threadIdx.x + c * NT, L - 1);
+#pragma unroll
+                                        for (int i = 0; i < H; ++i)
+                                            if (h * H + i < R) lds[i * STR + L0::pad(n2)] = v[c][h * H + i];
+                                    }
+                            }
+                        __syncthreads();
+                        if (h * H + wave < R) wl_row(lds + wave * STR, out, lane);
+                    }
+            }
     }
 };
 
@@ -598,7 +744,7 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(RP:
     uint32_t P, uint32_t nblocks)
 {
     using gsdr::pk::c2;
-    constexpr int R = RP::R, NT = RP::NT, H = RP::H, L = RP::L, CPL = RP::CPL;
+    constexpr int R = RP::R, NT = RP::NT, L = RP::L, CPL = RP::CPL;
     constexpr uint32_t N = RP::N;
     constexpr int NW = NT / 64;
     extern __shared__ float2 lds_raw[];
@@ -672,24 +818,8 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(RP:
         __device__ __forceinline__ float2 twiddle(int m_) const { return tw[m_ * R]; }  // W_L^m = W_N^{m R}
         __device__ __forceinline__ void value(c2 x, int) { m = __builtin_fmaxf(m, __builtin_fmaf(x.x, x.x, x.y * x.y)); }
     } out{tw, 0.0f};
-    // phase 2: rows k1 = h*H .. h*H+H-1 through LDS
-#pragma unroll
-    for (int h = 0; h < R / H; ++h)
-        {
-            if (h > 0) __syncthreads();  // the previous group's last-stage reads are done
-#pragma unroll
-            for (int c = 0; c < CPL; ++c)
-                {
-                    if (L % NT == 0 || wbase + c * NT < L)
-                        {
-                            const int n2 = min((int)threadIdx.x + c * NT, L - 1);
-#pragma unroll
-                            for (int i = 0; i < H; ++i) lds[i * L + n2] = v[c][h * H + i];
-                        }
-                }
-            __syncthreads();
-            RP::row_transforms(lds, out);
-        }
+    // phase 2: the rows k1 through LDS
+    RP::phase2(lds, v, out);
     float rmax = gsdr::wave_max(out.m);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if (lane == 0) red[wave] = rmax;
@@ -724,13 +854,15 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(RP:
 // Grid: one workgroup per (row = b*D + d, PRN p, sub-transform q), the ROUT*P
 // workgroups of one row on one XCD, each XCD walking its rows in groups of pgs
 // PRNs so its L2 holds pgs code rows while the X rows stream.
-template <int ROUT, class RP, bool HALF>
+// ABL (timing ablations for the profile, results meaningless): bit 0 replaces
+// phase 1's global loads by lane-computed values, bit 1 skips phase 2.
+template <int ROUT, class RP, bool HALF, int ABL = 0>
 __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(RP::WPE))) acq_correlate_split_kernel(
     const float2* __restrict__ X, const float2* __restrict__ code_fft, RowStat* __restrict__ stats,
     const float2* __restrict__ tw, uint32_t D, uint32_t P, uint32_t nblocks, uint32_t pgs)
 {
     using gsdr::pk::c2;
-    constexpr int R = RP::R, NT = RP::NT, H = RP::H, L = RP::L, CPL = RP::CPL;
+    constexpr int R = RP::R, NT = RP::NT, L = RP::L, CPL = RP::CPL;
     constexpr uint32_t M = RP::N;
     constexpr uint32_t N = M * ROUT;
     constexpr int NW = NT / 64;
@@ -765,6 +897,8 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(RP:
     const auto crs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float2*>(code_fft) + (size_t)p * N, 0, (int)(N * sizeof(c2)), 0x00020000);
     auto bload = [](decltype(xrs) rs, int voff, int soff) -> c2 {
+        if constexpr ((ABL & 1) != 0)
+            return c2{(float)(voff + soff) * 1e-6f, (float)(voff - soff) * 1e-6f};
         const auto u = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, 0);
         return c2{__uint_as_float(u[0]), __uint_as_float(u[1])};
     };
@@ -851,22 +985,14 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(RP:
             if (!HALF || k2 >= L / 2) m = __builtin_fmaxf(m, a);
         }
     } out{tw, 0.0f};
-#pragma unroll
-    for (int h = 0; h < R / H; ++h)
+    if constexpr ((ABL & 2) == 0)
+        RP::phase2(lds, v, out);
+    else
         {
-            if (h > 0) __syncthreads();
 #pragma unroll
             for (int c = 0; c < CPL; ++c)
-                {
-                    if (L % NT == 0 || wbase + c * NT < L)
-                        {
-                            const int n2 = min((int)threadIdx.x + c * NT, L - 1);
 #pragma unroll
-                            for (int i = 0; i < H; ++i) lds[i * L + n2] = v[c][h * H + i];
-                        }
-                }
-            __syncthreads();
-            RP::row_transforms(lds, out);
+                for (int i = 0; i < R; ++i) out.value(v[c][i], L - 1);
         }
     float rmax = gsdr::wave_max(out.m);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1670,7 +1796,8 @@ size_t item_bytes(int it) { return it == GSDR_ITEM_CSHORT ? 4 : (it == GSDR_ITEM
 // with the argmax recomputed for the selected row, 2 max only with the CFAR row
 // sum by Parseval -- see acq_correlate_pk_kernel).  93 runs the correlate on the
 // register four-step (acq_correlate_reg_kernel, N = 16000, PRN-group-major XCD
-// walk) and its forward / argmax passes on the listed plan.  The alternatives
+// walk) and its forward / argmax passes on the listed plan; 94 the same with
+// wave-local row transforms (RegFourStep H = 0).  The alternatives
 // measured in rounds 1-2 (other radix orders, per-stage twiddle tables, LDS root
 // copies, padded layouts, late barriers, 5 waves, PRN groups)
 // were within noise of or slower than these and are no longer built.
@@ -1678,6 +1805,7 @@ size_t item_bytes(int it) { return it == GSDR_ITEM_CSHORT ? 4 : (it == GSDR_ITEM
     X(61, (gsdr::pk::PkPlan<512, true, 20, 20, 20>), 1, 1, 1)           \
     X(62, (gsdr::pk::PkPlan<256, true, 20, 10, 10>), 1, 1, 1)           \
     X(93, (gsdr::pk::PkPlan<1024, 1, 16, 10, 10, 10>), 1, 1, 2)         \
+    X(94, (gsdr::pk::PkPlan<1024, 1, 16, 10, 10, 10>), 1, 1, 2)         \
     X(70, (gsdr::pk::PkPlan<256, 1, 25, 16, 10>), 1, 1, 2)
 
 template <class PT>

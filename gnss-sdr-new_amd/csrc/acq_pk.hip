@@ -10,6 +10,9 @@ namespace gsdr_acq_impl
 // four-step 16 x (10 x 10 x 10), 512 lanes, 8 rows per LDS round, each XCD's
 // rows walked in groups of 16 PRNs.
 using RegPlan93 = RegFourStep<16, 512, 8, 1 | (16 << 4), NoPads<1000>, 10, 10, 10>;
+// 94: 93 with wave-local rows (two rounds of 8 rows, one per wave, no barriers
+// inside a row transform)
+using RegPlan94 = RegFourStep<16, 512, 0, 1 | (16 << 4), NoPads<1000>, 10, 10, 10>;
 
 template <class RP>
 int launch_reg(gsdr_acq* a, uint32_t nblocks, hipStream_t s)
@@ -32,6 +35,7 @@ int launch_corr_variant(gsdr_acq* a, uint32_t nblocks, hipStream_t s)
     switch (a->corr_variant)
         {
         case 93: return launch_reg<RegPlan93>(a, nblocks, s);
+        case 94: return launch_reg<RegPlan94>(a, nblocks, s);
         default: break;
         }
 #define GSDR_PK_CASE(ID, MP, PG, WPE, ST)                                                                       \
@@ -131,6 +135,7 @@ int setup_corr_variant(gsdr_acq* a, int v)
             GSDR_HIP(hipFuncSetAttribute((const void*)acq_forward_pk_kernel<M, GSDR_ITEM_IBYTE>,               \
                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)M::lds_bytes()));                              \
             if (ID == 93 && setup_reg<RegPlan93>() != GSDR_OK) return GSDR_E_DEVICE;                           \
+            if (ID == 94 && setup_reg<RegPlan94>() != GSDR_OK) return GSDR_E_DEVICE;                           \
             a->corr_variant = ID;                                                                               \
             a->corr_stat = ST;                                                                                  \
             a->tw_entries = M::tw_entries();                                                                    \

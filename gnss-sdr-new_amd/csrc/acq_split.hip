@@ -16,6 +16,13 @@ using Reg32k = RegFourStep<32, 1024, 8, 1, NoPads<1000>, 10, 10, 10>;
 //   16000 = 16 x (10 x 10 x 10): the C3 plan (variant 93's register four-step), 512
 //           lanes, two columns per lane, 8 rows per LDS round (64 KB)
 using Reg16k = RegFourStep<16, 512, 8, 1, NoPads<1000>, 10, 10, 10>;
+// Wave-local rows (H = 0): each LDS round holds one row per wave and every wave
+// transforms its row without workgroup barriers.
+using Wl25k = RegFourStep<25, 512, 0, 1, NoPads<1000>, 10, 10, 10>;      // rounds 8 + 8 + 8 + 1
+using Wl25kW = RegFourStep<25, 1024, 0, 1, NoPads<1000>, 10, 10, 10>;    // one column per lane, rounds 16 + 9
+using Wl32k = RegFourStep<32, 1024, 0, 1, NoPads<1000>, 10, 10, 10>;     // rounds 16 + 16 (128 KB)
+using Wl32kP = RegFourStep<32, 1024, 0, 1, Pads1000, 10, 10, 10>;        // the same, bank-model pads
+using Wl16k = RegFourStep<16, 512, 0, 1, NoPads<1000>, 10, 10, 10>;      // rounds 8 + 8 (64 KB)
 
 // split ids: (N, outer radix ROUT, inner plan)
 //   1: 25000 = 1 x 25000 (C5 GPS L1 / BeiDou B1I at 25 Msps, 1 ms)
@@ -24,6 +31,10 @@ using Reg16k = RegFourStep<16, 512, 8, 1, NoPads<1000>, 10, 10, 10>;
 //   4: 100000 = 4 x 25000 (C5 Galileo E1 at 25 Msps, 4 ms)
 //   5: 32000 = 2 x 16000
 //   6: 64000 = 4 x 16000
+// wave-local rows:
+//   11: 25000 (Wl25k)   12: 32000 (Wl32k)   13: 64000 = 2 x Wl32k   14: 100000 = 4 x Wl25k
+//   15: 32000 = 2 x Wl16k   16: 64000 = 4 x Wl16k   17: 25000 (Wl25kW)   18: 100000 = 4 x Wl25kW
+//   19: 32000 (Wl32kP)   20: 64000 = 2 x Wl32kP
 namespace
 {
 struct SplitId
@@ -31,7 +42,11 @@ struct SplitId
     int id;
     uint32_t n;
 };
-constexpr SplitId kSplits[] = {{1, 25000}, {2, 32000}, {3, 64000}, {4, 100000}, {5, 32000}, {6, 64000}};
+constexpr SplitId kSplits[] = {{1, 25000}, {2, 32000}, {3, 64000}, {4, 100000}, {5, 32000}, {6, 64000}, {11, 25000},
+    {12, 32000}, {13, 64000}, {14, 100000}, {15, 32000}, {16, 64000}, {17, 25000}, {18, 100000}, {19, 32000},
+    {20, 64000}, {112, 32000}, {212, 32000}, {113, 64000}, {213, 64000}};
+// 112 / 212, 113 / 213: timing ablations of 12 / 13 (acq_correlate_split_kernel ABL:
+// 1xx without phase 1's global loads, 2xx without phase 2) -- profiles only
 
 // PRN group of an XCD pass: the largest divisor of P whose code rows fit in ~2 MB
 // (half an XCD's L2), so the rows of the group's codes stay resident while the X
@@ -45,7 +60,7 @@ uint32_t prn_group(uint32_t P, uint32_t N)
     return best;
 }
 
-template <int ROUT, class RP, bool HALF>
+template <int ROUT, class RP, bool HALF, int ABL = 0>
 int launch_one(gsdr_acq* a, uint32_t nblocks, hipStream_t s)
 {
     static_assert(RP::N * ROUT > 0, "plan");
@@ -57,16 +72,16 @@ int launch_one(gsdr_acq* a, uint32_t nblocks, hipStream_t s)
     if (ROUT > 1)
         GSDR_HIP(hipMemsetAsync(a->d_stats, 0, (size_t)nblocks * a->nprn * a->D * sizeof(RowStat), s));
     const uint32_t grid = nblocks * a->D * a->nprn * ROUT;
-    hipLaunchKernelGGL((acq_correlate_split_kernel<ROUT, RP, HALF>), dim3(grid), dim3(RP::NT), RP::lds_bytes(), s,
+    hipLaunchKernelGGL((acq_correlate_split_kernel<ROUT, RP, HALF, ABL>), dim3(grid), dim3(RP::NT), RP::lds_bytes(), s,
         a->d_X, a->d_code_fft, a->d_stats, a->d_tw, a->D, a->nprn, nblocks, prn_group(a->nprn, a->N));
     GSDR_HIP(hipGetLastError());
     return GSDR_OK;
 }
 
-template <int ROUT, class RP, bool HALF>
+template <int ROUT, class RP, bool HALF, int ABL = 0>
 int attrs_one()
 {
-    GSDR_HIP(hipFuncSetAttribute((const void*)acq_correlate_split_kernel<ROUT, RP, HALF>,
+    GSDR_HIP(hipFuncSetAttribute((const void*)acq_correlate_split_kernel<ROUT, RP, HALF, ABL>,
         hipFuncAttributeMaxDynamicSharedMemorySize, (int)RP::lds_bytes()));
     return GSDR_OK;
 }
@@ -83,6 +98,20 @@ int launch_split(gsdr_acq* a, uint32_t nblocks, hipStream_t s)
         case 4: return half ? launch_one<4, Reg25k, true>(a, nblocks, s) : launch_one<4, Reg25k, false>(a, nblocks, s);
         case 5: return half ? launch_one<2, Reg16k, true>(a, nblocks, s) : launch_one<2, Reg16k, false>(a, nblocks, s);
         case 6: return half ? launch_one<4, Reg16k, true>(a, nblocks, s) : launch_one<4, Reg16k, false>(a, nblocks, s);
+        case 11: return half ? launch_one<1, Wl25k, true>(a, nblocks, s) : launch_one<1, Wl25k, false>(a, nblocks, s);
+        case 12: return half ? launch_one<1, Wl32k, true>(a, nblocks, s) : launch_one<1, Wl32k, false>(a, nblocks, s);
+        case 13: return half ? launch_one<2, Wl32k, true>(a, nblocks, s) : launch_one<2, Wl32k, false>(a, nblocks, s);
+        case 14: return half ? launch_one<4, Wl25k, true>(a, nblocks, s) : launch_one<4, Wl25k, false>(a, nblocks, s);
+        case 15: return half ? launch_one<2, Wl16k, true>(a, nblocks, s) : launch_one<2, Wl16k, false>(a, nblocks, s);
+        case 16: return half ? launch_one<4, Wl16k, true>(a, nblocks, s) : launch_one<4, Wl16k, false>(a, nblocks, s);
+        case 17: return half ? launch_one<1, Wl25kW, true>(a, nblocks, s) : launch_one<1, Wl25kW, false>(a, nblocks, s);
+        case 18: return half ? launch_one<4, Wl25kW, true>(a, nblocks, s) : launch_one<4, Wl25kW, false>(a, nblocks, s);
+        case 19: return half ? launch_one<1, Wl32kP, true>(a, nblocks, s) : launch_one<1, Wl32kP, false>(a, nblocks, s);
+        case 20: return half ? launch_one<2, Wl32kP, true>(a, nblocks, s) : launch_one<2, Wl32kP, false>(a, nblocks, s);
+        case 112: return launch_one<1, Wl32k, false, 1>(a, nblocks, s);
+        case 212: return launch_one<1, Wl32k, false, 2>(a, nblocks, s);
+        case 113: return launch_one<2, Wl32k, true, 1>(a, nblocks, s);
+        case 213: return launch_one<2, Wl32k, true, 2>(a, nblocks, s);
         default: gsdr::set_error("internal: bad split variant %d", a->split); return GSDR_E_STATE;
         }
 }
@@ -121,6 +150,20 @@ int setup_split(gsdr_acq* a)
         case 4: rc = attrs_one<4, Reg25k, true>() | attrs_one<4, Reg25k, false>(); break;
         case 5: rc = attrs_one<2, Reg16k, true>() | attrs_one<2, Reg16k, false>(); break;
         case 6: rc = attrs_one<4, Reg16k, true>() | attrs_one<4, Reg16k, false>(); break;
+        case 11: rc = attrs_one<1, Wl25k, true>() | attrs_one<1, Wl25k, false>(); break;
+        case 12: rc = attrs_one<1, Wl32k, true>() | attrs_one<1, Wl32k, false>(); break;
+        case 13: rc = attrs_one<2, Wl32k, true>() | attrs_one<2, Wl32k, false>(); break;
+        case 14: rc = attrs_one<4, Wl25k, true>() | attrs_one<4, Wl25k, false>(); break;
+        case 15: rc = attrs_one<2, Wl16k, true>() | attrs_one<2, Wl16k, false>(); break;
+        case 16: rc = attrs_one<4, Wl16k, true>() | attrs_one<4, Wl16k, false>(); break;
+        case 17: rc = attrs_one<1, Wl25kW, true>() | attrs_one<1, Wl25kW, false>(); break;
+        case 18: rc = attrs_one<4, Wl25kW, true>() | attrs_one<4, Wl25kW, false>(); break;
+        case 19: rc = attrs_one<1, Wl32kP, true>() | attrs_one<1, Wl32kP, false>(); break;
+        case 20: rc = attrs_one<2, Wl32kP, true>() | attrs_one<2, Wl32kP, false>(); break;
+        case 112: rc = attrs_one<1, Wl32k, false, 1>(); break;
+        case 212: rc = attrs_one<1, Wl32k, false, 2>(); break;
+        case 113: rc = attrs_one<2, Wl32k, true, 1>(); break;
+        case 213: rc = attrs_one<2, Wl32k, true, 2>(); break;
         default: break;
         }
     if (rc != GSDR_OK) a->split = 0;

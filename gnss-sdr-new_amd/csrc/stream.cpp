@@ -13,8 +13,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <mutex>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "gsdr_internal.h"
@@ -34,6 +36,17 @@ struct gsdr_stream
     hipStream_t copy{nullptr};
     hipEvent_t pushed{nullptr};
     hipEvent_t read{nullptr};  // the last consumer launch reading the ring
+    // windows handed out by gsdr_stream_window_async whose reads are not yet
+    // released: a push that would overwrite one waits for its release (another
+    // thread's window) or fails (the pushing thread's own window)
+    struct OpenWindow
+    {
+        hipStream_t consumer;
+        uint64_t first;
+        std::thread::id owner;
+    };
+    std::vector<OpenWindow> open;
+    std::condition_variable released;
     std::mutex mu;
 };
 
@@ -147,7 +160,7 @@ void gsdr_stream_destroy(gsdr_stream* s)
 int gsdr_stream_push(gsdr_stream* s, const void* iq_host, uint64_t first_sample, uint64_t n)
 {
     GSDR_REQUIRE(s && (iq_host || n == 0), GSDR_E_ARG, "gsdr_stream_push: null argument");
-    std::lock_guard<std::mutex> lk(s->mu);
+    std::unique_lock<std::mutex> lk(s->mu);
     gsdr::DeviceGuard g(s->device);
     if (!s->started)
         {
@@ -160,6 +173,24 @@ int gsdr_stream_push(gsdr_stream* s, const void* iq_host, uint64_t first_sample,
     GSDR_REQUIRE(n <= s->cap, GSDR_E_ARG, "gsdr_stream_push: %llu items exceed the ring capacity %llu",
         (unsigned long long)n, (unsigned long long)s->cap);
     if (n == 0) return GSDR_OK;
+    // samples below new_oldest lose their ring positions: an async window still
+    // open over them must be released first (its reads are not enqueued yet, so
+    // the reader event cannot cover them)
+    const uint64_t new_oldest = s->head + n > s->cap ? s->head + n - s->cap : 0;
+    for (;;)
+        {
+            bool blocked = false;
+            for (const auto& w : s->open)
+                if (w.first < new_oldest)
+                    {
+                        GSDR_REQUIRE(w.owner != std::this_thread::get_id(), GSDR_E_STATE,
+                            "gsdr_stream_push: would overwrite the window at %llu this thread holds open "
+                            "(gsdr_stream_window_async); release it first", (unsigned long long)w.first);
+                        blocked = true;
+                    }
+            if (!blocked) break;
+            s->released.wait(lk);
+        }
     // overwrite only what no consumer launch still reads
     GSDR_HIP(hipStreamWaitEvent(s->copy, s->read, 0));
     const auto* src = static_cast<const uint8_t*>(iq_host);
@@ -211,6 +242,7 @@ int gsdr_stream_window_async(gsdr_stream* s, uint64_t first_sample, uint64_t n_i
     if (rc != GSDR_OK) return rc;
     gsdr::DeviceGuard g(s->device);
     GSDR_HIP(hipStreamWaitEvent((hipStream_t)consumer_stream, s->pushed, 0));
+    s->open.push_back({(hipStream_t)consumer_stream, first_sample, std::this_thread::get_id()});
     return GSDR_OK;
 }
 
@@ -219,7 +251,14 @@ int gsdr_stream_release(gsdr_stream* s, void* consumer_stream)
     GSDR_REQUIRE(s && consumer_stream, GSDR_E_ARG, "gsdr_stream_release: null argument");
     std::lock_guard<std::mutex> lk(s->mu);
     gsdr::DeviceGuard g(s->device);
-    return gsdr::release_locked(s, (hipStream_t)consumer_stream);
+    const int rc = gsdr::release_locked(s, (hipStream_t)consumer_stream);
+    // the reader event now covers this consumer's reads: its windows close
+    const hipStream_t c = (hipStream_t)consumer_stream;
+    s->open.erase(std::remove_if(s->open.begin(), s->open.end(), [c](const gsdr_stream::OpenWindow& w) {
+        return w.consumer == c;
+    }), s->open.end());
+    s->released.notify_all();
+    return rc;
 }
 
 int gsdr_stream_device(const gsdr_stream* s, int* device)

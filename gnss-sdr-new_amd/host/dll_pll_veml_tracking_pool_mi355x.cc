@@ -13,15 +13,20 @@ namespace
 std::runtime_error gsdr_error(const char* what) { return std::runtime_error(std::string(what) + ": " + gsdr_last_error()); }
 }  // namespace
 
-SharedTrackingPool::SharedTrackingPool(const Dll_Pll_Conf& conf, int32_t signal, uint32_t max_channels, int device)
+SharedTrackingPool::SharedTrackingPool(const Dll_Pll_Conf& conf, int32_t signal, uint32_t max_channels, int device,
+    uint32_t window_calls)
     : d_conf(conf), d_signal(signal), d_max(max_channels), d_device(device)
 {
     const gsdr_trk_conf c = d_conf.to_engine(signal, max_channels);
     if (gsdr_trk_create(device, &c, &d_engine) != GSDR_OK) throw gsdr_error("SharedTrackingPool");
     d_item_bytes = c.item_type == GSDR_ITEM_CSHORT ? 4 : (c.item_type == GSDR_ITEM_IBYTE ? 2 : 8);
-    // the newest window every channel's next call must fall in: a few calls' worth
-    // (two forecasts of slack behind the head), and twice that of ring positions
-    d_window = 8ULL * d_conf.vector_length;
+    // the newest window every channel's next call must fall in: window_calls calls'
+    // worth (default 8: four forecasts of slack behind the head), and twice that of
+    // ring positions.  A block whose nitems_read lags the pool head by more (a
+    // flowgraph buffer deeper than that) needs a larger <role>.mi355x_pool_window.
+    if (window_calls < 4)
+        throw std::invalid_argument("SharedTrackingPool: mi355x_pool_window must be >= 4 vector lengths");
+    d_window = static_cast<uint64_t>(window_calls) * d_conf.vector_length;
     if (gsdr_stream_create(device, c.item_type, 2 * d_window, d_window, &d_ring) != GSDR_OK)
         {
             gsdr_trk_destroy(d_engine);
@@ -40,14 +45,14 @@ SharedTrackingPool::~SharedTrackingPool()
 }
 
 std::shared_ptr<SharedTrackingPool> SharedTrackingPool::get(const std::string& key, const Dll_Pll_Conf& conf,
-    int32_t signal, uint32_t max_channels, int device)
+    int32_t signal, uint32_t max_channels, int device, uint32_t window_calls)
 {
     static std::mutex mu;
     static std::map<std::tuple<std::string, int, int32_t>, std::weak_ptr<SharedTrackingPool>> registry;
     std::lock_guard<std::mutex> lk(mu);
     auto& w = registry[std::make_tuple(key, device, signal)];
     if (auto p = w.lock()) return p;
-    auto p = std::make_shared<SharedTrackingPool>(conf, signal, max_channels, device);
+    auto p = std::make_shared<SharedTrackingPool>(conf, signal, max_channels, device, window_calls);
     w = p;
     return p;
 }
@@ -176,11 +181,11 @@ void SharedTrackingPool::drop(int slot)
 }
 
 dll_pll_veml_tracking_pool_mi355x::dll_pll_veml_tracking_pool_mi355x(const Dll_Pll_Conf& conf, int32_t signal,
-    uint32_t pool_channels, int device, const std::string& pool_key)
+    uint32_t pool_channels, int device, const std::string& pool_key, uint32_t window_calls)
     : d_conf(conf), d_signal(signal)
 {
     if (d_conf.dump) d_dump.configure(d_conf.dump_filename);
-    d_pool = SharedTrackingPool::get(pool_key, conf, signal, pool_channels, device);
+    d_pool = SharedTrackingPool::get(pool_key, conf, signal, pool_channels, device, window_calls);
     d_slot = d_pool->acquire_slot();
     if (d_slot < 0)
         throw std::runtime_error("dll_pll_veml_tracking_pool_mi355x: every slot of pool '" + pool_key + "' is taken");
@@ -260,8 +265,17 @@ int dll_pll_veml_tracking_pool_mi355x::work(const void* in, int ninput_items, ui
         }
     catch (const std::exception& e)
         {
-            // device error -> loss of lock, the reference's failure convention
+            // device error -> loss of lock, the reference's failure convention; the
+            // slot leaves the engine so later advances stop queueing its records
             std::cerr << "dll_pll_veml_tracking_pool_mi355x: " << e.what() << '\n';
+            try
+                {
+                    d_pool->stop(d_slot);
+                }
+            catch (const std::exception& e2)
+                {
+                    std::cerr << "dll_pll_veml_tracking_pool_mi355x: stop after error: " << e2.what() << '\n';
+                }
             d_state = 0;
             if (d_events) d_events(3);
             return 0;
@@ -299,6 +313,14 @@ int dll_pll_veml_tracking_pool_mi355x::work(const void* in, int ninput_items, ui
         }
     if (loss_of_lock)
         {
+            if (d_last.flags & GSDR_TRK_F_OVERRUN)
+                {
+                    // not a signal loss: the call fell out of the pool's ring window
+                    ++d_overruns;
+                    std::cerr << "dll_pll_veml_tracking_pool_mi355x: channel " << d_channel << " call at "
+                              << d_last.sample_counter << " fell out of the ring window (" << d_pool->window_items()
+                              << " items behind the newest pushed; raise <role>.mi355x_pool_window)\n";
+                }
             d_state = 0;
             if (d_events) d_events(3);
         }

@@ -33,7 +33,12 @@
 class SharedTrackingPool
 {
 public:
-    SharedTrackingPool(const Dll_Pll_Conf& conf, int32_t signal, uint32_t max_channels, int device);
+    // window_calls: the ring window in vector lengths -- how far (in items) a
+    // channel's next call may start behind the newest pushed item before the
+    // engine reports it as an overrun (loss of lock with GSDR_TRK_F_OVERRUN)
+    SharedTrackingPool(const Dll_Pll_Conf& conf, int32_t signal, uint32_t max_channels, int device,
+        uint32_t window_calls = kDefaultWindowCalls);
+    static constexpr uint32_t kDefaultWindowCalls = 8;
     ~SharedTrackingPool();
     SharedTrackingPool(const SharedTrackingPool&) = delete;
     SharedTrackingPool& operator=(const SharedTrackingPool&) = delete;
@@ -41,7 +46,7 @@ public:
     // the pool of (key, device, signal): created by the first block, shared by the
     // rest while any holds it (GNSSBlockFactory builds one block per channel)
     static std::shared_ptr<SharedTrackingPool> get(const std::string& key, const Dll_Pll_Conf& conf, int32_t signal,
-        uint32_t max_channels, int device);
+        uint32_t max_channels, int device, uint32_t window_calls = kDefaultWindowCalls);
 
     int acquire_slot();  // -1 when every slot is taken
     void release_slot(int slot);
@@ -61,6 +66,7 @@ public:
     size_t item_bytes() const { return d_item_bytes; }
     uint64_t launches() const { return d_launches; }
     uint64_t pushed() const { return d_head - d_origin; }
+    uint64_t window_items() const { return d_window; }
 
 private:
     void advance_locked();
@@ -87,9 +93,10 @@ private:
 class dll_pll_veml_tracking_pool_mi355x : public TrackingBlockMI355X
 {
 public:
-    // pool_key: the pool's registry key (the adapters use role + device)
+    // pool_key: the pool's registry key (the adapters use role + device);
+    // window_calls: <role>.mi355x_pool_window (SharedTrackingPool)
     dll_pll_veml_tracking_pool_mi355x(const Dll_Pll_Conf& conf, int32_t signal, uint32_t pool_channels, int device,
-        const std::string& pool_key);
+        const std::string& pool_key, uint32_t window_calls = SharedTrackingPool::kDefaultWindowCalls);
     ~dll_pll_veml_tracking_pool_mi355x() override;
 
     void set_gnss_synchro(Gnss_Synchro* p_gnss_synchro) override;
@@ -102,6 +109,9 @@ public:
     int32_t state() const override { return d_state; }
     const gsdr_trk_epoch& last_record() const override { return d_last; }
     SharedTrackingPool* pool() { return d_pool.get(); }
+    // loss-of-lock records the engine marked GSDR_TRK_F_OVERRUN (the channel's next
+    // call started before the oldest item the ring window still held)
+    uint64_t overruns() const { return d_overruns; }
 
 private:
     Dll_Pll_Conf d_conf;
@@ -114,6 +124,7 @@ private:
     gsdr_trk_epoch d_last{};
     std::function<void(int)> d_events;
     std::mutex d_setlock;
+    uint64_t d_overruns{0};
     TrackingDump d_dump;  // <role>.dump: the reference's per-channel .dat (log_data)
 };
 

@@ -1038,7 +1038,7 @@ PoolRun run_tracking_blocks(bool pooled, const std::vector<std::complex<float>>&
     config.set_property("Tracking_1C.dll_bw_hz", "4.0");
     config.set_property("Tracking_1C.pull_in_time_s", "0");
     config.set_property("Channels_1C.count", std::to_string(acq.size()));
-    if (pooled) config.set_property("Tracking_1C.mi355x_pool", "true");
+    config.set_property("Tracking_1C.mi355x_pool", pooled ? "true" : "false");
     if (!dump_filename.empty())
         {
             config.set_property("Tracking_1C.dump", "true");

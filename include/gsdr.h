@@ -105,10 +105,13 @@ int gsdr_stream_window(gsdr_stream* stream, uint64_t first_sample, uint64_t n_it
 /* Asynchronous reader: the same window, with consumer_stream (a hipStream_t)
  * made to wait for the pushes so far; after enqueuing its reads the caller calls
  * gsdr_stream_release(stream, consumer_stream), and every later push waits for
- * those reads before it overwrites ring positions.  With pushes from another
- * thread, the caller keeps the two calls and its launches between them free of
- * any wait on that thread.  The library's own consumers (gsdr_acq_run_stream,
- * gsdr_trk_run_stream) hold the ring lock from window to release. */
+ * those reads before it overwrites ring positions.  Between the two calls the
+ * window is open: a push from another thread that would overwrite it blocks
+ * until the release, and such a push from the thread that opened it returns
+ * GSDR_E_STATE (release first).  With pushes from another thread, the caller keeps
+ * the two calls and its launches between them free of any wait on that thread.
+ * The library's own consumers (gsdr_acq_run_stream, gsdr_trk_run_stream) hold the
+ * ring lock from window to release. */
 int gsdr_stream_window_async(gsdr_stream* stream, uint64_t first_sample, uint64_t n_items, void* consumer_stream,
     const void** iq_dev);
 int gsdr_stream_release(gsdr_stream* stream, void* consumer_stream);

@@ -34,6 +34,8 @@ def lib():
         L.orc_resampler_32fc_xn.argtypes = [_p, _p, _f, _f, _p, _u, _i, _u, _i]
         L.orc_high_dyn_resampler_32f_xn.argtypes = [_p, _p, _f, _f, _f, _p, _u, _i, _u]
         L.orc_rotator_dot_prod_32fc_32f_xn.argtypes = [_p, _p, _f, _f, _p, _p, _i, _u]
+        L.orc_rotator_dot_prod_32fc_32f_xn_avx.argtypes = [_p, _p, _f, _f, _p, _p, _i, _u]
+        L.orc_multicorrelator_real_codes_avx.argtypes = [_p, _p, _p, _u, _p, _i, _f, _f, _f, _f, _u]
         L.orc_rotator_dot_prod_32fc_x2_xn.argtypes = [_p, _p, _f, _f, _p, _p, _i, _u]
         L.orc_high_dyn_rotator_dot_prod_32fc_32f_xn.argtypes = [_p, _p, _f, _f, _f, _f, _p, _p, _i, _u]
         L.orc_s32f_sincos_32fc.argtypes = [_p, _f, _p, _u]
@@ -89,6 +91,18 @@ def rotator_dot_prod_32fc_32f_xn(x, inc, phase, a):
     return out, complex(ph[0], ph[1])
 
 
+def rotator_dot_prod_32fc_32f_xn_avx(x, inc, phase, a):
+    """The u_avx / a_avx rotator the reference dispatches on x86 (volk_oracle.c)."""
+    x = _c(x, np.complex64)
+    a = _c(a, np.float32)
+    K, N = a.shape
+    ph = np.array([phase.real, phase.imag], np.float32)
+    out = np.empty(K, np.complex64)
+    lib().orc_rotator_dot_prod_32fc_32f_xn_avx(_ptr(out), _ptr(x), float(inc.real), float(inc.imag), _ptr(ph),
+                                               _ptr(a), K, N)
+    return out, complex(ph[0], ph[1])
+
+
 def s32f_sincos_32fc(phase_inc, N, phase=0.0):
     out = np.empty(N, np.complex64)
     ph = np.array([phase], np.float32)
@@ -111,6 +125,17 @@ def multicorrelator_real_codes(sig, code, shifts, rem_carr, carr_step, rem_code,
     lib().orc_multicorrelator_real_codes(_ptr(out), _ptr(sig), _ptr(code), len(code), _ptr(shifts), len(shifts),
                                          rem_carr, carr_step, carr_rate, rem_code, code_step, code_rate, N,
                                          int(high_dyn), assoc)
+    return out
+
+
+def multicorrelator_real_codes_avx(sig, code, shifts, rem_carr, carr_step, rem_code, code_step, N):
+    """The same call with the AVX rotator (u_avx / a_avx) the reference runs on x86."""
+    sig = _c(sig, np.complex64)
+    code = _c(code, np.float32)
+    shifts = _c(shifts, np.float32)
+    out = np.empty(len(shifts), np.complex64)
+    lib().orc_multicorrelator_real_codes_avx(_ptr(out), _ptr(sig), _ptr(code), len(code), _ptr(shifts),
+                                             len(shifts), rem_carr, carr_step, rem_code, code_step, N)
     return out
 
 

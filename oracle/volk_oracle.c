@@ -163,6 +163,98 @@ void orc_rotator_dot_prod_32fc_32f_xn(float* result, const float* in, float inc_
     phase[1] = ph.im;
 }
 
+/* KERN/32fc_32f_rotator_dot_prod_32fc_xn.h:155-314 (u_avx) and :318-480 (a_avx,
+ * identical arithmetic): the kernel the reference's dispatcher runs on x86 with AVX
+ * (VOLK/lib/volk_gnsssdr_rank_archs.c:76-100 picks the highest-ranked machine).
+ * Sixteen phasor lanes z_j = phase * inc^j (C complex products, :188-193), each
+ * advanced by dz = inc^16 (four squarings, :200-204; normalised once, :211)
+ * after it is used; lane j of block m accumulates (x[16m+j] z_j) a_k[16m+j] in its
+ * own accumulator (:222-253); the lanes are renormalised when m % 64 == 0, after
+ * the block's update (:257-263); the 16 accumulators are summed as
+ * ((v_j + v_{4+j}) + v_{8+j}) + v_{12+j} per j < 4, then 0 + s_0 + s_1 + s_2 + s_3
+ * (:266-279); the tail continues from lane 0's phasor, normalised (:282-296), with
+ * the scalar product order of the generic kernel.
+ * _mm256_complexmul_ps (volk_gnsssdr_avx_intrinsics.h:20-29) = cmul;
+ * _mm256_complexnormalise_ps (:56-63): z / sqrtf(re*re + im*im) by division. */
+static inline cf32 cnorm_avx(cf32 z)
+{
+    const float r = sqrtf(z.re * z.re + z.im * z.im);
+    cf32 o = {z.re / r, z.im / r};
+    return o;
+}
+
+void orc_rotator_dot_prod_32fc_32f_xn_avx(float* result, const float* in, float inc_re, float inc_im,
+    float* phase, const float* a, int K, unsigned int N)
+{
+    cf32* res = (cf32*)result;
+    const cf32* x = (const cf32*)in;
+    const cf32 inc = {inc_re, inc_im};
+    cf32 ph = {phase[0], phase[1]};
+    const unsigned int sixteenth = N / 16;
+    cf32 z[16];
+    for (int j = 0; j < 16; j++)
+        {
+            z[j] = ph;
+            ph = cmul(ph, inc);
+        }
+    cf32 dz = inc;
+    dz = cmul(dz, dz);
+    dz = cmul(dz, dz);
+    dz = cmul(dz, dz);
+    dz = cmul(dz, dz);
+    dz = cnorm_avx(dz);
+    cf32* acc = (cf32*)calloc((size_t)K * 16, sizeof(cf32));
+    for (unsigned int m = 0; m < sixteenth; m++)
+        {
+            cf32 t[16];
+            for (int j = 0; j < 16; j++)
+                {
+                    t[j] = cmul(x[16 * m + j], z[j]);
+                    z[j] = cmul(z[j], dz);
+                }
+            for (int k = 0; k < K; k++)
+                for (int j = 0; j < 16; j++)
+                    {
+                        const float b = a[(size_t)k * N + 16 * m + j];
+                        cf32* v = &acc[(size_t)k * 16 + j];
+                        const float cr = t[j].re * b, ci = t[j].im * b;
+                        v->re = cr + v->re;
+                        v->im = ci + v->im;
+                    }
+            if (m % 64 == 0)
+                for (int j = 0; j < 16; j++) z[j] = cnorm_avx(z[j]);
+        }
+    for (int k = 0; k < K; k++)
+        {
+            const cf32* v = &acc[(size_t)k * 16];
+            cf32 r = {0.0f, 0.0f};
+            for (int j = 0; j < 4; j++)
+                {
+                    cf32 s;
+                    s.re = ((v[j].re + v[4 + j].re) + v[8 + j].re) + v[12 + j].re;
+                    s.im = ((v[j].im + v[4 + j].im) + v[8 + j].im) + v[12 + j].im;
+                    r.re += s.re;
+                    r.im += s.im;
+                }
+            res[k] = r;
+        }
+    free(acc);
+    ph = cnorm_avx(z[0]);
+    for (unsigned int n = sixteenth * 16; n < N; n++)
+        {
+            const cf32 wo = cmul(x[n], ph);
+            ph = cmul(ph, inc);
+            for (int k = 0; k < K; k++)
+                {
+                    const cf32 p = cscale(wo, a[(size_t)k * N + n]);
+                    res[k].re += p.re;
+                    res[k].im += p.im;
+                }
+        }
+    phase[0] = ph.re;
+    phase[1] = ph.im;
+}
+
 /* KERN/32fc_x2_rotator_dot_prod_32fc_xn.h:67-104 (generic, complex replicas). */
 void orc_rotator_dot_prod_32fc_x2_xn(float* result, const float* in, float inc_re, float inc_im,
     float* phase, const float* a, int K, unsigned int N)
@@ -287,6 +379,19 @@ void orc_multicorrelator_real_codes(float* out, const float* sig, const float* c
         {
             orc_rotator_dot_prod_32fc_32f_xn(out, sig, crealf(inc), cimagf(inc), ph, rs, K, N);
         }
+    free(rs);
+}
+
+/* The same correlator call with the rotator the reference dispatches on x86
+ * (u_avx / a_avx above) after the a_avx resampler association (assoc 1). */
+void orc_multicorrelator_real_codes_avx(float* out, const float* sig, const float* code, unsigned int L,
+    const float* shifts, int K, float rem_carr, float carr_step, float rem_code, float code_step, unsigned int N)
+{
+    float* rs = (float*)malloc((size_t)K * N * sizeof(float));
+    orc_resampler_32f_xn(rs, code, rem_code, code_step, shifts, L, K, N, 1);
+    float ph[2] = {cosf(rem_carr), -sinf(rem_carr)};
+    float complex inc = cexpf(0.0f + I * (-carr_step));
+    orc_rotator_dot_prod_32fc_32f_xn_avx(out, sig, crealf(inc), cimagf(inc), ph, rs, K, N);
     free(rs);
 }
 

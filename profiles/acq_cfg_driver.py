@@ -16,7 +16,7 @@ sys.path.insert(0, os.path.join(ROOT, "gnss-sdr-new_amd"))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--cfg", choices=["C3", "C4"], default="C3")
+    ap.add_argument("--cfg", choices=["C3", "C4", "C4s", "C5g", "C5e"], default="C3")
     ap.add_argument("--iters", type=int, default=3)
     a = ap.parse_args()
     import torch
@@ -30,6 +30,32 @@ def main():
         acq = gsdr.Acquisition(fs, N, 10000, 250, pfa=0.01, max_prns=32, max_blocks=B, num_doppler_bins=81)
         acq.set_local_codes(np.stack([synth.gps_ca_sampled(p, fs) for p in range(1, 33)]), np.arange(1, 33))
         P, n_call = 32, N
+    elif a.cfg == "C4s":  # C4 without bit transition: one 4 ms period, FFT 32000
+        fs, N, B = 8000000, 32000, 4
+        rng = np.random.default_rng(4)
+        gsats = [synth.GalileoSatellite(p, float(rng.uniform(-4000, 4000)), float(rng.uniform(0, 4092)), 46.0,
+                                        float(rng.uniform(0, 6.28))) for p in range(1, 9)]
+        iq = synth.gal_e1_iq(fs, B * N + N, gsats, seed_offset=4)
+        acq = gsdr.Acquisition(fs, N, 5000, 125, pfa=0.0, max_prns=36, max_blocks=B, sampled_ms=4, ms_per_code=4)
+        codes = np.stack([synth.gal_e1_sampled(p, fs, pilot=True)[:N] for p in range(1, 37)])
+        acq.set_local_codes(codes, np.arange(1, 37))
+        acq.set_threshold(2.5)
+        P, n_call = 36, N
+    elif a.cfg in ("C5g", "C5e"):  # one GPU's C5 share: GPS N = 25000 / Galileo N = 100000
+        fs, B = 25000000, 4
+        N = 25000 if a.cfg == "C5g" else 100000
+        sats = synth.random_constellation(8, seed_offset=5, prns=list(range(1, 9)))
+        iq = synth.gps_l1_iq(fs, B * N + N, sats, seed_offset=5)
+        ms = N // 25000
+        P = 32 if a.cfg == "C5g" else 36
+        acq = gsdr.Acquisition(fs, N, 10000 if ms == 1 else 5000, 250, pfa=0.01, max_prns=P, max_blocks=B,
+                               sampled_ms=ms, ms_per_code=ms)
+        if a.cfg == "C5g":
+            codes = np.stack([synth.gps_ca_sampled(p, fs) for p in range(1, 33)])
+        else:
+            codes = np.stack([synth.gal_e1_sampled(p, fs, pilot=True)[:N] for p in range(1, 37)])
+        acq.set_local_codes(codes, np.arange(1, P + 1))
+        n_call = N
     else:
         fs, N, B = 8000000, 32000, 4
         rng = np.random.default_rng(4)

@@ -75,6 +75,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--only", default="C3,C4,C5")
+    ap.add_argument("--acq-only", action="store_true", help="only the acquisition lines (A/B sweeps)")
     a = ap.parse_args()
     import torch
     import gsdr
@@ -90,47 +91,48 @@ def main():
         ms = 100
         iq = synth.gps_l1_iq(fs, ms * N + N, sats, seed_offset=3)
         iq_dev = torch.from_numpy(iq.view(np.float32).copy()).to(dev)
-        # 5-tap multicorrelator epochs (one launch per epoch, 12 channel jobs)
-        corr = gsdr.Correlator(nch, N + 64, max_taps=5)
-        sh = np.array([-0.5, -0.25, 0.0, 0.25, 0.5], np.float32)
-        for c, s in enumerate(sats):
-            corr.set_local_code_and_taps(c, synth.gps_ca_chips(s.prn), sh)
-        jl = []
-        for e in range(ms):
+        if not a.acq_only:
+            # 5-tap multicorrelator epochs (one launch per epoch, 12 channel jobs)
+            corr = gsdr.Correlator(nch, N + 64, max_taps=5)
+            sh = np.array([-0.5, -0.25, 0.0, 0.25, 0.5], np.float32)
             for c, s in enumerate(sats):
-                j = gsdr.CorrJob()
-                j.channel, j.n_samples, j.sample_offset = c, N, e * N
-                j.rem_carr_phase_rad = 0.1
-                j.carr_phase_step_rad = float(np.float32(2 * np.pi * s.doppler_hz / fs))
-                j.carr_phase_rate_step_rad = 0.0
-                j.rem_code_phase_chips = 0.3
-                j.code_phase_step_chips = float(np.float32(1.023e6 / fs))
-                j.code_phase_rate_step_chips = 0.0
-                jl.append(j)
-        jarr = (gsdr.CorrJob * len(jl))(*jl)
-        jbytes = bytes(jarr)
-        jobs_dev = torch.frombuffer(bytearray(jbytes), dtype=torch.uint8).to(dev)
-        out_dev = torch.zeros(ms * nch * 8 * 2, dtype=torch.float32, device=dev)
-        sec = timed(lambda: corr.run_epochs(jobs_dev.data_ptr(), nch, ms, iq_dev.data_ptr(), len(iq), out_dev.data_ptr()),
-                    a.reps, 3, torch)
-        emit("C3", "multicorrelator 12 ch x 5 taps (epoch launches)", fs, ms * N, sec,
-             {"hbm_gbps_algorithmic": round(ms * nch * (8 * N + 8 * 5) / sec / 1e9, 1)})
-        corr.close()
-        # tracking loop, 12 channels
-        trk = gsdr.Tracking(trk_conf(gsdr, fs, gsdr.SIGNAL_GPS_1C, nch, pll_bw_hz=40.0, dll_bw_hz=4.0))
-        for c, s in enumerate(sats):
-            tau = s.code_delay_chips / (1.023e6 * (1 + s.doppler_hz / 1.57542e9)) * fs
-            trk.start(c, s.prn, synth.gps_ca_chips(s.prn), float(round(tau) % N), 250.0 * round(s.doppler_hz / 250.0), 0, 0)
-        trk.save_state(0)
-        out = torch.zeros(nch * ms * gsdr.TRK_EPOCH_DTYPE.itemsize, dtype=torch.uint8, device=dev)
-        nout = torch.zeros(nch, dtype=torch.int32, device=dev)
+                corr.set_local_code_and_taps(c, synth.gps_ca_chips(s.prn), sh)
+            jl = []
+            for e in range(ms):
+                for c, s in enumerate(sats):
+                    j = gsdr.CorrJob()
+                    j.channel, j.n_samples, j.sample_offset = c, N, e * N
+                    j.rem_carr_phase_rad = 0.1
+                    j.carr_phase_step_rad = float(np.float32(2 * np.pi * s.doppler_hz / fs))
+                    j.carr_phase_rate_step_rad = 0.0
+                    j.rem_code_phase_chips = 0.3
+                    j.code_phase_step_chips = float(np.float32(1.023e6 / fs))
+                    j.code_phase_rate_step_chips = 0.0
+                    jl.append(j)
+            jarr = (gsdr.CorrJob * len(jl))(*jl)
+            jbytes = bytes(jarr)
+            jobs_dev = torch.frombuffer(bytearray(jbytes), dtype=torch.uint8).to(dev)
+            out_dev = torch.zeros(ms * nch * 8 * 2, dtype=torch.float32, device=dev)
+            sec = timed(lambda: corr.run_epochs(jobs_dev.data_ptr(), nch, ms, iq_dev.data_ptr(), len(iq), out_dev.data_ptr()),
+                        a.reps, 3, torch)
+            emit("C3", "multicorrelator 12 ch x 5 taps (epoch launches)", fs, ms * N, sec,
+                 {"hbm_gbps_algorithmic": round(ms * nch * (8 * N + 8 * 5) / sec / 1e9, 1)})
+            corr.close()
+            # tracking loop, 12 channels
+            trk = gsdr.Tracking(trk_conf(gsdr, fs, gsdr.SIGNAL_GPS_1C, nch, pll_bw_hz=40.0, dll_bw_hz=4.0))
+            for c, s in enumerate(sats):
+                tau = s.code_delay_chips / (1.023e6 * (1 + s.doppler_hz / 1.57542e9)) * fs
+                trk.start(c, s.prn, synth.gps_ca_chips(s.prn), float(round(tau) % N), 250.0 * round(s.doppler_hz / 250.0), 0, 0)
+            trk.save_state(0)
+            out = torch.zeros(nch * ms * gsdr.TRK_EPOCH_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+            nout = torch.zeros(nch, dtype=torch.int32, device=dev)
 
-        def trk_step():
-            trk.restore_state(0)
-            trk.run_device(iq_dev.data_ptr(), 0, len(iq), ms - 1, out.data_ptr(), nout.data_ptr())
-        sec = timed(trk_step, a.reps, 2, torch)
-        emit("C3", "tracking loop 12 ch (3-tap dll_pll_veml_tracking)", fs, (ms - 1) * N, sec)
-        trk.close()
+            def trk_step():
+                trk.restore_state(0)
+                trk.run_device(iq_dev.data_ptr(), 0, len(iq), ms - 1, out.data_ptr(), nout.data_ptr())
+            sec = timed(trk_step, a.reps, 2, torch)
+            emit("C3", "tracking loop 12 ch (3-tap dll_pll_veml_tracking)", fs, (ms - 1) * N, sec)
+            trk.close()
         # acquisition grid
         B = 16
         acq = gsdr.Acquisition(fs, N, 10000, 250, pfa=0.01, max_prns=32, max_blocks=B, num_doppler_bins=81)
@@ -149,24 +151,25 @@ def main():
         calls = 60
         iq = synth.gal_e1_iq(fs, calls * N + 2 * N, gsats, seed_offset=4)
         iq_dev = torch.from_numpy(iq.view(np.float32).copy()).to(dev)
-        trk = gsdr.Tracking(trk_conf(gsdr, fs, gsdr.SIGNAL_GAL_1B, nch, track_pilot=1, pll_bw_hz=4.0, dll_bw_hz=0.5,
-                                     pll_bw_narrow_hz=2.0, dll_bw_narrow_hz=0.25, extend_correlation_symbols=4,
-                                     early_late_space_chips=0.15, very_early_late_space_chips=0.6,
-                                     early_late_space_narrow_chips=0.06, very_early_late_space_narrow_chips=0.25))
-        for c, s in enumerate(gsats):
-            tau = s.code_delay_chips / (1.023e6 * (1 + s.doppler_hz / 1.57542e9)) * fs
-            trk.start(c, s.prn, synth.gal_e1_sinboc11(s.prn, pilot=True), float(round(tau) % N),
-                      125.0 * round(s.doppler_hz / 125.0), 0, 0, data_code=synth.gal_e1_sinboc11(s.prn))
-        trk.save_state(0)
-        out = torch.zeros(nch * calls * gsdr.TRK_EPOCH_DTYPE.itemsize, dtype=torch.uint8, device=dev)
-        nout = torch.zeros(nch, dtype=torch.int32, device=dev)
+        if not a.acq_only:
+            trk = gsdr.Tracking(trk_conf(gsdr, fs, gsdr.SIGNAL_GAL_1B, nch, track_pilot=1, pll_bw_hz=4.0, dll_bw_hz=0.5,
+                                         pll_bw_narrow_hz=2.0, dll_bw_narrow_hz=0.25, extend_correlation_symbols=4,
+                                         early_late_space_chips=0.15, very_early_late_space_chips=0.6,
+                                         early_late_space_narrow_chips=0.06, very_early_late_space_narrow_chips=0.25))
+            for c, s in enumerate(gsats):
+                tau = s.code_delay_chips / (1.023e6 * (1 + s.doppler_hz / 1.57542e9)) * fs
+                trk.start(c, s.prn, synth.gal_e1_sinboc11(s.prn, pilot=True), float(round(tau) % N),
+                          125.0 * round(s.doppler_hz / 125.0), 0, 0, data_code=synth.gal_e1_sinboc11(s.prn))
+            trk.save_state(0)
+            out = torch.zeros(nch * calls * gsdr.TRK_EPOCH_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+            nout = torch.zeros(nch, dtype=torch.int32, device=dev)
 
-        def trk_step():
-            trk.restore_state(0)
-            trk.run_device(iq_dev.data_ptr(), 0, len(iq), calls, out.data_ptr(), nout.data_ptr())
-        sec = timed(trk_step, a.reps, 2, torch)
-        emit("C4", "tracking loop 8 ch Galileo E1 VEML pilot (+data prompt)", fs, calls * N, sec)
-        trk.close()
+            def trk_step():
+                trk.restore_state(0)
+                trk.run_device(iq_dev.data_ptr(), 0, len(iq), calls, out.data_ptr(), nout.data_ptr())
+            sec = timed(trk_step, a.reps, 2, torch)
+            emit("C4", "tracking loop 8 ch Galileo E1 VEML pilot (+data prompt)", fs, calls * N, sec)
+            trk.close()
         # acquisition, bit transition: 2 x 4 ms consumed, FFT 64000 (four-step), peak ratio
         B = 4
         acq = gsdr.Acquisition(fs, 2 * N, 5000, 125, pfa=0.0, max_prns=36, max_blocks=B, sampled_ms=4,
@@ -197,38 +200,39 @@ def main():
             s.code_doppler = True
         iq = synth.gps_l1_iq(fs, ms * 25000 + 200000, gps, seed_offset=5)
         iq_dev = torch.from_numpy(iq.view(np.float32).copy()).to(dev)
-        rng = np.random.default_rng(5)
-        pools = []
-        conf_g = trk_conf(gsdr, fs, gsdr.SIGNAL_GPS_1C, 12, pll_bw_hz=40.0, dll_bw_hz=4.0)
-        tg = gsdr.Tracking(conf_g)
-        for c, s in enumerate(gps):
-            tau = s.code_delay_chips / (1.023e6 * (1 + s.doppler_hz / 1.57542e9)) * fs
-            tg.start(c, s.prn, synth.gps_ca_chips(s.prn), float(round(tau) % 25000), 250.0 * round(s.doppler_hz / 250.0), 0, 0)
-        pools.append((tg, ms - 2))
-        te = gsdr.Tracking(trk_conf(gsdr, fs, gsdr.SIGNAL_GAL_1B, 12, track_pilot=1, pll_bw_hz=15.0, dll_bw_hz=1.0))
-        for c in range(12):
-            te.start(c, c + 1, synth.gal_e1_sinboc11(c + 1, pilot=True), float(rng.integers(0, 100000)), 500.0, 0, 0,
-                     data_code=synth.gal_e1_sinboc11(c + 1))
-        pools.append((te, ms // 4 - 2))
-        tb = gsdr.Tracking(trk_conf(gsdr, fs, gsdr.SIGNAL_BDS_B1, 8, pll_bw_hz=15.0, dll_bw_hz=1.0))
-        for c in range(8):
-            tb.start(c, 6 + c, synth.bds_b1i_chips(6 + c), float(rng.integers(0, 25000)), -750.0, 0, 0)
-        pools.append((tb, ms - 2))
-        bufs = []
-        for t, n in pools:
-            t.save_state(0)
-            bufs.append((torch.zeros(t.max_channels * n * gsdr.TRK_EPOCH_DTYPE.itemsize, dtype=torch.uint8, device=dev),
-                         torch.zeros(t.max_channels, dtype=torch.int32, device=dev)))
+        if not a.acq_only:
+            rng = np.random.default_rng(5)
+            pools = []
+            conf_g = trk_conf(gsdr, fs, gsdr.SIGNAL_GPS_1C, 12, pll_bw_hz=40.0, dll_bw_hz=4.0)
+            tg = gsdr.Tracking(conf_g)
+            for c, s in enumerate(gps):
+                tau = s.code_delay_chips / (1.023e6 * (1 + s.doppler_hz / 1.57542e9)) * fs
+                tg.start(c, s.prn, synth.gps_ca_chips(s.prn), float(round(tau) % 25000), 250.0 * round(s.doppler_hz / 250.0), 0, 0)
+            pools.append((tg, ms - 2))
+            te = gsdr.Tracking(trk_conf(gsdr, fs, gsdr.SIGNAL_GAL_1B, 12, track_pilot=1, pll_bw_hz=15.0, dll_bw_hz=1.0))
+            for c in range(12):
+                te.start(c, c + 1, synth.gal_e1_sinboc11(c + 1, pilot=True), float(rng.integers(0, 100000)), 500.0, 0, 0,
+                         data_code=synth.gal_e1_sinboc11(c + 1))
+            pools.append((te, ms // 4 - 2))
+            tb = gsdr.Tracking(trk_conf(gsdr, fs, gsdr.SIGNAL_BDS_B1, 8, pll_bw_hz=15.0, dll_bw_hz=1.0))
+            for c in range(8):
+                tb.start(c, 6 + c, synth.bds_b1i_chips(6 + c), float(rng.integers(0, 25000)), -750.0, 0, 0)
+            pools.append((tb, ms - 2))
+            bufs = []
+            for t, n in pools:
+                t.save_state(0)
+                bufs.append((torch.zeros(t.max_channels * n * gsdr.TRK_EPOCH_DTYPE.itemsize, dtype=torch.uint8, device=dev),
+                             torch.zeros(t.max_channels, dtype=torch.int32, device=dev)))
 
-        def step():
-            for (t, n), (o, no) in zip(pools, bufs):
-                t.restore_state(0)
-                t.run_device(iq_dev.data_ptr(), 0, len(iq), n, o.data_ptr(), no.data_ptr())
-        sec = timed(step, a.reps, 2, torch)
-        emit("C5", "tracking pool 12 GPS + 12 Galileo + 8 BeiDou (one GPU's share), three streams", fs,
-             (ms - 2) * 25000, sec)
-        for t, _ in pools:
-            t.close()
+            def step():
+                for (t, n), (o, no) in zip(pools, bufs):
+                    t.restore_state(0)
+                    t.run_device(iq_dev.data_ptr(), 0, len(iq), n, o.data_ptr(), no.data_ptr())
+            sec = timed(step, a.reps, 2, torch)
+            emit("C5", "tracking pool 12 GPS + 12 Galileo + 8 BeiDou (one GPU's share), three streams", fs,
+                 (ms - 2) * 25000, sec)
+            for t, _ in pools:
+                t.close()
         # acquisition grids of one GPU's C5 share at 25 Msps: GPS L1 C/A and BeiDou B1I
         # (1 ms, N = 25000 = 5 x 5000 four-step), Galileo E1 (4 ms, N = 100000 = 25 x 4000)
         B = 4

@@ -110,7 +110,7 @@ def test_bit_transition(pfa):
             assert res[b, i]["samplestamp"] == b * 2 * C
 
 
-@pytest.mark.parametrize("split", ["1", "0", "2", "id6"])
+@pytest.mark.parametrize("split", ["1", "0", "2", "id6", "id13", "id16", "id20"])
 @pytest.mark.parametrize("pfa", [0.01, 0.0])
 def test_bit_transition_c4_four_step(monkeypatch, pfa, split):
     """Config C4's acquisition as the bench times it (pcps_acquisition.cc:85-92,
@@ -118,10 +118,11 @@ def test_bit_transition_c4_four_step(monkeypatch, pfa, split):
     64000 with the code in the second half and outputs [32000, 64000), +-10 kHz /
     250 Hz (80 bins): the split register four-step (default and GSDR_ACQ_SPLIT=2:
     ROUT = 2 over a 32000-point register transform, row maxima of outputs k >= N/2;
-    id6: ROUT = 4 over 16000 points) and the general (dwell) path over the packed
-    four-step (GSDR_ACQ_SPLIT=0)."""
-    if split == "id6":  # ROUT = 4 over the 16000-point register transform (acq_split.hip)
-        monkeypatch.setenv("GSDR_ACQ_SPLIT_ID", "6")
+    id6: ROUT = 4 over 16000 points; id13 / id16 / id20: the wave-local-row plans,
+    acq_split.hip) and the general (dwell) path over the packed four-step
+    (GSDR_ACQ_SPLIT=0)."""
+    if split.startswith("id"):  # a forced split id of N = 64000 (acq_split.hip)
+        monkeypatch.setenv("GSDR_ACQ_SPLIT_ID", split[2:])
         split = "2"
     monkeypatch.setenv("GSDR_ACQ_SPLIT", split)
     fs, C, dmax, dstep = 8000000, 32000, 10000, 250

@@ -82,7 +82,13 @@ def test_beidou_b1i_synthetic_batch(fs):
     assert set(vis) <= det
 
 
-@pytest.mark.parametrize("split", ["1", "0", "2", "id5", "id6"])
+# acq_split.hip split ids and their FFT sizes (5/6: 16000-based splits; 11-20: the
+# wave-local-row plans)
+SPLIT_IDS = {5: 32000, 6: 64000, 11: 25000, 12: 32000, 13: 64000, 14: 100000, 15: 32000, 16: 64000, 17: 25000,
+             18: 100000, 19: 32000, 20: 64000}
+
+
+@pytest.mark.parametrize("split", ["1", "0", "2"] + ["id%d" % i for i in sorted(SPLIT_IDS)])
 @pytest.mark.parametrize("fs,N,pfa", [(8000000, 32000, 0.01), (25000000, 25000, 0.0), (8000000, 64000, 0.01),
                                       (25000000, 100000, 0.01), (25000000, 25000, 0.01), (25000000, 100000, 0.0)])
 def test_large_fft_four_step(monkeypatch, fs, N, pfa, split):
@@ -91,11 +97,11 @@ def test_large_fft_four_step(monkeypatch, fs, N, pfa, split):
     configs C4/C5 -- on every correlate path: GSDR_ACQ_SPLIT=1 (default: the split
     register four-step for 25000 / 32000 / 64000, the packed four-step for 100000),
     0 (the packed four-step everywhere), 2 (the split also for 100000 = 4 x 25000),
-    id5 / id6 (32000 = 2 x 16000, 64000 = 4 x 16000).
+    idK: split id K forced (SPLIT_IDS: the 16000-based splits and the wave-local-row plans).
     Parity with the oracle grid statistics."""
     if split.startswith("id"):
         # a forced split of this N (acq_split.hip: 5 = 2 x 16000, 6 = 4 x 16000)
-        if {"id5": 32000, "id6": 64000}[split] != N:
+        if SPLIT_IDS[int(split[2:])] != N:
             pytest.skip("split id for another FFT size")
         monkeypatch.setenv("GSDR_ACQ_SPLIT_ID", split[2:])
         split = "2"

@@ -133,7 +133,8 @@ def test_c3_gps_16msps_12_channel_pool():
 def test_c4_galileo_8msps_ibyte_extended_veml():
     fs = 8.0e6
     # Dopplers within the narrow (15 Hz) PLL's pull-in of the 250 Hz acquisition grid
-    sats = [synth.GalileoSatellite(p, dop, dl, 48.0, ph) for p, dop, dl, ph in
+    # SURVEY §8(d)'s 45 dB-Hz (the pilot carries half of it)
+    sats = [synth.GalileoSatellite(p, dop, dl, 45.0, ph) for p, dop, dl, ph in
             ((11, 1234.5, 1000.3, 0.7), (19, -2740.0, 3001.7, 2.1), (26, 505.0, 77.2, 4.0), (30, -995.0, 2500.9, 1.3))]
     x = synth.gal_e1_iq(fs, int(1.3 * fs), sats, seed_offset=35)
     host = synth.to_ibyte(x, 16.0)
@@ -159,14 +160,15 @@ def test_c5_hybrid_25msps_pool_share():
     fs = 25.0e6
     ns = int(0.22 * fs)
     rng = np.random.default_rng(37)
-    gps = synth.random_constellation(12, seed_offset=37, cn0_dbhz=46.0)
+    # SURVEY §8(d)'s 45 dB-Hz for every signal of the hybrid share
+    gps = synth.random_constellation(12, seed_offset=37, cn0_dbhz=45.0)
     for s in gps:
         s.code_doppler = True
     gal_prns = rng.choice(np.arange(1, 37), 12, replace=False)
-    gal = [synth.GalileoSatellite(int(p), float(rng.uniform(-4000, 4000)), float(rng.uniform(0, 4092)), 46.0,
+    gal = [synth.GalileoSatellite(int(p), float(rng.uniform(-4000, 4000)), float(rng.uniform(0, 4092)), 45.0,
                                   float(rng.uniform(0, 6.28))) for p in gal_prns]
     bds_prns = [3, 6, 8, 11, 14, 21, 33, 59]
-    bds = [synth.Satellite(p, float(rng.uniform(-4000, 4000)), float(rng.uniform(0, 2046)), 46.0,
+    bds = [synth.Satellite(p, float(rng.uniform(-4000, 4000)), float(rng.uniform(0, 2046)), 45.0,
                            float(rng.uniform(0, 6.28))) for p in bds_prns]
     iq = (synth.gps_l1_iq(fs, ns, gps, seed_offset=37, noise=False, dtype=np.complex128) +
           synth.gal_e1_iq(fs, ns, gal, seed_offset=37, noise=False, dtype=np.complex128) +

@@ -190,3 +190,74 @@ def test_two_thread_push_and_consume():
         th.join()
     assert ref_acq.shape == (1, len(prns))
     ring.close()
+
+
+def test_async_window_blocks_overwrite():
+    """gsdr_stream_window_async .. gsdr_stream_release with a producer thread: a push
+    that would overwrite a window still open waits for its release, so every block
+    read through the async window (acquisition on the consumer's own stream) equals
+    the contiguous result even though the producer is allowed to run into the open
+    block; a push over its own open window from the opening thread is refused
+    (GSDR_E_STATE) and leaves the ring unchanged."""
+    import threading
+    import time
+    ms = 40
+    sats = synth.random_constellation(4, seed_offset=31)
+    x = synth.gps_l1_iq(FS, (ms + 1) * N, sats, seed_offset=31)
+    codes = np.stack([synth.gps_ca_sampled(s.prn, FS) for s in sats])
+    prns = np.array([s.prn for s in sats])
+    acq = gsdr.Acquisition(FS, N, 10000, 250, pfa=0.01, max_prns=len(prns))
+    acq.set_local_codes(codes, prns)
+    cap = 3 * N
+    ring = gsdr.Stream(gsdr.ITEM_GR_COMPLEX, capacity_items=cap, max_window_items=N)
+    cs = torch.cuda.Stream()
+    rbytes = len(prns) * gsdr.ACQ_RESULT_DTYPE.itemsize
+    res = torch.zeros(rbytes, dtype=torch.uint8, device="cuda")
+    # the opening thread's own overwrite is refused
+    ring.push(x[:cap], 0)
+    ring.window_async(0, N, cs.cuda_stream)
+    with pytest.raises(gsdr.GsdrError) as ei:
+        ring.push(x[cap:cap + 1000], cap)
+    assert ei.value.code == gsdr.GSDR_E_STATE
+    ring.release(cs.cuda_stream)
+    pushed = [cap]
+    allowed = [0]  # the producer may overwrite samples below this
+    cv = threading.Condition()
+
+    def producer():
+        while pushed[0] < ms * N:
+            n = 1000
+            with cv:
+                while pushed[0] + n - cap > allowed[0]:
+                    cv.wait(0.05)
+            ring.push(x[pushed[0]:pushed[0] + n], pushed[0])  # may wait inside for a release
+            with cv:
+                pushed[0] += n
+                cv.notify_all()
+
+    th = threading.Thread(target=producer)
+    th.start()
+    try:
+        for b in range(ms):
+            with cv:
+                while pushed[0] < (b + 1) * N:
+                    cv.wait(0.05)
+            p = ring.window_async(b * N, N, cs.cuda_stream)
+            with cv:
+                allowed[0] = (b + 1) * N  # block b itself is now guarded only by the open window
+                cv.notify_all()
+            time.sleep(0.002)  # let the producer run into the open window
+            acq.run_device(p, 1, N, b * N, res.data_ptr(), stream_ptr=cs.cuda_stream)
+            ring.release(cs.cuda_stream)
+            cs.synchronize()
+            got = res.cpu().numpy().view(gsdr.ACQ_RESULT_DTYPE).reshape(1, len(prns))
+            ref = acq.run(x[b * N:(b + 1) * N], 1, stamp0=b * N)
+            assert got.tobytes() == ref.tobytes(), b
+    finally:
+        ring.release(cs.cuda_stream)  # never leave the producer waiting on an open window
+        with cv:
+            allowed[0] = 1 << 62
+            cv.notify_all()
+        th.join()
+    ring.close()
+    acq.close()

@@ -23,7 +23,7 @@ import gsdr
 from gsdr import synth
 from oracle import trk, volk
 
-from conftest import vnorm_rel
+from conftest import ccompare
 
 TWO_PI = 2.0 * 3.1415926535898  # MATH_CONSTANTS.h:47-49
 
@@ -63,9 +63,14 @@ def _open_loop_taps(g, iq, code, fs, acq_dop, el=0.25):
         rem_code = float(np.float32(code_freq * rem_samples / fs))
         code_step = float(np.float32(code_freq / fs))
         n0 = int(g[e]["sample_counter"])
-        ref = volk.multicorrelator_real_codes(iq[n0:n0 + vl], code, shifts, rem_carr, carr_step, rem_code, code_step,
-                                              vl)
-        worst = max(worst, vnorm_rel(g["taps"][e][:6].view(np.complex64), ref))
+        x = iq[n0:n0 + vl]
+        # per tap (ccompare, VOLK QA metric) against the rotator the reference runs on
+        # x86 (u_avx / a_avx) and against the fp64 evaluation of the same model
+        ref = volk.multicorrelator_real_codes_avx(x, code, shifts, rem_carr, carr_step, rem_code, code_step, vl)
+        got = g["taps"][e][:6].view(np.complex64)
+        exact = volk.multicorrelator_real_codes_exact(x, code, shifts, rem_carr, carr_step, rem_code, code_step, vl)
+        assert ccompare(got, exact) <= 1e-4, (e, ccompare(got, exact))
+        worst = max(worst, ccompare(got, ref))
     return worst
 
 
@@ -229,8 +234,13 @@ def _open_loop_sig(g, iq, code, data_code, fs, acq_dop, shifts_chips, spc, chip_
                    spread=None):
     """Check 1 for any signal: every call's taps (and the data prompt) against the
     oracle correlator fed with the GPU's own incoming NCO state (narrow tap shifts
-    in states 3/4 of the extended correlator).  spread (a dict) receives the worst
-    GPU-vs-fp64 and generic-VOLK-vs-fp64 distances over the calls."""
+    in states 3/4 of the extended correlator), per tap (ccompare, the VOLK QA
+    metric).  The bar: every tap within 1e-4 of the fp64 evaluation of
+    the reference's correlation model and within 1e-4 of the rotator the reference
+    dispatches on x86 (u_avx / a_avx, returned as the worst distance); the generic
+    kernel's own fp32 phase drift reaches ~1e-4 at 100000 samples,
+    so against it the GPU is held to 1e-4 beyond that kernel's own distance to fp64.
+    spread (a dict) receives the worst per-tap distances over the calls."""
     wide = (np.asarray(shifts_chips, np.float32) * np.float32(spc)).astype(np.float32)
     narrow = None if narrow_chips is None else (np.asarray(narrow_chips, np.float32) * np.float32(spc)).astype(np.float32)
     worst = 0.0
@@ -247,25 +257,24 @@ def _open_loop_sig(g, iq, code, data_code, fs, acq_dop, shifts_chips, spc, chip_
         code_step = float(np.float32(np.float32(code_freq / fs) * np.float32(spc)))
         n0 = int(g[e]["sample_counter"])
         x = iq[n0:n0 + vl]
-        ref = volk.multicorrelator_real_codes(x, code, shifts, rem_carr, carr_step, rem_code, code_step, vl)
-        got = g["taps"][e][:2 * len(shifts)].view(np.complex64)
-        # at large N (C3: 16000, C5: 25000/100000 samples) the generic rotator's own
-        # fp32 phase drift is of the order of the 1e-4 bar, so the
-        # distance to the oracle is taken beyond the oracle's own distance to the
-        # float64 evaluation of the same correlation, and the taps must also sit
-        # within 1e-4 of that float64 value
+        gen = volk.multicorrelator_real_codes(x, code, shifts, rem_carr, carr_step, rem_code, code_step, vl)
+        avx = volk.multicorrelator_real_codes_avx(x, code, shifts, rem_carr, carr_step, rem_code, code_step, vl)
         exact = volk.multicorrelator_real_codes_exact(x, code, shifts, rem_carr, carr_step, rem_code, code_step, vl)
-        ge, re = vnorm_rel(got, exact), vnorm_rel(ref, exact)
-        assert ge <= 1e-4, (e, ge)
+        got = g["taps"][e][:2 * len(shifts)].view(np.complex64)
+        d = {"gpu_vs_fp64": ccompare(got, exact), "gpu_vs_avx": ccompare(got, avx), "gpu_vs_generic": ccompare(got, gen),
+             "avx_vs_fp64": ccompare(avx, exact), "generic_vs_fp64": ccompare(gen, exact),
+             "generic_vs_avx": ccompare(gen, avx)}
+        assert d["gpu_vs_fp64"] <= 1e-4, (e, d)
+        assert d["gpu_vs_generic"] <= 1e-4 + d["generic_vs_fp64"], (e, d)
         if spread is not None:
-            spread["gpu_vs_fp64"] = max(spread.get("gpu_vs_fp64", 0.0), ge)
-            spread["volk_generic_vs_fp64"] = max(spread.get("volk_generic_vs_fp64", 0.0), re)
+            for k, v in d.items():
+                spread[k] = max(spread.get(k, 0.0), v)
             spread["calls"] = spread.get("calls", 0) + 1
-        worst = max(worst, vnorm_rel(got, ref) - (re if vl > 8000 else 0.0))
+        worst = max(worst, d["gpu_vs_avx"])
         if data_code is not None:
-            refd = volk.multicorrelator_real_codes(x, data_code, shifts[iP:iP + 1], rem_carr, carr_step, rem_code,
-                                                   code_step, vl)
-            worst = max(worst, vnorm_rel(g["data_prompt"][e].view(np.complex64), refd))
+            refd = volk.multicorrelator_real_codes_avx(x, data_code, shifts[iP:iP + 1], rem_carr, carr_step, rem_code,
+                                                       code_step, vl)
+            worst = max(worst, ccompare(g["data_prompt"][e].view(np.complex64), refd))
     return worst
 
 

@@ -481,6 +481,52 @@ int gsdr_acq_dump_grid(gsdr_acq* a, const void* iq_host, uint32_t prn_slot, floa
     return GSDR_OK;
 }
 
+int gsdr_acq_dump_grid_step_two(gsdr_acq* a, const void* iq_host, uint32_t prn_slot, float doppler_center_hz,
+    float* grid_host)
+{
+    GSDR_REQUIRE(a && iq_host && grid_host, GSDR_E_ARG, "gsdr_acq_dump_grid_step_two: null argument");
+    GSDR_REQUIRE(prn_slot < a->nprn, GSDR_E_ARG, "gsdr_acq_dump_grid_step_two: prn_slot %u >= nprn %u", prn_slot,
+        a->nprn);
+    GSDR_REQUIRE(a->st2.nbins > 0, GSDR_E_STATE, "gsdr_acq_dump_grid_step_two: gsdr_acq_set_step_two first");
+    GSDR_REQUIRE(a->st2.nbins <= a->D, GSDR_E_UNSUPPORTED,
+        "gsdr_acq_dump_grid_step_two: %u narrow bins exceed the grid buffer's %u rows", a->st2.nbins, a->D);
+    std::lock_guard<std::mutex> lk(a->mu);
+    gsdr::DeviceGuard g(a->device);
+    const uint32_t nb = a->st2.nbins;
+    // update_grid_doppler_wipeoffs_step2 (pcps_acquisition.cc:307-314), as gsdr_acq_run_step_two
+    const float half = (float)std::floor((double)nb / 2.0);
+    std::vector<float> freqs(nb);
+    for (uint32_t d = 0; d < nb; ++d)
+        {
+            volatile float dop = ((float)d - half) * a->st2.step;
+            freqs[d] = doppler_center_hz + dop;
+        }
+    GSDR_HIP(hipMemcpyAsync(a->d_iq, iq_host, (size_t)a->consumed * item_bytes(a->conf.item_type),
+        hipMemcpyHostToDevice, a->stream));
+    GSDR_HIP(hipMemcpyAsync(a->st2.d_freq, freqs.data(), nb * sizeof(float), hipMemcpyHostToDevice, a->stream));
+    hipLaunchKernelGGL(acq_wipeoff_kernel, dim3(nb), dim3(256), 0, a->stream, a->st2.d_wipe, a->N,
+        (float)a->conf.fs_in, 0, 0, 0, 0, (const float*)a->st2.d_freq);
+    GSDR_HIP(hipGetLastError());
+    // the grid dump on a one-PRN view with the narrow Doppler rows
+    const uint32_t D0 = a->D, P0 = a->nprn;
+    float2* const wipe0 = a->d_wipe;
+    float2* const code0 = a->d_code_fft;
+    a->D = nb;
+    a->nprn = 1;
+    a->d_wipe = a->st2.d_wipe;
+    a->d_code_fft = code0 + (size_t)prn_slot * a->N;
+    const int rc = dispatch(a, 3, nullptr, 1, 0, 0, nullptr, a->stream, 0);
+    a->D = D0;
+    a->nprn = P0;
+    a->d_wipe = wipe0;
+    a->d_code_fft = code0;
+    if (rc != GSDR_OK) return rc;
+    GSDR_HIP(hipMemcpyAsync(grid_host, a->d_grid, (size_t)nb * a->N * sizeof(float), hipMemcpyDeviceToHost,
+        a->stream));
+    GSDR_HIP(hipStreamSynchronize(a->stream));
+    return GSDR_OK;
+}
+
 int gsdr_acq_set_step_two(gsdr_acq* a, uint32_t num_doppler_bins_step2, float doppler_step2, float pfa2)
 {
     GSDR_REQUIRE(a, GSDR_E_ARG, "gsdr_acq_set_step_two: null handle");

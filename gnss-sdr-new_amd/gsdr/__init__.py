@@ -43,6 +43,7 @@ EXPORTED = [
     "gsdr_stream_create", "gsdr_stream_destroy", "gsdr_stream_push", "gsdr_stream_span", "gsdr_stream_window",
     "gsdr_acq_set_step_two", "gsdr_acq_get_step_two_threshold", "gsdr_acq_run_step_two",
     "gsdr_trk_set_data_code", "gsdr_acq_read_profile_ex", "gsdr_stream_window_async", "gsdr_stream_release", "gsdr_stream_device",
+    "gsdr_acq_dump_grid_step_two",
 ]
 
 SIGNAL_GPS_1C = 0
@@ -231,6 +232,7 @@ def load():
     L.gsdr_acq_run.argtypes = [P, P, U32, U64, P]
     L.gsdr_acq_run_device.argtypes = [P, P, U32, U64, U64, P, P]
     L.gsdr_acq_dump_grid.argtypes = [P, P, U32, P]
+    L.gsdr_acq_dump_grid_step_two.argtypes = [P, P, U32, ctypes.c_float, P]
     L.gsdr_acq_dump_spectra.argtypes = [P, P, P]
     L.gsdr_corr_create.argtypes = [I, I, I, I, P]
     L.gsdr_corr_destroy.argtypes = [P]
@@ -402,6 +404,7 @@ class Acquisition:
         pfa_second_step; pcps_acquisition.cc:298-314, :717-773)."""
         _check(load().gsdr_acq_set_step_two(self._h, int(num_doppler_bins_step2), float(doppler_step2),
                                             float(pfa2)))
+        self._st2_bins = int(num_doppler_bins_step2)
 
     @property
     def step_two_threshold(self):
@@ -452,6 +455,13 @@ class Acquisition:
         iq = self._items(iq)
         g = np.zeros((self.num_doppler_bins, self.fft_size), np.float32)
         _check(load().gsdr_acq_dump_grid(self._h, _ptr(iq), int(prn_slot), _ptr(g)))
+        return g
+
+    def dump_grid_step_two(self, iq, prn_slot, doppler_center_hz):
+        """The make_two_steps narrow grid of one block (set_step_two first)."""
+        iq = self._items(iq)
+        g = np.zeros((self._st2_bins, self.fft_size), np.float32)
+        _check(load().gsdr_acq_dump_grid_step_two(self._h, _ptr(iq), int(prn_slot), float(doppler_center_hz), _ptr(g)))
         return g
 
     def dump_spectra(self, iq):

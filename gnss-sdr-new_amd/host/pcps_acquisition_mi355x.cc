@@ -2,8 +2,11 @@
 
 #include <cmath>
 #include <cstring>
+#include <filesystem>
 #include <iostream>
 #include <stdexcept>
+
+#include "mat5_writer.h"
 
 pcps_acquisition_mi355x::pcps_acquisition_mi355x(const Acq_Conf& conf, int device)
     : d_acq_parameters(conf),
@@ -19,6 +22,30 @@ pcps_acquisition_mi355x::pcps_acquisition_mi355x(const Acq_Conf& conf, int devic
     if (conf.make_2_steps && conf.max_dwells > 1 && !conf.bit_transition_flag)
         throw std::invalid_argument("pcps_acquisition_mi355x: make_two_steps with max_dwells > 1 is not supported");
     d_data_buffer.resize(static_cast<size_t>(d_consumed_samples) * conf.it_size);
+    // dump file stem and directory (:135-165): basename without extension, default
+    // "acquisition", in the dump_filename's directory (created), else "."
+    d_dump = conf.dump;
+    if (d_dump)
+        {
+            std::string name = conf.dump_filename, dir = ".";
+            const auto slash = name.find_last_of('/');
+            if (slash != std::string::npos)
+                {
+                    dir = name.substr(0, slash);
+                    name = name.substr(slash + 1);
+                }
+            if (name.empty()) name = "acquisition";
+            if (name.size() > 1 && name.substr(1).find_last_of('.') != std::string::npos)
+                name = name.substr(0, name.find_last_of('.'));
+            std::error_code ec;
+            std::filesystem::create_directories(dir, ec);
+            if (ec)
+                {
+                    std::cerr << "GNSS-SDR cannot create dump file for the Acquisition block. Wrong permissions?\n";
+                    d_dump = false;
+                }
+            d_dump_filename = dir + "/" + name;
+        }
 }
 
 // Acq_Conf::item_type -> engine item type.  cbyte (lv_8sc_t, it_size 2) is what
@@ -33,7 +60,11 @@ int pcps_acquisition_mi355x::engine_item_type(const std::string& item_type)
     throw std::invalid_argument("Unknown item type: " + item_type);
 }
 
-pcps_acquisition_mi355x::~pcps_acquisition_mi355x() { gsdr_acq_destroy(d_engine); }
+pcps_acquisition_mi355x::~pcps_acquisition_mi355x()
+{
+    if (d_worker.joinable()) d_worker.join();
+    gsdr_acq_destroy(d_engine);
+}
 
 void pcps_acquisition_mi355x::ensure_engine()
 {
@@ -73,6 +104,13 @@ void pcps_acquisition_mi355x::ensure_engine()
     uint32_t D = 0, N = 0;
     gsdr_acq_get_dims(d_engine, &D, &N);
     d_num_doppler_bins = D;
+    d_eff = d_acq_parameters.bit_transition_flag ? N / 2 : N;
+    if (d_dump)
+        {
+            // init (:287-292): zeroed grids of the effective FFT size
+            d_grid.assign(static_cast<size_t>(d_eff) * D, 0.0F);
+            d_narrow_grid.assign(static_cast<size_t>(d_eff) * d_acq_parameters.num_doppler_bins_step2, 0.0F);
+        }
     if (d_code_set)
         {
             const uint32_t prn = d_gnss_synchro ? d_gnss_synchro->PRN : 0;
@@ -201,6 +239,10 @@ void pcps_acquisition_mi355x::send_negative_acquisition()
 // (:831-869); make_two_steps searches the narrow grid (:717-773).
 void pcps_acquisition_mi355x::acquisition_core(uint64_t samp_count)
 {
+    // (:617) the core holds d_setlock; a blocking block releases it for the grid
+    // (:655-658), the worker of a non-blocking one keeps it to the end
+    std::unique_lock<std::mutex> lk(d_setlock);
+    if (d_acq_parameters.blocking) lk.unlock();
     d_mag = 0.0F;
     d_num_noncoherent_integrations_counter++;
     // the engine keeps the first-step threshold (calculate_threshold reads it back
@@ -230,9 +272,11 @@ void pcps_acquisition_mi355x::acquisition_core(uint64_t samp_count)
             d_state = 0;
             d_active = false;
             d_num_noncoherent_integrations_counter = 0;
+            d_worker_active = false;
             send_negative_acquisition();
             return;
         }
+    if (d_dump && d_channel == d_acq_parameters.dump_channel) dump_grid_dwell();
     d_mag = r.peak;
     // CFAR input power (:534) -- kept from the coarse step during step two (:531)
     if (!d_step_two) d_input_power = r.input_power;
@@ -337,22 +381,108 @@ void pcps_acquisition_mi355x::acquisition_core(uint64_t samp_count)
                     send_negative_acquisition();
                 }
         }
+    d_worker_active = false;
     if (d_num_noncoherent_integrations_counter == d_acq_parameters.max_dwells || d_positive_acq == 1 ||
         d_acq_parameters.bit_transition_flag)
         {
+            // record results to file if required (:873-877)
+            if (d_dump && d_channel == d_acq_parameters.dump_channel) dump_results();
             d_num_noncoherent_integrations_counter = 0U;
             d_positive_acq = 0;
         }
+}
+
+// The magnitude grid of this dwell for the dump channel (:680-685, :741-746): the
+// engine recomputes the block's |R|^2 grid (gsdr_acq_dump_grid, the narrow one in
+// step two), whose effective window (outputs [N - eff, N), :671) is stored -- on the
+// first dwell of the attempt -- or added in float (volk_32f_x2_add_32f, :673-675).
+void pcps_acquisition_mi355x::dump_grid_dwell()
+{
+    uint32_t D = 0, N = 0;
+    gsdr_acq_get_dims(d_engine, &D, &N);
+    const bool two = d_step_two;
+    const uint32_t rows = two ? d_acq_parameters.num_doppler_bins_step2 : D;
+    d_grid_tmp.resize(static_cast<size_t>(rows) * N);
+    const int rc = two ? gsdr_acq_dump_grid_step_two(d_engine, d_data_buffer.data(), 0, d_doppler_center_step_two,
+                             d_grid_tmp.data())
+                       : gsdr_acq_dump_grid(d_engine, d_data_buffer.data(), 0, d_grid_tmp.data());
+    if (rc != GSDR_OK)
+        {
+            std::cerr << "pcps_acquisition_mi355x: dump grid: " << gsdr_last_error() << '\n';
+            return;
+        }
+    std::vector<float>& g = two ? d_narrow_grid : d_grid;
+    g.resize(static_cast<size_t>(d_eff) * rows);
+    const uint32_t off = N - d_eff;
+    const bool first = d_num_noncoherent_integrations_counter == 1;
+    for (uint32_t d = 0; d < rows; ++d)
+        for (uint32_t i = 0; i < d_eff; ++i)
+            {
+                const float v = d_grid_tmp[static_cast<size_t>(d) * N + off + i];
+                float& o = g[static_cast<size_t>(d) * d_eff + i];
+                o = first ? v : o + v;
+            }
+}
+
+// dump_results (:408-508): <dump_filename>_<System>_<Signal>_ch_<channel>_<n>_sat_<PRN>.mat
+// with the reference's variables (names, classes, dimensions); Level-5 MAT-file
+// (mat5_writer.h) instead of matio's MAT 7.3.
+void pcps_acquisition_mi355x::dump_results()
+{
+    if (!d_gnss_synchro) return;
+    d_dump_number++;
+    std::string fn = d_dump_filename + "_";
+    fn.append(1, d_gnss_synchro->System);
+    fn += "_";
+    fn.append(1, d_gnss_synchro->Signal[0]);
+    fn.append(1, d_gnss_synchro->Signal[1]);
+    fn += "_ch_" + std::to_string(d_channel) + "_" + std::to_string(d_dump_number) + "_sat_" +
+          std::to_string(d_gnss_synchro->PRN) + ".mat";
+    Mat5Writer m;
+    if (!m.open(fn))
+        {
+            std::cout << "Unable to create or open Acquisition dump file\n";
+            return;
+        }
+    m.write("acq_grid", Mat5Writer::kSingle, d_eff, d_num_doppler_bins, d_grid.data());
+    m.write_int32("doppler_max", d_acq_parameters.doppler_max);
+    m.write_int32("doppler_step", static_cast<int32_t>(d_doppler_step));
+    m.write_int32("d_positive_acq", d_positive_acq);
+    m.write_single("acq_doppler_hz", static_cast<float>(d_gnss_synchro->Acq_doppler_hz));
+    m.write_single("acq_delay_samples", static_cast<float>(d_gnss_synchro->Acq_delay_samples));
+    m.write_single("test_statistic", d_test_statistics);
+    m.write_single("threshold", d_threshold);
+    m.write_single("input_power", d_input_power);
+    m.write_uint64("sample_counter", d_sample_counter);
+    m.write_uint32("PRN", d_gnss_synchro->PRN);
+    m.write_int32("num_dwells", static_cast<int32_t>(d_num_noncoherent_integrations_counter));
+    if (d_acq_parameters.make_2_steps)
+        {
+            m.write("acq_grid_narrow", Mat5Writer::kSingle, d_eff, d_acq_parameters.num_doppler_bins_step2,
+                d_narrow_grid.data());
+            m.write_single("doppler_step_narrow", d_acq_parameters.doppler_step2);
+            m.write_single("doppler_grid_narrow_min",
+                d_doppler_center_step_two -
+                    static_cast<float>(std::floor(d_acq_parameters.num_doppler_bins_step2 / 2.0)) *
+                        d_acq_parameters.doppler_step2);
+        }
+    if (!m.close())
+        std::cout << "Unable to create or open Acquisition dump file\n";
+    else
+        d_last_dump = fn;
 }
 
 // general_work (:912-1050) with blocking acquisition.
 int pcps_acquisition_mi355x::work(const void* in, int ninput_items)
 {
     std::unique_lock<std::mutex> lk(d_setlock);
-    if (!d_active)
+    if (!d_active || d_worker_active)
         {
+            // do not consume samples while performing a non-coherent integration (:928-936)
+            const bool consume_samples =
+                !d_active || d_num_noncoherent_integrations_counter == d_acq_parameters.max_dwells;
             int consumed = 0;
-            if (!d_acq_parameters.blocking_on_standby)
+            if (!d_acq_parameters.blocking_on_standby && consume_samples)
                 {
                     d_sample_counter += static_cast<uint64_t>(ninput_items);
                     consumed = ninput_items;
@@ -402,8 +532,19 @@ int pcps_acquisition_mi355x::work(const void* in, int ninput_items)
             }
         case 2:
             {
-                lk.unlock();
-                acquisition_core(d_sample_counter);
+                // :1013-1029: the core inline (blocking) or on a worker thread
+                if (d_acq_parameters.blocking)
+                    {
+                        lk.unlock();
+                        acquisition_core(d_sample_counter);
+                    }
+                else
+                    {
+                        if (d_worker.joinable()) d_worker.join();  // the previous core ended (d_worker_active false)
+                        d_worker_active = true;
+                        ++d_async_cores;
+                        d_worker = std::thread(&pcps_acquisition_mi355x::acquisition_core, this, d_sample_counter);
+                    }
                 d_buffer_count = 0U;
                 return 0;
             }

@@ -13,6 +13,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "acq_conf.h"
@@ -60,9 +61,17 @@ public:
 
     uint32_t num_noncoherent_integrations() const { return d_num_noncoherent_integrations_counter; }
     static int engine_item_type(const std::string& item_type);
+    // blocking = false: acquisition_core calls run on a worker thread (and how many did)
+    uint64_t async_cores() const { return d_async_cores; }
+    bool worker_active() const { return d_worker_active; }
+    // dump = true: the dump files written so far (dump_results), and the last one's path
+    int64_t dump_number() const { return d_dump_number; }
+    const std::string& last_dump_path() const { return d_last_dump; }
 
 private:
     void acquisition_core(uint64_t samp_count);
+    void dump_grid_dwell();
+    void dump_results();
     void ensure_engine();
     void send_positive_acquisition();
     void send_negative_acquisition();
@@ -97,6 +106,19 @@ private:
     bool d_step_two{false};                // make_2_steps: the next core call is the narrow grid
     float d_doppler_center_step_two{0.0F};
     bool d_step_repeat{false};  // fork's make_repeat_steps: keep re-acquiring after a positive
+    // blocking = false (:1013-1029): the core on a worker thread that holds d_setlock
+    std::thread d_worker;
+    bool d_worker_active{false};
+    uint64_t d_async_cores{0};
+    // dump (:135-165, :408-508): the magnitude grids of the attempt for the dump channel
+    bool d_dump{false};
+    std::string d_dump_filename;
+    std::string d_last_dump;
+    int64_t d_dump_number{0};
+    uint32_t d_eff{0};                 // effective_fft_size
+    std::vector<float> d_grid;         // eff x D, column-major (arma::fmat d_grid)
+    std::vector<float> d_narrow_grid;  // eff x num_doppler_bins_step2
+    std::vector<float> d_grid_tmp;
     std::mutex d_setlock;
 };
 

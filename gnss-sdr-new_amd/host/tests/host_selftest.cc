@@ -21,7 +21,9 @@
 //  8. The gflags overrides (--pll_bw_hz, --dll_bw_hz, --doppler_max) and defaults.
 // Usage: host_selftest <GPS_L1_CA_ID_1_Fs_4Msps_2ms.dat> [Galileo_E1_ID_1_Fs_4Msps_8ms.dat]
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <cstdlib>
 #include <cmath>
 #include <complex>
 #include <cstring>
@@ -153,6 +155,141 @@ void test_acquisition_validation(const std::vector<std::complex<float>>& capture
     std::printf("acquisition: message %d delay %.1f samples doppler %.0f Hz stat %.3f stamp %llu\n", rx_message,
         gnss_synchro.Acq_delay_samples, gnss_synchro.Acq_doppler_hz, acquisition.get_block()->test_statistics(),
         static_cast<unsigned long long>(gnss_synchro.Acq_samplestamp_samples));
+}
+
+// Acquisition_1C.blocking = false (pcps_acquisition.cc:1013-1029): the core runs on
+// a worker thread; general_work calls during it consume nothing (single dwell,
+// :928-936) and the answer equals the blocking block's.
+void test_acquisition_nonblocking(const std::vector<std::complex<float>>& capture)
+{
+    Gnss_Synchro res[2]{};
+    uint64_t cores = 0;
+    for (int blocking = 1; blocking >= 0; --blocking)
+        {
+            InMemoryConfiguration config;
+            config.set_property("GNSS-SDR.internal_fs_sps", "4000000");
+            config.set_property("Acquisition_1C.implementation", "GPS_L1_CA_PCPS_Acquisition_MI355X");
+            config.set_property("Acquisition_1C.item_type", "gr_complex");
+            config.set_property("Acquisition_1C.coherent_integration_time_ms", "1");
+            config.set_property("Acquisition_1C.doppler_max", "5000");
+            config.set_property("Acquisition_1C.doppler_step", "100");
+            config.set_property("Acquisition_1C.blocking", blocking ? "true" : "false");
+            Gnss_Synchro& gs = res[blocking];
+            gs.System = 'G';
+            gs.Signal[0] = '1';
+            gs.Signal[1] = 'C';
+            gs.PRN = 1;
+            GpsL1CaPcpsAcquisitionMI355X acquisition(&config, "Acquisition_1C", 1, 0);
+            std::atomic<int> rx_message{0};
+            acquisition.get_block()->set_event_handler([&](int ev) { rx_message = ev; });
+            acquisition.set_gnss_synchro(&gs);
+            acquisition.set_threshold(0.001);
+            acquisition.set_local_code();
+            acquisition.set_state(1);
+            acquisition.init();
+            acquisition.get_block()->start();
+            size_t pos = 0;
+            int guard = 0;
+            while (rx_message == 0 && guard++ < 10000)
+                {
+                    const int n = static_cast<int>(std::min<size_t>(1024, capture.size() - pos));
+                    pos += static_cast<size_t>(acquisition.get_block()->work(capture.data() + pos, n));
+                }
+            EXPECT(rx_message == 1, "blocking=" << blocking << ": positive acquisition");
+            if (!blocking) cores = acquisition.get_block()->async_cores();
+        }
+    EXPECT(cores >= 1, "blocking=false: the core ran on the worker thread");
+    EXPECT(res[0].Acq_delay_samples == res[1].Acq_delay_samples && res[0].Acq_doppler_hz == res[1].Acq_doppler_hz &&
+               res[0].Acq_samplestamp_samples == res[1].Acq_samplestamp_samples,
+        "blocking=false: same Gnss_Synchro as blocking");
+    std::printf("non-blocking acquisition: %llu worker cores, delay %.1f doppler %.0f stamp %llu\n",
+        static_cast<unsigned long long>(cores), res[0].Acq_delay_samples, res[0].Acq_doppler_hz,
+        static_cast<unsigned long long>(res[0].Acq_samplestamp_samples));
+}
+
+// Acquisition_1C.dump (pcps_acquisition.cc:135-165, :408-508): the dump channel's
+// grid and fields per decided attempt as a .mat file -- a single-step attempt on
+// channel 1 (dump_channel 1) and a make_two_steps attempt (with the narrow grid).
+// tests/test_host_mirror.py checks the files' grids against the oracle.
+void test_acquisition_dump(const std::vector<std::complex<float>>& capture, const std::string& dir)
+{
+    for (int two = 0; two <= 1; ++two)
+        {
+            InMemoryConfiguration config;
+            config.set_property("GNSS-SDR.internal_fs_sps", "4000000");
+            config.set_property("Acquisition_1C.implementation", "GPS_L1_CA_PCPS_Acquisition_MI355X");
+            config.set_property("Acquisition_1C.item_type", "gr_complex");
+            config.set_property("Acquisition_1C.coherent_integration_time_ms", "1");
+            config.set_property("Acquisition_1C.pfa", "0.01");
+            config.set_property("Acquisition_1C.doppler_max", "5000");
+            config.set_property("Acquisition_1C.doppler_step", two ? "500" : "100");
+            config.set_property("Acquisition_1C.dump", "true");
+            config.set_property("Acquisition_1C.dump_filename", dir + (two ? "/acq_two.dat" : "/acq_one.dat"));
+            config.set_property("Acquisition_1C.dump_channel", "1");
+            if (two)
+                {
+                    config.set_property("Acquisition_1C.make_two_steps", "true");
+                    config.set_property("Acquisition_1C.second_nbins", "5");
+                    config.set_property("Acquisition_1C.second_doppler_step", "100");
+                    config.set_property("Acquisition_1C.blocking_on_standby", "true");
+                }
+            Gnss_Synchro gs{};
+            gs.System = 'G';
+            gs.Signal[0] = '1';
+            gs.Signal[1] = 'C';
+            gs.PRN = 1;
+            GpsL1CaPcpsAcquisitionMI355X acquisition(&config, "Acquisition_1C", 1, 0);
+            int rx_message = 0;
+            acquisition.get_block()->set_event_handler([&](int ev) { rx_message = ev; });
+            acquisition.set_channel(1);
+            acquisition.set_gnss_synchro(&gs);
+            acquisition.set_local_code();
+            acquisition.set_state(1);
+            acquisition.init();
+            acquisition.get_block()->start();
+            size_t pos = 0;
+            int guard = 0;
+            while (rx_message == 0 && guard++ < 200)
+                {
+                    const int n = static_cast<int>(std::min<size_t>(1000, capture.size() - pos));
+                    pos += static_cast<size_t>(acquisition.get_block()->work(capture.data() + pos, n));
+                }
+            EXPECT(rx_message == 1, "dump " << (two ? "two-step" : "single-step") << ": positive acquisition");
+            const std::string want = dir + (two ? "/acq_two" : "/acq_one") + "_G_1C_ch_1_1_sat_1.mat";
+            EXPECT(acquisition.get_block()->dump_number() == 1 && acquisition.get_block()->last_dump_path() == want,
+                "dump file " << want << " (got " << acquisition.get_block()->last_dump_path() << ")");
+            EXPECT(std::filesystem::exists(want), "dump file exists: " << want);
+            std::printf("acquisition dump: %s (delay %.1f doppler %.0f)\n", want.c_str(), gs.Acq_delay_samples,
+                gs.Acq_doppler_hz);
+        }
+    // a channel other than dump_channel writes nothing
+    InMemoryConfiguration config;
+    config.set_property("GNSS-SDR.internal_fs_sps", "4000000");
+    config.set_property("Acquisition_1C.implementation", "GPS_L1_CA_PCPS_Acquisition_MI355X");
+    config.set_property("Acquisition_1C.pfa", "0.01");
+    config.set_property("Acquisition_1C.dump", "true");
+    config.set_property("Acquisition_1C.dump_filename", dir + "/acq_other.dat");
+    config.set_property("Acquisition_1C.dump_channel", "1");
+    Gnss_Synchro gs{};
+    gs.System = 'G';
+    gs.Signal[0] = '1';
+    gs.Signal[1] = 'C';
+    gs.PRN = 1;
+    GpsL1CaPcpsAcquisitionMI355X acquisition(&config, "Acquisition_1C", 1, 0);
+    int rx_message = 0;
+    acquisition.get_block()->set_event_handler([&](int ev) { rx_message = ev; });
+    acquisition.set_channel(2);
+    acquisition.set_gnss_synchro(&gs);
+    acquisition.set_local_code();
+    acquisition.set_state(1);
+    acquisition.init();
+    acquisition.get_block()->start();
+    size_t pos = 0;
+    int guard = 0;
+    while (rx_message == 0 && guard++ < 200)
+        pos += static_cast<size_t>(acquisition.get_block()->work(capture.data() + pos,
+            static_cast<int>(std::min<size_t>(1000, capture.size() - pos))));
+    EXPECT(acquisition.get_block()->dump_number() == 0, "no dump for a channel other than dump_channel");
 }
 
 // make_two_steps on the same capture: coarse 500 Hz grid on the first millisecond,
@@ -1252,6 +1389,11 @@ int main(int argc, char** argv)
             return 2;
         }
     test_acquisition_validation(capture);
+    test_acquisition_nonblocking(capture);
+    {
+        const char* d = std::getenv("GSDR_SELFTEST_DUMP_DIR");
+        test_acquisition_dump(capture, d ? std::string(d) : std::string("/tmp/gsdr_selftest_dump"));
+    }
     test_acquisition_two_steps(capture);
     test_acquisition_repeat_steps(capture);
     test_acquisition_service(capture);

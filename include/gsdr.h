@@ -225,6 +225,15 @@ int gsdr_acq_run_stream(gsdr_acq* acq, gsdr_stream* stream, uint64_t first_sampl
  * |R|^2 grid of PRN slot `prn_slot` for one host block into grid_host
  * (D rows of fft_size floats, Doppler-major).  Synchronous. */
 int gsdr_acq_dump_grid(gsdr_acq* acq, const void* iq_host, uint32_t prn_slot, float* grid_host);
+/* The narrow grid of make_two_steps for the same dump (d_narrow_grid,
+ * pcps_acquisition.cc:743-746, written by dump_results :493-506): the |R|^2 grid of
+ * PRN slot prn_slot over the num_doppler_bins_step2 rows centred on
+ * doppler_center_hz (update_grid_doppler_wipeoffs_step2, :307-314) for one host
+ * block, into grid_host (num_doppler_bins_step2 rows of fft_size floats).  Needs
+ * gsdr_acq_set_step_two and num_doppler_bins_step2 <= the handle's Doppler bins.
+ * Synchronous. */
+int gsdr_acq_dump_grid_step_two(gsdr_acq* acq, const void* iq_host, uint32_t prn_slot, float doppler_center_hz,
+    float* grid_host);
 
 /* make_two_steps (pcps_acquisition.cc:298-314, :717-773, :781-800, :894-909;
  * Acq_Conf second_nbins / second_doppler_step / pfa_second_step, acq_conf.cc:63-76).

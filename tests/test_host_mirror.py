@@ -61,14 +61,66 @@ def test_cpp_replica_and_acq_conf_match_oracle(tmp_path):
     assert f[4] == "10000" and f[5] == "1" and f[6] == "8"
 
 
+def test_mat5_writer_reads_back(tmp_path):
+    """The acquisition dump's Level-5 MAT-file writer (host/mat5_writer.cc): names,
+    classes, dimensions and column-major data as scipy.io.loadmat reads them."""
+    sio = pytest.importorskip("scipy.io")
+    exe = os.path.join(BUILD, "mat5_probe")
+    if not os.path.exists(exe):
+        subprocess.check_call(["make", "-C", HOST, exe])
+    path = tmp_path / "probe.mat"
+    subprocess.check_call([exe, str(path)])
+    m = sio.loadmat(str(path))
+    g = m["acq_grid"]
+    assert g.dtype == np.float32 and g.shape == (5, 3)
+    np.testing.assert_array_equal(g, np.arange(5)[:, None] + 0.25 * np.arange(3)[None, :])
+    assert m["doppler_max"].dtype == np.int32 and int(m["doppler_max"][0, 0]) == -5000
+    assert m["test_statistic"].dtype == np.float32 and float(m["test_statistic"][0, 0]) == 3.5
+    assert m["PRN"].dtype == np.uint32 and int(m["PRN"][0, 0]) == 17
+    assert m["sample_counter"].dtype == np.uint64 and int(m["sample_counter"][0, 0]) == 123456789012345
+
+
 @pytest.mark.gpu
-def test_host_selftest_on_gpu():
+def test_host_selftest_on_gpu(tmp_path):
     exe = os.path.join(BUILD, "host_selftest")
     if not os.path.exists(exe):
         subprocess.check_call(["make", "-C", HOST])
     cap = os.path.join(ROOT, "tests", "golden", "GPS_L1_CA_ID_1_Fs_4Msps_2ms.dat")
     gal = os.path.join(ROOT, "tests", "golden", "Galileo_E1_ID_1_Fs_4Msps_8ms.dat")
-    r = subprocess.run([exe, cap, gal], capture_output=True, text=True, timeout=120)
+    env = dict(os.environ, GSDR_SELFTEST_DUMP_DIR=str(tmp_path))
+    r = subprocess.run([exe, cap, gal], capture_output=True, text=True, timeout=120, env=env)
     print(r.stdout, r.stderr)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "host_selftest: PASS" in r.stdout
+    _check_acq_dumps(tmp_path, cap)
+
+
+def _check_acq_dumps(d, cap_path):
+    """The acquisition dump files the self-test wrote (dump_results,
+    pcps_acquisition.cc:408-508) against the oracle grid of the same block."""
+    sio = pytest.importorskip("scipy.io")
+    from oracle import pcps
+    x = np.fromfile(cap_path, np.complex64)
+    fs, N = 4000000, 4000
+    code = replica.gps_l1_ca_code_complex_sampled(1, fs)
+    cf = pcps.fft_code(code, N, N)
+    # single step: +-5 kHz / 100 Hz on the first millisecond
+    m = sio.loadmat(str(d / "acq_one_G_1C_ch_1_1_sat_1.mat"))
+    M = pcps.magnitude_grid(x[:N], pcps.doppler_wipeoffs(fs, N, 5000, 100, 100), cf)  # D x N
+    g = m["acq_grid"]
+    assert g.shape == (N, 100) and g.dtype == np.float32
+    assert np.max(np.abs(g.T - M)) <= 1e-4 * M.max()
+    ti, di, gmax, ip, stat = pcps.max_to_input_power_statistic(M)
+    assert abs(float(m["test_statistic"][0, 0]) - stat) <= 1e-4 * stat
+    assert int(m["PRN"][0, 0]) == 1 and int(m["num_dwells"][0, 0]) == 1 and int(m["d_positive_acq"][0, 0]) == 1
+    assert int(m["doppler_max"][0, 0]) == 5000 and int(m["doppler_step"][0, 0]) == 100
+    assert int(m["sample_counter"][0, 0]) == N
+    assert abs(float(m["acq_delay_samples"][0, 0]) - 524) * 1023 / fs < 0.5
+    # two steps: the narrow 5 x 100 Hz grid around the coarse Doppler on the second millisecond
+    m = sio.loadmat(str(d / "acq_two_G_1C_ch_1_1_sat_1.mat"))
+    assert m["acq_grid"].shape == (N, 20) and m["acq_grid_narrow"].shape == (N, 5)
+    step2, lo = float(m["doppler_step_narrow"][0, 0]), float(m["doppler_grid_narrow_min"][0, 0])
+    assert step2 == 100.0
+    center = lo + 2 * step2
+    Mn = pcps.magnitude_grid(x[N:2 * N], pcps.doppler_wipeoffs_step2(fs, N, center, step2, 5), cf)
+    assert np.max(np.abs(m["acq_grid_narrow"].T - Mn)) <= 1e-4 * Mn.max()

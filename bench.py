@@ -264,12 +264,21 @@ def cpu_baseline(iq, codes, sats, budget_s=12.0):
     corr_rate = reps * N / (time.perf_counter() - tc) / 1e6
     value = nblk * N / dt / 1e6
     socket_cores = info.get("cores_per_socket") or nt
+    # whole-socket estimate from the measured scaling curve (Amdahl's law fitted to
+    # thread_scaling_msps: speedup(n) = 1 / (s + (1 - s) / n), s the median of the
+    # per-point serial fractions), not a linear extrapolation
+    r1 = scaling.get(1)
+    fits = [((n / (r / r1)) - 1.0) / (n - 1.0) for n, r in scaling.items() if n > 1 and r1 and r > 0]
+    serial = float(np.clip(np.median(fits), 0.0, 1.0)) if fits else 0.0
+    socket_est = r1 / (serial + (1.0 - serial) / socket_cores) if r1 else value * socket_cores / nt
     return {"value": round(value, 4), "unit": "Msamples/s", "cores": nt, "kind": "port",
             "thread_scaling_msps": scaling,
-            "full_socket_estimate": {"value": round(value * socket_cores / nt, 3), "cores": socket_cores,
-                                     "basis": "the measured rate per thread x the socket's cores (linear; the job's "
-                                              "CPU share is %d threads, thread_scaling_msps shows the scaling inside "
-                                              "it); an estimate, not a measurement" % nt},
+            "full_socket_estimate": {"value": round(socket_est, 3), "cores": socket_cores,
+                                     "serial_fraction": round(serial, 4),
+                                     "linear_upper_bound": round(value * socket_cores / nt, 3),
+                                     "basis": "Amdahl's law fitted to thread_scaling_msps (the job's CPU share is %d "
+                                              "threads; the box's OMP/MAX_JOBS limit), evaluated at the socket's "
+                                              "cores; an estimate, not a measurement" % nt},
             "sample": "%d blocks of 1 ms (4000 samples) in %.1f s: 32 PRN x 81 Doppler CFAR PCPS per block "
                       "(oracle/cpu_baseline.cc: own 8-lane AVX2 mixed-radix FFT, no FFTW3f/pocketfft on the image) "
                       "+ one dll_pll_veml_tracking call for each of 8 channels (fused AVX2 correlator + DLL/PLL "
@@ -325,10 +334,17 @@ def run_c5(args):
     blocks; rank r runs the acquisition of its block span (c5_rank_plan: GPS L1 C/A
     and BeiDou B1I 32 PRN x 81 Doppler grids, N = 25000, on alternate milliseconds,
     one Galileo E1 36 PRN x 41 Doppler 4 ms grid, N = 100000, per 4 ms group) and
-    re-tracks its channels of the 256 (three signal pools, device-resident
-    dll_pll_veml_tracking) over the whole span from their saved start states.
-    Inputs resident in HBM; value = world x B x 25000 samples per step / max-over-
-    ranks time (weak scaling)."""
+    tracks its channels of the 256 (three signal pools, device-resident
+    dll_pll_veml_tracking).  Tracking (default, as C2's --trk-stream) follows one
+    continuous stream: the span is periodic (B = 100 ms: Galileo's 100 ms secondary
+    code, carriers on whole cycles per span) and repeated end to end, one launch per
+    pool covering all timed steps, so every channel is in steady state and even the
+    4 ms Galileo channels make tens of calls per timed region; --trk-replay re-tracks
+    the span from saved start states every step (B = 8 ms).  Inputs resident in HBM;
+    value = world x B x 25000 samples per step / max-over-ranks time (weak scaling).
+    Also reported: per-pool and acquisition-alone rates, the roofline of both stages,
+    and the H2D ingest time of the rank's stream span (pinned host memory), which is
+    never part of value."""
     import torch
     import gsdr
     from gsdr import synth
@@ -342,26 +358,40 @@ def run_c5(args):
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
-    B = args.blocks if args.blocks % 4 == 0 and args.blocks != 64 else 8
+    stream = not args.trk_replay
+    B = args.blocks if args.blocks % 4 == 0 and args.blocks != 64 else (100 if stream else 8)
     W, K = args.warmup, args.steps
     plan = c5_rank_plan(world, rank, B)
     total = plan["total_blocks"]
     lo, hi = plan["blocks"]
     fs, n = C5_FS, C5_N
-    # the stream: 12 GPS + 12 Galileo + 8 BeiDou satellites at 45 dB-Hz, + one
-    # Galileo code period of slack for the last tracking calls
+    # the stream: 12 GPS + 12 Galileo + 8 BeiDou satellites at 45 dB-Hz
     rng = np.random.default_rng(500)
     gps = synth.random_constellation(12, seed_offset=500, cn0_dbhz=45.0, prns=list(range(1, 13)), max_doppler=4000.0)
     gal = [synth.GalileoSatellite(p, float(rng.uniform(-4000, 4000)), float(rng.uniform(0, 4092)), 45.0,
                                   float(rng.uniform(0, 6.28))) for p in range(1, 13)]
     bds = [synth.Satellite(p, float(rng.uniform(-4000, 4000)), float(rng.uniform(0, 2046)), 45.0,
                            float(rng.uniform(0, 6.28))) for p in (6, 7, 8, 9, 10, 11, 12, 13)]
-    ns = total * n + 4 * n
+    if stream:
+        # a whole number of carrier cycles per span: the span repeated end to end is a
+        # continuous signal (no code Doppler; codes, secondary codes and data bits
+        # are periodic in whole milliseconds of the span)
+        span = total * n / fs
+        for s in gps + gal + bds:
+            s.doppler_hz = round(s.doppler_hz * span) / span
+        ns = total * n
+    else:
+        ns = total * n + 4 * n  # + one Galileo code period of slack for the last calls
     iq = (synth.gps_l1_iq(fs, ns, gps, seed_offset=500, noise=False, dtype=np.complex128) +
           synth.gal_e1_iq(fs, ns, gal, seed_offset=500, noise=False, dtype=np.complex128) +
           synth.bds_b1i_iq(fs, ns, bds, seed_offset=500, noise=True, dtype=np.complex128)).astype(np.complex64)
     iq_dev = torch.from_numpy(iq.view(np.float32).copy()).to(dev)
     base = iq_dev.data_ptr()
+    if stream:
+        iq_long = iq_dev.repeat(W + K + 1)  # warmup + timed steps end to end, + one span of slack
+        tbase, t_items = iq_long.data_ptr(), (W + K + 1) * ns
+    else:
+        iq_long, tbase, t_items = iq_dev, base, ns
     # acquisition handles of this rank's span
     acq_specs = (
         ("gps", n, 32, 10000, 250, 1, lambda: np.stack([synth.gps_ca_sampled(p, fs) for p in range(1, 33)]),
@@ -396,8 +426,10 @@ def run_c5(args):
             c["track_pilot"] = 1
         t = gsdr.Tracking(c, device=local)
         chip, per = ((1.023e6, n), (1.023e6, 4 * n), (2.046e6, n))[sig]
+        truth = []
         for i, gc in enumerate(chans):
             s = sats_of[sig][c5_channel_signal(gc)[1]]
+            truth.append(s.doppler_hz)
             tau = s.code_delay_chips / (chip * (1 + s.doppler_hz / 1.57542e9)) * fs
             dop = 250.0 * round(s.doppler_hz / 250.0)
             if sig == 0:
@@ -408,25 +440,39 @@ def run_c5(args):
             else:
                 t.start(i, s.prn, synth.bds_b1i_chips(s.prn), float(round(tau) % per), dop, 0, 0)
         t.save_state(0)
-        epochs = total * n // per + 1
+        per_step = total * n // per  # general_work calls per channel per step
+        epochs = (max(W, K) * per_step) if stream else per_step + 1
         out = torch.zeros(len(chans) * epochs * gsdr.TRK_EPOCH_DTYPE.itemsize, dtype=torch.uint8, device=dev)
         cnt = torch.zeros(len(chans), dtype=torch.int32, device=dev)
-        pools.append((sig, t, epochs, out, cnt, len(chans)))
-    n_items = len(iq)
+        pools.append(dict(sig=sig, t=t, per=per, per_step=per_step, epochs=epochs, out=out, cnt=cnt,
+                          nch=len(chans), truth=np.array(truth)))
 
-    def step():
-        for sig, t, epochs, out, cnt, _ in pools:
-            t.restore_state(0)
-            t.run_device(base, 0, n_items, epochs, out.data_ptr(), cnt.data_ptr())
+    def trk_launch(nsteps):
+        # stream mode: one launch per pool for nsteps spans, continuing the stream
+        for pl in pools:
+            pl["t"].run_device(tbase, 0, t_items, nsteps * pl["per_step"], pl["out"].data_ptr(), pl["cnt"].data_ptr())
+
+    def acq_step():
         for name, a, b0, nb, stride, res, P5, N5 in acqs:
             a.run_device(base + b0 * n * 8, nb, stride, b0 * n, res.data_ptr())
 
+    def step():
+        if not stream:
+            for pl in pools:
+                pl["t"].restore_state(0)
+                pl["t"].run_device(base, 0, ns, pl["epochs"], pl["out"].data_ptr(), pl["cnt"].data_ptr())
+        acq_step()
+
+    if stream:
+        trk_launch(W)
     for _ in range(W):
         step()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    if stream:
+        trk_launch(K)
     for _ in range(K):
         step()
     torch.cuda.synchronize(dev)
@@ -438,19 +484,67 @@ def run_c5(args):
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     # sanity on the timed region's outputs: acquisitions of the visible satellites,
-    # tracking records per channel
+    # tracking records per channel, carrier Doppler of the last 16 calls vs the truth
     det = {}
     for name, a, b0, nb, stride, res, P5, N5 in acqs:
         r = res.cpu().numpy().view(gsdr.ACQ_RESULT_DTYPE).reshape(nb, P5)
         det[name] = sorted({int(x["prn"]) for x in r[0] if x["positive"]})
-    calls = {("gps", "gal", "bds")[sig]: int(cnt.cpu().numpy().min()) for sig, _, _, _, cnt, _ in pools}
-    import math
+    names = ("gps", "gal", "bds")
+    calls, conv = {}, {}
+    for pl in pools:
+        cnt = pl["cnt"].cpu().numpy()
+        calls[names[pl["sig"]]] = int(cnt.min())
+        recs = pl["out"].cpu().numpy().view(gsdr.TRK_EPOCH_DTYPE).reshape(pl["nch"], pl["epochs"])
+        err = [abs(float(np.mean(recs[i][max(cnt[i] - 16, 0):cnt[i]]["carrier_doppler_hz"])) - pl["truth"][i])
+               for i in range(pl["nch"]) if cnt[i] > 0]
+        conv[names[pl["sig"]]] = {"median_mean16_doppler_err_hz": round(float(np.median(err)), 2) if err else None,
+                                  "channels_within_25hz": int(np.sum(np.array(err) < 25.0)), "channels": pl["nch"]}
     flops = 0.0
     for name, a, b0, nb, stride, res, P5, N5 in acqs:
         Dn = a.num_doppler_bins
         flops += nb * (Dn * (5 * N5 * math.log2(N5) + 6 * N5) + P5 * Dn * (5 * N5 * math.log2(N5) + 11 * N5))
     samples = world * K * B * n
     value = samples / elapsed / 1e6
+
+    def timed_part(fn):
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize(dev)
+        return time.perf_counter() - t1
+
+    # components after the timed region: acquisition alone over K steps, each pool alone
+    # over K spans (from its saved start state), the H2D ingest of the rank's span
+    comp = {}
+    ta = timed_part(lambda: [acq_step() for _ in range(K)])
+    comp["acq_only_msps"] = round(B * n * K / ta / 1e6, 2)
+    trk_bytes, trk_time = 0.0, 0.0
+    for pl in pools:
+        pl["t"].restore_state(0)
+        if stream:
+            tp = timed_part(lambda: pl["t"].run_device(tbase, 0, t_items, K * pl["per_step"], pl["out"].data_ptr(),
+                                                       pl["cnt"].data_ptr()))
+            span_items = K * total * n
+        else:
+            tp = timed_part(lambda: [(pl["t"].restore_state(0),
+                                      pl["t"].run_device(base, 0, ns, pl["epochs"], pl["out"].data_ptr(),
+                                                         pl["cnt"].data_ptr())) for _ in range(K)])
+            span_items = K * total * n
+        ncalls = int(pl["cnt"].cpu().numpy().sum())
+        # algorithmic HBM bytes of a call: its IQ window (8 B per sample) + the record
+        b = ncalls * (8.0 * pl["per"] + gsdr.TRK_EPOCH_DTYPE.itemsize)
+        trk_bytes += b
+        trk_time += tp
+        comp["trk_%s_msps" % names[pl["sig"]]] = round(span_items / tp / 1e6, 2)
+        comp["trk_%s_channels" % names[pl["sig"]]] = pl["nch"]
+        comp["trk_%s_gbps" % names[pl["sig"]]] = round(b / tp / 1e9, 2)
+    host = torch.from_numpy(iq.view(np.float32)).pin_memory()
+    scratch = torch.empty_like(iq_dev)
+    scratch.copy_(host, non_blocking=True)  # first touch
+    th = timed_part(lambda: [scratch.copy_(host, non_blocking=True) for _ in range(4)]) / 4
+    del scratch, host
+    comp["note"] = ("each stage alone after the timed region over the same K spans; trk_<pool>_msps = the stream's IQ "
+                    "rate through that pool (every channel processes every sample)")
     line = {
         "metric": METRIC,
         "value": round(value, 3),
@@ -474,20 +568,33 @@ def run_c5(args):
                            "Galileo %d, BeiDou %d) on rank %d of %d, no data-path collective"
                            % (total, lo, hi, len(plan["channels"]), len(plan["pools"][0]), len(plan["pools"][1]),
                               len(plan["pools"][2]), rank, world),
-            "tracking": "each step re-tracks the span from the channels' saved start states (three pools, one "
-                        "launch each)"},
+            "tracking": ("one continuous stream (periodic %d ms span repeated end to end), one launch per pool per "
+                         "timed region" % total if stream else
+                         "each step re-tracks the span from the channels' saved start states (one launch per pool)")},
         "real_time_factor": round(value * 1e6 / fs, 2),
         "roofline": {"bound": "valu", "achieved": round(flops * K / elapsed / 1e12, 2), "peak": FP32_PEAK / 1e12,
                      "unit": "TFLOP/s", "frac": round(flops * K / elapsed / FP32_PEAK, 4), "traffic": None,
                      "note": "nominal FFT flops of the rank's acquisition grids over the whole step (tracking and "
-                             "acquisition share the GPU)"},
-        "check": {"acquired_block0": det, "trk_calls_min_per_pool": calls},
+                             "acquisition share the GPU)",
+                     "acquisition_alone": {"achieved": round(flops * K / ta / 1e12, 2), "unit": "TFLOP/s",
+                                           "frac": round(flops * K / ta / FP32_PEAK, 4)},
+                     "tracking_alone": {"bound": "hbm", "achieved": round(trk_bytes / trk_time / 1e9, 2),
+                                        "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                                        "frac": round(trk_bytes / trk_time / HBM_PEAK, 5),
+                                        "note": "each pool's calls x (8 B x vector_length + one record) over the "
+                                                "pools' summed alone time: a serial per-channel loop, latency-bound"}},
+        "components": comp,
+        "h2d_ingest": {"bytes_per_step": int(ns * 8), "ms_per_step": round(th * 1e3, 3),
+                       "gbps": round(ns * 8 / th / 1e9, 2), "frac_of_step": round(th / (elapsed / K), 4),
+                       "note": "pinned host -> HBM copy of the rank's stream span per step (every rank ingests the "
+                               "whole stream); not part of value"},
+        "check": {"acquired_block0": det, "trk_calls_min_per_pool": calls, "tracking_convergence": conv},
         "cpu_baseline": None,
     }
     if rank == 0:
         print(json.dumps(line), flush=True)
-    for _, t, _, _, _, _ in pools:
-        t.close()
+    for pl in pools:
+        pl["t"].close()
     for _, a, *_ in acqs:
         a.close()
     if dist is not None:
@@ -626,6 +733,9 @@ def main():
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    # common time base for the chains' stage intervals (their busy-time union)
+    ref_ev = torch.cuda.Event(enable_timing=True)
+    ref_ev.record()
     t0 = time.perf_counter()
     if args.trk_stream:
         trk_stream_launch(K)
@@ -661,7 +771,24 @@ def main():
                                     sats[c].doppler_hz) for i, c in enumerate(my_ch)])
     stage_ms, stage_n, stage_busy = (np.zeros(4), np.zeros(4, np.uint32), np.zeros(4))
     trk_ms, trk_launches = 0.0, 0
+    corr_union_ms = None
     if not args.no_profile_events:
+        # the correlate stage's busy time over all chains: the union of every
+        # launch interval of every handle against one reference event
+        iv = []
+        for a in acqs:
+            st, en = a.read_profile_intervals(ref_ev.cuda_event, 1)
+            iv += list(zip(st.tolist(), en.tolist()))
+        if iv:
+            iv.sort()
+            corr_union_ms, lo_t, hi_t = 0.0, iv[0][0], iv[0][1]
+            for x0, x1 in iv[1:]:
+                if x0 > hi_t:
+                    corr_union_ms += hi_t - lo_t
+                    lo_t, hi_t = x0, x1
+                else:
+                    hi_t = max(hi_t, x1)
+            corr_union_ms += hi_t - lo_t
         for a in acqs:
             ms_a, n_a, busy_a = a.read_profile_ex()
             stage_ms = stage_ms + ms_a
@@ -709,12 +836,13 @@ def main():
         # a step holds stage_n / steps correlate launches (one per chain), each over
         # B * steps / stage_n blocks.  The chains' launches run concurrently on
         # their streams and share the chip, so a launch's duration counts the time
-        # it shares with the other chain; the kernel's wall time is the union of the
-        # launch intervals (busy time; per handle from gsdr_acq_read_profile_ex, and
-        # for nch lock-stepped chains the launch time x launches / nch).
+        # it shares with the other chain; the kernel's wall time is the union of all
+        # chains' launch intervals against one reference event
+        # (gsdr_acq_read_profile_intervals)
         corr_launch_s = stage_ms[1] / stage_n[1] / 1e3
         blocks_per_launch = B * args.steps / stage_n[1]
-        corr_busy_s = stage_busy[1] / 1e3 if nch == 1 else corr_launch_s * stage_n[1] / nch
+        corr_busy_s = (corr_union_ms / 1e3 if corr_union_ms is not None
+                       else (stage_busy[1] / 1e3 if nch == 1 else corr_launch_s * stage_n[1] / nch))
         blocks_timed = B * args.steps
         achieved = correlate_kernel_bytes_per_block() * blocks_timed / corr_busy_s
         pmc = load_pmc_traffic()
@@ -736,6 +864,8 @@ def main():
             "traffic_source": (pmc or {}).get("file"),
             "kernel": "acq_correlate_pk_kernel", "avg_launch_us": round(corr_launch_s * 1e6, 2),
             "busy_us_per_step": round(corr_busy_s / args.steps * 1e6, 2),
+            "busy_source": ("union of every chain's correlate launch intervals (one reference event)"
+                            if corr_union_ms is not None else "per-handle busy time"),
             "blocks_per_launch": blocks_per_launch,
             "launch_overlap": round(corr_launch_s * stage_n[1] / corr_busy_s, 3),
             "nominal_flops_per_launch": int(correlate_kernel_flops_per_block() * blocks_per_launch),

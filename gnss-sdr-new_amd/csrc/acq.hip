@@ -230,6 +230,10 @@ int gsdr_acq_create(int device, const gsdr_acq_conf* conf, gsdr_acq** out)
             if (e == hipSuccess) e = hipMemset(a->d_acc_slots, 0, (size_t)a->acc_words * sizeof(uint32_t));
         }
     if (e == hipSuccess) e = hipMalloc(&a->d_grid, (size_t)a->D * N * sizeof(float));
+    // split path with the peak-ratio statistic: one |R|^2 row per (block, PRN) for the
+    // merged first/second-peak pass (acq_argmax_second_four_kernel)
+    if (e == hipSuccess && a->split > 0 && !(conf->pfa > 0.0f))
+        e = hipMalloc(&a->d_rowbuf, nB * nP * N * sizeof(float));
     if (four)
         {
             // scratch slots: at least the resident workgroup count of the chip
@@ -300,7 +304,7 @@ void gsdr_acq_destroy(gsdr_acq* a)
         }
     for (hipEvent_t e : a->prof_pool) (void)hipEventDestroy(e);
     void* bufs[] = {a->st2.d_wipe, a->st2.d_freq, a->d_tw, a->d_wipe, a->d_code_fft, a->d_code_stage, a->d_prn, a->d_X, a->d_stats, a->d_res,
-        a->d_iq, a->d_grid, a->d_dgrid, a->d_tw_sub, a->d_scratch, a->d_slots, a->d_resk, a->d_acc, a->d_acc_slots};
+        a->d_iq, a->d_grid, a->d_rowbuf, a->d_dgrid, a->d_tw_sub, a->d_scratch, a->d_slots, a->d_resk, a->d_acc, a->d_acc_slots};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     if (a->stream) (void)hipStreamDestroy(a->stream);
@@ -703,6 +707,34 @@ int gsdr_acq_read_profile_ex(gsdr_acq* a, double* stage_ms, uint32_t* launches, 
             a->prof_pool.push_back(r.b);
         }
     a->prof_recs.clear();
+    return GSDR_OK;
+}
+
+int gsdr_acq_read_profile_intervals(gsdr_acq* a, const void* ref_event, int stage, double* start_ms, double* end_ms,
+    uint32_t max_n, uint32_t* n)
+{
+    GSDR_REQUIRE(a && ref_event && n && (max_n == 0 || (start_ms && end_ms)), GSDR_E_ARG,
+        "gsdr_acq_read_profile_intervals: null argument");
+    GSDR_REQUIRE(stage >= 0 && stage < 4, GSDR_E_ARG, "gsdr_acq_read_profile_intervals: stage %d", stage);
+    std::lock_guard<std::mutex> lk(a->mu);
+    gsdr::DeviceGuard g(a->device);
+    hipEvent_t ref = (hipEvent_t)const_cast<void*>(ref_event);
+    uint32_t k = 0;
+    for (auto& r : a->prof_recs)
+        {
+            if (r.stage != stage) continue;
+            if (k < max_n)
+                {
+                    GSDR_HIP(hipEventSynchronize(r.b));
+                    float t0 = 0.0f, t1 = 0.0f;
+                    GSDR_HIP(hipEventElapsedTime(&t0, ref, r.a));
+                    GSDR_HIP(hipEventElapsedTime(&t1, ref, r.b));
+                    start_ms[k] = t0;
+                    end_ms[k] = t1;
+                }
+            ++k;
+        }
+    *n = k;
     return GSDR_OK;
 }
 

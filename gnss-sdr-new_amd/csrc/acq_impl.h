@@ -26,6 +26,12 @@ namespace
 
 using gsdr::fft::Plan;
 
+// GSDR_SPLIT_TWF 1: the split correlate's input factor W_N^{m q} as a compile-time
+// root per column row and one table read per column (acq_correlate_split_kernel)
+#ifndef GSDR_SPLIT_TWF
+#define GSDR_SPLIT_TWF 0
+#endif
+
 // Default correlate variant at N = 4000 (see GSDR_PK_VARIANTS).
 constexpr int kDefaultCorrVariant4000 = 70;
 
@@ -35,7 +41,7 @@ inline int default_pk_variant(uint32_t N)
     switch (N)
         {
         case 4000: return kDefaultCorrVariant4000;
-        case 16000: return 93;
+        case 16000: return 94;  // r04a: wave-local rows, +3 % over 93
         case 8000: return 61;
         case 2000: return 62;
         default: return 0;
@@ -325,7 +331,7 @@ __global__ void __launch_bounds__(MP::NT) __attribute__((amdgpu_waves_per_eu(WPE
 {
     constexpr int PG = pg_count(PG_);
     constexpr bool PREFETCH = PG_ > 0;
-    static_assert(STAT == 1 || STAT == 2, "row statistic 1 (max + sum) or 2 (max)");
+    static_assert(STAT == 1 || STAT == 2 || STAT == 3, "row statistic 1 (max + sum), 2 (max) or 3 (max, atomic)");
     using gsdr::pk::c2;
     constexpr int NT = MP::NT;
     constexpr int NW = NT / 64;
@@ -418,6 +424,18 @@ __global__ void __launch_bounds__(MP::NT) __attribute__((amdgpu_waves_per_eu(WPE
                     };
                     MP::template run<false>(lds, tw, load, store, hook);
                     rmax = gsdr::wave_max(rmax);
+                    if constexpr (STAT == 3)
+                        {
+                            // each wave merges its maximum into the row statistic (zeroed by the
+                            // host; non-negative floats order as their bit patterns): no LDS
+                            // exchange and no workgroup barrier at the end of the transform
+                            if ((threadIdx.x & 63) == 0)
+                                __hip_atomic_fetch_max(
+                                    reinterpret_cast<uint32_t*>(&stats[((size_t)b * P + p0 + q) * D + d].max),
+                                    __float_as_uint(rmax), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            if (q + 1 < np) __syncthreads();  // the next transform's first LDS writes
+                            continue;
+                        }
                     if constexpr (STAT == 1)
                         {
 #pragma unroll
@@ -515,14 +533,7 @@ __device__ __forceinline__ void rows_stage(gsdr::pk::c2* lds, Out& out)
                     if constexpr (Ns > 1)
                         {
                             k = jb[b] % Ns;
-                            const c2 w1 = gsdr::pk::from(out.twiddle(k * TSTRIDE));
-                            c2 w = w1;
-#pragma unroll
-                            for (int r = 1; r < R; ++r)
-                                {
-                                    if (r > 1) w = gsdr::pk::mul(w, w1);
-                                    v[b][r] = gsdr::pk::mul(v[b][r], w);
-                                }
+                            gsdr::pk::apply_powers<R>(v[b], gsdr::pk::from(out.twiddle(k * TSTRIDE)));
                         }
                     gsdr::pk::Dft<R>::run(v[b]);
                     if constexpr (LAST)
@@ -611,14 +622,7 @@ __device__ __forceinline__ void wl_stage(gsdr::pk::c2* row, Out& out, int lane)
             if constexpr (Ns > 1)
                 {
                     k = jb[b] % Ns;
-                    const c2 w1 = gsdr::pk::from(out.twiddle(k * TSTRIDE));
-                    c2 w = w1;
-#pragma unroll
-                    for (int r = 1; r < R; ++r)
-                        {
-                            if (r > 1) w = gsdr::pk::mul(w, w1);
-                            v[b][r] = gsdr::pk::mul(v[b][r], w);
-                        }
+                    gsdr::pk::apply_powers<R>(v[b], gsdr::pk::from(out.twiddle(k * TSTRIDE)));
                 }
             gsdr::pk::Dft<R>::run(v[b]);
             if constexpr (LAST)
@@ -801,14 +805,7 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(RP:
                     for (int n1 = 0; n1 < R; ++n1)
                         v[c][n1] = gsdr::pk::conj_mul(bload(xrs, n2 * 8, n1 * L * 8), bload(crs, n2 * 8, n1 * L * 8));
                     gsdr::pk::Dft<R>::run(v[c]);
-                    const c2 w1 = gsdr::pk::from(tw[n2]);
-                    c2 w = w1;
-#pragma unroll
-                    for (int k1 = 1; k1 < R; ++k1)
-                        {
-                            if (k1 > 1) w = gsdr::pk::mul(w, w1);
-                            v[c][k1] = gsdr::pk::mul(v[c][k1], w);
-                        }
+                    gsdr::pk::apply_powers<R>(v[c], gsdr::pk::from(tw[n2]));
                 }
         }
     struct Out
@@ -917,10 +914,10 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(RP:
                 if (L % NT == 0 || wbase + c * NT < L)
                     {
                         const int n2 = min((int)threadIdx.x + c * NT, L - 1);
-#pragma unroll
-                        for (int n1 = 0; n1 < R; ++n1)
-                            {
+                        auto column_input = [&](auto n1c) {
+                                constexpr int n1 = decltype(n1c)::value;
                                 const int m = n1 * L + n2;
+                                (void)m;
                                 c2 z = gsdr::pk::conj_mul(bload(xrs, n2 * 8, n1 * L * 8), bload(crs, n2 * 8, n1 * L * 8));
 #pragma unroll
                                 for (int r = 1; r < ROUT; ++r)
@@ -938,19 +935,28 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(RP:
                                         else
                                             z = gsdr::pk::sub_mi(z, y);  // z + i y
                                     }
-                                if constexpr (Q > 0) z = gsdr::pk::mul(z, gsdr::pk::from(tw[m * Q]));
+                                if constexpr (Q > 0)
+                                    {
+                                        if constexpr (GSDR_SPLIT_TWF)
+                                            z = gsdr::pk::mul_root<Q * n1, ROUT * R>(z);
+                                        else
+                                            z = gsdr::pk::mul(z, gsdr::pk::from(tw[m * Q]));
+                                    }
                                 v[c][n1] = z;
-                            }
+                        };
+                        gsdr::pk::static_for<0, R>(column_input);
                         gsdr::pk::Dft<R>::run(v[c]);
-                        // W_M^{n2 k1} = W_N^{ROUT n2 k1}
-                        const c2 w1 = gsdr::pk::from(tw[ROUT * n2]);
-                        c2 w = w1;
-#pragma unroll
-                        for (int k1 = 1; k1 < R; ++k1)
+                        // W_M^{n2 k1} = W_N^{ROUT n2 k1}; GSDR_SPLIT_TWF: the input factor
+                        // W_N^{m Q} = W_{ROUT R}^{Q n1} W_N^{Q n2} -- the first a compile-time
+                        // root above, the second common to the column, so applied to its
+                        // outputs here: one table read instead of R
+                        if constexpr (Q > 0 && GSDR_SPLIT_TWF)
                             {
-                                if (k1 > 1) w = gsdr::pk::mul(w, w1);
-                                v[c][k1] = gsdr::pk::mul(v[c][k1], w);
+                                const c2 w0 = gsdr::pk::from(tw[Q * n2]);
+#pragma unroll
+                                for (int k1 = 0; k1 < R; ++k1) v[c][k1] = gsdr::pk::mul(v[c][k1], w0);
                             }
+                        gsdr::pk::apply_powers<R>(v[c], gsdr::pk::from(tw[ROUT * n2]));
                     }
             }
     };
@@ -1164,7 +1170,7 @@ __global__ void __launch_bounds__(MP::NT) acq_argmax_pk_kernel(const float2* __r
             res[bp].code_phase = idx;
             res[bp].acq_delay_samples = (double)fmodf((float)idx, samples_per_code);
         }
-    if constexpr (STAT == 2)
+    if constexpr (STAT >= 2)
         {
             // CFAR input power of the row opposite the peak (pcps_acquisition.cc:531-533)
             // by Parseval: accumulate(|R|^2) / fft_size = sum_k |X_opp[k]|^2 |C[k]|^2
@@ -1707,6 +1713,104 @@ __global__ void __launch_bounds__(PT::NT) acq_second_peak_kernel(const float2* _
         }
 }
 
+// Peak ratio on the split path in one pass over the selected row: recompute row d*
+// of (b, p) on PT once (acq_argmax_four_kernel + acq_second_peak_kernel recomputed
+// it twice), keep its |R|^2 in the workgroup's row of rowbuf while finding the
+// first maximum (index_max rule), then scan that row again for the maximum
+// outside the exclusion window around it (pcps_acquisition.cc:580-604, wrapped at
+// d_fft_size as the reference does).  Values bit-identical to the two kernels'.
+template <class PT>
+__global__ void __launch_bounds__(PT::NT) acq_argmax_second_four_kernel(const float2* __restrict__ X,
+    const float2* __restrict__ code_fft, gsdr_acq_result* __restrict__ res, const float2* __restrict__ tw,
+    typename PT::PlanT plan, AcqParams ap, float* __restrict__ rowbuf)
+{
+    constexpr int NT = PT::NT;
+    constexpr int NW = NT / 64;
+    extern __shared__ float2 lds[];
+    __shared__ unsigned long long s_key[NW];
+    const uint32_t bp = blockIdx.x;
+    const uint32_t b = bp / ap.P, p = bp - b * ap.P;
+    const uint32_t N = ap.N;
+    const uint32_t d = res[bp].doppler_index;
+    if (d >= ap.D) return;  // uniform: no maximum found (an all-NaN grid)
+    const float2* x = X + ((size_t)b * ap.D + d) * N;
+    const float2* c = code_fft + (size_t)p * N;
+    const int off = (int)ap.out_off;
+    const uint32_t eff = N - (uint32_t)off;
+    float* row = rowbuf + (size_t)bp * N;
+    auto load = [&](int i) -> float2 {
+        const float2 a = x[i], k = c[i];
+        return make_float2(a.x * k.x + a.y * k.y, a.x * k.y - a.y * k.x);
+    };
+    unsigned long long key = 0ull;
+    auto store = [&](int i, float2 v) {
+        const int j = i - off;
+        if (j < 0) return;
+        const float m = __builtin_fmaf(v.x, v.x, v.y * v.y);
+        row[j] = m;
+        const unsigned long long k = ((unsigned long long)__float_as_uint(m) << 32) | (0xffffffffu - (uint32_t)j);
+        key = k > key ? k : key;
+    };
+    PT::run(plan, lds, tw, load, store);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+        {
+            const unsigned long long t = __shfl_xor(key, o);
+            key = t > key ? t : key;
+        }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) s_key[wave] = key;
+    __syncthreads();  // also orders every lane's row stores before the scan below
+#pragma unroll
+    for (int w = 0; w < NW; ++w) key = s_key[w] > key ? s_key[w] : key;
+    const uint32_t idx = 0xffffffffu - (uint32_t)(key & 0xffffffffu);
+    const float peak = __uint_as_float((uint32_t)(key >> 32));
+    // second peak (acq_second_peak_kernel's window and tie rule)
+    const int32_t ti = (int32_t)idx;
+    int32_t e1 = ti - (int32_t)ap.samples_per_chip;
+    int32_t e2 = ti + (int32_t)ap.samples_per_chip;
+    if (e1 < 0)
+        e1 = (int32_t)N + e1;
+    else if (e2 >= (int32_t)N)
+        e2 = e2 - (int32_t)N;
+    float best = 0.0f;
+    uint32_t bidx = 0;
+    for (uint32_t j = threadIdx.x; j < eff; j += NT)
+        {
+            const int32_t jj = (int32_t)j;
+            const bool excluded = (e1 < e2) ? (jj >= e1 && jj < e2) : (jj >= e1 || jj < e2);
+            const float m = excluded ? 0.0f : row[j];
+            if (stat_better(m, j, best, bidx))
+                {
+                    best = m;
+                    bidx = j;
+                }
+        }
+    __syncthreads();  // s_key reuse
+    unsigned long long k2 = ((unsigned long long)__float_as_uint(best) << 32) | (0xffffffffu - bidx);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+        {
+            const unsigned long long t = __shfl_xor(k2, o);
+            k2 = t > k2 ? t : k2;
+        }
+    if (lane == 0) s_key[wave] = k2;
+    __syncthreads();
+    if (threadIdx.x == 0)
+        {
+#pragma unroll
+            for (int w = 0; w < NW; ++w) k2 = s_key[w] > k2 ? s_key[w] : k2;
+            gsdr_acq_result r = res[bp];
+            r.code_phase = idx;
+            r.acq_delay_samples = (double)fmodf((float)idx, ap.samples_per_code);
+            r.peak = peak;
+            r.second_peak = __uint_as_float((uint32_t)(k2 >> 32));
+            r.test_statistic = r.peak / r.second_peak;
+            r.positive = r.test_statistic > ap.threshold ? 1 : 0;
+            res[bp] = r;
+        }
+}
+
 }  // namespace
 
 // ====================================================================== handle
@@ -1747,6 +1851,7 @@ struct gsdr_acq
     gsdr_acq_result* d_res{nullptr};
     void* d_iq{nullptr};
     float* d_grid{nullptr};
+    float* d_rowbuf{nullptr};  // split path, peak ratio: the selected rows' |R|^2 (max_blocks x max_prns x N)
     float* d_dgrid{nullptr};     // gsdr_acq_run_dwell: the |R|^2 grid kept across calls (max_prns x D x eff)
     float2* d_tw_sub{nullptr};   // four-step: W_N2 table
     float2* d_scratch{nullptr};  // four-step: slot rows of N complex
@@ -1794,7 +1899,8 @@ size_t item_bytes(int it) { return it == GSDR_ITEM_CSHORT ? 4 : (it == GSDR_ITEM
 // size (default_pk_variant; GSDR_ACQ_CORR_VARIANT selects one for tests):
 // (id, plan, PRNs per workgroup, waves-per-EU hint, row statistic: 1 max + sum
 // with the argmax recomputed for the selected row, 2 max only with the CFAR row
-// sum by Parseval -- see acq_correlate_pk_kernel).  93 runs the correlate on the
+// sum by Parseval -- see acq_correlate_pk_kernel; 3 the same maximum merged per wave
+// by an atomic, without the end-of-transform barrier).  93 runs the correlate on the
 // register four-step (acq_correlate_reg_kernel, N = 16000, PRN-group-major XCD
 // walk) and its forward / argmax passes on the listed plan; 94 the same with
 // wave-local row transforms (RegFourStep H = 0).  The alternatives
@@ -1806,7 +1912,8 @@ size_t item_bytes(int it) { return it == GSDR_ITEM_CSHORT ? 4 : (it == GSDR_ITEM
     X(62, (gsdr::pk::PkPlan<256, true, 20, 10, 10>), 1, 1, 1)           \
     X(93, (gsdr::pk::PkPlan<1024, 1, 16, 10, 10, 10>), 1, 1, 2)         \
     X(94, (gsdr::pk::PkPlan<1024, 1, 16, 10, 10, 10>), 1, 1, 2)         \
-    X(70, (gsdr::pk::PkPlan<256, 1, 25, 16, 10>), 1, 1, 2)
+    X(70, (gsdr::pk::PkPlan<256, 1, 25, 16, 10>), 1, 1, 2)          \
+    X(71, (gsdr::pk::PkPlan<256, 1, 25, 16, 10>), 1, 1, 3)
 
 template <class PT>
 int set_lds_attrs(size_t bytes)
@@ -1832,8 +1939,12 @@ int set_lds_attrs(size_t bytes)
     GSDR_HIP(hipFuncSetAttribute((const void*)acq_dwell_grid_kernel<PT>, hipFuncAttributeMaxDynamicSharedMemorySize,
         (int)bytes));
     if constexpr (std::is_same<typename PT::PlanT, gsdr::fft::Plan4>::value)
-        GSDR_HIP(hipFuncSetAttribute((const void*)acq_argmax_four_kernel<PT>,
-            hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+        {
+            GSDR_HIP(hipFuncSetAttribute((const void*)acq_argmax_four_kernel<PT>,
+                hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+            GSDR_HIP(hipFuncSetAttribute((const void*)acq_argmax_second_four_kernel<PT>,
+                hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+        }
     return GSDR_OK;
 }
 
@@ -2046,11 +2157,21 @@ int launch_split_all(gsdr_acq* a, const void* iq, int item_type, uint32_t nblock
     hipLaunchKernelGGL(acq_reduce_kernel, dim3(nblocks * a->nprn), dim3(64), 0, s, a->d_stats, res, a->d_prn, ap,
         stamp0, stride);
     GSDR_HIP(hipGetLastError());
-    hipLaunchKernelGGL((acq_argmax_four_kernel<PT>), dim3(nblocks * a->nprn), dim3(PT::NT), lds, s, a->d_X,
-        a->d_code_fft, res, a->d_tw, plan_of<PT>(a), ap);
-    GSDR_HIP(hipGetLastError());
+    if (ap.cfar || !a->d_rowbuf)
+        {
+            hipLaunchKernelGGL((acq_argmax_four_kernel<PT>), dim3(nblocks * a->nprn), dim3(PT::NT), lds, s, a->d_X,
+                a->d_code_fft, res, a->d_tw, plan_of<PT>(a), ap);
+            GSDR_HIP(hipGetLastError());
+        }
+    else
+        {
+            // peak ratio: first and second peak from one recomputation of the row
+            hipLaunchKernelGGL((acq_argmax_second_four_kernel<PT>), dim3(nblocks * a->nprn), dim3(PT::NT), lds, s,
+                a->d_X, a->d_code_fft, res, a->d_tw, plan_of<PT>(a), ap, a->d_rowbuf);
+            GSDR_HIP(hipGetLastError());
+        }
     t.end(2);
-    if (!ap.cfar)
+    if (!ap.cfar && !a->d_rowbuf)
         {
             t.begin();
             hipLaunchKernelGGL((acq_second_peak_kernel<PT>), dim3(nblocks * a->nprn), dim3(PT::NT), lds, s, a->d_X,

@@ -43,6 +43,8 @@ int launch_corr_variant(gsdr_acq* a, uint32_t nblocks, hipStream_t s)
         {                                                                                                       \
             using M = GSDR_UNPAREN MP;                                                                          \
             const uint32_t groups = (a->nprn + pg_count(PG) - 1) / pg_count(PG);                                                  \
+            if (ST == 3)                                                                                        \
+                GSDR_HIP(hipMemsetAsync(a->d_stats, 0, (size_t)nblocks * a->nprn * a->D * sizeof(RowStat), s)); \
             hipLaunchKernelGGL((acq_correlate_pk_kernel<M, PG, WPE, ST>), dim3(nblocks * a->D * groups),         \
                 dim3(M::NT), a->corr_lds_bytes, s, a->d_X, a->d_code_fft, a->d_stats, a->d_tw, a->D, a->nprn,   \
                 nblocks);                                                                                       \

@@ -42,8 +42,10 @@ struct SplitId
     int id;
     uint32_t n;
 };
-constexpr SplitId kSplits[] = {{1, 25000}, {2, 32000}, {3, 64000}, {4, 100000}, {5, 32000}, {6, 64000}, {11, 25000},
-    {12, 32000}, {13, 64000}, {14, 100000}, {15, 32000}, {16, 64000}, {17, 25000}, {18, 100000}, {19, 32000},
+// the first entry of a size is its default (r04a: wave-local rows 12 / 13 for 32000 /
+// 64000, +4 % / +10 % over 2 / 3; the 512-lane 25000 plan keeps its LDS rounds)
+constexpr SplitId kSplits[] = {{1, 25000}, {12, 32000}, {13, 64000}, {4, 100000}, {2, 32000}, {3, 64000}, {5, 32000},
+    {6, 64000}, {11, 25000}, {14, 100000}, {15, 32000}, {16, 64000}, {17, 25000}, {18, 100000}, {19, 32000},
     {20, 64000}, {112, 32000}, {212, 32000}, {113, 64000}, {213, 64000}};
 // 112 / 212, 113 / 213: timing ablations of 12 / 13 (acq_correlate_split_kernel ABL:
 // 1xx without phase 1's global loads, 2xx without phase 2) -- profiles only
@@ -132,7 +134,7 @@ int setup_split(gsdr_acq* a)
     if (mode == 0) return GSDR_OK;
     for (const SplitId& sp : kSplits)
         if (sp.n == a->N && !a->split) a->split = sp.id;
-    if (a->split == 4 && mode < 2) a->split = 0;
+    if ((a->split == 4 || a->split == 14 || a->split == 18) && mode < 2) a->split = 0;
     // experiments: GSDR_ACQ_SPLIT_ID forces a split of the handle's N
     if (const char* e = std::getenv("GSDR_ACQ_SPLIT_ID"))
         {

@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <type_traits>
 
 #include "fft_lds.h"
 #include "fft_multi.h"
@@ -102,6 +103,62 @@ __device__ __forceinline__ c2 mul_root(c2 a)
             // (a.x wr - a.y wi, a.y wr + a.x wi)
             const c2 t = a * c2{wr, wr};
             return __builtin_elementwise_fma(a.yx, c2{-wi, wi}, t);
+        }
+}
+
+// compile-time loop: f(std::integral_constant<int, I>) for I = B .. E-1
+template <int B, int E, class F>
+__device__ __forceinline__ void static_for(F& f)
+{
+    if constexpr (B < E)
+        {
+            f(std::integral_constant<int, B>{});
+            static_for<B + 1, E>(f);
+        }
+}
+
+// ---- twiddle powers ----
+// v[r] *= w1^r for r = 1 .. R-1.  GSDR_TW_TREE 0: one chain w <- w w1 (R-2
+// dependent complex products); 1: baby-step / giant-step -- the powers w^1 .. w^(S-1)
+// and the giants w^(S a), then w^(S a + b) = w^(S a) w^b -- the same R-2 products
+// with a dependency depth of about log2(S) + R/S instead of R-2.
+#ifndef GSDR_TW_TREE
+#define GSDR_TW_TREE 0
+#endif
+template <int R>
+__device__ __forceinline__ void apply_powers(c2* v, c2 w1)
+{
+    if constexpr (R <= 2 || !GSDR_TW_TREE)
+        {
+            c2 w = w1;
+#pragma unroll
+            for (int r = 1; r < R; ++r)
+                {
+                    if (r > 1) w = mul(w, w1);
+                    v[r] = mul(v[r], w);
+                }
+        }
+    else
+        {
+            constexpr int S = R >= 32 ? 8 : (R % 5 == 0 ? 5 : 4);
+            c2 b[S];  // b[k] = w^k, k < S
+            b[1] = w1;
+#pragma unroll
+            for (int k = 2; k < S; ++k) b[k] = mul(b[k / 2], b[k - k / 2]);
+            const c2 g1 = mul(b[S / 2], b[S - S / 2]);  // w^S
+            c2 g = g1;
+#pragma unroll
+            for (int r = 1; r < R; ++r)
+                {
+                    const int a = r / S, k = r % S;
+                    if (a > 1 && k == 0) g = mul(g, g1);  // w^(S a)
+                    if (a == 0)
+                        v[r] = mul(v[r], b[k]);
+                    else if (k == 0)
+                        v[r] = mul(v[r], g);
+                    else
+                        v[r] = mul(v[r], mul(g, b[k]));
+                }
         }
 }
 
@@ -399,14 +456,7 @@ __device__ __forceinline__ void stage(c2* lds, const float2* __restrict__ tw, Lo
                                 }
                             else if constexpr (MODE == 1)
                                 {
-                                    const c2 w1 = from(tw[step]);
-                                    c2 w = w1;
-#pragma unroll
-                                    for (int r = 1; r < R; ++r)
-                                        {
-                                            if (r > 1) w = mul(w, w1);
-                                            v[b][r] = mul(v[b][r], w);
-                                        }
+                                    apply_powers<R>(v[b], from(tw[step]));
                                 }
                             else
                                 {

@@ -43,7 +43,7 @@ EXPORTED = [
     "gsdr_stream_create", "gsdr_stream_destroy", "gsdr_stream_push", "gsdr_stream_span", "gsdr_stream_window",
     "gsdr_acq_set_step_two", "gsdr_acq_get_step_two_threshold", "gsdr_acq_run_step_two",
     "gsdr_trk_set_data_code", "gsdr_acq_read_profile_ex", "gsdr_stream_window_async", "gsdr_stream_release", "gsdr_stream_device",
-    "gsdr_acq_dump_grid_step_two",
+    "gsdr_acq_dump_grid_step_two", "gsdr_acq_read_profile_intervals",
 ]
 
 SIGNAL_GPS_1C = 0
@@ -233,6 +233,7 @@ def load():
     L.gsdr_acq_run_device.argtypes = [P, P, U32, U64, U64, P, P]
     L.gsdr_acq_dump_grid.argtypes = [P, P, U32, P]
     L.gsdr_acq_dump_grid_step_two.argtypes = [P, P, U32, ctypes.c_float, P]
+    L.gsdr_acq_read_profile_intervals.argtypes = [P, P, ctypes.c_int, P, P, U32, P]
     L.gsdr_acq_dump_spectra.argtypes = [P, P, P]
     L.gsdr_corr_create.argtypes = [I, I, I, I, P]
     L.gsdr_corr_destroy.argtypes = [P]
@@ -450,6 +451,17 @@ class Acquisition:
         busy = np.zeros(4, np.float64)
         _check(load().gsdr_acq_read_profile_ex(self._h, _ptr(ms), _ptr(n), _ptr(busy)))
         return ms, n, busy
+
+    def read_profile_intervals(self, ref_event, stage, max_n=4096):
+        """[start, end) ms of each recorded launch of `stage` against ref_event (a
+        hipEvent_t handle, e.g. torch.cuda.Event(enable_timing=True).cuda_event)."""
+        st = np.zeros(max_n, np.float64)
+        en = np.zeros(max_n, np.float64)
+        n = ctypes.c_uint32(0)
+        _check(load().gsdr_acq_read_profile_intervals(self._h, ctypes.c_void_p(ref_event), int(stage), _ptr(st),
+                                                      _ptr(en), int(max_n), ctypes.byref(n)))
+        k = min(n.value, max_n)
+        return st[:k], en[:k]
 
     def dump_grid(self, iq, prn_slot):
         iq = self._items(iq)

@@ -48,6 +48,7 @@
 #include "hip_multicorrelator_real_codes.h"
 #include "tracking_dump.h"
 #include "tracking_pool.h"
+#include "synth_stream.h"
 #include <unistd.h>
 
 namespace
@@ -715,55 +716,6 @@ void test_galileo_acquisition(const std::vector<std::complex<float>>& capture)
     std::printf("galileo acquisition: message %d delay %.1f samples doppler %.0f Hz stat %.2f (thr %.2f)\n", ev,
         gs.Acq_delay_samples, gs.Acq_doppler_hz, acquisition->get_block()->test_statistics(),
         acquisition->get_block()->threshold());
-}
-
-// ---- synthetic streams: code x carrier (+ data bits) + AWGN, code Doppler included
-struct SynthSat
-{
-    std::vector<float> chips;  // one sample per chip (or sub-chip replica)
-    double chip_rate;          // replica samples per second (chips/s x samples per chip)
-    double carrier_hz;         // L1 / E1 / B1I carrier [Hz]
-    double delay_samples;      // code start sample
-    double doppler_hz;
-    double amplitude;
-    std::vector<float> secondary;  // per code period (empty: none)
-    std::vector<float> data;       // navigation symbols, data_period_s each (empty: none)
-    double data_period_s{0.02};
-};
-
-std::vector<std::complex<float>> synth_stream(const std::vector<SynthSat>& sats, double fs, size_t n, uint32_t seed,
-    double noise_sigma)
-{
-    std::vector<std::complex<float>> x(n);
-    std::mt19937 gen(seed);
-    std::normal_distribution<double> nd(0.0, noise_sigma);
-    for (size_t i = 0; i < n; ++i) x[i] = std::complex<float>(static_cast<float>(nd(gen)), static_cast<float>(nd(gen)));
-    for (const auto& s : sats)
-        {
-            const double L = static_cast<double>(s.chips.size());
-            const double rate = s.chip_rate * (1.0 + s.doppler_hz / s.carrier_hz);
-            for (size_t i = 0; i < n; ++i)
-                {
-                    const double t = (static_cast<double>(i) - s.delay_samples) / fs;
-                    const double c = t * rate;                   // replica samples since the code start
-                    const double period = std::floor(c / L);
-                    double k = c - period * L;
-                    const auto idx = static_cast<size_t>(std::min(L - 1.0, std::max(0.0, std::floor(k))));
-                    double v = s.chips[idx];
-                    if (!s.secondary.empty())
-                        {
-                            const auto p = static_cast<long long>(period);
-                            const long long ns = static_cast<long long>(s.secondary.size());
-                            v *= s.secondary[static_cast<size_t>(((p % ns) + ns) % ns)];
-                        }
-                    if (!s.data.empty() && t >= 0.0)
-                        v *= s.data[static_cast<size_t>(std::floor(t / s.data_period_s)) % s.data.size()];
-                    const double ph = 2.0 * M_PI * s.doppler_hz * static_cast<double>(i) / fs + 0.3;
-                    x[i] += std::complex<float>(static_cast<float>(s.amplitude * v * std::cos(ph)),
-                        static_cast<float>(s.amplitude * v * std::sin(ph)));
-                }
-        }
-    return x;
 }
 
 void test_beidou_acquisition()

@@ -1,0 +1,293 @@
+// Throughput of the drop-in receiver path at configuration scale:
+// the factory-built pooled TrackingInterface blocks (dll_pll_veml_tracking_pool_mi355x,
+// the MI355X adapters' default) fed GNU-Radio style -- every block's work() with the
+// items its upstream buffer holds at its own nitems_read -- beside AcquisitionService
+// grids on the GPU's device IQ ring (host pushes), searching the PRNs that no channel
+// tracks (each answer re-arms the request, as a receiver's idle channels keep
+// searching).  The reference's shape: gnss_flowgraph.cc:1007-1135 (one tracking and
+// one acquisition block per channel over the conditioner output).
+//   receiver_bench c3|c5 [seconds]
+// C3: GPS L1 C/A at 16 Msps, 12 tracked channels; C5: one GPU's share of the 25 Msps
+// hybrid job, 12 GPS L1 C/A + 12 Galileo E1 (pilot) + 8 BeiDou B1I channels.
+// Prints one JSON line: stream Msps through the whole receiver path (host loop,
+// pushes, launches, records) and per-signal outputs / Doppler errors.
+#include <chrono>
+#include <cmath>
+#include <complex>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "acquisition_service.h"
+#include "gnss_block_factory_mi355x.h"
+#include "gnss_replicas.h"
+#include "gnss_tracking_mi355x.h"
+#include "synth_stream.h"
+
+namespace
+{
+struct Sig
+{
+    const char* role;       // Tracking_<xx> / Acquisition_<xx>
+    const char* impl_trk;
+    const char* impl_acq;
+    char sys;
+    char s0, s1;
+    int nch;                // tracked channels
+    int nprn;               // PRNs of the constellation (the rest are searched)
+    double chip_rate;       // chips/s
+    double carrier;
+    int code_ms;            // code period [ms]
+};
+
+std::vector<float> code_of(char sys, uint32_t prn)
+{
+    if (sys == 'E') return galileo_e1_code_gen_sinboc11_float("1B", prn);
+    if (sys == 'C') return beidou_b1i_code_gen_float(static_cast<int32_t>(prn), 0);
+    return gps_l1_ca_code_gen_float(static_cast<int32_t>(prn), 0);
+}
+}  // namespace
+
+int main(int argc, char** argv)
+{
+    const std::string cfg = argc > 1 ? argv[1] : "c3";
+    const bool c5 = cfg == "c5";
+    const double fs = c5 ? 25.0e6 : 16.0e6;
+    const double seconds = argc > 2 ? std::atof(argv[2]) : 0.4;
+    std::vector<Sig> sigs = {{"1C", "GPS_L1_CA_DLL_PLL_Tracking_MI355X", "GPS_L1_CA_PCPS_Acquisition_MI355X", 'G', '1',
+        'C', 12, 32, 1.023e6, 1575.42e6, 1}};
+    if (c5)
+        {
+            sigs.push_back({"1B", "Galileo_E1_DLL_PLL_VEML_Tracking_MI355X", "Galileo_E1_PCPS_Ambiguous_Acquisition_MI355X",
+                'E', '1', 'B', 12, 36, 1.023e6, 1575.42e6, 4});
+            sigs.push_back({"B1", "BEIDOU_B1I_DLL_PLL_Tracking_MI355X", "BEIDOU_B1I_PCPS_Acquisition_MI355X", 'C', 'B',
+                '1', 8, 63, 2.046e6, 1561.098e6, 1});
+        }
+    // the stream: every tracked satellite at 45 dB-Hz, seeded delays and Dopplers
+    const size_t n = static_cast<size_t>(fs * seconds);
+    const double sigma = 1.0;
+    const double amp = std::sqrt(2.0 * std::pow(10.0, 4.5) / fs) * sigma;
+    std::mt19937 gen(42);
+    std::uniform_real_distribution<double> ud(0.0, 1.0);
+    std::vector<SynthSat> sats;
+    struct Truth
+    {
+        uint32_t prn;
+        double delay, doppler;
+    };
+    std::vector<std::vector<Truth>> truth(sigs.size());
+    const std::vector<float> bits = {1, -1, -1, -1, 1, -1, 1, 1};
+    std::vector<float> e1c_sec(25);
+    const char* sec_str = "0011100000001010110110010";
+    for (int i = 0; i < 25; ++i) e1c_sec[i] = sec_str[i] == '0' ? 1.0F : -1.0F;
+    for (size_t g = 0; g < sigs.size(); ++g)
+        for (int c = 0; c < sigs[g].nch; ++c)
+            {
+                const auto& s = sigs[g];
+                const uint32_t prn = static_cast<uint32_t>(c + (s.sys == 'C' ? 6 : 1));
+                const double per = fs * s.code_ms / 1000.0;
+                const double delay = std::floor(ud(gen) * per);
+                const double dop = 250.0 * std::round((ud(gen) * 8000.0 - 4000.0) / 250.0) + 37.0;
+                truth[g].push_back({prn, delay, dop});
+                if (s.sys == 'E')
+                    {
+                        // E1-B data + E1-C pilot (secondary code), 2 replica samples per chip
+                        const double a = amp / std::sqrt(2.0);
+                        auto e1c = galileo_e1_code_gen_sinboc11_float("1C", prn);
+                        for (auto& v : e1c) v = -v;
+                        sats.push_back({galileo_e1_code_gen_sinboc11_float("1B", prn), 2.046e6, s.carrier, delay, dop, a,
+                            {}, {}, 0.004});
+                        sats.push_back({e1c, 2.046e6, s.carrier, delay, dop, a, e1c_sec, {}, 0.004});
+                    }
+                else
+                    sats.push_back({code_of(s.sys, prn), s.chip_rate, s.carrier, delay, dop, amp, {}, bits,
+                        s.sys == 'C' ? 0.02 : 0.02});
+            }
+    const auto x = synth_stream(sats, fs, n, 7, sigma);
+
+    InMemoryConfiguration config;
+    config.set_property("GNSS-SDR.internal_fs_sps", std::to_string(static_cast<long long>(fs)));
+    for (const auto& s : sigs)
+        {
+            const std::string t = std::string("Tracking_") + s.role, a = std::string("Acquisition_") + s.role;
+            config.set_property(t + ".implementation", s.impl_trk);
+            config.set_property(t + ".item_type", "gr_complex");
+            config.set_property(t + ".pll_bw_hz", s.sys == 'G' ? "40.0" : "15.0");
+            config.set_property(t + ".dll_bw_hz", s.sys == 'G' ? "4.0" : "1.0");
+            config.set_property(t + ".pull_in_time_s", "0");
+            if (s.sys == 'E') config.set_property(t + ".track_pilot", "true");
+            config.set_property(std::string("Channels_") + s.role + ".count", std::to_string(s.nch));
+            config.set_property(a + ".implementation", s.impl_acq);
+            config.set_property(a + ".item_type", "gr_complex");
+            config.set_property(a + ".coherent_integration_time_ms", std::to_string(s.code_ms));
+            config.set_property(a + ".pfa", "0.01");
+            config.set_property(a + ".doppler_max", "5000");
+            config.set_property(a + ".doppler_step", "250");
+        }
+    // tracking blocks (pooled, the adapters' default) started from the true acquisition
+    struct Ch
+    {
+        std::unique_ptr<TrackingInterface> trk;
+        TrackingBlockMI355X* blk;
+        Gnss_Synchro gs;
+        uint64_t nread;
+        size_t sig;
+        double truth_dop;
+        int outputs;
+        double dop;
+    };
+    std::vector<Ch> chans;
+    chans.reserve(64);
+    for (size_t g = 0; g < sigs.size(); ++g)
+        for (int c = 0; c < sigs[g].nch; ++c)
+            {
+                chans.push_back({});
+                Ch& ch = chans.back();
+                ch.trk = gsdr_factory::GetTrkBlock(&config, std::string("Tracking_") + sigs[g].role, 1, 1, 0);
+                ch.blk = dynamic_cast<DllPllTrackingAdapterMI355X*>(ch.trk.get())->get_block();
+                const double per = fs * sigs[g].code_ms / 1000.0;
+                ch.gs = Gnss_Synchro{};
+                ch.gs.System = sigs[g].sys;
+                ch.gs.Signal[0] = sigs[g].s0;
+                ch.gs.Signal[1] = sigs[g].s1;
+                ch.gs.PRN = truth[g][c].prn;
+                ch.gs.Acq_delay_samples = std::fmod(truth[g][c].delay, per);
+                ch.gs.Acq_doppler_hz = 250.0 * std::round(truth[g][c].doppler / 250.0);
+                ch.gs.Acq_samplestamp_samples = 0;
+                ch.trk->set_channel(static_cast<unsigned int>(chans.size() - 1));
+                ch.trk->set_gnss_synchro(&ch.gs);
+                ch.trk->start_tracking();
+                ch.nread = 0;
+                ch.sig = g;
+                ch.truth_dop = truth[g][c].doppler;
+                ch.outputs = 0;
+                ch.dop = 0.0;
+            }
+    // acquisition services on the device ring: every untracked PRN of each signal,
+    // re-armed after each answer
+    gsdr_stream* ring = nullptr;
+    const uint64_t per_max = static_cast<uint64_t>(fs * 4 / 1000);
+    if (gsdr_stream_create(0, GSDR_ITEM_GR_COMPLEX, 16 * per_max, 8 * per_max, &ring) != GSDR_OK)
+        {
+            std::fprintf(stderr, "ring: %s\n", gsdr_last_error());
+            return 1;
+        }
+    std::vector<std::unique_ptr<AcquisitionService>> svcs;
+    std::vector<std::vector<std::vector<std::complex<float>>>> reps(sigs.size());
+    std::vector<uint64_t> answers(sigs.size(), 0), positives(sigs.size(), 0);
+    std::vector<std::unique_ptr<AcquisitionService::Callback>> cbs;
+    for (size_t g = 0; g < sigs.size(); ++g)
+        {
+            Acq_Conf ac;
+            ac.ms_per_code = static_cast<uint32_t>(sigs[g].code_ms);
+            ac.SetFromConfiguration(&config, std::string("Acquisition_") + sigs[g].role, sigs[g].chip_rate,
+                sigs[g].sys == 'C' ? 4000000.0 : 2000000.0);
+            const int nsearch = sigs[g].nprn - sigs[g].nch;
+            svcs.push_back(std::make_unique<AcquisitionService>(ac, static_cast<uint32_t>(nsearch), 0));
+            for (int k = 0; k < nsearch; ++k)
+                {
+                    const uint32_t prn = static_cast<uint32_t>(sigs[g].nch + k + (sigs[g].sys == 'C' ? 6 : 1));
+                    std::vector<std::complex<float>> r;
+                    if (sigs[g].sys == 'E')
+                        r = galileo_e1_code_gen_complex_sampled("1B", false, prn, static_cast<int32_t>(fs), 0, false);
+                    else if (sigs[g].sys == 'C')
+                        r = beidou_b1i_code_gen_complex_sampled(static_cast<int32_t>(prn), static_cast<int32_t>(fs), 0);
+                    else
+                        r = gps_l1_ca_code_gen_complex_sampled(prn, static_cast<int32_t>(fs), 0);
+                    reps[g].push_back(std::move(r));
+                }
+            AcquisitionService* svc = svcs.back().get();
+            for (int k = 0; k < nsearch; ++k)
+                {
+                    const uint32_t prn = static_cast<uint32_t>(sigs[g].nch + k + (sigs[g].sys == 'C' ? 6 : 1));
+                    auto* code = reps[g][k].data();
+                    // the callback lives in cbs (stable storage): an answer re-arms the
+                    // request with a copy of it -- the idle channel keeps searching
+                    cbs.push_back(std::make_unique<AcquisitionService::Callback>());
+                    AcquisitionService::Callback* cb = cbs.back().get();
+                    *cb = [&answers, &positives, g, prn, code, svc, cb](uint32_t c, const gsdr_acq_result&, bool pos) {
+                        ++answers[g];
+                        if (pos) ++positives[g];
+                        svc->request(c, prn, code, *cb);
+                    };
+                    svc->request(static_cast<uint32_t>(k), prn, code, *cb);
+                }
+        }
+    for (auto& s : svcs) s->work_ring(ring, 0);
+
+    const auto t0 = std::chrono::steady_clock::now();
+    size_t pushed = 0;
+    const size_t chunk = 16384;
+    bool progress = true;
+    uint64_t trk_calls = 0;
+    while (progress)
+        {
+            progress = false;
+            if (pushed < n)
+                {
+                    const size_t m = std::min(chunk, n - pushed);
+                    if (gsdr_stream_push(ring, x.data() + pushed, pushed, m) != GSDR_OK)
+                        {
+                            std::fprintf(stderr, "push: %s\n", gsdr_last_error());
+                            return 1;
+                        }
+                    pushed += m;
+                    progress = true;
+                    for (auto& s : svcs) s->work_ring(ring, pushed);
+                }
+            // every tracking block gets what the upstream buffer holds at its position
+            for (auto& ch : chans)
+                for (;;)
+                    {
+                        if (ch.nread >= pushed) break;
+                        const int fc = ch.blk->forecast();
+                        const uint64_t avail = pushed - ch.nread;
+                        if (avail < static_cast<uint64_t>(fc) && pushed < n) break;
+                        const int give = static_cast<int>(std::min<uint64_t>(std::max<uint64_t>(chunk, fc), avail));
+                        Gnss_Synchro out{};
+                        int nout = 0;
+                        const int used = ch.blk->work(x.data() + ch.nread, give, ch.nread, &out, &nout);
+                        if (used <= 0) break;
+                        progress = true;
+                        ch.nread += static_cast<uint64_t>(used);
+                        ++trk_calls;
+                        if (nout == 1)
+                            {
+                                if (out.Flag_valid_symbol_output) ++ch.outputs;
+                                ch.dop = out.Carrier_Doppler_hz;
+                            }
+                    }
+        }
+    const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    std::string per_sig;
+    for (size_t g = 0; g < sigs.size(); ++g)
+        {
+            int outs = 0, within = 0;
+            for (const auto& ch : chans)
+                if (ch.sig == g)
+                    {
+                        outs += ch.outputs;
+                        within += std::abs(ch.dop - ch.truth_dop) < 25.0 ? 1 : 0;
+                    }
+            char buf[256];
+            std::snprintf(buf, sizeof buf,
+                "%s\"%c%c%c\": {\"channels\": %d, \"outputs\": %d, \"channels_within_25hz\": %d, \"acq_answers\": %llu, "
+                "\"acq_positive\": %llu, \"acq_grids\": %llu}",
+                g ? ", " : "", sigs[g].sys, sigs[g].s0, sigs[g].s1, sigs[g].nch, outs, within,
+                static_cast<unsigned long long>(answers[g]), static_cast<unsigned long long>(positives[g]),
+                static_cast<unsigned long long>(svcs[g]->grids_run()));
+            per_sig += buf;
+        }
+    std::printf("{\"config\": \"%s\", \"path\": \"factory-built pooled TrackingInterface blocks (work() per block at its "
+                "nitems_read) + AcquisitionService grids on the device IQ ring, host pushes of %zu-item chunks\", "
+                "\"fs_sps\": %.0f, \"samples\": %zu, \"seconds\": %.4f, \"msps\": %.2f, \"real_time_factor\": %.2f, "
+                "\"tracking_channels\": %zu, \"trk_work_calls\": %llu, \"signals\": {%s}}\n",
+        cfg.c_str(), chunk, fs, n, sec, n / sec / 1e6, n / sec / fs, chans.size(),
+        static_cast<unsigned long long>(trk_calls), per_sig.c_str());
+    chans.clear();
+    svcs.clear();
+    gsdr_stream_destroy(ring);
+    return 0;
+}

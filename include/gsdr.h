@@ -268,6 +268,14 @@ int gsdr_acq_read_profile(gsdr_acq* acq, double* stage_ms, uint32_t* launches);
  * the handle overlap (runs issued on several streams); stage_ms / launches then
  * over-counts it. */
 int gsdr_acq_read_profile_ex(gsdr_acq* acq, double* stage_ms, uint32_t* launches, double* stage_busy_ms);
+/* The recorded launches of one stage (0 forward, 1 correlate, 2 reduce/argmax,
+ * 3 second peak) as [start, end) in ms against the caller's hipEvent_t ref_event
+ * (recorded on the same device before them), so the busy time of one stage over
+ * several handles -- chains on their own streams -- is the union of all their
+ * intervals.  *n = the stage's launch count (entries beyond max_n not written).
+ * Read before gsdr_acq_read_profile[_ex], which releases the records. */
+int gsdr_acq_read_profile_intervals(gsdr_acq* acq, const void* ref_event, int stage, double* start_ms, double* end_ms,
+    uint32_t max_n, uint32_t* n);
 
 /* Debug/verification: device forward spectrum for one host block,
  * D rows x fft_size complex<float> (= FFT(x .* w_d)). */

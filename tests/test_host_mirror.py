@@ -124,3 +124,22 @@ def _check_acq_dumps(d, cap_path):
     center = lo + 2 * step2
     Mn = pcps.magnitude_grid(x[N:2 * N], pcps.doppler_wipeoffs_step2(fs, N, center, step2, 5), cf)
     assert np.max(np.abs(m["acq_grid_narrow"].T - Mn)) <= 1e-4 * Mn.max()
+
+
+@pytest.mark.gpu
+def test_receiver_bench_c3_tracks_every_channel():
+    """The drop-in receiver path at config C3's scale (host/tests/receiver_bench.cc):
+    12 factory-built pooled tracking blocks at 16 Msps beside the acquisition service
+    on the device ring -- every channel converges and the searched PRNs are answered."""
+    import json
+    exe = os.path.join(BUILD, "receiver_bench")
+    if not os.path.exists(exe):
+        subprocess.check_call(["make", "-C", HOST, exe])
+    r = subprocess.run([exe, "c3", "0.15"], capture_output=True, text=True, timeout=180)
+    print(r.stdout, r.stderr[-2000:])
+    assert r.returncode == 0, r.stderr
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    g = d["signals"]["G1C"]
+    assert g["channels"] == 12 and g["channels_within_25hz"] == 12, d
+    assert g["acq_answers"] > 0, d  # the untracked PRNs keep being searched (pfa 0.01: rare false alarms)
+    assert d["msps"] > 0

@@ -431,7 +431,10 @@ def run_c5(args):
             s = sats_of[sig][c5_channel_signal(gc)[1]]
             truth.append(s.doppler_hz)
             tau = s.code_delay_chips / (chip * (1 + s.doppler_hz / 1.57542e9)) * fs
-            dop = 250.0 * round(s.doppler_hz / 250.0)
+            # the acquisition's Doppler: the 250 Hz grid for GPS (40 Hz PLL); Galileo and
+            # BeiDou (15 Hz PLLs) start from a make_two_steps refinement on a 25 Hz narrow grid
+            grid = 250.0 if sig == 0 else 25.0
+            dop = grid * round(s.doppler_hz / grid)
             if sig == 0:
                 t.start(i, s.prn, synth.gps_ca_chips(s.prn), float(round(tau) % per), dop, 0, 0)
             elif sig == 1:

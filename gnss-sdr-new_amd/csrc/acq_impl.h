@@ -26,10 +26,11 @@ namespace
 
 using gsdr::fft::Plan;
 
-// GSDR_SPLIT_TWF 1: the split correlate's input factor W_N^{m q} as a compile-time
-// root per column row and one table read per column (acq_correlate_split_kernel)
+// GSDR_SPLIT_TWF 1 (default since r04e: C4 bit transition +11 %): the split
+// correlate's input factor W_N^{m q} as a compile-time root per column row and one
+// table read per column instead of R (acq_correlate_split_kernel)
 #ifndef GSDR_SPLIT_TWF
-#define GSDR_SPLIT_TWF 0
+#define GSDR_SPLIT_TWF 1
 #endif
 
 // Default correlate variant at N = 4000 (see GSDR_PK_VARIANTS).
@@ -228,6 +229,85 @@ __global__ void __launch_bounds__(PT::NT) acq_forward_kernel(const void* __restr
     };
     auto store = [&](int i, float2 v) { out[i] = v; };
     PT::run(plan, lds, tw, load, store);
+}
+
+// plan types with a packed sub-plan (FourStepPkPlan): the two-launch forward
+template <class PT, class = void>
+struct requires_subplan : std::false_type
+{
+};
+template <class PT>
+struct requires_subplan<PT, std::void_t<typename PT::SubPlan>> : std::true_type
+{
+};
+
+// ---------------------------------------------------------------- K_forward, two launches (split path)
+// The four-step forward transform of the large sizes as two launches instead of one
+// workgroup per (b, d) spectrum (320 workgroups at C4 for 256 CUs -- latency-bound):
+// acq_forward4_cols_kernel runs the R-point column DFTs of every (b, d) row on
+// all CUs (one lane per column, coalesced loads of the wiped-off input, the
+// inter-step twiddle W_N^{n2 k1}) into a scratch image of the rows k1 (N2 points
+// each, contiguous); acq_forward4_rows_kernel then runs the R * nblocks * D
+// sub-transforms on the packed N2-point plan, one per workgroup, storing
+// X[k1 + R k2].  The R workgroups of one (b, d) share an XCD, so its L2 merges
+// their interleaved output writes.  Same arithmetic as FourStepPkPlan::run.
+template <class PT, int IT>
+__global__ void __launch_bounds__(256) acq_forward4_cols_kernel(const void* __restrict__ iq, uint64_t block_stride,
+    const float2* __restrict__ wipe, float2* __restrict__ scratch, const float2* __restrict__ tw, uint32_t consumed,
+    uint32_t D)
+{
+    using gsdr::pk::c2;
+    constexpr int R = PT::R, N2 = PT::N2, N = PT::N;
+    const uint32_t row = blockIdx.y;  // b * D + d
+    const uint32_t b = row / D, d = row - (row / D) * D;
+    const int n2 = (int)(blockIdx.x * 256 + threadIdx.x);
+    if (n2 >= N2) return;
+    const size_t base = (size_t)b * block_stride;
+    const float2* w = wipe + (size_t)d * N;
+    c2 v[R];
+#pragma unroll
+    for (int n1 = 0; n1 < R; ++n1)
+        {
+            const int i = n1 * N2 + n2;
+            v[n1] = i < (int)consumed ? gsdr::pk::from(gsdr::fft::cmul(load_item<IT>(iq, base + i), w[i]))
+                                      : c2{0.0f, 0.0f};
+        }
+    gsdr::pk::Dft<R>::run(v);
+    const gsdr::fft::ColTwiddles<R> cw(tw, n2);
+    float2* out = scratch + (size_t)row * N;
+    out[n2] = gsdr::pk::to(v[0]);
+#pragma unroll
+    for (int k1 = 1; k1 < R; ++k1) out[(size_t)k1 * N2 + n2] = gsdr::pk::to(gsdr::pk::mul(v[k1], cw(k1)));
+}
+
+template <class PT>
+__global__ void __launch_bounds__(PT::NT) acq_forward4_rows_kernel(const float2* __restrict__ scratch,
+    float2* __restrict__ X, const float2* __restrict__ tw_sub, uint32_t nrows)
+{
+    using gsdr::pk::c2;
+    using SP = typename PT::SubPlan;
+    constexpr int R = PT::R, N2 = PT::N2, N = PT::N;
+    extern __shared__ float2 lds_raw[];
+    // (row, k1), the R workgroups of a row on one XCD (ids dealt round-robin)
+    const uint32_t id = blockIdx.x, full = nrows >> 3;
+    uint32_t row, k1;
+    if (id < full * 8u * R)
+        {
+            const uint32_t xcd = id & 7u, slot = id >> 3;
+            row = (slot / R) * 8u + xcd;
+            k1 = slot - (slot / R) * R;
+        }
+    else
+        {
+            const uint32_t t = id - full * 8u * R;
+            row = full * 8u + t / R;
+            k1 = t - (t / R) * R;
+        }
+    const c2* rk = reinterpret_cast<const c2*>(scratch) + (size_t)row * N + (size_t)k1 * N2;
+    float2* out = X + (size_t)row * N;
+    auto ld = [&](int, int, int i) -> c2 { return rk[i]; };
+    auto st = [&](int k2, c2 v, int) { out[k1 + R * k2] = gsdr::pk::to(v); };
+    SP::template run<false>(reinterpret_cast<c2*>(lds_raw), tw_sub, ld, st, [] {});
 }
 
 // ---------------------------------------------------------------- K_correlate
@@ -1852,6 +1932,7 @@ struct gsdr_acq
     void* d_iq{nullptr};
     float* d_grid{nullptr};
     float* d_rowbuf{nullptr};  // split path, peak ratio: the selected rows' |R|^2 (max_blocks x max_prns x N)
+    float2* d_fscratch{nullptr};  // split path: the two-launch forward's column-DFT rows (max_blocks x D x N)
     float* d_dgrid{nullptr};     // gsdr_acq_run_dwell: the |R|^2 grid kept across calls (max_prns x D x eff)
     float2* d_tw_sub{nullptr};   // four-step: W_N2 table
     float2* d_scratch{nullptr};  // four-step: slot rows of N complex
@@ -1899,8 +1980,9 @@ size_t item_bytes(int it) { return it == GSDR_ITEM_CSHORT ? 4 : (it == GSDR_ITEM
 // size (default_pk_variant; GSDR_ACQ_CORR_VARIANT selects one for tests):
 // (id, plan, PRNs per workgroup, waves-per-EU hint, row statistic: 1 max + sum
 // with the argmax recomputed for the selected row, 2 max only with the CFAR row
-// sum by Parseval -- see acq_correlate_pk_kernel; 3 the same maximum merged per wave
-// by an atomic, without the end-of-transform barrier).  93 runs the correlate on the
+// sum by Parseval -- see acq_correlate_pk_kernel; 3, the same maximum merged per wave
+// by an atomic without the end-of-transform barrier, measured 2 % slower at N = 4000
+// in r04e and is not built).  93 runs the correlate on the
 // register four-step (acq_correlate_reg_kernel, N = 16000, PRN-group-major XCD
 // walk) and its forward / argmax passes on the listed plan; 94 the same with
 // wave-local row transforms (RegFourStep H = 0).  The alternatives
@@ -1912,8 +1994,7 @@ size_t item_bytes(int it) { return it == GSDR_ITEM_CSHORT ? 4 : (it == GSDR_ITEM
     X(62, (gsdr::pk::PkPlan<256, true, 20, 10, 10>), 1, 1, 1)           \
     X(93, (gsdr::pk::PkPlan<1024, 1, 16, 10, 10, 10>), 1, 1, 2)         \
     X(94, (gsdr::pk::PkPlan<1024, 1, 16, 10, 10, 10>), 1, 1, 2)         \
-    X(70, (gsdr::pk::PkPlan<256, 1, 25, 16, 10>), 1, 1, 2)          \
-    X(71, (gsdr::pk::PkPlan<256, 1, 25, 16, 10>), 1, 1, 3)
+    X(70, (gsdr::pk::PkPlan<256, 1, 25, 16, 10>), 1, 1, 2)
 
 template <class PT>
 int set_lds_attrs(size_t bytes)
@@ -1944,6 +2025,9 @@ int set_lds_attrs(size_t bytes)
                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
             GSDR_HIP(hipFuncSetAttribute((const void*)acq_argmax_second_four_kernel<PT>,
                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+            if constexpr (requires_subplan<PT>::value)
+                GSDR_HIP(hipFuncSetAttribute((const void*)acq_forward4_rows_kernel<PT>,
+                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)PT::SubPlan::lds_bytes()));
         }
     return GSDR_OK;
 }
@@ -2096,6 +2180,25 @@ void launch_forward(gsdr_acq* a, const void* iq, int item_type, uint32_t nblocks
             a->lds_bytes, s, iq, stride, a->d_wipe, a->d_X, a->d_tw, plan_of<PT>(a), a->consumed, a->D);
 }
 
+// The two-launch forward (acq_forward4_cols_kernel + acq_forward4_rows_kernel).
+template <class PT>
+void launch_forward_two(gsdr_acq* a, const void* iq, int item_type, uint32_t nblocks, uint64_t stride, hipStream_t s)
+{
+    const uint32_t nrows = nblocks * a->D;
+    const dim3 cg((PT::N2 + 255) / 256, nrows);
+    if (item_type == GSDR_ITEM_GR_COMPLEX)
+        hipLaunchKernelGGL((acq_forward4_cols_kernel<PT, GSDR_ITEM_GR_COMPLEX>), cg, dim3(256), 0, s, iq, stride,
+            a->d_wipe, a->d_fscratch, a->d_tw, a->consumed, a->D);
+    else if (item_type == GSDR_ITEM_CSHORT)
+        hipLaunchKernelGGL((acq_forward4_cols_kernel<PT, GSDR_ITEM_CSHORT>), cg, dim3(256), 0, s, iq, stride,
+            a->d_wipe, a->d_fscratch, a->d_tw, a->consumed, a->D);
+    else
+        hipLaunchKernelGGL((acq_forward4_cols_kernel<PT, GSDR_ITEM_IBYTE>), cg, dim3(256), 0, s, iq, stride,
+            a->d_wipe, a->d_fscratch, a->d_tw, a->consumed, a->D);
+    hipLaunchKernelGGL((acq_forward4_rows_kernel<PT>), dim3(nrows * PT::R), dim3(PT::NT), PT::SubPlan::lds_bytes(), s,
+        a->d_fscratch, a->d_X, a->d_tw_sub, nrows);
+}
+
 // General path (max_dwells > 1 and/or bit_transition_flag): forward spectra of
 // all nblocks*K blocks, the dwell-accumulating correlate kernel, per-dwell
 // statistics and the dwell decision.
@@ -2144,7 +2247,15 @@ int launch_split_all(gsdr_acq* a, const void* iq, int item_type, uint32_t nblock
 {
     const size_t lds = a->lds_bytes;
     t.begin();
-    launch_forward<PT>(a, iq, item_type, nblocks, stride, s);
+    if constexpr (requires_subplan<PT>::value)
+        {
+            if (a->d_fscratch)
+                launch_forward_two<PT>(a, iq, item_type, nblocks, stride, s);
+            else
+                launch_forward<PT>(a, iq, item_type, nblocks, stride, s);
+        }
+    else
+        launch_forward<PT>(a, iq, item_type, nblocks, stride, s);
     GSDR_HIP(hipGetLastError());
     t.end(0);
     AcqParams ap = params_of(a);

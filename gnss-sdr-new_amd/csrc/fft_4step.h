@@ -206,6 +206,7 @@ struct FourStepPkPlan
     static constexpr int N2 = SP::N;
     static constexpr int N = R * N2;
     using PlanT = Plan4;
+    using SubPlan = SP;
     // tw: W_N^m for m < N (the handle's full-size table); p.tw_sub: W_N2^m, m < N2
     template <class Load, class Store>
     __device__ __forceinline__ static void run(const Plan4& p, float2* lds, const float2* __restrict__ tw, Load load,

@@ -6,7 +6,9 @@
 // tracks (each answer re-arms the request, as a receiver's idle channels keep
 // searching).  The reference's shape: gnss_flowgraph.cc:1007-1135 (one tracking and
 // one acquisition block per channel over the conditioner output).
-//   receiver_bench c3|c5 [seconds]
+//   receiver_bench c3|c5 [seconds] [search]
+// search 1 (default): the acquisition services search every untracked PRN of GPS
+// and Galileo and BeiDou PRNs up to 32 on every block; 0: the tracking blocks only.
 // C3: GPS L1 C/A at 16 Msps, 12 tracked channels; C5: one GPU's share of the 25 Msps
 // hybrid job, 12 GPS L1 C/A + 12 Galileo E1 (pilot) + 8 BeiDou B1I channels.
 // Prints one JSON line: stream Msps through the whole receiver path (host loop,
@@ -56,6 +58,7 @@ int main(int argc, char** argv)
     const bool c5 = cfg == "c5";
     const double fs = c5 ? 25.0e6 : 16.0e6;
     const double seconds = argc > 2 ? std::atof(argv[2]) : 0.4;
+    const bool search = argc > 3 ? std::atoi(argv[3]) != 0 : true;
     std::vector<Sig> sigs = {{"1C", "GPS_L1_CA_DLL_PLL_Tracking_MI355X", "GPS_L1_CA_PCPS_Acquisition_MI355X", 'G', '1',
         'C', 12, 32, 1.023e6, 1575.42e6, 1}};
     if (c5)
@@ -184,7 +187,13 @@ int main(int argc, char** argv)
             ac.ms_per_code = static_cast<uint32_t>(sigs[g].code_ms);
             ac.SetFromConfiguration(&config, std::string("Acquisition_") + sigs[g].role, sigs[g].chip_rate,
                 sigs[g].sys == 'C' ? 4000000.0 : 2000000.0);
-            const int nsearch = sigs[g].nprn - sigs[g].nch;
+            // the searched PRNs: every untracked one (BeiDou: up to PRN 32)
+            const int nsearch = search ? std::min(sigs[g].nprn, 32) - sigs[g].nch - (sigs[g].sys == 'C' ? 5 : 0) : 0;
+            if (nsearch <= 0)
+                {
+                    svcs.push_back(nullptr);
+                    continue;
+                }
             svcs.push_back(std::make_unique<AcquisitionService>(ac, static_cast<uint32_t>(nsearch), 0));
             for (int k = 0; k < nsearch; ++k)
                 {
@@ -215,7 +224,8 @@ int main(int argc, char** argv)
                     svc->request(static_cast<uint32_t>(k), prn, code, *cb);
                 }
         }
-    for (auto& s : svcs) s->work_ring(ring, 0);
+    for (auto& s : svcs)
+        if (s) s->work_ring(ring, 0);
 
     const auto t0 = std::chrono::steady_clock::now();
     size_t pushed = 0;
@@ -235,7 +245,8 @@ int main(int argc, char** argv)
                         }
                     pushed += m;
                     progress = true;
-                    for (auto& s : svcs) s->work_ring(ring, pushed);
+                    for (auto& s : svcs)
+                        if (s) s->work_ring(ring, pushed);
                 }
             // every tracking block gets what the upstream buffer holds at its position
             for (auto& ch : chans)
@@ -244,7 +255,7 @@ int main(int argc, char** argv)
                         if (ch.nread >= pushed) break;
                         const int fc = ch.blk->forecast();
                         const uint64_t avail = pushed - ch.nread;
-                        if (avail < static_cast<uint64_t>(fc) && pushed < n) break;
+                        if (avail < static_cast<uint64_t>(fc)) break;  // GNU Radio's forecast: wait for more items
                         const int give = static_cast<int>(std::min<uint64_t>(std::max<uint64_t>(chunk, fc), avail));
                         Gnss_Synchro out{};
                         int nout = 0;
@@ -253,11 +264,8 @@ int main(int argc, char** argv)
                         progress = true;
                         ch.nread += static_cast<uint64_t>(used);
                         ++trk_calls;
-                        if (nout == 1)
-                            {
-                                if (out.Flag_valid_symbol_output) ++ch.outputs;
-                                ch.dop = out.Carrier_Doppler_hz;
-                            }
+                        if (nout == 1 && out.Flag_valid_symbol_output) ++ch.outputs;
+                        if (ch.blk->state() >= 2) ch.dop = ch.blk->last_record().carrier_doppler_hz;
                     }
         }
     const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -277,14 +285,14 @@ int main(int argc, char** argv)
                 "\"acq_positive\": %llu, \"acq_grids\": %llu}",
                 g ? ", " : "", sigs[g].sys, sigs[g].s0, sigs[g].s1, sigs[g].nch, outs, within,
                 static_cast<unsigned long long>(answers[g]), static_cast<unsigned long long>(positives[g]),
-                static_cast<unsigned long long>(svcs[g]->grids_run()));
+                static_cast<unsigned long long>(svcs[g] ? svcs[g]->grids_run() : 0));
             per_sig += buf;
         }
-    std::printf("{\"config\": \"%s\", \"path\": \"factory-built pooled TrackingInterface blocks (work() per block at its "
+    std::printf("{\"config\": \"%s\", \"search\": %d, \"path\": \"factory-built pooled TrackingInterface blocks (work() per block at its "
                 "nitems_read) + AcquisitionService grids on the device IQ ring, host pushes of %zu-item chunks\", "
                 "\"fs_sps\": %.0f, \"samples\": %zu, \"seconds\": %.4f, \"msps\": %.2f, \"real_time_factor\": %.2f, "
                 "\"tracking_channels\": %zu, \"trk_work_calls\": %llu, \"signals\": {%s}}\n",
-        cfg.c_str(), chunk, fs, n, sec, n / sec / 1e6, n / sec / fs, chans.size(),
+        cfg.c_str(), search ? 1 : 0, chunk, fs, n, sec, n / sec / 1e6, n / sec / fs, chans.size(),
         static_cast<unsigned long long>(trk_calls), per_sig.c_str());
     chans.clear();
     svcs.clear();

@@ -8,17 +8,17 @@
 #     C5 at 45 dB-Hz, async ring windows, host self-test with blocking=false and the
 #     acquisition dump).
 # A stage that times out or crashes ends the script (no further GPU work).
-#   gpurun --timeout 1200 -- bash profiles/gpu_r04e.sh TAG lib1 lib2 ...
+#   gpurun --timeout 1200 -- bash profiles/gpu_r04e.sh TAG "name|lib|ENV=.. ENV=.." ...
 set -o pipefail
 TAG=${1:-r04e}; shift
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 fatal() { local rc=$1; [ $rc -eq 124 ] || [ $rc -eq 137 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; }
-for LIB in "$@"; do
-  name=$(basename $(dirname $LIB))
-  echo "== configs $name"
-  GSDR_LIB=$LIB timeout -k 10 240 python -u profiles/configs_bench.py --only C3,C4,C5 --acq-only --reps 6 \
+for SPEC in "$@"; do
+  IFS='|' read -r name LIB ENVS <<< "$SPEC"
+  echo "== configs $name ($LIB $ENVS)"
+  env $ENVS GSDR_LIB=$LIB timeout -k 10 240 python -u profiles/configs_bench.py --only C3,C4,C5 --acq-only --reps 6 \
       > "$OUT/cfg_$name.jsonl" 2> "$OUT/cfg_$name.err"; rc=$?
   if fatal $rc; then echo "fatal $rc"; exit $rc; fi
   python3 -c "
@@ -28,7 +28,7 @@ for l in open('$OUT/cfg_$name.jsonl'):
         d=json.loads(l); print('   ', d['config'], d['stage'][:48], d['msps'], d.get('roofline',{}).get('frac'))
 "
   echo "== c2 $name"
-  GSDR_LIB=$LIB timeout -k 10 240 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline > "$OUT/c2_$name.json" \
+  env $ENVS GSDR_LIB=$LIB timeout -k 10 240 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline > "$OUT/c2_$name.json" \
       2> "$OUT/c2_$name.err"; rc=$?
   if fatal $rc; then echo "fatal $rc"; exit $rc; fi
   python3 -c "

@@ -27,7 +27,7 @@ echo "== torchrun (world size 1, RCCL init + barrier + max-reduce path of bench.
 timeout -k 10 200 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
     --master-port 29517 bench.py --gpus 1 --steps 10 --warmup 5 --no-cpu-baseline > "$OUT/bench_torchrun.json" 2> "$OUT/bench_torchrun.err" &&
 echo "== c5" &&
-timeout -k 10 300 python bench.py --workload c5 --steps 5 --warmup 2 > "$OUT/bench_c5.json" 2> "$OUT/bench_c5.err" &&
+timeout -k 10 300 python bench.py --workload c5 --steps 20 --warmup 5 > "$OUT/bench_c5.json" 2> "$OUT/bench_c5.err" &&
 echo "== configs" &&
 timeout -k 10 300 python -u profiles/configs_bench.py --reps 5 > "$OUT/configs.jsonl" 2> "$OUT/configs.err"
 rc=$?

@@ -1283,6 +1283,89 @@ void test_pooled_tracking()
         pool.seconds / static_cast<double>(pool.calls) * 1e6);
 }
 
+// A lagging pooled block: block B tracks while block A (same pool, standby) is
+// handed items far past B's next call -- a flowgraph buffer deeper than the
+// pool's ring window.  B's next call must come back as a loss of lock marked
+// GSDR_TRK_F_OVERRUN (counted by overruns(), reported on stderr) instead of a
+// stall or a call over overwritten items; within the window nothing is reported.
+void test_pool_overrun()
+{
+    const double fs = 4000000.0;
+    const double amp = std::sqrt(2.0 * std::pow(10.0, 4.8) / fs);
+    SynthSat s{gps_l1_ca_code_gen_float(7), 1.023e6, 1575.42e6, 1200.4, 1250.0, amp, {}, {1, -1}, 0.02};
+    const auto x = synth_stream({s}, fs, static_cast<size_t>(fs * 0.2), 31, 1.0);
+    InMemoryConfiguration config;
+    config.set_property("GNSS-SDR.internal_fs_sps", "4000000");
+    config.set_property("Tracking_1C.implementation", "GPS_L1_CA_DLL_PLL_Tracking_MI355X");
+    config.set_property("Tracking_1C.item_type", "gr_complex");
+    config.set_property("Tracking_1C.pll_bw_hz", "40.0");
+    config.set_property("Tracking_1C.dll_bw_hz", "4.0");
+    config.set_property("Channels_1C.count", "2");
+    config.set_property("Tracking_1C.mi355x_pool_window", "4");  // 4 calls = 16000 items
+    Gnss_Synchro g{};
+    g.System = 'G';
+    g.Signal[0] = '1';
+    g.Signal[1] = 'C';
+    g.PRN = 7;
+    g.Acq_delay_samples = 1200.0;
+    g.Acq_doppler_hz = 1250.0;
+    g.Acq_samplestamp_samples = 0;
+    auto ta = gsdr_factory::GetTrkBlock(&config, "Tracking_1C", 1, 1, 0);
+    auto tb = gsdr_factory::GetTrkBlock(&config, "Tracking_1C", 1, 1, 0);
+    Gnss_Synchro ga = g;
+    ta->set_channel(0);
+    ta->set_gnss_synchro(&ga);
+    tb->set_channel(1);
+    tb->set_gnss_synchro(&g);
+    tb->start_tracking();
+    auto* a = dynamic_cast<DllPllTrackingAdapterMI355X*>(ta.get())->get_block();
+    auto* b = dynamic_cast<dll_pll_veml_tracking_pool_mi355x*>(
+        dynamic_cast<DllPllTrackingAdapterMI355X*>(tb.get())->get_block());
+    EXPECT(b != nullptr, "pool overrun: pooled block");
+    if (!b) return;
+    EXPECT(b->pool()->window_items() == 16000, "pool overrun: <role>.mi355x_pool_window sets the window in calls");
+    uint64_t na = 0, nb = 0;
+    int calls = 0;
+    bool in_window_clean = true;
+    // both blocks within the window: B tracks 20 calls, A (standby) consumes alongside
+    while (calls < 20)
+        {
+            Gnss_Synchro out{};
+            int nout = 0;
+            const int used = b->work(x.data() + nb, 8000, nb, &out, &nout);
+            if (used <= 0) break;
+            if (b->state() >= 2 && b->last_record().sample_counter == nb) ++calls;
+            in_window_clean = in_window_clean && (b->last_record().flags & GSDR_TRK_F_OVERRUN) == 0;
+            nb += static_cast<uint64_t>(used);
+            while (na < nb)
+                {
+                    const int ua = a->work(x.data() + na, static_cast<int>(std::min<uint64_t>(4000, nb - na)), na, &out, &nout);
+                    if (ua <= 0) break;
+                    na += static_cast<uint64_t>(ua);
+                }
+        }
+    EXPECT(calls == 20 && in_window_clean && b->overruns() == 0, "pool overrun: none while every block stays in the window");
+    // A runs 40000 items (2.5 windows) past B, which the scheduler has not called
+    while (na < nb + 40000)
+        {
+            Gnss_Synchro out{};
+            int nout = 0;
+            const int ua = a->work(x.data() + na, 8000, na, &out, &nout);
+            if (ua <= 0) break;
+            na += static_cast<uint64_t>(ua);
+        }
+    Gnss_Synchro out{};
+    int nout = 0;
+    b->work(x.data() + nb, 8000, nb, &out, &nout);
+    const auto& r = b->last_record();
+    EXPECT((r.flags & GSDR_TRK_F_OVERRUN) && (r.flags & GSDR_TRK_F_LOSS_OF_LOCK) && r.sample_counter == nb,
+        "pool overrun: the lagging call is a loss-of-lock record marked GSDR_TRK_F_OVERRUN");
+    EXPECT(nout == 1 && !out.Flag_valid_symbol_output && b->state() == 0 && b->overruns() == 1,
+        "pool overrun: invalid output, block back to standby, counted once");
+    std::printf("pool overrun: %d calls in the window, then a call %llu items behind the head -> overrun record at %llu\n",
+        calls, static_cast<unsigned long long>(na - nb), static_cast<unsigned long long>(r.sample_counter));
+}
+
 void test_multicorrelator(const std::vector<std::complex<float>>& capture)
 {
     const int n = 4000;
@@ -1369,6 +1452,7 @@ int main(int argc, char** argv)
     test_channel_fsm_handoff(capture);
     test_flag_overrides();
     test_pooled_tracking();
+    test_pool_overrun();
     if (failures == 0) std::printf("host_selftest: PASS\n");
     return failures == 0 ? 0 : 1;
 }

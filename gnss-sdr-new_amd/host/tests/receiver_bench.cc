@@ -157,7 +157,11 @@ int main(int argc, char** argv)
                 ch.gs.Signal[1] = sigs[g].s1;
                 ch.gs.PRN = truth[g][c].prn;
                 ch.gs.Acq_delay_samples = std::fmod(truth[g][c].delay, per);
-                ch.gs.Acq_doppler_hz = 250.0 * std::round(truth[g][c].doppler / 250.0);
+                // GPS from the 250 Hz grid (40 Hz PLL pulls in from <= 125 Hz); Galileo /
+                // BeiDou (15 Hz PLL) from a 25 Hz grid, as a make_two_steps fine search
+                // hands over -- from 125 Hz their narrow loops take longer than the run
+                const double grid = sigs[g].sys == 'G' ? 250.0 : 25.0;
+                ch.gs.Acq_doppler_hz = grid * std::round(truth[g][c].doppler / grid);
                 ch.gs.Acq_samplestamp_samples = 0;
                 ch.trk->set_channel(static_cast<unsigned int>(chans.size() - 1));
                 ch.trk->set_gnss_synchro(&ch.gs);

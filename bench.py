@@ -830,6 +830,10 @@ def main():
             "cu_partition": ({"tracking": args.trk_cus or nloc, "acquisition": 256 - (args.trk_cus or nloc)}
                              if args.cu_partition else None),
             "acq_chains": nch,
+            # the carrier model and the forward spectra computed per block (include/gsdr.h
+            # gsdr_acq_set_wipeoff / gsdr_acq_get_spectrum_reuse)
+            "carrier": ["exact", "generic", "avx2"][acqs[0].wipe_mode],
+            "forward_spectra_per_block": acqs[0].spectrum_reuse[0],
         },
         "real_time_factor": round(value * 1e6 / FS, 2),
     }

@@ -18,6 +18,7 @@
 #include "acq_impl.h"
 
 #include <algorithm>
+#include <string>
 #include <utility>
 #include "gsdr_stream_internal.h"
 
@@ -28,6 +29,9 @@ namespace
 int dispatch(gsdr_acq* a, int op, const void* iq, uint32_t nblocks, uint64_t stride, uint64_t stamp0,
     gsdr_acq_result* res, hipStream_t s, uint32_t aux)
 {
+    // the forward-spectrum layout of these launches: the main grid's (XMap), or the
+    // plain one when a narrow step-two grid has replaced the wipe-off rows
+    a->xm = (a->st2.active || a->d_wipe != a->d_wipe_grid) ? XMap{a->D, 0u, a->N} : a->xm_grid;
     if (a->variant >= 20) return gsdr_acq_impl::dispatch_four(a, op, iq, nblocks, stride, stamp0, res, s, aux);
     if (a->variant >= 10) return gsdr_acq_impl::dispatch_runtime(a, op, iq, nblocks, stride, stamp0, res, s, aux);
     return gsdr_acq_impl::dispatch_static(a, op, iq, nblocks, stride, stamp0, res, s, aux);
@@ -149,6 +153,11 @@ int gsdr_acq_create(int device, const gsdr_acq_conf* conf, gsdr_acq** out)
     if (a->conf.bit_transition_flag) a->conf.max_dwells = 1;
     a->K = a->conf.max_dwells;
     a->consumed = conf->consumed_samples;
+    if (const char* w = std::getenv("GSDR_ACQ_WIPE"))
+        {
+            const std::string m(w);
+            a->wipe_mode = m == "generic" ? GSDR_WIPE_GENERIC : (m == "avx2" ? GSDR_WIPE_AVX2 : GSDR_WIPE_EXACT);
+        }
     // pcps_acquisition.cc:85-92
     uint32_t N = conf->fft_size;
     if (N == 0) N = (conf->sampled_ms == conf->ms_per_code || conf->sampled_ms == 0) ? a->consumed : 2 * a->consumed;
@@ -211,6 +220,7 @@ int gsdr_acq_create(int device, const gsdr_acq_conf* conf, gsdr_acq** out)
     const size_t tw_n = std::max<size_t>(N, a->tw_entries);
     if (e == hipSuccess) e = hipMalloc(&a->d_tw, tw_n * sizeof(float2));
     if (e == hipSuccess) e = hipMalloc(&a->d_wipe, (size_t)a->D * N * sizeof(float2));
+    a->d_wipe_grid = a->d_wipe;
     if (e == hipSuccess) e = hipMalloc(&a->d_code_fft, nP * N * sizeof(float2));
     if (e == hipSuccess) e = hipMalloc(&a->d_code_stage, nP * a->consumed * sizeof(float2));
     if (e == hipSuccess) e = hipMalloc(&a->d_prn, nP * sizeof(uint32_t));
@@ -361,6 +371,25 @@ int gsdr_acq_set_doppler(gsdr_acq* a, int32_t doppler_max, uint32_t doppler_step
     return GSDR_OK;
 }
 
+int gsdr_acq_set_wipeoff(gsdr_acq* a, int mode)
+{
+    GSDR_REQUIRE(a, GSDR_E_ARG, "gsdr_acq_set_wipeoff: null handle");
+    GSDR_REQUIRE(mode == GSDR_WIPE_EXACT || mode == GSDR_WIPE_GENERIC || mode == GSDR_WIPE_AVX2, GSDR_E_ARG,
+        "gsdr_acq_set_wipeoff: unknown mode %d", mode);
+    std::lock_guard<std::mutex> lk(a->mu);
+    gsdr::DeviceGuard g(a->device);
+    a->wipe_mode = mode;
+    return rebuild_wipeoffs(a);
+}
+
+int gsdr_acq_get_spectrum_reuse(const gsdr_acq* a, uint32_t* q, uint32_t* p)
+{
+    GSDR_REQUIRE(a, GSDR_E_ARG, "gsdr_acq_get_spectrum_reuse: null handle");
+    if (q) *q = a->xm_grid.q;
+    if (p) *p = a->xm_grid.p;
+    return GSDR_OK;
+}
+
 int gsdr_acq_set_threshold(gsdr_acq* a, float threshold)
 {
     GSDR_REQUIRE(a, GSDR_E_ARG, "gsdr_acq_set_threshold: null handle");
@@ -470,8 +499,10 @@ int gsdr_acq_dump_spectra(gsdr_acq* a, const void* iq_host, float* spectra_host)
         hipMemcpyHostToDevice, a->stream));
     int rc = dispatch(a, 2, nullptr, 1, 0, 0, nullptr, a->stream, 0);
     if (rc != GSDR_OK) return rc;
-    GSDR_HIP(hipMemcpyAsync(spectra_host, a->d_X, (size_t)a->D * a->N * sizeof(float2), hipMemcpyDeviceToHost,
-        a->stream));
+    // row d of block 0 wherever the layout keeps it (XMap: a window of a shared spectrum)
+    for (uint32_t d = 0; d < a->D; ++d)
+        GSDR_HIP(hipMemcpyAsync(spectra_host + (size_t)d * a->N * 2, a->d_X + a->xm.off(0, d),
+            (size_t)a->N * sizeof(float2), hipMemcpyDeviceToHost, a->stream));
     GSDR_HIP(hipStreamSynchronize(a->stream));
     return GSDR_OK;
 }
@@ -516,7 +547,7 @@ int gsdr_acq_dump_grid_step_two(gsdr_acq* a, const void* iq_host, uint32_t prn_s
         hipMemcpyHostToDevice, a->stream));
     GSDR_HIP(hipMemcpyAsync(a->st2.d_freq, freqs.data(), nb * sizeof(float), hipMemcpyHostToDevice, a->stream));
     hipLaunchKernelGGL(acq_wipeoff_kernel, dim3(nb), dim3(256), 0, a->stream, a->st2.d_wipe, a->N,
-        (float)a->conf.fs_in, 0, 0, 0, 0, (const float*)a->st2.d_freq);
+        (float)a->conf.fs_in, 0, 0, 0, 0, (const float*)a->st2.d_freq, a->wipe_mode);
     GSDR_HIP(hipGetLastError());
     // the grid dump on a one-PRN view with the narrow Doppler rows
     const uint32_t D0 = a->D, P0 = a->nprn;
@@ -598,7 +629,7 @@ int gsdr_acq_run_step_two(gsdr_acq* a, const void* iq_host, uint32_t nsel, const
     GSDR_HIP(hipMemcpyAsync(a->st2.d_freq, freqs.data(), freqs.size() * sizeof(float), hipMemcpyHostToDevice,
         a->stream));
     hipLaunchKernelGGL(acq_wipeoff_kernel, dim3(nsel * nb), dim3(256), 0, a->stream, a->st2.d_wipe, a->N,
-        (float)a->conf.fs_in, 0, 0, 0, 0, (const float*)a->st2.d_freq);
+        (float)a->conf.fs_in, 0, 0, 0, 0, (const float*)a->st2.d_freq, a->wipe_mode);
     GSDR_HIP(hipGetLastError());
     // one narrow grid per PRN (each has its own centre): the engine's launches on a
     // one-PRN view of the handle

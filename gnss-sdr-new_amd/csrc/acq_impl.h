@@ -57,8 +57,31 @@ struct RowStat
     uint32_t pad;
 };
 
+// Where the forward spectrum of (block-dwell bk, Doppler d) lives in d_X.  Doppler
+// bins commensurate with the FFT bin spacing (doppler_step * N / fs = p / q in
+// lowest terms, q <= D / 2) with the exact carrier (GSDR_WIPE_EXACT) make
+// X_d[k] = X_{d mod q}[k + (d / q) p] an exact identity: the wipe-off of Doppler
+// f + a q step is the one of f times exp(-j 2 pi a p n / N), a circular shift of
+// the spectrum by a p bins.  The forward pass then computes only q spectra per
+// block-dwell, each stored with its first E = ((D - 1) / q) p bins repeated after
+// bin N - 1 (stride N + E), and every Doppler row is a window into one of them --
+// no wrap arithmetic in the readers.  q = D, p = 0, stride = N is the plain layout
+// (one spectrum per Doppler bin).
+struct XMap
+{
+    uint32_t q;       // stored spectra per block-dwell
+    uint32_t p;       // bin shift per class step
+    uint32_t stride;  // complex elements per stored spectrum (N + E)
+    __host__ __device__ __forceinline__ size_t off(uint32_t bk, uint32_t d) const
+    {
+        const uint32_t a = d / q, c = d - a * q;
+        return ((size_t)bk * q + c) * stride + (size_t)a * p;
+    }
+};
+
 struct AcqParams
 {
+    XMap xm;             // forward-spectrum layout (see XMap)
     uint32_t N;          // fft size
     uint32_t consumed;   // valid samples per block
     uint32_t lead_zeros; // zero samples placed before the code (sampled_ms != ms_per_code)
@@ -156,22 +179,117 @@ __device__ __forceinline__ void block_reduce_stat(float& m, uint32_t& idx, float
 }
 
 // ---------------------------------------------------------------- K_wipe
-// One workgroup per Doppler bin.  Lane 0 replays the generic sincos phase
-// accumulation (KERN/s32f_sincos_32fc.h:390-403) sequentially in fp32; the
-// workgroup then evaluates cos/sin in parallel.
+// One workgroup per Doppler bin; the carrier model (GSDR_WIPE_*, gsdr.h):
+//   EXACT   exp(-j 2 pi f n / fs) with the phase f n / fs reduced mod 1 in fp64 and
+//           cos / sin in fp64, rounded once to fp32 (the default);
+//   GENERIC the generic sincos protokernel (KERN/s32f_sincos_32fc.h:390-403): lane 0
+//           replays the fp32 phase accumulation sequentially, the workgroup then
+//           evaluates cosf / sinf in parallel;
+//   AVX2    the a_avx2 protokernel (:448-627) the reference dispatches on AVX2 x86-64:
+//           lanes 0..7 replay the eight fp32 accumulators (start phase + k inc, step
+//           8 inc), the workgroup evaluates the Cephes polynomials in the kernel's fp32
+//           operation order (no contraction), the N % 8 tail with cosf / sinf.
+__device__ __forceinline__ float2 cephes_sincos_avx2(float x0)
+{
+    const float FOPI = 1.27323954473516f;
+    const float DP1 = -0.78515625f, DP2 = -2.4187564849853515625e-4f, DP3 = -3.77489497744594108e-8f;
+    const float C0 = 2.443315711809948E-005f, C1 = -1.388731625493765E-003f, C2 = 4.166664568298827E-002f;
+    const float S0 = -1.9515295891E-4f, S1 = 8.3321608736E-3f, S2 = -1.6666654611E-1f;
+    const uint32_t bits = __float_as_uint(x0);
+    bool sign_sin = (bits >> 31) != 0;
+    float x = __uint_as_float(bits & 0x7fffffffu);
+    float y = __fmul_rn(x, FOPI);
+    int32_t j = (int32_t)y;  // cvttps: truncation
+    j = (j + 1) & ~1;
+    y = (float)j;
+    const bool swap = (j & 4) != 0;
+    const bool poly = (j & 2) == 0;
+    x = __fadd_rn(x, __fmul_rn(y, DP1));
+    x = __fadd_rn(x, __fmul_rn(y, DP2));
+    x = __fadd_rn(x, __fmul_rn(y, DP3));
+    const bool sign_cos = ((~(j - 2)) & 4) != 0;
+    sign_sin = sign_sin != swap;
+    const float z = __fmul_rn(x, x);
+    float yc = __fmul_rn(C0, z);
+    yc = __fadd_rn(yc, C1);
+    yc = __fmul_rn(yc, z);
+    yc = __fadd_rn(yc, C2);
+    yc = __fmul_rn(yc, z);
+    yc = __fmul_rn(yc, z);
+    yc = __fsub_rn(yc, __fmul_rn(z, 0.5f));
+    yc = __fadd_rn(yc, 1.0f);
+    float ys = __fmul_rn(S0, z);
+    ys = __fadd_rn(ys, S1);
+    ys = __fmul_rn(ys, z);
+    ys = __fadd_rn(ys, S2);
+    ys = __fmul_rn(ys, z);
+    ys = __fmul_rn(ys, x);
+    ys = __fadd_rn(ys, x);
+    const float sv = poly ? ys : yc, cv = poly ? yc : ys;
+    return make_float2(sign_cos ? -cv : cv, sign_sin ? -sv : sv);
+}
+
 __global__ void __launch_bounds__(256) acq_wipeoff_kernel(float2* __restrict__ wipe, uint32_t N, float fs,
     int32_t doppler_max, int32_t doppler_center, int32_t doppler_step, int32_t doppler_bias,
-    const float* __restrict__ freqs)
+    const float* __restrict__ freqs, int mode)
 {
     const uint32_t d = blockIdx.x;
     float2* row = wipe + (size_t)d * N;
+    // freqs: the step-two grid (update_grid_doppler_wipeoffs_step2, :307-314)
+    const int32_t doppler = -doppler_max + doppler_center + doppler_step * (int32_t)d;
+    const float freq = freqs ? freqs[d] : (float)(doppler_bias + doppler);
+    if (mode == GSDR_WIPE_EXACT)
+        {
+            for (uint32_t i = threadIdx.x; i < N; i += blockDim.x)
+                {
+                    const double t = (double)freq * (double)i / (double)fs;
+                    double s, c;
+                    sincos(-6.283185307179586 * (t - floor(t)), &s, &c);
+                    row[i] = make_float2((float)c, (float)s);
+                }
+            return;
+        }
+    const float phase_step = __fdiv_rn(__fmul_rn(6.283185307179586f, freq), fs);
+    const float inc = -phase_step;
+    if (mode == GSDR_WIPE_AVX2)
+        {
+            const uint32_t iters = N / 8;
+            if (threadIdx.x < 8)
+                {
+                    const uint32_t k = threadIdx.x;
+                    float ph = k == 0 ? 0.0f : __fmul_rn((float)k, inc);
+                    const float inc8 = __fmul_rn(8.0f, inc);
+                    for (uint32_t it = 0; it < iters; ++it)
+                        {
+                            row[8 * it + k].x = ph;
+                            ph = __fadd_rn(ph, inc8);
+                        }
+                }
+            else if (threadIdx.x == 8)
+                {
+                    float ph = __fmul_rn(inc, (float)(iters * 8));
+                    for (uint32_t i = iters * 8; i < N; ++i)
+                        {
+                            row[i].x = ph;
+                            ph = __fadd_rn(ph, inc);
+                        }
+                }
+            __syncthreads();
+            for (uint32_t i = threadIdx.x; i < N; i += blockDim.x)
+                {
+                    if (i < iters * 8)
+                        row[i] = cephes_sincos_avx2(row[i].x);
+                    else
+                        {
+                            float s, c;
+                            sincosf(row[i].x, &s, &c);
+                            row[i] = make_float2(c, s);
+                        }
+                }
+            return;
+        }
     if (threadIdx.x == 0)
         {
-            // freqs: the step-two grid (update_grid_doppler_wipeoffs_step2, :307-314)
-            const int32_t doppler = -doppler_max + doppler_center + doppler_step * (int32_t)d;
-            const float freq = freqs ? freqs[d] : (float)(doppler_bias + doppler);
-            const float phase_step = __fdiv_rn(__fmul_rn(6.283185307179586f, freq), fs);
-            const float inc = -phase_step;
             float ph = 0.0f;
             for (uint32_t i = 0; i < N; ++i)
                 {
@@ -213,21 +331,26 @@ __global__ void __launch_bounds__(PT::NT) acq_code_fft_kernel(const float2* __re
 template <class PT, int IT>
 __global__ void __launch_bounds__(PT::NT) acq_forward_kernel(const void* __restrict__ iq, uint64_t block_stride,
     const float2* __restrict__ wipe, float2* __restrict__ X, const float2* __restrict__ tw, typename PT::PlanT plan,
-    uint32_t consumed, uint32_t D)
+    uint32_t consumed, XMap xm)
 {
     extern __shared__ float2 lds[];
-    // blockIdx.x = block, blockIdx.y = Doppler bin: the workgroups of one wipe-off
-    // row w_d are consecutive, so each XCD's L2 fetches the row once per launch
-    // (with d fastest every row was re-read from HBM for every block)
+    // blockIdx.x = block, blockIdx.y = Doppler bin (of the xm.q stored spectra):
+    // the workgroups of one wipe-off row w_d are consecutive, so each XCD's L2
+    // fetches the row once per launch (with d fastest every row was re-read from
+    // HBM for every block)
     const uint32_t b = blockIdx.x, d = blockIdx.y;
     const size_t base = (size_t)b * block_stride;
     const float2* w = wipe + (size_t)d * plan.n;
-    float2* out = X + ((size_t)b * D + d) * plan.n;
+    float2* out = X + xm.off(b, d);
+    const int ext = (int)(xm.stride - plan.n);  // bins repeated after N - 1 (XMap)
     auto load = [&](int i) -> float2 {
         if (i >= (int)consumed) return make_float2(0.f, 0.f);
         return gsdr::fft::cmul(load_item<IT>(iq, base + i), w[i]);
     };
-    auto store = [&](int i, float2 v) { out[i] = v; };
+    auto store = [&](int i, float2 v) {
+        out[i] = v;
+        if (i < ext) out[plan.n + i] = v;
+    };
     PT::run(plan, lds, tw, load, store);
 }
 
@@ -282,7 +405,7 @@ __global__ void __launch_bounds__(256) acq_forward4_cols_kernel(const void* __re
 
 template <class PT>
 __global__ void __launch_bounds__(PT::NT) acq_forward4_rows_kernel(const float2* __restrict__ scratch,
-    float2* __restrict__ X, const float2* __restrict__ tw_sub, uint32_t nrows)
+    float2* __restrict__ X, const float2* __restrict__ tw_sub, uint32_t nrows, uint32_t xstride)
 {
     using gsdr::pk::c2;
     using SP = typename PT::SubPlan;
@@ -304,9 +427,16 @@ __global__ void __launch_bounds__(PT::NT) acq_forward4_rows_kernel(const float2*
             k1 = t - (t / R) * R;
         }
     const c2* rk = reinterpret_cast<const c2*>(scratch) + (size_t)row * N + (size_t)k1 * N2;
-    float2* out = X + (size_t)row * N;
+    // stored spectrum `row` (= b q + d of XMap, d < q) with its E = xstride - N
+    // repeated leading bins
+    float2* out = X + (size_t)row * xstride;
+    const int ext = (int)(xstride - (uint32_t)N);
     auto ld = [&](int, int, int i) -> c2 { return rk[i]; };
-    auto st = [&](int k2, c2 v, int) { out[k1 + R * k2] = gsdr::pk::to(v); };
+    auto st = [&](int k2, c2 v, int) {
+        const int k = (int)k1 + R * k2;
+        out[k] = gsdr::pk::to(v);
+        if (k < ext) out[N + k] = gsdr::pk::to(v);
+    };
     SP::template run<false>(reinterpret_cast<c2*>(lds_raw), tw_sub, ld, st, [] {});
 }
 
@@ -316,7 +446,7 @@ __global__ void __launch_bounds__(PT::NT) acq_forward4_rows_kernel(const float2*
 template <class PT, bool GRID>
 __global__ void __launch_bounds__(PT::NT) acq_correlate_kernel(const float2* __restrict__ X,
     const float2* __restrict__ code_fft, RowStat* __restrict__ stats, float* __restrict__ grid,
-    const float2* __restrict__ tw, typename PT::PlanT plan, uint32_t D, uint32_t P, uint32_t prn_slot_for_grid)
+    const float2* __restrict__ tw, typename PT::PlanT plan, uint32_t D, uint32_t P, uint32_t prn_slot_for_grid, XMap xm)
 {
     extern __shared__ float2 lds[];
     RowStat* scratch = reinterpret_cast<RowStat*>(lds + gsdr::fft::lds_elems_dev(plan));
@@ -353,7 +483,7 @@ __global__ void __launch_bounds__(PT::NT) acq_correlate_kernel(const float2* __r
             b = row / D;
             d = row - b * D;
         }
-    const float2* x = X + ((size_t)b * D + d) * N;
+    const float2* x = X + xm.off(b, d);
     const float2* c = code_fft + (size_t)p * N;
     float best = -1.0f, sum = 0.0f;
     uint32_t bidx = 0xffffffffu;
@@ -407,7 +537,7 @@ constexpr int pg_count(int pg) { return pg < 0 ? -pg : pg; }
 template <class MP, int PG_, int WPE, int STAT>
 __global__ void __launch_bounds__(MP::NT) __attribute__((amdgpu_waves_per_eu(WPE))) acq_correlate_pk_kernel(const float2* __restrict__ X,
     const float2* __restrict__ code_fft, RowStat* __restrict__ stats, const float2* __restrict__ tw, uint32_t D,
-    uint32_t P, uint32_t nblocks)
+    uint32_t P, uint32_t nblocks, XMap xm)
 {
     constexpr int PG = pg_count(PG_);
     constexpr bool PREFETCH = PG_ > 0;
@@ -444,7 +574,7 @@ __global__ void __launch_bounds__(MP::NT) __attribute__((amdgpu_waves_per_eu(WPE
     // wave-uniform values: per-lane byte offset j*8 in voffset, r*NB1*8 as the
     // scalar/immediate offset -- no 64-bit address arithmetic per load
     const auto xrs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float2*>(X) + (size_t)row * N, 0, (int)(N * sizeof(c2)), 0x00020000);
+        const_cast<float2*>(X) + xm.off(b, d), 0, (int)(N * sizeof(c2)), 0x00020000);
     const auto crs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float2*>(code_fft) + (size_t)p0 * N, 0, (int)((size_t)np * N * sizeof(c2)), 0x00020000);
     auto bload = [](decltype(xrs) rs, int voff, int soff) -> c2 {
@@ -825,7 +955,7 @@ struct RegFourStep
 template <class RP>
 __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(RP::WPE))) acq_correlate_reg_kernel(const float2* __restrict__ X,
     const float2* __restrict__ code_fft, RowStat* __restrict__ stats, const float2* __restrict__ tw, uint32_t D,
-    uint32_t P, uint32_t nblocks)
+    uint32_t P, uint32_t nblocks, XMap xm)
 {
     using gsdr::pk::c2;
     constexpr int R = RP::R, NT = RP::NT, L = RP::L, CPL = RP::CPL;
@@ -864,7 +994,7 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(RP:
         }
     const uint32_t b = row / D, d = row - (row / D) * D;
     const auto xrs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float2*>(X) + (size_t)row * N, 0, (int)(N * sizeof(c2)), 0x00020000);
+        const_cast<float2*>(X) + xm.off(b, d), 0, (int)(N * sizeof(c2)), 0x00020000);
     const auto crs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float2*>(code_fft) + (size_t)p * N, 0, (int)(N * sizeof(c2)), 0x00020000);
     auto bload = [](decltype(xrs) rs, int voff, int soff) -> c2 {
@@ -936,7 +1066,7 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(RP:
 template <int ROUT, class RP, bool HALF, int ABL = 0>
 __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(RP::WPE))) acq_correlate_split_kernel(
     const float2* __restrict__ X, const float2* __restrict__ code_fft, RowStat* __restrict__ stats,
-    const float2* __restrict__ tw, uint32_t D, uint32_t P, uint32_t nblocks, uint32_t pgs)
+    const float2* __restrict__ tw, uint32_t D, uint32_t P, uint32_t nblocks, uint32_t pgs, XMap xm)
 {
     using gsdr::pk::c2;
     constexpr int R = RP::R, NT = RP::NT, L = RP::L, CPL = RP::CPL;
@@ -970,7 +1100,7 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(RP:
     const uint32_t p = pv / ROUT, q = pv - p * ROUT;
     const uint32_t b = row / D, d = row - (row / D) * D;
     const auto xrs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float2*>(X) + (size_t)row * N, 0, (int)(N * sizeof(c2)), 0x00020000);
+        const_cast<float2*>(X) + xm.off(b, d), 0, (int)(N * sizeof(c2)), 0x00020000);
     const auto crs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float2*>(code_fft) + (size_t)p * N, 0, (int)(N * sizeof(c2)), 0x00020000);
     auto bload = [](decltype(xrs) rs, int voff, int soff) -> c2 {
@@ -1136,7 +1266,7 @@ __global__ void __launch_bounds__(PT::NT) acq_argmax_four_kernel(const float2* _
         const unsigned long long k = ((unsigned long long)__float_as_uint(m) << 32) | (0xffffffffu - (uint32_t)j);
         key = k > key ? k : key;
     };
-    PT::run(plan, lds, tw, row_load(X + ((size_t)b * ap.D + d) * N), store);
+    PT::run(plan, lds, tw, row_load(X + ap.xm.off(b, d)), store);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1)
         {
@@ -1154,7 +1284,7 @@ __global__ void __launch_bounds__(PT::NT) acq_argmax_four_kernel(const float2* _
     if (ap.cfar && !ap.step_two)
         {
             const uint32_t opp = (d + ap.D / 2) % ap.D;
-            const float2* xo = X + ((size_t)b * ap.D + opp) * N;
+            const float2* xo = X + ap.xm.off(b, opp);
             float acc = 0.0f;
             if (off == 0)
                 {
@@ -1224,7 +1354,7 @@ __global__ void __launch_bounds__(MP::NT) acq_argmax_pk_kernel(const float2* __r
     const uint32_t b = bp / P, p = bp - b * P;
     const uint32_t d = res[bp].doppler_index;
     if (d >= D) return;  // uniform: no maximum found (an all-NaN grid)
-    const c2* x = reinterpret_cast<const c2*>(X) + ((size_t)b * D + d) * N;
+    const c2* x = reinterpret_cast<const c2*>(X) + ap.xm.off(b, d);
     const c2* c = reinterpret_cast<const c2*>(code_fft) + (size_t)p * N;
     unsigned long long key = 0ull;
     auto load = [&](int, int, int i) -> c2 { return gsdr::pk::conj_mul(x[i], c[i]); };
@@ -1256,7 +1386,7 @@ __global__ void __launch_bounds__(MP::NT) acq_argmax_pk_kernel(const float2* __r
             // by Parseval: accumulate(|R|^2) / fft_size = sum_k |X_opp[k]|^2 |C[k]|^2
             if (!ap.cfar || ap.step_two) return;
             const uint32_t opp = (d + D / 2) % D;
-            const c2* xo = reinterpret_cast<const c2*>(X) + ((size_t)b * D + opp) * N;
+            const c2* xo = reinterpret_cast<const c2*>(X) + ap.xm.off(b, opp);
             float acc = 0.0f;
             for (uint32_t i = threadIdx.x; i < N; i += NT)
                 {
@@ -1383,7 +1513,7 @@ __global__ void __launch_bounds__(PT::NT) acq_correlate_dwell_kernel(const float
     const float2* c = code_fft + (size_t)p * N;
     for (uint32_t k = 0; k < K; ++k)
         {
-            const float2* x = X + ((size_t)(b * K + k) * ap.D + d) * N;
+            const float2* x = X + ap.xm.off(b * K + k, d);
             float best = -1.0f, sum = 0.0f;
             uint32_t bidx = 0xffffffffu;
             auto load = [&](int i) -> float2 {
@@ -1516,7 +1646,7 @@ __global__ void __launch_bounds__(PT::NT) acq_second_peak_dwell_kernel(const flo
     uint32_t bidx = 0;
     for (uint32_t k = 0; k <= kk; ++k)
         {
-            const float2* x = X + ((size_t)(b * K + k) * ap.D + d) * N;
+            const float2* x = X + ap.xm.off(b * K + k, d);
             const bool last = k == kk;
             auto load = [&](int i) -> float2 {
                 float2 a = x[i], q = c[i];
@@ -1584,7 +1714,7 @@ __global__ void __launch_bounds__(PT::NT) acq_dwell_grid_kernel(const float2* __
     const uint32_t N = plan.n;
     const uint32_t d = blockIdx.x / ap.P, p = blockIdx.x - d * ap.P;
     float* row = grid + ((size_t)p * ap.D + d) * ap.eff;
-    const float2* x = X + (size_t)d * N;
+    const float2* x = X + ap.xm.off(0, d);
     const float2* c = code_fft + (size_t)p * N;
     float best = -1.0f, sum = 0.0f;
     uint32_t bidx = 0xffffffffu;
@@ -1658,7 +1788,7 @@ __global__ void __launch_bounds__(256) acq_grid_second_peak_kernel(const float* 
 // acq_forward_kernel.
 template <class MP, int IT>
 __global__ void __launch_bounds__(MP::NT) acq_forward_pk_kernel(const void* __restrict__ iq, uint64_t block_stride,
-    const float2* __restrict__ wipe, float2* __restrict__ X, const float2* __restrict__ tw, uint32_t consumed, uint32_t D)
+    const float2* __restrict__ wipe, float2* __restrict__ X, const float2* __restrict__ tw, uint32_t consumed, XMap xm)
 {
     using gsdr::pk::c2;
     extern __shared__ float2 lds_raw[];
@@ -1667,12 +1797,16 @@ __global__ void __launch_bounds__(MP::NT) acq_forward_pk_kernel(const void* __re
     constexpr uint32_t N = MP::N;
     const size_t base = (size_t)b * block_stride;
     const c2* w = reinterpret_cast<const c2*>(wipe) + (size_t)d * N;
-    c2* out = reinterpret_cast<c2*>(X) + ((size_t)b * D + d) * N;
+    c2* out = reinterpret_cast<c2*>(X) + xm.off(b, d);
+    const int ext = (int)(xm.stride - N);  // bins repeated after N - 1 (XMap)
     auto load = [&](int, int, int i) -> c2 {
         if (i >= (int)consumed) return c2{0.f, 0.f};
         return gsdr::pk::mul(gsdr::pk::from(load_item<IT>(iq, base + i)), w[i]);
     };
-    auto store = [&](int i, c2 v, int) { out[i] = v; };
+    auto store = [&](int i, c2 v, int) {
+        out[i] = v;
+        if (i < ext) out[N + i] = v;
+    };
     MP::run(lds, tw, load, store, [] {});
 }
 
@@ -1762,7 +1896,7 @@ __global__ void __launch_bounds__(PT::NT) acq_second_peak_kernel(const float2* _
         e1 = (int32_t)N + e1;
     else if (e2 >= (int32_t)N)
         e2 = e2 - (int32_t)N;
-    const float2* x = X + ((size_t)b * ap.D + d) * N;
+    const float2* x = X + ap.xm.off(b, d);
     const float2* c = code_fft + (size_t)p * N;
     float best = 0.0f, sum = 0.0f;
     uint32_t bidx = 0;
@@ -1813,7 +1947,7 @@ __global__ void __launch_bounds__(PT::NT) acq_argmax_second_four_kernel(const fl
     const uint32_t N = ap.N;
     const uint32_t d = res[bp].doppler_index;
     if (d >= ap.D) return;  // uniform: no maximum found (an all-NaN grid)
-    const float2* x = X + ((size_t)b * ap.D + d) * N;
+    const float2* x = X + ap.xm.off(b, d);
     const float2* c = code_fft + (size_t)p * N;
     const int off = (int)ap.out_off;
     const uint32_t eff = N - (uint32_t)off;
@@ -1900,6 +2034,9 @@ struct gsdr_acq
     gsdr_acq_conf conf{};
     uint32_t N{0}, D{0}, consumed{0}, lead{0};
     uint32_t K{1};       // max_dwells
+    int wipe_mode{GSDR_WIPE_EXACT};  // carrier model of the Doppler grid (gsdr_acq_set_wipeoff)
+    XMap xm_grid{};      // forward-spectrum layout of the main Doppler grid (rebuild_wipeoffs)
+    XMap xm{};           // the layout of the launches being issued (set by dispatch)
     uint32_t eff{0};     // effective FFT size (outputs [N - eff, N))
     bool general{false}; // dwells > 1 or bit transition: the general kernels
     gsdr_acq_result* d_resk{nullptr};  // per-dwell results (general path)
@@ -1922,6 +2059,7 @@ struct gsdr_acq
     hipStream_t stream{nullptr};
     float2* d_tw{nullptr};
     float2* d_wipe{nullptr};
+    float2* d_wipe_grid{nullptr};  // the main grid's wipe-off rows (d_wipe points elsewhere during step two)
     float2* d_code_fft{nullptr};
     float2* d_code_stage{nullptr};
     uint32_t* d_prn{nullptr};
@@ -2035,6 +2173,7 @@ int set_lds_attrs(size_t bytes)
 AcqParams params_of(const gsdr_acq* a)
 {
     AcqParams ap{};
+    ap.xm = a->xm;
     ap.N = a->N;
     ap.consumed = a->consumed;
     ap.lead_zeros = a->lead;
@@ -2063,11 +2202,42 @@ AcqParams params_of(const gsdr_acq* a)
     return ap;
 }
 
+// The forward-spectrum reuse of the main grid (XMap): with the exact carrier and
+// doppler_step * N / fs = p / q in lowest terms, q <= D / 2, the q spectra of
+// Doppler bins 0..q-1 (each extended by E = ((D - 1) / q) p bins) hold every row;
+// else the plain layout.  GSDR_ACQ_XSHIFT=0 keeps the plain layout.
+XMap grid_xmap(const gsdr_acq* a)
+{
+    XMap plain{a->D, 0u, a->N};
+    if (a->wipe_mode != GSDR_WIPE_EXACT) return plain;
+    if (const char* e = std::getenv("GSDR_ACQ_XSHIFT"))
+        if (std::atoi(e) == 0) return plain;
+    const int64_t fs = a->conf.fs_in;
+    if (fs <= 0) return plain;
+    int64_t num = (int64_t)a->conf.doppler_step * (int64_t)a->N, den = fs;
+    int64_t g0 = num, g1 = den;
+    while (g1)  // gcd
+        {
+            const int64_t t = g0 % g1;
+            g0 = g1;
+            g1 = t;
+        }
+    if (g0 <= 0) return plain;
+    const int64_t p = num / g0, q = den / g0;
+    if (q < 1 || 2 * q > (int64_t)a->D) return plain;
+    const int64_t ext = ((int64_t)(a->D - 1) / q) * p;
+    // the stored spectra must fit the plain layout's allocation
+    if (q * ((int64_t)a->N + ext) > (int64_t)a->D * (int64_t)a->N) return plain;
+    return XMap{(uint32_t)q, (uint32_t)p, (uint32_t)(a->N + ext)};
+}
+
 int rebuild_wipeoffs(gsdr_acq* a)
 {
-    hipLaunchKernelGGL(acq_wipeoff_kernel, dim3(a->D), dim3(256), 0, a->stream, a->d_wipe, a->N,
+    a->xm_grid = grid_xmap(a);
+    // rows 0..q-1 suffice with the reuse (the other rows would be their shifts)
+    hipLaunchKernelGGL(acq_wipeoff_kernel, dim3(a->xm_grid.q), dim3(256), 0, a->stream, a->d_wipe, a->N,
         (float)a->conf.fs_in, a->conf.doppler_max, a->conf.doppler_center, (int32_t)a->conf.doppler_step,
-        a->conf.doppler_bias, (const float*)nullptr);
+        a->conf.doppler_bias, (const float*)nullptr, a->wipe_mode);
     GSDR_HIP(hipGetLastError());
     GSDR_HIP(hipStreamSynchronize(a->stream));
     return GSDR_OK;
@@ -2170,33 +2340,34 @@ template <class PT>
 void launch_forward(gsdr_acq* a, const void* iq, int item_type, uint32_t nblocks, uint64_t stride, hipStream_t s)
 {
     if (item_type == GSDR_ITEM_GR_COMPLEX)
-        hipLaunchKernelGGL((acq_forward_kernel<PT, GSDR_ITEM_GR_COMPLEX>), dim3(nblocks, a->D), dim3(PT::NT),
-            a->lds_bytes, s, iq, stride, a->d_wipe, a->d_X, a->d_tw, plan_of<PT>(a), a->consumed, a->D);
+        hipLaunchKernelGGL((acq_forward_kernel<PT, GSDR_ITEM_GR_COMPLEX>), dim3(nblocks, a->xm.q), dim3(PT::NT),
+            a->lds_bytes, s, iq, stride, a->d_wipe, a->d_X, a->d_tw, plan_of<PT>(a), a->consumed, a->xm);
     else if (item_type == GSDR_ITEM_CSHORT)
-        hipLaunchKernelGGL((acq_forward_kernel<PT, GSDR_ITEM_CSHORT>), dim3(nblocks, a->D), dim3(PT::NT),
-            a->lds_bytes, s, iq, stride, a->d_wipe, a->d_X, a->d_tw, plan_of<PT>(a), a->consumed, a->D);
+        hipLaunchKernelGGL((acq_forward_kernel<PT, GSDR_ITEM_CSHORT>), dim3(nblocks, a->xm.q), dim3(PT::NT),
+            a->lds_bytes, s, iq, stride, a->d_wipe, a->d_X, a->d_tw, plan_of<PT>(a), a->consumed, a->xm);
     else
-        hipLaunchKernelGGL((acq_forward_kernel<PT, GSDR_ITEM_IBYTE>), dim3(nblocks, a->D), dim3(PT::NT),
-            a->lds_bytes, s, iq, stride, a->d_wipe, a->d_X, a->d_tw, plan_of<PT>(a), a->consumed, a->D);
+        hipLaunchKernelGGL((acq_forward_kernel<PT, GSDR_ITEM_IBYTE>), dim3(nblocks, a->xm.q), dim3(PT::NT),
+            a->lds_bytes, s, iq, stride, a->d_wipe, a->d_X, a->d_tw, plan_of<PT>(a), a->consumed, a->xm);
 }
 
 // The two-launch forward (acq_forward4_cols_kernel + acq_forward4_rows_kernel).
 template <class PT>
 void launch_forward_two(gsdr_acq* a, const void* iq, int item_type, uint32_t nblocks, uint64_t stride, hipStream_t s)
 {
-    const uint32_t nrows = nblocks * a->D;
+    // the xm.q stored spectra per block (XMap): rows b * q + d, d < q
+    const uint32_t nrows = nblocks * a->xm.q;
     const dim3 cg((PT::N2 + 255) / 256, nrows);
     if (item_type == GSDR_ITEM_GR_COMPLEX)
         hipLaunchKernelGGL((acq_forward4_cols_kernel<PT, GSDR_ITEM_GR_COMPLEX>), cg, dim3(256), 0, s, iq, stride,
-            a->d_wipe, a->d_fscratch, a->d_tw, a->consumed, a->D);
+            a->d_wipe, a->d_fscratch, a->d_tw, a->consumed, a->xm.q);
     else if (item_type == GSDR_ITEM_CSHORT)
         hipLaunchKernelGGL((acq_forward4_cols_kernel<PT, GSDR_ITEM_CSHORT>), cg, dim3(256), 0, s, iq, stride,
-            a->d_wipe, a->d_fscratch, a->d_tw, a->consumed, a->D);
+            a->d_wipe, a->d_fscratch, a->d_tw, a->consumed, a->xm.q);
     else
         hipLaunchKernelGGL((acq_forward4_cols_kernel<PT, GSDR_ITEM_IBYTE>), cg, dim3(256), 0, s, iq, stride,
-            a->d_wipe, a->d_fscratch, a->d_tw, a->consumed, a->D);
+            a->d_wipe, a->d_fscratch, a->d_tw, a->consumed, a->xm.q);
     hipLaunchKernelGGL((acq_forward4_rows_kernel<PT>), dim3(nrows * PT::R), dim3(PT::NT), PT::SubPlan::lds_bytes(), s,
-        a->d_fscratch, a->d_X, a->d_tw_sub, nrows);
+        a->d_fscratch, a->d_X, a->d_tw_sub, nrows, a->xm.stride);
 }
 
 // General path (max_dwells > 1 and/or bit_transition_flag): forward spectra of
@@ -2323,7 +2494,7 @@ int launch_all(gsdr_acq* a, const void* iq, int item_type, uint32_t nblocks, uin
     else
         {
             hipLaunchKernelGGL((acq_correlate_kernel<PT, false>), dim3(a->D * a->nprn, nblocks), dim3(PT::NT), lds, s,
-                a->d_X, a->d_code_fft, a->d_stats, (float*)nullptr, a->d_tw, plan_of<PT>(a), a->D, a->nprn, 0u);
+                a->d_X, a->d_code_fft, a->d_stats, (float*)nullptr, a->d_tw, plan_of<PT>(a), a->D, a->nprn, 0u, a->xm);
         }
     GSDR_HIP(hipGetLastError());
     t.end(1);
@@ -2390,7 +2561,7 @@ int launch_dump(gsdr_acq* a, bool grid, uint32_t prn_slot)
     if (grid)
         {
             hipLaunchKernelGGL((acq_correlate_kernel<PT, true>), dim3(a->D, 1), dim3(PT::NT), a->lds_bytes, a->stream,
-                a->d_X, a->d_code_fft, a->d_stats, a->d_grid, a->d_tw, plan_of<PT>(a), a->D, a->nprn, prn_slot);
+                a->d_X, a->d_code_fft, a->d_stats, a->d_grid, a->d_tw, plan_of<PT>(a), a->D, a->nprn, prn_slot, a->xm);
             GSDR_HIP(hipGetLastError());
         }
     return GSDR_OK;

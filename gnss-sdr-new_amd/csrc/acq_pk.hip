@@ -18,7 +18,7 @@ template <class RP>
 int launch_reg(gsdr_acq* a, uint32_t nblocks, hipStream_t s)
 {
     hipLaunchKernelGGL((acq_correlate_reg_kernel<RP>), dim3(nblocks * a->D * a->nprn), dim3(RP::NT), RP::lds_bytes(),
-        s, a->d_X, a->d_code_fft, a->d_stats, a->d_tw, a->D, a->nprn, nblocks);
+        s, a->d_X, a->d_code_fft, a->d_stats, a->d_tw, a->D, a->nprn, nblocks, a->xm);
     return GSDR_OK;
 }
 
@@ -47,7 +47,7 @@ int launch_corr_variant(gsdr_acq* a, uint32_t nblocks, hipStream_t s)
                 GSDR_HIP(hipMemsetAsync(a->d_stats, 0, (size_t)nblocks * a->nprn * a->D * sizeof(RowStat), s)); \
             hipLaunchKernelGGL((acq_correlate_pk_kernel<M, PG, WPE, ST>), dim3(nblocks * a->D * groups),         \
                 dim3(M::NT), a->corr_lds_bytes, s, a->d_X, a->d_code_fft, a->d_stats, a->d_tw, a->D, a->nprn,   \
-                nblocks);                                                                                       \
+                nblocks, a->xm);                                                                                \
             return GSDR_OK;                                                                                     \
         }
 #define GSDR_UNPAREN(...) __VA_ARGS__
@@ -91,14 +91,14 @@ int launch_forward_pk(gsdr_acq* a, const void* iq, int item_type, uint32_t nbloc
         {                                                                                                       \
             using M = GSDR_UNPAREN MP;                                                                          \
             if (item_type == GSDR_ITEM_GR_COMPLEX)                                                              \
-                hipLaunchKernelGGL((acq_forward_pk_kernel<M, GSDR_ITEM_GR_COMPLEX>), dim3(nblocks, a->D),       \
-                    dim3(M::NT), M::lds_bytes(), s, iq, stride, a->d_wipe, a->d_X, a->d_tw, a->consumed, a->D); \
+                hipLaunchKernelGGL((acq_forward_pk_kernel<M, GSDR_ITEM_GR_COMPLEX>), dim3(nblocks, a->xm.q),       \
+                    dim3(M::NT), M::lds_bytes(), s, iq, stride, a->d_wipe, a->d_X, a->d_tw, a->consumed, a->xm); \
             else if (item_type == GSDR_ITEM_CSHORT)                                                             \
-                hipLaunchKernelGGL((acq_forward_pk_kernel<M, GSDR_ITEM_CSHORT>), dim3(nblocks, a->D),           \
-                    dim3(M::NT), M::lds_bytes(), s, iq, stride, a->d_wipe, a->d_X, a->d_tw, a->consumed, a->D); \
+                hipLaunchKernelGGL((acq_forward_pk_kernel<M, GSDR_ITEM_CSHORT>), dim3(nblocks, a->xm.q),           \
+                    dim3(M::NT), M::lds_bytes(), s, iq, stride, a->d_wipe, a->d_X, a->d_tw, a->consumed, a->xm); \
             else                                                                                                \
-                hipLaunchKernelGGL((acq_forward_pk_kernel<M, GSDR_ITEM_IBYTE>), dim3(nblocks, a->D),            \
-                    dim3(M::NT), M::lds_bytes(), s, iq, stride, a->d_wipe, a->d_X, a->d_tw, a->consumed, a->D); \
+                hipLaunchKernelGGL((acq_forward_pk_kernel<M, GSDR_ITEM_IBYTE>), dim3(nblocks, a->xm.q),            \
+                    dim3(M::NT), M::lds_bytes(), s, iq, stride, a->d_wipe, a->d_X, a->d_tw, a->consumed, a->xm); \
             GSDR_HIP(hipGetLastError());                                                                        \
             return GSDR_OK;                                                                                     \
         }

@@ -75,7 +75,7 @@ int launch_one(gsdr_acq* a, uint32_t nblocks, hipStream_t s)
         GSDR_HIP(hipMemsetAsync(a->d_stats, 0, (size_t)nblocks * a->nprn * a->D * sizeof(RowStat), s));
     const uint32_t grid = nblocks * a->D * a->nprn * ROUT;
     hipLaunchKernelGGL((acq_correlate_split_kernel<ROUT, RP, HALF, ABL>), dim3(grid), dim3(RP::NT), RP::lds_bytes(), s,
-        a->d_X, a->d_code_fft, a->d_stats, a->d_tw, a->D, a->nprn, nblocks, prn_group(a->nprn, a->N));
+        a->d_X, a->d_code_fft, a->d_stats, a->d_tw, a->D, a->nprn, nblocks, prn_group(a->nprn, a->N), a->xm);
     GSDR_HIP(hipGetLastError());
     return GSDR_OK;
 }

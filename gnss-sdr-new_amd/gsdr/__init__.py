@@ -43,9 +43,11 @@ EXPORTED = [
     "gsdr_stream_create", "gsdr_stream_destroy", "gsdr_stream_push", "gsdr_stream_span", "gsdr_stream_window",
     "gsdr_acq_set_step_two", "gsdr_acq_get_step_two_threshold", "gsdr_acq_run_step_two",
     "gsdr_trk_set_data_code", "gsdr_acq_read_profile_ex", "gsdr_stream_window_async", "gsdr_stream_release", "gsdr_stream_device",
-    "gsdr_acq_dump_grid_step_two", "gsdr_acq_read_profile_intervals",
+    "gsdr_acq_dump_grid_step_two", "gsdr_acq_read_profile_intervals", "gsdr_acq_set_wipeoff",
+    "gsdr_acq_get_spectrum_reuse",
 ]
 
+WIPE_EXACT, WIPE_GENERIC, WIPE_AVX2 = 0, 1, 2
 SIGNAL_GPS_1C = 0
 SIGNAL_GAL_1B = 1
 SIGNAL_BDS_B1 = 2
@@ -234,6 +236,8 @@ def load():
     L.gsdr_acq_dump_grid.argtypes = [P, P, U32, P]
     L.gsdr_acq_dump_grid_step_two.argtypes = [P, P, U32, ctypes.c_float, P]
     L.gsdr_acq_read_profile_intervals.argtypes = [P, P, ctypes.c_int, P, P, U32, P]
+    L.gsdr_acq_set_wipeoff.argtypes = [P, ctypes.c_int]
+    L.gsdr_acq_get_spectrum_reuse.argtypes = [P, P, P]
     L.gsdr_acq_dump_spectra.argtypes = [P, P, P]
     L.gsdr_corr_create.argtypes = [I, I, I, I, P]
     L.gsdr_corr_destroy.argtypes = [P]
@@ -363,6 +367,30 @@ class Acquisition:
 
     def set_doppler(self, doppler_max, doppler_step, doppler_center=0):
         _check(load().gsdr_acq_set_doppler(self._h, int(doppler_max), int(doppler_step), int(doppler_center)))
+
+    def set_wipeoff(self, mode):
+        """Carrier model of the Doppler grid: WIPE_EXACT (default), WIPE_GENERIC, WIPE_AVX2
+        (include/gsdr.h gsdr_acq_set_wipeoff); accepts the names too."""
+        if isinstance(mode, str):
+            mode = {"exact": WIPE_EXACT, "generic": WIPE_GENERIC, "avx2": WIPE_AVX2}[mode]
+        _check(load().gsdr_acq_set_wipeoff(self._h, int(mode)))
+        self._wipe_mode = int(mode)
+
+    @property
+    def wipe_mode(self):
+        """The carrier model in effect (the handle starts from GSDR_ACQ_WIPE, else exact)."""
+        if getattr(self, "_wipe_mode", None) is None:
+            env = os.environ.get("GSDR_ACQ_WIPE", "exact")
+            self._wipe_mode = {"generic": WIPE_GENERIC, "avx2": WIPE_AVX2}.get(env, WIPE_EXACT)
+        return self._wipe_mode
+
+    @property
+    def spectrum_reuse(self):
+        """(q, p): q forward spectra per block (== D: none), p bins of shift per class step."""
+        q = np.zeros(1, np.uint32)
+        p = np.zeros(1, np.uint32)
+        _check(load().gsdr_acq_get_spectrum_reuse(self._h, _ptr(q), _ptr(p)))
+        return int(q[0]), int(p[0])
 
     def set_threshold(self, t):
         _check(load().gsdr_acq_set_threshold(self._h, float(t)))

@@ -181,6 +181,28 @@ int gsdr_acq_set_local_codes(gsdr_acq* acq, const float* codes, const uint32_t* 
  * rebuild the Doppler wipe-off grid on the device. */
 int gsdr_acq_set_doppler(gsdr_acq* acq, int32_t doppler_max, uint32_t doppler_step, int32_t doppler_center);
 
+/* Carrier wipe-off model of the Doppler grid (update_local_carrier,
+ * pcps_acquisition.cc:233-246, through volk_gnsssdr_s32f_sincos_32fc):
+ *   GSDR_WIPE_EXACT   exp(-j 2 pi f n / fs), phase reduced and evaluated in fp64,
+ *                     rounded once (default);
+ *   GSDR_WIPE_GENERIC the generic protokernel bit for bit (KERN/s32f_sincos_32fc.h:390-403:
+ *                     one fp32 phase accumulator, cosf / sinf);
+ *   GSDR_WIPE_AVX2    the a_avx2 protokernel the reference dispatches on AVX2 x86-64
+ *                     (:448-627: eight fp32 accumulators, Cephes polynomials).
+ * The protokernels' fp32 phase accumulators drift from the exact carrier (GPS 4 Msps:
+ * 1e-3 / 2e-5 rad over 1 ms; Galileo 8 Msps, 8 ms: 0.15 / 0.01 rad); DESIGN.md 3.
+ * With EXACT and Doppler bins commensurate with the FFT bins (doppler_step * N / fs =
+ * p / q, q <= D / 2) the forward pass computes q spectra per block and every Doppler
+ * row is an exact circular shift of one of them (gsdr_acq_get_spectrum_reuse).
+ * Initial mode: GSDR_ACQ_WIPE=exact|generic|avx2 in the environment, else EXACT. */
+#define GSDR_WIPE_EXACT 0
+#define GSDR_WIPE_GENERIC 1
+#define GSDR_WIPE_AVX2 2
+int gsdr_acq_set_wipeoff(gsdr_acq* acq, int mode);
+/* The forward-spectrum reuse in effect: *q spectra per block (== D: none), each
+ * Doppler class step shifting by *p bins. */
+int gsdr_acq_get_spectrum_reuse(const gsdr_acq* acq, uint32_t* q, uint32_t* p);
+
 /* Threshold: set explicitly (set_threshold) or computed from pfa exactly as
  * calculate_threshold (pcps_acquisition.cc:894-909). */
 int gsdr_acq_set_threshold(gsdr_acq* acq, float threshold);

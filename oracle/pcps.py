@@ -30,16 +30,42 @@ def doppler_hz(d, doppler_max, doppler_step, doppler_center=0):
     return -int(doppler_max) + int(doppler_center) + int(doppler_step) * int(d)
 
 
-def doppler_wipeoffs(fs, N, doppler_max, doppler_step, D, doppler_center=0, doppler_bias=0):
-    """update_grid_doppler_wipeoffs (:298-305) + update_local_carrier (:233-246):
-    phase_step = float(TWO_PI) * f / float(fs) in float32, then the generic
-    s32f_sincos with -phase_step (fp32 accumulated phase)."""
+# Carrier wipe-off models (GNSS-SDR computes the carrier with the VOLK protokernel
+# volk_gnsssdr_s32f_sincos_32fc that its dispatcher selects for the host):
+#   "exact"   exp(-j 2 pi f n / fs) evaluated in fp64 and rounded once -- the MI355X
+#             engine's default (gsdr_acq_set_wipeoff, GSDR_WIPE_EXACT);
+#   "generic" the generic protokernel (KERN/s32f_sincos_32fc.h:390-403): one fp32
+#             phase accumulator, cosf / sinf;
+#   "avx2"    the a_avx2 / u_avx2 protokernel (:448-627) an AVX2 x86-64 host runs:
+#             eight fp32 accumulators advancing by 8 inc, Cephes polynomials.
+# The two protokernels' accumulated fp32 phase drifts from the exact carrier (C2:
+# 1e-3 / 2e-5 rad, C4 64000 points: 0.15 / 0.01 rad); DESIGN.md 3 states the bar.
+WIPE_MODES = ("exact", "generic", "avx2")
+
+
+def carrier(freq, fs, N, mode="exact"):
+    """One wipe-off row for the float frequency freq (update_local_carrier, :233-246)."""
     f32 = np.float32
+    f = f32(freq)
+    if mode == "exact":
+        t = float(f) * np.arange(N, dtype=np.float64) / float(fs)
+        return np.exp(-2j * np.pi * (t - np.floor(t))).astype(np.complex64)
+    step = f32(TWO_PI) * f / f32(fs)
+    if mode == "generic":
+        return volk.s32f_sincos_32fc(float(-step), N)
+    if mode == "avx2":
+        return volk.s32f_sincos_32fc_avx2(float(-step), N)
+    raise ValueError(mode)
+
+
+def doppler_wipeoffs(fs, N, doppler_max, doppler_step, D, doppler_center=0, doppler_bias=0, mode="exact"):
+    """update_grid_doppler_wipeoffs (:298-305) + update_local_carrier (:233-246):
+    phase_step = float(TWO_PI) * f / float(fs) in float32 and -phase_step through the
+    sincos model `mode` (see carrier)."""
     w = np.empty((D, N), np.complex64)
     for d in range(D):
-        f = f32(doppler_bias + doppler_hz(d, doppler_max, doppler_step, doppler_center))
-        step = f32(TWO_PI) * f / f32(fs)
-        w[d] = volk.s32f_sincos_32fc(float(-step), N)
+        f = np.float32(doppler_bias + doppler_hz(d, doppler_max, doppler_step, doppler_center))
+        w[d] = carrier(f, fs, N, mode)
     return w
 
 
@@ -185,13 +211,11 @@ def step_two_freqs(center2, doppler_step2, nbins2):
     return [f32(f32(center2) + f32(f32(f32(d) - half) * f32(doppler_step2))) for d in range(nbins2)]
 
 
-def doppler_wipeoffs_step2(fs, N, center2, doppler_step2, nbins2):
+def doppler_wipeoffs_step2(fs, N, center2, doppler_step2, nbins2, mode="exact"):
     """The narrow grid's carriers (update_local_carrier with float freq, :233-246)."""
-    f32 = np.float32
     w = np.empty((nbins2, N), np.complex64)
     for d, f in enumerate(step_two_freqs(center2, doppler_step2, nbins2)):
-        step = f32(TWO_PI) * f32(f) / f32(fs)
-        w[d] = volk.s32f_sincos_32fc(float(-step), N)
+        w[d] = carrier(np.float32(f), fs, N, mode)
     return w
 
 

@@ -39,6 +39,7 @@ def lib():
         L.orc_rotator_dot_prod_32fc_x2_xn.argtypes = [_p, _p, _f, _f, _p, _p, _i, _u]
         L.orc_high_dyn_rotator_dot_prod_32fc_32f_xn.argtypes = [_p, _p, _f, _f, _f, _f, _p, _p, _i, _u]
         L.orc_s32f_sincos_32fc.argtypes = [_p, _f, _p, _u]
+        L.orc_s32f_sincos_32fc_avx2.argtypes = [_p, _f, _p, _u]
         L.orc_index_max_32u.argtypes = [_p, ctypes.c_uint32]
         L.orc_index_max_32u.restype = ctypes.c_uint32
         L.orc_multicorrelator_real_codes.argtypes = [_p, _p, _p, _u, _p, _i, _f, _f, _f, _f, _f, _f, _u, _i, _i]
@@ -107,6 +108,14 @@ def s32f_sincos_32fc(phase_inc, N, phase=0.0):
     out = np.empty(N, np.complex64)
     ph = np.array([phase], np.float32)
     lib().orc_s32f_sincos_32fc(_ptr(out), phase_inc, _ptr(ph), N)
+    return out
+
+
+def s32f_sincos_32fc_avx2(phase_inc, N, phase=0.0):
+    """The a_avx2 / u_avx2 protokernel (KERN/s32f_sincos_32fc.h:448-627)."""
+    out = np.empty(N, np.complex64)
+    ph = np.array([phase], np.float32)
+    lib().orc_s32f_sincos_32fc_avx2(_ptr(out), phase_inc, _ptr(ph), N)
     return out
 
 

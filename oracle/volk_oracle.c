@@ -337,6 +337,75 @@ void orc_s32f_sincos_32fc(float* out, float phase_inc, float* phase, unsigned in
     *phase = p;
 }
 
+/* KERN/s32f_sincos_32fc.h:448-627 (a_avx2 / u_avx2, the kernel the reference's
+ * dispatcher picks on an AVX2 x86-64 host): eight lanes start at phase + k*inc and
+ * advance by 8*inc (fp32), each lane's cos/sin from the Cephes polynomials after
+ * the three-constant range reduction; the N % 8 tail continues from
+ * phase + inc * (8 * iters) with cosf/sinf.  Restated per lane in the same fp32
+ * operation order (the file is built with -ffp-contract=off). */
+static void cephes_sincos_f32(float x0, float* s, float* c)
+{
+    const float FOPI = 1.27323954473516f;
+    const float DP1 = -0.78515625f, DP2 = -2.4187564849853515625e-4f, DP3 = -3.77489497744594108e-8f;
+    const float C0 = 2.443315711809948E-005f, C1 = -1.388731625493765E-003f, C2 = 4.166664568298827E-002f;
+    const float S0 = -1.9515295891E-4f, S1 = 8.3321608736E-3f, S2 = -1.6666654611E-1f;
+    int sign_sin = signbit(x0) ? 1 : 0;
+    float x = fabsf(x0);
+    float y = x * FOPI;
+    int32_t j = (int32_t)y; /* cvttps: truncation (|y| < 2^31 here) */
+    j = (j + 1) & ~1;
+    y = (float)j;
+    const int swap = (j & 4) != 0;
+    const int poly = (j & 2) == 0;
+    x = x + y * DP1;
+    x = x + y * DP2;
+    x = x + y * DP3;
+    const int sign_cos = ((~(j - 2)) & 4) != 0;
+    sign_sin ^= swap;
+    const float z = x * x;
+    float yc = C0 * z;
+    yc = yc + C1;
+    yc = yc * z;
+    yc = yc + C2;
+    yc = yc * z;
+    yc = yc * z;
+    yc = yc - z * 0.5f;
+    yc = yc + 1.0f;
+    float ys = S0 * z;
+    ys = ys + S1;
+    ys = ys * z;
+    ys = ys + S2;
+    ys = ys * z;
+    ys = ys * x;
+    ys = ys + x;
+    float sv = poly ? ys : yc, cv = poly ? yc : ys;
+    *s = sign_sin ? -sv : sv;
+    *c = sign_cos ? -cv : cv;
+}
+
+void orc_s32f_sincos_32fc_avx2(float* out, float phase_inc, float* phase, unsigned int N)
+{
+    const float p0 = *phase;
+    const unsigned int iters = N / 8;
+    float lane[8];
+    for (int k = 0; k < 8; k++) lane[k] = k == 0 ? p0 : p0 + (float)k * phase_inc;
+    const float inc8 = 8.0f * phase_inc;
+    for (unsigned int it = 0; it < iters; it++)
+        for (int k = 0; k < 8; k++)
+            {
+                cephes_sincos_f32(lane[k], &out[2 * (8 * it + k) + 1], &out[2 * (8 * it + k)]);
+                lane[k] = lane[k] + inc8;
+            }
+    float p = p0 + phase_inc * (float)(iters * 8);
+    for (unsigned int i = iters * 8; i < N; i++)
+        {
+            out[2 * i] = cosf(p);
+            out[2 * i + 1] = sinf(p);
+            p += phase_inc;
+        }
+    *phase = p;
+}
+
 /* KERN/32f_index_max_32u.h:446-467 (generic): first index of the maximum (strict >). */
 uint32_t orc_index_max_32u(const float* src, uint32_t N)
 {

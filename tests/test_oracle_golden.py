@@ -123,6 +123,44 @@ def test_oracle_rotator_avx_vs_generic_and_exact(N):
     assert rel_a < rel_g or rel_g < 1e-5
 
 
+def test_oracle_sincos_avx2_restatement():
+    """The a_avx2 sincos restatement (volk_oracle.c, KERN/s32f_sincos_32fc.h:448-627):
+    lane k of block m holds the fp32 phase k*inc accumulated by 8*inc m times (and the
+    N % 8 tail continues from inc * 8 iters one inc at a time); each output is the
+    Cephes polynomial pair of that phase, within 1e-6 of fp64 cos / sin."""
+    f = np.float32
+    for N, freq, fs in ((4003, 9750.0, 4e6), (16000, -10000.0, 16e6)):
+        inc = -(f(f(6.283185307179586) * f(freq)) / f(fs))
+        w = volk.s32f_sincos_32fc_avx2(float(inc), N)
+        ph = np.empty(N, np.float32)
+        lanes = np.array([f(0.0)] + [f(f(k) * inc) for k in range(1, 8)], np.float32)
+        for m in range(N // 8):
+            ph[8 * m:8 * m + 8] = lanes
+            lanes = (lanes + f(8) * inc).astype(np.float32)
+        p = f(inc * f(8 * (N // 8)))
+        for n in range(8 * (N // 8), N):
+            ph[n] = p
+            p = f(p + inc)
+        ref = np.exp(1j * ph.astype(np.float64))
+        assert np.max(np.abs(w - ref)) < 1e-6
+
+
+@pytest.mark.parametrize("name,fs,N,freq,avx2_max,generic_max", [
+    ("C2", 4e6, 4000, 10000.0, 5e-5, 2e-3),
+    ("C4 bit transition", 8e6, 64000, 5000.0, 2e-2, 0.3)])
+def test_oracle_carrier_models_vs_exact(name, fs, N, freq, avx2_max, generic_max):
+    """The two reference protokernels' accumulated phase against the exact carrier
+    (pcps.carrier 'exact'): the AVX2 one (what an x86-64 AVX2 host dispatches) drifts
+    an order of magnitude less than the generic one -- the spread DESIGN.md 3 bounds
+    the GPU's exact-carrier results by."""
+    e = pcps.carrier(freq, fs, N, "exact")
+    n = np.arange(N)
+    assert np.max(np.abs(e - np.exp(-2j * np.pi * freq * n / fs))) < 1e-6
+    d_a = np.max(np.abs(np.angle(pcps.carrier(freq, fs, N, "avx2") * np.conj(e))))
+    d_g = np.max(np.abs(np.angle(pcps.carrier(freq, fs, N, "generic") * np.conj(e))))
+    assert d_a < avx2_max and d_g < generic_max and d_a < d_g, (name, d_a, d_g)
+
+
 @pytest.fixture(scope="module")
 def gal_capture():
     """Reference capture src/tests/signal_samples/Galileo_E1_ID_1_Fs_4Msps_8ms.dat (CC-BY-4.0)."""

@@ -384,7 +384,8 @@ def run_c5(args):
         ns = total * n + 4 * n  # + one Galileo code period of slack for the last calls
     iq = (synth.gps_l1_iq(fs, ns, gps, seed_offset=500, noise=False, dtype=np.complex128) +
           synth.gal_e1_iq(fs, ns, gal, seed_offset=500, noise=False, dtype=np.complex128) +
-          synth.bds_b1i_iq(fs, ns, bds, seed_offset=500, noise=True, dtype=np.complex128)).astype(np.complex64)
+          synth.bds_b1i_iq(fs, ns, bds, seed_offset=500, noise=True, dtype=np.complex128,
+                           code_doppler=not stream)).astype(np.complex64)
     iq_dev = torch.from_numpy(iq.view(np.float32).copy()).to(dev)
     base = iq_dev.data_ptr()
     if stream:

@@ -244,6 +244,9 @@ int gsdr_acq_create(int device, const gsdr_acq_conf* conf, gsdr_acq** out)
     // merged first/second-peak pass (acq_argmax_second_four_kernel)
     if (e == hipSuccess && a->split > 0 && !(conf->pfa > 0.0f))
         e = hipMalloc(&a->d_rowbuf, nB * nP * N * sizeof(float));
+    // split path: the selected rows' first-maximum keys (acq_correlate_split_kernel<ARG>)
+    if (e == hipSuccess && a->split > 0) e = hipMalloc(&a->d_keys, nB * nP * sizeof(unsigned long long));
+    if (e == hipSuccess && a->split > 0) e = hipMalloc(&a->d_psum, nB * nP * 4 * sizeof(float));
     // split path: the two-launch forward's scratch rows (GSDR_ACQ_FWD2=0: the
     // one-workgroup-per-spectrum forward)
     {
@@ -321,7 +324,7 @@ void gsdr_acq_destroy(gsdr_acq* a)
         }
     for (hipEvent_t e : a->prof_pool) (void)hipEventDestroy(e);
     void* bufs[] = {a->st2.d_wipe, a->st2.d_freq, a->d_tw, a->d_wipe, a->d_code_fft, a->d_code_stage, a->d_prn, a->d_X, a->d_stats, a->d_res,
-        a->d_iq, a->d_grid, a->d_rowbuf, a->d_fscratch, a->d_dgrid, a->d_tw_sub, a->d_scratch, a->d_slots, a->d_resk, a->d_acc, a->d_acc_slots};
+        a->d_iq, a->d_grid, a->d_rowbuf, a->d_keys, a->d_psum, a->d_fscratch, a->d_dgrid, a->d_tw_sub, a->d_scratch, a->d_slots, a->d_resk, a->d_acc, a->d_acc_slots};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     if (a->stream) (void)hipStreamDestroy(a->stream);

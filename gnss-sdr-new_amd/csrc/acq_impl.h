@@ -703,7 +703,7 @@ struct RowPad
 };
 
 template <int R, int NT, int L, int H, int Ns, bool LAST, class In, class OutL, class Out>
-__device__ __forceinline__ void rows_stage(gsdr::pk::c2* lds, Out& out)
+__device__ __forceinline__ void rows_stage(gsdr::pk::c2* lds, Out& out, int row0)
 {
     using gsdr::pk::c2;
     constexpr int NB = L / R;       // butterflies per row
@@ -749,7 +749,7 @@ __device__ __forceinline__ void rows_stage(gsdr::pk::c2* lds, Out& out)
                     if constexpr (LAST)
                         {
 #pragma unroll
-                            for (int r = 0; r < R; ++r) out.value(v[b][r], jb[b] + r * Ns);  // row output jb + r Ns
+                            for (int r = 0; r < R; ++r) out.value(v[b][r], jb[b] + r * Ns, row0 + rw[b]);  // row output jb + r Ns
                         }
                     else
                         {
@@ -765,13 +765,13 @@ __device__ __forceinline__ void rows_stage(gsdr::pk::c2* lds, Out& out)
 }
 
 template <int NT, int L, int H, int Ns, class Pads, int Si, int R, int... Rest, class Out>
-__device__ __forceinline__ void rows_stages(gsdr::pk::c2* lds, Out& out)
+__device__ __forceinline__ void rows_stages(gsdr::pk::c2* lds, Out& out, int row0)
 {
     constexpr bool LAST = sizeof...(Rest) == 0;
     using In = typename Pads::template layout<Si>;
     using OutL = typename Pads::template layout<LAST ? Si : Si + 1>;
-    rows_stage<R, NT, L, H, Ns, LAST, In, OutL>(lds, out);
-    if constexpr (!LAST) rows_stages<NT, L, H, Ns * R, Pads, Si + 1, Rest...>(lds, out);
+    rows_stage<R, NT, L, H, Ns, LAST, In, OutL>(lds, out, row0);
+    if constexpr (!LAST) rows_stages<NT, L, H, Ns * R, Pads, Si + 1, Rest...>(lds, out, row0);
 }
 
 // Pads for the buffers between the row stages (buffer 0 = phase 1's rows); a
@@ -805,7 +805,7 @@ struct Pads1000
 // butterfly count repeat the last butterfly (same values to the same addresses,
 // repeated outputs for an order-free maximum), so no lane is predicated off.
 template <int R, int L, int Ns, bool LAST, class In, class OutL, class Out>
-__device__ __forceinline__ void wl_stage(gsdr::pk::c2* row, Out& out, int lane)
+__device__ __forceinline__ void wl_stage(gsdr::pk::c2* row, Out& out, int lane, int k1)
 {
     using gsdr::pk::c2;
     constexpr int NB = L / R;
@@ -838,7 +838,7 @@ __device__ __forceinline__ void wl_stage(gsdr::pk::c2* row, Out& out, int lane)
             if constexpr (LAST)
                 {
 #pragma unroll
-                    for (int r = 0; r < R; ++r) out.value(v[b][r], jb[b] + r * Ns);
+                    for (int r = 0; r < R; ++r) out.value(v[b][r], jb[b] + r * Ns, k1);
                 }
             else
                 {
@@ -851,13 +851,13 @@ __device__ __forceinline__ void wl_stage(gsdr::pk::c2* row, Out& out, int lane)
 }
 
 template <int L, int Ns, class Pads, int Si, int R, int... Rest, class Out>
-__device__ __forceinline__ void wl_stages(gsdr::pk::c2* row, Out& out, int lane)
+__device__ __forceinline__ void wl_stages(gsdr::pk::c2* row, Out& out, int lane, int k1)
 {
     constexpr bool LAST = sizeof...(Rest) == 0;
     using In = typename Pads::template layout<Si>;
     using OutL = typename Pads::template layout<LAST ? Si : Si + 1>;
-    wl_stage<R, L, Ns, LAST, In, OutL>(row, out, lane);
-    if constexpr (!LAST) wl_stages<L, Ns * R, Pads, Si + 1, Rest...>(row, out, lane);
+    wl_stage<R, L, Ns, LAST, In, OutL>(row, out, lane, k1);
+    if constexpr (!LAST) wl_stages<L, Ns * R, Pads, Si + 1, Rest...>(row, out, lane, k1);
 }
 
 // WPE_ packs the waves-per-EU hint (bits 0-3) and PGS (bits 4+): with PGS > 0 an
@@ -888,15 +888,15 @@ struct RegFourStep
     static constexpr size_t lds_bytes() { return (size_t)lds_elems * sizeof(float2) + (NT / 64) * sizeof(float); }
     static_assert(WL || R % H == 0, "rows go through LDS in groups of H");
     template <class Out>
-    __device__ __forceinline__ static void row_transforms(gsdr::pk::c2* lds, Out& out)
+    __device__ __forceinline__ static void row_transforms(gsdr::pk::c2* lds, Out& out, int row0)
     {
-        rows_stages<NT, L, H, 1, Pads, 0, Rs...>(lds, out);
+        rows_stages<NT, L, H, 1, Pads, 0, Rs...>(lds, out, row0);
     }
     // WL: one row (at lds, max_stride() elements) by the calling wave
     template <class Out>
-    __device__ __forceinline__ static void wl_row(gsdr::pk::c2* row, Out& out, int lane)
+    __device__ __forceinline__ static void wl_row(gsdr::pk::c2* row, Out& out, int lane, int k1)
     {
-        wl_stages<L, 1, Pads, 0, Rs...>(row, out, lane);
+        wl_stages<L, 1, Pads, 0, Rs...>(row, out, lane, k1);
     }
 
     // Phase 2 of a register four-step: the R rows (phase 1's v[c][k1], lane column
@@ -922,7 +922,7 @@ struct RegFourStep
                                     }
                             }
                         __syncthreads();
-                        row_transforms(lds, out);
+                        row_transforms(lds, out, h * H);
                     }
             }
         else
@@ -946,7 +946,7 @@ struct RegFourStep
                                     }
                             }
                         __syncthreads();
-                        if (h * H + wave < R) wl_row(lds + wave * STR, out, lane);
+                        if (h * H + wave < R) wl_row(lds + wave * STR, out, lane, h * H + wave);
                     }
             }
     }
@@ -1023,7 +1023,7 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(RP:
         const float2* tw;
         float m;
         __device__ __forceinline__ float2 twiddle(int m_) const { return tw[m_ * R]; }  // W_L^m = W_N^{m R}
-        __device__ __forceinline__ void value(c2 x, int) { m = __builtin_fmaxf(m, __builtin_fmaf(x.x, x.x, x.y * x.y)); }
+        __device__ __forceinline__ void value(c2 x, int, int) { m = __builtin_fmaxf(m, __builtin_fmaf(x.x, x.x, x.y * x.y)); }
     } out{tw, 0.0f};
     // phase 2: the rows k1 through LDS
     RP::phase2(lds, v, out);
@@ -1063,10 +1063,22 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(RP:
 // PRNs so its L2 holds pgs code rows while the X rows stream.
 // ABL (timing ablations for the profile, results meaningless): bit 0 replaces
 // phase 1's global loads by lane-computed values, bit 1 skips phase 2.
-template <int ROUT, class RP, bool HALF, int ABL = 0>
+// ARG: the selected row's pass instead of the grid (acq_reduce_kernel chose Doppler
+// row d* of (b, p) from the row maxima): grid (b*P + p, q), the same arithmetic as
+// the grid pass (the recomputed values are bit-identical to those the row maximum
+// came from), each output's key (|R|^2 bits, ~j) merged into keys[b*P + p] by a
+// 64-bit atomic maximum -- the first maximum over the effective window j = k -
+// (N - eff), index_max's rule (KERN/32f_index_max_32u.h:446-467) -- and, for the
+// peak ratio, |R|^2 into the row's rowbuf entries; acq_argmax_split_finish_kernel
+// turns the key into the result fields.  One workgroup per transform of a
+// 100000-point row spreads the pass over ROUT x more CUs than the one-workgroup
+// recomputation (acq_argmax_four_kernel: 144 workgroups at C5 Galileo).
+template <int ROUT, class RP, bool HALF, int ABL = 0, bool ARG = false>
 __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(RP::WPE))) acq_correlate_split_kernel(
     const float2* __restrict__ X, const float2* __restrict__ code_fft, RowStat* __restrict__ stats,
-    const float2* __restrict__ tw, uint32_t D, uint32_t P, uint32_t nblocks, uint32_t pgs, XMap xm)
+    const float2* __restrict__ tw, uint32_t D, uint32_t P, uint32_t nblocks, uint32_t pgs, XMap xm,
+    const gsdr_acq_result* __restrict__ sel, unsigned long long* __restrict__ keys, float* __restrict__ rowbuf,
+    float* __restrict__ psum)
 {
     using gsdr::pk::c2;
     constexpr int R = RP::R, NT = RP::NT, L = RP::L, CPL = RP::CPL;
@@ -1081,7 +1093,15 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(RP:
     const uint32_t id = blockIdx.x;
     const uint32_t full = nrows >> 3;
     uint32_t row, pv;
-    if (id < full * 8u * PV)
+    if constexpr (ARG)
+        {
+            const uint32_t bp = id / ROUT;
+            const uint32_t dsel = sel[bp].doppler_index;
+            if (dsel >= D) return;  // uniform: no maximum found (an all-NaN grid)
+            row = (bp / P) * D + dsel;
+            pv = (bp - (bp / P) * P) * ROUT + (id - bp * ROUT);
+        }
+    else if (id < full * 8u * PV)
         {
             const uint32_t xcd = id & 7u, slot = id >> 3;
             const uint32_t G = pgs * ROUT;  // PV % G == 0 (host)
@@ -1193,14 +1213,31 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(RP:
     {
         const float2* tw;
         float m;
+        unsigned long long key;
+        float* row;  // ARG with the peak ratio: the row's |R|^2 (effective window)
+        uint32_t q;
         // W_L^m = W_N^{m R ROUT}
         __device__ __forceinline__ float2 twiddle(int m_) const { return tw[m_ * R * ROUT]; }
-        __device__ __forceinline__ void value(c2 x, int k2)
+        __device__ __forceinline__ void value(c2 x, int k2, int k1)
         {
             const float a = __builtin_fmaf(x.x, x.x, x.y * x.y);
-            if (!HALF || k2 >= L / 2) m = __builtin_fmaxf(m, a);
+            if (HALF && k2 < L / 2) return;
+            if constexpr (ARG)
+                {
+                    // output k = q + ROUT (k1 + R k2); effective index j = k - (N - eff)
+                    const uint32_t j = q + (uint32_t)ROUT * ((uint32_t)k1 + (uint32_t)R * (uint32_t)k2) - (HALF ? N / 2 : 0u);
+                    const unsigned long long kk = ((unsigned long long)__float_as_uint(a) << 32) | (0xffffffffu - j);
+                    key = kk > key ? kk : key;
+                    if (row) row[j] = a;
+                }
+            else
+                m = __builtin_fmaxf(m, a);
         }
-    } out{tw, 0.0f};
+    } out{tw, 0.0f, 0ull, nullptr, q};
+    if constexpr (ARG)
+        {
+            if (rowbuf) out.row = rowbuf + (size_t)(id / ROUT) * (HALF ? N / 2 : N);
+        }
     if constexpr ((ABL & 2) == 0)
         RP::phase2(lds, v, out);
     else
@@ -1208,10 +1245,60 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(RP:
 #pragma unroll
             for (int c = 0; c < CPL; ++c)
 #pragma unroll
-                for (int i = 0; i < R; ++i) out.value(v[c][i], L - 1);
+                for (int i = 0; i < R; ++i) out.value(v[c][i], L - 1, i);
+        }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if constexpr (ARG)
+        {
+            unsigned long long k = out.key;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1)
+                {
+                    const unsigned long long t = __shfl_xor(k, o);
+                    k = t > k ? t : k;
+                }
+            unsigned long long* sk = reinterpret_cast<unsigned long long*>(lds_raw);
+            __syncthreads();  // every wave's phase-2 LDS reads are done: reuse the row buffer
+            if (lane == 0) sk[wave] = k;
+            __syncthreads();
+            if (threadIdx.x == 0)
+                {
+#pragma unroll
+                    for (int w2 = 1; w2 < NW; ++w2) k = sk[w2] > k ? sk[w2] : k;
+                    __hip_atomic_fetch_max(&keys[id / ROUT], k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            if (psum)
+                {
+                    // CFAR: this sub-transform's share of the Parseval sum of the row
+                    // opposite the peak (pcps_acquisition.cc:531-533): sum |conj(X_opp) C|^2
+                    // over inputs [q M, (q + 1) M), lane-strided, then wave and workgroup
+                    // sums in a fixed order; the finish kernel adds the ROUT shares in q order
+                    const uint32_t bp = id / ROUT;
+                    const uint32_t opp = (d + D / 2) % D;
+                    const c2* xo = reinterpret_cast<const c2*>(X) + xm.off(b, opp) + (size_t)q * M;
+                    const c2* co = reinterpret_cast<const c2*>(code_fft) + (size_t)p * N + (size_t)q * M;
+                    float acc = 0.0f;
+                    for (uint32_t i = threadIdx.x; i < M; i += NT)
+                        {
+                            const c2 y = gsdr::pk::conj_mul(xo[i], co[i]);
+                            acc = __builtin_fmaf(y.x, y.x, __builtin_fmaf(y.y, y.y, acc));
+                        }
+#pragma unroll
+                    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+                    float* sf = reinterpret_cast<float*>(sk + NW);
+                    if (lane == 0) sf[wave] = acc;
+                    __syncthreads();
+                    if (threadIdx.x == 0)
+                        {
+                            float tot = 0.0f;
+#pragma unroll
+                            for (int w2 = 0; w2 < NW; ++w2) tot += sf[w2];
+                            psum[(size_t)bp * ROUT + q] = tot;
+                        }
+                }
+            return;
         }
     float rmax = gsdr::wave_max(out.m);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if (lane == 0) red[wave] = rmax;
     __syncthreads();
     if (threadIdx.x == 0)
@@ -1225,6 +1312,118 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(RP:
             else  // non-negative floats order as their bit patterns (row zeroed by the host)
                 __hip_atomic_fetch_max(reinterpret_cast<uint32_t*>(&st->max), __float_as_uint(best), __ATOMIC_RELAXED,
                     __HIP_MEMORY_SCOPE_AGENT);
+        }
+}
+
+// The selected rows' results from acq_correlate_split_kernel<ARG>'s keys: code
+// phase, Acq_delay_samples = fmod(indext, samples_per_code) (pcps_acquisition.cc:709)
+// and the peak from the key; CFAR: the input power of the row opposite the peak by
+// Parseval (:531-533, as acq_argmax_four_kernel over the whole row, same summation
+// order); peak ratio: the second peak outside the +-1 chip window around the first
+// (:580-604, wrapped at d_fft_size as the reference does) from the rowbuf row.
+// One 256-lane workgroup per (b, p).  Not for CFAR with bit transition (the
+// opposite row's half window needs its transform: acq_argmax_four_kernel).
+template <int NT>
+__global__ void __launch_bounds__(NT) acq_argmax_split_finish_kernel(const float2* __restrict__ X,
+    const float2* __restrict__ code_fft, gsdr_acq_result* __restrict__ res, const unsigned long long* __restrict__ keys,
+    const float* __restrict__ rowbuf, const float* __restrict__ psum, uint32_t nps, AcqParams ap)
+{
+    constexpr int NW = NT / 64;
+    __shared__ unsigned long long s_key[NW];
+    __shared__ float s_sum[NW];
+    const uint32_t bp = blockIdx.x;
+    const uint32_t b = bp / ap.P, p = bp - b * ap.P;
+    const uint32_t N = ap.N;
+    const uint32_t d = res[bp].doppler_index;
+    if (d >= ap.D) return;  // uniform
+    const unsigned long long key = keys[bp];
+    const uint32_t idx = 0xffffffffu - (uint32_t)(key & 0xffffffffu);
+    const float peak = __uint_as_float((uint32_t)(key >> 32));
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    float ip = 0.0f, second = 0.0f;
+    if (ap.cfar && !ap.step_two && psum)
+        {
+            // the split pass's per-sub-transform shares, in sub-transform order
+            float tot = 0.0f;
+            for (uint32_t i = 0; i < nps; ++i) tot += psum[(size_t)bp * nps + i];
+            ip = (float)((double)tot / 2.0 / (double)ap.counter);
+        }
+    else if (ap.cfar && !ap.step_two)
+        {
+            const uint32_t opp = (d + ap.D / 2) % ap.D;
+            const float2* xo = X + ap.xm.off(b, opp);
+            const float2* c = code_fft + (size_t)p * N;
+            float acc = 0.0f;
+            for (uint32_t i = threadIdx.x; i < N; i += NT)
+                {
+                    const float2 a = xo[i], k = c[i];
+                    const float yr = a.x * k.x + a.y * k.y, yi = a.x * k.y - a.y * k.x;
+                    acc = __builtin_fmaf(yr, yr, __builtin_fmaf(yi, yi, acc));
+                }
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+            if (lane == 0) s_sum[wave] = acc;
+            __syncthreads();
+            float tot = 0.0f;
+#pragma unroll
+            for (int w = 0; w < NW; ++w) tot += s_sum[w];
+            ip = (float)((double)tot / 2.0 / (double)ap.counter);
+        }
+    else if (!ap.cfar)
+        {
+            const uint32_t eff = ap.eff;
+            const float* row = rowbuf + (size_t)bp * eff;
+            const int32_t ti = (int32_t)idx;
+            int32_t e1 = ti - (int32_t)ap.samples_per_chip;
+            int32_t e2 = ti + (int32_t)ap.samples_per_chip;
+            if (e1 < 0)
+                e1 = (int32_t)N + e1;
+            else if (e2 >= (int32_t)N)
+                e2 = e2 - (int32_t)N;
+            float best = 0.0f;
+            uint32_t bidx = 0;
+            for (uint32_t j = threadIdx.x; j < eff; j += NT)
+                {
+                    const int32_t jj = (int32_t)j;
+                    const bool excluded = (e1 < e2) ? (jj >= e1 && jj < e2) : (jj >= e1 || jj < e2);
+                    const float m = excluded ? 0.0f : row[j];
+                    if (stat_better(m, j, best, bidx))
+                        {
+                            best = m;
+                            bidx = j;
+                        }
+                }
+            unsigned long long k2 = ((unsigned long long)__float_as_uint(best) << 32) | (0xffffffffu - bidx);
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1)
+                {
+                    const unsigned long long t = __shfl_xor(k2, o);
+                    k2 = t > k2 ? t : k2;
+                }
+            if (lane == 0) s_key[wave] = k2;
+            __syncthreads();
+#pragma unroll
+            for (int w = 0; w < NW; ++w) k2 = s_key[w] > k2 ? s_key[w] : k2;
+            second = __uint_as_float((uint32_t)(k2 >> 32));
+        }
+    if (threadIdx.x == 0)
+        {
+            gsdr_acq_result r = res[bp];
+            r.code_phase = idx;
+            r.acq_delay_samples = (double)fmodf((float)idx, ap.samples_per_code);
+            r.peak = peak;
+            if (ap.cfar)
+                {
+                    if (!ap.step_two) r.input_power = ip;
+                    r.test_statistic = r.peak / r.input_power;
+                }
+            else
+                {
+                    r.second_peak = second;
+                    r.test_statistic = r.peak / r.second_peak;
+                }
+            r.positive = r.test_statistic > ap.threshold ? 1 : 0;
+            res[bp] = r;
         }
 }
 
@@ -2070,6 +2269,8 @@ struct gsdr_acq
     void* d_iq{nullptr};
     float* d_grid{nullptr};
     float* d_rowbuf{nullptr};  // split path, peak ratio: the selected rows' |R|^2 (max_blocks x max_prns x N)
+    unsigned long long* d_keys{nullptr};  // split path: the selected rows' first-maximum keys (max_blocks x max_prns)
+    float* d_psum{nullptr};               // split path, CFAR: Parseval shares per sub-transform (max_blocks x max_prns x 4)
     float2* d_fscratch{nullptr};  // split path: the two-launch forward's column-DFT rows (max_blocks x D x N)
     float* d_dgrid{nullptr};     // gsdr_acq_run_dwell: the |R|^2 grid kept across calls (max_prns x D x eff)
     float2* d_tw_sub{nullptr};   // four-step: W_N2 table
@@ -2314,6 +2515,7 @@ int launch_forward_pk(gsdr_acq* a, const void* iq, int item_type, uint32_t nbloc
 int setup_corr_variant(gsdr_acq* a, int v);
 int setup_split(gsdr_acq* a);
 int launch_split(gsdr_acq* a, uint32_t nblocks, hipStream_t s);
+int launch_split_argmax(gsdr_acq* a, uint32_t nblocks, gsdr_acq_result* res, hipStream_t s);
 int dispatch_static(gsdr_acq* a, int op, const void* iq, uint32_t nblocks, uint64_t stride, uint64_t stamp0,
     gsdr_acq_result* res, hipStream_t s, uint32_t aux);
 int dispatch_runtime(gsdr_acq* a, int op, const void* iq, uint32_t nblocks, uint64_t stride, uint64_t stamp0,
@@ -2439,7 +2641,15 @@ int launch_split_all(gsdr_acq* a, const void* iq, int item_type, uint32_t nblock
     hipLaunchKernelGGL(acq_reduce_kernel, dim3(nblocks * a->nprn), dim3(64), 0, s, a->d_stats, res, a->d_prn, ap,
         stamp0, stride);
     GSDR_HIP(hipGetLastError());
-    if (ap.cfar || !a->d_rowbuf)
+    // the selected rows on the split plan itself (GSDR_ACQ_SPLIT_ARG=0: recomputed on PT);
+    // CFAR with bit transition needs the opposite row's half window: recomputed on PT
+    static const bool split_arg = !(std::getenv("GSDR_ACQ_SPLIT_ARG") && std::atoi(std::getenv("GSDR_ACQ_SPLIT_ARG")) == 0);
+    if (split_arg && a->d_keys && !(ap.cfar && a->eff != a->N) && (ap.cfar || a->d_rowbuf))
+        {
+            int rc2 = gsdr_acq_impl::launch_split_argmax(a, nblocks, res, s);
+            if (rc2 != GSDR_OK) return rc2;
+        }
+    else if (ap.cfar || !a->d_rowbuf)
         {
             hipLaunchKernelGGL((acq_argmax_four_kernel<PT>), dim3(nblocks * a->nprn), dim3(PT::NT), lds, s, a->d_X,
                 a->d_code_fft, res, a->d_tw, plan_of<PT>(a), ap);

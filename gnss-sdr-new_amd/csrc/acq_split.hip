@@ -62,20 +62,26 @@ uint32_t prn_group(uint32_t P, uint32_t N)
     return best;
 }
 
-template <int ROUT, class RP, bool HALF, int ABL = 0>
-int launch_one(gsdr_acq* a, uint32_t nblocks, hipStream_t s)
+// ARG = false: the grid pass (row maxima into d_stats); ARG = true: the selected
+// rows' pass (keys into d_keys, |R|^2 rows into rowbuf for the peak ratio; the
+// caller zeroes d_keys and runs acq_argmax_split_finish_kernel)
+template <int ROUT, class RP, bool HALF, int ABL = 0, bool ARG = false>
+int launch_one(gsdr_acq* a, uint32_t nblocks, hipStream_t s, const gsdr_acq_result* sel = nullptr,
+    float* rowbuf = nullptr, float* psum = nullptr, uint32_t* rout = nullptr)
 {
+    if (rout) *rout = ROUT;
     static_assert(RP::N * ROUT > 0, "plan");
     if (RP::N * ROUT != (int)a->N)
         {
             gsdr::set_error("internal: split plan for N = %d, handle N = %u", RP::N * ROUT, a->N);
             return GSDR_E_STATE;
         }
-    if (ROUT > 1)
+    if (ROUT > 1 && !ARG)
         GSDR_HIP(hipMemsetAsync(a->d_stats, 0, (size_t)nblocks * a->nprn * a->D * sizeof(RowStat), s));
-    const uint32_t grid = nblocks * a->D * a->nprn * ROUT;
-    hipLaunchKernelGGL((acq_correlate_split_kernel<ROUT, RP, HALF, ABL>), dim3(grid), dim3(RP::NT), RP::lds_bytes(), s,
-        a->d_X, a->d_code_fft, a->d_stats, a->d_tw, a->D, a->nprn, nblocks, prn_group(a->nprn, a->N), a->xm);
+    const uint32_t grid = ARG ? nblocks * a->nprn * ROUT : nblocks * a->D * a->nprn * ROUT;
+    hipLaunchKernelGGL((acq_correlate_split_kernel<ROUT, RP, HALF, ABL, ARG>), dim3(grid), dim3(RP::NT),
+        RP::lds_bytes(), s, a->d_X, a->d_code_fft, a->d_stats, a->d_tw, a->D, a->nprn, nblocks,
+        prn_group(a->nprn, a->N), a->xm, sel, a->d_keys, rowbuf, psum);
     GSDR_HIP(hipGetLastError());
     return GSDR_OK;
 }
@@ -85,9 +91,61 @@ int attrs_one()
 {
     GSDR_HIP(hipFuncSetAttribute((const void*)acq_correlate_split_kernel<ROUT, RP, HALF, ABL>,
         hipFuncAttributeMaxDynamicSharedMemorySize, (int)RP::lds_bytes()));
+    if constexpr (ABL == 0)
+        GSDR_HIP(hipFuncSetAttribute((const void*)acq_correlate_split_kernel<ROUT, RP, HALF, 0, true>,
+            hipFuncAttributeMaxDynamicSharedMemorySize, (int)RP::lds_bytes()));
     return GSDR_OK;
 }
+
+// The selected rows' pass on the handle's split plan (ablation ids on their base plan).
+int launch_split_arg(gsdr_acq* a, uint32_t nblocks, hipStream_t s, const gsdr_acq_result* sel, float* rowbuf,
+    float* psum, uint32_t* rout)
+{
+    const bool half = a->eff != a->N;
+#define GSDR_ARG(RO, RP)                                                                                    \
+    return half ? launch_one<RO, RP, true, 0, true>(a, nblocks, s, sel, rowbuf, psum, rout)                 \
+                : launch_one<RO, RP, false, 0, true>(a, nblocks, s, sel, rowbuf, psum, rout)
+    switch (a->split)
+        {
+        case 1: GSDR_ARG(1, Reg25k);
+        case 2: GSDR_ARG(1, Reg32k);
+        case 3: GSDR_ARG(2, Reg32k);
+        case 4: GSDR_ARG(4, Reg25k);
+        case 5: GSDR_ARG(2, Reg16k);
+        case 6: GSDR_ARG(4, Reg16k);
+        case 11: GSDR_ARG(1, Wl25k);
+        case 12: case 112: case 212: GSDR_ARG(1, Wl32k);
+        case 13: case 113: case 213: GSDR_ARG(2, Wl32k);
+        case 14: GSDR_ARG(4, Wl25k);
+        case 15: GSDR_ARG(2, Wl16k);
+        case 16: GSDR_ARG(4, Wl16k);
+        case 17: GSDR_ARG(1, Wl25kW);
+        case 18: GSDR_ARG(4, Wl25kW);
+        case 19: GSDR_ARG(1, Wl32kP);
+        case 20: GSDR_ARG(2, Wl32kP);
+        default: gsdr::set_error("internal: bad split variant %d", a->split); return GSDR_E_STATE;
+        }
+#undef GSDR_ARG
+}
 }  // namespace
+
+int launch_split_argmax(gsdr_acq* a, uint32_t nblocks, gsdr_acq_result* res, hipStream_t s)
+{
+    const bool half = a->eff != a->N;
+    const AcqParams ap = params_of(a);
+    GSDR_HIP(hipMemsetAsync(a->d_keys, 0, (size_t)nblocks * a->nprn * sizeof(unsigned long long), s));
+    float* rowbuf = ap.cfar ? nullptr : a->d_rowbuf;
+    // CFAR (not in step two, whose input power is the first step's): the Parseval
+    // shares of the opposite row come from the split pass itself
+    float* psum = (ap.cfar && !ap.step_two && !half) ? a->d_psum : nullptr;
+    uint32_t rout = 1;
+    int rc = launch_split_arg(a, nblocks, s, res, rowbuf, psum, &rout);
+    if (rc != GSDR_OK) return rc;
+    hipLaunchKernelGGL((acq_argmax_split_finish_kernel<1024>), dim3(nblocks * a->nprn), dim3(1024), 0, s, a->d_X,
+        a->d_code_fft, res, a->d_keys, rowbuf, psum, rout, ap);
+    GSDR_HIP(hipGetLastError());
+    return GSDR_OK;
+}
 
 int launch_split(gsdr_acq* a, uint32_t nblocks, hipStream_t s)
 {
@@ -119,12 +177,13 @@ int launch_split(gsdr_acq* a, uint32_t nblocks, hipStream_t s)
 }
 
 // Select the split correlate for a single-dwell four-step handle (K = 1, with or
-// without bit transition).  Default: 25000 / 32000 (ROUT = 1) and 64000 = 2 x 32000
-// (C4 bit transition: 52 -> 61 Msps, profiles/r03q); 100000 = 4 x 25000 measured
-// slower than the packed four-step (87 vs 100 Msps: every sub-transform re-reads the
-// whole X and code rows, 64 B per point from L2) and runs only with GSDR_ACQ_SPLIT=2,
-// as do the 16000-based splits 5 / 6 (GSDR_ACQ_SPLIT_ID).  GSDR_ACQ_SPLIT=0 keeps
-// the packed four-step everywhere.
+// without bit transition).  Default: 25000 / 32000 (ROUT = 1), 64000 = 2 x 32000
+// (C4 bit transition: 52 -> 61 Msps, profiles/r03q) and 100000 = 4 x 25000.  The last
+// was slower than the packed four-step (87 vs 100 Msps: every sub-transform re-reads
+// the whole X and code rows) until the forward-spectrum reuse (XMap) left one X row
+// per block in L2: 116 vs 107 Msps (profiles/r04h).  The wave-local 100000 plans
+// (14 / 18) and the 16000-based splits 5 / 6 / 15 / 16 run with GSDR_ACQ_SPLIT=2 /
+// GSDR_ACQ_SPLIT_ID; GSDR_ACQ_SPLIT=0 keeps the packed four-step everywhere.
 int setup_split(gsdr_acq* a)
 {
     a->split = 0;
@@ -134,7 +193,7 @@ int setup_split(gsdr_acq* a)
     if (mode == 0) return GSDR_OK;
     for (const SplitId& sp : kSplits)
         if (sp.n == a->N && !a->split) a->split = sp.id;
-    if ((a->split == 4 || a->split == 14 || a->split == 18) && mode < 2) a->split = 0;
+    if ((a->split == 14 || a->split == 18) && mode < 2) a->split = 0;
     // experiments: GSDR_ACQ_SPLIT_ID forces a split of the handle's N
     if (const char* e = std::getenv("GSDR_ACQ_SPLIT_ID"))
         {
@@ -162,10 +221,10 @@ int setup_split(gsdr_acq* a)
         case 18: rc = attrs_one<4, Wl25kW, true>() | attrs_one<4, Wl25kW, false>(); break;
         case 19: rc = attrs_one<1, Wl32kP, true>() | attrs_one<1, Wl32kP, false>(); break;
         case 20: rc = attrs_one<2, Wl32kP, true>() | attrs_one<2, Wl32kP, false>(); break;
-        case 112: rc = attrs_one<1, Wl32k, false, 1>(); break;
-        case 212: rc = attrs_one<1, Wl32k, false, 2>(); break;
-        case 113: rc = attrs_one<2, Wl32k, true, 1>(); break;
-        case 213: rc = attrs_one<2, Wl32k, true, 2>(); break;
+        case 112: rc = attrs_one<1, Wl32k, false, 1>() | attrs_one<1, Wl32k, true>() | attrs_one<1, Wl32k, false>(); break;
+        case 212: rc = attrs_one<1, Wl32k, false, 2>() | attrs_one<1, Wl32k, true>() | attrs_one<1, Wl32k, false>(); break;
+        case 113: rc = attrs_one<2, Wl32k, true, 1>() | attrs_one<2, Wl32k, true>() | attrs_one<2, Wl32k, false>(); break;
+        case 213: rc = attrs_one<2, Wl32k, true, 2>() | attrs_one<2, Wl32k, true>() | attrs_one<2, Wl32k, false>(); break;
         default: break;
         }
     if (rc != GSDR_OK) a->split = 0;

@@ -296,18 +296,19 @@ def bds_is_geo(prn):
     return 0 < prn < 6 or prn > 58
 
 
-def bds_b1i_iq(fs, n_samples, sats, seed_offset=0, noise=True, dtype=np.complex64):
+def bds_b1i_iq(fs, n_samples, sats, seed_offset=0, noise=True, dtype=np.complex64, code_doppler=True):
     """B1I signal; sats are Satellite objects whose code_delay_chips is in B1I chips
     (2.046 Mcps).  MEO/IGSO (D1): code x NH(20) x 50 bps data.  GEO (PRN 1-5,
     59-63, D2): code x 500 bps data (2 code periods per bit) carrying the D2
-    preamble every 300 bits."""
+    preamble every 300 bits.  code_doppler=False keeps the chip rate at 2.046 Mcps
+    (a span repeated end to end is then continuous in code phase)."""
     rng = np.random.default_rng(SEED + 3000 + seed_offset)
     t = np.arange(n_samples, dtype=np.float64) / fs
     out = np.zeros(n_samples, np.complex128)
     nh = np.array([1.0 if c == "0" else -1.0 for c in BDS_B1I_NH])
     for s in sats:
         amp = np.sqrt(10.0 ** (s.cn0_dbhz / 10.0) / fs)
-        cp = t * 2.046e6 * (1.0 + s.doppler_hz / BDS_B1I_HZ) - s.code_delay_chips
+        cp = t * 2.046e6 * ((1.0 + s.doppler_hz / BDS_B1I_HZ) if code_doppler else 1.0) - s.code_delay_chips
         chip = np.floor(cp).astype(np.int64)
         epoch = np.floor_divide(chip, 2046)
         c = bds_b1i_chips(s.prn)[chip % 2046]

@@ -1364,6 +1364,24 @@ void test_pool_overrun()
         "pool overrun: invalid output, block back to standby, counted once");
     std::printf("pool overrun: %d calls in the window, then a call %llu items behind the head -> overrun record at %llu\n",
         calls, static_cast<unsigned long long>(na - nb), static_cast<unsigned long long>(r.sample_counter));
+
+    // a failing feed (items the pool never saw: the scheduler skipped ahead of every
+    // pooled block) -> the block reports a loss of lock and takes its slot out of the
+    // engine, so later advances queue nothing for it
+    int events = 0;
+    b->set_event_handler([&events](int e) { events += e == 3 ? 1 : 0; });
+    tb->start_tracking();
+    b->work(x.data() + na, 8000, na, &out, &nout);  // pull-in at the head
+    EXPECT(b->state() == 2, "pool failing feed: block restarted at the head");
+    const uint64_t skip = na + 100000;
+    nout = 0;
+    const int used = b->work(x.data() + na, 8000, skip, &out, &nout);
+    EXPECT(used == 0 && b->state() == 0 && events == 1, "pool failing feed: loss of lock (event 3), block in standby");
+    // another block's advance must not resurrect the stopped slot
+    ta->start_tracking();
+    a->work(x.data() + na, 8000, na, &out, &nout);
+    a->work(x.data() + na, 8000, na, &out, &nout);
+    EXPECT(b->state() == 0, "pool failing feed: the slot stays stopped");
 }
 
 void test_multicorrelator(const std::vector<std::complex<float>>& capture)

@@ -95,8 +95,8 @@ def test_large_fft_four_step(monkeypatch, fs, N, pfa, split):
     """N beyond one workgroup's LDS: Galileo E1 at 8 Msps (4 ms: 32000; 8 ms:
     64000), BeiDou B1I at 25 Msps (1 ms: 25000), Galileo at 25 Msps (100000) --
     configs C4/C5 -- on every correlate path: GSDR_ACQ_SPLIT=1 (default: the split
-    register four-step for 25000 / 32000 / 64000, the packed four-step for 100000),
-    0 (the packed four-step everywhere), 2 (the split also for 100000 = 4 x 25000),
+    register four-step for 25000 / 32000 / 64000 / 100000 = 4 x 25000), 0 (the packed
+    four-step everywhere), 2 (also the wave-local 100000 plans when forced),
     idK: split id K forced (SPLIT_IDS: the 16000-based splits and the wave-local-row plans).
     Parity with the oracle grid statistics."""
     if split.startswith("id"):

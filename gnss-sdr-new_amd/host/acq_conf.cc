@@ -55,6 +55,9 @@ void Acq_Conf::SetFromConfiguration(const ConfigurationInterface* configuration,
     make_2_steps = configuration->property(role + ".make_two_steps", make_2_steps);
     make_repeat_steps = configuration->property(role + ".make_repeat_steps", make_repeat_steps);
     blocking_on_standby = configuration->property(role + ".blocking_on_standby", blocking_on_standby);
+    mi355x_carrier = configuration->property(role + ".mi355x_carrier", mi355x_carrier);
+    if (mi355x_carrier != "exact" && mi355x_carrier != "generic" && mi355x_carrier != "avx2")
+        throw std::invalid_argument("Acq_Conf: " + role + ".mi355x_carrier must be exact, generic or avx2");
     if (pfa <= 0.0) use_CFAR_algorithm_flag = false;
     enable_monitor_output = configuration->property("AcquisitionMonitor.enable_monitor", false);
     SetDerivedParams();

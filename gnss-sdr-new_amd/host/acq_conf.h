@@ -52,6 +52,10 @@ public:
     bool dump{false};
     bool blocking{true};
     bool blocking_on_standby{false};
+    // MI355X extension: the Doppler grid's carrier model (gsdr_acq_set_wipeoff): "exact"
+    // (default), "generic" or "avx2" -- the VOLK sincos protokernel replayed bit for bit
+    std::string mi355x_carrier{"exact"};
+    int wipeoff_mode() const { return mi355x_carrier == "generic" ? 1 : (mi355x_carrier == "avx2" ? 2 : 0); }
     bool make_2_steps{false};
     bool make_repeat_steps{false};
     bool use_automatic_resampler{false};

@@ -30,6 +30,8 @@ AcquisitionService::AcquisitionService(const Acq_Conf& conf, uint32_t max_reques
     c.ms_per_code = conf.ms_per_code;
     if (gsdr_acq_create(device, &c, &d_engine) != GSDR_OK)
         throw std::runtime_error(std::string("AcquisitionService: ") + gsdr_last_error());
+    if (conf.wipeoff_mode() != GSDR_WIPE_EXACT && gsdr_acq_set_wipeoff(d_engine, conf.wipeoff_mode()) != GSDR_OK)
+        throw std::runtime_error(std::string("AcquisitionService: ") + gsdr_last_error());
     gsdr_acq_get_threshold(d_engine, &d_threshold);
     d_buffer.resize(static_cast<size_t>(d_consumed) * d_isz);
 }

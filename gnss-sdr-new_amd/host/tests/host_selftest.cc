@@ -35,6 +35,7 @@
 #include <vector>
 
 #include <random>
+#include <stdexcept>
 
 #include "acquisition_service.h"
 #include "beidou_b1i_pcps_acquisition_mi355x.h"
@@ -103,9 +104,12 @@ std::vector<std::complex<double>> exact_correlation(const std::complex<float>* x
     return out;
 }
 
-void test_acquisition_validation(const std::vector<std::complex<float>>& capture)
+// carrier: Acquisition_1C.mi355x_carrier (exact, or the generic / AVX2 sincos
+// protokernel replayed); returns the test statistic
+double test_acquisition_validation(const std::vector<std::complex<float>>& capture, const char* carrier = "exact")
 {
     InMemoryConfiguration config;
+    config.set_property("Acquisition_1C.mi355x_carrier", carrier);
     config.set_property("GNSS-SDR.internal_fs_sps", "4000000");
     config.set_property("Acquisition_1C.implementation", "GPS_L1_CA_PCPS_Acquisition_MI355X");
     config.set_property("Acquisition_1C.item_type", "gr_complex");
@@ -153,9 +157,34 @@ void test_acquisition_validation(const std::vector<std::complex<float>>& capture
     EXPECT(doppler_error_hz <= 666, "Doppler error exceeds 666 Hz");
     EXPECT(delay_error_chips < 0.5, "Delay error exceeds 0.5 chips");
     EXPECT(acquisition.get_block()->num_doppler_bins() == 100, "D = ceil(2*5000/100)");
-    std::printf("acquisition: message %d delay %.1f samples doppler %.0f Hz stat %.3f stamp %llu\n", rx_message,
-        gnss_synchro.Acq_delay_samples, gnss_synchro.Acq_doppler_hz, acquisition.get_block()->test_statistics(),
-        static_cast<unsigned long long>(gnss_synchro.Acq_samplestamp_samples));
+    std::printf("acquisition (%s carrier): message %d delay %.1f samples doppler %.0f Hz stat %.6f stamp %llu\n",
+        carrier, rx_message, gnss_synchro.Acq_delay_samples, gnss_synchro.Acq_doppler_hz,
+        acquisition.get_block()->test_statistics(), static_cast<unsigned long long>(gnss_synchro.Acq_samplestamp_samples));
+    return acquisition.get_block()->test_statistics();
+}
+
+// the three carrier models agree on the reference capture within the protokernels'
+// own drift (C1: 4 Msps, +-5 kHz, 1 ms: well under 1e-3 of the statistic); an unknown
+// model is a configuration error
+void test_acquisition_carriers(const std::vector<std::complex<float>>& capture)
+{
+    const double e = test_acquisition_validation(capture, "exact");
+    const double g = test_acquisition_validation(capture, "generic");
+    const double a = test_acquisition_validation(capture, "avx2");
+    EXPECT(std::abs(g - e) <= 1e-3 * e && std::abs(a - e) <= 1e-3 * e, "carrier models: statistics agree");
+    InMemoryConfiguration config;
+    config.set_property("Acquisition_1C.mi355x_carrier", "fast");
+    bool threw = false;
+    try
+        {
+            Acq_Conf c;
+            c.SetFromConfiguration(&config, "Acquisition_1C", 1.023e6, 0.001);
+        }
+    catch (const std::invalid_argument&)
+        {
+            threw = true;
+        }
+    EXPECT(threw, "carrier models: unknown .mi355x_carrier rejected");
 }
 
 // Acquisition_1C.blocking = false (pcps_acquisition.cc:1013-1029): the core runs on
@@ -1441,7 +1470,7 @@ int main(int argc, char** argv)
             std::cerr << "cannot read capture " << argv[1] << '\n';
             return 2;
         }
-    test_acquisition_validation(capture);
+    test_acquisition_carriers(capture);  // the validation case with each carrier model
     test_acquisition_nonblocking(capture);
     {
         const char* d = std::getenv("GSDR_SELFTEST_DUMP_DIR");

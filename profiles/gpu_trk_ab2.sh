@@ -10,12 +10,12 @@ fatal() { local rc=$1; [ $rc -eq 124 ] || [ $rc -eq 137 ] || [ $rc -eq 134 ] || 
 for SPEC in "$@"; do
   IFS='|' read -r name LIB <<< "$SPEC"
   echo "== $name tests ($LIB)"
-  GSDR_LIB=$LIB timeout -k 10 400 python -u -m pytest tests/test_gpu_trk.py tests/test_gpu_configs.py -m gpu -x -q \
+  env ${LIB:+GSDR_LIB=$LIB} timeout -k 10 400 python -u -m pytest tests/test_gpu_trk.py tests/test_gpu_configs.py -m gpu -x -q \
       --timeout 200 --timeout-method thread -p no:cacheprovider > "$OUT/pytest_$name.log" 2>&1; rc=$?
   tail -2 "$OUT/pytest_$name.log"
   if [ $rc -ne 0 ]; then grep -E "FAILED|Error" "$OUT/pytest_$name.log" | head; exit $rc; fi
   echo "== $name configs"
-  GSDR_LIB=$LIB timeout -k 10 300 python -u profiles/configs_bench.py --only C3,C4,C5 --reps 5 > "$OUT/cfg_$name.jsonl" \
+  env ${LIB:+GSDR_LIB=$LIB} timeout -k 10 300 python -u profiles/configs_bench.py --only C3,C4,C5 --reps 5 > "$OUT/cfg_$name.jsonl" \
       2> "$OUT/cfg_$name.err"; rc=$?
   if fatal $rc; then echo "fatal $rc"; exit $rc; fi
   python3 -c "
@@ -25,7 +25,7 @@ for l in open('$OUT/cfg_$name.jsonl'):
         d=json.loads(l); print('   ', d['config'], d['stage'][:60], d['msps'], d.get('real_time_factor'))
 "
   echo "== $name c2"
-  GSDR_LIB=$LIB timeout -k 10 240 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline > "$OUT/c2_$name.json" \
+  env ${LIB:+GSDR_LIB=$LIB} timeout -k 10 240 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline > "$OUT/c2_$name.json" \
       2> "$OUT/c2_$name.err"; rc=$?
   if fatal $rc; then echo "fatal $rc"; exit $rc; fi
   python3 -c "

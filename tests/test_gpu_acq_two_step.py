@@ -71,8 +71,10 @@ def _check(acq, sats, prns, codes, x1, coarse, sel, fine, fs, N, pfa, nbins2, st
 
 
 @pytest.mark.parametrize("fs,pfa,pfa2", [(4000000, 0.01, 0.0), (4000000, 0.01, 0.001), (3000000, 0.01, 0.0),
-                                         (4000000, 0.0, 0.0)])
+                                         (4000000, 0.0, 0.0), (25000000, 0.01, 0.0), (25000000, 0.0, 0.0)])
 def test_two_steps_parity(fs, pfa, pfa2):
+    """25 Msps: N = 25000 on the split register four-step (coarse grid with two reused
+    forward spectra, the narrow grid's selected rows on the split plan)."""
     N = fs // 1000
     nbins2, step2 = 5, 100.0
     out = _run_two_steps(fs, N, pfa, nbins2, step2, pfa2)

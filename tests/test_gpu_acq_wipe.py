@@ -193,3 +193,21 @@ def test_exact_carrier_vs_reference_protokernels(cfg_name):
           "reuse": list(acq.spectrum_reuse), "exact_cells": int(exact_cells),
           "peak_rel_max": {k: float("%.3g" % v) for k, v in worst.items()}})
     assert exact_cells >= len(cfg["prns"]) - 1
+
+
+def test_grid_dump_with_reuse_at_split_size():
+    """gsdr_acq_dump_grid (the reference's dump grid, pcps_acquisition.cc:408-508) at a
+    split size with reused spectra (C5 GPS: N = 25000, 4 spectra per block) against the
+    oracle's exact-carrier grid."""
+    fs, N, dmax, dstep = 25000000, 25000, 10000, 250
+    sats = synth.random_constellation(4, seed_offset=41)
+    x = synth.gps_l1_iq(fs, N, sats, seed_offset=41)
+    prns = np.array([sats[0].prn, 32])
+    codes = np.stack([synth.gps_ca_sampled(int(p), fs, N) for p in prns])
+    acq = gsdr.Acquisition(fs, N, dmax, dstep, pfa=0.01, max_prns=2)
+    acq.set_local_codes(codes, prns)
+    assert acq.spectrum_reuse == (4, 1)
+    g = acq.dump_grid(x, 0)
+    wipe = pcps.doppler_wipeoffs(fs, N, dmax, dstep, acq.num_doppler_bins)
+    M = pcps.magnitude_grid(x, wipe, pcps.fft_code(codes[0], N, N))
+    assert np.max(np.abs(g - M)) <= 1e-5 * M.max()

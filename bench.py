@@ -715,15 +715,23 @@ def main():
             trk.run_device(iq_long.data_ptr(), 0, (W + K + 1) * total * N, nsteps * total, trk_out.data_ptr(),
                            trk_n.data_ptr())
 
+    step_no = [0]
+
     def step():
         if do_trk and not args.trk_stream:
             trk.restore_state(0)
             trk.run_device(iq_dev.data_ptr(), 0, total * N, total, trk_out.data_ptr(), trk_n.data_ptr())
         if args.only != "trk":
+            # with the continuous stream each step acquires its own span of it (new HBM
+            # addresses every step, as a receiver's ingest would be; not the same 2 MB
+            # re-read from L2 / MALL)
+            span = step_no[0] % (W + K + 1) if args.trk_stream else 0
+            src = iq_long if args.trk_stream else iq_dev
             for i, a in enumerate(acqs):
                 b0 = lo + i * Bc
-                a.run_device(iq_dev.data_ptr() + b0 * N * 8, Bc, N, b0 * N,
+                a.run_device(src.data_ptr() + (span * total + b0) * N * 8, Bc, N, (span * total + b0) * N,
                              res_dev.data_ptr() + i * Bc * P * gsdr.ACQ_RESULT_DTYPE.itemsize)
+        step_no[0] += 1
 
     if args.trk_stream:
         trk_stream_launch(W)
@@ -836,6 +844,8 @@ def main():
             "cu_partition": ({"tracking": args.trk_cus or nloc, "acquisition": 256 - (args.trk_cus or nloc)}
                              if args.cu_partition else None),
             "acq_chains": nch,
+            "acq_input": ("each step acquires its own span of the continuous stream (new HBM addresses)"
+                          if args.trk_stream else "the same span every step"),
             # the carrier model and the forward spectra computed per block (include/gsdr.h
             # gsdr_acq_set_wipeoff / gsdr_acq_get_spectrum_reuse)
             "carrier": ["exact", "generic", "avx2"][acqs[0].wipe_mode],
@@ -940,10 +950,12 @@ def main():
             return time.perf_counter() - t
 
         def acq_only():
-            for _ in range(K):
+            for k in range(K):
+                span = k if args.trk_stream else 0  # the timed region's spans (step())
+                src = iq_long if args.trk_stream else iq_dev
                 for i, a in enumerate(acqs):
                     b0 = lo + i * Bc
-                    a.run_device(iq_dev.data_ptr() + b0 * N * 8, Bc, N, b0 * N,
+                    a.run_device(src.data_ptr() + (span * total + b0) * N * 8, Bc, N, (span * total + b0) * N,
                                  res_dev.data_ptr() + i * Bc * P * gsdr.ACQ_RESULT_DTYPE.itemsize)
 
         def trk_only():

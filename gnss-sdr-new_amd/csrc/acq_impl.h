@@ -2333,7 +2333,8 @@ size_t item_bytes(int it) { return it == GSDR_ITEM_CSHORT ? 4 : (it == GSDR_ITEM
     X(62, (gsdr::pk::PkPlan<256, true, 20, 10, 10>), 1, 1, 1)           \
     X(93, (gsdr::pk::PkPlan<1024, 1, 16, 10, 10, 10>), 1, 1, 2)         \
     X(94, (gsdr::pk::PkPlan<1024, 1, 16, 10, 10, 10>), 1, 1, 2)         \
-    X(70, (gsdr::pk::PkPlan<256, 1, 25, 16, 10>), 1, 1, 2)
+    X(70, (gsdr::pk::PkPlan<256, 1, 25, 16, 10>), 1, 1, 2)            \
+    X(72, (gsdr::pk::PkPlan<256, 1 | (1 << 9), 25, 16, 10>), 1, 1, 2)
 
 template <class PT>
 int set_lds_attrs(size_t bytes)

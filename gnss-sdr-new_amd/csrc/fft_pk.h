@@ -375,6 +375,10 @@ __device__ __forceinline__ void stage(c2* lds, const float2* __restrict__ tw, Lo
     // stage needs none (its caller separates the next LDS writes with a barrier)
     constexpr bool LATE = ((TWP_ >> 8) & 1) != 0;
     constexpr bool DEFER = LATE && !FIRST && !LAST;
+    // LASTNB (TWP_ bit 9): only the last stage's read barrier dropped -- it writes no
+    // LDS, and every caller separates the next transform's LDS writes by a barrier of
+    // its own (the correlate's row-statistic exchange, FourStepPkPlan's per-row sync)
+    constexpr bool LASTNB = ((TWP_ >> 9) & 1) != 0;
     // elements before the TWP 3 table: N plus the last-stage pads (this stage is
     // the penultimate one whenever it reads the table)
     constexpr int DATA = N + (N / (Ns * R) - 1) * PADL;
@@ -416,7 +420,7 @@ __device__ __forceinline__ void stage(c2* lds, const float2* __restrict__ tw, Lo
         }
     if constexpr (FIRST)
         hook();
-    else if constexpr (!LATE)
+    else if constexpr (!LATE && !(LAST && LASTNB))
         __syncthreads();
     int kk[BPT];
 #pragma unroll

@@ -23,6 +23,9 @@ using Wl25kW = RegFourStep<25, 1024, 0, 1, NoPads<1000>, 10, 10, 10>;    // one 
 using Wl32k = RegFourStep<32, 1024, 0, 1, NoPads<1000>, 10, 10, 10>;     // rounds 16 + 16 (128 KB)
 using Wl32kP = RegFourStep<32, 1024, 0, 1, Pads1000, 10, 10, 10>;        // the same, bank-model pads
 using Wl16k = RegFourStep<16, 512, 0, 1, NoPads<1000>, 10, 10, 10>;      // rounds 8 + 8 (64 KB)
+//   50000 = 25 x (20 x 10 x 10): 512 lanes, four columns per lane (100 complex in
+//           VGPRs), one 2000-point row per wave, rounds 8 + 8 + 8 + 1 (128 KB)
+using Wl50k = RegFourStep<25, 512, 0, 1, NoPads<2000>, 20, 10, 10>;
 
 // split ids: (N, outer radix ROUT, inner plan)
 //   1: 25000 = 1 x 25000 (C5 GPS L1 / BeiDou B1I at 25 Msps, 1 ms)
@@ -34,7 +37,8 @@ using Wl16k = RegFourStep<16, 512, 0, 1, NoPads<1000>, 10, 10, 10>;      // roun
 // wave-local rows:
 //   11: 25000 (Wl25k)   12: 32000 (Wl32k)   13: 64000 = 2 x Wl32k   14: 100000 = 4 x Wl25k
 //   15: 32000 = 2 x Wl16k   16: 64000 = 4 x Wl16k   17: 25000 (Wl25kW)   18: 100000 = 4 x Wl25kW
-//   19: 32000 (Wl32kP)   20: 64000 = 2 x Wl32kP
+//   19: 32000 (Wl32kP)   20: 64000 = 2 x Wl32kP   21: 100000 = 2 x Wl50k (half the
+//   re-read loads of 4 x 25000, one workgroup per CU)
 namespace
 {
 struct SplitId
@@ -46,7 +50,7 @@ struct SplitId
 // 64000, +4 % / +10 % over 2 / 3; the 512-lane 25000 plan keeps its LDS rounds)
 constexpr SplitId kSplits[] = {{1, 25000}, {12, 32000}, {13, 64000}, {4, 100000}, {2, 32000}, {3, 64000}, {5, 32000},
     {6, 64000}, {11, 25000}, {14, 100000}, {15, 32000}, {16, 64000}, {17, 25000}, {18, 100000}, {19, 32000},
-    {20, 64000}, {112, 32000}, {212, 32000}, {113, 64000}, {213, 64000}};
+    {20, 64000}, {21, 100000}, {112, 32000}, {212, 32000}, {113, 64000}, {213, 64000}};
 // 112 / 212, 113 / 213: timing ablations of 12 / 13 (acq_correlate_split_kernel ABL:
 // 1xx without phase 1's global loads, 2xx without phase 2) -- profiles only
 
@@ -123,6 +127,7 @@ int launch_split_arg(gsdr_acq* a, uint32_t nblocks, hipStream_t s, const gsdr_ac
         case 18: GSDR_ARG(4, Wl25kW);
         case 19: GSDR_ARG(1, Wl32kP);
         case 20: GSDR_ARG(2, Wl32kP);
+        case 21: GSDR_ARG(2, Wl50k);
         default: gsdr::set_error("internal: bad split variant %d", a->split); return GSDR_E_STATE;
         }
 #undef GSDR_ARG
@@ -168,6 +173,7 @@ int launch_split(gsdr_acq* a, uint32_t nblocks, hipStream_t s)
         case 18: return half ? launch_one<4, Wl25kW, true>(a, nblocks, s) : launch_one<4, Wl25kW, false>(a, nblocks, s);
         case 19: return half ? launch_one<1, Wl32kP, true>(a, nblocks, s) : launch_one<1, Wl32kP, false>(a, nblocks, s);
         case 20: return half ? launch_one<2, Wl32kP, true>(a, nblocks, s) : launch_one<2, Wl32kP, false>(a, nblocks, s);
+        case 21: return half ? launch_one<2, Wl50k, true>(a, nblocks, s) : launch_one<2, Wl50k, false>(a, nblocks, s);
         case 112: return launch_one<1, Wl32k, false, 1>(a, nblocks, s);
         case 212: return launch_one<1, Wl32k, false, 2>(a, nblocks, s);
         case 113: return launch_one<2, Wl32k, true, 1>(a, nblocks, s);
@@ -193,7 +199,7 @@ int setup_split(gsdr_acq* a)
     if (mode == 0) return GSDR_OK;
     for (const SplitId& sp : kSplits)
         if (sp.n == a->N && !a->split) a->split = sp.id;
-    if ((a->split == 14 || a->split == 18) && mode < 2) a->split = 0;
+    if ((a->split == 14 || a->split == 18 || a->split == 21) && mode < 2) a->split = 0;
     // experiments: GSDR_ACQ_SPLIT_ID forces a split of the handle's N
     if (const char* e = std::getenv("GSDR_ACQ_SPLIT_ID"))
         {
@@ -221,6 +227,7 @@ int setup_split(gsdr_acq* a)
         case 18: rc = attrs_one<4, Wl25kW, true>() | attrs_one<4, Wl25kW, false>(); break;
         case 19: rc = attrs_one<1, Wl32kP, true>() | attrs_one<1, Wl32kP, false>(); break;
         case 20: rc = attrs_one<2, Wl32kP, true>() | attrs_one<2, Wl32kP, false>(); break;
+        case 21: rc = attrs_one<2, Wl50k, true>() | attrs_one<2, Wl50k, false>(); break;
         case 112: rc = attrs_one<1, Wl32k, false, 1>() | attrs_one<1, Wl32k, true>() | attrs_one<1, Wl32k, false>(); break;
         case 212: rc = attrs_one<1, Wl32k, false, 2>() | attrs_one<1, Wl32k, true>() | attrs_one<1, Wl32k, false>(); break;
         case 113: rc = attrs_one<2, Wl32k, true, 1>() | attrs_one<2, Wl32k, true>() | attrs_one<2, Wl32k, false>(); break;

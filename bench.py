@@ -626,6 +626,10 @@ def main():
                     help="split the step's blocks over this many acquisition handles, each on its own stream "
                          "(2: one chain's forward spectra overlap the other's correlate grid; at most 3 with the "
                          "tracking stream, GPU_MAX_HW_QUEUES = 4)")
+    ap.add_argument("--acq-sizes", default="",
+                    help="comma list of the chains' block counts (sum = --blocks), overriding --acq-chains: unequal "
+                         "chains drift out of step, so one chain's forward / reduce / argmax launches overlap the "
+                         "other's correlate instead of coinciding with it")
     ap.add_argument("--trk-stream", action="store_true",
                     help="(default) tracking follows one continuous stream: the batch repeated end to end (Dopplers on "
                          "whole cycles per batch, so the repetition is a continuous signal), one tracking launch "
@@ -681,12 +685,18 @@ def main():
     trk_out = torch.zeros(nloc * trk_epochs * gsdr.TRK_EPOCH_DTYPE.itemsize, dtype=torch.uint8, device=dev)
     trk_n = torch.zeros(nloc, dtype=torch.int32, device=dev)
 
-    nch = max(1, args.acq_chains)
-    assert B % nch == 0, "--blocks must be a multiple of --acq-chains"
-    Bc = B // nch
+    if args.acq_sizes:
+        sizes = [int(v) for v in args.acq_sizes.split(",")]
+        assert sum(sizes) == B and min(sizes) > 0, "--acq-sizes must sum to --blocks"
+    else:
+        nch0 = max(1, args.acq_chains)
+        assert B % nch0 == 0, "--blocks must be a multiple of --acq-chains"
+        sizes = [B // nch0] * nch0
+    nch = len(sizes)
+    offs = [sum(sizes[:i]) for i in range(nch)]  # each chain's first block within the rank's span
     acqs = []
-    for _ in range(nch):
-        a = gsdr.Acquisition(FS, N, DMAX, DSTEP, pfa=PFA, max_prns=P, max_blocks=Bc, num_doppler_bins=D,
+    for i in range(nch):
+        a = gsdr.Acquisition(FS, N, DMAX, DSTEP, pfa=PFA, max_prns=P, max_blocks=sizes[i], num_doppler_bins=D,
                              device=local)
         a.set_local_codes(codes, np.arange(1, P + 1))
         acqs.append(a)
@@ -728,9 +738,9 @@ def main():
             span = step_no[0] % (W + K + 1) if args.trk_stream else 0
             src = iq_long if args.trk_stream else iq_dev
             for i, a in enumerate(acqs):
-                b0 = lo + i * Bc
-                a.run_device(src.data_ptr() + (span * total + b0) * N * 8, Bc, N, (span * total + b0) * N,
-                             res_dev.data_ptr() + i * Bc * P * gsdr.ACQ_RESULT_DTYPE.itemsize)
+                b0 = lo + offs[i]
+                a.run_device(src.data_ptr() + (span * total + b0) * N * 8, sizes[i], N, (span * total + b0) * N,
+                             res_dev.data_ptr() + offs[i] * P * gsdr.ACQ_RESULT_DTYPE.itemsize)
         step_no[0] += 1
 
     if args.trk_stream:
@@ -844,6 +854,7 @@ def main():
             "cu_partition": ({"tracking": args.trk_cus or nloc, "acquisition": 256 - (args.trk_cus or nloc)}
                              if args.cu_partition else None),
             "acq_chains": nch,
+            "acq_chain_blocks": sizes,
             "acq_input": ("each step acquires its own span of the continuous stream (new HBM addresses)"
                           if args.trk_stream else "the same span every step"),
             # the carrier model and the forward spectra computed per block (include/gsdr.h
@@ -954,9 +965,9 @@ def main():
                 span = k if args.trk_stream else 0  # the timed region's spans (step())
                 src = iq_long if args.trk_stream else iq_dev
                 for i, a in enumerate(acqs):
-                    b0 = lo + i * Bc
-                    a.run_device(src.data_ptr() + (span * total + b0) * N * 8, Bc, N, (span * total + b0) * N,
-                                 res_dev.data_ptr() + i * Bc * P * gsdr.ACQ_RESULT_DTYPE.itemsize)
+                    b0 = lo + offs[i]
+                    a.run_device(src.data_ptr() + (span * total + b0) * N * 8, sizes[i], N, (span * total + b0) * N,
+                                 res_dev.data_ptr() + offs[i] * P * gsdr.ACQ_RESULT_DTYPE.itemsize)
 
         def trk_only():
             trk.restore_state(0)

@@ -29,6 +29,11 @@ using gsdr::fft::Plan;
 // GSDR_SPLIT_TWF 1 (default since r04e: C4 bit transition +11 %): the split
 // correlate's input factor W_N^{m q} as a compile-time root per column row and one
 // table read per column instead of R (acq_correlate_split_kernel)
+// occupancy target of the mirror-pair (HERM) split correlate: 4 waves per SIMD keeps
+// two 512-lane workgroups per CU (at most 128 VGPRs)
+#ifndef GSDR_HERM_WPE
+#define GSDR_HERM_WPE 4
+#endif
 #ifndef GSDR_SPLIT_TWF
 #define GSDR_SPLIT_TWF 1
 #endif
@@ -901,10 +906,27 @@ struct RegFourStep
 
     // Phase 2 of a register four-step: the R rows (phase 1's v[c][k1], lane column
     // n2 = threadIdx.x + c NT, clamped) through LDS and the L-point row transforms.
-    template <int CPL, class Out>
+    // HC (two columns per lane, NT > L / 2): lane t holds the mirror pair a = min(t,
+    // L/2), b = L - a instead (acq_correlate_split_kernel's Hermitian code loads); the
+    // b slot is stored only for 1 <= t < L/2.
+    template <int CPL, bool HC = false, class Out>
     __device__ __forceinline__ static void phase2(gsdr::pk::c2* lds, gsdr::pk::c2 (&v)[CPL][R], Out& out)
     {
         const int wbase = (int)(threadIdx.x & ~63u);
+        static_assert(!HC || (CPL == 2 && NT > L / 2), "mirror pairs: two columns per lane");
+        auto column = [&](int c, int& n2) -> bool {
+            if constexpr (HC)
+                {
+                    const int t = (int)threadIdx.x, a = min(t, L / 2);
+                    n2 = c == 0 ? a : L - a;
+                    return c == 0 || (t >= 1 && t < L / 2);
+                }
+            else
+                {
+                    n2 = min((int)threadIdx.x + c * NT, L - 1);
+                    return L % NT == 0 || wbase + c * NT < L;
+                }
+        };
         if constexpr (!WL)
             {
 #pragma unroll
@@ -914,9 +936,9 @@ struct RegFourStep
 #pragma unroll
                         for (int c = 0; c < CPL; ++c)
                             {
-                                if (L % NT == 0 || wbase + c * NT < L)
+                                int n2;
+                                if (column(c, n2))
                                     {
-                                        const int n2 = min((int)threadIdx.x + c * NT, L - 1);
 #pragma unroll
                                         for (int i = 0; i < H; ++i) lds[i * L + n2] = v[c][h * H + i];
                                     }
@@ -937,9 +959,9 @@ struct RegFourStep
 #pragma unroll
                         for (int c = 0; c < CPL; ++c)
                             {
-                                if (L % NT == 0 || wbase + c * NT < L)
+                                int n2;
+                                if (column(c, n2))
                                     {
-                                        const int n2 = min((int)threadIdx.x + c * NT, L - 1);
 #pragma unroll
                                         for (int i = 0; i < H; ++i)
                                             if (h * H + i < R) lds[i * STR + L0::pad(n2)] = v[c][h * H + i];
@@ -1073,8 +1095,13 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(RP:
 // turns the key into the result fields.  One workgroup per transform of a
 // 100000-point row spreads the pass over ROUT x more CUs than the one-workgroup
 // recomputation (acq_argmax_four_kernel: 144 workgroups at C5 Galileo).
-template <int ROUT, class RP, bool HALF, int ABL = 0, bool ARG = false>
-__global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(RP::WPE))) acq_correlate_split_kernel(
+// HERM (real code replicas, so C[N - k] = conj(C[k]); plans with two columns per
+// lane): lane t takes the mirror columns a = min(t, L/2) and b = L - a; the code
+// value of column b at (quarter r, row R-1-n1) is conj(C) of column a at (quarter
+// ROUT-1-r, row n1), so one code load serves both columns -- 3 ROUT loads per row
+// pair instead of 4 ROUT (X of a, X of b, C of a).
+template <int ROUT, class RP, bool HALF, int ABL = 0, bool ARG = false, bool HERM = false>
+__global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(HERM ? GSDR_HERM_WPE : RP::WPE))) acq_correlate_split_kernel(
     const float2* __restrict__ X, const float2* __restrict__ code_fft, RowStat* __restrict__ stats,
     const float2* __restrict__ tw, uint32_t D, uint32_t P, uint32_t nblocks, uint32_t pgs, XMap xm,
     const gsdr_acq_result* __restrict__ sel, unsigned long long* __restrict__ keys, float* __restrict__ rowbuf,
@@ -1190,23 +1217,92 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(RP:
                     }
             }
     };
+    // HERM: the mirror-pair phase 1 (see above); v[0] = column a, v[1] = column b
+    auto phase1h = [&](auto qc) {
+        constexpr int Q = decltype(qc)::value;
+        static_assert(CPL == 2 && NT > L / 2, "mirror pairs: two columns per lane");
+        const int t = (int)threadIdx.x;
+        const int a = min(t, L / 2);
+        const int bcol = (t >= 1 && t < L / 2) ? L - a : a;  // lanes without a pair repeat a (not stored)
+        auto combine = [&](c2 z, const c2 y, int r) -> c2 {
+            const int e = ((r * Q) % ROUT) * (4 / ROUT);
+            if (e == 0) return z + y;
+            if (e == 1) return gsdr::pk::add_mi(z, y);
+            if (e == 2) return z - y;
+            return gsdr::pk::sub_mi(z, y);
+        };
+        auto pair_input = [&](auto n1c) {
+            constexpr int n1 = decltype(n1c)::value;
+            constexpr int n1b = R - 1 - n1;
+            c2 ca[ROUT];
+#pragma unroll
+            for (int r = 0; r < ROUT; ++r) ca[r] = bload(crs, a * 8, (int)((r * M + n1 * L) * 8));
+            auto mirror = [&](c2 x, c2 c) -> c2 {  // conj(x) conj(c) = conj(x c)
+                const c2 m = gsdr::pk::mul(x, c);
+                return c2{m.x, -m.y};
+            };
+            c2 za = gsdr::pk::conj_mul(bload(xrs, a * 8, n1 * L * 8), ca[0]);
+            c2 zb = mirror(bload(xrs, bcol * 8, n1b * L * 8), ca[ROUT - 1]);
+#pragma unroll
+            for (int r = 1; r < ROUT; ++r)
+                {
+                    za = combine(za, gsdr::pk::conj_mul(bload(xrs, a * 8, (int)((r * M + n1 * L) * 8)), ca[r]), r);
+                    zb = combine(zb, mirror(bload(xrs, bcol * 8, (int)((r * M + n1b * L) * 8)), ca[ROUT - 1 - r]), r);
+                }
+            if constexpr (Q > 0)
+                {
+                    if constexpr (GSDR_SPLIT_TWF)
+                        {
+                            za = gsdr::pk::mul_root<Q * n1, ROUT * R>(za);
+                            zb = gsdr::pk::mul_root<Q * n1b, ROUT * R>(zb);
+                        }
+                    else
+                        {
+                            za = gsdr::pk::mul(za, gsdr::pk::from(tw[(n1 * L + a) * Q]));
+                            zb = gsdr::pk::mul(zb, gsdr::pk::from(tw[(n1b * L + bcol) * Q]));
+                        }
+                }
+            v[0][n1] = za;
+            v[1][n1b] = zb;
+        };
+        gsdr::pk::static_for<0, R>(pair_input);
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+            {
+                const int n2 = c == 0 ? a : bcol;
+                gsdr::pk::Dft<R>::run(v[c]);
+                if constexpr (Q > 0 && GSDR_SPLIT_TWF)
+                    {
+                        const c2 w0 = gsdr::pk::from(tw[Q * n2]);
+#pragma unroll
+                        for (int k1 = 0; k1 < R; ++k1) v[c][k1] = gsdr::pk::mul(v[c][k1], w0);
+                    }
+                gsdr::pk::apply_powers<R>(v[c], gsdr::pk::from(tw[ROUT * n2]));
+            }
+    };
+    auto run_phase1 = [&](auto qc) {
+        if constexpr (HERM)
+            phase1h(qc);
+        else
+            phase1(qc);
+    };
     if constexpr (ROUT == 1)
-        phase1(std::integral_constant<int, 0>{});
+        run_phase1(std::integral_constant<int, 0>{});
     else if constexpr (ROUT == 2)
         {
             if (q == 0)
-                phase1(std::integral_constant<int, 0>{});
+                run_phase1(std::integral_constant<int, 0>{});
             else
-                phase1(std::integral_constant<int, 1>{});
+                run_phase1(std::integral_constant<int, 1>{});
         }
     else
         {
             switch (q)
                 {
-                case 0: phase1(std::integral_constant<int, 0>{}); break;
-                case 1: phase1(std::integral_constant<int, 1>{}); break;
-                case 2: phase1(std::integral_constant<int, 2>{}); break;
-                default: phase1(std::integral_constant<int, 3>{}); break;
+                case 0: run_phase1(std::integral_constant<int, 0>{}); break;
+                case 1: run_phase1(std::integral_constant<int, 1>{}); break;
+                case 2: run_phase1(std::integral_constant<int, 2>{}); break;
+                default: run_phase1(std::integral_constant<int, 3>{}); break;
                 }
         }
     struct Out
@@ -1239,7 +1335,7 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(RP:
             if (rowbuf) out.row = rowbuf + (size_t)(id / ROUT) * (HALF ? N / 2 : N);
         }
     if constexpr ((ABL & 2) == 0)
-        RP::phase2(lds, v, out);
+        RP::template phase2<CPL, HERM>(lds, v, out);
     else
         {
 #pragma unroll
@@ -2247,6 +2343,8 @@ struct gsdr_acq
     int variant{0};
     int corr_variant{0};      // 0: the generic LDS kernels; >0: a GSDR_PK_VARIANTS id (packed forward + correlate)
     int split{0};             // >0: the single-dwell split register four-step correlate (acq_split.hip)
+    bool codes_real{false};   // every local code is real (imaginary parts 0): Hermitian code spectra
+    bool herm_arg{false};     // the split ARG pass takes the mirror-pair loads too (GSDR_ACQ_HERM=2)
     uint32_t split_pgs{1};    // its PRN group per XCD pass
     int corr_stat{0};         // the variant's row statistic (1/2: argmax recomputed by acq_argmax_pk_kernel)
     size_t tw_entries{0};     // twiddle entries the packed variant reads (W_N + its per-stage table)

@@ -69,11 +69,31 @@ uint32_t prn_group(uint32_t P, uint32_t N)
 // ARG = false: the grid pass (row maxima into d_stats); ARG = true: the selected
 // rows' pass (keys into d_keys, |R|^2 rows into rowbuf for the peak ratio; the
 // caller zeroes d_keys and runs acq_argmax_split_finish_kernel)
+// plans whose lanes hold two columns with NT > L / 2: the mirror-pair (Hermitian
+// code) phase 1 applies (acq_correlate_split_kernel HERM)
+template <class RP>
+constexpr bool herm_ok = RP::CPL == 2 && RP::NT > RP::L / 2;
+
 template <int ROUT, class RP, bool HALF, int ABL = 0, bool ARG = false>
 int launch_one(gsdr_acq* a, uint32_t nblocks, hipStream_t s, const gsdr_acq_result* sel = nullptr,
     float* rowbuf = nullptr, float* psum = nullptr, uint32_t* rout = nullptr)
 {
     if (rout) *rout = ROUT;
+    if constexpr (herm_ok<RP> && ABL == 0)
+        {
+            if (a->codes_real && (!ARG || a->herm_arg))
+                {
+                    if (RP::N * ROUT != (int)a->N) return GSDR_E_STATE;
+                    if (ROUT > 1 && !ARG)
+                        GSDR_HIP(hipMemsetAsync(a->d_stats, 0, (size_t)nblocks * a->nprn * a->D * sizeof(RowStat), s));
+                    const uint32_t grid = ARG ? nblocks * a->nprn * ROUT : nblocks * a->D * a->nprn * ROUT;
+                    hipLaunchKernelGGL((acq_correlate_split_kernel<ROUT, RP, HALF, 0, ARG, true>), dim3(grid),
+                        dim3(RP::NT), RP::lds_bytes(), s, a->d_X, a->d_code_fft, a->d_stats, a->d_tw, a->D, a->nprn,
+                        nblocks, prn_group(a->nprn, a->N), a->xm, sel, a->d_keys, rowbuf, psum);
+                    GSDR_HIP(hipGetLastError());
+                    return GSDR_OK;
+                }
+        }
     static_assert(RP::N * ROUT > 0, "plan");
     if (RP::N * ROUT != (int)a->N)
         {
@@ -98,6 +118,13 @@ int attrs_one()
     if constexpr (ABL == 0)
         GSDR_HIP(hipFuncSetAttribute((const void*)acq_correlate_split_kernel<ROUT, RP, HALF, 0, true>,
             hipFuncAttributeMaxDynamicSharedMemorySize, (int)RP::lds_bytes()));
+    if constexpr (ABL == 0 && herm_ok<RP>)
+        {
+            GSDR_HIP(hipFuncSetAttribute((const void*)acq_correlate_split_kernel<ROUT, RP, HALF, 0, false, true>,
+                hipFuncAttributeMaxDynamicSharedMemorySize, (int)RP::lds_bytes()));
+            GSDR_HIP(hipFuncSetAttribute((const void*)acq_correlate_split_kernel<ROUT, RP, HALF, 0, true, true>,
+                hipFuncAttributeMaxDynamicSharedMemorySize, (int)RP::lds_bytes()));
+        }
     return GSDR_OK;
 }
 

@@ -88,7 +88,13 @@ SPLIT_IDS = {5: 32000, 6: 64000, 11: 25000, 12: 32000, 13: 64000, 14: 100000, 15
              18: 100000, 19: 32000, 20: 64000}
 
 
-@pytest.mark.parametrize("split", ["1", "0", "2"] + ["id%d" % i for i in sorted(SPLIT_IDS)])
+# plans with two columns per lane and NT > L / 2: the mirror-pair (Hermitian code)
+# correlate applies (acq_split.hip herm_ok), forced by GSDR_ACQ_HERM
+HERM_IDS = (11, 14, 15, 16)
+
+
+@pytest.mark.parametrize("split", ["1", "0", "2", "h1", "h2"] + ["id%d" % i for i in sorted(SPLIT_IDS)]
+                         + ["id%dh" % i for i in HERM_IDS])
 @pytest.mark.parametrize("fs,N,pfa", [(8000000, 32000, 0.01), (25000000, 25000, 0.0), (8000000, 64000, 0.01),
                                       (25000000, 100000, 0.01), (25000000, 25000, 0.01), (25000000, 100000, 0.0)])
 def test_large_fft_four_step(monkeypatch, fs, N, pfa, split):
@@ -97,8 +103,16 @@ def test_large_fft_four_step(monkeypatch, fs, N, pfa, split):
     configs C4/C5 -- on every correlate path: GSDR_ACQ_SPLIT=1 (default: the split
     register four-step for 25000 / 32000 / 64000 / 100000 = 4 x 25000), 0 (the packed
     four-step everywhere), 2 (also the wave-local 100000 plans when forced),
-    idK: split id K forced (SPLIT_IDS: the 16000-based splits and the wave-local-row plans).
+    idK: split id K forced (SPLIT_IDS: the 16000-based splits and the wave-local-row plans);
+    h1 / h2 / idKh: the mirror-pair code loads (GSDR_ACQ_HERM=1: the grid pass, 2: also
+    the ARG pass) on the default plans / split id K.
     Parity with the oracle grid statistics."""
+    if split.startswith("h"):
+        monkeypatch.setenv("GSDR_ACQ_HERM", split[1:])
+        split = "1"
+    elif split.endswith("h"):
+        monkeypatch.setenv("GSDR_ACQ_HERM", "2")
+        split = split[:-1]
     if split.startswith("id"):
         # a forced split of this N (acq_split.hip: 5 = 2 x 16000, 6 = 4 x 16000)
         if SPLIT_IDS[int(split[2:])] != N:

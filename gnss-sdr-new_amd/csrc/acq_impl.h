@@ -2425,7 +2425,11 @@ size_t item_bytes(int it) { return it == GSDR_ITEM_CSHORT ? 4 : (it == GSDR_ITEM
 // wave-local row transforms (RegFourStep H = 0).  The alternatives
 // measured in rounds 1-2 (other radix orders, per-stage twiddle tables, LDS root
 // copies, padded layouts, late barriers, 5 waves, PRN groups)
-// were within noise of or slower than these and are no longer built.
+// were within noise of or slower than these and are no longer built.  Round 4
+// (profiles/r04t): variant 70 at 104 VGPRs runs 4 workgroups (16 waves) per CU; 5
+// per CU (waves-per-EU 5: 96 VGPRs + 36 B/lane spills, or the code loaded in the
+// first stage without the prefetch: 61 VGPRs) measured 19 % slower, and 3 / 2 per
+// CU (GSDR_PK_LDS_EXTRA bytes of LDS padding per workgroup) 8 % / 26 % slower.
 #define GSDR_PK_VARIANTS(X)                                              \
     X(61, (gsdr::pk::PkPlan<512, true, 20, 20, 20>), 1, 1, 1)           \
     X(62, (gsdr::pk::PkPlan<256, true, 20, 10, 10>), 1, 1, 1)           \

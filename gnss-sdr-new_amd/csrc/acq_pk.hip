@@ -1,5 +1,6 @@
 // Packed-f32 correlate-kernel variants for N = 4000 (the C2 bench configuration):
 // launch and one-time setup, selected by gsdr_acq::corr_variant.
+#include <cstdlib>
 #include "acq_impl.h"
 
 namespace gsdr_acq_impl
@@ -121,6 +122,8 @@ int setup_corr_variant(gsdr_acq* a, int v)
         {                                                                                                       \
             using M = GSDR_UNPAREN MP;                                                                          \
             a->corr_lds_bytes = M::lds_bytes() + (size_t)2 * (M::NT / 64) * sizeof(RowStat);                   \
+            /* A/B knob: LDS padding per workgroup caps the workgroups per CU */                               \
+            if (const char* e = std::getenv("GSDR_PK_LDS_EXTRA")) a->corr_lds_bytes += (size_t)std::atoi(e);  \
             GSDR_HIP(hipFuncSetAttribute((const void*)acq_correlate_pk_kernel<M, PG, WPE, ST>,                  \
                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)a->corr_lds_bytes));                           \
             GSDR_HIP(hipFuncSetAttribute((const void*)acq_argmax_pk_kernel<M, ST>,                              \

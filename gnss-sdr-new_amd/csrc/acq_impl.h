@@ -31,6 +31,10 @@ using gsdr::fft::Plan;
 // table read per column instead of R (acq_correlate_split_kernel)
 // occupancy target of the mirror-pair (HERM) split correlate: 4 waves per SIMD keeps
 // two 512-lane workgroups per CU (at most 128 VGPRs)
+// occupancy target of the split ARG pass (one selected row per (b, p): few workgroups)
+#ifndef GSDR_ARG_WPE
+#define GSDR_ARG_WPE 1
+#endif
 #ifndef GSDR_HERM_WPE
 #define GSDR_HERM_WPE 4
 #endif
@@ -1101,7 +1105,7 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(RP:
 // ROUT-1-r, row n1), so one code load serves both columns -- 3 ROUT loads per row
 // pair instead of 4 ROUT (X of a, X of b, C of a).
 template <int ROUT, class RP, bool HALF, int ABL = 0, bool ARG = false, bool HERM = false>
-__global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(HERM ? GSDR_HERM_WPE : RP::WPE))) acq_correlate_split_kernel(
+__global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(HERM ? GSDR_HERM_WPE : (ARG ? GSDR_ARG_WPE : RP::WPE)))) acq_correlate_split_kernel(
     const float2* __restrict__ X, const float2* __restrict__ code_fft, RowStat* __restrict__ stats,
     const float2* __restrict__ tw, uint32_t D, uint32_t P, uint32_t nblocks, uint32_t pgs, XMap xm,
     const gsdr_acq_result* __restrict__ sel, unsigned long long* __restrict__ keys, float* __restrict__ rowbuf,

@@ -1,6 +1,7 @@
 // Split register four-step correlate (acq_correlate_split_kernel, acq_impl.h) for
 // the FFT sizes of configs C4 / C5 beyond the LDS engine: plan choice, launch and
 // one-time setup, selected by gsdr_acq::split.
+#include <cstdlib>
 #include "acq_impl.h"
 
 namespace gsdr_acq_impl
@@ -60,9 +61,14 @@ constexpr SplitId kSplits[] = {{1, 25000}, {12, 32000}, {13, 64000}, {4, 100000}
 uint32_t prn_group(uint32_t P, uint32_t N)
 {
     const size_t row = (size_t)N * sizeof(float2);
+    // code bytes per group walked by every XCD at once (A/B knob GSDR_ACQ_PGS_KB)
+    static const size_t cap = [] {
+        const char* e = std::getenv("GSDR_ACQ_PGS_KB");
+        return e ? (size_t)std::atoi(e) << 10 : (size_t)2 << 20;
+    }();
     uint32_t best = 1;
     for (uint32_t g = 1; g <= P; ++g)
-        if (P % g == 0 && (size_t)g * row <= (2u << 20)) best = g;
+        if (P % g == 0 && (size_t)g * row <= cap) best = g;
     return best;
 }
 

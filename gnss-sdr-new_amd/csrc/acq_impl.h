@@ -541,7 +541,10 @@ __global__ void __launch_bounds__(PT::NT) acq_correlate_kernel(const float2* __r
 // PG < 0: groups of -PG PRNs without the next-code prefetch (the code values are
 // loaded by the first stage itself) -- for plans whose registers cannot hold
 // both first-stage operand sets through a transform (N = 16000 on 1024 lanes).
-constexpr int pg_count(int pg) { return pg < 0 ? -pg : pg; }
+// PG == 0: one PRN per workgroup with the first stage's products conj(X) C formed
+// in two halves of its rows before the transform (half the operand registers in
+// flight; a scheduling barrier keeps the second half's loads behind the first's).
+constexpr int pg_count(int pg) { return pg < 0 ? -pg : (pg == 0 ? 1 : pg); }
 
 template <class MP, int PG_, int WPE, int STAT>
 __global__ void __launch_bounds__(MP::NT) __attribute__((amdgpu_waves_per_eu(WPE))) acq_correlate_pk_kernel(const float2* __restrict__ X,
@@ -550,6 +553,7 @@ __global__ void __launch_bounds__(MP::NT) __attribute__((amdgpu_waves_per_eu(WPE
 {
     constexpr int PG = pg_count(PG_);
     constexpr bool PREFETCH = PG_ > 0;
+    constexpr bool HALVES = PG_ == 0;
     static_assert(STAT == 1 || STAT == 2 || STAT == 3, "row statistic 1 (max + sum), 2 (max) or 3 (max, atomic)");
     using gsdr::pk::c2;
     constexpr int NT = MP::NT;
@@ -594,6 +598,35 @@ __global__ void __launch_bounds__(MP::NT) __attribute__((amdgpu_waves_per_eu(WPE
     // lanes' clamped, in-bounds copies keep every register defined, so no
     // zero-fill code); a wave with none skips the loads
     c2 xr[BPT1][R1], cr[BPT1][R1];
+    if constexpr (HALVES)
+        {
+            // xr <- the products, rows [0, R1/2) then [R1/2, R1)
+            auto half = [&](auto r0c, auto r1c) {
+                constexpr int r0 = decltype(r0c)::value, r1 = decltype(r1c)::value;
+#pragma unroll
+                for (int bb = 0; bb < BPT1; ++bb)
+                    {
+                        const int j = (int)threadIdx.x + bb * NT;
+                        const int j0 = (int)(threadIdx.x & ~63u) + bb * NT;
+                        if (NB1 % NT == 0 || j0 < NB1)
+                            {
+                                const int jj = min(j, NB1 - 1);
+#pragma unroll
+                                for (int r = r0; r < r1; ++r)
+                                    {
+                                        xr[bb][r] = bload(xrs, jj * 8, r * NB1 * 8);
+                                        cr[bb][r] = bload(crs, jj * 8, r * NB1 * 8);
+                                    }
+#pragma unroll
+                                for (int r = r0; r < r1; ++r) xr[bb][r] = gsdr::pk::conj_mul(xr[bb][r], cr[bb][r]);
+                            }
+                    }
+            };
+            half(std::integral_constant<int, 0>{}, std::integral_constant<int, R1 / 2>{});
+            __builtin_amdgcn_sched_barrier(0);
+            half(std::integral_constant<int, R1 / 2>{}, std::integral_constant<int, R1>{});
+        }
+    else
 #pragma unroll
     for (int bb = 0; bb < BPT1; ++bb)
         {
@@ -615,7 +648,9 @@ __global__ void __launch_bounds__(MP::NT) __attribute__((amdgpu_waves_per_eu(WPE
             {
                     float rmax = 0.0f, sum = 0.0f;
                     auto load = [&](int bb, int r, int i) -> c2 {
-                        if constexpr (PREFETCH)
+                        if constexpr (HALVES)
+                            return xr[bb][r];
+                        else if constexpr (PREFETCH)
                             return gsdr::pk::conj_mul(xr[bb][r], cr[bb][r]);
                         else
                             return gsdr::pk::conj_mul(xr[bb][r], bload(crs, i * 8, (int)(q * N * 8)));
@@ -2433,7 +2468,10 @@ size_t item_bytes(int it) { return it == GSDR_ITEM_CSHORT ? 4 : (it == GSDR_ITEM
 // (profiles/r04t): variant 70 at 104 VGPRs runs 4 workgroups (16 waves) per CU; 5
 // per CU (waves-per-EU 5: 96 VGPRs + 36 B/lane spills, or the code loaded in the
 // first stage without the prefetch: 61 VGPRs) measured 19 % slower, and 3 / 2 per
-// CU (GSDR_PK_LDS_EXTRA bytes of LDS padding per workgroup) 8 % / 26 % slower.
+// CU (GSDR_PK_LDS_EXTRA bytes of LDS padding per workgroup) 8 % / 26 % slower;
+// 5 per CU without spills (PG 0: the first-stage products formed in two halves,
+// 96 VGPRs) 2 % slower, the same as the two halves at 4 per CU (r04y): beyond 4
+// workgroups the CU's issue, not latency, bounds the transform.
 #define GSDR_PK_VARIANTS(X)                                              \
     X(61, (gsdr::pk::PkPlan<512, true, 20, 20, 20>), 1, 1, 1)           \
     X(62, (gsdr::pk::PkPlan<256, true, 20, 10, 10>), 1, 1, 1)           \

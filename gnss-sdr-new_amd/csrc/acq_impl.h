@@ -2471,7 +2471,9 @@ size_t item_bytes(int it) { return it == GSDR_ITEM_CSHORT ? 4 : (it == GSDR_ITEM
 // CU (GSDR_PK_LDS_EXTRA bytes of LDS padding per workgroup) 8 % / 26 % slower;
 // 5 per CU without spills (PG 0: the first-stage products formed in two halves,
 // 96 VGPRs) 2 % slower, the same as the two halves at 4 per CU (r04y): beyond 4
-// workgroups the CU's issue, not latency, bounds the transform.
+// workgroups the CU's issue, not latency, bounds the transform.  Twiddles from the
+// per-stage table instead of powers of one root (TWP 2, 16-byte loads: -23 %) or
+// the middle stage's roots from an LDS copy (TWP 3: -2.5 %) did not pay (r04z).
 #define GSDR_PK_VARIANTS(X)                                              \
     X(61, (gsdr::pk::PkPlan<512, true, 20, 20, 20>), 1, 1, 1)           \
     X(62, (gsdr::pk::PkPlan<256, true, 20, 10, 10>), 1, 1, 1)           \

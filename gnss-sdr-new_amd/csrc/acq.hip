@@ -247,6 +247,21 @@ int gsdr_acq_create(int device, const gsdr_acq_conf* conf, gsdr_acq** out)
     // split path: the selected rows' first-maximum keys (acq_correlate_split_kernel<ARG>)
     if (e == hipSuccess && a->split > 0) e = hipMalloc(&a->d_keys, nB * nP * sizeof(unsigned long long));
     if (e == hipSuccess && a->split > 0) e = hipMalloc(&a->d_psum, nB * nP * 4 * sizeof(float));
+    // split path, opt-in: the outer DIF step as its own pass (acq_split_pre_kernel)
+    {
+        const char* pe = std::getenv("GSDR_ACQ_PRE");
+        a->pre = pe && std::atoi(pe) != 0;
+        if (a->split > 0 && a->pre)
+            {
+                // chunks of GSDR_ACQ_PRE PRNs (>= max_prns: the whole set in one pass), two buffers
+                const uint32_t c = (uint32_t)std::atoi(pe);
+                a->pre_chunk = c < nP ? c : (uint32_t)nP;
+                const size_t nbuf = a->pre_chunk < nP ? 2 : 1;
+                if (e == hipSuccess) e = hipMalloc(&a->d_pre, nbuf * nB * a->D * a->pre_chunk * N * sizeof(float2));
+                if (e == hipSuccess) e = hipStreamCreateWithFlags(&a->pre_stream, hipStreamNonBlocking);
+                for (int i = 0; i < 4 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&a->pre_ev[i], hipEventDisableTiming);
+            }
+    }
     // split path: the two-launch forward's scratch rows (GSDR_ACQ_FWD2=0: the
     // one-workgroup-per-spectrum forward)
     {
@@ -324,9 +339,12 @@ void gsdr_acq_destroy(gsdr_acq* a)
         }
     for (hipEvent_t e : a->prof_pool) (void)hipEventDestroy(e);
     void* bufs[] = {a->st2.d_wipe, a->st2.d_freq, a->d_tw, a->d_wipe, a->d_code_fft, a->d_code_stage, a->d_prn, a->d_X, a->d_stats, a->d_res,
-        a->d_iq, a->d_grid, a->d_rowbuf, a->d_keys, a->d_psum, a->d_fscratch, a->d_dgrid, a->d_tw_sub, a->d_scratch, a->d_slots, a->d_resk, a->d_acc, a->d_acc_slots};
+        a->d_iq, a->d_grid, a->d_rowbuf, a->d_keys, a->d_psum, a->d_pre, a->d_fscratch, a->d_dgrid, a->d_tw_sub, a->d_scratch, a->d_slots, a->d_resk, a->d_acc, a->d_acc_slots};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
+    for (hipEvent_t ev : a->pre_ev)
+        if (ev) (void)hipEventDestroy(ev);
+    if (a->pre_stream) (void)hipStreamDestroy(a->pre_stream);
     if (a->stream) (void)hipStreamDestroy(a->stream);
     delete a;
 }

@@ -1139,16 +1139,64 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(RP:
 // value of column b at (quarter r, row R-1-n1) is conj(C) of column a at (quarter
 // ROUT-1-r, row n1), so one code load serves both columns -- 3 ROUT loads per row
 // pair instead of 4 ROUT (X of a, X of b, C of a).
-template <int ROUT, class RP, bool HALF, int ABL = 0, bool ARG = false, bool HERM = false>
+// The split plan's outer decimation-in-frequency step as its own pass (GSDR_ACQ_PRE):
+// for every (row, p) and q < ROUT the M-point sub-transform input
+//   y_q[m] = W_N^{q m} sum_r W_ROUT^{r q} conj(X[m + r M]) C[m + r M],  m < M = N / ROUT,
+// stored contiguously, so the grid pass's workgroups read M points each instead of the
+// whole X and code rows (acq_correlate_split_kernel PRE).  Grid (ceil(M/256), rows, P).
+template <int ROUT>
+__global__ void __launch_bounds__(256) acq_split_pre_kernel(const float2* __restrict__ X,
+    const float2* __restrict__ code_fft, float2* __restrict__ Y, const float2* __restrict__ tw, uint32_t D,
+    uint32_t P, uint32_t M, XMap xm, uint32_t p0 = 0)
+{
+    using gsdr::pk::c2;
+    const uint32_t m = blockIdx.x * 256u + threadIdx.x;
+    if (m >= M) return;
+    const uint32_t row = blockIdx.y, p = blockIdx.z;
+    const uint32_t b = row / D, d = row - (row / D) * D;
+    const size_t N = (size_t)M * ROUT;
+    const float2* x = X + xm.off(b, d);
+    const float2* c = code_fft + (size_t)(p0 + p) * N;  // Y: chunk-local p
+    c2 pr[ROUT];
+#pragma unroll
+    for (int r = 0; r < ROUT; ++r)
+        pr[r] = gsdr::pk::conj_mul(gsdr::pk::from(x[m + (size_t)r * M]), gsdr::pk::from(c[m + (size_t)r * M]));
+    float2* y = Y + ((size_t)row * P + p) * ROUT * M + m;
+#pragma unroll
+    for (int q = 0; q < ROUT; ++q)
+        {
+            c2 z = pr[0];
+#pragma unroll
+            for (int r = 1; r < ROUT; ++r)
+                {
+                    const int e = ((r * q) % ROUT) * (4 / ROUT);
+                    if (e == 0)
+                        z = z + pr[r];
+                    else if (e == 1)
+                        z = gsdr::pk::add_mi(z, pr[r]);
+                    else if (e == 2)
+                        z = z - pr[r];
+                    else
+                        z = gsdr::pk::sub_mi(z, pr[r]);
+                }
+            if (q > 0) z = gsdr::pk::mul(z, gsdr::pk::from(tw[(size_t)q * m]));
+            y[(size_t)q * M] = gsdr::pk::to(z);
+        }
+}
+
+template <int ROUT, class RP, bool HALF, int ABL = 0, bool ARG = false, bool HERM = false, bool PRE = false>
 __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(HERM ? GSDR_HERM_WPE : (ARG ? GSDR_ARG_WPE : RP::WPE)))) acq_correlate_split_kernel(
     const float2* __restrict__ X, const float2* __restrict__ code_fft, RowStat* __restrict__ stats,
     const float2* __restrict__ tw, uint32_t D, uint32_t P, uint32_t nblocks, uint32_t pgs, XMap xm,
     const gsdr_acq_result* __restrict__ sel, unsigned long long* __restrict__ keys, float* __restrict__ rowbuf,
-    float* __restrict__ psum)
+    float* __restrict__ psum, uint32_t pchunk = 0)
 {
     using gsdr::pk::c2;
     constexpr int R = RP::R, NT = RP::NT, L = RP::L, CPL = RP::CPL;
     constexpr uint32_t M = RP::N;
+    // pchunk (PRE, chunked): PRNs [p_base, p_base + P) of P_all, so the row statistic
+    // lands at the handle's (b, p_base + p, d)
+    const uint32_t P_all = pchunk ? (pchunk & 0xffffu) : P, p_base = pchunk >> 16;
     constexpr uint32_t N = M * ROUT;
     constexpr int NW = NT / 64;
     extern __shared__ float2 lds_raw[];
@@ -1185,8 +1233,10 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(HER
         }
     const uint32_t p = pv / ROUT, q = pv - p * ROUT;
     const uint32_t b = row / D, d = row - (row / D) * D;
+    // PRE: X holds acq_split_pre_kernel's sub-transform inputs, M per (row, p, q)
     const auto xrs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float2*>(X) + xm.off(b, d), 0, (int)(N * sizeof(c2)), 0x00020000);
+        const_cast<float2*>(X) + (PRE ? (((size_t)row * P + p) * ROUT + q) * M : xm.off(b, d)), 0,
+        (int)((PRE ? M : N) * sizeof(c2)), 0x00020000);
     const auto crs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float2*>(code_fft) + (size_t)p * N, 0, (int)(N * sizeof(c2)), 0x00020000);
     auto bload = [](decltype(xrs) rs, int voff, int soff) -> c2 {
@@ -1319,8 +1369,25 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(HER
                 gsdr::pk::apply_powers<R>(v[c], gsdr::pk::from(tw[ROUT * n2]));
             }
     };
+    // PRE: the inputs arrive combined and twiddled; only the column DFTs remain
+    auto phase1p = [&](auto) {
+#pragma unroll
+        for (int c = 0; c < CPL; ++c)
+            {
+                if (L % NT == 0 || wbase + c * NT < L)
+                    {
+                        const int n2 = min((int)threadIdx.x + c * NT, L - 1);
+#pragma unroll
+                        for (int n1 = 0; n1 < R; ++n1) v[c][n1] = bload(xrs, n2 * 8, n1 * L * 8);
+                        gsdr::pk::Dft<R>::run(v[c]);
+                        gsdr::pk::apply_powers<R>(v[c], gsdr::pk::from(tw[ROUT * n2]));
+                    }
+            }
+    };
     auto run_phase1 = [&](auto qc) {
-        if constexpr (HERM)
+        if constexpr (PRE)
+            phase1p(qc);
+        else if constexpr (HERM)
             phase1h(qc);
         else
             phase1(qc);
@@ -1441,7 +1508,7 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(HER
             float best = red[0];
 #pragma unroll
             for (int w2 = 1; w2 < NW; ++w2) best = __builtin_fmaxf(best, red[w2]);
-            RowStat* st = stats + ((size_t)b * P + p) * D + d;
+            RowStat* st = stats + ((size_t)b * P_all + p_base + p) * D + d;
             if constexpr (ROUT == 1)
                 *st = RowStat{best, 0u, 0.0f, 0};
             else  // non-negative floats order as their bit patterns (row zeroed by the host)
@@ -2384,6 +2451,11 @@ struct gsdr_acq
     int split{0};             // >0: the single-dwell split register four-step correlate (acq_split.hip)
     bool codes_real{false};   // every local code is real (imaginary parts 0): Hermitian code spectra
     bool herm_arg{false};     // the split ARG pass takes the mirror-pair loads too (GSDR_ACQ_HERM=2)
+    bool pre{false};          // split grid pass through acq_split_pre_kernel (GSDR_ACQ_PRE=1)
+    float2* d_pre{nullptr};   // its sub-transform inputs: two chunks of pre_chunk PRNs (nblocks * D * N each)
+    uint32_t pre_chunk{0};    // PRNs per chunk; chunk i + 1's pass overlaps chunk i's grid pass
+    hipStream_t pre_stream{nullptr};
+    hipEvent_t pre_ev[4]{};   // [0,1] chunk inputs written (per buffer), [2,3] buffer read
     uint32_t split_pgs{1};    // its PRN group per XCD pass
     int corr_stat{0};         // the variant's row statistic (1/2: argmax recomputed by acq_argmax_pk_kernel)
     size_t tw_entries{0};     // twiddle entries the packed variant reads (W_N + its per-stage table)

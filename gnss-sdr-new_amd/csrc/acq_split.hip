@@ -109,6 +109,37 @@ int launch_one(gsdr_acq* a, uint32_t nblocks, hipStream_t s, const gsdr_acq_resu
     if (ROUT > 1 && !ARG)
         GSDR_HIP(hipMemsetAsync(a->d_stats, 0, (size_t)nblocks * a->nprn * a->D * sizeof(RowStat), s));
     const uint32_t grid = ARG ? nblocks * a->nprn * ROUT : nblocks * a->D * a->nprn * ROUT;
+    if constexpr (ROUT > 1 && ABL == 0 && !ARG)
+        {
+            if (a->pre && a->d_pre)
+                {
+                    // the outer DIF step as its own pass, then M-point sub-transforms; in
+                    // chunks of pre_chunk PRNs over two buffers, chunk i + 1's pass on
+                    // pre_stream overlapping chunk i's grid pass on s
+                    constexpr uint32_t M = RP::N;
+                    const uint32_t C = a->pre_chunk, P = a->nprn;
+                    const size_t per = (size_t)nblocks * a->D * C * a->N;  // buffer stride (complex)
+                    GSDR_HIP(hipEventRecord(a->pre_ev[2], s));  // s's earlier work (the forward spectra, the memset)
+                    GSDR_HIP(hipStreamWaitEvent(a->pre_stream, a->pre_ev[2], 0));
+                    for (uint32_t p0 = 0, i = 0; p0 < P; p0 += C, ++i)
+                        {
+                            const uint32_t np = P - p0 < C ? P - p0 : C, k = i & 1;
+                            float2* buf = a->d_pre + k * per;
+                            if (i >= 2) GSDR_HIP(hipStreamWaitEvent(a->pre_stream, a->pre_ev[2 + k], 0));
+                            hipLaunchKernelGGL((acq_split_pre_kernel<ROUT>), dim3((M + 255) / 256, nblocks * a->D, np),
+                                dim3(256), 0, a->pre_stream, a->d_X, a->d_code_fft, buf, a->d_tw, a->D, np, M, a->xm, p0);
+                            GSDR_HIP(hipEventRecord(a->pre_ev[k], a->pre_stream));
+                            GSDR_HIP(hipStreamWaitEvent(s, a->pre_ev[k], 0));
+                            hipLaunchKernelGGL((acq_correlate_split_kernel<ROUT, RP, HALF, 0, false, false, true>),
+                                dim3(nblocks * a->D * np * ROUT), dim3(RP::NT), RP::lds_bytes(), s, buf, a->d_code_fft,
+                                a->d_stats, a->d_tw, a->D, np, nblocks, prn_group(np, a->N), a->xm, sel, a->d_keys, rowbuf,
+                                psum, (p0 << 16) | P);
+                            GSDR_HIP(hipEventRecord(a->pre_ev[2 + k], s));
+                        }
+                    GSDR_HIP(hipGetLastError());
+                    return GSDR_OK;
+                }
+        }
     hipLaunchKernelGGL((acq_correlate_split_kernel<ROUT, RP, HALF, ABL, ARG>), dim3(grid), dim3(RP::NT),
         RP::lds_bytes(), s, a->d_X, a->d_code_fft, a->d_stats, a->d_tw, a->D, a->nprn, nblocks,
         prn_group(a->nprn, a->N), a->xm, sel, a->d_keys, rowbuf, psum);
@@ -123,6 +154,9 @@ int attrs_one()
         hipFuncAttributeMaxDynamicSharedMemorySize, (int)RP::lds_bytes()));
     if constexpr (ABL == 0)
         GSDR_HIP(hipFuncSetAttribute((const void*)acq_correlate_split_kernel<ROUT, RP, HALF, 0, true>,
+            hipFuncAttributeMaxDynamicSharedMemorySize, (int)RP::lds_bytes()));
+    if constexpr (ABL == 0 && ROUT > 1)
+        GSDR_HIP(hipFuncSetAttribute((const void*)acq_correlate_split_kernel<ROUT, RP, HALF, 0, false, false, true>,
             hipFuncAttributeMaxDynamicSharedMemorySize, (int)RP::lds_bytes()));
     if constexpr (ABL == 0 && herm_ok<RP>)
         {

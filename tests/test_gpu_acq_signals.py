@@ -93,7 +93,7 @@ SPLIT_IDS = {5: 32000, 6: 64000, 11: 25000, 12: 32000, 13: 64000, 14: 100000, 15
 HERM_IDS = (11, 14, 15, 16)
 
 
-@pytest.mark.parametrize("split", ["1", "0", "2", "h1", "h2"] + ["id%d" % i for i in sorted(SPLIT_IDS)]
+@pytest.mark.parametrize("split", ["1", "0", "2", "h1", "h2", "pre1", "pre64"] + ["id%d" % i for i in sorted(SPLIT_IDS)]
                          + ["id%dh" % i for i in HERM_IDS])
 @pytest.mark.parametrize("fs,N,pfa", [(8000000, 32000, 0.01), (25000000, 25000, 0.0), (8000000, 64000, 0.01),
                                       (25000000, 100000, 0.01), (25000000, 25000, 0.01), (25000000, 100000, 0.0)])
@@ -104,10 +104,16 @@ def test_large_fft_four_step(monkeypatch, fs, N, pfa, split):
     register four-step for 25000 / 32000 / 64000 / 100000 = 4 x 25000), 0 (the packed
     four-step everywhere), 2 (also the wave-local 100000 plans when forced),
     idK: split id K forced (SPLIT_IDS: the 16000-based splits and the wave-local-row plans);
+    preC: the split plan's outer DIF step as its own pass, C PRNs per chunk (GSDR_ACQ_PRE);
     h1 / h2 / idKh: the mirror-pair code loads (GSDR_ACQ_HERM=1: the grid pass, 2: also
     the ARG pass) on the default plans / split id K.
     Parity with the oracle grid statistics."""
-    if split.startswith("h"):
+    if split.startswith("pre"):
+        # the outer DIF step as its own pass (GSDR_ACQ_PRE: PRNs per chunk, two
+        # buffers, the next chunk's pass overlapping this one's grid; plans with ROUT > 1)
+        monkeypatch.setenv("GSDR_ACQ_PRE", split[3:])
+        split = "1"
+    elif split.startswith("h"):
         monkeypatch.setenv("GSDR_ACQ_HERM", split[1:])
         split = "1"
     elif split.endswith("h"):

@@ -18,6 +18,7 @@
 #include "acq_impl.h"
 
 #include <algorithm>
+#include <cstring>
 #include <string>
 #include <utility>
 #include "gsdr_stream_internal.h"
@@ -217,7 +218,7 @@ int gsdr_acq_create(int device, const gsdr_acq_conf* conf, gsdr_acq** out)
     const size_t nP = conf->max_prns, nB = conf->max_blocks;
     hipError_t e = hipStreamCreateWithFlags(&a->stream, hipStreamNonBlocking);
 
-    const size_t tw_n = std::max<size_t>(N, a->tw_entries);
+    const size_t tw_n = N;
     if (e == hipSuccess) e = hipMalloc(&a->d_tw, tw_n * sizeof(float2));
     if (e == hipSuccess) e = hipMalloc(&a->d_wipe, (size_t)a->D * N * sizeof(float2));
     a->d_wipe_grid = a->d_wipe;
@@ -247,28 +248,9 @@ int gsdr_acq_create(int device, const gsdr_acq_conf* conf, gsdr_acq** out)
     // split path: the selected rows' first-maximum keys (acq_correlate_split_kernel<ARG>)
     if (e == hipSuccess && a->split > 0) e = hipMalloc(&a->d_keys, nB * nP * sizeof(unsigned long long));
     if (e == hipSuccess && a->split > 0) e = hipMalloc(&a->d_psum, nB * nP * 4 * sizeof(float));
-    // split path, opt-in: the outer DIF step as its own pass (acq_split_pre_kernel)
-    {
-        const char* pe = std::getenv("GSDR_ACQ_PRE");
-        a->pre = pe && std::atoi(pe) != 0;
-        if (a->split > 0 && a->pre)
-            {
-                // chunks of GSDR_ACQ_PRE PRNs (>= max_prns: the whole set in one pass), two buffers
-                const uint32_t c = (uint32_t)std::atoi(pe);
-                a->pre_chunk = c < nP ? c : (uint32_t)nP;
-                const size_t nbuf = a->pre_chunk < nP ? 2 : 1;
-                if (e == hipSuccess) e = hipMalloc(&a->d_pre, nbuf * nB * a->D * a->pre_chunk * N * sizeof(float2));
-                if (e == hipSuccess) e = hipStreamCreateWithFlags(&a->pre_stream, hipStreamNonBlocking);
-                for (int i = 0; i < 4 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&a->pre_ev[i], hipEventDisableTiming);
-            }
-    }
-    // split path: the two-launch forward's scratch rows (GSDR_ACQ_FWD2=0: the
-    // one-workgroup-per-spectrum forward)
-    {
-        const char* f2 = std::getenv("GSDR_ACQ_FWD2");
-        if (e == hipSuccess && a->split > 0 && !(f2 && std::atoi(f2) == 0))
-            e = hipMalloc(&a->d_fscratch, nB * a->K * a->D * N * sizeof(float2));
-    }
+    // split path: the two-launch forward's scratch rows (columns on every CU, then rows:
+    // +8-12 % on C4 / C5 over one workgroup per spectrum, r04e)
+    if (e == hipSuccess && a->split > 0) e = hipMalloc(&a->d_fscratch, nB * a->K * a->D * N * sizeof(float2));
     if (four)
         {
             // scratch slots: at least the resident workgroup count of the chip
@@ -309,7 +291,6 @@ int gsdr_acq_create(int device, const gsdr_acq_conf* conf, gsdr_acq** out)
             const double ang = 2.0 * M_PI * (double)m / (double)N;
             tw[m] = make_float2((float)std::cos(ang), (float)(-std::sin(ang)));
         }
-    if (a->tw_fill && a->tw_entries > N) a->tw_fill(tw.data());  // packed variant's per-stage table
     if ((e = hipMemcpy(a->d_tw, tw.data(), tw_n * sizeof(float2), hipMemcpyHostToDevice)) != hipSuccess)
         {
             gsdr::set_error("gsdr_acq_create: twiddle upload: %s", hipGetErrorString(e));
@@ -338,13 +319,12 @@ void gsdr_acq_destroy(gsdr_acq* a)
             (void)hipEventDestroy(r.b);
         }
     for (hipEvent_t e : a->prof_pool) (void)hipEventDestroy(e);
+    if (a->sub_done) (void)hipEventDestroy(a->sub_done);
+    if (a->h_res) (void)hipHostFree(a->h_res);
     void* bufs[] = {a->st2.d_wipe, a->st2.d_freq, a->d_tw, a->d_wipe, a->d_code_fft, a->d_code_stage, a->d_prn, a->d_X, a->d_stats, a->d_res,
-        a->d_iq, a->d_grid, a->d_rowbuf, a->d_keys, a->d_psum, a->d_pre, a->d_fscratch, a->d_dgrid, a->d_tw_sub, a->d_scratch, a->d_slots, a->d_resk, a->d_acc, a->d_acc_slots};
+        a->d_iq, a->d_grid, a->d_rowbuf, a->d_keys, a->d_psum, a->d_fscratch, a->d_dgrid, a->d_tw_sub, a->d_scratch, a->d_slots, a->d_resk, a->d_acc, a->d_acc_slots};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
-    for (hipEvent_t ev : a->pre_ev)
-        if (ev) (void)hipEventDestroy(ev);
-    if (a->pre_stream) (void)hipStreamDestroy(a->pre_stream);
     if (a->stream) (void)hipStreamDestroy(a->stream);
     delete a;
 }
@@ -369,17 +349,36 @@ int gsdr_acq_set_local_codes(gsdr_acq* a, const float* codes, const uint32_t* pr
     GSDR_HIP(hipMemcpyAsync(a->d_prn, prn, nprn * sizeof(uint32_t), hipMemcpyHostToDevice, a->stream));
     int rc = dispatch(a, 1, nullptr, 0, 0, 0, nullptr, nullptr, nprn);
     if (rc != GSDR_OK) return rc;
-    // real replicas (every GNSS code of this path: GPS C/A, Galileo E1 BOC/CBOC, BeiDou
-    // B1I) have Hermitian spectra, which the split correlate's mirror-pair loads can
-    // use (acq_correlate_split_kernel HERM): opt-in, GSDR_ACQ_HERM=1 (grid pass) or 2
-    // (also the ARG pass) -- measured within +-3 % of the plain loads at C5
-    bool real = true;
-    for (size_t i = 0; i < (size_t)nprn * a->consumed && real; ++i) real = codes[2 * i + 1] == 0.0f;
-    const char* he = std::getenv("GSDR_ACQ_HERM");
-    const int herm = he ? std::atoi(he) : 0;
-    a->codes_real = real && herm >= 1;
-    a->herm_arg = herm == 2;
     GSDR_HIP(hipStreamSynchronize(a->stream));
+    a->nprn = nprn;
+    return GSDR_OK;
+}
+
+int gsdr_acq_set_local_code(gsdr_acq* a, uint32_t slot, const float* code, uint32_t prn)
+{
+    GSDR_REQUIRE(a && code, GSDR_E_ARG, "gsdr_acq_set_local_code: null argument");
+    GSDR_REQUIRE(slot < a->conf.max_prns && slot < 0xffffu, GSDR_E_ARG, "gsdr_acq_set_local_code: slot %u outside [0,%u)",
+        slot, a->conf.max_prns);
+    std::lock_guard<std::mutex> lk(a->mu);
+    gsdr::DeviceGuard g(a->device);
+    // ordered after every launch issued so far on the handle's stream (the slot's
+    // previous spectrum may still be read by a submitted grid)
+    GSDR_HIP(hipMemcpyAsync(a->d_code_stage + (size_t)slot * a->consumed, code, (size_t)a->consumed * sizeof(float2),
+        hipMemcpyHostToDevice, a->stream));
+    GSDR_HIP(hipMemcpyAsync(a->d_prn + slot, &prn, sizeof(uint32_t), hipMemcpyHostToDevice, a->stream));
+    int rc = dispatch(a, 1, nullptr, 0, 0, 0, nullptr, nullptr, (slot << 16) | 1u);
+    if (rc != GSDR_OK) return rc;
+    GSDR_HIP(hipStreamSynchronize(a->stream));
+    if (a->nprn <= slot) a->nprn = slot + 1;
+    return GSDR_OK;
+}
+
+int gsdr_acq_set_active_prns(gsdr_acq* a, uint32_t nprn)
+{
+    GSDR_REQUIRE(a, GSDR_E_ARG, "gsdr_acq_set_active_prns: null handle");
+    GSDR_REQUIRE(nprn > 0 && nprn <= a->conf.max_prns, GSDR_E_ARG, "gsdr_acq_set_active_prns: %u outside [1,%u]", nprn,
+        a->conf.max_prns);
+    std::lock_guard<std::mutex> lk(a->mu);
     a->nprn = nprn;
     return GSDR_OK;
 }
@@ -497,6 +496,60 @@ int gsdr_acq_run_stream(gsdr_acq* a, gsdr_stream* ring, uint64_t first_sample, u
     GSDR_HIP(hipMemcpyAsync(out, a->d_res, (size_t)nblocks * a->nprn * sizeof(gsdr_acq_result), hipMemcpyDeviceToHost,
         a->stream));
     GSDR_HIP(hipStreamSynchronize(a->stream));
+    return GSDR_OK;
+}
+
+int gsdr_acq_submit_stream(gsdr_acq* a, gsdr_stream* ring, uint64_t first_sample, uint32_t nblocks, uint64_t stamp0)
+{
+    GSDR_REQUIRE(a && ring, GSDR_E_ARG, "gsdr_acq_submit_stream: null argument");
+    GSDR_REQUIRE(a->nprn > 0, GSDR_E_STATE, "gsdr_acq_submit_stream: set_local_codes first");
+    GSDR_REQUIRE(nblocks > 0 && nblocks <= a->conf.max_blocks, GSDR_E_ARG,
+        "gsdr_acq_submit_stream: nblocks %u outside [1,%u]", nblocks, a->conf.max_blocks);
+    GSDR_REQUIRE(gsdr::stream_item_type(ring) == a->conf.item_type, GSDR_E_ARG,
+        "gsdr_acq_submit_stream: ring item type %d != acquisition item type %d", gsdr::stream_item_type(ring),
+        a->conf.item_type);
+    GSDR_REQUIRE(gsdr::stream_device(ring) == a->device, GSDR_E_ARG,
+        "gsdr_acq_submit_stream: ring on device %d, acquisition handle on device %d", gsdr::stream_device(ring), a->device);
+    GSDR_REQUIRE(!a->sub_pending, GSDR_E_STATE, "gsdr_acq_submit_stream: collect the previous submission first");
+    std::lock_guard<std::mutex> lk(a->mu);
+    gsdr::DeviceGuard g(a->device);
+    if (!a->h_res)
+        {
+            GSDR_HIP(hipHostMalloc(&a->h_res, (size_t)a->conf.max_blocks * a->conf.max_prns * sizeof(gsdr_acq_result),
+                hipHostMallocDefault));
+            GSDR_HIP(hipEventCreateWithFlags(&a->sub_done, hipEventDisableTiming));
+        }
+    {
+        gsdr::StreamReader rd(ring);  // ring lock from view to reader-event record
+        const void* iq = nullptr;
+        int rc = rd.view(first_sample, (uint64_t)nblocks * a->K * a->consumed, &iq);
+        if (rc != GSDR_OK) return rc;
+        rc = rd.acquire(a->stream);
+        if (rc != GSDR_OK) return rc;
+        rc = dispatch(a, 0, iq, nblocks, a->consumed, stamp0, a->d_res, a->stream, 0);
+        if (rc != GSDR_OK) return rc;
+        rc = rd.release(a->stream);
+        if (rc != GSDR_OK) return rc;
+    }
+    GSDR_HIP(hipMemcpyAsync(a->h_res, a->d_res, (size_t)nblocks * a->nprn * sizeof(gsdr_acq_result),
+        hipMemcpyDeviceToHost, a->stream));
+    GSDR_HIP(hipEventRecord(a->sub_done, a->stream));
+    a->sub_blocks = nblocks;
+    a->sub_nprn = a->nprn;
+    a->sub_pending = true;
+    return GSDR_OK;
+}
+
+int gsdr_acq_collect(gsdr_acq* a, gsdr_acq_result* out, uint32_t* nblocks, uint32_t* nprn)
+{
+    GSDR_REQUIRE(a && out, GSDR_E_ARG, "gsdr_acq_collect: null argument");
+    GSDR_REQUIRE(a->sub_pending, GSDR_E_STATE, "gsdr_acq_collect: nothing submitted");
+    gsdr::DeviceGuard g(a->device);
+    a->sub_pending = false;
+    GSDR_HIP(hipEventSynchronize(a->sub_done));
+    std::memcpy(out, a->h_res, (size_t)a->sub_blocks * a->sub_nprn * sizeof(gsdr_acq_result));
+    if (nblocks) *nblocks = a->sub_blocks;
+    if (nprn) *nprn = a->sub_nprn;
     return GSDR_OK;
 }
 

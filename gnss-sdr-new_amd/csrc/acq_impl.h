@@ -26,21 +26,6 @@ namespace
 
 using gsdr::fft::Plan;
 
-// GSDR_SPLIT_TWF 1 (default since r04e: C4 bit transition +11 %): the split
-// correlate's input factor W_N^{m q} as a compile-time root per column row and one
-// table read per column instead of R (acq_correlate_split_kernel)
-// occupancy target of the mirror-pair (HERM) split correlate: 4 waves per SIMD keeps
-// two 512-lane workgroups per CU (at most 128 VGPRs)
-// occupancy target of the split ARG pass (one selected row per (b, p): few workgroups)
-#ifndef GSDR_ARG_WPE
-#define GSDR_ARG_WPE 1
-#endif
-#ifndef GSDR_HERM_WPE
-#define GSDR_HERM_WPE 4
-#endif
-#ifndef GSDR_SPLIT_TWF
-#define GSDR_SPLIT_TWF 1
-#endif
 
 // Default correlate variant at N = 4000 (see GSDR_PK_VARIANTS).
 constexpr int kDefaultCorrVariant4000 = 70;
@@ -541,20 +526,17 @@ __global__ void __launch_bounds__(PT::NT) acq_correlate_kernel(const float2* __r
 // PG < 0: groups of -PG PRNs without the next-code prefetch (the code values are
 // loaded by the first stage itself) -- for plans whose registers cannot hold
 // both first-stage operand sets through a transform (N = 16000 on 1024 lanes).
-// PG == 0: one PRN per workgroup with the first stage's products conj(X) C formed
-// in two halves of its rows before the transform (half the operand registers in
-// flight; a scheduling barrier keeps the second half's loads behind the first's).
-constexpr int pg_count(int pg) { return pg < 0 ? -pg : (pg == 0 ? 1 : pg); }
+constexpr int pg_count(int pg) { return pg < 0 ? -pg : pg; }
 
 template <class MP, int PG_, int WPE, int STAT>
 __global__ void __launch_bounds__(MP::NT) __attribute__((amdgpu_waves_per_eu(WPE))) acq_correlate_pk_kernel(const float2* __restrict__ X,
     const float2* __restrict__ code_fft, RowStat* __restrict__ stats, const float2* __restrict__ tw, uint32_t D,
     uint32_t P, uint32_t nblocks, XMap xm)
 {
+    static_assert(PG_ != 0, "PRN group");
     constexpr int PG = pg_count(PG_);
     constexpr bool PREFETCH = PG_ > 0;
-    constexpr bool HALVES = PG_ == 0;
-    static_assert(STAT == 1 || STAT == 2 || STAT == 3, "row statistic 1 (max + sum), 2 (max) or 3 (max, atomic)");
+    static_assert(STAT == 1 || STAT == 2, "row statistic 1 (max + sum) or 2 (max)");
     using gsdr::pk::c2;
     constexpr int NT = MP::NT;
     constexpr int NW = NT / 64;
@@ -598,35 +580,6 @@ __global__ void __launch_bounds__(MP::NT) __attribute__((amdgpu_waves_per_eu(WPE
     // lanes' clamped, in-bounds copies keep every register defined, so no
     // zero-fill code); a wave with none skips the loads
     c2 xr[BPT1][R1], cr[BPT1][R1];
-    if constexpr (HALVES)
-        {
-            // xr <- the products, rows [0, R1/2) then [R1/2, R1)
-            auto half = [&](auto r0c, auto r1c) {
-                constexpr int r0 = decltype(r0c)::value, r1 = decltype(r1c)::value;
-#pragma unroll
-                for (int bb = 0; bb < BPT1; ++bb)
-                    {
-                        const int j = (int)threadIdx.x + bb * NT;
-                        const int j0 = (int)(threadIdx.x & ~63u) + bb * NT;
-                        if (NB1 % NT == 0 || j0 < NB1)
-                            {
-                                const int jj = min(j, NB1 - 1);
-#pragma unroll
-                                for (int r = r0; r < r1; ++r)
-                                    {
-                                        xr[bb][r] = bload(xrs, jj * 8, r * NB1 * 8);
-                                        cr[bb][r] = bload(crs, jj * 8, r * NB1 * 8);
-                                    }
-#pragma unroll
-                                for (int r = r0; r < r1; ++r) xr[bb][r] = gsdr::pk::conj_mul(xr[bb][r], cr[bb][r]);
-                            }
-                    }
-            };
-            half(std::integral_constant<int, 0>{}, std::integral_constant<int, R1 / 2>{});
-            __builtin_amdgcn_sched_barrier(0);
-            half(std::integral_constant<int, R1 / 2>{}, std::integral_constant<int, R1>{});
-        }
-    else
 #pragma unroll
     for (int bb = 0; bb < BPT1; ++bb)
         {
@@ -648,9 +601,7 @@ __global__ void __launch_bounds__(MP::NT) __attribute__((amdgpu_waves_per_eu(WPE
             {
                     float rmax = 0.0f, sum = 0.0f;
                     auto load = [&](int bb, int r, int i) -> c2 {
-                        if constexpr (HALVES)
-                            return xr[bb][r];
-                        else if constexpr (PREFETCH)
+                        if constexpr (PREFETCH)
                             return gsdr::pk::conj_mul(xr[bb][r], cr[bb][r]);
                         else
                             return gsdr::pk::conj_mul(xr[bb][r], bload(crs, i * 8, (int)(q * N * 8)));
@@ -678,18 +629,6 @@ __global__ void __launch_bounds__(MP::NT) __attribute__((amdgpu_waves_per_eu(WPE
                     };
                     MP::template run<false>(lds, tw, load, store, hook);
                     rmax = gsdr::wave_max(rmax);
-                    if constexpr (STAT == 3)
-                        {
-                            // each wave merges its maximum into the row statistic (zeroed by the
-                            // host; non-negative floats order as their bit patterns): no LDS
-                            // exchange and no workgroup barrier at the end of the transform
-                            if ((threadIdx.x & 63) == 0)
-                                __hip_atomic_fetch_max(
-                                    reinterpret_cast<uint32_t*>(&stats[((size_t)b * P + p0 + q) * D + d].max),
-                                    __float_as_uint(rmax), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                            if (q + 1 < np) __syncthreads();  // the next transform's first LDS writes
-                            continue;
-                        }
                     if constexpr (STAT == 1)
                         {
 #pragma unroll
@@ -945,26 +884,13 @@ struct RegFourStep
 
     // Phase 2 of a register four-step: the R rows (phase 1's v[c][k1], lane column
     // n2 = threadIdx.x + c NT, clamped) through LDS and the L-point row transforms.
-    // HC (two columns per lane, NT > L / 2): lane t holds the mirror pair a = min(t,
-    // L/2), b = L - a instead (acq_correlate_split_kernel's Hermitian code loads); the
-    // b slot is stored only for 1 <= t < L/2.
-    template <int CPL, bool HC = false, class Out>
+    template <int CPL, class Out>
     __device__ __forceinline__ static void phase2(gsdr::pk::c2* lds, gsdr::pk::c2 (&v)[CPL][R], Out& out)
     {
         const int wbase = (int)(threadIdx.x & ~63u);
-        static_assert(!HC || (CPL == 2 && NT > L / 2), "mirror pairs: two columns per lane");
         auto column = [&](int c, int& n2) -> bool {
-            if constexpr (HC)
-                {
-                    const int t = (int)threadIdx.x, a = min(t, L / 2);
-                    n2 = c == 0 ? a : L - a;
-                    return c == 0 || (t >= 1 && t < L / 2);
-                }
-            else
-                {
-                    n2 = min((int)threadIdx.x + c * NT, L - 1);
-                    return L % NT == 0 || wbase + c * NT < L;
-                }
+            n2 = min((int)threadIdx.x + c * NT, L - 1);
+            return L % NT == 0 || wbase + c * NT < L;
         };
         if constexpr (!WL)
             {
@@ -1122,8 +1048,6 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(RP:
 // Grid: one workgroup per (row = b*D + d, PRN p, sub-transform q), the ROUT*P
 // workgroups of one row on one XCD, each XCD walking its rows in groups of pgs
 // PRNs so its L2 holds pgs code rows while the X rows stream.
-// ABL (timing ablations for the profile, results meaningless): bit 0 replaces
-// phase 1's global loads by lane-computed values, bit 1 skips phase 2.
 // ARG: the selected row's pass instead of the grid (acq_reduce_kernel chose Doppler
 // row d* of (b, p) from the row maxima): grid (b*P + p, q), the same arithmetic as
 // the grid pass (the recomputed values are bit-identical to those the row maximum
@@ -1134,69 +1058,18 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(RP:
 // turns the key into the result fields.  One workgroup per transform of a
 // 100000-point row spreads the pass over ROUT x more CUs than the one-workgroup
 // recomputation (acq_argmax_four_kernel: 144 workgroups at C5 Galileo).
-// HERM (real code replicas, so C[N - k] = conj(C[k]); plans with two columns per
-// lane): lane t takes the mirror columns a = min(t, L/2) and b = L - a; the code
-// value of column b at (quarter r, row R-1-n1) is conj(C) of column a at (quarter
-// ROUT-1-r, row n1), so one code load serves both columns -- 3 ROUT loads per row
-// pair instead of 4 ROUT (X of a, X of b, C of a).
-// The split plan's outer decimation-in-frequency step as its own pass (GSDR_ACQ_PRE):
-// for every (row, p) and q < ROUT the M-point sub-transform input
-//   y_q[m] = W_N^{q m} sum_r W_ROUT^{r q} conj(X[m + r M]) C[m + r M],  m < M = N / ROUT,
-// stored contiguously, so the grid pass's workgroups read M points each instead of the
-// whole X and code rows (acq_correlate_split_kernel PRE).  Grid (ceil(M/256), rows, P).
-template <int ROUT>
-__global__ void __launch_bounds__(256) acq_split_pre_kernel(const float2* __restrict__ X,
-    const float2* __restrict__ code_fft, float2* __restrict__ Y, const float2* __restrict__ tw, uint32_t D,
-    uint32_t P, uint32_t M, XMap xm, uint32_t p0 = 0)
-{
-    using gsdr::pk::c2;
-    const uint32_t m = blockIdx.x * 256u + threadIdx.x;
-    if (m >= M) return;
-    const uint32_t row = blockIdx.y, p = blockIdx.z;
-    const uint32_t b = row / D, d = row - (row / D) * D;
-    const size_t N = (size_t)M * ROUT;
-    const float2* x = X + xm.off(b, d);
-    const float2* c = code_fft + (size_t)(p0 + p) * N;  // Y: chunk-local p
-    c2 pr[ROUT];
-#pragma unroll
-    for (int r = 0; r < ROUT; ++r)
-        pr[r] = gsdr::pk::conj_mul(gsdr::pk::from(x[m + (size_t)r * M]), gsdr::pk::from(c[m + (size_t)r * M]));
-    float2* y = Y + ((size_t)row * P + p) * ROUT * M + m;
-#pragma unroll
-    for (int q = 0; q < ROUT; ++q)
-        {
-            c2 z = pr[0];
-#pragma unroll
-            for (int r = 1; r < ROUT; ++r)
-                {
-                    const int e = ((r * q) % ROUT) * (4 / ROUT);
-                    if (e == 0)
-                        z = z + pr[r];
-                    else if (e == 1)
-                        z = gsdr::pk::add_mi(z, pr[r]);
-                    else if (e == 2)
-                        z = z - pr[r];
-                    else
-                        z = gsdr::pk::sub_mi(z, pr[r]);
-                }
-            if (q > 0) z = gsdr::pk::mul(z, gsdr::pk::from(tw[(size_t)q * m]));
-            y[(size_t)q * M] = gsdr::pk::to(z);
-        }
-}
-
-template <int ROUT, class RP, bool HALF, int ABL = 0, bool ARG = false, bool HERM = false, bool PRE = false>
-__global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(HERM ? GSDR_HERM_WPE : (ARG ? GSDR_ARG_WPE : RP::WPE)))) acq_correlate_split_kernel(
+// The input factor W_N^{m q} of sub-transform q is a compile-time root per column row
+// and one table read per column (r04e: C4 bit transition +11 % over R reads).
+template <int ROUT, class RP, bool HALF, bool ARG = false>
+__global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(ARG ? 1 : RP::WPE))) acq_correlate_split_kernel(
     const float2* __restrict__ X, const float2* __restrict__ code_fft, RowStat* __restrict__ stats,
     const float2* __restrict__ tw, uint32_t D, uint32_t P, uint32_t nblocks, uint32_t pgs, XMap xm,
     const gsdr_acq_result* __restrict__ sel, unsigned long long* __restrict__ keys, float* __restrict__ rowbuf,
-    float* __restrict__ psum, uint32_t pchunk = 0)
+    float* __restrict__ psum)
 {
     using gsdr::pk::c2;
     constexpr int R = RP::R, NT = RP::NT, L = RP::L, CPL = RP::CPL;
     constexpr uint32_t M = RP::N;
-    // pchunk (PRE, chunked): PRNs [p_base, p_base + P) of P_all, so the row statistic
-    // lands at the handle's (b, p_base + p, d)
-    const uint32_t P_all = pchunk ? (pchunk & 0xffffu) : P, p_base = pchunk >> 16;
     constexpr uint32_t N = M * ROUT;
     constexpr int NW = NT / 64;
     extern __shared__ float2 lds_raw[];
@@ -1233,15 +1106,11 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(HER
         }
     const uint32_t p = pv / ROUT, q = pv - p * ROUT;
     const uint32_t b = row / D, d = row - (row / D) * D;
-    // PRE: X holds acq_split_pre_kernel's sub-transform inputs, M per (row, p, q)
-    const auto xrs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float2*>(X) + (PRE ? (((size_t)row * P + p) * ROUT + q) * M : xm.off(b, d)), 0,
-        (int)((PRE ? M : N) * sizeof(c2)), 0x00020000);
+    const auto xrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float2*>(X) + xm.off(b, d), 0, (int)(N * sizeof(c2)),
+        0x00020000);
     const auto crs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float2*>(code_fft) + (size_t)p * N, 0, (int)(N * sizeof(c2)), 0x00020000);
     auto bload = [](decltype(xrs) rs, int voff, int soff) -> c2 {
-        if constexpr ((ABL & 1) != 0)
-            return c2{(float)(voff + soff) * 1e-6f, (float)(voff - soff) * 1e-6f};
         const auto u = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, 0);
         return c2{__uint_as_float(u[0]), __uint_as_float(u[1])};
     };
@@ -1281,22 +1150,16 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(HER
                                         else
                                             z = gsdr::pk::sub_mi(z, y);  // z + i y
                                     }
-                                if constexpr (Q > 0)
-                                    {
-                                        if constexpr (GSDR_SPLIT_TWF)
-                                            z = gsdr::pk::mul_root<Q * n1, ROUT * R>(z);
-                                        else
-                                            z = gsdr::pk::mul(z, gsdr::pk::from(tw[m * Q]));
-                                    }
+                                if constexpr (Q > 0) z = gsdr::pk::mul_root<Q * n1, ROUT * R>(z);
                                 v[c][n1] = z;
                         };
                         gsdr::pk::static_for<0, R>(column_input);
                         gsdr::pk::Dft<R>::run(v[c]);
-                        // W_M^{n2 k1} = W_N^{ROUT n2 k1}; GSDR_SPLIT_TWF: the input factor
-                        // W_N^{m Q} = W_{ROUT R}^{Q n1} W_N^{Q n2} -- the first a compile-time
-                        // root above, the second common to the column, so applied to its
+                        // W_M^{n2 k1} = W_N^{ROUT n2 k1}; the input factor W_N^{m Q} =
+                        // W_{ROUT R}^{Q n1} W_N^{Q n2} -- the first a compile-time root
+                        // above, the second common to the column, so applied to its
                         // outputs here: one table read instead of R
-                        if constexpr (Q > 0 && GSDR_SPLIT_TWF)
+                        if constexpr (Q > 0)
                             {
                                 const c2 w0 = gsdr::pk::from(tw[Q * n2]);
 #pragma unroll
@@ -1306,92 +1169,7 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(HER
                     }
             }
     };
-    // HERM: the mirror-pair phase 1 (see above); v[0] = column a, v[1] = column b
-    auto phase1h = [&](auto qc) {
-        constexpr int Q = decltype(qc)::value;
-        static_assert(CPL == 2 && NT > L / 2, "mirror pairs: two columns per lane");
-        const int t = (int)threadIdx.x;
-        const int a = min(t, L / 2);
-        const int bcol = (t >= 1 && t < L / 2) ? L - a : a;  // lanes without a pair repeat a (not stored)
-        auto combine = [&](c2 z, const c2 y, int r) -> c2 {
-            const int e = ((r * Q) % ROUT) * (4 / ROUT);
-            if (e == 0) return z + y;
-            if (e == 1) return gsdr::pk::add_mi(z, y);
-            if (e == 2) return z - y;
-            return gsdr::pk::sub_mi(z, y);
-        };
-        auto pair_input = [&](auto n1c) {
-            constexpr int n1 = decltype(n1c)::value;
-            constexpr int n1b = R - 1 - n1;
-            c2 ca[ROUT];
-#pragma unroll
-            for (int r = 0; r < ROUT; ++r) ca[r] = bload(crs, a * 8, (int)((r * M + n1 * L) * 8));
-            auto mirror = [&](c2 x, c2 c) -> c2 {  // conj(x) conj(c) = conj(x c)
-                const c2 m = gsdr::pk::mul(x, c);
-                return c2{m.x, -m.y};
-            };
-            c2 za = gsdr::pk::conj_mul(bload(xrs, a * 8, n1 * L * 8), ca[0]);
-            c2 zb = mirror(bload(xrs, bcol * 8, n1b * L * 8), ca[ROUT - 1]);
-#pragma unroll
-            for (int r = 1; r < ROUT; ++r)
-                {
-                    za = combine(za, gsdr::pk::conj_mul(bload(xrs, a * 8, (int)((r * M + n1 * L) * 8)), ca[r]), r);
-                    zb = combine(zb, mirror(bload(xrs, bcol * 8, (int)((r * M + n1b * L) * 8)), ca[ROUT - 1 - r]), r);
-                }
-            if constexpr (Q > 0)
-                {
-                    if constexpr (GSDR_SPLIT_TWF)
-                        {
-                            za = gsdr::pk::mul_root<Q * n1, ROUT * R>(za);
-                            zb = gsdr::pk::mul_root<Q * n1b, ROUT * R>(zb);
-                        }
-                    else
-                        {
-                            za = gsdr::pk::mul(za, gsdr::pk::from(tw[(n1 * L + a) * Q]));
-                            zb = gsdr::pk::mul(zb, gsdr::pk::from(tw[(n1b * L + bcol) * Q]));
-                        }
-                }
-            v[0][n1] = za;
-            v[1][n1b] = zb;
-        };
-        gsdr::pk::static_for<0, R>(pair_input);
-#pragma unroll
-        for (int c = 0; c < 2; ++c)
-            {
-                const int n2 = c == 0 ? a : bcol;
-                gsdr::pk::Dft<R>::run(v[c]);
-                if constexpr (Q > 0 && GSDR_SPLIT_TWF)
-                    {
-                        const c2 w0 = gsdr::pk::from(tw[Q * n2]);
-#pragma unroll
-                        for (int k1 = 0; k1 < R; ++k1) v[c][k1] = gsdr::pk::mul(v[c][k1], w0);
-                    }
-                gsdr::pk::apply_powers<R>(v[c], gsdr::pk::from(tw[ROUT * n2]));
-            }
-    };
-    // PRE: the inputs arrive combined and twiddled; only the column DFTs remain
-    auto phase1p = [&](auto) {
-#pragma unroll
-        for (int c = 0; c < CPL; ++c)
-            {
-                if (L % NT == 0 || wbase + c * NT < L)
-                    {
-                        const int n2 = min((int)threadIdx.x + c * NT, L - 1);
-#pragma unroll
-                        for (int n1 = 0; n1 < R; ++n1) v[c][n1] = bload(xrs, n2 * 8, n1 * L * 8);
-                        gsdr::pk::Dft<R>::run(v[c]);
-                        gsdr::pk::apply_powers<R>(v[c], gsdr::pk::from(tw[ROUT * n2]));
-                    }
-            }
-    };
-    auto run_phase1 = [&](auto qc) {
-        if constexpr (PRE)
-            phase1p(qc);
-        else if constexpr (HERM)
-            phase1h(qc);
-        else
-            phase1(qc);
-    };
+    auto run_phase1 = [&](auto qc) { phase1(qc); };
     if constexpr (ROUT == 1)
         run_phase1(std::integral_constant<int, 0>{});
     else if constexpr (ROUT == 2)
@@ -1440,15 +1218,7 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(HER
         {
             if (rowbuf) out.row = rowbuf + (size_t)(id / ROUT) * (HALF ? N / 2 : N);
         }
-    if constexpr ((ABL & 2) == 0)
-        RP::template phase2<CPL, HERM>(lds, v, out);
-    else
-        {
-#pragma unroll
-            for (int c = 0; c < CPL; ++c)
-#pragma unroll
-                for (int i = 0; i < R; ++i) out.value(v[c][i], L - 1, i);
-        }
+    RP::template phase2<CPL>(lds, v, out);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if constexpr (ARG)
         {
@@ -1508,7 +1278,7 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(HER
             float best = red[0];
 #pragma unroll
             for (int w2 = 1; w2 < NW; ++w2) best = __builtin_fmaxf(best, red[w2]);
-            RowStat* st = stats + ((size_t)b * P_all + p_base + p) * D + d;
+            RowStat* st = stats + ((size_t)b * P + p) * D + d;
             if constexpr (ROUT == 1)
                 *st = RowStat{best, 0u, 0.0f, 0};
             else  // non-negative floats order as their bit patterns (row zeroed by the host)
@@ -2449,17 +2219,8 @@ struct gsdr_acq
     int variant{0};
     int corr_variant{0};      // 0: the generic LDS kernels; >0: a GSDR_PK_VARIANTS id (packed forward + correlate)
     int split{0};             // >0: the single-dwell split register four-step correlate (acq_split.hip)
-    bool codes_real{false};   // every local code is real (imaginary parts 0): Hermitian code spectra
-    bool herm_arg{false};     // the split ARG pass takes the mirror-pair loads too (GSDR_ACQ_HERM=2)
-    bool pre{false};          // split grid pass through acq_split_pre_kernel (GSDR_ACQ_PRE=1)
-    float2* d_pre{nullptr};   // its sub-transform inputs: two chunks of pre_chunk PRNs (nblocks * D * N each)
-    uint32_t pre_chunk{0};    // PRNs per chunk; chunk i + 1's pass overlaps chunk i's grid pass
-    hipStream_t pre_stream{nullptr};
-    hipEvent_t pre_ev[4]{};   // [0,1] chunk inputs written (per buffer), [2,3] buffer read
     uint32_t split_pgs{1};    // its PRN group per XCD pass
     int corr_stat{0};         // the variant's row statistic (1/2: argmax recomputed by acq_argmax_pk_kernel)
-    size_t tw_entries{0};     // twiddle entries the packed variant reads (W_N + its per-stage table)
-    void (*tw_fill)(float2*){nullptr};  // fills the per-stage table after W_N
     size_t corr_lds_bytes{0};
     Plan plan{};
     gsdr::fft::Plan4 plan4{};  // four-step plan (variants 20-22, N beyond one workgroup's LDS)
@@ -2475,6 +2236,12 @@ struct gsdr_acq
     float2* d_X{nullptr};
     RowStat* d_stats{nullptr};
     gsdr_acq_result* d_res{nullptr};
+    // gsdr_acq_submit_stream / gsdr_acq_collect: pinned results of the submitted
+    // attempts (max_blocks x max_prns), their completion event and shape
+    gsdr_acq_result* h_res{nullptr};
+    hipEvent_t sub_done{nullptr};
+    uint32_t sub_blocks{0}, sub_nprn{0};
+    bool sub_pending{false};
     void* d_iq{nullptr};
     float* d_grid{nullptr};
     float* d_rowbuf{nullptr};  // split path, peak ratio: the selected rows' |R|^2 (max_blocks x max_prns x N)
@@ -2528,31 +2295,22 @@ size_t item_bytes(int it) { return it == GSDR_ITEM_CSHORT ? 4 : (it == GSDR_ITEM
 // size (default_pk_variant; GSDR_ACQ_CORR_VARIANT selects one for tests):
 // (id, plan, PRNs per workgroup, waves-per-EU hint, row statistic: 1 max + sum
 // with the argmax recomputed for the selected row, 2 max only with the CFAR row
-// sum by Parseval -- see acq_correlate_pk_kernel; 3, the same maximum merged per wave
-// by an atomic without the end-of-transform barrier, measured 2 % slower at N = 4000
-// in r04e and is not built).  93 runs the correlate on the
+// sum by Parseval -- see acq_correlate_pk_kernel).  93 runs the correlate on the
 // register four-step (acq_correlate_reg_kernel, N = 16000, PRN-group-major XCD
 // walk) and its forward / argmax passes on the listed plan; 94 the same with
-// wave-local row transforms (RegFourStep H = 0).  The alternatives
-// measured in rounds 1-2 (other radix orders, per-stage twiddle tables, LDS root
-// copies, padded layouts, late barriers, 5 waves, PRN groups)
-// were within noise of or slower than these and are no longer built.  Round 4
-// (profiles/r04t): variant 70 at 104 VGPRs runs 4 workgroups (16 waves) per CU; 5
-// per CU (waves-per-EU 5: 96 VGPRs + 36 B/lane spills, or the code loaded in the
-// first stage without the prefetch: 61 VGPRs) measured 19 % slower, and 3 / 2 per
-// CU (GSDR_PK_LDS_EXTRA bytes of LDS padding per workgroup) 8 % / 26 % slower;
-// 5 per CU without spills (PG 0: the first-stage products formed in two halves,
-// 96 VGPRs) 2 % slower, the same as the two halves at 4 per CU (r04y): beyond 4
-// workgroups the CU's issue, not latency, bounds the transform.  Twiddles from the
-// per-stage table instead of powers of one root (TWP 2, 16-byte loads: -23 %) or
-// the middle stage's roots from an LDS copy (TWP 3: -2.5 %) did not pay (r04z).
+// wave-local row transforms (RegFourStep H = 0).  The alternatives measured in
+// rounds 1-4 and removed: other radix orders, per-stage twiddle
+// tables (-23 %) and LDS root copies (-2.5 %), padded layouts, late or dropped
+// barriers, 5 waves per SIMD (with spills -19 %; without, the first-stage products
+// in two halves, -2 %), 3 / 2 workgroups per CU (-8 % / -26 %), per-wave atomic row
+// maxima (-2 %), multi-transform workgroups: variant 70 at 104 VGPRs runs 4
+// workgroups (16 waves) per CU, where the CU's issue, not latency, bounds it.
 #define GSDR_PK_VARIANTS(X)                                              \
     X(61, (gsdr::pk::PkPlan<512, true, 20, 20, 20>), 1, 1, 1)           \
     X(62, (gsdr::pk::PkPlan<256, true, 20, 10, 10>), 1, 1, 1)           \
     X(93, (gsdr::pk::PkPlan<1024, 1, 16, 10, 10, 10>), 1, 1, 2)         \
     X(94, (gsdr::pk::PkPlan<1024, 1, 16, 10, 10, 10>), 1, 1, 2)         \
-    X(70, (gsdr::pk::PkPlan<256, 1, 25, 16, 10>), 1, 1, 2)            \
-    X(72, (gsdr::pk::PkPlan<256, 1 | (1 << 9), 25, 16, 10>), 1, 1, 2)
+    X(70, (gsdr::pk::PkPlan<256, 1, 25, 16, 10>), 1, 1, 2)
 
 template <class PT>
 int set_lds_attrs(size_t bytes)
@@ -2973,11 +2731,15 @@ int launch_dwell(gsdr_acq* a, uint32_t dwell, uint64_t stamp, gsdr_acq_result* r
     return GSDR_OK;
 }
 
+// aux: slot count in bits 0-15, first slot in bits 16+ (gsdr_acq_set_local_code
+// transforms one slot, gsdr_acq_set_local_codes slots [0, nprn))
 template <class PT>
-int launch_code_fft(gsdr_acq* a, uint32_t nprn)
+int launch_code_fft(gsdr_acq* a, uint32_t aux)
 {
-    hipLaunchKernelGGL((acq_code_fft_kernel<PT>), dim3(nprn), dim3(PT::NT), a->lds_bytes, a->stream, a->d_code_stage,
-        a->d_code_fft, a->d_tw, plan_of<PT>(a), a->consumed, a->lead);
+    const uint32_t nprn = aux & 0xffffu, first = aux >> 16;
+    hipLaunchKernelGGL((acq_code_fft_kernel<PT>), dim3(nprn), dim3(PT::NT), a->lds_bytes, a->stream,
+        a->d_code_stage + (size_t)first * a->consumed, a->d_code_fft + (size_t)first * a->N, a->d_tw, plan_of<PT>(a),
+        a->consumed, a->lead);
     GSDR_HIP(hipGetLastError());
     return GSDR_OK;
 }

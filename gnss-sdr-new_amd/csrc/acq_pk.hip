@@ -122,8 +122,6 @@ int setup_corr_variant(gsdr_acq* a, int v)
         {                                                                                                       \
             using M = GSDR_UNPAREN MP;                                                                          \
             a->corr_lds_bytes = M::lds_bytes() + (size_t)2 * (M::NT / 64) * sizeof(RowStat);                   \
-            /* A/B knob: LDS padding per workgroup caps the workgroups per CU */                               \
-            if (const char* e = std::getenv("GSDR_PK_LDS_EXTRA")) a->corr_lds_bytes += (size_t)std::atoi(e);  \
             GSDR_HIP(hipFuncSetAttribute((const void*)acq_correlate_pk_kernel<M, PG, WPE, ST>,                  \
                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)a->corr_lds_bytes));                           \
             GSDR_HIP(hipFuncSetAttribute((const void*)acq_argmax_pk_kernel<M, ST>,                              \
@@ -143,8 +141,6 @@ int setup_corr_variant(gsdr_acq* a, int v)
             if (ID == 94 && setup_reg<RegPlan94>() != GSDR_OK) return GSDR_E_DEVICE;                           \
             a->corr_variant = ID;                                                                               \
             a->corr_stat = ST;                                                                                  \
-            a->tw_entries = M::tw_entries();                                                                    \
-            a->tw_fill = &M::fill_stage_tw;                                                                     \
             return GSDR_OK;                                                                                     \
         }
 #define GSDR_UNPAREN(...) __VA_ARGS__

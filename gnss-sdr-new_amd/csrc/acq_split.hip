@@ -24,9 +24,6 @@ using Wl25kW = RegFourStep<25, 1024, 0, 1, NoPads<1000>, 10, 10, 10>;    // one 
 using Wl32k = RegFourStep<32, 1024, 0, 1, NoPads<1000>, 10, 10, 10>;     // rounds 16 + 16 (128 KB)
 using Wl32kP = RegFourStep<32, 1024, 0, 1, Pads1000, 10, 10, 10>;        // the same, bank-model pads
 using Wl16k = RegFourStep<16, 512, 0, 1, NoPads<1000>, 10, 10, 10>;      // rounds 8 + 8 (64 KB)
-//   50000 = 25 x (20 x 10 x 10): 512 lanes, four columns per lane (100 complex in
-//           VGPRs), one 2000-point row per wave, rounds 8 + 8 + 8 + 1 (128 KB)
-using Wl50k = RegFourStep<25, 512, 0, 1, NoPads<2000>, 20, 10, 10>;
 
 // split ids: (N, outer radix ROUT, inner plan)
 //   1: 25000 = 1 x 25000 (C5 GPS L1 / BeiDou B1I at 25 Msps, 1 ms)
@@ -38,8 +35,10 @@ using Wl50k = RegFourStep<25, 512, 0, 1, NoPads<2000>, 20, 10, 10>;
 // wave-local rows:
 //   11: 25000 (Wl25k)   12: 32000 (Wl32k)   13: 64000 = 2 x Wl32k   14: 100000 = 4 x Wl25k
 //   15: 32000 = 2 x Wl16k   16: 64000 = 4 x Wl16k   17: 25000 (Wl25kW)   18: 100000 = 4 x Wl25kW
-//   19: 32000 (Wl32kP)   20: 64000 = 2 x Wl32kP   21: 100000 = 2 x Wl50k (half the
-//   re-read loads of 4 x 25000, one workgroup per CU)
+//   19: 32000 (Wl32kP)   20: 64000 = 2 x Wl32kP
+// (round 4 measured and removed: 100000 = 2 x 50000 (25 x 2000 register four-step,
+// 164 B/lane of spills, -3.5 %), the outer DIF step as its own pass (-11 % / -29 %),
+// mirror-pair loads of the Hermitian code spectra (within +-3 %))
 namespace
 {
 struct SplitId
@@ -51,9 +50,7 @@ struct SplitId
 // 64000, +4 % / +10 % over 2 / 3; the 512-lane 25000 plan keeps its LDS rounds)
 constexpr SplitId kSplits[] = {{1, 25000}, {12, 32000}, {13, 64000}, {4, 100000}, {2, 32000}, {3, 64000}, {5, 32000},
     {6, 64000}, {11, 25000}, {14, 100000}, {15, 32000}, {16, 64000}, {17, 25000}, {18, 100000}, {19, 32000},
-    {20, 64000}, {21, 100000}, {112, 32000}, {212, 32000}, {113, 64000}, {213, 64000}};
-// 112 / 212, 113 / 213: timing ablations of 12 / 13 (acq_correlate_split_kernel ABL:
-// 1xx without phase 1's global loads, 2xx without phase 2) -- profiles only
+    {20, 64000}};
 
 // PRN group of an XCD pass: the largest divisor of P whose code rows fit in ~2 MB
 // (half an XCD's L2), so the rows of the group's codes stay resident while the X
@@ -61,11 +58,9 @@ constexpr SplitId kSplits[] = {{1, 25000}, {12, 32000}, {13, 64000}, {4, 100000}
 uint32_t prn_group(uint32_t P, uint32_t N)
 {
     const size_t row = (size_t)N * sizeof(float2);
-    // code bytes per group walked by every XCD at once (A/B knob GSDR_ACQ_PGS_KB)
-    static const size_t cap = [] {
-        const char* e = std::getenv("GSDR_ACQ_PGS_KB");
-        return e ? (size_t)std::atoi(e) << 10 : (size_t)2 << 20;
-    }();
+    // code bytes per group walked by every XCD at once: 2 MB (r04x: 1 MB within
+    // noise, 4 MB -7 % at Galileo, 8 MB -10-12 %: the per-XCD L2 sets it)
+    constexpr size_t cap = (size_t)2 << 20;
     uint32_t best = 1;
     for (uint32_t g = 1; g <= P; ++g)
         if (P % g == 0 && (size_t)g * row <= cap) best = g;
@@ -75,31 +70,11 @@ uint32_t prn_group(uint32_t P, uint32_t N)
 // ARG = false: the grid pass (row maxima into d_stats); ARG = true: the selected
 // rows' pass (keys into d_keys, |R|^2 rows into rowbuf for the peak ratio; the
 // caller zeroes d_keys and runs acq_argmax_split_finish_kernel)
-// plans whose lanes hold two columns with NT > L / 2: the mirror-pair (Hermitian
-// code) phase 1 applies (acq_correlate_split_kernel HERM)
-template <class RP>
-constexpr bool herm_ok = RP::CPL == 2 && RP::NT > RP::L / 2;
-
-template <int ROUT, class RP, bool HALF, int ABL = 0, bool ARG = false>
+template <int ROUT, class RP, bool HALF, bool ARG = false>
 int launch_one(gsdr_acq* a, uint32_t nblocks, hipStream_t s, const gsdr_acq_result* sel = nullptr,
     float* rowbuf = nullptr, float* psum = nullptr, uint32_t* rout = nullptr)
 {
     if (rout) *rout = ROUT;
-    if constexpr (herm_ok<RP> && ABL == 0)
-        {
-            if (a->codes_real && (!ARG || a->herm_arg))
-                {
-                    if (RP::N * ROUT != (int)a->N) return GSDR_E_STATE;
-                    if (ROUT > 1 && !ARG)
-                        GSDR_HIP(hipMemsetAsync(a->d_stats, 0, (size_t)nblocks * a->nprn * a->D * sizeof(RowStat), s));
-                    const uint32_t grid = ARG ? nblocks * a->nprn * ROUT : nblocks * a->D * a->nprn * ROUT;
-                    hipLaunchKernelGGL((acq_correlate_split_kernel<ROUT, RP, HALF, 0, ARG, true>), dim3(grid),
-                        dim3(RP::NT), RP::lds_bytes(), s, a->d_X, a->d_code_fft, a->d_stats, a->d_tw, a->D, a->nprn,
-                        nblocks, prn_group(a->nprn, a->N), a->xm, sel, a->d_keys, rowbuf, psum);
-                    GSDR_HIP(hipGetLastError());
-                    return GSDR_OK;
-                }
-        }
     static_assert(RP::N * ROUT > 0, "plan");
     if (RP::N * ROUT != (int)a->N)
         {
@@ -109,62 +84,20 @@ int launch_one(gsdr_acq* a, uint32_t nblocks, hipStream_t s, const gsdr_acq_resu
     if (ROUT > 1 && !ARG)
         GSDR_HIP(hipMemsetAsync(a->d_stats, 0, (size_t)nblocks * a->nprn * a->D * sizeof(RowStat), s));
     const uint32_t grid = ARG ? nblocks * a->nprn * ROUT : nblocks * a->D * a->nprn * ROUT;
-    if constexpr (ROUT > 1 && ABL == 0 && !ARG)
-        {
-            if (a->pre && a->d_pre)
-                {
-                    // the outer DIF step as its own pass, then M-point sub-transforms; in
-                    // chunks of pre_chunk PRNs over two buffers, chunk i + 1's pass on
-                    // pre_stream overlapping chunk i's grid pass on s
-                    constexpr uint32_t M = RP::N;
-                    const uint32_t C = a->pre_chunk, P = a->nprn;
-                    const size_t per = (size_t)nblocks * a->D * C * a->N;  // buffer stride (complex)
-                    GSDR_HIP(hipEventRecord(a->pre_ev[2], s));  // s's earlier work (the forward spectra, the memset)
-                    GSDR_HIP(hipStreamWaitEvent(a->pre_stream, a->pre_ev[2], 0));
-                    for (uint32_t p0 = 0, i = 0; p0 < P; p0 += C, ++i)
-                        {
-                            const uint32_t np = P - p0 < C ? P - p0 : C, k = i & 1;
-                            float2* buf = a->d_pre + k * per;
-                            if (i >= 2) GSDR_HIP(hipStreamWaitEvent(a->pre_stream, a->pre_ev[2 + k], 0));
-                            hipLaunchKernelGGL((acq_split_pre_kernel<ROUT>), dim3((M + 255) / 256, nblocks * a->D, np),
-                                dim3(256), 0, a->pre_stream, a->d_X, a->d_code_fft, buf, a->d_tw, a->D, np, M, a->xm, p0);
-                            GSDR_HIP(hipEventRecord(a->pre_ev[k], a->pre_stream));
-                            GSDR_HIP(hipStreamWaitEvent(s, a->pre_ev[k], 0));
-                            hipLaunchKernelGGL((acq_correlate_split_kernel<ROUT, RP, HALF, 0, false, false, true>),
-                                dim3(nblocks * a->D * np * ROUT), dim3(RP::NT), RP::lds_bytes(), s, buf, a->d_code_fft,
-                                a->d_stats, a->d_tw, a->D, np, nblocks, prn_group(np, a->N), a->xm, sel, a->d_keys, rowbuf,
-                                psum, (p0 << 16) | P);
-                            GSDR_HIP(hipEventRecord(a->pre_ev[2 + k], s));
-                        }
-                    GSDR_HIP(hipGetLastError());
-                    return GSDR_OK;
-                }
-        }
-    hipLaunchKernelGGL((acq_correlate_split_kernel<ROUT, RP, HALF, ABL, ARG>), dim3(grid), dim3(RP::NT),
-        RP::lds_bytes(), s, a->d_X, a->d_code_fft, a->d_stats, a->d_tw, a->D, a->nprn, nblocks,
-        prn_group(a->nprn, a->N), a->xm, sel, a->d_keys, rowbuf, psum);
+    hipLaunchKernelGGL((acq_correlate_split_kernel<ROUT, RP, HALF, ARG>), dim3(grid), dim3(RP::NT), RP::lds_bytes(), s,
+        a->d_X, a->d_code_fft, a->d_stats, a->d_tw, a->D, a->nprn, nblocks, prn_group(a->nprn, a->N), a->xm, sel,
+        a->d_keys, rowbuf, psum);
     GSDR_HIP(hipGetLastError());
     return GSDR_OK;
 }
 
-template <int ROUT, class RP, bool HALF, int ABL = 0>
+template <int ROUT, class RP, bool HALF>
 int attrs_one()
 {
-    GSDR_HIP(hipFuncSetAttribute((const void*)acq_correlate_split_kernel<ROUT, RP, HALF, ABL>,
+    GSDR_HIP(hipFuncSetAttribute((const void*)acq_correlate_split_kernel<ROUT, RP, HALF>,
         hipFuncAttributeMaxDynamicSharedMemorySize, (int)RP::lds_bytes()));
-    if constexpr (ABL == 0)
-        GSDR_HIP(hipFuncSetAttribute((const void*)acq_correlate_split_kernel<ROUT, RP, HALF, 0, true>,
-            hipFuncAttributeMaxDynamicSharedMemorySize, (int)RP::lds_bytes()));
-    if constexpr (ABL == 0 && ROUT > 1)
-        GSDR_HIP(hipFuncSetAttribute((const void*)acq_correlate_split_kernel<ROUT, RP, HALF, 0, false, false, true>,
-            hipFuncAttributeMaxDynamicSharedMemorySize, (int)RP::lds_bytes()));
-    if constexpr (ABL == 0 && herm_ok<RP>)
-        {
-            GSDR_HIP(hipFuncSetAttribute((const void*)acq_correlate_split_kernel<ROUT, RP, HALF, 0, false, true>,
-                hipFuncAttributeMaxDynamicSharedMemorySize, (int)RP::lds_bytes()));
-            GSDR_HIP(hipFuncSetAttribute((const void*)acq_correlate_split_kernel<ROUT, RP, HALF, 0, true, true>,
-                hipFuncAttributeMaxDynamicSharedMemorySize, (int)RP::lds_bytes()));
-        }
+    GSDR_HIP(hipFuncSetAttribute((const void*)acq_correlate_split_kernel<ROUT, RP, HALF, true>,
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)RP::lds_bytes()));
     return GSDR_OK;
 }
 
@@ -174,8 +107,8 @@ int launch_split_arg(gsdr_acq* a, uint32_t nblocks, hipStream_t s, const gsdr_ac
 {
     const bool half = a->eff != a->N;
 #define GSDR_ARG(RO, RP)                                                                                    \
-    return half ? launch_one<RO, RP, true, 0, true>(a, nblocks, s, sel, rowbuf, psum, rout)                 \
-                : launch_one<RO, RP, false, 0, true>(a, nblocks, s, sel, rowbuf, psum, rout)
+    return half ? launch_one<RO, RP, true, true>(a, nblocks, s, sel, rowbuf, psum, rout)                    \
+                : launch_one<RO, RP, false, true>(a, nblocks, s, sel, rowbuf, psum, rout)
     switch (a->split)
         {
         case 1: GSDR_ARG(1, Reg25k);
@@ -185,8 +118,8 @@ int launch_split_arg(gsdr_acq* a, uint32_t nblocks, hipStream_t s, const gsdr_ac
         case 5: GSDR_ARG(2, Reg16k);
         case 6: GSDR_ARG(4, Reg16k);
         case 11: GSDR_ARG(1, Wl25k);
-        case 12: case 112: case 212: GSDR_ARG(1, Wl32k);
-        case 13: case 113: case 213: GSDR_ARG(2, Wl32k);
+        case 12: GSDR_ARG(1, Wl32k);
+        case 13: GSDR_ARG(2, Wl32k);
         case 14: GSDR_ARG(4, Wl25k);
         case 15: GSDR_ARG(2, Wl16k);
         case 16: GSDR_ARG(4, Wl16k);
@@ -194,7 +127,6 @@ int launch_split_arg(gsdr_acq* a, uint32_t nblocks, hipStream_t s, const gsdr_ac
         case 18: GSDR_ARG(4, Wl25kW);
         case 19: GSDR_ARG(1, Wl32kP);
         case 20: GSDR_ARG(2, Wl32kP);
-        case 21: GSDR_ARG(2, Wl50k);
         default: gsdr::set_error("internal: bad split variant %d", a->split); return GSDR_E_STATE;
         }
 #undef GSDR_ARG
@@ -240,11 +172,6 @@ int launch_split(gsdr_acq* a, uint32_t nblocks, hipStream_t s)
         case 18: return half ? launch_one<4, Wl25kW, true>(a, nblocks, s) : launch_one<4, Wl25kW, false>(a, nblocks, s);
         case 19: return half ? launch_one<1, Wl32kP, true>(a, nblocks, s) : launch_one<1, Wl32kP, false>(a, nblocks, s);
         case 20: return half ? launch_one<2, Wl32kP, true>(a, nblocks, s) : launch_one<2, Wl32kP, false>(a, nblocks, s);
-        case 21: return half ? launch_one<2, Wl50k, true>(a, nblocks, s) : launch_one<2, Wl50k, false>(a, nblocks, s);
-        case 112: return launch_one<1, Wl32k, false, 1>(a, nblocks, s);
-        case 212: return launch_one<1, Wl32k, false, 2>(a, nblocks, s);
-        case 113: return launch_one<2, Wl32k, true, 1>(a, nblocks, s);
-        case 213: return launch_one<2, Wl32k, true, 2>(a, nblocks, s);
         default: gsdr::set_error("internal: bad split variant %d", a->split); return GSDR_E_STATE;
         }
 }
@@ -266,7 +193,7 @@ int setup_split(gsdr_acq* a)
     if (mode == 0) return GSDR_OK;
     for (const SplitId& sp : kSplits)
         if (sp.n == a->N && !a->split) a->split = sp.id;
-    if ((a->split == 14 || a->split == 18 || a->split == 21) && mode < 2) a->split = 0;
+    if ((a->split == 14 || a->split == 18) && mode < 2) a->split = 0;
     // experiments: GSDR_ACQ_SPLIT_ID forces a split of the handle's N
     if (const char* e = std::getenv("GSDR_ACQ_SPLIT_ID"))
         {
@@ -294,11 +221,6 @@ int setup_split(gsdr_acq* a)
         case 18: rc = attrs_one<4, Wl25kW, true>() | attrs_one<4, Wl25kW, false>(); break;
         case 19: rc = attrs_one<1, Wl32kP, true>() | attrs_one<1, Wl32kP, false>(); break;
         case 20: rc = attrs_one<2, Wl32kP, true>() | attrs_one<2, Wl32kP, false>(); break;
-        case 21: rc = attrs_one<2, Wl50k, true>() | attrs_one<2, Wl50k, false>(); break;
-        case 112: rc = attrs_one<1, Wl32k, false, 1>() | attrs_one<1, Wl32k, true>() | attrs_one<1, Wl32k, false>(); break;
-        case 212: rc = attrs_one<1, Wl32k, false, 2>() | attrs_one<1, Wl32k, true>() | attrs_one<1, Wl32k, false>(); break;
-        case 113: rc = attrs_one<2, Wl32k, true, 1>() | attrs_one<2, Wl32k, true>() | attrs_one<2, Wl32k, false>(); break;
-        case 213: rc = attrs_one<2, Wl32k, true, 2>() | attrs_one<2, Wl32k, true>() | attrs_one<2, Wl32k, false>(); break;
         default: break;
         }
     if (rc != GSDR_OK) a->split = 0;

@@ -118,49 +118,18 @@ __device__ __forceinline__ void static_for(F& f)
 }
 
 // ---- twiddle powers ----
-// v[r] *= w1^r for r = 1 .. R-1.  GSDR_TW_TREE 0: one chain w <- w w1 (R-2
-// dependent complex products); 1: baby-step / giant-step -- the powers w^1 .. w^(S-1)
-// and the giants w^(S a), then w^(S a + b) = w^(S a) w^b -- the same R-2 products
-// with a dependency depth of about log2(S) + R/S instead of R-2.  Measured in r04e:
-// within noise at N = 4000 / 16000 / 32000, 7 % slower on the 64000 split (register
-// pressure), so off.
-#ifndef GSDR_TW_TREE
-#define GSDR_TW_TREE 0
-#endif
+// v[r] *= w1^r for r = 1 .. R-1 by one chain w <- w w1 (R-2 dependent complex
+// products).  A baby-step / giant-step tree with a shorter dependency (r04e) was
+// within noise at N = 4000 / 16000 / 32000 and 7 % slower on the 64000 split.
 template <int R>
 __device__ __forceinline__ void apply_powers(c2* v, c2 w1)
 {
-    if constexpr (R <= 2 || !GSDR_TW_TREE)
+    c2 w = w1;
+#pragma unroll
+    for (int r = 1; r < R; ++r)
         {
-            c2 w = w1;
-#pragma unroll
-            for (int r = 1; r < R; ++r)
-                {
-                    if (r > 1) w = mul(w, w1);
-                    v[r] = mul(v[r], w);
-                }
-        }
-    else
-        {
-            constexpr int S = R >= 32 ? 8 : (R % 5 == 0 ? 5 : 4);
-            c2 b[S];  // b[k] = w^k, k < S
-            b[1] = w1;
-#pragma unroll
-            for (int k = 2; k < S; ++k) b[k] = mul(b[k / 2], b[k - k / 2]);
-            const c2 g1 = mul(b[S / 2], b[S - S / 2]);  // w^S
-            c2 g = g1;
-#pragma unroll
-            for (int r = 1; r < R; ++r)
-                {
-                    const int a = r / S, k = r % S;
-                    if (a > 1 && k == 0) g = mul(g, g1);  // w^(S a)
-                    if (a == 0)
-                        v[r] = mul(v[r], b[k]);
-                    else if (k == 0)
-                        v[r] = mul(v[r], g);
-                    else
-                        v[r] = mul(v[r], mul(g, b[k]));
-                }
+            if (r > 1) w = mul(w, w1);
+            v[r] = mul(v[r], w);
         }
 }
 
@@ -305,52 +274,6 @@ struct Dft<32> : DftCT<4, 8>
 {
 };
 
-// ---- per-stage twiddle table (TWP == 2) ----
-// Row length for a radix-R stage: the R-1 roots, padded to an even count.
-constexpr int stage_tw_row(int R) { return (R - 1 + 1) & ~1; }
-// LDS copy of the middle stage's table (TWP == 3): rows of stage_tw_row(R) + 2
-// entries, so 16 lanes reading 16 different rows with ds_read_b128 hit 16
-// different bank quads (row stride 36 dwords for R = 16).
-constexpr int lds_tw_row(int R) { return stage_tw_row(R) + 2; }
-
-template <int... Rs>
-constexpr size_t stage_tw_entries()
-{
-    constexpr int r[] = {Rs...};
-    size_t n = 0;
-    int ns = r[0];
-    for (size_t s = 1; s < sizeof...(Rs); ++s)
-        {
-            n += (size_t)ns * stage_tw_row(r[s]);
-            ns *= r[s];
-        }
-    return n;
-}
-
-// Host: entries N, N+1, ... of the table the kernels read: for every non-first
-// stage s (radix R, Ns-point sub-transforms, TSTRIDE = N/(Ns R)) and k < Ns the
-// row W_N^{r k TSTRIDE}, r = 1..R-1 (angles in double, rounded once).
-template <int... Rs>
-inline void stage_tw_fill(float2* tw, int N)
-{
-    constexpr int r[] = {Rs...};
-    size_t o = (size_t)N;
-    int ns = r[0];
-    for (size_t s = 1; s < sizeof...(Rs); ++s)
-        {
-            const int R = r[s], row = stage_tw_row(R), ts = N / (ns * R);
-            for (int k = 0; k < ns; ++k)
-                for (int q = 0; q < row; ++q)
-                    {
-                        const long m = q + 1 < R ? (long)(q + 1) * k * ts % N : 0;
-                        const double ang = 2.0 * 3.141592653589793238462643383279502884 * (double)m / (double)N;
-                        tw[o + (size_t)k * row + q] = make_float2((float)std::cos(ang), (float)(-std::sin(ang)));
-                    }
-            o += (size_t)ns * row;
-            ns *= R;
-        }
-}
-
 // One Stockham stage over an N-point LDS buffer of c2.
 //   TWP: inter-stage twiddles as powers of one table root (1 VMEM load per
 //        butterfly, R-2 extra complex multiplies); else R-1 table loads.
@@ -358,30 +281,13 @@ inline void stage_tw_fill(float2* tw, int N)
 //        first-maximum scan needs it); without ORD it visits butterfly by
 //        butterfly, so a partially filled pass is skipped as a whole instead of
 //        predicating every output (order-free reductions: max, sum).
-//   PADL (TWP_ >> 4): the buffer the last stage reads holds its N/RL-element
-//        blocks at a stride of N/RL + PADL, so the penultimate stage's strided
-//        writes spread over the LDS banks (bank model of MI355X_MICROARCH.md LDS:
-//        PADL = 9 makes the 25 x 16 x 10 plan's transposes conflict-free).
-template <int R, int NT, int N, int Ns, int TWP_, int TOFF, bool FIRST, bool LAST, bool PEN, bool ORD, class Load,
-    class Store, class Hook>
+// Measured and removed: twiddles from a per-stage table (-23 %)
+// or an LDS copy of the middle stage's roots (-2.5 %), last-stage block padding
+// (modelled conflicts removed, no gain), the barrier moved behind the butterflies
+// or dropped before the last stage (within noise).
+template <int R, int NT, int N, int Ns, bool TWP, bool FIRST, bool LAST, bool ORD, class Load, class Store, class Hook>
 __device__ __forceinline__ void stage(c2* lds, const float2* __restrict__ tw, Load& load, Store& store, Hook& hook)
 {
-    constexpr int TWP = TWP_ & 15;
-    constexpr int PADL = (TWP_ >> 4) & 15;
-    // LATE (TWP_ bit 8): the barrier that keeps the in-place Stockham exchange
-    // safe (every wave's reads done before any wave's writes) moves from between
-    // this stage's LDS reads and its butterflies to between the butterflies and its
-    // writes, so the read latency overlaps the twiddles and the DFT; the last
-    // stage needs none (its caller separates the next LDS writes with a barrier)
-    constexpr bool LATE = ((TWP_ >> 8) & 1) != 0;
-    constexpr bool DEFER = LATE && !FIRST && !LAST;
-    // LASTNB (TWP_ bit 9): only the last stage's read barrier dropped -- it writes no
-    // LDS, and every caller separates the next transform's LDS writes by a barrier of
-    // its own (the correlate's row-statistic exchange, FourStepPkPlan's per-row sync)
-    constexpr bool LASTNB = ((TWP_ >> 9) & 1) != 0;
-    // elements before the TWP 3 table: N plus the last-stage pads (this stage is
-    // the penultimate one whenever it reads the table)
-    constexpr int DATA = N + (N / (Ns * R) - 1) * PADL;
     constexpr int BPT = fft::bpt_for(R);
     constexpr int NB = N / R;
     constexpr int TSTRIDE = N / (Ns * R);
@@ -403,7 +309,7 @@ __device__ __forceinline__ void stage(c2* lds, const float2* __restrict__ tw, Lo
                             if constexpr (FIRST)
                                 v[b][r] = load(b, r, jj + r * NB);
                             else
-                                v[b][r] = lds[jj + r * NB + (LAST ? r * PADL : 0)];
+                                v[b][r] = lds[jj + r * NB];
                         }
                 }
             else if (NB % NT == 0 || j < NB)
@@ -414,20 +320,18 @@ __device__ __forceinline__ void stage(c2* lds, const float2* __restrict__ tw, Lo
                             if constexpr (FIRST)
                                 v[b][r] = load(b, r, j + r * NB);
                             else
-                                v[b][r] = lds[j + r * NB + (LAST ? r * PADL : 0)];
+                                v[b][r] = lds[j + r * NB];
                         }
                 }
         }
     if constexpr (FIRST)
         hook();
-    else if constexpr (!LATE && !(LAST && LASTNB))
+    else
         __syncthreads();
-    int kk[BPT];
 #pragma unroll
     for (int b = 0; b < BPT; ++b)
         {
             const int j = (int)threadIdx.x + b * NT;
-            kk[b] = 0;
             if (NB % NT == 0 || j < NB)
                 {
                     int k = 0;
@@ -435,35 +339,8 @@ __device__ __forceinline__ void stage(c2* lds, const float2* __restrict__ tw, Lo
                         {
                             k = j % Ns;
                             const int step = k * TSTRIDE;
-                            // TWP 3: the middle stage reads its roots from the LDS copy
-                            // of the per-stage table (PkPlan::run fills it), the last
-                            // stage forms powers as TWP 1
-                            constexpr int MODE = TWP == 3 ? (LAST ? 1 : 3) : TWP;
-                            if constexpr (MODE == 3)
-                                {
-                                    const c2* lt = lds + DATA + k * lds_tw_row(R);
-#pragma unroll
-                                    for (int r = 1; r < R; ++r) v[b][r] = mul(v[b][r], lt[r - 1]);
-                                }
-                            else if constexpr (MODE == 2)
-                                {
-                                    // per-stage table (stage_tw_fill): row k holds W_N^{r k TSTRIDE},
-                                    // r = 1..R-1, padded to an even count -> 16-byte loads
-                                    constexpr int PR = stage_tw_row(R);
-                                    const float4* t4 = reinterpret_cast<const float4*>(tw + TOFF + k * PR);
-#pragma unroll
-                                    for (int h = 0; h < PR / 2; ++h)
-                                        {
-                                            const float4 q = t4[h];
-                                            const int r0 = 2 * h + 1;
-                                            v[b][r0] = mul(v[b][r0], c2{q.x, q.y});
-                                            if (r0 + 1 < R) v[b][r0 + 1] = mul(v[b][r0 + 1], c2{q.z, q.w});
-                                        }
-                                }
-                            else if constexpr (MODE == 1)
-                                {
-                                    apply_powers<R>(v[b], from(tw[step]));
-                                }
+                            if constexpr (TWP)
+                                apply_powers<R>(v[b], from(tw[step]));
                             else
                                 {
 #pragma unroll
@@ -471,27 +348,10 @@ __device__ __forceinline__ void stage(c2* lds, const float2* __restrict__ tw, Lo
                                 }
                         }
                     Dft<R>::run(v[b]);
-                    kk[b] = k;
-                    if constexpr (!LAST && !DEFER)
+                    if constexpr (!LAST)
                         {
                             // block (j - k) R / (Ns R) = j / Ns of the last stage's input
-                            const int base = (j - k) * R + k + (PEN ? (j / Ns) * PADL : 0);
-#pragma unroll
-                            for (int r = 0; r < R; ++r) lds[base + r * Ns] = v[b][r];
-                        }
-                }
-        }
-    if constexpr (DEFER)
-        {
-            __syncthreads();
-#pragma unroll
-            for (int b = 0; b < BPT; ++b)
-                {
-                    const int j = (int)threadIdx.x + b * NT;
-                    if (NB % NT == 0 || j < NB)
-                        {
-                            const int k = kk[b];
-                            const int base = (j - k) * R + k + (PEN ? (j / Ns) * PADL : 0);
+                            const int base = (j - k) * R + k;
 #pragma unroll
                             for (int r = 0; r < R; ++r) lds[base + r * Ns] = v[b][r];
                         }
@@ -532,48 +392,30 @@ __device__ __forceinline__ void stage(c2* lds, const float2* __restrict__ tw, Lo
         __syncthreads();
 }
 
-// TOFF: the stage's first entry in the per-stage twiddle table (TWP == 2), which
-// follows the N-entry W_N table; a stage of radix R over Ns-point sub-transforms
-// holds Ns rows of stage_tw_row(R) entries.
-template <int NT, int N, int Ns, int TWP, int TOFF, bool FIRST, bool ORD, int R, int... Rest, class Load, class Store,
-    class Hook>
+template <int NT, int N, int Ns, bool TWP, bool FIRST, bool ORD, int R, int... Rest, class Load, class Store, class Hook>
 __device__ __forceinline__ void stages(c2* lds, const float2* __restrict__ tw, Load& load, Store& store, Hook& hook)
 {
     constexpr bool LAST = sizeof...(Rest) == 0;
-    constexpr bool PEN = sizeof...(Rest) == 1;
-    stage<R, NT, N, Ns, TWP, TOFF, FIRST, LAST, PEN, ORD>(lds, tw, load, store, hook);
-    constexpr int NEXT = FIRST ? TOFF : TOFF + Ns * stage_tw_row(R);
-    if constexpr (!LAST) stages<NT, N, Ns * R, TWP, NEXT, false, ORD, Rest...>(lds, tw, load, store, hook);
+    stage<R, NT, N, Ns, TWP, FIRST, LAST, ORD>(lds, tw, load, store, hook);
+    if constexpr (!LAST) stages<NT, N, Ns * R, TWP, false, ORD, Rest...>(lds, tw, load, store, hook);
 }
 
 // Compile-time packed plan.  load(b, r, i) -> c2 returns input element i
 // (= j + r*N/R1 of this lane's b-th first-stage butterfly j); store(i, c2)
 // consumes output element i, visited in increasing i per lane; hook() runs
 // once the first stage's inputs are in registers (before its butterflies).
-//   TWP: 0 inter-stage twiddles as R-1 loads from the W_N table, 1 as powers of one
-//        loaded root, 2 from the per-stage table (stage_tw_fill: R-1 consecutive
-//        roots per butterfly, 16-byte loads, no multiplies to form them).
+//   TWP: inter-stage twiddles as powers of one loaded root (1) or R-1 loads (0).
 template <int NT_, int TWP_, int... Rs>
 struct PkPlan
 {
     static constexpr int NT = NT_;
-    static constexpr int TWP = TWP_ & 15;   // TWP_ >> 4: PADL (stage())
-    static constexpr int PADL = (TWP_ >> 4) & 15;
-    // entries of the twiddle table the kernels read: W_N (N) + the per-stage table
-    static constexpr size_t tw_entries() { return (size_t)N + (TWP >= 2 ? stage_tw_entries<Rs...>() : 0); }
-    // host: fill tw[N ..) with the per-stage table (tw[0, N) = W_N^m is the caller's)
-    static void fill_stage_tw(float2* tw) { stage_tw_fill<Rs...>(tw, N); }
+    static constexpr bool TWP = TWP_ != 0;
     static constexpr int N = (Rs * ...);
     static constexpr int nstages = sizeof...(Rs);
     static constexpr int R1 = fft::FirstRadix<Rs...>::value;
     static constexpr int BPT1 = fft::bpt_for(R1);
     static constexpr int NB1 = N / R1;
-    static constexpr int R2 = fft::SecondRadix<Rs...>::value;
-    static_assert(TWP != 3 || sizeof...(Rs) == 3, "TWP 3: one middle stage");
-    // TWP 3: the middle stage's table (R1 rows of its R2 - 1 roots) after the data
-    static constexpr int LTW = TWP == 3 ? R1 * lds_tw_row(R2) : 0;
-    static constexpr int DATA = N + ((0, ..., Rs) - 1) * PADL;  // N + (RL - 1) PADL
-    static constexpr size_t lds_bytes() { return (size_t)(DATA + LTW) * sizeof(c2); }
+    static constexpr size_t lds_bytes() { return (size_t)N * sizeof(c2); }
     // last stage: radix, butterflies per thread, output stride; store(i, v, slot)
     // receives slot = r*BPTL + b in [0, RL*BPTL), this lane's output order
     static constexpr int RL = (0, ..., Rs);
@@ -587,20 +429,7 @@ struct PkPlan
     template <bool ORD = true, class Load, class Store, class Hook>
     __device__ __forceinline__ static void run(c2* lds, const float2* __restrict__ tw, Load load, Store store, Hook hook)
     {
-        if constexpr (TWP == 3)
-            {
-                // copy the middle stage's rows (global per-stage table at tw[N]) to
-                // LDS; the first stage's barrier orders these writes before the
-                // middle stage's reads, and a rewrite (next transform) stores the
-                // same values
-                constexpr int RW = stage_tw_row(R2);
-                for (int i = (int)threadIdx.x; i < R1 * RW; i += NT)
-                    {
-                        const int row = i / RW, q = i - row * RW;
-                        lds[DATA + row * lds_tw_row(R2) + q] = from(tw[N + i]);
-                    }
-            }
-        stages<NT, N, 1, TWP_, N, true, ORD, Rs...>(lds, tw, load, store, hook);
+        stages<NT, N, 1, TWP, true, ORD, Rs...>(lds, tw, load, store, hook);
     }
 };
 

@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <condition_variable>
 #include <mutex>
 #include <new>
@@ -167,18 +168,23 @@ int gsdr_stream_push(gsdr_stream* s, const void* iq_host, uint64_t first_sample,
             s->started = true;
             s->base = s->head = first_sample;
         }
-    GSDR_REQUIRE(first_sample == s->head, GSDR_E_ARG,
-        "gsdr_stream_push: items must be contiguous (next is %llu, got %llu)", (unsigned long long)s->head,
-        (unsigned long long)first_sample);
     GSDR_REQUIRE(n <= s->cap, GSDR_E_ARG, "gsdr_stream_push: %llu items exceed the ring capacity %llu",
         (unsigned long long)n, (unsigned long long)s->cap);
-    if (n == 0) return GSDR_OK;
     // samples below new_oldest lose their ring positions: an async window still
     // open over them must be released first (its reads are not enqueued yet, so
-    // the reader event cannot cover them)
-    const uint64_t new_oldest = s->head + n > s->cap ? s->head + n - s->cap : 0;
+    // the reader event cannot cover them).  The wait drops the lock, so the head
+    // (another pusher) and the windows are re-read after every wakeup; a window
+    // left open for kStallLimit (a consumer that failed before its release) ends
+    // the push with GSDR_E_STATE instead of hanging it.
+    constexpr auto kStallLimit = std::chrono::seconds(10);
+    const auto deadline = std::chrono::steady_clock::now() + kStallLimit;
     for (;;)
         {
+            GSDR_REQUIRE(first_sample == s->head, GSDR_E_ARG,
+                "gsdr_stream_push: items must be contiguous (next is %llu, got %llu)", (unsigned long long)s->head,
+                (unsigned long long)first_sample);
+            if (n == 0) return GSDR_OK;
+            const uint64_t new_oldest = s->head + n > s->cap ? s->head + n - s->cap : 0;
             bool blocked = false;
             for (const auto& w : s->open)
                 if (w.first < new_oldest)
@@ -189,7 +195,9 @@ int gsdr_stream_push(gsdr_stream* s, const void* iq_host, uint64_t first_sample,
                         blocked = true;
                     }
             if (!blocked) break;
-            s->released.wait(lk);
+            GSDR_REQUIRE(s->released.wait_until(lk, deadline) != std::cv_status::timeout, GSDR_E_STATE,
+                "gsdr_stream_push: a window over the items it would overwrite stayed open for %lld s "
+                "(gsdr_stream_release missing)", (long long)kStallLimit.count());
         }
     // overwrite only what no consumer launch still reads
     GSDR_HIP(hipStreamWaitEvent(s->copy, s->read, 0));

@@ -2433,6 +2433,25 @@ int gsdr_trk_stop(gsdr_trk* k, int ch)
     return GSDR_OK;
 }
 
+// msg_handler_telemetry_to_trk (dll_pll_veml_tracking.cc:614-637): a telemetry fault
+// sets d_carrier_lock_fail_counter = 200000, so the next lock check that evaluates the
+// counters (states 2 / 4 with a full CN0 buffer, :986-1024) reports the loss of lock.
+// Written into the channel's device state between launches, like gsdr_trk_stop.
+int gsdr_trk_force_loss_of_lock(gsdr_trk* k, int ch)
+{
+    GSDR_REQUIRE(k, GSDR_E_ARG, "gsdr_trk_force_loss_of_lock: null handle");
+    GSDR_REQUIRE(ch >= 0 && ch < (int)k->conf.max_channels, GSDR_E_ARG, "gsdr_trk_force_loss_of_lock: channel %d", ch);
+    std::lock_guard<std::mutex> lk(k->mu);
+    gsdr::DeviceGuard g(k->device);
+    const int32_t forced = 200000;
+    GSDR_HIP(hipStreamWaitEvent(k->stream, k->last_launch, 0));
+    GSDR_HIP(hipMemcpyAsync(reinterpret_cast<char*>(k->d_chans + ch) + offsetof(TrkChan, h) +
+                                offsetof(TrkHot, carrier_lock_fail_counter),
+        &forced, sizeof(forced), hipMemcpyHostToDevice, k->stream));
+    GSDR_HIP(hipStreamSynchronize(k->stream));
+    return GSDR_OK;
+}
+
 int gsdr_trk_run_device(gsdr_trk* k, const void* iq_dev, uint64_t iq_first_sample, uint64_t iq_items, uint32_t max_epochs,
     gsdr_trk_epoch* out_dev, uint32_t* n_out_dev, void* stream)
 {

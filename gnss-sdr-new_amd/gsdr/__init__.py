@@ -3,6 +3,7 @@ engine).  Thin ctypes layer over the C ABI declared in include/gsdr.h; used by t
 tests, bench.py and __graft_entry__.  It has no compute of its own and no CPU
 fallback: if the HIP library cannot be loaded, every entry point raises.
 """
+import contextlib
 import ctypes
 import os
 
@@ -44,7 +45,8 @@ EXPORTED = [
     "gsdr_acq_set_step_two", "gsdr_acq_get_step_two_threshold", "gsdr_acq_run_step_two",
     "gsdr_trk_set_data_code", "gsdr_acq_read_profile_ex", "gsdr_stream_window_async", "gsdr_stream_release", "gsdr_stream_device",
     "gsdr_acq_dump_grid_step_two", "gsdr_acq_read_profile_intervals", "gsdr_acq_set_wipeoff",
-    "gsdr_acq_get_spectrum_reuse",
+    "gsdr_acq_get_spectrum_reuse", "gsdr_trk_force_loss_of_lock", "gsdr_acq_set_local_code",
+    "gsdr_acq_set_active_prns", "gsdr_acq_submit_stream", "gsdr_acq_collect",
 ]
 
 WIPE_EXACT, WIPE_GENERIC, WIPE_AVX2 = 0, 1, 2
@@ -262,6 +264,11 @@ def load():
     L.gsdr_trk_destroy.restype = None
     L.gsdr_trk_start.argtypes = [P, I, U32, P, I, ctypes.c_double, ctypes.c_double, U64, U64, P]
     L.gsdr_trk_stop.argtypes = [P, I]
+    L.gsdr_trk_force_loss_of_lock.argtypes = [P, I]
+    L.gsdr_acq_set_local_code.argtypes = [P, U32, P, U32]
+    L.gsdr_acq_set_active_prns.argtypes = [P, U32]
+    L.gsdr_acq_submit_stream.argtypes = [P, P, U64, U32, U64]
+    L.gsdr_acq_collect.argtypes = [P, P, P, P]
     L.gsdr_trk_set_data_code.argtypes = [P, I, P, I]
     L.gsdr_trk_run_device.argtypes = [P, P, U64, U64, U32, P, P, P]
     L.gsdr_trk_run.argtypes = [P, P, U64, U64, U32, P, P]
@@ -635,6 +642,11 @@ class Tracking:
     def stop(self, ch):
         _check(load().gsdr_trk_stop(self._h, int(ch)))
 
+    def force_loss_of_lock(self, ch):
+        """A telemetry fault for channel ch (msg_handler_telemetry_to_trk,
+        dll_pll_veml_tracking.cc:614-637): its next lock check reports loss of lock."""
+        _check(load().gsdr_trk_force_loss_of_lock(self._h, int(ch)))
+
     def run(self, iq, iq_first_sample, max_epochs):
         """Synchronous: host IQ -> (records [max_channels, max_epochs], counts [max_channels])."""
         item = int(self.conf["item_type"][0])
@@ -738,6 +750,17 @@ class Stream:
 
     def release(self, consumer_stream):
         _check(load().gsdr_stream_release(self._h, ctypes.c_void_p(consumer_stream)))
+
+    @contextlib.contextmanager
+    def reading(self, first_sample, n_items, consumer_stream):
+        """window_async .. release as a context: the window is released (the
+        reads enqueued so far covered) even when the consumer's code raises, so a
+        later push never waits on a window nobody will close."""
+        p = self.window_async(first_sample, n_items, consumer_stream)
+        try:
+            yield p
+        finally:
+            self.release(consumer_stream)
 
     @property
     def device(self):

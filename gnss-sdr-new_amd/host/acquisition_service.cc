@@ -7,11 +7,12 @@
 #include <stdexcept>
 #include <string>
 
-AcquisitionService::AcquisitionService(const Acq_Conf& conf, uint32_t max_requests, int device)
+AcquisitionService::AcquisitionService(const Acq_Conf& conf, uint32_t max_requests, int device, uint32_t batch_blocks)
     : d_conf(conf),
       d_max(max_requests),
       d_consumed(static_cast<uint32_t>(conf.sampled_ms * conf.samples_per_ms)),
-      d_isz(conf.it_size)
+      d_isz(conf.it_size),
+      d_batch(batch_blocks ? batch_blocks : 1)
 {
     if (max_requests == 0) throw std::invalid_argument("AcquisitionService: max_requests must be > 0");
     gsdr_acq_conf c{};
@@ -25,92 +26,145 @@ AcquisitionService::AcquisitionService(const Acq_Conf& conf, uint32_t max_reques
     c.max_dwells = 1;
     c.item_type = pcps_acquisition_mi355x::engine_item_type(conf.item_type);
     c.max_prns = max_requests;
-    c.max_blocks = 1;
+    c.max_blocks = d_batch;
     c.sampled_ms = conf.sampled_ms;
     c.ms_per_code = conf.ms_per_code;
     if (gsdr_acq_create(device, &c, &d_engine) != GSDR_OK)
         throw std::runtime_error(std::string("AcquisitionService: ") + gsdr_last_error());
-    if (conf.wipeoff_mode() != GSDR_WIPE_EXACT && gsdr_acq_set_wipeoff(d_engine, conf.wipeoff_mode()) != GSDR_OK)
+    // the configuration's carrier model, whatever GSDR_ACQ_WIPE says
+    if (gsdr_acq_set_wipeoff(d_engine, conf.wipeoff_mode()) != GSDR_OK)
         throw std::runtime_error(std::string("AcquisitionService: ") + gsdr_last_error());
     gsdr_acq_get_threshold(d_engine, &d_threshold);
     d_buffer.resize(static_cast<size_t>(d_consumed) * d_isz);
+    d_slots.resize(max_requests);
+    d_res.resize(static_cast<size_t>(d_batch) * max_requests);
 }
 
-AcquisitionService::~AcquisitionService() { gsdr_acq_destroy(d_engine); }
+AcquisitionService::~AcquisitionService()
+{
+    if (d_flight.active)
+        {
+            uint32_t nb = 0, np = 0;
+            gsdr_acq_collect(d_engine, d_res.data(), &nb, &np);
+        }
+    gsdr_acq_destroy(d_engine);
+}
 
 void AcquisitionService::request(uint32_t channel, uint32_t prn, const std::complex<float>* code, Callback done)
 {
     std::lock_guard<std::mutex> lk(d_mu);
-    auto it = std::find_if(d_requests.begin(), d_requests.end(), [&](const Request& r) { return r.channel == channel; });
-    Request r{channel, prn, std::vector<std::complex<float>>(code, code + d_consumed), std::move(done)};
-    if (it != d_requests.end())
-        *it = std::move(r);
-    else
+    Slot* s = nullptr;
+    for (auto& x : d_slots)
+        if (x.used && x.channel == channel) s = &x;
+    if (!s)
         {
-            if (d_requests.size() >= d_max) throw std::length_error("AcquisitionService: more requests than max_requests");
-            d_requests.push_back(std::move(r));
+            // a free slot, preferably one still holding this PRN's spectrum
+            for (auto& x : d_slots)
+                if (!x.used && (!s || (x.loaded && x.prn == prn && !(s->loaded && s->prn == prn)))) s = &x;
+            if (!s) throw std::length_error("AcquisitionService: more requests than max_requests");
+            s->used = true;
+            s->channel = channel;
         }
-    d_codes_dirty = true;
+    if (!s->loaded || s->prn != prn)
+        {
+            s->prn = prn;
+            s->loaded = false;
+            s->code.assign(code, code + d_consumed);
+        }
+    s->armed = true;
+    s->done = std::move(done);
 }
 
 void AcquisitionService::cancel(uint32_t channel)
 {
     std::lock_guard<std::mutex> lk(d_mu);
-    const auto n = d_requests.size();
-    d_requests.erase(std::remove_if(d_requests.begin(), d_requests.end(),
-                         [&](const Request& r) { return r.channel == channel; }),
-        d_requests.end());
-    if (d_requests.size() != n) d_codes_dirty = true;
+    for (auto& x : d_slots)
+        if (x.used && x.channel == channel)
+            {
+                x.used = false;
+                x.armed = false;
+                x.done = nullptr;
+            }
 }
 
 size_t AcquisitionService::pending() const
 {
     std::lock_guard<std::mutex> lk(d_mu);
-    return d_requests.size();
+    size_t n = 0;
+    for (const auto& x : d_slots) n += x.armed ? 1 : 0;
+    return n;
 }
 
-// One batched acquisition_core over all pending requests; each request is
-// answered once (the channel re-arms it for another attempt, as the channel FSM
-// re-arms its acquisition block after a negative result).
-void AcquisitionService::run_grid(gsdr_stream* ring, uint64_t first_sample)
+bool AcquisitionService::prepare_locked(std::vector<uint64_t>& gen)
 {
-    std::vector<Request> reqs;
-    {
-        std::lock_guard<std::mutex> lk(d_mu);
-        if (d_requests.empty()) return;
-        const uint32_t P = static_cast<uint32_t>(d_requests.size());
-        if (d_codes_dirty)
-            {
-                std::vector<std::complex<float>> codes(static_cast<size_t>(P) * d_consumed);
-                std::vector<uint32_t> prns(P);
-                for (uint32_t i = 0; i < P; ++i)
-                    {
-                        std::copy(d_requests[i].code.begin(), d_requests[i].code.end(), codes.begin() + static_cast<size_t>(i) * d_consumed);
-                        prns[i] = d_requests[i].prn;
-                    }
-                if (gsdr_acq_set_local_codes(d_engine, reinterpret_cast<const float*>(codes.data()), prns.data(), P) != GSDR_OK)
-                    throw std::runtime_error(std::string("AcquisitionService: ") + gsdr_last_error());
-                d_codes_dirty = false;
-            }
-        reqs.swap(d_requests);
-        d_codes_dirty = true;
-    }
-    std::vector<gsdr_acq_result> res(reqs.size());
-    // sample stamp: the counter after the block (pcps_acquisition.cc:1009, :1019)
-    const int rc = ring ? gsdr_acq_run_stream(d_engine, ring, first_sample, 1, first_sample + d_consumed, res.data())
-                        : gsdr_acq_run(d_engine, d_buffer.data(), 1, d_sample_counter, res.data());
-    ++d_grids;
-    for (size_t i = 0; i < reqs.size(); ++i)
+    uint32_t top = 0;
+    for (uint32_t i = 0; i < d_max; ++i)
         {
-            if (rc != GSDR_OK)
+            Slot& s = d_slots[i];
+            if (!s.armed) continue;
+            top = i + 1;
+            if (!s.loaded)
                 {
-                    // device failure: a negative acquisition, the reference's failure convention
-                    gsdr_acq_result r{};
-                    r.prn = reqs[i].prn;
-                    reqs[i].done(reqs[i].channel, r, false);
+                    // set_local_code (pcps_acquisition.cc:176-209) for this slot only
+                    if (gsdr_acq_set_local_code(d_engine, i, reinterpret_cast<const float*>(s.code.data()), s.prn) != GSDR_OK)
+                        throw std::runtime_error(std::string("AcquisitionService: ") + gsdr_last_error());
+                    s.loaded = true;
+                    ++s.gen;
+                    ++d_code_uploads;
+                    std::vector<std::complex<float>>().swap(s.code);
                 }
-            else
-                reqs[i].done(reqs[i].channel, res[i], res[i].test_statistic > d_threshold);
+        }
+    if (top == 0) return false;
+    // slots below the highest armed one without a spectrum yet (never requested)
+    // are searched with whatever they hold and not answered
+    if (gsdr_acq_set_active_prns(d_engine, top) != GSDR_OK)
+        throw std::runtime_error(std::string("AcquisitionService: ") + gsdr_last_error());
+    gen.resize(top);
+    for (uint32_t i = 0; i < top; ++i) gen[i] = d_slots[i].loaded ? d_slots[i].gen : ~0ULL;
+    return true;
+}
+
+void AcquisitionService::answer(const std::vector<gsdr_acq_result>& res, uint32_t nblocks, uint32_t nprn,
+    const std::vector<uint64_t>& gen, bool device_error)
+{
+    struct Ans
+    {
+        uint32_t channel;
+        Callback done;
+        gsdr_acq_result r;
+        bool positive;
+    };
+    std::vector<Ans> ans;
+    for (uint32_t b = 0; b < nblocks; ++b)
+        {
+            ans.clear();
+            {
+                std::lock_guard<std::mutex> lk(d_mu);
+                for (uint32_t i = 0; i < nprn && i < d_max; ++i)
+                    {
+                        Slot& s = d_slots[i];
+                        // answered by this block when armed with the spectrum the launch used
+                        if (!s.armed || !s.loaded || s.gen != gen[i]) continue;
+                        s.armed = false;
+                        if (device_error)
+                            {
+                                // device failure: a negative acquisition, the reference's failure convention
+                                gsdr_acq_result r{};
+                                r.prn = s.prn;
+                                ans.push_back({s.channel, s.done, r, false});
+                            }
+                        else
+                            {
+                                const gsdr_acq_result& r = res[static_cast<size_t>(b) * nprn + i];
+                                ans.push_back({s.channel, s.done, r, r.test_statistic > d_threshold});
+                            }
+                    }
+            }
+            // callbacks outside the lock: they may re-arm (same PRN: answered by the
+            // next block of this launch)
+            for (auto& a : ans)
+                if (a.done) a.done(a.channel, a.r, a.positive);
+            if (device_error) break;
         }
 }
 
@@ -128,11 +182,33 @@ int AcquisitionService::work(const void* in, int ninput_items)
             d_sample_counter += take;
             if (d_fill == d_consumed)
                 {
-                    run_grid();
                     d_fill = 0;
+                    std::vector<uint64_t> gen;
+                    bool any;
+                    {
+                        std::lock_guard<std::mutex> lk(d_mu);
+                        any = prepare_locked(gen);
+                    }
+                    if (!any) continue;
+                    const auto nprn = static_cast<uint32_t>(gen.size());
+                    // sample stamp: the counter after the block (pcps_acquisition.cc:1009, :1019)
+                    const int rc = gsdr_acq_run(d_engine, d_buffer.data(), 1, d_sample_counter, d_res.data());
+                    ++d_grids;
+                    ++d_launches;
+                    answer(d_res, 1, nprn, gen, rc != GSDR_OK);
                 }
         }
     return used;
+}
+
+void AcquisitionService::flush()
+{
+    if (!d_flight.active) return;
+    d_flight.active = false;
+    uint32_t nb = 0, np = 0;
+    const int rc = gsdr_acq_collect(d_engine, d_res.data(), &nb, &np);
+    answer(d_res, rc == GSDR_OK ? nb : 1, rc == GSDR_OK ? np : static_cast<uint32_t>(d_flight.gen.size()), d_flight.gen,
+        rc != GSDR_OK);
 }
 
 int AcquisitionService::work_ring(gsdr_stream* ring, uint64_t head)
@@ -141,15 +217,48 @@ int AcquisitionService::work_ring(gsdr_stream* ring, uint64_t head)
         {
             d_ring_started = true;
             d_ring_cursor = head;
+            d_sample_counter = head;
             return 0;
         }
+    const uint64_t ready = head > d_ring_cursor ? (head - d_ring_cursor) / d_consumed : 0;
+    if (ready < d_batch) return 0;  // a full batch of blocks per launch
+    // the launch in flight first: its answers re-arm the requests of this one
+    flush();
     int blocks = 0;
-    while (d_ring_cursor + d_consumed <= head)
+    // blocks the ring no longer holds (the caller pushed past them) are skipped
+    uint64_t span_first = 0, span_n = 0;
+    if (gsdr_stream_span(ring, &span_first, &span_n) == GSDR_OK && span_first > d_ring_cursor)
         {
-            run_grid(ring, d_ring_cursor);
-            d_ring_cursor += d_consumed;
+            const uint64_t skip = (span_first - d_ring_cursor + d_consumed - 1) / d_consumed;
+            d_ring_cursor += skip * d_consumed;
             d_sample_counter = d_ring_cursor;
-            ++blocks;
+        }
+    uint64_t left = head > d_ring_cursor ? (head - d_ring_cursor) / d_consumed : 0;
+    while (left >= d_batch)
+        {
+            const uint32_t nb = d_batch;
+            bool any;
+            {
+                std::lock_guard<std::mutex> lk(d_mu);
+                any = prepare_locked(d_flight.gen);
+            }
+            if (any)
+                {
+                    // sample stamps: the counter after each block (pcps_acquisition.cc:1009, :1019)
+                    const int rc = gsdr_acq_submit_stream(d_engine, ring, d_ring_cursor, nb, d_ring_cursor + d_consumed);
+                    ++d_launches;
+                    d_grids += nb;
+                    if (rc != GSDR_OK)
+                        answer(d_res, 1, static_cast<uint32_t>(d_flight.gen.size()), d_flight.gen, true);
+                    else
+                        d_flight.active = true;
+                }
+            d_ring_cursor += static_cast<uint64_t>(nb) * d_consumed;
+            d_sample_counter = d_ring_cursor;
+            blocks += static_cast<int>(nb);
+            left -= nb;
+            // more than one batch behind: answer this one before the next
+            if (left >= d_batch) flush();
         }
     return blocks;
 }

@@ -16,9 +16,15 @@ dll_pll_veml_tracking_mi355x::dll_pll_veml_tracking_mi355x(const Dll_Pll_Conf& c
     d_vector_length = d_conf.vector_length;
     if (d_conf.dump) d_dump.configure(d_conf.dump_filename);
     d_item_bytes = c.item_type == GSDR_ITEM_CSHORT ? 4 : (c.item_type == GSDR_ITEM_IBYTE ? 2 : 8);
+    d_output = TrackingOutput(d_conf.fs_in, signal);
 }
 
-dll_pll_veml_tracking_mi355x::~dll_pll_veml_tracking_mi355x() { gsdr_trk_destroy(d_engine); }
+dll_pll_veml_tracking_mi355x::~dll_pll_veml_tracking_mi355x()
+{
+    // the destructor's .dat close and save_matfile (:884-906)
+    if (d_conf.dump && d_conf.dump_mat) d_dump.save_matfile();
+    gsdr_trk_destroy(d_engine);
+}
 
 void dll_pll_veml_tracking_mi355x::set_gnss_synchro(Gnss_Synchro* p_gnss_synchro)
 {
@@ -44,7 +50,25 @@ void dll_pll_veml_tracking_mi355x::stop_tracking()
 {
     std::lock_guard<std::mutex> l(d_setlock);
     d_state = 0;
+    d_fault_pending = false;
     gsdr_trk_stop(d_engine, 0);
+}
+
+void dll_pll_veml_tracking_mi355x::msg_handler_telemetry_to_trk(int tlm_event)
+{
+    if (tlm_event != 1) return;
+    std::lock_guard<std::mutex> l(d_setlock);
+    // d_carrier_lock_fail_counter = 200000 (:625): on the engine's channel while it
+    // tracks; between start_tracking and the pull-in the engine's start (which
+    // resets the counters, as start_tracking does at :836) comes first, so the
+    // fault is applied right after it; in standby the next start_tracking resets it
+    if (d_state == 2)
+        {
+            if (gsdr_trk_force_loss_of_lock(d_engine, 0) != GSDR_OK)
+                std::cerr << "dll_pll_veml_tracking_mi355x: " << gsdr_last_error() << '\n';
+        }
+    else if (d_state == 1)
+        d_fault_pending = true;
 }
 
 // The tracking replica of start_tracking (:661-700): GPS gps_l1_ca_code_gen_float,
@@ -73,10 +97,11 @@ void dll_pll_veml_tracking_mi355x::load_codes(uint32_t prn, std::vector<float>& 
 }
 
 int dll_pll_veml_tracking_mi355x::work(const void* in, int ninput_items, uint64_t nitems_read, Gnss_Synchro* out,
-    int* noutput)
+    int* noutput, TrackingTags* tags)
 {
     std::lock_guard<std::mutex> l(d_setlock);
     *noutput = 0;
+    if (tags) tags->has_out = false;
     switch (d_state)
         {
         case 0:  // standby: consume at full throttle (:1806-1811)
@@ -103,12 +128,18 @@ int dll_pll_veml_tracking_mi355x::work(const void* in, int ninput_items, uint64_
                             d_acquisition_gnss_synchro->Acq_delay_samples),
                         d_acquisition_gnss_synchro->Acq_doppler_hz);
                 d_state = 2;
+                if (d_fault_pending)
+                    {
+                        d_fault_pending = false;
+                        gsdr_trk_force_loss_of_lock(d_engine, 0);
+                    }
                 return static_cast<int>(first - nitems_read);
             }
         default:
             break;
         }
     // states 2..4: one general_work call of the engine over the forecast window
+    if (ninput_items <= 0 || !in) return 0;
     const int n = std::min(ninput_items, forecast());
     uint32_t nrec = 0;
     if (gsdr_trk_run(d_engine, in, nitems_read, static_cast<uint64_t>(n), 1, &d_last, &nrec) != GSDR_OK)
@@ -120,26 +151,12 @@ int dll_pll_veml_tracking_mi355x::work(const void* in, int ninput_items, uint64_
             return 0;
         }
     if (nrec == 0) return 0;  // not enough input for the call: wait for more items
+    if (d_record_sink) d_record_sink(d_last);
     if (d_conf.dump) d_dump.write(d_last, d_conf.fs_in, d_signal == GSDR_SIGNAL_GAL_1B, d_conf.track_pilot);
     const bool loss_of_lock = (d_last.flags & GSDR_TRK_F_LOSS_OF_LOCK) != 0;
-    if ((d_last.flags & GSDR_TRK_F_VALID_OUTPUT) || loss_of_lock)
-        {
-            // output record (:2000-2017, :2120-2127)
-            Gnss_Synchro s = *d_acquisition_gnss_synchro;
-            s.Prompt_I = d_last.prompt_i;
-            s.Prompt_Q = d_last.prompt_q;
-            s.Code_phase_samples = d_last.rem_code_phase_samples;
-            s.Carrier_phase_rads = d_last.acc_carrier_phase_rad;
-            s.Carrier_Doppler_hz = d_last.carrier_doppler_hz;
-            s.CN0_dB_hz = d_last.cn0_db_hz;
-            s.EVM = d_last.evm;
-            s.fs = static_cast<int64_t>(d_conf.fs_in);
-            s.Tracking_sample_counter = nitems_read;
-            s.Flag_valid_symbol_output = !loss_of_lock;
-            s.Flag_PLL_180_deg_phase_locked = (d_last.flags & GSDR_TRK_F_PLL_180) != 0;
-            *out = s;
-            *noutput = 1;
-        }
+    if (d_output.emit(d_last, *d_acquisition_gnss_synchro, nitems_read, out)) *noutput = 1;
+    d_output.call_tags(tags, nitems_read, d_last.consumed, *noutput ? out : nullptr, d_nitems_written);
+    d_nitems_written += static_cast<uint64_t>(*noutput);
     if (loss_of_lock)
         {
             d_state = 0;

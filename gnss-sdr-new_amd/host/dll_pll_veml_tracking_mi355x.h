@@ -17,6 +17,7 @@
 #include "gsdr.h"
 #include "tracking_block_mi355x.h"
 #include "tracking_dump.h"
+#include "tracking_output.h"
 
 class dll_pll_veml_tracking_mi355x : public TrackingBlockMI355X
 {
@@ -35,6 +36,7 @@ public:
     void start_tracking() override;
     void stop_tracking() override;
     void set_event_handler(std::function<void(int)> h) override { d_events = std::move(h); }
+    void msg_handler_telemetry_to_trk(int tlm_event) override;
 
     // forecast (:604-611): items general_work needs
     int forecast() const override { return 2 * static_cast<int>(d_vector_length); }
@@ -42,7 +44,9 @@ public:
     // first one being input sample nitems_read.  Returns the items consumed
     // (consume_each); *noutput = 1 with *out filled when a Gnss_Synchro is
     // emitted (valid symbol output or loss of lock), else 0.
-    int work(const void* in, int ninput_items, uint64_t nitems_read, Gnss_Synchro* out, int* noutput) override;
+    int work(const void* in, int ninput_items, uint64_t nitems_read, Gnss_Synchro* out, int* noutput,
+        TrackingTags* tags) override;
+    using TrackingBlockMI355X::work;
 
     int32_t state() const override { return d_state; }
     const gsdr_trk_epoch& last_record() const override { return d_last; }
@@ -62,7 +66,9 @@ private:
     gsdr_trk_epoch d_last{};
     std::function<void(int)> d_events;
     std::mutex d_setlock;
-    TrackingDump d_dump;  // <role>.dump: the reference's per-channel .dat (log_data)
+    TrackingDump d_dump;  // <role>.dump: the reference's per-channel .dat (log_data), .mat on destruction
+    TrackingOutput d_output;
+    bool d_fault_pending{false};  // telemetry fault between start_tracking and the pull-in
 };
 
 #endif

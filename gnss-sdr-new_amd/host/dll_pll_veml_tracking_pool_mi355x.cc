@@ -14,19 +14,23 @@ std::runtime_error gsdr_error(const char* what) { return std::runtime_error(std:
 }  // namespace
 
 SharedTrackingPool::SharedTrackingPool(const Dll_Pll_Conf& conf, int32_t signal, uint32_t max_channels, int device,
-    uint32_t window_calls)
+    uint32_t window_calls, uint32_t batch_calls)
     : d_conf(conf), d_signal(signal), d_max(max_channels), d_device(device)
 {
     const gsdr_trk_conf c = d_conf.to_engine(signal, max_channels);
     if (gsdr_trk_create(device, &c, &d_engine) != GSDR_OK) throw gsdr_error("SharedTrackingPool");
     d_item_bytes = c.item_type == GSDR_ITEM_CSHORT ? 4 : (c.item_type == GSDR_ITEM_IBYTE ? 2 : 8);
-    // the newest window every channel's next call must fall in: window_calls calls'
-    // worth (default 8: four forecasts of slack behind the head), and twice that of
-    // ring positions.  A block whose nitems_read lags the pool head by more (a
-    // flowgraph buffer deeper than that) needs a larger <role>.mi355x_pool_window.
+    // the newest window the channels' calls are read from (window_calls vector
+    // lengths, twice that of ring positions); the pool advances every channel
+    // whenever half a window arrived, so a channel is never more than that behind
+    // the head, and a channel started by a block whose nitems_read lags the head by
+    // up to the ring's extent still finds its items
     if (window_calls < 4)
         throw std::invalid_argument("SharedTrackingPool: mi355x_pool_window must be >= 4 vector lengths");
+    if (batch_calls < 1 || batch_calls > window_calls / 2)
+        throw std::invalid_argument("SharedTrackingPool: mi355x_pool_batch must be in [1, mi355x_pool_window / 2]");
     d_window = static_cast<uint64_t>(window_calls) * d_conf.vector_length;
+    d_batch = static_cast<uint64_t>(batch_calls) * d_conf.vector_length;
     if (gsdr_stream_create(device, c.item_type, 2 * d_window, d_window, &d_ring) != GSDR_OK)
         {
             gsdr_trk_destroy(d_engine);
@@ -45,14 +49,14 @@ SharedTrackingPool::~SharedTrackingPool()
 }
 
 std::shared_ptr<SharedTrackingPool> SharedTrackingPool::get(const std::string& key, const Dll_Pll_Conf& conf,
-    int32_t signal, uint32_t max_channels, int device, uint32_t window_calls)
+    int32_t signal, uint32_t max_channels, int device, uint32_t window_calls, uint32_t batch_calls)
 {
     static std::mutex mu;
     static std::map<std::tuple<std::string, int, int32_t>, std::weak_ptr<SharedTrackingPool>> registry;
     std::lock_guard<std::mutex> lk(mu);
     auto& w = registry[std::make_tuple(key, device, signal)];
     if (auto p = w.lock()) return p;
-    auto p = std::make_shared<SharedTrackingPool>(conf, signal, max_channels, device, window_calls);
+    auto p = std::make_shared<SharedTrackingPool>(conf, signal, max_channels, device, window_calls, batch_calls);
     w = p;
     return p;
 }
@@ -109,6 +113,13 @@ uint64_t SharedTrackingPool::start(int slot, uint32_t prn, const char signal[2],
     return first;
 }
 
+void SharedTrackingPool::force_loss_of_lock(int slot)
+{
+    std::lock_guard<std::mutex> lk(d_mu);
+    if (slot < 0 || static_cast<uint32_t>(slot) >= d_max) return;
+    if (gsdr_trk_force_loss_of_lock(d_engine, slot) != GSDR_OK) throw gsdr_error("SharedTrackingPool::force_loss_of_lock");
+}
+
 void SharedTrackingPool::stop(int slot)
 {
     std::lock_guard<std::mutex> lk(d_mu);
@@ -120,7 +131,7 @@ void SharedTrackingPool::stop(int slot)
 
 void SharedTrackingPool::advance_locked()
 {
-    const uint32_t me = 16;  // calls per channel per launch
+    const uint32_t me = 32;  // calls per channel per launch
     d_recs.resize(static_cast<size_t>(d_max) * me);
     for (;;)
         {
@@ -136,34 +147,40 @@ void SharedTrackingPool::advance_locked()
                 }
             if (most < me) break;  // a full batch: more calls may be ready in the ring
         }
+    d_advanced = d_head;
 }
 
-void SharedTrackingPool::feed(const void* in, uint64_t nitems_read, int n, bool advance)
+void SharedTrackingPool::feed(const void* in, uint64_t nitems_read, int n)
 {
     std::lock_guard<std::mutex> lk(d_mu);
     const uint64_t end = nitems_read + static_cast<uint64_t>(std::max(n, 0));
     if (!d_started)
         {
             d_started = true;
-            d_origin = d_head = nitems_read;
+            d_origin = d_head = d_advanced = nitems_read;
         }
     if (nitems_read > d_head)
         throw std::logic_error("SharedTrackingPool::feed: the stream skipped items no pooled block has seen");
     const auto* bytes = static_cast<const uint8_t*>(in);
-    // chunks of half the window, the channels advanced after each, so no active
-    // channel falls out of the ring's newest window
-    const uint64_t chunk = std::max<uint64_t>(1, d_window / 2);
-    bool pushed = false;
+    // chunks of at most half the window, the channels advanced whenever half a
+    // window arrived since the last advance: no started channel's next call ever
+    // leaves the ring's newest window
+    const uint64_t half = std::max<uint64_t>(1, d_window / 2);
     while (d_head < end)
         {
-            const uint64_t len = std::min(chunk, end - d_head);
+            const uint64_t len = std::min(half - std::min(half - 1, d_head - d_advanced), end - d_head);
             if (gsdr_stream_push(d_ring, bytes + (d_head - nitems_read) * d_item_bytes, d_head, len) != GSDR_OK)
                 throw gsdr_error("SharedTrackingPool::feed");
             d_head += len;
-            pushed = true;
-            if (advance) advance_locked();
+            if (d_head - d_advanced >= half) advance_locked();
         }
-    if (advance && !pushed) advance_locked();
+}
+
+void SharedTrackingPool::advance_if_due(bool force)
+{
+    std::lock_guard<std::mutex> lk(d_mu);
+    if (!d_started || d_head == d_advanced) return;
+    if (force || d_head - d_advanced >= d_batch) advance_locked();
 }
 
 bool SharedTrackingPool::peek(int slot, gsdr_trk_epoch* rec)
@@ -181,17 +198,23 @@ void SharedTrackingPool::drop(int slot)
 }
 
 dll_pll_veml_tracking_pool_mi355x::dll_pll_veml_tracking_pool_mi355x(const Dll_Pll_Conf& conf, int32_t signal,
-    uint32_t pool_channels, int device, const std::string& pool_key, uint32_t window_calls)
+    uint32_t pool_channels, int device, const std::string& pool_key, uint32_t window_calls, uint32_t batch_calls)
     : d_conf(conf), d_signal(signal)
 {
     if (d_conf.dump) d_dump.configure(d_conf.dump_filename);
-    d_pool = SharedTrackingPool::get(pool_key, conf, signal, pool_channels, device, window_calls);
+    d_output = TrackingOutput(d_conf.fs_in, signal);
+    d_pool = SharedTrackingPool::get(pool_key, conf, signal, pool_channels, device, window_calls, batch_calls);
     d_slot = d_pool->acquire_slot();
     if (d_slot < 0)
         throw std::runtime_error("dll_pll_veml_tracking_pool_mi355x: every slot of pool '" + pool_key + "' is taken");
 }
 
-dll_pll_veml_tracking_pool_mi355x::~dll_pll_veml_tracking_pool_mi355x() { d_pool->release_slot(d_slot); }
+dll_pll_veml_tracking_pool_mi355x::~dll_pll_veml_tracking_pool_mi355x()
+{
+    d_pool->release_slot(d_slot);
+    // the destructor's .dat close and save_matfile (:884-906)
+    if (d_conf.dump && d_conf.dump_mat) d_dump.save_matfile();
+}
 
 void dll_pll_veml_tracking_pool_mi355x::set_gnss_synchro(Gnss_Synchro* p_gnss_synchro)
 {
@@ -218,50 +241,88 @@ void dll_pll_veml_tracking_pool_mi355x::stop_tracking()
 {
     std::lock_guard<std::mutex> l(d_setlock);
     d_state = 0;
+    d_fault_pending = false;
     d_pool->stop(d_slot);
 }
 
+void dll_pll_veml_tracking_pool_mi355x::msg_handler_telemetry_to_trk(int tlm_event)
+{
+    if (tlm_event != 1) return;
+    std::lock_guard<std::mutex> l(d_setlock);
+    // as dll_pll_veml_tracking_mi355x: on the pool's channel while it tracks (the
+    // records the pool already computed for this block precede the fault and are
+    // handed out first), after the pull-in when one is pending
+    try
+        {
+            if (d_state == 2)
+                d_pool->force_loss_of_lock(d_slot);
+            else if (d_state == 1)
+                d_fault_pending = true;
+        }
+    catch (const std::exception& e)
+        {
+            std::cerr << "dll_pll_veml_tracking_pool_mi355x: " << e.what() << '\n';
+        }
+}
+
+void dll_pll_veml_tracking_pool_mi355x::flush()
+{
+    std::lock_guard<std::mutex> l(d_setlock);
+    try
+        {
+            d_pool->advance_if_due(true);
+        }
+    catch (const std::exception& e)
+        {
+            std::cerr << "dll_pll_veml_tracking_pool_mi355x: " << e.what() << '\n';
+        }
+}
+
 int dll_pll_veml_tracking_pool_mi355x::work(const void* in, int ninput_items, uint64_t nitems_read, Gnss_Synchro* out,
-    int* noutput)
+    int* noutput, TrackingTags* tags)
 {
     std::lock_guard<std::mutex> l(d_setlock);
     *noutput = 0;
+    if (tags) tags->has_out = false;
+    const int n = std::max(ninput_items, 0);
     try
         {
+            // the items handed over go into the pool's ring and are consumed; their
+            // time tags wait for the calls that cover them
+            d_pool->feed(in, nitems_read, n);
+            if (tags)
+                for (int i = 0; i < tags->n_in; ++i)
+                    if (tags->in[i].offset >= nitems_read && tags->in[i].offset < nitems_read + static_cast<uint64_t>(n))
+                        d_tags.push_back(tags->in[i]);
             switch (d_state)
                 {
-                case 0:  // standby: consume at full throttle (:1806-1811), keeping the ring gap-free
-                    d_pool->feed(in, nitems_read, ninput_items, false);
-                    return ninput_items;
+                case 0:  // standby: consume at full throttle (:1806-1811)
+                    d_tags.clear();
+                    return n;
                 case 1:
                     {
-                        // pull-in (:1813-1844): align to the next code start after nitems_read
+                        // pull-in (:1813-1844): the channel aligns to the next code start
+                        // after nitems_read on the device
                         const Gnss_Synchro* g = d_acquisition_gnss_synchro;
-                        d_pool->feed(in, nitems_read, ninput_items, false);
-                        const uint64_t first = d_pool->start(d_slot, g->PRN, g->Signal, g->Acq_delay_samples,
-                            g->Acq_doppler_hz, g->Acq_samplestamp_samples, nitems_read);
+                        d_pool->start(d_slot, g->PRN, g->Signal, g->Acq_delay_samples, g->Acq_doppler_hz,
+                            g->Acq_samplestamp_samples, nitems_read);
                         if (d_conf.dump)
                             d_dump.set_acquisition(g->PRN,
                                 TrackingDump::pull_in_code_phase(d_signal, d_conf.fs_in, nitems_read,
                                     g->Acq_samplestamp_samples, g->Acq_delay_samples),
                                 g->Acq_doppler_hz);
                         d_state = 2;
-                        return static_cast<int>(first - nitems_read);
+                        if (d_fault_pending)
+                            {
+                                d_fault_pending = false;
+                                d_pool->force_loss_of_lock(d_slot);
+                            }
+                        return n;
                     }
                 default:
                     break;
                 }
-            gsdr_trk_epoch rec;
-            if (!d_pool->peek(d_slot, &rec))
-                {
-                    d_pool->feed(in, nitems_read, ninput_items, true);
-                    if (!d_pool->peek(d_slot, &rec)) return 0;  // the call needs more items
-                }
-            // a block consumes at most what the scheduler handed it: a call computed
-            // from items other blocks pushed waits until this block is given them
-            if (rec.sample_counter == nitems_read && rec.consumed > ninput_items) return 0;
-            d_pool->drop(d_slot);
-            d_last = rec;
+            d_pool->advance_if_due(false);
         }
     catch (const std::exception& e)
         {
@@ -278,51 +339,51 @@ int dll_pll_veml_tracking_pool_mi355x::work(const void* in, int ninput_items, ui
                 }
             d_state = 0;
             if (d_events) d_events(3);
-            return 0;
+            return n;
         }
-    if (d_last.sample_counter != nitems_read)
+    // hand out this channel's computed calls in order, up to the first that emits
+    gsdr_trk_epoch rec;
+    while (d_state == 2 && d_pool->peek(d_slot, &rec))
         {
-            // the record belongs to another position than the scheduler's: a desync
-            // (items dropped upstream); report it as a loss of lock
-            std::cerr << "dll_pll_veml_tracking_pool_mi355x: record at " << d_last.sample_counter << ", input at "
-                      << nitems_read << '\n';
-            d_pool->stop(d_slot);
-            d_state = 0;
-            if (d_events) d_events(3);
-            return 0;
-        }
-    if (d_conf.dump) d_dump.write(d_last, d_conf.fs_in, d_signal == GSDR_SIGNAL_GAL_1B, d_conf.track_pilot);
-    const bool loss_of_lock = (d_last.flags & GSDR_TRK_F_LOSS_OF_LOCK) != 0;
-    if ((d_last.flags & GSDR_TRK_F_VALID_OUTPUT) || loss_of_lock)
-        {
-            // output record (:2000-2017, :2120-2127)
-            Gnss_Synchro s = *d_acquisition_gnss_synchro;
-            s.Prompt_I = d_last.prompt_i;
-            s.Prompt_Q = d_last.prompt_q;
-            s.Code_phase_samples = d_last.rem_code_phase_samples;
-            s.Carrier_phase_rads = d_last.acc_carrier_phase_rad;
-            s.Carrier_Doppler_hz = d_last.carrier_doppler_hz;
-            s.CN0_dB_hz = d_last.cn0_db_hz;
-            s.EVM = d_last.evm;
-            s.fs = static_cast<int64_t>(d_conf.fs_in);
-            s.Tracking_sample_counter = nitems_read;
-            s.Flag_valid_symbol_output = !loss_of_lock;
-            s.Flag_PLL_180_deg_phase_locked = (d_last.flags & GSDR_TRK_F_PLL_180) != 0;
-            *out = s;
-            *noutput = 1;
-        }
-    if (loss_of_lock)
-        {
-            if (d_last.flags & GSDR_TRK_F_OVERRUN)
+            d_pool->drop(d_slot);
+            d_last = rec;
+            if (d_record_sink) d_record_sink(rec);
+            if (d_conf.dump) d_dump.write(rec, d_conf.fs_in, d_signal == GSDR_SIGNAL_GAL_1B, d_conf.track_pilot);
+            const bool loss_of_lock = (rec.flags & GSDR_TRK_F_LOSS_OF_LOCK) != 0;
+            if (d_output.emit(rec, *d_acquisition_gnss_synchro, rec.sample_counter, out)) *noutput = 1;
+            // the call's time tags: those on [sample_counter, sample_counter + consumed)
+            const uint64_t end = rec.sample_counter + static_cast<uint64_t>(std::max(rec.consumed, 0));
+            std::vector<GnssTimeTag> in_call;
+            while (!d_tags.empty() && d_tags.front().offset < end)
                 {
-                    // not a signal loss: the call fell out of the pool's ring window
-                    ++d_overruns;
-                    std::cerr << "dll_pll_veml_tracking_pool_mi355x: channel " << d_channel << " call at "
-                              << d_last.sample_counter << " fell out of the ring window (" << d_pool->window_items()
-                              << " items behind the newest pushed; raise <role>.mi355x_pool_window)\n";
+                    if (d_tags.front().offset >= rec.sample_counter) in_call.push_back(d_tags.front());
+                    d_tags.pop_front();
                 }
-            d_state = 0;
-            if (d_events) d_events(3);
+            TrackingTags call_tags;
+            call_tags.in = in_call.data();
+            call_tags.n_in = static_cast<int>(in_call.size());
+            d_output.call_tags(&call_tags, rec.sample_counter, rec.consumed, *noutput ? out : nullptr, d_nitems_written);
+            if (tags && call_tags.has_out)
+                {
+                    tags->has_out = true;
+                    tags->out = call_tags.out;
+                }
+            d_nitems_written += static_cast<uint64_t>(*noutput);
+            if (loss_of_lock)
+                {
+                    if (rec.flags & GSDR_TRK_F_OVERRUN)
+                        {
+                            // not a signal loss: the channel started before the ring's oldest item
+                            ++d_overruns;
+                            std::cerr << "dll_pll_veml_tracking_pool_mi355x: channel " << d_channel << " call at "
+                                      << rec.sample_counter << " fell out of the ring window ("
+                                      << d_pool->window_items() << " items; raise <role>.mi355x_pool_window)\n";
+                        }
+                    d_state = 0;
+                    d_tags.clear();
+                    if (d_events) d_events(3);
+                }
+            if (*noutput) break;
         }
-    return d_last.consumed;
+    return n;
 }

@@ -5,14 +5,18 @@
 //
 // The reference runs one dll_pll_veml_tracking block per channel, each on its own
 // scheduler thread over the shared conditioner output (gnss_flowgraph.cc:1007-1135,
-// dll_pll_veml_tracking.cc:1784-2152).  The per-channel MI355X block keeps that
-// shape and pays one synchronous H2D + launch + D2H + sync per general_work call
-// (SURVEY §7 H6).  Here the blocks keep their GNU Radio contract -- work() gets the
-// stream at nitems_read and returns the items its channel consumed, one Gnss_Synchro
-// per valid call -- while the pool pushes each stretch of the stream once (whichever
-// block sees it first), advances every started channel over the ring in one launch
-// per chunk, and queues each channel's per-call records for its block to hand out
-// in order.
+// dll_pll_veml_tracking.cc:1784-2152), consuming exactly one correlation's items per
+// general_work call.  The per-channel MI355X block keeps that shape and pays one
+// synchronous H2D + launch + D2H + sync per call.  The pooled block
+// decouples consumption from computation: work() pushes the items it is handed into
+// the pool's ring (whichever block sees a stretch first) and consumes them; the
+// pool advances every started channel over the ring in one launch per batch of
+// batch_calls correlation lengths (and whenever window/2 items arrived since the
+// last advance, so no channel falls out of the ring whatever the scheduler's buffer
+// sizes); each block then hands out its channel's per-call records in order, one
+// Gnss_Synchro per work() call that emits (Tracking_sample_counter = the call's
+// nitems_read, as the reference).  The per-call records equal the per-channel
+// block's bit for bit (host self-test); outputs come up to one batch later.
 #ifndef GSDR_HOST_DLL_PLL_VEML_TRACKING_POOL_MI355X_H
 #define GSDR_HOST_DLL_PLL_VEML_TRACKING_POOL_MI355X_H
 
@@ -29,16 +33,17 @@
 #include "gsdr.h"
 #include "tracking_block_mi355x.h"
 #include "tracking_dump.h"
+#include "tracking_output.h"
 
 class SharedTrackingPool
 {
 public:
-    // window_calls: the ring window in vector lengths -- how far (in items) a
-    // channel's next call may start behind the newest pushed item before the
-    // engine reports it as an overrun (loss of lock with GSDR_TRK_F_OVERRUN)
+    // window_calls: the ring window in vector lengths (the ring holds twice that);
+    // batch_calls: vector lengths of new items per advance launch
     SharedTrackingPool(const Dll_Pll_Conf& conf, int32_t signal, uint32_t max_channels, int device,
-        uint32_t window_calls = kDefaultWindowCalls);
-    static constexpr uint32_t kDefaultWindowCalls = 8;
+        uint32_t window_calls = kDefaultWindowCalls, uint32_t batch_calls = kDefaultBatchCalls);
+    static constexpr uint32_t kDefaultWindowCalls = 64;
+    static constexpr uint32_t kDefaultBatchCalls = 8;
     ~SharedTrackingPool();
     SharedTrackingPool(const SharedTrackingPool&) = delete;
     SharedTrackingPool& operator=(const SharedTrackingPool&) = delete;
@@ -46,7 +51,8 @@ public:
     // the pool of (key, device, signal): created by the first block, shared by the
     // rest while any holds it (GNSSBlockFactory builds one block per channel)
     static std::shared_ptr<SharedTrackingPool> get(const std::string& key, const Dll_Pll_Conf& conf, int32_t signal,
-        uint32_t max_channels, int device, uint32_t window_calls = kDefaultWindowCalls);
+        uint32_t max_channels, int device, uint32_t window_calls = kDefaultWindowCalls,
+        uint32_t batch_calls = kDefaultBatchCalls);
 
     int acquire_slot();  // -1 when every slot is taken
     void release_slot(int slot);
@@ -55,10 +61,14 @@ public:
     uint64_t start(int slot, uint32_t prn, const char signal[2], double acq_delay_samples, double acq_doppler_hz,
         uint64_t acq_samplestamp, uint64_t nitems_read);
     void stop(int slot);
+    // a telemetry fault on `slot` (gsdr_trk_force_loss_of_lock)
+    void force_loss_of_lock(int slot);
     // input items [nitems_read, nitems_read + n): the part the ring has not seen is
-    // pushed (chunked), and every started channel advances over the ring after each
-    // chunk (advance = false: push only, for blocks in standby)
-    void feed(const void* in, uint64_t nitems_read, int n, bool advance = true);
+    // pushed, with an advance of every started channel after each window/2 items
+    void feed(const void* in, uint64_t nitems_read, int n);
+    // an advance launch when batch_calls vector lengths arrived since the last one
+    // (force: when anything arrived)
+    void advance_if_due(bool force);
     // the next per-call record of `slot` (in call order), left in the queue by peek
     bool peek(int slot, gsdr_trk_epoch* rec);
     void drop(int slot);
@@ -67,6 +77,7 @@ public:
     uint64_t launches() const { return d_launches; }
     uint64_t pushed() const { return d_head - d_origin; }
     uint64_t window_items() const { return d_window; }
+    uint64_t batch_items() const { return d_batch; }
 
 private:
     void advance_locked();
@@ -77,10 +88,12 @@ private:
     int d_device;
     size_t d_item_bytes{8};
     uint64_t d_window{0};
+    uint64_t d_batch{0};
     gsdr_trk* d_engine{nullptr};
     gsdr_stream* d_ring{nullptr};
     bool d_started{false};
     uint64_t d_origin{0}, d_head{0};
+    uint64_t d_advanced{0};  // the head at the last advance
     uint64_t d_launches{0};
     std::vector<bool> d_used;
     std::vector<bool> d_active;
@@ -94,9 +107,10 @@ class dll_pll_veml_tracking_pool_mi355x : public TrackingBlockMI355X
 {
 public:
     // pool_key: the pool's registry key (the adapters use role + device);
-    // window_calls: <role>.mi355x_pool_window (SharedTrackingPool)
+    // window_calls / batch_calls: <role>.mi355x_pool_window / .mi355x_pool_batch
     dll_pll_veml_tracking_pool_mi355x(const Dll_Pll_Conf& conf, int32_t signal, uint32_t pool_channels, int device,
-        const std::string& pool_key, uint32_t window_calls = SharedTrackingPool::kDefaultWindowCalls);
+        const std::string& pool_key, uint32_t window_calls = SharedTrackingPool::kDefaultWindowCalls,
+        uint32_t batch_calls = SharedTrackingPool::kDefaultBatchCalls);
     ~dll_pll_veml_tracking_pool_mi355x() override;
 
     void set_gnss_synchro(Gnss_Synchro* p_gnss_synchro) override;
@@ -104,13 +118,18 @@ public:
     void start_tracking() override;
     void stop_tracking() override;
     void set_event_handler(std::function<void(int)> h) override { d_events = std::move(h); }
-    int forecast() const override { return 2 * static_cast<int>(d_conf.vector_length); }
-    int work(const void* in, int ninput_items, uint64_t nitems_read, Gnss_Synchro* out, int* noutput) override;
+    void msg_handler_telemetry_to_trk(int tlm_event) override;
+    // any items are useful: work() consumes what it is handed
+    int forecast() const override { return 1; }
+    int work(const void* in, int ninput_items, uint64_t nitems_read, Gnss_Synchro* out, int* noutput,
+        TrackingTags* tags) override;
+    using TrackingBlockMI355X::work;
+    void flush() override;
     int32_t state() const override { return d_state; }
     const gsdr_trk_epoch& last_record() const override { return d_last; }
     SharedTrackingPool* pool() { return d_pool.get(); }
-    // loss-of-lock records the engine marked GSDR_TRK_F_OVERRUN (the channel's next
-    // call started before the oldest item the ring window still held)
+    // loss-of-lock records the engine marked GSDR_TRK_F_OVERRUN (a channel started
+    // before the oldest item the ring still held)
     uint64_t overruns() const { return d_overruns; }
 
 private:
@@ -125,7 +144,10 @@ private:
     std::function<void(int)> d_events;
     std::mutex d_setlock;
     uint64_t d_overruns{0};
-    TrackingDump d_dump;  // <role>.dump: the reference's per-channel .dat (log_data)
+    TrackingDump d_dump;  // <role>.dump: the reference's per-channel .dat (log_data), .mat on destruction
+    TrackingOutput d_output;
+    std::deque<GnssTimeTag> d_tags;  // input time tags not yet matched to a call
+    bool d_fault_pending{false};     // telemetry fault between start_tracking and the pull-in
 };
 
 #endif

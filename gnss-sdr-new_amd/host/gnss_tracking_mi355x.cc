@@ -17,8 +17,9 @@ void DllPllTrackingAdapterMI355X::make_block(const ConfigurationInterface* confi
 {
     item_size_ = trk_params_.item_type == "cshort" ? 4 : (trk_params_.item_type == "cbyte" ? 2 : 8);
     // pooled by default: every channel of the signal on this GPU in one engine
-    // handle over the device ring (5.9 us per general_work call against 64.8 us
-    // for a per-channel block's synchronous H2D + launch + D2H, host self-test)
+    // handle over the device ring, one launch per <role>.mi355x_pool_batch
+    // correlation lengths for all its channels, instead of a per-channel block's
+    // synchronous H2D + launch + D2H per general_work call
     pooled_ = configuration->property(role_ + ".mi355x_pool", true);
     if (!pooled_)
         {
@@ -34,8 +35,11 @@ void DllPllTrackingAdapterMI355X::make_block(const ConfigurationInterface* confi
     const int slots = configuration->property(role_ + ".mi355x_pool_channels", count > 0 ? count : 32);
     const int window = configuration->property(role_ + ".mi355x_pool_window",
         static_cast<int>(SharedTrackingPool::kDefaultWindowCalls));
+    const int batch = configuration->property(role_ + ".mi355x_pool_batch",
+        static_cast<int>(SharedTrackingPool::kDefaultBatchCalls));
     tracking_ = std::make_unique<dll_pll_veml_tracking_pool_mi355x>(trk_params_, signal,
-        static_cast<uint32_t>(slots > 0 ? slots : 32), device, role_, static_cast<uint32_t>(window));
+        static_cast<uint32_t>(slots > 0 ? slots : 32), device, role_, static_cast<uint32_t>(window),
+        static_cast<uint32_t>(batch));
 }
 
 // gps_l1_ca_dll_pll_tracking.cc:34-91

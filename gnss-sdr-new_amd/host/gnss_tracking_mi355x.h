@@ -10,7 +10,8 @@
 // channel), or with <role>.mi355x_pool=true a dll_pll_veml_tracking_pool_mi355x
 // slot in the GPU's shared pool of that role (every channel of the signal on the
 // GPU in one engine handle over the device IQ ring; <role>.mi355x_pool_channels
-// slots, default Channels_<signal>.count).
+// slots, default Channels_<signal>.count; <role>.mi355x_pool_window /
+// .mi355x_pool_batch the ring window and the launch batch in vector lengths).
 #ifndef GSDR_HOST_GNSS_TRACKING_MI355X_H
 #define GSDR_HOST_GNSS_TRACKING_MI355X_H
 

@@ -5,7 +5,7 @@
 namespace
 {
 // data types of the sub-elements (MAT-File Format, Table 1-1)
-constexpr uint32_t miINT8 = 1, miINT32 = 5, miUINT32 = 6, miSINGLE = 7, miUINT64 = 13, miMATRIX = 14;
+constexpr uint32_t miINT8 = 1, miINT32 = 5, miUINT32 = 6, miSINGLE = 7, miDOUBLE = 9, miUINT64 = 13, miMATRIX = 14;
 
 uint32_t pad8(uint32_t n) { return (n + 7u) & ~7u; }
 
@@ -16,11 +16,12 @@ uint32_t elem_type(Mat5Writer::Class c)
         case Mat5Writer::kSingle: return miSINGLE;
         case Mat5Writer::kInt32: return miINT32;
         case Mat5Writer::kUint32: return miUINT32;
+        case Mat5Writer::kDouble: return miDOUBLE;
         default: return miUINT64;
         }
 }
 
-uint32_t elem_bytes(Mat5Writer::Class c) { return c == Mat5Writer::kUint64 ? 8u : 4u; }
+uint32_t elem_bytes(Mat5Writer::Class c) { return c == Mat5Writer::kUint64 || c == Mat5Writer::kDouble ? 8u : 4u; }
 }  // namespace
 
 bool Mat5Writer::open(const std::string& path)
@@ -32,7 +33,7 @@ bool Mat5Writer::open(const std::string& path)
     // 116 bytes of text, 8 bytes of subsystem offset, version 0x0100, endian "IM"
     char hdr[128];
     std::memset(hdr, ' ', sizeof hdr);
-    const char* text = "MATLAB 5.0 MAT-file, written by gnss-sdr-new_amd (pcps_acquisition dump_results layout)";
+    const char* text = "MATLAB 5.0 MAT-file, written by gnss-sdr-new_amd (GNSS-SDR dump layout)";
     std::memcpy(hdr, text, std::strlen(text));
     std::memset(hdr + 116, 0, 8);
     const uint16_t version = 0x0100;

@@ -1,5 +1,6 @@
 // Minimal Level-5 MAT-file writer for the acquisition dump (dump_results,
-// pcps_acquisition.cc:408-508).  The reference writes its .mat files through
+// pcps_acquisition.cc:408-508) and the tracking dump's conversion (save_matfile,
+// dll_pll_veml_tracking.cc:1511-1729).  The reference writes its .mat files through
 // matio (MAT_FT_MAT73, zlib-compressed); matio is not on this image, so the dump
 // is written as an uncompressed Level-5 MAT-file with the same variable names,
 // classes and dimensions -- MATLAB, Octave and scipy.io.loadmat read both the
@@ -19,6 +20,7 @@ class Mat5Writer
 public:
     enum Class : uint8_t
     {
+        kDouble = 6,  // mxDOUBLE_CLASS
         kSingle = 7,  // mxSINGLE_CLASS
         kInt32 = 12,  // mxINT32_CLASS
         kUint32 = 13, // mxUINT32_CLASS

@@ -96,8 +96,8 @@ void pcps_acquisition_mi355x::ensure_engine()
         }
     d_engine_dmax = dmax;
     d_engine_step = d_doppler_step;
-    if (d_acq_parameters.wipeoff_mode() != GSDR_WIPE_EXACT &&
-        gsdr_acq_set_wipeoff(d_engine, d_acq_parameters.wipeoff_mode()) != GSDR_OK)
+    // the configuration's carrier model, whatever GSDR_ACQ_WIPE says
+    if (gsdr_acq_set_wipeoff(d_engine, d_acq_parameters.wipeoff_mode()) != GSDR_OK)
         throw std::runtime_error(std::string("pcps_acquisition_mi355x: ") + gsdr_last_error());
     // make_two_steps narrow grid (Acq_Conf second_nbins / second_doppler_step / pfa2)
     if (d_acq_parameters.make_2_steps &&

@@ -57,7 +57,9 @@ int main(int argc, char** argv)
     const std::string cfg = argc > 1 ? argv[1] : "c3";
     const bool c5 = cfg == "c5";
     const double fs = c5 ? 25.0e6 : 16.0e6;
-    const double seconds = argc > 2 ? std::atof(argv[2]) : 0.4;
+    // >= 1.5 s: the pull-in transitory ends after 1 s (integer seconds,
+    // dll_pll_veml_tracking.cc:1797), then bit / secondary-code sync and outputs
+    const double seconds = argc > 2 ? std::atof(argv[2]) : 1.6;
     const bool search = argc > 3 ? std::atoi(argv[3]) != 0 : true;
     std::vector<Sig> sigs = {{"1C", "GPS_L1_CA_DLL_PLL_Tracking_MI355X", "GPS_L1_CA_PCPS_Acquisition_MI355X", 'G', '1',
         'C', 12, 32, 1.023e6, 1575.42e6, 1}};
@@ -140,6 +142,7 @@ int main(int argc, char** argv)
         double truth_dop;
         int outputs;
         double dop;
+        uint64_t calls;  // correlation calls run (records handed out)
     };
     std::vector<Ch> chans;
     chans.reserve(64);
@@ -171,7 +174,16 @@ int main(int argc, char** argv)
                 ch.truth_dop = truth[g][c].doppler;
                 ch.outputs = 0;
                 ch.dop = 0.0;
+                ch.calls = 0;
             }
+    for (auto& ch : chans)
+        {
+            Ch* p = &ch;
+            ch.blk->set_record_sink([p](const gsdr_trk_epoch& r) {
+                p->dop = r.carrier_doppler_hz;
+                ++p->calls;
+            });
+        }
     // acquisition services on the device ring: every untracked PRN of each signal,
     // re-armed after each answer
     gsdr_stream* ring = nullptr;
@@ -264,36 +276,60 @@ int main(int argc, char** argv)
                         Gnss_Synchro out{};
                         int nout = 0;
                         const int used = ch.blk->work(x.data() + ch.nread, give, ch.nread, &out, &nout);
-                        if (used <= 0) break;
-                        progress = true;
-                        ch.nread += static_cast<uint64_t>(used);
-                        ++trk_calls;
                         if (nout == 1 && out.Flag_valid_symbol_output) ++ch.outputs;
-                        if (ch.blk->state() >= 2) ch.dop = ch.blk->last_record().carrier_doppler_hz;
+                        if (used <= 0 && nout == 0) break;
+                        progress = true;
+                        ch.nread += static_cast<uint64_t>(std::max(used, 0));
+                        ++trk_calls;
                     }
         }
+    // end of the stream: the blocks compute what they were handed and hand out the rest
+    for (auto& ch : chans)
+        {
+            ch.blk->flush();
+            for (int guard = 0; guard < 1000000; ++guard)
+                {
+                    Gnss_Synchro out{};
+                    int nout = 0;
+                    ch.blk->work(nullptr, 0, ch.nread, &out, &nout);
+                    if (nout == 0) break;
+                    if (out.Flag_valid_symbol_output) ++ch.outputs;
+                }
+        }
+    for (auto& s : svcs)
+        if (s) s->flush();
     const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     std::string per_sig;
     for (size_t g = 0; g < sigs.size(); ++g)
         {
-            int outs = 0, within = 0;
+            int outs = 0, within = 0, with_outputs = 0, min_out = -1;
+            uint64_t calls = 0;
             for (const auto& ch : chans)
                 if (ch.sig == g)
                     {
                         outs += ch.outputs;
+                        with_outputs += ch.outputs > 0 ? 1 : 0;
+                        min_out = min_out < 0 ? ch.outputs : std::min(min_out, ch.outputs);
                         within += std::abs(ch.dop - ch.truth_dop) < 25.0 ? 1 : 0;
+                        calls += ch.calls;
                     }
-            char buf[256];
+            char buf[512];
             std::snprintf(buf, sizeof buf,
-                "%s\"%c%c%c\": {\"channels\": %d, \"outputs\": %d, \"channels_within_25hz\": %d, \"acq_answers\": %llu, "
-                "\"acq_positive\": %llu, \"acq_grids\": %llu}",
-                g ? ", " : "", sigs[g].sys, sigs[g].s0, sigs[g].s1, sigs[g].nch, outs, within,
-                static_cast<unsigned long long>(answers[g]), static_cast<unsigned long long>(positives[g]),
-                static_cast<unsigned long long>(svcs[g] ? svcs[g]->grids_run() : 0));
+                "%s\"%c%c%c\": {\"channels\": %d, \"outputs\": %d, \"channels_with_outputs\": %d, "
+                "\"min_outputs_per_channel\": %d, \"channels_within_25hz\": %d, \"trk_calls\": %llu, "
+                "\"acq_answers\": %llu, \"acq_positive\": %llu, \"acq_grids\": %llu, \"acq_launches\": %llu, "
+                "\"acq_code_uploads\": %llu}",
+                g ? ", " : "", sigs[g].sys, sigs[g].s0, sigs[g].s1, sigs[g].nch, outs, with_outputs, min_out, within,
+                static_cast<unsigned long long>(calls), static_cast<unsigned long long>(answers[g]),
+                static_cast<unsigned long long>(positives[g]),
+                static_cast<unsigned long long>(svcs[g] ? svcs[g]->grids_run() : 0),
+                static_cast<unsigned long long>(svcs[g] ? svcs[g]->launches() : 0),
+                static_cast<unsigned long long>(svcs[g] ? svcs[g]->code_uploads() : 0));
             per_sig += buf;
         }
     std::printf("{\"config\": \"%s\", \"search\": %d, \"path\": \"factory-built pooled TrackingInterface blocks (work() per block at its "
-                "nitems_read) + AcquisitionService grids on the device IQ ring, host pushes of %zu-item chunks\", "
+                "nitems_read, batched advances) + AcquisitionService grids on the device IQ ring (batched, asynchronous), host "
+                "pushes of %zu-item chunks\", "
                 "\"fs_sps\": %.0f, \"samples\": %zu, \"seconds\": %.4f, \"msps\": %.2f, \"real_time_factor\": %.2f, "
                 "\"tracking_channels\": %zu, \"trk_work_calls\": %llu, \"signals\": {%s}}\n",
         cfg.c_str(), search ? 1 : 0, chunk, fs, n, sec, n / sec / 1e6, n / sec / fs, chans.size(),

@@ -1,10 +1,13 @@
 #include "tracking_dump.h"
 
+#include "mat5_writer.h"
+
 #include <cmath>
 #include <cstring>
 #include <filesystem>
 #include <iostream>
 #include <system_error>
+#include <vector>
 
 namespace
 {
@@ -48,6 +51,7 @@ bool TrackingDump::configure(const std::string& dump_filename)
 bool TrackingDump::open(uint32_t channel)
 {
     // set_channel (:1733-1760): the file of the first channel the block is given
+    channel_ = channel;
     if (stem_.empty() || file_.is_open()) return file_.is_open();
     path_ = stem_ + std::to_string(channel) + ".dat";
     file_.open(path_, std::ios::out | std::ios::binary);
@@ -125,4 +129,64 @@ void TrackingDump::write(const gsdr_trk_epoch& r, double fs_in, bool veml, bool 
     encode(r, fs_in, veml, track_pilot, prn_, acq_code_phase_, acq_doppler_, buf);
     file_.write(buf, kRecordBytes);
     if (!file_) std::cerr << "Exception writing trk dump file " << path_ << '\n';
+}
+
+bool TrackingDump::save_matfile()
+{
+    if (stem_.empty()) return false;
+    if (file_.is_open()) file_.close();
+    // :1511-1600: read every 108-byte epoch of <stem><channel>.dat
+    const std::string dat = stem_ + std::to_string(channel_) + ".dat";
+    std::ifstream in(dat, std::ios::binary | std::ios::ate);
+    if (!in.is_open())
+        {
+            std::cerr << "Problem opening dump file:" << dat << '\n';
+            return false;
+        }
+    const auto size = static_cast<int64_t>(in.tellg());
+    const size_t n = static_cast<size_t>(size / static_cast<int64_t>(kRecordBytes));
+    in.seekg(0, std::ios::beg);
+    std::vector<char> raw(n * kRecordBytes);
+    if (n && !in.read(raw.data(), static_cast<std::streamsize>(raw.size())))
+        {
+            std::cerr << "Problem reading dump file:" << dat << '\n';
+            return false;
+        }
+    // the record's fields in file order: 7 floats, the uint64 sample count, 12 floats,
+    // the double aux2, the uint32 PRN, 3 floats (log_data, :1403-1500)
+    static const char* const kF1[7] = {"abs_VE", "abs_E", "abs_P", "abs_L", "abs_VL", "Prompt_I", "Prompt_Q"};
+    static const char* const kF2[12] = {"acc_carrier_phase_rad", "carrier_doppler_hz", "carrier_doppler_rate_hz",
+        "code_freq_chips", "code_freq_rate_chips", "carr_error_hz", "carr_error_filt_hz", "code_error_chips",
+        "code_error_filt_chips", "CN0_SNV_dB_Hz", "carrier_lock_test", "aux1"};
+    static const char* const kF3[3] = {"acq_code_phase_samples", "acq_carrier_doppler_hz", "EVM"};
+    std::vector<std::vector<float>> f1(7, std::vector<float>(n)), f2(12, std::vector<float>(n)),
+        f3(3, std::vector<float>(n));
+    std::vector<uint64_t> start(n);
+    std::vector<double> aux2(n);
+    std::vector<uint32_t> prn(n);
+    for (size_t i = 0; i < n; ++i)
+        {
+            const char* p = raw.data() + i * kRecordBytes;
+            for (int k = 0; k < 7; ++k, p += 4) std::memcpy(&f1[k][i], p, 4);
+            std::memcpy(&start[i], p, 8);
+            p += 8;
+            for (int k = 0; k < 12; ++k, p += 4) std::memcpy(&f2[k][i], p, 4);
+            std::memcpy(&aux2[i], p, 8);
+            p += 8;
+            std::memcpy(&prn[i], p, 4);
+            p += 4;
+            for (int k = 0; k < 3; ++k, p += 4) std::memcpy(&f3[k][i], p, 4);
+        }
+    // :1602-1726: <stem><channel>.mat, every variable 1 x num_epoch, in this order
+    const std::string mat = stem_ + std::to_string(channel_) + ".mat";
+    Mat5Writer w;
+    if (!w.open(mat)) return false;
+    const auto cols = static_cast<uint32_t>(n);
+    for (int k = 0; k < 7; ++k) w.write(kF1[k], Mat5Writer::kSingle, 1, cols, f1[k].data());
+    w.write("PRN_start_sample_count", Mat5Writer::kUint64, 1, cols, start.data());
+    for (int k = 0; k < 12; ++k) w.write(kF2[k], Mat5Writer::kSingle, 1, cols, f2[k].data());
+    w.write("aux2", Mat5Writer::kDouble, 1, cols, aux2.data());
+    w.write("PRN", Mat5Writer::kUint32, 1, cols, prn.data());
+    for (int k = 0; k < 3; ++k) w.write(kF3[k], Mat5Writer::kSingle, 1, cols, f3[k].data());
+    return w.close();
 }

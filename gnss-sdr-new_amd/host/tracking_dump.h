@@ -3,8 +3,10 @@
 // the engine's gsdr_trk_epoch records: the engine flags the calls at which the
 // reference calls log_data() (GSDR_TRK_F_LOGGED) and carries the accumulator
 // magnitudes and loop errors of that point, so the file holds the same 108-byte
-// records in the same order.  The .mat conversion (save_matfile, dump_mat) needs
-// matio and is not reproduced; the .dat layout is what it reads.
+// records in the same order.  save_matfile (:1511-1729, run by the destructor when
+// dump_mat, :884-906) converts the channel's .dat into <stem><channel>.mat with the
+// reference's 25 variable names, classes and 1 x epochs dimensions, as a Level-5
+// MAT-file (Mat5Writer; the reference's matio writes MAT 7.3, which needs HDF5).
 #ifndef GSDR_HOST_TRACKING_DUMP_H
 #define GSDR_HOST_TRACKING_DUMP_H
 
@@ -35,6 +37,9 @@ public:
     // the record bytes alone (no file): out must hold kRecordBytes
     static void encode(const gsdr_trk_epoch& r, double fs_in, bool veml, bool track_pilot, uint32_t prn,
         double acq_code_phase_samples, double acq_carrier_doppler_hz, char* out);
+    // close the .dat and convert <stem><channel>.dat of the last set_channel into
+    // <stem><channel>.mat (save_matfile); false when the .dat cannot be read
+    bool save_matfile();
     bool is_open() const { return file_.is_open(); }
     const std::string& stem() const { return stem_; }
     const std::string& path() const { return path_; }
@@ -43,6 +48,7 @@ private:
     std::string stem_;
     std::string path_;
     std::ofstream file_;
+    uint32_t channel_{0};  // d_channel: save_matfile reads the file of the last set_channel
     uint32_t prn_{0};
     double acq_code_phase_{0.0};
     double acq_doppler_{0.0};

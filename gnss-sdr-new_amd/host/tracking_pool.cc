@@ -11,6 +11,7 @@ TrackingPool::TrackingPool(const Dll_Pll_Conf& conf, int32_t signal, uint32_t ma
     const gsdr_trk_conf c = d_conf.to_engine(signal, max_channels);
     if (gsdr_trk_create(device, &c, &d_engine) != GSDR_OK)
         throw std::runtime_error(std::string("TrackingPool: ") + gsdr_last_error());
+    d_output = TrackingOutput(d_conf.fs_in, signal);
     d_synchro.assign(max_channels, nullptr);
     d_n.assign(max_channels, 0);
 }
@@ -66,20 +67,8 @@ uint64_t TrackingPool::advance(const Output& out, uint32_t max_epochs)
                     for (uint32_t e = 0; e < d_n[c]; ++e)
                         {
                             const gsdr_trk_epoch& r = d_recs[static_cast<size_t>(c) * max_epochs + e];
-                            const bool lol = (r.flags & GSDR_TRK_F_LOSS_OF_LOCK) != 0;
-                            if (!d_synchro[c] || !((r.flags & GSDR_TRK_F_VALID_OUTPUT) || lol)) continue;
-                            Gnss_Synchro s = *d_synchro[c];
-                            s.Prompt_I = r.prompt_i;
-                            s.Prompt_Q = r.prompt_q;
-                            s.Code_phase_samples = r.rem_code_phase_samples;
-                            s.Carrier_phase_rads = r.acc_carrier_phase_rad;
-                            s.Carrier_Doppler_hz = r.carrier_doppler_hz;
-                            s.CN0_dB_hz = r.cn0_db_hz;
-                            s.EVM = r.evm;
-                            s.fs = static_cast<int64_t>(d_conf.fs_in);
-                            s.Tracking_sample_counter = r.sample_counter;
-                            s.Flag_valid_symbol_output = !lol;
-                            s.Flag_PLL_180_deg_phase_locked = (r.flags & GSDR_TRK_F_PLL_180) != 0;
+                            Gnss_Synchro s;
+                            if (!d_synchro[c] || !d_output.emit(r, *d_synchro[c], r.sample_counter, &s)) continue;
                             out(c, s);
                         }
                 }

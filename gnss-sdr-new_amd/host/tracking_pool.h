@@ -17,6 +17,7 @@
 #include "dll_pll_conf.h"
 #include "gnss_synchro.h"
 #include "gsdr.h"
+#include "tracking_output.h"
 
 class TrackingPool
 {
@@ -46,6 +47,7 @@ private:
     std::vector<Gnss_Synchro*> d_synchro;
     std::vector<gsdr_trk_epoch> d_recs;
     std::vector<uint32_t> d_n;
+    TrackingOutput d_output;
 };
 
 #endif

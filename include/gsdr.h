@@ -176,6 +176,15 @@ int gsdr_acq_get_dims(const gsdr_acq* acq, uint32_t* num_doppler_bins, uint32_t*
  * the FFT buffer, transforms and conjugates on the device.  prn[] are the PRN ids
  * reported back in gsdr_acq_result. */
 int gsdr_acq_set_local_codes(gsdr_acq* acq, const float* codes, const uint32_t* prn, uint32_t nprn);
+/* set_local_code of one PRN slot (pcps_acquisition.cc:176-209, called once per PRN
+ * assignment by the channel, gps_l1_ca_pcps_acquisition.cc:151-170): code is
+ * consumed_samples complex<float> (host), transformed into slot `slot` of the
+ * handle's code spectra; the other slots keep theirs.  Extends the active PRN
+ * count to slot + 1 if needed.  Ordered after the launches already issued. */
+int gsdr_acq_set_local_code(gsdr_acq* acq, uint32_t slot, const float* code, uint32_t prn);
+/* Number of PRN slots [0, nprn) the grid launches search (each with a spectrum set
+ * by gsdr_acq_set_local_code[s]). */
+int gsdr_acq_set_active_prns(gsdr_acq* acq, uint32_t nprn);
 
 /* Doppler setters (AcquisitionInterface, acquisition_interface.h:56-59).  They
  * rebuild the Doppler wipe-off grid on the device. */
@@ -242,6 +251,15 @@ int gsdr_acq_run_device(gsdr_acq* acq, const void* iq_dev, uint32_t nblocks, uin
  * later pushes overwrite the window.  Synchronous (results on the host). */
 int gsdr_acq_run_stream(gsdr_acq* acq, gsdr_stream* stream, uint64_t first_sample, uint32_t nblocks, uint64_t stamp0,
     gsdr_acq_result* out_host);
+/* Asynchronous ring form (the batched acquisition service's call, gnss_flowgraph.cc:
+ * 1796-1901 answered per block): the grids of nblocks attempts from first_sample are
+ * launched on the handle's stream with the results copied into the handle's pinned
+ * buffer; returns without waiting.  gsdr_acq_collect waits for them and copies the
+ * nblocks * nprn results (block-major, nprn = the active count at submission) to
+ * out_host.  One submission in flight per handle. */
+int gsdr_acq_submit_stream(gsdr_acq* acq, gsdr_stream* stream, uint64_t first_sample, uint32_t nblocks,
+    uint64_t stamp0);
+int gsdr_acq_collect(gsdr_acq* acq, gsdr_acq_result* out_host, uint32_t* nblocks, uint32_t* nprn);
 
 /* The reference's acquisition grid dump (pcps_acquisition.cc:408-508): writes the
  * |R|^2 grid of PRN slot `prn_slot` for one host block into grid_host
@@ -502,6 +520,12 @@ int gsdr_trk_start(gsdr_trk* trk, int ch, uint32_t prn, const float* code, int c
 int gsdr_trk_set_data_code(gsdr_trk* trk, int ch, const float* data_code, int code_samples);
 /* stop_tracking: channel to state 0 (standby). */
 int gsdr_trk_stop(gsdr_trk* trk, int ch);
+/* msg_handler_telemetry_to_trk with tlm_event 1 (dll_pll_veml_tracking.cc:614-637,
+ * port registered :142-147): a telemetry fault forces d_carrier_lock_fail_counter to
+ * 200000, so the channel's next lock check past the CN0 fill (states 2 / 4) reports
+ * the loss of lock (GSDR_TRK_F_LOSS_OF_LOCK).  Takes effect at the channel's next
+ * call on the device (synchronous; ordered after the handle's last launch). */
+int gsdr_trk_force_loss_of_lock(gsdr_trk* trk, int ch);
 
 /* Advance every channel in states 2..4 by up to max_epochs general_work calls
  * over iq_dev, which holds iq_items items whose first item is absolute input

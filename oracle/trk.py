@@ -58,6 +58,7 @@ def _lib():
         L.orc_trk_call.restype = _i
         L.orc_trk_call_taps.argtypes = [_p, _p, _u64, _p]
         L.orc_trk_call_taps.restype = _i
+        L.orc_trk_force_loss_of_lock.argtypes = [_p]
         L.orc_trk_state.argtypes = [_p]
         L.orc_trk_state.restype = ctypes.c_int32
         L.orc_trk_vector_length.argtypes = [_p]
@@ -143,12 +144,20 @@ class Channel:
             k += 1
         return recs[:k], n
 
-    def replay(self, records):
+    def force_loss_of_lock(self):
+        """msg_handler_telemetry_to_trk with a telemetry fault (:614-637)."""
+        _lib().orc_trk_force_loss_of_lock(self._h)
+
+    def replay(self, records, force_before=()):
         """Feed the correlator outputs of another implementation's records through
         this channel's loop (orc_trk_call_taps), call by call at the same input
-        positions; returns this channel's own records."""
+        positions; returns this channel's own records.  force_before: record
+        indices before which a telemetry fault arrives (force_loss_of_lock)."""
         out = np.zeros(len(records), TRK_EPOCH_DTYPE)
+        force = set(int(i) for i in force_before)
         for k, rec in enumerate(records):
+            if k in force:
+                self.force_loss_of_lock()
             taps = np.concatenate([rec["taps"], rec["data_prompt"]]).astype(np.float32)
             if not _lib().orc_trk_call_taps(self._h, taps.ctypes.data, int(rec["sample_counter"]), out[k:k + 1].ctypes.data):
                 return out[:k]

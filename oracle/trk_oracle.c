@@ -770,6 +770,9 @@ int orc_trk_start(orc_trk* t, uint32_t prn, const float* code, int code_samples,
 
 void orc_trk_stop(orc_trk* t) { t->state = 0; }
 
+/* msg_handler_telemetry_to_trk, tlm_event 1 (:614-637) */
+void orc_trk_force_loss_of_lock(orc_trk* t) { t->carrier_lock_fail_counter = 200000; }
+
 /* do_correlation_step (:1064-1089) */
 static void do_correlation_step(orc_trk* t, const float* in)
 {

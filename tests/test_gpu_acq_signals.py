@@ -84,45 +84,35 @@ def test_beidou_b1i_synthetic_batch(fs):
 
 # acq_split.hip split ids and their FFT sizes (5/6: 16000-based splits; 11-20: the
 # wave-local-row plans)
-SPLIT_IDS = {5: 32000, 6: 64000, 11: 25000, 12: 32000, 13: 64000, 14: 100000, 15: 32000, 16: 64000, 17: 25000, 21: 100000,
+SPLIT_IDS = {5: 32000, 6: 64000, 11: 25000, 12: 32000, 13: 64000, 14: 100000, 15: 32000, 16: 64000, 17: 25000,
              18: 100000, 19: 32000, 20: 64000}
 
 
-# plans with two columns per lane and NT > L / 2: the mirror-pair (Hermitian code)
-# correlate applies (acq_split.hip herm_ok), forced by GSDR_ACQ_HERM
-HERM_IDS = (11, 14, 15, 16)
+LARGE_CONFIGS = [(8000000, 32000, 0.01), (25000000, 25000, 0.0), (8000000, 64000, 0.01), (25000000, 100000, 0.01),
+                 (25000000, 25000, 0.01), (25000000, 100000, 0.0)]
 
 
-@pytest.mark.parametrize("split", ["1", "0", "2", "h1", "h2", "pre1", "pre64"] + ["id%d" % i for i in sorted(SPLIT_IDS)]
-                         + ["id%dh" % i for i in HERM_IDS])
-@pytest.mark.parametrize("fs,N,pfa", [(8000000, 32000, 0.01), (25000000, 25000, 0.0), (8000000, 64000, 0.01),
-                                      (25000000, 100000, 0.01), (25000000, 25000, 0.01), (25000000, 100000, 0.0)])
+def _split_cases():
+    """Every configuration on the three modes, and on each forced split id of its N
+    (no cross-product cases that would only skip)."""
+    cases = []
+    for fs, n, pfa in LARGE_CONFIGS:
+        for split in ["1", "0", "2"] + ["id%d" % i for i, m in sorted(SPLIT_IDS.items()) if m == n]:
+            cases.append((fs, n, pfa, split))
+    return cases
+
+
+@pytest.mark.parametrize("fs,N,pfa,split", _split_cases())
 def test_large_fft_four_step(monkeypatch, fs, N, pfa, split):
     """N beyond one workgroup's LDS: Galileo E1 at 8 Msps (4 ms: 32000; 8 ms:
     64000), BeiDou B1I at 25 Msps (1 ms: 25000), Galileo at 25 Msps (100000) --
     configs C4/C5 -- on every correlate path: GSDR_ACQ_SPLIT=1 (default: the split
     register four-step for 25000 / 32000 / 64000 / 100000 = 4 x 25000), 0 (the packed
     four-step everywhere), 2 (also the wave-local 100000 plans when forced),
-    idK: split id K forced (SPLIT_IDS: the 16000-based splits and the wave-local-row plans);
-    preC: the split plan's outer DIF step as its own pass, C PRNs per chunk (GSDR_ACQ_PRE);
-    h1 / h2 / idKh: the mirror-pair code loads (GSDR_ACQ_HERM=1: the grid pass, 2: also
-    the ARG pass) on the default plans / split id K.
+    idK: split id K forced (SPLIT_IDS: the 16000-based splits and the wave-local-row plans).
     Parity with the oracle grid statistics."""
-    if split.startswith("pre"):
-        # the outer DIF step as its own pass (GSDR_ACQ_PRE: PRNs per chunk, two
-        # buffers, the next chunk's pass overlapping this one's grid; plans with ROUT > 1)
-        monkeypatch.setenv("GSDR_ACQ_PRE", split[3:])
-        split = "1"
-    elif split.startswith("h"):
-        monkeypatch.setenv("GSDR_ACQ_HERM", split[1:])
-        split = "1"
-    elif split.endswith("h"):
-        monkeypatch.setenv("GSDR_ACQ_HERM", "2")
-        split = split[:-1]
     if split.startswith("id"):
         # a forced split of this N (acq_split.hip: 5 = 2 x 16000, 6 = 4 x 16000)
-        if SPLIT_IDS[int(split[2:])] != N:
-            pytest.skip("split id for another FFT size")
         monkeypatch.setenv("GSDR_ACQ_SPLIT_ID", split[2:])
         split = "2"
     monkeypatch.setenv("GSDR_ACQ_SPLIT", split)

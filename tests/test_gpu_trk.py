@@ -191,6 +191,39 @@ def test_channel_pool_across_launches(item):
         _free_check(g, orc, "ch%d" % c)
 
 
+@pytest.mark.parametrize("at", [300, 2000])
+def test_telemetry_fault_forces_loss_of_lock(at):
+    """msg_handler_telemetry_to_trk (dll_pll_veml_tracking.cc:614-637): a telemetry
+    fault between two calls sets the carrier lock fail counter to 200000, so the next
+    call's lock check (state 2 in the pull-in transitory at call 300, state 4 after
+    bit sync at call 2000) reports the loss of lock: the GPU's records, replayed
+    through the oracle with the fault before the same call, agree flag for flag."""
+    fs = 2.0e6
+    sat = synth.Satellite(7, 1234.5, 300.3, 45.0, 0.7, preamble_every_bits=25, code_doppler=True)
+    iq = synth.gps_l1_iq(fs, int(2.4 * fs), [sat], seed_offset=5)
+    delay, dop = _acq(sat, fs)
+    code = synth.gps_ca_chips(7)
+    t = gsdr.Tracking(_conf(fs))
+    t.start(0, 7, code, delay, dop, 0, 2000)
+    a, na = t.run(iq, 0, at)
+    assert na[0] == at
+    t.force_loss_of_lock(0)
+    b, nb = t.run(iq, 0, 3000)
+    g = np.concatenate([a[0][:na[0]], b[0][:nb[0]]])
+    # the fault's call is the last one: loss of lock, channel back to standby
+    assert len(g) == at + 1, len(g)
+    assert g["flags"][at] & gsdr.TRK_F_LOSS_OF_LOCK and not np.any(g["flags"][:at] & gsdr.TRK_F_LOSS_OF_LOCK)
+    assert g["state"][at] == (2 if at < 1000 else 4)
+    assert t.channel(0)["state"] == 0
+    o = _oracle_channel(fs, code, delay, dop, 2000)[0].replay(g, force_before=[at])
+    for f in ("sample_counter", "consumed", "state", "flags"):
+        np.testing.assert_array_equal(g[f], o[f], err_msg=f)
+    np.testing.assert_array_equal(g["prompt_i"], o["prompt_i"])
+    # without the fault the oracle keeps the lock through the same calls
+    o2 = _oracle_channel(fs, code, delay, dop, 2000)[0].replay(g)
+    assert not np.any(o2["flags"] & gsdr.TRK_F_LOSS_OF_LOCK)
+
+
 def test_save_restore_replays_identically():
     fs = 2.0e6
     sat = synth.Satellite(12, -2200.0, 77.7, 47.0, 1.1, code_doppler=True)

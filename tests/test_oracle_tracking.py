@@ -96,6 +96,30 @@ def test_channel_loses_lock_on_noise():
     assert ch.state == 0
 
 
+@pytest.mark.parametrize("at,cn0_fill", [(10, False), (300, True), (1300, True)])
+def test_telemetry_fault_forces_loss_of_lock(at, cn0_fill):
+    """msg_handler_telemetry_to_trk (dll_pll_veml_tracking.cc:614-637): the counter
+    forced to 200000 fails the next lock check that evaluates the counters -- not
+    before the CN0 buffer is full (:972-977, call 10 here waits for call 20) -- and
+    the counters reset with the loss (:1022-1023).  The pull-in transitory ends at
+    1 s (pull_in_time_s 0, integer seconds, :1797) and resets the counter too, so a
+    fault in the transitory still fires at the next check inside it."""
+    fs = 2.0e6
+    sat = synth.Satellite(7, 1234.5, 300.3, 45.0, 0.7, preamble_every_bits=50, code_doppler=True)
+    iq = synth.gps_l1_iq(fs, int(1.5 * fs), [sat], seed_offset=5)
+    ch = trk.Channel(_conf(fs))
+    tau = sat.code_delay_chips / (1.023e6 * (1 + sat.doppler_hz / 1.57542e9)) * fs
+    first = ch.start(synth.gps_ca_chips(7), float(round(tau)), 1250.0, 0, 2000)
+    a, n = ch.run(iq, 0, first, at)
+    assert len(a) == at and not np.any(a["flags"] & trk.F_LOSS_OF_LOCK)
+    ch.force_loss_of_lock()
+    b, _ = ch.run(iq, 0, n, 4000)
+    k = np.nonzero(b["flags"] & trk.F_LOSS_OF_LOCK)[0]
+    assert len(k) == 1 and k[0] == len(b) - 1 and ch.state == 0
+    # cn0_samples = 20: the first check that evaluates the counters is call 20
+    assert at + k[0] == (at if cn0_fill else 20)
+
+
 def _conf_sig(fs, sig, pilot=1):
     c = trk.conf_default()
     c["fs_in"] = fs

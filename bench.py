@@ -461,16 +461,21 @@ def run_c5(args):
         for pl in pools:
             pl["t"].run_device(tbase, 0, t_items, nsteps * pl["per_step"], pl["out"].data_ptr(), pl["cnt"].data_ptr())
 
-    def acq_step():
+    step_no = [0]
+
+    def acq_step(span=0):
+        # stream mode: step k acquires span k of the continuous stream (new HBM
+        # addresses every step, as the C2 line; not the same span re-read from L2)
         for name, a, b0, nb, stride, res, P5, N5 in acqs:
-            a.run_device(base + b0 * n * 8, nb, stride, b0 * n, res.data_ptr())
+            a.run_device(tbase + (span * ns + b0 * n) * 8, nb, stride, span * ns + b0 * n, res.data_ptr())
 
     def step():
         if not stream:
             for pl in pools:
                 pl["t"].restore_state(0)
                 pl["t"].run_device(base, 0, ns, pl["epochs"], pl["out"].data_ptr(), pl["cnt"].data_ptr())
-        acq_step()
+        acq_step(step_no[0] % (W + K + 1) if stream else 0)
+        step_no[0] += 1
 
     if stream:
         trk_launch(W)
@@ -525,7 +530,7 @@ def run_c5(args):
     # components after the timed region: acquisition alone over K steps, each pool alone
     # over K spans (from its saved start state), the H2D ingest of the rank's span
     comp = {}
-    ta = timed_part(lambda: [acq_step() for _ in range(K)])
+    ta = timed_part(lambda: [acq_step(k % (W + K + 1) if stream else 0) for k in range(K)])
     comp["acq_only_msps"] = round(B * n * K / ta / 1e6, 2)
     trk_bytes, trk_time = 0.0, 0.0
     for pl in pools:
@@ -597,7 +602,11 @@ def run_c5(args):
                        "gbps": round(ns * 8 / th / 1e9, 2), "frac_of_step": round(th / (elapsed / K), 4),
                        "note": "pinned host -> HBM copy of the rank's stream span per step (every rank ingests the "
                                "whole stream); not part of value"},
-        "check": {"acquired_block0": det, "trk_calls_min_per_pool": calls, "tracking_convergence": conv},
+        "check": {"acquired_block0": det, "trk_calls_min_per_pool": calls, "tracking_convergence": conv,
+                  "notes": ("stream mode: each step acquires its own span of the continuous stream; BeiDou Dopplers "
+                            "drawn within +-1 kHz (the repeated span carries no code Doppler), so the BeiDou "
+                            "convergence is not comparable with full-Doppler runs" if stream else
+                            "replay mode: the same span every step, full +-4 kHz Dopplers")},
         "cpu_baseline": None,
     }
     if rank == 0:
@@ -610,7 +619,35 @@ def run_c5(args):
         dist.destroy_process_group()
 
 
-def main():
+class DeviceBackend:
+    """The device side of the C2 bench: torch's HIP device (HBM buffers, stream
+    synchronisation, events), the gsdr engine and the rank collective's backend
+    (RCCL: "nccl").  tests/test_shard_gloo.py substitutes a CPU stand-in (gloo,
+    stubbed engine calls) to rehearse the multi-rank control flow -- process-group
+    init, the barriers, the max-over-ranks timing, each rank's block span and
+    channel set -- without a GPU (the replaced device split:
+    cuda_multicorrelator.cu:135-155)."""
+
+    dist_backend = "nccl"
+
+    def __init__(self, local):
+        import torch
+        import gsdr
+        self.torch, self.gsdr = torch, gsdr
+        torch.cuda.set_device(local)
+        self.dev = torch.device("cuda", local)
+
+    def dist_kwargs(self):
+        return {"device_id": self.dev}
+
+    def synchronize(self):
+        self.torch.cuda.synchronize(self.dev)
+
+    def event(self):
+        return self.torch.cuda.Event(enable_timing=True)
+
+
+def main(argv=None, backend=DeviceBackend):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
@@ -642,25 +679,20 @@ def main():
     ap.add_argument("--workload", choices=["c2", "c5"], default="c2",
                     help="c2 (default, the metric's configuration) or c5: the 25 Msps hybrid GPS/Galileo/BeiDou "
                          "job, 256 channels sharded c %% world, acquisition block spans per rank")
-    args = ap.parse_args()
+    args = ap.parse_args(argv)
     args.trk_stream = not args.trk_replay
     if args.workload == "c5":
         return run_c5(args)
 
-    import torch
-    import gsdr
-
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    be = backend(local)
+    torch, gsdr, dev = be.torch, be.gsdr, be.dev
     dist = None
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+        dist.init_process_group(be.dist_backend, **be.dist_kwargs())
     B = args.blocks
     W, K = args.warmup, args.steps
     # One stream for the whole job: every rank ingests the full
@@ -759,16 +791,17 @@ def main():
             trk.read_profile()
     if dist is not None:
         dist.barrier()
-    torch.cuda.synchronize(dev)
+    be.synchronize()
     # common time base for the chains' stage intervals (their busy-time union)
-    ref_ev = torch.cuda.Event(enable_timing=True)
-    ref_ev.record()
+    ref_ev = None if args.no_profile_events else be.event()
+    if ref_ev is not None:
+        ref_ev.record()
     t0 = time.perf_counter()
     if args.trk_stream:
         trk_stream_launch(K)
     for _ in range(args.steps):
         step()
-    torch.cuda.synchronize(dev)
+    be.synchronize()
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -954,10 +987,10 @@ def main():
             trk.set_profiling(False)
 
         def timed_part(fn):
-            torch.cuda.synchronize(dev)
+            be.synchronize()
             t = time.perf_counter()
             fn()
-            torch.cuda.synchronize(dev)
+            be.synchronize()
             return time.perf_counter() - t
 
         def acq_only():

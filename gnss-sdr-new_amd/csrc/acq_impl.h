@@ -777,6 +777,20 @@ struct Pads1000
         std::conditional_t<I == 2, RowPad<1000, 50, 3>, RowPad<1000, 0, 0>>>;
 };
 
+// Pads of the 10 x 10 x 10 row plan for workgroup-wide rows (RegFourStep H > 0, the
+// 25000-point split plan's 5 rows per round): stage 1's stride-10 writes go to a
+// buffer with one pad element every 10 (22-dword lane stride, conflict-free 16-lane
+// write groups), stage 2's to one with 6 every 100 (its 100-element row blocks shift
+// by 12 dwords).  Bank model (MI355X_MICROARCH.md LDS, ds_write_b64 4 x 16 lanes mod
+// 32, ds_read_b64 2 x 32 lanes mod 64) over the three stages of 5 rows on 512 lanes:
+// conflict cycles 43 % -> 15 % of the LDS-array cycles, LDS time -18 %.
+struct Pads25k
+{
+    template <int I>
+    using layout = std::conditional_t<I == 1, RowPad<1000, 10, 1>,
+        std::conditional_t<I == 2, RowPad<1000, 100, 6>, RowPad<1000, 0, 0>>>;
+};
+
 // ---- wave-local row transforms
 // One wave transforms one L-point row in place in its own LDS row buffer: the
 // Stockham exchange between the row stages needs no workgroup barrier, because
@@ -2404,6 +2418,9 @@ XMap grid_xmap(const gsdr_acq* a)
     const int64_t p = num / g0, q = den / g0;
     if (q < 1 || 2 * q > (int64_t)a->D) return plain;
     const int64_t ext = ((int64_t)(a->D - 1) / q) * p;
+    // the forward stores mirror bins i < N after bin N - 1 (out[N + i], i < ext), so
+    // a Doppler span wider than fs (ext > N) would leave rows reading unwritten bins
+    if (ext > (int64_t)a->N) return plain;
     // the stored spectra must fit the plain layout's allocation
     if (q * ((int64_t)a->N + ext) > (int64_t)a->D * (int64_t)a->N) return plain;
     return XMap{(uint32_t)q, (uint32_t)p, (uint32_t)(a->N + ext)};

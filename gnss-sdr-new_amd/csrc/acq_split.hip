@@ -13,6 +13,7 @@ namespace gsdr_acq_impl
 //   32000 = 32 x (10 x 10 x 10): 1024 lanes, one column per lane (32 complex),
 //           8 rows per LDS round (64 KB)
 using Reg25k = RegFourStep<25, 512, 5, 1, NoPads<1000>, 10, 10, 10>;
+using Reg25kP = RegFourStep<25, 512, 5, 1, Pads25k, 10, 10, 10>;  // the same with the bank-model pads
 using Reg32k = RegFourStep<32, 1024, 8, 1, NoPads<1000>, 10, 10, 10>;
 //   16000 = 16 x (10 x 10 x 10): the C3 plan (variant 93's register four-step), 512
 //           lanes, two columns per lane, 8 rows per LDS round (64 KB)
@@ -30,6 +31,7 @@ using Wl16k = RegFourStep<16, 512, 0, 1, NoPads<1000>, 10, 10, 10>;      // roun
 //   2: 32000 = 1 x 32000 (Galileo E1 at 8 Msps, 4 ms)
 //   3: 64000 = 2 x 32000 (C4: Galileo E1 at 8 Msps with bit transition)
 //   4: 100000 = 4 x 25000 (C5 Galileo E1 at 25 Msps, 4 ms)
+//   7: 25000 (Reg25kP)   8: 100000 = 4 x Reg25kP (padded row layouts)
 //   5: 32000 = 2 x 16000
 //   6: 64000 = 4 x 16000
 // wave-local rows:
@@ -50,7 +52,7 @@ struct SplitId
 // 64000, +4 % / +10 % over 2 / 3; the 512-lane 25000 plan keeps its LDS rounds)
 constexpr SplitId kSplits[] = {{1, 25000}, {12, 32000}, {13, 64000}, {4, 100000}, {2, 32000}, {3, 64000}, {5, 32000},
     {6, 64000}, {11, 25000}, {14, 100000}, {15, 32000}, {16, 64000}, {17, 25000}, {18, 100000}, {19, 32000},
-    {20, 64000}};
+    {20, 64000}, {7, 25000}, {8, 100000}};
 
 // PRN group of an XCD pass: the largest divisor of P whose code rows fit in ~2 MB
 // (half an XCD's L2), so the rows of the group's codes stay resident while the X
@@ -115,6 +117,8 @@ int launch_split_arg(gsdr_acq* a, uint32_t nblocks, hipStream_t s, const gsdr_ac
         case 2: GSDR_ARG(1, Reg32k);
         case 3: GSDR_ARG(2, Reg32k);
         case 4: GSDR_ARG(4, Reg25k);
+        case 7: GSDR_ARG(1, Reg25kP);
+        case 8: GSDR_ARG(4, Reg25kP);
         case 5: GSDR_ARG(2, Reg16k);
         case 6: GSDR_ARG(4, Reg16k);
         case 11: GSDR_ARG(1, Wl25k);
@@ -160,6 +164,8 @@ int launch_split(gsdr_acq* a, uint32_t nblocks, hipStream_t s)
         case 2: return half ? launch_one<1, Reg32k, true>(a, nblocks, s) : launch_one<1, Reg32k, false>(a, nblocks, s);
         case 3: return half ? launch_one<2, Reg32k, true>(a, nblocks, s) : launch_one<2, Reg32k, false>(a, nblocks, s);
         case 4: return half ? launch_one<4, Reg25k, true>(a, nblocks, s) : launch_one<4, Reg25k, false>(a, nblocks, s);
+        case 7: return half ? launch_one<1, Reg25kP, true>(a, nblocks, s) : launch_one<1, Reg25kP, false>(a, nblocks, s);
+        case 8: return half ? launch_one<4, Reg25kP, true>(a, nblocks, s) : launch_one<4, Reg25kP, false>(a, nblocks, s);
         case 5: return half ? launch_one<2, Reg16k, true>(a, nblocks, s) : launch_one<2, Reg16k, false>(a, nblocks, s);
         case 6: return half ? launch_one<4, Reg16k, true>(a, nblocks, s) : launch_one<4, Reg16k, false>(a, nblocks, s);
         case 11: return half ? launch_one<1, Wl25k, true>(a, nblocks, s) : launch_one<1, Wl25k, false>(a, nblocks, s);
@@ -209,6 +215,8 @@ int setup_split(gsdr_acq* a)
         case 2: rc = attrs_one<1, Reg32k, true>() | attrs_one<1, Reg32k, false>(); break;
         case 3: rc = attrs_one<2, Reg32k, true>() | attrs_one<2, Reg32k, false>(); break;
         case 4: rc = attrs_one<4, Reg25k, true>() | attrs_one<4, Reg25k, false>(); break;
+        case 7: rc = attrs_one<1, Reg25kP, true>() | attrs_one<1, Reg25kP, false>(); break;
+        case 8: rc = attrs_one<4, Reg25kP, true>() | attrs_one<4, Reg25kP, false>(); break;
         case 5: rc = attrs_one<2, Reg16k, true>() | attrs_one<2, Reg16k, false>(); break;
         case 6: rc = attrs_one<4, Reg16k, true>() | attrs_one<4, Reg16k, false>(); break;
         case 11: rc = attrs_one<1, Wl25k, true>() | attrs_one<1, Wl25k, false>(); break;

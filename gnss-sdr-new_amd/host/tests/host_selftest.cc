@@ -1457,7 +1457,7 @@ void test_pool_overrun()
 // Gnss_Synchro emission of both tracking blocks (dll_pll_veml_tracking.cc:1784-2152)
 // on a GPS channel driven past bit synchronisation, with GnssTime "timetag" input
 // tags every 100 ms and a telemetry fault (msg_handler_telemetry_to_trk, :614-637)
-// at 1.5 s.  Each block's per-call records, emitted Gnss_Synchro items, output tags
+// at 1.9 s.  Each block's per-call records, emitted Gnss_Synchro items, output tags
 // and the channel's acquisition record go to <dir>/synchro_<kind>.txt, which
 // tests/test_host_mirror.py replays through the oracle channel (with the fault
 // before the same call) and checks field by field.
@@ -1467,9 +1467,9 @@ void test_synchro_emission(const std::string& dir)
     const double amp = std::sqrt(2.0 * std::pow(10.0, 5.0) / fs);
     const std::vector<float> bits = {1, -1, -1, -1, 1, -1, 1, 1};
     SynthSat g{gps_l1_ca_code_gen_float(1), 1.023e6, 1575.42e6, 524.3, 1680.0, amp, {}, bits, 0.02};
-    const auto x = synth_stream({g}, fs, static_cast<size_t>(fs * 1.8), 11, 1.0);
+    const auto x = synth_stream({g}, fs, static_cast<size_t>(fs * 2.2), 11, 1.0);
     std::vector<GnssTimeTag> tags;
-    for (int k = 0; k < 18; ++k)
+    for (int k = 0; k < 22; ++k)
         {
             GnssTimeTag t;
             t.offset = static_cast<uint64_t>(k) * 400000 + 1234;
@@ -1532,7 +1532,7 @@ void test_synchro_emission(const std::string& dir)
             };
             while (nread + static_cast<uint64_t>(blk->forecast()) <= x.size() && blk->state() != 0)
                 {
-                    if (!faulted && nread >= 6000000)
+                    if (!faulted && nread >= 7600000)
                         {
                             blk->msg_handler_telemetry_to_trk(1);
                             faulted = true;
@@ -1605,6 +1605,10 @@ void test_synchro_emission(const std::string& dir)
             for (const auto& e : outs) (e.s.Flag_valid_symbol_output ? valid : lol) += 1;
             EXPECT(valid > 20 && lol == 1 && events == 1 && faulted,
                 "synchro emission: valid outputs, then the telemetry fault's loss of lock (one invalid output, event 3)");
+            if (!(valid > 20 && lol == 1 && events == 1 && faulted))
+                std::fprintf(stderr, "synchro emission (%s): %zu calls, valid %d, lol %d, events %d, faulted %d, nread %llu\n",
+                    pooled ? "pooled" : "per-channel", recs.size(), valid, lol, events, faulted ? 1 : 0,
+                    static_cast<unsigned long long>(nread));
             std::printf("synchro emission (%s block): %zu calls, %d valid outputs, %d loss-of-lock output, %s\n",
                 pooled ? "pooled" : "per-channel", recs.size(), valid, lol, path.c_str());
         }

@@ -87,6 +87,12 @@ int main(int argc, char** argv)
     std::vector<float> e1c_sec(25);
     const char* sec_str = "0011100000001010110110010";
     for (int i = 0; i < 25; ++i) e1c_sec[i] = sec_str[i] == '0' ? 1.0F : -1.0F;
+    // BeiDou B1I D1 (MEO / IGSO, PRN 6..58): the NH secondary code on every 1 ms code
+    // period under the 50 bps data (Beidou_B1I.h:40-48), which the tracking loop's
+    // secondary-code synchronisation needs before it emits
+    std::vector<float> bds_nh(20);
+    const char* nh_str = "00000100110101001110";
+    for (int i = 0; i < 20; ++i) bds_nh[i] = nh_str[i] == '0' ? 1.0F : -1.0F;
     for (size_t g = 0; g < sigs.size(); ++g)
         for (int c = 0; c < sigs[g].nch; ++c)
             {
@@ -107,8 +113,8 @@ int main(int argc, char** argv)
                         sats.push_back({e1c, 2.046e6, s.carrier, delay, dop, a, e1c_sec, {}, 0.004});
                     }
                 else
-                    sats.push_back({code_of(s.sys, prn), s.chip_rate, s.carrier, delay, dop, amp, {}, bits,
-                        s.sys == 'C' ? 0.02 : 0.02});
+                    sats.push_back({code_of(s.sys, prn), s.chip_rate, s.carrier, delay, dop, amp,
+                        s.sys == 'C' ? bds_nh : std::vector<float>{}, bits, 0.02});
             }
     const auto x = synth_stream(sats, fs, n, 7, sigma);
 

@@ -5,7 +5,9 @@
 set -o pipefail
 OUT=gpurun_out/${1:-r05a}
 shift
-mkdir -p "$OUT"
+mkdir -p "$OUT/synchro"
+GSDR_SELFTEST_ONLY=synchro GSDR_SELFTEST_DUMP_DIR="$OUT/synchro" timeout -k 10 120 \
+    ./gnss-sdr-new_amd/build/host_selftest tests/golden/GPS_L1_CA_ID_1_Fs_4Msps_2ms.dat > "$OUT/synchro.txt" 2>&1
 timeout -k 10 600 python -u -m pytest -x -v --timeout 240 --timeout-method thread -m gpu \
     tests/test_host_mirror.py tests/test_gpu_trk.py "$@" > "$OUT/pytest.txt" 2>&1 &&
 timeout -k 10 200 ./gnss-sdr-new_amd/build/receiver_bench c3 2 1 > "$OUT/receiver_c3_s1.json" 2> "$OUT/receiver_c3_s1.err" &&

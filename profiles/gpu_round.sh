@@ -29,7 +29,12 @@ timeout -k 10 200 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 
 echo "== c5" &&
 timeout -k 10 300 python bench.py --workload c5 --steps 20 --warmup 5 > "$OUT/bench_c5.json" 2> "$OUT/bench_c5.err" &&
 echo "== configs" &&
-timeout -k 10 300 python -u profiles/configs_bench.py --reps 5 > "$OUT/configs.jsonl" 2> "$OUT/configs.err"
+timeout -k 10 300 python -u profiles/configs_bench.py --reps 5 > "$OUT/configs.jsonl" 2> "$OUT/configs.err" &&
+echo "== receiver (the drop-in path: factory-built pooled tracking blocks + acquisition services, 2 s)" &&
+for cfg in c3 c5; do for s in 1 0; do
+    timeout -k 10 300 ./gnss-sdr-new_amd/build/receiver_bench $cfg 2 $s > "$OUT/receiver_${cfg}_s$s.json" \
+        2> "$OUT/receiver_${cfg}_s$s.err" && cat "$OUT/receiver_${cfg}_s$s.json" || exit 1
+done; done
 rc=$?
 echo "exit $rc"
 exit $rc

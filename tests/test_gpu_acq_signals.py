@@ -84,7 +84,7 @@ def test_beidou_b1i_synthetic_batch(fs):
 
 # acq_split.hip split ids and their FFT sizes (5/6: 16000-based splits; 11-20: the
 # wave-local-row plans)
-SPLIT_IDS = {5: 32000, 6: 64000, 11: 25000, 12: 32000, 13: 64000, 14: 100000, 15: 32000, 16: 64000, 17: 25000,
+SPLIT_IDS = {5: 32000, 6: 64000, 7: 25000, 8: 100000, 11: 25000, 12: 32000, 13: 64000, 14: 100000, 15: 32000, 16: 64000, 17: 25000,
              18: 100000, 19: 32000, 20: 64000}
 
 

@@ -131,6 +131,10 @@ def test_spectrum_reuse_factors():
     # 4 Msps / 1 kHz bins, 333 Hz step: q = 1000 > D / 2 -- plain layout
     acq = gsdr.Acquisition(4000000, 4000, 5000, 333, pfa=0.01, max_prns=1)
     assert acq.spectrum_reuse == (acq.num_doppler_bins, 0)
+    # a Doppler span wider than fs (step fs/2 over 5 bins: ext = 4 N/2 > N): the mirrored
+    # bins would not cover the rows' windows -- plain layout
+    acq = gsdr.Acquisition(2000000, 2000, 2500000, 1000000, pfa=0.01, max_prns=1)
+    assert acq.num_doppler_bins == 5 and acq.spectrum_reuse == (5, 0)
 
 
 @pytest.mark.parametrize("cfg_name", ["C2", "C4bt"])

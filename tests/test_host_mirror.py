@@ -214,6 +214,7 @@ def _expected_tags(recs, emits, tags, fs):
     consumed); an output re-emits it at output item nitems_written + 1 with the tow
     advanced by the (signed) sample distance."""
     import math
+    import gsdr
     out, waiting, last, written = [], False, None, 0
     for r in recs:
         sc, n = int(r["sample_counter"]), int(r["consumed"])

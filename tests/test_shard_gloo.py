@@ -217,3 +217,148 @@ def test_c5_plan_two_rank_gloo():
     assert tmax == 1.5
     assert sorted(plans[0]["channels"] + plans[1]["channels"]) == list(range(256))
     assert plans[0]["blocks"] == (0, 8) and plans[1]["blocks"] == (8, 16)
+
+
+class _StubEngine:
+    """CPU stand-in for the gsdr engine calls of bench.main's C2 path: the same
+    Python API (gsdr.Acquisition / gsdr.Tracking), recording each launch instead of
+    running it.  Rank 1's launches take longer, so the max over ranks is visible."""
+
+    def __init__(self, log, rank):
+        import gsdr
+        self._log, self._rank = log, rank
+        self.ACQ_RESULT_DTYPE, self.TRK_EPOCH_DTYPE = gsdr.ACQ_RESULT_DTYPE, gsdr.TRK_EPOCH_DTYPE
+        self.synth = synth
+        eng = self
+
+        class Acquisition:
+            def __init__(self, fs, n, dmax, dstep, max_blocks=1, **kw):
+                self.n, self.max_blocks, self.wipe_mode, self.spectrum_reuse = n, max_blocks, 0, (4, 16)
+
+            def set_local_codes(self, codes, prns):
+                eng._log.append(("codes", len(prns)))
+
+            def run_device(self, iq_ptr, nblocks, stride, stamp0, res_ptr, stream=None):
+                assert 0 < nblocks <= self.max_blocks
+                eng._log.append(("acq", int(stamp0) // self.n, int(nblocks)))
+                import time
+                time.sleep(0.002 * (1 + eng._rank))
+
+            def set_profiling(self, on):
+                pass
+
+            def close(self):
+                pass
+
+        class Tracking:
+            def __init__(self, conf, device=0):
+                self.nch = int(conf["max_channels"][0])
+
+            def start(self, ch, prn, code, delay, dop, stamp, nread):
+                eng._log.append(("trk_start", int(ch), int(prn)))
+
+            def save_state(self, slot):
+                pass
+
+            def restore_state(self, slot):
+                pass
+
+            def run_device(self, iq_ptr, first, items, max_epochs, out_ptr, n_ptr, stream=None):
+                eng._log.append(("trk", int(max_epochs)))
+
+            def set_profiling(self, on):
+                pass
+
+            def close(self):
+                pass
+
+        self.Acquisition, self.Tracking = Acquisition, Tracking
+
+    def trk_conf_default(self):
+        import gsdr
+        return np.zeros(1, gsdr.TRK_CONF_DTYPE)
+
+
+def _bench_worker(rank, world, port, q):
+    """One rank of `bench.py --gpus 2` under torch.distributed.run, the device calls
+    stubbed: bench.main itself does the process-group init (gloo instead of RCCL),
+    the barriers around the timed region and the max-over-ranks time."""
+    import contextlib
+    import io
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import bench
+    log = []
+
+    class CpuBackend:
+        dist_backend = "gloo"
+
+        def __init__(self, local):
+            self.torch, self.dev = torch, torch.device("cpu")
+            self.gsdr = _StubEngine(log, rank)
+
+        def dist_kwargs(self):
+            return {}
+
+        def synchronize(self):
+            pass
+
+        def event(self):
+            raise AssertionError("no profile events in this rehearsal")
+
+    out = io.StringIO()
+    try:
+        with contextlib.redirect_stdout(out):
+            bench.main(["--gpus", str(world), "--steps", "3", "--warmup", "1", "--no-profile-events",
+                        "--no-cpu-baseline"], backend=CpuBackend)
+    except BaseException as e:  # report instead of leaving the parent waiting
+        q.put((rank, None, repr(e)))
+        raise
+    q.put((rank, log, out.getvalue()))
+
+
+def test_bench_main_two_rank_gloo_control_flow():
+    """bench.py's real C2 control flow at world size 2 with the device calls stubbed
+    (tests the multi-rank path before an 8-GPU measurement): each rank acquires its
+    own block span of the one stream every step and tracks channels c % 2; rank 0
+    prints the one JSON line, whose value is all ranks' samples over the slowest
+    rank's time."""
+    import json
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    os.environ["PYTHONPATH"] = os.pathsep.join([here, root, os.path.join(root, "gnss-sdr-new_amd"),
+                                                os.environ.get("PYTHONPATH", "")])
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict((r, (log, out)) for r, log, out in (q.get(timeout=240), q.get(timeout=240)))
+    assert all(v[0] is not None for v in got.values()), got
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    import bench
+    line = json.loads(got[0][1].strip().splitlines()[-1])
+    assert got[1][1].strip() == ""  # only rank 0 prints
+    assert line["n_gpus"] == 2 and line["steps"] == 3 and line["scaling"] == "weak"
+    B = line["config"]["blocks_per_step"]
+    # all ranks' samples over the max-over-ranks time: rank 1 (slower) sets it
+    assert abs(line["value"] - 2 * 3 * B * bench.N / (line["ms_per_step"] * 3e-3) / 1e6) <= 1e-3 * line["value"]
+    assert line["ms_per_step"] >= 2 * 0.002 * 2 * 1e3 * 0.9  # rank 1's two chains sleep 4 ms per step
+    total = 2 * B
+    for r in (0, 1):
+        log = got[r][0]
+        lo, hi = bench.rank_plan(2, r, B, bench.CHANNELS)["blocks"]
+        acq = [e for e in log if e[0] == "acq"]
+        # two chains x (1 warmup + 3 timed steps + 3 steps of the acquisition-only rate)
+        assert len(acq) == 2 * 7
+        for s in range(4):
+            spans = sorted((e[1] - s * total, e[2]) for e in acq[2 * s:2 * s + 2])
+            assert spans[0][0] == lo and spans[0][0] + spans[0][1] == spans[1][0] and spans[1][0] + spans[1][1] == hi
+        mine = bench.rank_plan(2, r, B, bench.CHANNELS)["channels"]
+        assert [e[1] for e in log if e[0] == "trk_start"] == list(range(len(mine)))
+        assert all(c % 2 == r for c in mine) and len(mine) == bench.CHANNELS // 2
+        # one tracking launch for the warmup, one for the timed steps, one for the tracking-only rate
+        assert [e for e in log if e[0] == "trk"] == [("trk", 1 * total), ("trk", 3 * total), ("trk", 3 * total)]

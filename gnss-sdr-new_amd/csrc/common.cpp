@@ -116,4 +116,18 @@ int gsdr_device_count(int* count)
     return GSDR_OK;
 }
 
+int gsdr_host_register(void* ptr, size_t bytes)
+{
+    GSDR_REQUIRE(ptr && bytes > 0, GSDR_E_ARG, "gsdr_host_register: null or empty buffer");
+    GSDR_HIP(hipHostRegister(ptr, bytes, hipHostRegisterDefault));
+    return GSDR_OK;
+}
+
+int gsdr_host_unregister(void* ptr)
+{
+    GSDR_REQUIRE(ptr, GSDR_E_ARG, "gsdr_host_unregister: null buffer");
+    GSDR_HIP(hipHostUnregister(ptr));
+    return GSDR_OK;
+}
+
 }  // extern "C"

@@ -4,6 +4,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstdint>
 #include <mutex>
 
 #include "gsdr.h"
@@ -30,11 +31,12 @@ public:
     int span(uint64_t* first, uint64_t* n);
     // make `consumer` wait for the pushes so far
     int acquire(hipStream_t consumer);
-    // record the consumer's reads (the next push waits for them)
+    // record the consumer's reads (a push overwriting the oldest item viewed waits for them)
     int release(hipStream_t consumer);
 
 private:
     gsdr_stream* s_;
+    uint64_t lo_{UINT64_MAX};  // the oldest item viewed
     std::unique_lock<std::mutex> lk_;
 };
 }  // namespace gsdr

@@ -9,7 +9,10 @@
 // `window` positions after the end, so any window of up to `window` items is one
 // contiguous device span (no consumer handles the wrap).  Pushes run on the
 // ring's own copy stream; a consumer launch waits on the last push's event and
-// records a reader event that the next push waits on before it overwrites.
+// records a reader event of its own, tagged with the oldest item it reads; a push
+// waits only for the readers whose oldest item it overwrites.  Consumers on other
+// streams (the tracking pools of several signals, the acquisition services) thus
+// run concurrently with each other and with the pushes of newer items.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -36,7 +39,16 @@ struct gsdr_stream
     uint64_t head{0};  // absolute index of the next item to push
     hipStream_t copy{nullptr};
     hipEvent_t pushed{nullptr};
-    hipEvent_t read{nullptr};  // the last consumer launch reading the ring
+    // consumer launches that may still read the ring: the oldest item each reads and
+    // the event recorded behind it on its stream
+    struct Reader
+    {
+        uint64_t lo;
+        hipEvent_t ev;
+    };
+    std::vector<Reader> readers;
+    std::vector<hipEvent_t> retired;  // waited for by a push, recycled once complete
+    std::vector<hipEvent_t> spare;
     // windows handed out by gsdr_stream_window_async whose reads are not yet
     // released: a push that would overwrite one waits for its release (another
     // thread's window) or fails (the pushing thread's own window)
@@ -84,25 +96,58 @@ int span_locked(gsdr_stream* s, uint64_t* first, uint64_t* n)
     return GSDR_OK;
 }
 
-int release_locked(gsdr_stream* s, hipStream_t consumer)
+// reader events that completed go back to the spare list (ring lock held)
+void recycle_locked(gsdr_stream* s)
 {
-    // one reader event suffices: the consumer first waits for the previous reader,
-    // so the event recorded here completes only after every earlier read
-    GSDR_HIP(hipStreamWaitEvent(consumer, s->read, 0));
-    GSDR_HIP(hipEventRecord(s->read, consumer));
+    auto done = [s](hipEvent_t ev) {
+        if (hipEventQuery(ev) != hipSuccess) return false;
+        s->spare.push_back(ev);
+        return true;
+    };
+    s->readers.erase(std::remove_if(s->readers.begin(), s->readers.end(),
+                         [&](const gsdr_stream::Reader& r) { return done(r.ev); }),
+        s->readers.end());
+    s->retired.erase(std::remove_if(s->retired.begin(), s->retired.end(), done), s->retired.end());
+}
+
+// the consumer's reads of items >= lo are enqueued on `consumer`: a push that
+// overwrites any of them waits for the event recorded here
+int release_locked(gsdr_stream* s, hipStream_t consumer, uint64_t lo)
+{
+    if (s->readers.size() + s->retired.size() >= 16) recycle_locked(s);
+    hipEvent_t ev = nullptr;
+    if (!s->spare.empty())
+        {
+            ev = s->spare.back();
+            s->spare.pop_back();
+        }
+    else
+        GSDR_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    const hipError_t e = hipEventRecord(ev, consumer);
+    if (e != hipSuccess)
+        {
+            s->spare.push_back(ev);
+            GSDR_HIP(e);
+        }
+    s->readers.push_back({lo, ev});
     return GSDR_OK;
 }
 }  // namespace
 
 StreamReader::StreamReader(gsdr_stream* s) : s_(s), lk_(s->mu) {}
-int StreamReader::view(uint64_t first, uint64_t n, const void** ptr) { return view_locked(s_, first, n, ptr); }
+int StreamReader::view(uint64_t first, uint64_t n, const void** ptr)
+{
+    const int rc = view_locked(s_, first, n, ptr);
+    if (rc == GSDR_OK) lo_ = std::min(lo_, first);
+    return rc;
+}
 int StreamReader::span(uint64_t* first, uint64_t* n) { return span_locked(s_, first, n); }
 int StreamReader::acquire(hipStream_t consumer)
 {
     GSDR_HIP(hipStreamWaitEvent(consumer, s_->pushed, 0));
     return GSDR_OK;
 }
-int StreamReader::release(hipStream_t consumer) { return release_locked(s_, consumer); }
+int StreamReader::release(hipStream_t consumer) { return release_locked(s_, consumer, lo_ == UINT64_MAX ? 0 : lo_); }
 }  // namespace gsdr
 
 namespace
@@ -134,7 +179,6 @@ int gsdr_stream_create(int device, int item_type, uint64_t capacity_items, uint6
     hipError_t e = hipMalloc(&s->d_ring, (size_t)(s->cap + s->window) * s->item_bytes);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&s->copy, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&s->pushed, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&s->read, hipEventDisableTiming);
     if (e != hipSuccess)
         {
             gsdr::set_error("gsdr_stream_create: %s", hipGetErrorString(e));
@@ -150,9 +194,18 @@ void gsdr_stream_destroy(gsdr_stream* s)
     if (!s) return;
     gsdr::DeviceGuard g(s->device);
     if (s->copy) (void)hipStreamSynchronize(s->copy);
-    if (s->read) (void)hipEventSynchronize(s->read);
+    for (const auto& r : s->readers)
+        {
+            (void)hipEventSynchronize(r.ev);
+            (void)hipEventDestroy(r.ev);
+        }
+    for (hipEvent_t ev : s->retired)
+        {
+            (void)hipEventSynchronize(ev);
+            (void)hipEventDestroy(ev);
+        }
+    for (hipEvent_t ev : s->spare) (void)hipEventDestroy(ev);
     if (s->pushed) (void)hipEventDestroy(s->pushed);
-    if (s->read) (void)hipEventDestroy(s->read);
     if (s->copy) (void)hipStreamDestroy(s->copy);
     if (s->d_ring) (void)hipFree(s->d_ring);
     delete s;
@@ -199,8 +252,20 @@ int gsdr_stream_push(gsdr_stream* s, const void* iq_host, uint64_t first_sample,
                 "gsdr_stream_push: a window over the items it would overwrite stayed open for %lld s "
                 "(gsdr_stream_release missing)", (long long)kStallLimit.count());
         }
-    // overwrite only what no consumer launch still reads
-    GSDR_HIP(hipStreamWaitEvent(s->copy, s->read, 0));
+    // overwrite only what no consumer launch still reads: the copy waits for the
+    // readers of items below the new oldest (later pushes are ordered behind it)
+    const uint64_t overwritten = s->head + n > s->cap ? s->head + n - s->cap : 0;
+    for (auto it = s->readers.begin(); it != s->readers.end();)
+        {
+            if (it->lo < overwritten)
+                {
+                    GSDR_HIP(hipStreamWaitEvent(s->copy, it->ev, 0));
+                    s->retired.push_back(it->ev);
+                    it = s->readers.erase(it);
+                }
+            else
+                ++it;
+        }
     const auto* src = static_cast<const uint8_t*>(iq_host);
     uint64_t done = 0;
     while (done < n)
@@ -259,9 +324,14 @@ int gsdr_stream_release(gsdr_stream* s, void* consumer_stream)
     GSDR_REQUIRE(s && consumer_stream, GSDR_E_ARG, "gsdr_stream_release: null argument");
     std::lock_guard<std::mutex> lk(s->mu);
     gsdr::DeviceGuard g(s->device);
-    const int rc = gsdr::release_locked(s, (hipStream_t)consumer_stream);
-    // the reader event now covers this consumer's reads: its windows close
     const hipStream_t c = (hipStream_t)consumer_stream;
+    // the oldest item of the windows this consumer holds open (none: every item)
+    uint64_t lo = UINT64_MAX;
+    for (const auto& w : s->open)
+        if (w.consumer == c) lo = std::min(lo, w.first);
+    if (lo == UINT64_MAX) lo = 0;
+    const int rc = gsdr::release_locked(s, c, lo);
+    // the reader event now covers this consumer's reads: its windows close
     s->open.erase(std::remove_if(s->open.begin(), s->open.end(), [c](const gsdr_stream::OpenWindow& w) {
         return w.consumer == c;
     }), s->open.end());

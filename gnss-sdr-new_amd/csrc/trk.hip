@@ -1811,6 +1811,16 @@ struct gsdr_trk
     // d_chans (start / stop / get_channel) wait for it, so a launch in flight on a
     // caller stream cannot write a stale channel back over them
     hipEvent_t last_launch{nullptr};
+    // gsdr_trk_submit_stream / gsdr_trk_collect: device records of the submission,
+    // their pinned host image and the event of its copy
+    gsdr_trk_epoch* d_sub_out{nullptr};
+    uint32_t* d_sub_nout{nullptr};
+    gsdr_trk_epoch* h_sub_out{nullptr};
+    uint32_t* h_sub_nout{nullptr};
+    uint32_t sub_cap{0};  // records per channel the submission buffers hold
+    uint32_t sub_epochs{0};
+    bool sub_pending{false};
+    hipEvent_t sub_done{nullptr};
     std::mutex mu;
 };
 
@@ -2256,6 +2266,15 @@ void gsdr_trk_destroy(gsdr_trk* k)
             (void)hipEventDestroy(r.second);
         }
     for (hipEvent_t e : k->prof_pool) (void)hipEventDestroy(e);
+    if (k->sub_done)
+        {
+            (void)hipEventSynchronize(k->sub_done);
+            (void)hipEventDestroy(k->sub_done);
+        }
+    if (k->h_sub_out) (void)hipHostFree(k->h_sub_out);
+    if (k->h_sub_nout) (void)hipHostFree(k->h_sub_nout);
+    if (k->d_sub_out) (void)hipFree(k->d_sub_out);
+    if (k->d_sub_nout) (void)hipFree(k->d_sub_nout);
     if (k->last_launch)
         {
             (void)hipEventSynchronize(k->last_launch);
@@ -2507,6 +2526,71 @@ int gsdr_trk_run_stream_host(gsdr_trk* k, gsdr_stream* ring, uint32_t max_epochs
     GSDR_HIP(hipMemcpyAsync(out_host, k->d_out, (size_t)k->conf.max_channels * max_epochs * sizeof(gsdr_trk_epoch),
         hipMemcpyDeviceToHost, k->stream));
     GSDR_HIP(hipStreamSynchronize(k->stream));
+    return GSDR_OK;
+}
+
+int gsdr_trk_submit_stream(gsdr_trk* k, gsdr_stream* ring, uint32_t max_epochs)
+{
+    GSDR_REQUIRE(k && ring, GSDR_E_ARG, "gsdr_trk_submit_stream: null argument");
+    GSDR_REQUIRE(max_epochs >= 1, GSDR_E_ARG, "gsdr_trk_submit_stream: max_epochs must be >= 1");
+    {
+        std::lock_guard<std::mutex> lk(k->mu);
+        GSDR_REQUIRE(!k->sub_pending, GSDR_E_STATE, "gsdr_trk_submit_stream: collect the previous submission first");
+        gsdr::DeviceGuard g(k->device);
+        const uint32_t nch = k->conf.max_channels;
+        if (max_epochs > k->sub_cap)
+            {
+                // nothing in flight reads them (sub_pending is false)
+                if (k->d_sub_out) GSDR_HIP(hipFree(k->d_sub_out));
+                if (k->h_sub_out) GSDR_HIP(hipHostFree(k->h_sub_out));
+                k->d_sub_out = nullptr;
+                k->h_sub_out = nullptr;
+                k->sub_cap = 0;
+                GSDR_HIP(hipMalloc(&k->d_sub_out, (size_t)nch * max_epochs * sizeof(gsdr_trk_epoch)));
+                GSDR_HIP(hipHostMalloc(reinterpret_cast<void**>(&k->h_sub_out), (size_t)nch * max_epochs * sizeof(gsdr_trk_epoch),
+                    hipHostMallocDefault));
+                k->sub_cap = max_epochs;
+            }
+        if (!k->d_sub_nout)
+            {
+                GSDR_HIP(hipMalloc(&k->d_sub_nout, nch * sizeof(uint32_t)));
+                GSDR_HIP(hipHostMalloc(reinterpret_cast<void**>(&k->h_sub_nout), nch * sizeof(uint32_t), hipHostMallocDefault));
+                GSDR_HIP(hipEventCreateWithFlags(&k->sub_done, hipEventDisableTiming));
+            }
+    }
+    int rc = gsdr_trk_run_stream(k, ring, max_epochs, k->d_sub_out, k->d_sub_nout, nullptr);
+    if (rc != GSDR_OK) return rc;
+    std::lock_guard<std::mutex> lk(k->mu);
+    gsdr::DeviceGuard g(k->device);
+    const uint32_t nch = k->conf.max_channels;
+    GSDR_HIP(hipMemcpyAsync(k->h_sub_nout, k->d_sub_nout, nch * sizeof(uint32_t), hipMemcpyDeviceToHost, k->stream));
+    GSDR_HIP(hipMemcpyAsync(k->h_sub_out, k->d_sub_out, (size_t)nch * max_epochs * sizeof(gsdr_trk_epoch),
+        hipMemcpyDeviceToHost, k->stream));
+    GSDR_HIP(hipEventRecord(k->sub_done, k->stream));
+    k->sub_epochs = max_epochs;
+    k->sub_pending = true;
+    return GSDR_OK;
+}
+
+int gsdr_trk_collect(gsdr_trk* k, int wait, gsdr_trk_epoch* out_host, uint32_t* n_out_host, uint32_t* max_epochs)
+{
+    GSDR_REQUIRE(k && out_host && n_out_host, GSDR_E_ARG, "gsdr_trk_collect: null argument");
+    std::lock_guard<std::mutex> lk(k->mu);
+    GSDR_REQUIRE(k->sub_pending, GSDR_E_STATE, "gsdr_trk_collect: nothing submitted");
+    gsdr::DeviceGuard g(k->device);
+    if (!wait)
+        {
+            const hipError_t q = hipEventQuery(k->sub_done);
+            if (q == hipErrorNotReady) return 1;
+            GSDR_HIP(q);
+        }
+    else
+        GSDR_HIP(hipEventSynchronize(k->sub_done));
+    k->sub_pending = false;
+    const uint32_t nch = k->conf.max_channels, me = k->sub_epochs;
+    std::memcpy(n_out_host, k->h_sub_nout, nch * sizeof(uint32_t));
+    std::memcpy(out_host, k->h_sub_out, (size_t)nch * me * sizeof(gsdr_trk_epoch));
+    if (max_epochs) *max_epochs = me;
     return GSDR_OK;
 }
 

@@ -46,7 +46,8 @@ EXPORTED = [
     "gsdr_trk_set_data_code", "gsdr_acq_read_profile_ex", "gsdr_stream_window_async", "gsdr_stream_release", "gsdr_stream_device",
     "gsdr_acq_dump_grid_step_two", "gsdr_acq_read_profile_intervals", "gsdr_acq_set_wipeoff",
     "gsdr_acq_get_spectrum_reuse", "gsdr_trk_force_loss_of_lock", "gsdr_acq_set_local_code",
-    "gsdr_acq_set_active_prns", "gsdr_acq_submit_stream", "gsdr_acq_collect",
+    "gsdr_acq_set_active_prns", "gsdr_acq_submit_stream", "gsdr_acq_collect", "gsdr_host_register",
+    "gsdr_host_unregister", "gsdr_trk_submit_stream", "gsdr_trk_collect",
 ]
 
 WIPE_EXACT, WIPE_GENERIC, WIPE_AVX2 = 0, 1, 2
@@ -269,6 +270,8 @@ def load():
     L.gsdr_acq_set_active_prns.argtypes = [P, U32]
     L.gsdr_acq_submit_stream.argtypes = [P, P, U64, U32, U64]
     L.gsdr_acq_collect.argtypes = [P, P, P, P]
+    L.gsdr_host_register.argtypes = [P, ctypes.c_size_t]
+    L.gsdr_host_unregister.argtypes = [P]
     L.gsdr_trk_set_data_code.argtypes = [P, I, P, I]
     L.gsdr_trk_run_device.argtypes = [P, P, U64, U64, U32, P, P, P]
     L.gsdr_trk_run.argtypes = [P, P, U64, U64, U32, P, P]
@@ -296,6 +299,8 @@ def load():
     L.gsdr_acq_run_stream.argtypes = [P, P, U64, U32, U64, P]
     L.gsdr_trk_run_stream.argtypes = [P, P, U32, P, P, P]
     L.gsdr_trk_run_stream_host.argtypes = [P, P, U32, P, P]
+    L.gsdr_trk_submit_stream.argtypes = [P, P, U32]
+    L.gsdr_trk_collect.argtypes = [P, ctypes.c_int, P, P, P]
     _lib = L
     return L
 
@@ -675,6 +680,23 @@ class Tracking:
         n = np.zeros(self.max_channels, np.uint32)
         _check(load().gsdr_trk_run_stream_host(self._h, ring._h, int(max_epochs), _ptr(out), _ptr(n)))
         return out.reshape(self.max_channels, max_epochs), n
+
+    def submit_stream(self, ring, max_epochs):
+        """gsdr_trk_submit_stream: the ring form with the records copied back behind it; no wait."""
+        _check(load().gsdr_trk_submit_stream(self._h, ring._h, int(max_epochs)))
+        self._sub_epochs = int(max_epochs)
+
+    def collect(self, wait=True):
+        """gsdr_trk_collect -> (records, counts), or None while the submission is in flight (wait=False)."""
+        me = self._sub_epochs
+        out = np.zeros(self.max_channels * me, TRK_EPOCH_DTYPE)
+        n = np.zeros(self.max_channels, np.uint32)
+        got = ctypes.c_uint32()
+        rc = load().gsdr_trk_collect(self._h, 1 if wait else 0, _ptr(out), _ptr(n), ctypes.byref(got))
+        if rc == 1:
+            return None
+        _check(rc)
+        return out.reshape(self.max_channels, me), n
 
     def channel(self, ch):
         st, nxt, dop, cn0 = ctypes.c_int32(), ctypes.c_uint64(), ctypes.c_double(), ctypes.c_double()

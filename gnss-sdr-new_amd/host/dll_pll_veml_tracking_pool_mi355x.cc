@@ -1,6 +1,7 @@
 #include "dll_pll_veml_tracking_pool_mi355x.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <iostream>
 #include <map>
 #include <stdexcept>
@@ -14,12 +15,11 @@ std::runtime_error gsdr_error(const char* what) { return std::runtime_error(std:
 }  // namespace
 
 SharedTrackingPool::SharedTrackingPool(const Dll_Pll_Conf& conf, int32_t signal, uint32_t max_channels, int device,
-    uint32_t window_calls, uint32_t batch_calls)
+    uint32_t window_calls, uint32_t batch_calls, const std::string& ring_key)
     : d_conf(conf), d_signal(signal), d_max(max_channels), d_device(device)
 {
     const gsdr_trk_conf c = d_conf.to_engine(signal, max_channels);
     if (gsdr_trk_create(device, &c, &d_engine) != GSDR_OK) throw gsdr_error("SharedTrackingPool");
-    d_item_bytes = c.item_type == GSDR_ITEM_CSHORT ? 4 : (c.item_type == GSDR_ITEM_IBYTE ? 2 : 8);
     // the newest window the channels' calls are read from (window_calls vector
     // lengths, twice that of ring positions); the pool advances every channel
     // whenever half a window arrived, so a channel is never more than that behind
@@ -31,32 +31,50 @@ SharedTrackingPool::SharedTrackingPool(const Dll_Pll_Conf& conf, int32_t signal,
         throw std::invalid_argument("SharedTrackingPool: mi355x_pool_batch must be in [1, mi355x_pool_window / 2]");
     d_window = static_cast<uint64_t>(window_calls) * d_conf.vector_length;
     d_batch = static_cast<uint64_t>(batch_calls) * d_conf.vector_length;
-    if (gsdr_stream_create(device, c.item_type, 2 * d_window, d_window, &d_ring) != GSDR_OK)
+    try
+        {
+            d_ring = DeviceIqRing::get(device, c.item_type, d_window, ring_key);
+        }
+    catch (...)
         {
             gsdr_trk_destroy(d_engine);
-            throw gsdr_error("SharedTrackingPool ring");
+            throw;
         }
     d_used.assign(max_channels, false);
     d_active.assign(max_channels, false);
+    d_gen.assign(max_channels, 0);
+    d_sub_gen.assign(max_channels, 0);
+    // one submission covers every call a channel can have in the ring: a channel is
+    // advanced whenever half a window arrived, so it never lags the head by more
+    d_epochs = window_calls + 2;
+    d_sync = std::getenv("GSDR_POOL_SYNC") != nullptr;  // A/B: wait for every advance
     d_queue.resize(max_channels);
     d_n.assign(max_channels, 0);
+    d_hook = d_ring->add_hook([this](uint64_t from, uint64_t head) { on_pushed(from, head); });
 }
 
 SharedTrackingPool::~SharedTrackingPool()
 {
-    gsdr_stream_destroy(d_ring);
+    d_ring->remove_hook(d_hook);
+    if (d_pending)
+        {
+            uint32_t me = 0;
+            d_recs.resize(static_cast<size_t>(d_max) * d_epochs);
+            (void)gsdr_trk_collect(d_engine, 1, d_recs.data(), d_n.data(), &me);
+        }
     gsdr_trk_destroy(d_engine);
 }
 
 std::shared_ptr<SharedTrackingPool> SharedTrackingPool::get(const std::string& key, const Dll_Pll_Conf& conf,
-    int32_t signal, uint32_t max_channels, int device, uint32_t window_calls, uint32_t batch_calls)
+    int32_t signal, uint32_t max_channels, int device, uint32_t window_calls, uint32_t batch_calls,
+    const std::string& ring_key)
 {
     static std::mutex mu;
     static std::map<std::tuple<std::string, int, int32_t>, std::weak_ptr<SharedTrackingPool>> registry;
     std::lock_guard<std::mutex> lk(mu);
     auto& w = registry[std::make_tuple(key, device, signal)];
     if (auto p = w.lock()) return p;
-    auto p = std::make_shared<SharedTrackingPool>(conf, signal, max_channels, device, window_calls, batch_calls);
+    auto p = std::make_shared<SharedTrackingPool>(conf, signal, max_channels, device, window_calls, batch_calls, ring_key);
     w = p;
     return p;
 }
@@ -80,6 +98,7 @@ void SharedTrackingPool::release_slot(int slot)
     gsdr_trk_stop(d_engine, slot);
     d_used[slot] = false;
     d_active[slot] = false;
+    ++d_gen[slot];
     d_queue[slot].clear();
 }
 
@@ -110,6 +129,7 @@ uint64_t SharedTrackingPool::start(int slot, uint32_t prn, const char signal[2],
         throw gsdr_error("SharedTrackingPool::start");
     d_queue[slot].clear();
     d_active[slot] = true;
+    ++d_gen[slot];  // records of a submission in flight belong to the previous track
     return first;
 }
 
@@ -126,67 +146,95 @@ void SharedTrackingPool::stop(int slot)
     if (slot < 0 || static_cast<uint32_t>(slot) >= d_max) return;
     gsdr_trk_stop(d_engine, slot);
     d_active[slot] = false;
+    ++d_gen[slot];
     d_queue[slot].clear();
 }
 
-void SharedTrackingPool::advance_locked()
+bool SharedTrackingPool::take_locked(bool wait)
 {
-    const uint32_t me = 32;  // calls per channel per launch
-    d_recs.resize(static_cast<size_t>(d_max) * me);
+    if (!d_pending) return true;
+    d_recs.resize(static_cast<size_t>(d_max) * d_epochs);
+    uint32_t me = 0;
+    const int rc = gsdr_trk_collect(d_engine, wait ? 1 : 0, d_recs.data(), d_n.data(), &me);
+    if (rc == 1) return false;  // still in flight
+    d_pending = false;
+    if (rc != GSDR_OK) throw gsdr_error("SharedTrackingPool::advance");
+    uint32_t most = 0;
+    for (uint32_t c = 0; c < d_max; ++c)
+        {
+            most = std::max(most, d_n[c]);
+            // a slot started or stopped since the submission: its records are stale
+            if (!d_active[c] || d_gen[c] != d_sub_gen[c]) continue;
+            for (uint32_t e = 0; e < d_n[c]; ++e) d_queue[c].push_back(d_recs[static_cast<size_t>(c) * me + e]);
+        }
+    d_more = most >= me;  // a full batch: more calls may be ready in the ring
+    return true;
+}
+
+void SharedTrackingPool::advance_locked(uint64_t head, bool wait)
+{
+    take_locked(true);  // one submission in flight per pool
     for (;;)
         {
-            if (gsdr_trk_run_stream_host(d_engine, d_ring, me, d_recs.data(), d_n.data()) != GSDR_OK)
+            // on the engine's stream, ordered after the ring's pushes; the records come
+            // back behind it while the host pushes and runs the blocks
+            if (gsdr_trk_submit_stream(d_engine, d_ring->stream(), d_epochs) != GSDR_OK)
                 throw gsdr_error("SharedTrackingPool::advance");
+            d_pending = true;
+            d_sub_gen = d_gen;
             ++d_launches;
-            uint32_t most = 0;
-            for (uint32_t c = 0; c < d_max; ++c)
-                {
-                    most = std::max(most, d_n[c]);
-                    if (!d_active[c]) continue;
-                    for (uint32_t e = 0; e < d_n[c]; ++e) d_queue[c].push_back(d_recs[static_cast<size_t>(c) * me + e]);
-                }
-            if (most < me) break;  // a full batch: more calls may be ready in the ring
+            d_advanced = head;
+            if (!wait && !d_sync) return;
+            take_locked(true);
+            if (!d_more) return;
         }
-    d_advanced = d_head;
+}
+
+void SharedTrackingPool::on_pushed(uint64_t from, uint64_t head)
+{
+    std::lock_guard<std::mutex> lk(d_mu);
+    if (!d_seen)
+        {
+            d_seen = true;
+            d_advanced = from;
+        }
+    // no started channel's next call may leave the ring: advance after half a window
+    if (head - d_advanced >= d_window / 2) advance_locked(head, false);
 }
 
 void SharedTrackingPool::feed(const void* in, uint64_t nitems_read, int n)
 {
-    std::lock_guard<std::mutex> lk(d_mu);
-    const uint64_t end = nitems_read + static_cast<uint64_t>(std::max(n, 0));
-    if (!d_started)
-        {
-            d_started = true;
-            d_origin = d_head = d_advanced = nitems_read;
-        }
-    if (nitems_read > d_head)
-        throw std::logic_error("SharedTrackingPool::feed: the stream skipped items no pooled block has seen");
-    const auto* bytes = static_cast<const uint8_t*>(in);
-    // chunks of at most half the window, the channels advanced whenever half a
-    // window arrived since the last advance: no started channel's next call ever
-    // leaves the ring's newest window
-    const uint64_t half = std::max<uint64_t>(1, d_window / 2);
-    while (d_head < end)
-        {
-            const uint64_t len = std::min(half - std::min(half - 1, d_head - d_advanced), end - d_head);
-            if (gsdr_stream_push(d_ring, bytes + (d_head - nitems_read) * d_item_bytes, d_head, len) != GSDR_OK)
-                throw gsdr_error("SharedTrackingPool::feed");
-            d_head += len;
-            if (d_head - d_advanced >= half) advance_locked();
-        }
+    // without the pool's lock: the ring runs every pool's hook (this one's included)
+    d_ring->feed(in, nitems_read, n);
 }
 
 void SharedTrackingPool::advance_if_due(bool force)
 {
     std::lock_guard<std::mutex> lk(d_mu);
-    if (!d_started || d_head == d_advanced) return;
-    if (force || d_head - d_advanced >= d_batch) advance_locked();
+    uint64_t head = 0;
+    if (!d_ring->head(&head)) return;
+    if (!d_seen)
+        {
+            d_seen = true;
+            d_advanced = head;
+        }
+    if (force)
+        {
+            if (head != d_advanced || d_more)
+                advance_locked(head, true);
+            else
+                take_locked(true);
+            return;
+        }
+    if (head == d_advanced && !d_more) return;
+    if (d_more || head - d_advanced >= d_batch) advance_locked(head, false);
 }
 
 bool SharedTrackingPool::peek(int slot, gsdr_trk_epoch* rec)
 {
     std::lock_guard<std::mutex> lk(d_mu);
-    if (slot < 0 || d_queue[slot].empty()) return false;
+    if (slot < 0) return false;
+    if (d_queue[slot].empty()) return false;
     *rec = d_queue[slot].front();
     return true;
 }
@@ -198,12 +246,13 @@ void SharedTrackingPool::drop(int slot)
 }
 
 dll_pll_veml_tracking_pool_mi355x::dll_pll_veml_tracking_pool_mi355x(const Dll_Pll_Conf& conf, int32_t signal,
-    uint32_t pool_channels, int device, const std::string& pool_key, uint32_t window_calls, uint32_t batch_calls)
+    uint32_t pool_channels, int device, const std::string& pool_key, uint32_t window_calls, uint32_t batch_calls,
+    const std::string& ring_key)
     : d_conf(conf), d_signal(signal)
 {
     if (d_conf.dump) d_dump.configure(d_conf.dump_filename);
     d_output = TrackingOutput(d_conf.fs_in, signal);
-    d_pool = SharedTrackingPool::get(pool_key, conf, signal, pool_channels, device, window_calls, batch_calls);
+    d_pool = SharedTrackingPool::get(pool_key, conf, signal, pool_channels, device, window_calls, batch_calls, ring_key);
     d_slot = d_pool->acquire_slot();
     if (d_slot < 0)
         throw std::runtime_error("dll_pll_veml_tracking_pool_mi355x: every slot of pool '" + pool_key + "' is taken");

@@ -28,6 +28,7 @@
 #include <string>
 #include <vector>
 
+#include "device_iq_ring.h"
 #include "dll_pll_conf.h"
 #include "gnss_synchro.h"
 #include "gsdr.h"
@@ -40,8 +41,10 @@ class SharedTrackingPool
 public:
     // window_calls: the ring window in vector lengths (the ring holds twice that);
     // batch_calls: vector lengths of new items per advance launch
+    // ring_key: the input stream's DeviceIqRing key (pools of one key read one stream)
     SharedTrackingPool(const Dll_Pll_Conf& conf, int32_t signal, uint32_t max_channels, int device,
-        uint32_t window_calls = kDefaultWindowCalls, uint32_t batch_calls = kDefaultBatchCalls);
+        uint32_t window_calls = kDefaultWindowCalls, uint32_t batch_calls = kDefaultBatchCalls,
+        const std::string& ring_key = "rf0");
     static constexpr uint32_t kDefaultWindowCalls = 64;
     static constexpr uint32_t kDefaultBatchCalls = 8;
     ~SharedTrackingPool();
@@ -52,7 +55,7 @@ public:
     // rest while any holds it (GNSSBlockFactory builds one block per channel)
     static std::shared_ptr<SharedTrackingPool> get(const std::string& key, const Dll_Pll_Conf& conf, int32_t signal,
         uint32_t max_channels, int device, uint32_t window_calls = kDefaultWindowCalls,
-        uint32_t batch_calls = kDefaultBatchCalls);
+        uint32_t batch_calls = kDefaultBatchCalls, const std::string& ring_key = "rf0");
 
     int acquire_slot();  // -1 when every slot is taken
     void release_slot(int slot);
@@ -63,43 +66,51 @@ public:
     void stop(int slot);
     // a telemetry fault on `slot` (gsdr_trk_force_loss_of_lock)
     void force_loss_of_lock(int slot);
-    // input items [nitems_read, nitems_read + n): the part the ring has not seen is
-    // pushed, with an advance of every started channel after each window/2 items
+    // input items [nitems_read, nitems_read + n): the part the GPU's shared ring
+    // (DeviceIqRing) has not seen is pushed; every pool on the ring advances its
+    // started channels whenever half its window arrived since its last advance
     void feed(const void* in, uint64_t nitems_read, int n);
-    // an advance launch when batch_calls vector lengths arrived since the last one
-    // (force: when anything arrived)
+    // an advance launch when batch_calls vector lengths arrived since the last one,
+    // asynchronous: its records land in the queues when a later call finds it done
+    // (force: when anything arrived, and wait for the records)
     void advance_if_due(bool force);
     // the next per-call record of `slot` (in call order), left in the queue by peek
     bool peek(int slot, gsdr_trk_epoch* rec);
     void drop(int slot);
 
-    size_t item_bytes() const { return d_item_bytes; }
     uint64_t launches() const { return d_launches; }
-    uint64_t pushed() const { return d_head - d_origin; }
     uint64_t window_items() const { return d_window; }
+    DeviceIqRing* ring() const { return d_ring.get(); }
     uint64_t batch_items() const { return d_batch; }
 
 private:
-    void advance_locked();
+    void advance_locked(uint64_t head, bool wait);
+    bool take_locked(bool wait);  // the submission in flight -> the queues (false: not landed)
+    void on_pushed(uint64_t from, uint64_t head);  // the ring's hook
 
     Dll_Pll_Conf d_conf;
     int32_t d_signal;
     uint32_t d_max;
     int d_device;
-    size_t d_item_bytes{8};
     uint64_t d_window{0};
     uint64_t d_batch{0};
     gsdr_trk* d_engine{nullptr};
-    gsdr_stream* d_ring{nullptr};
-    bool d_started{false};
-    uint64_t d_origin{0}, d_head{0};
-    uint64_t d_advanced{0};  // the head at the last advance
+    std::shared_ptr<DeviceIqRing> d_ring;
+    int d_hook{-1};
+    bool d_seen{false};      // d_advanced holds a ring head
+    uint64_t d_advanced{0};  // the ring head at the last advance
     uint64_t d_launches{0};
     std::vector<bool> d_used;
     std::vector<bool> d_active;
     std::vector<std::deque<gsdr_trk_epoch>> d_queue;
     std::vector<gsdr_trk_epoch> d_recs;
     std::vector<uint32_t> d_n;
+    std::vector<uint32_t> d_gen;      // per slot: bumped by start / stop / release
+    std::vector<uint32_t> d_sub_gen;  // d_gen when the submission in flight was made
+    uint32_t d_epochs{0};             // calls per channel per submission
+    bool d_pending{false};            // a submission in flight (gsdr_trk_submit_stream)
+    bool d_more{false};               // the last one filled a channel's batch
+    bool d_sync{false};               // GSDR_POOL_SYNC: every advance waits (A/B)
     std::mutex d_mu;
 };
 
@@ -107,10 +118,11 @@ class dll_pll_veml_tracking_pool_mi355x : public TrackingBlockMI355X
 {
 public:
     // pool_key: the pool's registry key (the adapters use role + device);
-    // window_calls / batch_calls: <role>.mi355x_pool_window / .mi355x_pool_batch
+    // window_calls / batch_calls: <role>.mi355x_pool_window / .mi355x_pool_batch;
+    // ring_key: <role>.mi355x_ring, the input stream's shared device ring
     dll_pll_veml_tracking_pool_mi355x(const Dll_Pll_Conf& conf, int32_t signal, uint32_t pool_channels, int device,
         const std::string& pool_key, uint32_t window_calls = SharedTrackingPool::kDefaultWindowCalls,
-        uint32_t batch_calls = SharedTrackingPool::kDefaultBatchCalls);
+        uint32_t batch_calls = SharedTrackingPool::kDefaultBatchCalls, const std::string& ring_key = "rf0");
     ~dll_pll_veml_tracking_pool_mi355x() override;
 
     void set_gnss_synchro(Gnss_Synchro* p_gnss_synchro) override;

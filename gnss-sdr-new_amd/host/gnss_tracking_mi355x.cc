@@ -37,9 +37,13 @@ void DllPllTrackingAdapterMI355X::make_block(const ConfigurationInterface* confi
         static_cast<int>(SharedTrackingPool::kDefaultWindowCalls));
     const int batch = configuration->property(role_ + ".mi355x_pool_batch",
         static_cast<int>(SharedTrackingPool::kDefaultBatchCalls));
+    // the input stream's shared device ring: roles naming the same ring read the same
+    // conditioner output (a multi-constellation receiver on one front end names one
+    // ring for all its signals, so the stream crosses PCIe once); default: the role's own
+    const std::string ring = configuration->property(role_ + ".mi355x_ring", role_);
     tracking_ = std::make_unique<dll_pll_veml_tracking_pool_mi355x>(trk_params_, signal,
         static_cast<uint32_t>(slots > 0 ? slots : 32), device, role_, static_cast<uint32_t>(window),
-        static_cast<uint32_t>(batch));
+        static_cast<uint32_t>(batch), ring);
 }
 
 // gps_l1_ca_dll_pll_tracking.cc:34-91

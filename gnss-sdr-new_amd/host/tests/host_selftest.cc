@@ -1454,6 +1454,40 @@ void test_pool_overrun()
     EXPECT(b->state() == 0, "pool failing feed: the slot stays stopped");
 }
 
+// The shared device ring of an input stream (DeviceIqRing): one ring per key, shared
+// by the pools of every role that names it, and two input streams under one key
+// refused on the first overlapping feed.
+void test_ring_keys()
+{
+    const auto r1 = DeviceIqRing::get(0, GSDR_ITEM_GR_COMPLEX, 1 << 16, "selftest_a");
+    const auto r2 = DeviceIqRing::get(0, GSDR_ITEM_GR_COMPLEX, 1 << 16, "selftest_a");
+    const auto r3 = DeviceIqRing::get(0, GSDR_ITEM_GR_COMPLEX, 1 << 16, "selftest_b");
+    EXPECT(r1 == r2 && r1 != r3, "ring keys: one ring per key, shared by its consumers");
+    std::vector<std::complex<float>> a(8000), b(8000);
+    for (size_t i = 0; i < a.size(); ++i)
+        {
+            a[i] = {static_cast<float>(i), 1.0F};
+            b[i] = {static_cast<float>(i), 2.0F};
+        }
+    uint64_t head = 0;
+    r1->feed(a.data(), 0, 4000);
+    r2->feed(a.data(), 0, 6000);  // the same stream, further: pushes [4000, 6000)
+    EXPECT(r1->head(&head) && head == 6000, "ring keys: a second feeder of the same stream pushes only what is new");
+    bool refused = false;
+    try
+        {
+            r2->feed(b.data(), 0, 8000);  // another stream under the same key
+        }
+    catch (const std::logic_error&)
+        {
+            refused = true;
+        }
+    EXPECT(refused && r1->head(&head) && head == 6000, "ring keys: a different stream under the same key is refused");
+    r3->feed(b.data(), 0, 8000);
+    EXPECT(r3->head(&head) && head == 8000, "ring keys: another key is another stream");
+    std::printf("ring keys: shared ring per key, mismatching feeder refused\n");
+}
+
 // Gnss_Synchro emission of both tracking blocks (dll_pll_veml_tracking.cc:1784-2152)
 // on a GPS channel driven past bit synchronisation, with GnssTime "timetag" input
 // tags every 100 ms and a telemetry fault (msg_handler_telemetry_to_trk, :614-637)
@@ -1709,6 +1743,7 @@ int main(int argc, char** argv)
     test_flag_overrides();
     test_pooled_tracking();
     test_pool_overrun();
+    test_ring_keys();
     {
         const char* d = std::getenv("GSDR_SELFTEST_DUMP_DIR");
         test_synchro_emission(d ? std::string(d) : std::string("/tmp/gsdr_selftest_dump"));

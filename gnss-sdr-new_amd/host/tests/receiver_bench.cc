@@ -6,9 +6,13 @@
 // tracks (each answer re-arms the request, as a receiver's idle channels keep
 // searching).  The reference's shape: gnss_flowgraph.cc:1007-1135 (one tracking and
 // one acquisition block per channel over the conditioner output).
-//   receiver_bench c3|c5 [seconds] [search]
+//   receiver_bench c3|c5 [seconds] [search] [pinned]
 // search 1 (default): the acquisition services search every untracked PRN of GPS
 // and Galileo and BeiDou PRNs up to 32 on every block; 0: the tracking blocks only.
+// pinned 1 (default): the host sample buffer is page-locked (gsdr_host_register), as
+// a flowgraph's buffers would be for DMA; 0: pageable (a staging copy per push).
+// Every consumer reads the GPU's one shared ring (DeviceIqRing, key "rf0"): each stretch of the
+// stream crosses PCIe once.
 // C3: GPS L1 C/A at 16 Msps, 12 tracked channels; C5: one GPU's share of the 25 Msps
 // hybrid job, 12 GPS L1 C/A + 12 Galileo E1 (pilot) + 8 BeiDou B1I channels.
 // Prints one JSON line: stream Msps through the whole receiver path (host loop,
@@ -23,6 +27,7 @@
 #include <vector>
 
 #include "acquisition_service.h"
+#include "device_iq_ring.h"
 #include "gnss_block_factory_mi355x.h"
 #include "gnss_replicas.h"
 #include "gnss_tracking_mi355x.h"
@@ -61,6 +66,7 @@ int main(int argc, char** argv)
     // dll_pll_veml_tracking.cc:1797), then bit / secondary-code sync and outputs
     const double seconds = argc > 2 ? std::atof(argv[2]) : 1.6;
     const bool search = argc > 3 ? std::atoi(argv[3]) != 0 : true;
+    const bool pinned = argc > 4 ? std::atoi(argv[4]) != 0 : true;
     std::vector<Sig> sigs = {{"1C", "GPS_L1_CA_DLL_PLL_Tracking_MI355X", "GPS_L1_CA_PCPS_Acquisition_MI355X", 'G', '1',
         'C', 12, 32, 1.023e6, 1575.42e6, 1}};
     if (c5)
@@ -125,6 +131,7 @@ int main(int argc, char** argv)
             const std::string t = std::string("Tracking_") + s.role, a = std::string("Acquisition_") + s.role;
             config.set_property(t + ".implementation", s.impl_trk);
             config.set_property(t + ".item_type", "gr_complex");
+            config.set_property(t + ".mi355x_ring", "rf0");  // every signal reads the one front end
             config.set_property(t + ".pll_bw_hz", s.sys == 'G' ? "40.0" : "15.0");
             config.set_property(t + ".dll_bw_hz", s.sys == 'G' ? "4.0" : "1.0");
             config.set_property(t + ".pull_in_time_s", "0");
@@ -192,11 +199,14 @@ int main(int argc, char** argv)
         }
     // acquisition services on the device ring: every untracked PRN of each signal,
     // re-armed after each answer
-    gsdr_stream* ring = nullptr;
+    // the GPU's shared ring (the pooled tracking blocks' too): the bench pushes the
+    // stream into it, the pools' hooks keep their channels inside its window
     const uint64_t per_max = static_cast<uint64_t>(fs * 4 / 1000);
-    if (gsdr_stream_create(0, GSDR_ITEM_GR_COMPLEX, 16 * per_max, 8 * per_max, &ring) != GSDR_OK)
+    const auto hub = DeviceIqRing::get(0, GSDR_ITEM_GR_COMPLEX, 8 * per_max, "rf0");
+    gsdr_stream* ring = hub->stream();
+    if (pinned && gsdr_host_register(const_cast<std::complex<float>*>(x.data()), x.size() * sizeof(x[0])) != GSDR_OK)
         {
-            std::fprintf(stderr, "ring: %s\n", gsdr_last_error());
+            std::fprintf(stderr, "pin: %s\n", gsdr_last_error());
             return 1;
         }
     std::vector<std::unique_ptr<AcquisitionService>> svcs;
@@ -260,11 +270,7 @@ int main(int argc, char** argv)
             if (pushed < n)
                 {
                     const size_t m = std::min(chunk, n - pushed);
-                    if (gsdr_stream_push(ring, x.data() + pushed, pushed, m) != GSDR_OK)
-                        {
-                            std::fprintf(stderr, "push: %s\n", gsdr_last_error());
-                            return 1;
-                        }
+                    hub->feed(x.data() + pushed, pushed, static_cast<int>(m));
                     pushed += m;
                     progress = true;
                     for (auto& s : svcs)
@@ -336,12 +342,12 @@ int main(int argc, char** argv)
     std::printf("{\"config\": \"%s\", \"search\": %d, \"path\": \"factory-built pooled TrackingInterface blocks (work() per block at its "
                 "nitems_read, batched advances) + AcquisitionService grids on the device IQ ring (batched, asynchronous), host "
                 "pushes of %zu-item chunks\", "
-                "\"fs_sps\": %.0f, \"samples\": %zu, \"seconds\": %.4f, \"msps\": %.2f, \"real_time_factor\": %.2f, "
+                "\"host_buffer\": \"%s\", \"fs_sps\": %.0f, \"samples\": %zu, \"seconds\": %.4f, \"msps\": %.2f, \"real_time_factor\": %.2f, "
                 "\"tracking_channels\": %zu, \"trk_work_calls\": %llu, \"signals\": {%s}}\n",
-        cfg.c_str(), search ? 1 : 0, chunk, fs, n, sec, n / sec / 1e6, n / sec / fs, chans.size(),
+        cfg.c_str(), search ? 1 : 0, chunk, pinned ? "pinned" : "pageable", fs, n, sec, n / sec / 1e6, n / sec / fs, chans.size(),
         static_cast<unsigned long long>(trk_calls), per_sig.c_str());
     chans.clear();
     svcs.clear();
-    gsdr_stream_destroy(ring);
+    if (pinned) gsdr_host_unregister(const_cast<std::complex<float>*>(x.data()));
     return 0;
 }

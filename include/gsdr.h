@@ -65,6 +65,12 @@ const char* gsdr_last_error(void);
 int gsdr_abi_version(void);
 /* Number of HIP devices visible to this process. */
 int gsdr_device_count(int* count);
+/* Page-lock a host buffer (the flowgraph's sample buffer upstream of the blocks) so
+ * gsdr_stream_push / the host-input calls copy it to HBM by DMA without a staging
+ * copy; gsdr_host_unregister before the buffer is freed.  No reference counterpart
+ * (GNU Radio buffers are pageable; gr-cuda style custom buffers would pin them). */
+int gsdr_host_register(void* ptr, size_t bytes);
+int gsdr_host_unregister(void* ptr);
 
 /* ======================================================================== */
 /* Device IQ ring indexed by absolute sample count                           */
@@ -549,6 +555,18 @@ int gsdr_trk_run_stream(gsdr_trk* trk, gsdr_stream* ring, uint32_t max_epochs, g
  * handle's own stream and record buffers): the tracking pool service's call. */
 int gsdr_trk_run_stream_host(gsdr_trk* trk, gsdr_stream* ring, uint32_t max_epochs, gsdr_trk_epoch* out_host,
     uint32_t* n_out_host);
+
+/* Asynchronous ring form for a host consumer (the pooled tracking blocks of
+ * dll_pll_veml_tracking_pool_mi355x, which replace the per-channel general_work
+ * round trips of dll_pll_veml_tracking.cc:1784-2152): gsdr_trk_run_stream on the
+ * handle's stream into the handle's own submission buffers, the records and counts
+ * copied into pinned host memory behind it; returns without waiting.  One submission
+ * at a time.  gsdr_trk_collect copies them out: out_host holds max_channels *
+ * max_epochs records (channel-major), n_out_host max_channels counts, *max_epochs
+ * (may be NULL) the submission's max_epochs; wait != 0 waits for the copy, wait == 0
+ * returns 1 without copying while it is in flight. */
+int gsdr_trk_submit_stream(gsdr_trk* trk, gsdr_stream* ring, uint32_t max_epochs);
+int gsdr_trk_collect(gsdr_trk* trk, int wait, gsdr_trk_epoch* out_host, uint32_t* n_out_host, uint32_t* max_epochs);
 
 /* Host form of the same call (synchronous): copies the records back. */
 int gsdr_trk_run(gsdr_trk* trk, const void* iq_host, uint64_t iq_first_sample, uint64_t iq_items,

@@ -261,3 +261,54 @@ def test_async_window_blocks_overwrite():
         th.join()
     ring.close()
     acq.close()
+
+
+def test_submit_collect_matches_contiguous():
+    """gsdr_trk_submit_stream / gsdr_trk_collect (the pooled tracking blocks' advance):
+    a submission in flight while the next stretch is pushed (the push waits on its
+    reader event before overwriting), polled without waiting, gives records
+    identical to one contiguous gsdr_trk_run; collect without a submission and a
+    second submission before the collect are refused."""
+    ms = 120
+    sats = synth.random_constellation(4, seed_offset=37)
+    x = synth.gps_l1_iq(FS, ms * N, sats, seed_offset=37)
+    ref = gsdr.Tracking(_conf(len(sats)))
+    t = gsdr.Tracking(_conf(len(sats)))
+    for c, s in enumerate(sats):
+        d, f = _acq_result(s)
+        ref.start(c, s.prn, synth.gps_ca_chips(s.prn), d, f, 0, 0)
+        t.start(c, s.prn, synth.gps_ca_chips(s.prn), d, f, 0, 0)
+    ref_recs, ref_n = ref.run(x, 0, ms + 2)
+    ring = gsdr.Stream(gsdr.ITEM_GR_COMPLEX, capacity_items=32 * N, max_window_items=16 * N)
+    t._sub_epochs = 1
+    with pytest.raises(gsdr.GsdrError):
+        t.collect()
+    got = [[] for _ in sats]
+
+    def take(res):
+        rec, n = res
+        for c in range(len(sats)):
+            got[c].extend(rec[c, :n[c]].copy())
+
+    pushed, pending, polls = 0, False, 0
+    while pushed < ms * N:
+        ring.push(x[pushed:pushed + 4 * N], pushed)
+        pushed += 4 * N
+        if pending:
+            res = t.collect(wait=False)
+            polls += res is None
+            if res is None:
+                res = t.collect(wait=True)
+            take(res)
+        t.submit_stream(ring, 18)
+        pending = True
+        if pushed == 8 * N:
+            with pytest.raises(gsdr.GsdrError):
+                t.submit_stream(ring, 18)
+    take(t.collect(wait=True))
+    for c in range(len(sats)):
+        g = np.array(got[c], dtype=gsdr.TRK_EPOCH_DTYPE)
+        r = ref_recs[c, :ref_n[c]]
+        assert len(g) == len(r) and len(g) >= ms - 2, (c, len(g), len(r))
+        assert g.tobytes() == r.tobytes(), c
+    ring.close()

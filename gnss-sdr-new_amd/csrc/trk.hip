@@ -61,8 +61,8 @@ constexpr int kWinCore = kSpl * kTrkThreads;  // 4096: the next call's window st
 constexpr int kHalo = 16;                     // slack around the predicted next start
 constexpr int kStreamRow = 64 * 16;           // bytes one wave's global_load_lds_dwordx4 writes
 constexpr int kCodeMargin = 32;              // replica samples copied on each side of the LDS replica
-constexpr int kTimingSlots = 9;              // GSDR_TRK_TIMING record per call: 8 stamps + stream-wait ticks
-constexpr int kStampSlots = 8;
+constexpr int kTimingSlots = 11;             // GSDR_TRK_TIMING record per call: 10 stamps + stream-wait ticks
+constexpr int kStampSlots = 10;
 
 // MATH_CONSTANTS.h:47-50
 constexpr double kGnssPi = 3.1415926535898;
@@ -1648,6 +1648,8 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
             if (wave == 0)
                 {
                     TrkHot t = s_t;
+                    uint64_t tmA = 0;
+                    if (timing) tmA = wall_clock64();
                     float2 taps[kMaxTrkTaps + 1], epl[3];
                     tap_totals(taps, epl);
                     const uint64_t n_read = t.next_sample;
@@ -1719,12 +1721,13 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                                     tr[0] = tm0;
                                     tr[1] = tm1;
                                     tr[2] = tm2;
-                                    tr[3] = tm3;
-                                    tr[4] = pr[0] ? pr[0] : tm3;
-                                    tr[5] = pr[1] ? pr[1] : tr[4];
-                                    tr[6] = pr[2] ? pr[2] : tr[5];
-                                    tr[7] = wall_clock64();
-                                    tr[8] = swait;
+                                    tr[3] = tmA;
+                                    tr[4] = tm3;
+                                    tr[5] = pr[0] ? pr[0] : tm3;
+                                    tr[6] = pr[1] ? pr[1] : tr[5];
+                                    tr[7] = pr[2] ? pr[2] : tr[6];
+                                    tr[8] = wall_clock64();
+                                    tr[10] = swait;
                                 }
                         }
                     t.next_sample = n_read + (uint64_t)(int64_t)t.current_prn_length_samples;
@@ -1734,6 +1737,7 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                     const Prep pn = make_prep(c, t, e + 1 < max_epochs, iq_first, iq_items, vl, K, L, use_window, streamed,
                         stream_chunk, use_window ? nb : win_base, streamed ? nb : pf_first);
                     if (lane == 0) prep = pn;
+                    if (timing && lane == 0) timing[((size_t)ch * max_epochs + e) * kTimingSlots + 9] = wall_clock64();
                 }
             if (use_window) win_base = nb;
             // the next iteration's prep barrier orders the window writes and s_red reuse
@@ -2252,8 +2256,8 @@ void gsdr_trk_destroy(gsdr_trk* k)
         }
     if (k->timing_on && k->tcount)
         {
-            static const char* names[kTimingSlots] = {"prep", "correlate", "tap-sum", "cn0-lock", "dll-pll", "update-vars",
-                "rest", "window-write", "(correlate's stream-wait)"};
+            static const char* names[kTimingSlots] = {"prep", "correlate", "state-load", "tap-sum", "cn0-lock", "dll-pll",
+                "update-vars", "rest", "next-plan", "loop-top", "(correlate's stream-wait)"};
             std::fprintf(stderr, "gsdr_trk timing: %llu calls, %s ticks per call:", (unsigned long long)k->tcount,
                 "wall_clock64 (100 MHz)");
             for (int q = 0; q < kTimingSlots; ++q) std::fprintf(stderr, " %s %.0f", names[q], k->tsum[q] / k->tcount);

@@ -669,13 +669,12 @@ __global__ void __launch_bounds__(MP::NT) __attribute__((amdgpu_waves_per_eu(WPE
 // acq_argmax_pk_kernel recomputes the selected row on the full-LDS plan for the
 // first-maximum index and the exact peak.
 // Row layouts in LDS: row rw at rw * stride, element e at e + (e / S) * P -- one
-// pad of P elements every S, so the strided Stockham writes spread over the banks.
+// pad of P elements every S, so strided Stockham writes could spread over the banks.
 // The stage functions need S | Ns (writes) and S | L/R (reads) so every address
-// is a per-butterfly base plus a compile-time offset.  Pads chosen with an LDS
-// bank model (ds_write_b64: 4 x 16 lanes, ds_read_b64: 2 x 32 lanes; see
-// MI355X_MICROARCH.md LDS): for L = 1000, radix 10, the buffers written by the
-// first and second row stages pad (S, P) = (10, 1) and (50, 3) -- 25 % fewer LDS
-// cycles than the plain layout.
+// is a per-butterfly base plus a compile-time offset.  Pads chosen with an LDS bank
+// model halved the measured bank conflicts of the 1000-point rows (0.30 -> 0.15 of
+// the LDS-active cycles) and left the time unchanged -- the rows are VALU-issue bound
+// (profiles/r05p) -- so every plan runs unpadded (NoPads).
 template <int L, int S, int P>
 struct RowPad
 {
@@ -764,31 +763,6 @@ struct NoPads
 {
     template <int I>
     using layout = RowPad<L, 0, 0>;
-};
-
-// The bank-model pads of the 10 x 10 x 10 row plan: the buffers the
-// first and second row stages write hold one pad element every 10 / 3 every 50,
-// so stage 1's stride-10 writes (22-dword lane stride) and stage 2's writes
-// spread over the LDS banks.
-struct Pads1000
-{
-    template <int I>
-    using layout = std::conditional_t<I == 1, RowPad<1000, 10, 1>,
-        std::conditional_t<I == 2, RowPad<1000, 50, 3>, RowPad<1000, 0, 0>>>;
-};
-
-// Pads of the 10 x 10 x 10 row plan for workgroup-wide rows (RegFourStep H > 0, the
-// 25000-point split plan's 5 rows per round): stage 1's stride-10 writes go to a
-// buffer with one pad element every 10 (22-dword lane stride, conflict-free 16-lane
-// write groups), stage 2's to one with 6 every 100 (its 100-element row blocks shift
-// by 12 dwords).  Bank model (MI355X_MICROARCH.md LDS, ds_write_b64 4 x 16 lanes mod
-// 32, ds_read_b64 2 x 32 lanes mod 64) over the three stages of 5 rows on 512 lanes:
-// conflict cycles 43 % -> 15 % of the LDS-array cycles, LDS time -18 %.
-struct Pads25k
-{
-    template <int I>
-    using layout = std::conditional_t<I == 1, RowPad<1000, 10, 1>,
-        std::conditional_t<I == 2, RowPad<1000, 100, 6>, RowPad<1000, 0, 0>>>;
 };
 
 // ---- wave-local row transforms

@@ -47,7 +47,6 @@ SharedTrackingPool::SharedTrackingPool(const Dll_Pll_Conf& conf, int32_t signal,
     // one submission covers every call a channel can have in the ring: a channel is
     // advanced whenever half a window arrived, so it never lags the head by more
     d_epochs = window_calls + 2;
-    d_sync = std::getenv("GSDR_POOL_SYNC") != nullptr;  // A/B: wait for every advance
     d_queue.resize(max_channels);
     d_n.assign(max_channels, 0);
     d_hook = d_ring->add_hook([this](uint64_t from, uint64_t head) { on_pushed(from, head); });
@@ -184,7 +183,7 @@ void SharedTrackingPool::advance_locked(uint64_t head, bool wait)
             d_sub_gen = d_gen;
             ++d_launches;
             d_advanced = head;
-            if (!wait && !d_sync) return;
+            if (!wait) return;
             take_locked(true);
             if (!d_more) return;
         }

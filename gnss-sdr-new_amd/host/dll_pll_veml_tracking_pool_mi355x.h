@@ -110,7 +110,6 @@ private:
     uint32_t d_epochs{0};             // calls per channel per submission
     bool d_pending{false};            // a submission in flight (gsdr_trk_submit_stream)
     bool d_more{false};               // the last one filled a channel's batch
-    bool d_sync{false};               // GSDR_POOL_SYNC: every advance waits (A/B)
     std::mutex d_mu;
 };
 

@@ -14,9 +14,7 @@ timeout -k 10 200 ./gnss-sdr-new_amd/build/receiver_bench c3 2 1 > "$OUT/receive
 timeout -k 10 200 ./gnss-sdr-new_amd/build/receiver_bench c3 2 0 > "$OUT/receiver_c3_s0.json" 2> "$OUT/receiver_c3_s0.err" &&
 timeout -k 10 300 ./gnss-sdr-new_amd/build/receiver_bench c5 2 1 > "$OUT/receiver_c5_s1.json" 2> "$OUT/receiver_c5_s1.err" &&
 timeout -k 10 300 ./gnss-sdr-new_amd/build/receiver_bench c5 2 0 > "$OUT/receiver_c5_s0.json" 2> "$OUT/receiver_c5_s0.err" &&
-timeout -k 10 300 ./gnss-sdr-new_amd/build/receiver_bench c5 2 0 0 > "$OUT/receiver_c5_s0_pageable.json" 2> "$OUT/receiver_c5_s0_pageable.err" &&
-GSDR_POOL_SYNC=1 timeout -k 10 300 ./gnss-sdr-new_amd/build/receiver_bench c3 2 0 > "$OUT/receiver_c3_s0_sync.json" 2> "$OUT/receiver_c3_s0_sync.err" &&
-GSDR_POOL_SYNC=1 timeout -k 10 300 ./gnss-sdr-new_amd/build/receiver_bench c5 2 0 > "$OUT/receiver_c5_s0_sync.json" 2> "$OUT/receiver_c5_s0_sync.err"
+timeout -k 10 300 ./gnss-sdr-new_amd/build/receiver_bench c5 2 0 0 > "$OUT/receiver_c5_s0_pageable.json" 2> "$OUT/receiver_c5_s0_pageable.err"
 rc=$?
 tail -5 "$OUT/pytest.txt"
 cat "$OUT"/receiver_*.json

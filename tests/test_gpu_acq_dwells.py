@@ -110,20 +110,16 @@ def test_bit_transition(pfa):
             assert res[b, i]["samplestamp"] == b * 2 * C
 
 
-@pytest.mark.parametrize("split", ["1", "0", "2", "id6", "id13", "id16", "id20"])
+@pytest.mark.parametrize("split", ["1", "0"])
 @pytest.mark.parametrize("pfa", [0.01, 0.0])
 def test_bit_transition_c4_four_step(monkeypatch, pfa, split):
     """Config C4's acquisition as the bench times it (pcps_acquisition.cc:85-92,
     :188-193, :671): Galileo E1 at 8 Msps, 4 ms code, bit_transition_flag -> FFT
     64000 with the code in the second half and outputs [32000, 64000), +-10 kHz /
-    250 Hz (80 bins): the split register four-step (default and GSDR_ACQ_SPLIT=2:
-    ROUT = 2 over a 32000-point register transform, row maxima of outputs k >= N/2;
-    id6: ROUT = 4 over 16000 points; id13 / id16 / id20: the wave-local-row plans,
-    acq_split.hip) and the general (dwell) path over the packed four-step
+    250 Hz (80 bins): the split register four-step (default: ROUT = 2 over a
+    32000-point wave-local-row register transform, row maxima of outputs k >= N/2,
+    acq_split.hip id 13) and the general (dwell) path over the packed four-step
     (GSDR_ACQ_SPLIT=0)."""
-    if split.startswith("id"):  # a forced split id of N = 64000 (acq_split.hip)
-        monkeypatch.setenv("GSDR_ACQ_SPLIT_ID", split[2:])
-        split = "2"
     monkeypatch.setenv("GSDR_ACQ_SPLIT", split)
     fs, C, dmax, dstep = 8000000, 32000, 10000, 250
     rng = np.random.default_rng(64)

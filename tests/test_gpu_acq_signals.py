@@ -82,39 +82,22 @@ def test_beidou_b1i_synthetic_batch(fs):
     assert set(vis) <= det
 
 
-# acq_split.hip split ids and their FFT sizes (5/6: 16000-based splits; 11-20: the
-# wave-local-row plans)
-SPLIT_IDS = {5: 32000, 6: 64000, 7: 25000, 8: 100000, 11: 25000, 12: 32000, 13: 64000, 14: 100000, 15: 32000, 16: 64000, 17: 25000,
-             18: 100000, 19: 32000, 20: 64000}
-
-
 LARGE_CONFIGS = [(8000000, 32000, 0.01), (25000000, 25000, 0.0), (8000000, 64000, 0.01), (25000000, 100000, 0.01),
                  (25000000, 25000, 0.01), (25000000, 100000, 0.0)]
 
 
 def _split_cases():
-    """Every configuration on the three modes, and on each forced split id of its N
-    (no cross-product cases that would only skip)."""
-    cases = []
-    for fs, n, pfa in LARGE_CONFIGS:
-        for split in ["1", "0", "2"] + ["id%d" % i for i, m in sorted(SPLIT_IDS.items()) if m == n]:
-            cases.append((fs, n, pfa, split))
-    return cases
+    """Every configuration on both correlate paths."""
+    return [(fs, n, pfa, split) for fs, n, pfa in LARGE_CONFIGS for split in ("1", "0")]
 
 
 @pytest.mark.parametrize("fs,N,pfa,split", _split_cases())
 def test_large_fft_four_step(monkeypatch, fs, N, pfa, split):
     """N beyond one workgroup's LDS: Galileo E1 at 8 Msps (4 ms: 32000; 8 ms:
     64000), BeiDou B1I at 25 Msps (1 ms: 25000), Galileo at 25 Msps (100000) --
-    configs C4/C5 -- on every correlate path: GSDR_ACQ_SPLIT=1 (default: the split
-    register four-step for 25000 / 32000 / 64000 / 100000 = 4 x 25000), 0 (the packed
-    four-step everywhere), 2 (also the wave-local 100000 plans when forced),
-    idK: split id K forced (SPLIT_IDS: the 16000-based splits and the wave-local-row plans).
-    Parity with the oracle grid statistics."""
-    if split.startswith("id"):
-        # a forced split of this N (acq_split.hip: 5 = 2 x 16000, 6 = 4 x 16000)
-        monkeypatch.setenv("GSDR_ACQ_SPLIT_ID", split[2:])
-        split = "2"
+    configs C4/C5 -- on both correlate paths: GSDR_ACQ_SPLIT=1 (default: the split
+    register four-step for 25000 / 32000 / 64000 / 100000 = 4 x 25000) and 0 (the
+    packed four-step everywhere).  Parity with the oracle grid statistics."""
     monkeypatch.setenv("GSDR_ACQ_SPLIT", split)
     dmax, dstep = 2000, 500
     rng = np.random.default_rng(N)

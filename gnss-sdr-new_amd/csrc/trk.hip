@@ -1028,8 +1028,8 @@ __device__ __forceinline__ int floor_i(float x)
     return r;
 }
 
-// One correlation chunk of kSpl samples per lane (n = n0 + tid + j*kTrkThreads),
-// KT taps, no branches inside.  FULL: every sample of the chunk lies inside the
+// One correlation chunk of SPL (<= kSpl) samples per lane (n = n0 + tid +
+// j*kTrkThreads), KT taps, no branches inside.  FULL: every sample of the chunk lies inside the
 // call; otherwise samples past the end are zero and their index clamped.
 // WRAP: 2 = every code index of the call lies in [-kCodeMargin, L + kCodeMargin),
 // read straight from the margin-padded replica; 1 = in [-L, 2L), one conditional
@@ -1038,16 +1038,16 @@ __device__ __forceinline__ int floor_i(float x)
 // DATA: one more accumulator, acc[kMaxTrkTaps], on the data-component replica
 // s_data at the prompt tap's index (the pilot-tracking data correlator of
 // do_correlation_step, whose only tap sits at the prompt shift).
-template <int IT, int SRC, int WRAP, bool FULL, int KT, bool DATA>
+template <int IT, int SRC, int WRAP, bool FULL, int KT, bool DATA, int SPL = kSpl>
 __device__ __forceinline__ void correlate_chunk(const void* __restrict__ iq, const float2* s_win, const float* s_code,
     const float* s_data, const Prep& p, int n0, int vl, int L, const float (&sh_rem)[kMaxTrkTaps], float2& ph,
     float2 (&acc)[kMaxTrkTaps + 1], const char* sbuf = nullptr, int sboff = 0)
 {
     using gsdr::pk::c2;
     constexpr int IPK = KT / 2;  // prompt slot: 1 of E,P,L / 2 of VE,E,P,L,VL
-    c2 xs[kSpl];
+    c2 xs[SPL];
 #pragma unroll
-    for (int j = 0; j < kSpl; ++j)
+    for (int j = 0; j < SPL; ++j)
         {
             const int n = n0 + (int)threadIdx.x + j * kTrkThreads;
             const int nc = FULL ? n : min(n, vl - 1);
@@ -1061,13 +1061,13 @@ __device__ __forceinline__ void correlate_chunk(const void* __restrict__ iq, con
             xs[j] = (FULL || n < vl) ? gsdr::pk::from(v) : c2{0.f, 0.f};
         }
     // Three phases -- every replica index, then every replica gather, then the
-    // FMAs -- so the chunk's kSpl*KT LDS gathers are in flight together; written
+    // FMAs -- so the chunk's SPL*KT LDS gathers are in flight together; written
     // as one loop the scheduler issued them one at a time, each behind its own
     // lgkmcnt(0) wait.  The FMA order per accumulator is unchanged.
-    float cv[kSpl][KT];
-    float dv[kSpl];
+    float cv[SPL][KT];
+    float dv[SPL];
 #pragma unroll
-    for (int j = 0; j < kSpl; ++j)
+    for (int j = 0; j < SPL; ++j)
         {
             const int n0j = n0 + (int)threadIdx.x + j * kTrkThreads;
             const int n = FULL ? n0j : min(n0j, vl - 1);
@@ -1088,7 +1088,7 @@ __device__ __forceinline__ void correlate_chunk(const void* __restrict__ iq, con
                 }
         }
 #pragma unroll
-    for (int j = 0; j < kSpl; ++j)
+    for (int j = 0; j < SPL; ++j)
         {
             if (DATA) dv[j] = s_data[__float_as_int(cv[j][IPK])];
 #pragma unroll
@@ -1100,7 +1100,7 @@ __device__ __forceinline__ void correlate_chunk(const void* __restrict__ iq, con
     c2 phv = gsdr::pk::from(ph);
     const c2 ws = gsdr::pk::from(p.wstep);
 #pragma unroll
-    for (int j = 0; j < kSpl; ++j)
+    for (int j = 0; j < SPL; ++j)
         {
             const c2 tt = gsdr::pk::mul(xs[j], phv);
 #pragma unroll
@@ -1117,22 +1117,46 @@ __device__ __forceinline__ void correlate_chunk(const void* __restrict__ iq, con
 }
 
 // the chunk at n0 with the call's wrap mode; FULL when the whole chunk is inside the call
+template <int IT, int SRC, int KT, bool DATA, int SPL>
+__device__ __forceinline__ void correlate_chunk_wrap(const void* __restrict__ iq, const float2* s_win, const float* s_code,
+    const float* s_data, const Prep& p, int n0, int vl, int L, const float (&sh_rem)[kMaxTrkTaps], float2& ph,
+    float2 (&acc)[kMaxTrkTaps + 1], const char* sbuf, int sboff)
+{
+    if (p.wrap == 2)
+        {
+            if (SPL == kSpl && n0 + kWinCore <= vl)
+                correlate_chunk<IT, SRC, 2, true, KT, DATA, SPL>(iq, s_win, s_code, s_data, p, n0, vl, L, sh_rem, ph, acc,
+                    sbuf, sboff);
+            else
+                correlate_chunk<IT, SRC, 2, false, KT, DATA, SPL>(iq, s_win, s_code, s_data, p, n0, vl, L, sh_rem, ph, acc,
+                    sbuf, sboff);
+        }
+    else if (p.wrap == 1)
+        correlate_chunk<IT, SRC, 1, false, KT, DATA, SPL>(iq, s_win, s_code, s_data, p, n0, vl, L, sh_rem, ph, acc, sbuf,
+            sboff);
+    else
+        correlate_chunk<IT, SRC, 0, false, KT, DATA, SPL>(iq, s_win, s_code, s_data, p, n0, vl, L, sh_rem, ph, acc, sbuf,
+            sboff);
+}
+
+// A call's last chunk that holds fewer than kWinCore samples runs with as few
+// samples per lane as cover it (1, 2, 4 or kSpl): a 25000-sample call's last 424
+// samples take one sample per lane instead of a full chunk of masked ones.  The
+// samples and their order are those of the full chunk (a masked sample adds 0).
 template <int IT, int SRC, int KT, bool DATA>
 __device__ __forceinline__ void correlate_chunk_any(const void* __restrict__ iq, const float2* s_win, const float* s_code,
     const float* s_data, const Prep& p, int n0, int vl, int L, const float (&sh_rem)[kMaxTrkTaps], float2& ph,
     float2 (&acc)[kMaxTrkTaps + 1], const char* sbuf = nullptr, int sboff = 0)
 {
-    if (p.wrap == 2)
-        {
-            if (n0 + kWinCore <= vl)
-                correlate_chunk<IT, SRC, 2, true, KT, DATA>(iq, s_win, s_code, s_data, p, n0, vl, L, sh_rem, ph, acc, sbuf, sboff);
-            else
-                correlate_chunk<IT, SRC, 2, false, KT, DATA>(iq, s_win, s_code, s_data, p, n0, vl, L, sh_rem, ph, acc, sbuf, sboff);
-        }
-    else if (p.wrap == 1)
-        correlate_chunk<IT, SRC, 1, false, KT, DATA>(iq, s_win, s_code, s_data, p, n0, vl, L, sh_rem, ph, acc, sbuf, sboff);
+    const int rest = vl - n0;
+    if (rest >= kWinCore || rest > 4 * kTrkThreads || kSpl <= 4)
+        correlate_chunk_wrap<IT, SRC, KT, DATA, kSpl>(iq, s_win, s_code, s_data, p, n0, vl, L, sh_rem, ph, acc, sbuf, sboff);
+    else if (rest > 2 * kTrkThreads)
+        correlate_chunk_wrap<IT, SRC, KT, DATA, 4>(iq, s_win, s_code, s_data, p, n0, vl, L, sh_rem, ph, acc, sbuf, sboff);
+    else if (rest > kTrkThreads)
+        correlate_chunk_wrap<IT, SRC, KT, DATA, 2>(iq, s_win, s_code, s_data, p, n0, vl, L, sh_rem, ph, acc, sbuf, sboff);
     else
-        correlate_chunk<IT, SRC, 0, false, KT, DATA>(iq, s_win, s_code, s_data, p, n0, vl, L, sh_rem, ph, acc, sbuf, sboff);
+        correlate_chunk_wrap<IT, SRC, KT, DATA, 1>(iq, s_win, s_code, s_data, p, n0, vl, L, sh_rem, ph, acc, sbuf, sboff);
 }
 
 // high_dyn correlation (do_correlation_step with set_high_dynamics_resampler(true)):

@@ -23,8 +23,6 @@
 // the CPU restatement (oracle/trk_oracle.c) to fp rounding.
 #include <hip/hip_runtime.h>
 
-#include <atomic>
-
 #include <algorithm>
 #include <cmath>
 #include <cstddef>
@@ -1357,7 +1355,7 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
     TrkChan* __restrict__ chans, const float* const* __restrict__ codes, const float* const* __restrict__ data_codes,
     const void* __restrict__ iq, uint64_t iq_first, uint64_t iq_items, uint32_t max_epochs, gsdr_trk_epoch* __restrict__ out,
     uint32_t* __restrict__ nout, int code_pad, int data_pad, uint64_t* __restrict__ timing, int timing_wall, int stream_chunk,
-    int sbuf_bytes, int xcd_sel)
+    int sbuf_bytes)
 {
     // LDS: [replica | data replica (pilot tracking) | next call's input window]
     extern __shared__ float s_dyn[];
@@ -1384,16 +1382,7 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
     // 256 VGPRs and the compiler serialised the sample loads)
     __shared__ TrkHot s_t;
     __shared__ int s_overrun;  // the channel fell behind the input (one loss-of-lock record)
-    // xcd_sel >= 0: the grid is 8 x channels and channel c runs on the workgroup of
-    // slot c whose XCD (blockIdx % 8) is xcd_sel (+1 per 32 channels), so one pool's
-    // channels, which stream overlapping stretches of the same input, share one L2
-    int ch = blockIdx.x;
-    if (xcd_sel >= 0)
-        {
-            const int slot = (int)(blockIdx.x >> 3);
-            if ((int)(blockIdx.x & 7u) != ((xcd_sel + slot / 32) & 7)) return;
-            ch = slot;
-        }
+    const int ch = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const TrkConst& c = consts[ch];
     TrkChan* gc = chans + ch;
@@ -1568,11 +1557,12 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                 }
             if (streamed)
                 {
-                    // chunk 0 of the call most likely next, fetched by waves 1.. while
+                    // chunk 0 of the call most likely next, fetched by waves 3.. while
                     // wave 0 runs the loop update (its own memory waits stay unaffected)
+                    // and waves 1 / 2 the speculative DLL/PLL and the EVM
                     const int64_t nb = p_off + vl - kHalo / 2;
                     pf_start = stream_fetch(iq, iq_items * (uint64_t)item_bytes<IT>(), nb * item_bytes<IT>(),
-                        (stream_chunk + kHalo) * item_bytes<IT>(), s_sb, 1);
+                        (stream_chunk + kHalo) * item_bytes<IT>(), s_sb, 3);
                     pf_first = nb;
                 }
             // lane k sums tap k over the waves in wave order (one batch of LDS reads
@@ -1850,7 +1840,6 @@ struct gsdr_trk
     // d_chans (start / stop / get_channel) wait for it, so a launch in flight on a
     // caller stream cannot write a stale channel back over them
     hipEvent_t last_launch{nullptr};
-    int xcd_sel{-1};  // GSDR_TRK_XCD: the XCD the pool's channels run on (-1: channel c on blockIdx c)
     // gsdr_trk_submit_stream / gsdr_trk_collect: device records of the submission,
     // their pinned host image and the event of its copy
     gsdr_trk_epoch* d_sub_out{nullptr};
@@ -2107,21 +2096,21 @@ int launch(gsdr_trk* k, const void* iq, uint64_t iq_first, uint64_t iq_items, ui
                 }
             GSDR_HIP(hipEventRecord(e0, s));
         }
-    const dim3 grid(k->xcd_sel >= 0 ? 8 * k->conf.max_channels : k->conf.max_channels);
+    const dim3 grid(k->conf.max_channels);
     int chunk = 0, sbuf = 0;
     stream_plan(k->lds_bytes, k->code_pad, k->data_pad, item_size(k->conf.item_type), chunk, sbuf);
     if (k->conf.item_type == GSDR_ITEM_GR_COMPLEX)
         hipLaunchKernelGGL((trk_kernel<GSDR_ITEM_GR_COMPLEX>), grid, dim3(kTrkThreads), k->lds_bytes, s, k->d_consts, k->d_chans,
             (const float* const*)k->d_codes, (const float* const*)k->d_data_codes, iq, iq_first, iq_items, max_epochs, out,
-            nout, k->code_pad, k->data_pad, timing, k->timing_wall, chunk, sbuf, k->xcd_sel);
+            nout, k->code_pad, k->data_pad, timing, k->timing_wall, chunk, sbuf);
     else if (k->conf.item_type == GSDR_ITEM_CSHORT)
         hipLaunchKernelGGL((trk_kernel<GSDR_ITEM_CSHORT>), grid, dim3(kTrkThreads), k->lds_bytes, s, k->d_consts, k->d_chans,
             (const float* const*)k->d_codes, (const float* const*)k->d_data_codes, iq, iq_first, iq_items, max_epochs, out,
-            nout, k->code_pad, k->data_pad, timing, k->timing_wall, chunk, sbuf, k->xcd_sel);
+            nout, k->code_pad, k->data_pad, timing, k->timing_wall, chunk, sbuf);
     else
         hipLaunchKernelGGL((trk_kernel<GSDR_ITEM_IBYTE>), grid, dim3(kTrkThreads), k->lds_bytes, s, k->d_consts, k->d_chans,
             (const float* const*)k->d_codes, (const float* const*)k->d_data_codes, iq, iq_first, iq_items, max_epochs, out,
-            nout, k->code_pad, k->data_pad, timing, k->timing_wall, chunk, sbuf, k->xcd_sel);
+            nout, k->code_pad, k->data_pad, timing, k->timing_wall, chunk, sbuf);
     GSDR_HIP(hipGetLastError());
     GSDR_HIP(hipEventRecord(k->last_launch, s));
     if (k->profiling)
@@ -2226,12 +2215,6 @@ int gsdr_trk_create(int device, const gsdr_trk_conf* conf, gsdr_trk** out)
         {
             k->timing_on = std::atoi(tv) != 0;
             k->timing_wall = std::atoi(tv) == 2;
-        }
-    if (const char* xv = std::getenv("GSDR_TRK_XCD"))
-        {
-            // each handle's channels on one XCD, handles round-robin over the XCDs
-            static std::atomic<int> next_xcd{0};
-            if (std::atoi(xv) != 0) k->xcd_sel = next_xcd.fetch_add(1) & 7;
         }
     hipError_t e = hipStreamCreateWithFlags(&k->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&k->last_launch, hipEventDisableTiming);

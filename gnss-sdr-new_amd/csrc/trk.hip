@@ -1241,6 +1241,13 @@ __device__ __forceinline__ void correlate_call_stream(const void* __restrict__ i
     const uint64_t nbytes = iq_items * (uint64_t)isz;
     const uintptr_t s0 = reinterpret_cast<uintptr_t>(iq) + (uintptr_t)p.off * isz;  // byte address of sample 0
     uintptr_t bstart[2];
+    if (!pf_ok)
+        {
+            // a prefetch into buffer 0 that missed this call may still be landing, its
+            // rows from other waves than this fetch's: let it land before refilling
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+        }
     bstart[0] = pf_ok ? pf_start : stream_fetch(iq, nbytes, p.off * isz, chunk * isz, sb, 0);
     bstart[1] = 0;
     const int nch = (vl + chunk - 1) / chunk;

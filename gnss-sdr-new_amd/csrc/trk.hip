@@ -1849,14 +1849,20 @@ struct gsdr_trk
     hipEvent_t last_launch{nullptr};
     // gsdr_trk_submit_stream / gsdr_trk_collect: device records of the submission,
     // their pinned host image and the event of its copy
-    gsdr_trk_epoch* d_sub_out{nullptr};
-    uint32_t* d_sub_nout{nullptr};
-    gsdr_trk_epoch* h_sub_out{nullptr};
-    uint32_t* h_sub_nout{nullptr};
-    uint32_t sub_cap{0};  // records per channel the submission buffers hold
-    uint32_t sub_epochs{0};
-    bool sub_pending{false};
-    hipEvent_t sub_done{nullptr};
+    struct Submission
+    {
+        gsdr_trk_epoch* d_out{nullptr};
+        uint32_t* d_nout{nullptr};
+        gsdr_trk_epoch* h_out{nullptr};
+        uint32_t* h_nout{nullptr};
+        uint32_t cap{0};  // records per channel the buffers hold
+        uint32_t epochs{0};
+        hipEvent_t done{nullptr};
+    };
+    static constexpr int kSubmissions = 2;  // in flight at once (collected oldest first)
+    Submission sub[kSubmissions];
+    int sub_head{0};   // the oldest pending submission
+    int sub_count{0};  // pending submissions
     std::mutex mu;
 };
 
@@ -2302,15 +2308,18 @@ void gsdr_trk_destroy(gsdr_trk* k)
             (void)hipEventDestroy(r.second);
         }
     for (hipEvent_t e : k->prof_pool) (void)hipEventDestroy(e);
-    if (k->sub_done)
+    for (auto& u : k->sub)
         {
-            (void)hipEventSynchronize(k->sub_done);
-            (void)hipEventDestroy(k->sub_done);
+            if (u.done)
+                {
+                    (void)hipEventSynchronize(u.done);
+                    (void)hipEventDestroy(u.done);
+                }
+            if (u.h_out) (void)hipHostFree(u.h_out);
+            if (u.h_nout) (void)hipHostFree(u.h_nout);
+            if (u.d_out) (void)hipFree(u.d_out);
+            if (u.d_nout) (void)hipFree(u.d_nout);
         }
-    if (k->h_sub_out) (void)hipHostFree(k->h_sub_out);
-    if (k->h_sub_nout) (void)hipHostFree(k->h_sub_nout);
-    if (k->d_sub_out) (void)hipFree(k->d_sub_out);
-    if (k->d_sub_nout) (void)hipFree(k->d_sub_nout);
     if (k->last_launch)
         {
             (void)hipEventSynchronize(k->last_launch);
@@ -2569,42 +2578,46 @@ int gsdr_trk_submit_stream(gsdr_trk* k, gsdr_stream* ring, uint32_t max_epochs)
 {
     GSDR_REQUIRE(k && ring, GSDR_E_ARG, "gsdr_trk_submit_stream: null argument");
     GSDR_REQUIRE(max_epochs >= 1, GSDR_E_ARG, "gsdr_trk_submit_stream: max_epochs must be >= 1");
+    gsdr_trk::Submission* u = nullptr;
     {
         std::lock_guard<std::mutex> lk(k->mu);
-        GSDR_REQUIRE(!k->sub_pending, GSDR_E_STATE, "gsdr_trk_submit_stream: collect the previous submission first");
+        GSDR_REQUIRE(k->sub_count < gsdr_trk::kSubmissions, GSDR_E_STATE,
+            "gsdr_trk_submit_stream: %d submissions in flight, collect the oldest first", gsdr_trk::kSubmissions);
         gsdr::DeviceGuard g(k->device);
         const uint32_t nch = k->conf.max_channels;
-        if (max_epochs > k->sub_cap)
+        u = &k->sub[(k->sub_head + k->sub_count) % gsdr_trk::kSubmissions];
+        if (max_epochs > u->cap)
             {
-                // nothing in flight reads them (sub_pending is false)
-                if (k->d_sub_out) GSDR_HIP(hipFree(k->d_sub_out));
-                if (k->h_sub_out) GSDR_HIP(hipHostFree(k->h_sub_out));
-                k->d_sub_out = nullptr;
-                k->h_sub_out = nullptr;
-                k->sub_cap = 0;
-                GSDR_HIP(hipMalloc(&k->d_sub_out, (size_t)nch * max_epochs * sizeof(gsdr_trk_epoch)));
-                GSDR_HIP(hipHostMalloc(reinterpret_cast<void**>(&k->h_sub_out), (size_t)nch * max_epochs * sizeof(gsdr_trk_epoch),
+                // not pending: nothing in flight reads this slot's buffers
+                if (u->d_out) GSDR_HIP(hipFree(u->d_out));
+                if (u->h_out) GSDR_HIP(hipHostFree(u->h_out));
+                u->d_out = nullptr;
+                u->h_out = nullptr;
+                u->cap = 0;
+                GSDR_HIP(hipMalloc(&u->d_out, (size_t)nch * max_epochs * sizeof(gsdr_trk_epoch)));
+                GSDR_HIP(hipHostMalloc(reinterpret_cast<void**>(&u->h_out), (size_t)nch * max_epochs * sizeof(gsdr_trk_epoch),
                     hipHostMallocDefault));
-                k->sub_cap = max_epochs;
+                u->cap = max_epochs;
             }
-        if (!k->d_sub_nout)
+        if (!u->d_nout)
             {
-                GSDR_HIP(hipMalloc(&k->d_sub_nout, nch * sizeof(uint32_t)));
-                GSDR_HIP(hipHostMalloc(reinterpret_cast<void**>(&k->h_sub_nout), nch * sizeof(uint32_t), hipHostMallocDefault));
-                GSDR_HIP(hipEventCreateWithFlags(&k->sub_done, hipEventDisableTiming));
+                GSDR_HIP(hipMalloc(&u->d_nout, nch * sizeof(uint32_t)));
+                GSDR_HIP(hipHostMalloc(reinterpret_cast<void**>(&u->h_nout), nch * sizeof(uint32_t), hipHostMallocDefault));
+                GSDR_HIP(hipEventCreateWithFlags(&u->done, hipEventDisableTiming));
             }
     }
-    int rc = gsdr_trk_run_stream(k, ring, max_epochs, k->d_sub_out, k->d_sub_nout, nullptr);
+    // on the handle's stream: ordered after the submissions still in flight
+    int rc = gsdr_trk_run_stream(k, ring, max_epochs, u->d_out, u->d_nout, nullptr);
     if (rc != GSDR_OK) return rc;
     std::lock_guard<std::mutex> lk(k->mu);
     gsdr::DeviceGuard g(k->device);
     const uint32_t nch = k->conf.max_channels;
-    GSDR_HIP(hipMemcpyAsync(k->h_sub_nout, k->d_sub_nout, nch * sizeof(uint32_t), hipMemcpyDeviceToHost, k->stream));
-    GSDR_HIP(hipMemcpyAsync(k->h_sub_out, k->d_sub_out, (size_t)nch * max_epochs * sizeof(gsdr_trk_epoch),
-        hipMemcpyDeviceToHost, k->stream));
-    GSDR_HIP(hipEventRecord(k->sub_done, k->stream));
-    k->sub_epochs = max_epochs;
-    k->sub_pending = true;
+    GSDR_HIP(hipMemcpyAsync(u->h_nout, u->d_nout, nch * sizeof(uint32_t), hipMemcpyDeviceToHost, k->stream));
+    GSDR_HIP(hipMemcpyAsync(u->h_out, u->d_out, (size_t)nch * max_epochs * sizeof(gsdr_trk_epoch), hipMemcpyDeviceToHost,
+        k->stream));
+    GSDR_HIP(hipEventRecord(u->done, k->stream));
+    u->epochs = max_epochs;
+    k->sub_count++;
     return GSDR_OK;
 }
 
@@ -2612,20 +2625,24 @@ int gsdr_trk_collect(gsdr_trk* k, int wait, gsdr_trk_epoch* out_host, uint32_t* 
 {
     GSDR_REQUIRE(k && out_host && n_out_host, GSDR_E_ARG, "gsdr_trk_collect: null argument");
     std::lock_guard<std::mutex> lk(k->mu);
-    GSDR_REQUIRE(k->sub_pending, GSDR_E_STATE, "gsdr_trk_collect: nothing submitted");
+    GSDR_REQUIRE(k->sub_count > 0, GSDR_E_STATE, "gsdr_trk_collect: nothing submitted");
     gsdr::DeviceGuard g(k->device);
+    gsdr_trk::Submission& u = k->sub[k->sub_head];
     if (!wait)
         {
-            const hipError_t q = hipEventQuery(k->sub_done);
+            const hipError_t q = hipEventQuery(u.done);
             if (q == hipErrorNotReady) return 1;
             GSDR_HIP(q);
         }
     else
-        GSDR_HIP(hipEventSynchronize(k->sub_done));
-    k->sub_pending = false;
-    const uint32_t nch = k->conf.max_channels, me = k->sub_epochs;
-    std::memcpy(n_out_host, k->h_sub_nout, nch * sizeof(uint32_t));
-    std::memcpy(out_host, k->h_sub_out, (size_t)nch * me * sizeof(gsdr_trk_epoch));
+        GSDR_HIP(hipEventSynchronize(u.done));
+    k->sub_head = (k->sub_head + 1) % gsdr_trk::kSubmissions;
+    k->sub_count--;
+    const uint32_t nch = k->conf.max_channels, me = u.epochs;
+    std::memcpy(n_out_host, u.h_nout, nch * sizeof(uint32_t));
+    // each channel's records only (a few of max_epochs per advance)
+    for (uint32_t c = 0; c < nch; ++c)
+        std::memcpy(out_host + (size_t)c * me, u.h_out + (size_t)c * me, std::min(u.h_nout[c], me) * sizeof(gsdr_trk_epoch));
     if (max_epochs) *max_epochs = me;
     return GSDR_OK;
 }

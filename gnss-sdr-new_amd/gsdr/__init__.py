@@ -682,13 +682,17 @@ class Tracking:
         return out.reshape(self.max_channels, max_epochs), n
 
     def submit_stream(self, ring, max_epochs):
-        """gsdr_trk_submit_stream: the ring form with the records copied back behind it; no wait."""
+        """gsdr_trk_submit_stream: the ring form with the records copied back behind it; no wait
+        (up to two submissions in flight)."""
         _check(load().gsdr_trk_submit_stream(self._h, ring._h, int(max_epochs)))
-        self._sub_epochs = int(max_epochs)
+        self._sub_epochs = getattr(self, "_sub_epochs", [])
+        self._sub_epochs.append(int(max_epochs))
 
     def collect(self, wait=True):
-        """gsdr_trk_collect -> (records, counts), or None while the submission is in flight (wait=False)."""
-        me = self._sub_epochs
+        """gsdr_trk_collect -> (records, counts) of the oldest submission, or None while it is in
+        flight (wait=False)."""
+        pending = getattr(self, "_sub_epochs", [])
+        me = pending[0] if pending else 1
         out = np.zeros(self.max_channels * me, TRK_EPOCH_DTYPE)
         n = np.zeros(self.max_channels, np.uint32)
         got = ctypes.c_uint32()
@@ -696,6 +700,7 @@ class Tracking:
         if rc == 1:
             return None
         _check(rc)
+        pending.pop(0)
         return out.reshape(self.max_channels, me), n
 
     def channel(self, ch):

@@ -58,6 +58,21 @@ bool DeviceIqRing::head(uint64_t* h) const
 
 void DeviceIqRing::feed(const void* in, uint64_t nitems_read, int n)
 {
+    const uint64_t end0 = nitems_read + static_cast<uint64_t>(std::max(n, 0));
+    {
+        // the common case of a ring shared by many blocks: another feeder pushed these
+        // items already (the same stream check as below, without the push lock)
+        std::lock_guard<std::mutex> lk(d_mu);
+        if (d_started && d_head >= end0 && nitems_read <= d_head)
+            {
+                if (d_head > 0 && d_head - 1 >= nitems_read && d_head - 1 < end0 &&
+                    std::memcmp(static_cast<const uint8_t*>(in) + (d_head - 1 - nitems_read) * d_item_bytes, d_last,
+                        d_item_bytes) != 0)
+                    throw std::logic_error(
+                        "DeviceIqRing::feed: two input streams under one ring key (<role>.mi355x_ring)");
+                return;
+            }
+    }
     std::lock_guard<std::mutex> push_lk(d_push_mu);
     const uint64_t end = nitems_read + static_cast<uint64_t>(std::max(n, 0));
     const auto* bytes = static_cast<const uint8_t*>(in);

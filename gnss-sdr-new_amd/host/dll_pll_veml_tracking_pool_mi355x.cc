@@ -43,7 +43,6 @@ SharedTrackingPool::SharedTrackingPool(const Dll_Pll_Conf& conf, int32_t signal,
     d_used.assign(max_channels, false);
     d_active.assign(max_channels, false);
     d_gen.assign(max_channels, 0);
-    d_sub_gen.assign(max_channels, 0);
     // one submission covers every call a channel can have in the ring: a channel is
     // advanced whenever half a window arrived, so it never lags the head by more
     d_epochs = window_calls + 2;
@@ -55,10 +54,10 @@ SharedTrackingPool::SharedTrackingPool(const Dll_Pll_Conf& conf, int32_t signal,
 SharedTrackingPool::~SharedTrackingPool()
 {
     d_ring->remove_hook(d_hook);
-    if (d_pending)
+    d_recs.resize(static_cast<size_t>(d_max) * d_epochs);
+    for (; !d_sub_gens.empty(); d_sub_gens.pop_front())
         {
             uint32_t me = 0;
-            d_recs.resize(static_cast<size_t>(d_max) * d_epochs);
             (void)gsdr_trk_collect(d_engine, 1, d_recs.data(), d_n.data(), &me);
         }
     gsdr_trk_destroy(d_engine);
@@ -151,19 +150,20 @@ void SharedTrackingPool::stop(int slot)
 
 bool SharedTrackingPool::take_locked(bool wait)
 {
-    if (!d_pending) return true;
+    if (d_sub_gens.empty()) return true;
     d_recs.resize(static_cast<size_t>(d_max) * d_epochs);
     uint32_t me = 0;
     const int rc = gsdr_trk_collect(d_engine, wait ? 1 : 0, d_recs.data(), d_n.data(), &me);
     if (rc == 1) return false;  // still in flight
-    d_pending = false;
+    const std::vector<uint32_t> gens = std::move(d_sub_gens.front());
+    d_sub_gens.pop_front();
     if (rc != GSDR_OK) throw gsdr_error("SharedTrackingPool::advance");
     uint32_t most = 0;
     for (uint32_t c = 0; c < d_max; ++c)
         {
             most = std::max(most, d_n[c]);
             // a slot started or stopped since the submission: its records are stale
-            if (!d_active[c] || d_gen[c] != d_sub_gen[c]) continue;
+            if (!d_active[c] || d_gen[c] != gens[c]) continue;
             for (uint32_t e = 0; e < d_n[c]; ++e) d_queue[c].push_back(d_recs[static_cast<size_t>(c) * me + e]);
         }
     d_more = most >= me;  // a full batch: more calls may be ready in the ring
@@ -172,19 +172,21 @@ bool SharedTrackingPool::take_locked(bool wait)
 
 void SharedTrackingPool::advance_locked(uint64_t head, bool wait)
 {
-    take_locked(true);  // one submission in flight per pool
+    // two submissions in flight: the next launch queues behind the one running, so the
+    // GPU does not idle while the host collects; collect the oldest before a third
+    if (d_sub_gens.size() >= kInFlight) take_locked(true);
     for (;;)
         {
-            // on the engine's stream, ordered after the ring's pushes; the records come
-            // back behind it while the host pushes and runs the blocks
+            // on the engine's stream, ordered after the ring's pushes and the launch in
+            // flight; the records come back behind it while the host pushes and runs
+            // the blocks
             if (gsdr_trk_submit_stream(d_engine, d_ring->stream(), d_epochs) != GSDR_OK)
                 throw gsdr_error("SharedTrackingPool::advance");
-            d_pending = true;
-            d_sub_gen = d_gen;
+            d_sub_gens.push_back(d_gen);
             ++d_launches;
             d_advanced = head;
             if (!wait) return;
-            take_locked(true);
+            while (!d_sub_gens.empty()) take_locked(true);
             if (!d_more) return;
         }
 }
@@ -222,11 +224,20 @@ void SharedTrackingPool::advance_if_due(bool force)
             if (head != d_advanced || d_more)
                 advance_locked(head, true);
             else
-                take_locked(true);
+                while (!d_sub_gens.empty()) take_locked(true);
             return;
         }
     if (head == d_advanced && !d_more) return;
     if (d_more || head - d_advanced >= d_batch) advance_locked(head, false);
+}
+
+bool SharedTrackingPool::pop(int slot, gsdr_trk_epoch* rec)
+{
+    std::lock_guard<std::mutex> lk(d_mu);
+    if (slot < 0 || d_queue[slot].empty()) return false;
+    *rec = d_queue[slot].front();
+    d_queue[slot].pop_front();
+    return true;
 }
 
 bool SharedTrackingPool::peek(int slot, gsdr_trk_epoch* rec)
@@ -391,9 +402,8 @@ int dll_pll_veml_tracking_pool_mi355x::work(const void* in, int ninput_items, ui
         }
     // hand out this channel's computed calls in order, up to the first that emits
     gsdr_trk_epoch rec;
-    while (d_state == 2 && d_pool->peek(d_slot, &rec))
+    while (d_state == 2 && d_pool->pop(d_slot, &rec))
         {
-            d_pool->drop(d_slot);
             d_last = rec;
             if (d_record_sink) d_record_sink(rec);
             if (d_conf.dump) d_dump.write(rec, d_conf.fs_in, d_signal == GSDR_SIGNAL_GAL_1B, d_conf.track_pilot);
@@ -401,15 +411,15 @@ int dll_pll_veml_tracking_pool_mi355x::work(const void* in, int ninput_items, ui
             if (d_output.emit(rec, *d_acquisition_gnss_synchro, rec.sample_counter, out)) *noutput = 1;
             // the call's time tags: those on [sample_counter, sample_counter + consumed)
             const uint64_t end = rec.sample_counter + static_cast<uint64_t>(std::max(rec.consumed, 0));
-            std::vector<GnssTimeTag> in_call;
+            d_in_call.clear();  // a member: no allocation per call
             while (!d_tags.empty() && d_tags.front().offset < end)
                 {
-                    if (d_tags.front().offset >= rec.sample_counter) in_call.push_back(d_tags.front());
+                    if (d_tags.front().offset >= rec.sample_counter) d_in_call.push_back(d_tags.front());
                     d_tags.pop_front();
                 }
             TrackingTags call_tags;
-            call_tags.in = in_call.data();
-            call_tags.n_in = static_cast<int>(in_call.size());
+            call_tags.in = d_in_call.data();
+            call_tags.n_in = static_cast<int>(d_in_call.size());
             d_output.call_tags(&call_tags, rec.sample_counter, rec.consumed, *noutput ? out : nullptr, d_nitems_written);
             if (tags && call_tags.has_out)
                 {

@@ -74,7 +74,9 @@ public:
     // asynchronous: its records land in the queues when a later call finds it done
     // (force: when anything arrived, and wait for the records)
     void advance_if_due(bool force);
-    // the next per-call record of `slot` (in call order), left in the queue by peek
+    // the next per-call record of `slot` (in call order): taken out by pop, left in the
+    // queue by peek
+    bool pop(int slot, gsdr_trk_epoch* rec);
     bool peek(int slot, gsdr_trk_epoch* rec);
     void drop(int slot);
 
@@ -85,7 +87,7 @@ public:
 
 private:
     void advance_locked(uint64_t head, bool wait);
-    bool take_locked(bool wait);  // the submission in flight -> the queues (false: not landed)
+    bool take_locked(bool wait);  // the oldest submission in flight -> the queues (false: not landed)
     void on_pushed(uint64_t from, uint64_t head);  // the ring's hook
 
     Dll_Pll_Conf d_conf;
@@ -105,11 +107,11 @@ private:
     std::vector<std::deque<gsdr_trk_epoch>> d_queue;
     std::vector<gsdr_trk_epoch> d_recs;
     std::vector<uint32_t> d_n;
-    std::vector<uint32_t> d_gen;      // per slot: bumped by start / stop / release
-    std::vector<uint32_t> d_sub_gen;  // d_gen when the submission in flight was made
-    uint32_t d_epochs{0};             // calls per channel per submission
-    bool d_pending{false};            // a submission in flight (gsdr_trk_submit_stream)
-    bool d_more{false};               // the last one filled a channel's batch
+    std::vector<uint32_t> d_gen;                  // per slot: bumped by start / stop / release
+    std::deque<std::vector<uint32_t>> d_sub_gens;  // d_gen at each submission in flight, oldest first
+    static constexpr size_t kInFlight = 2;         // gsdr_trk_submit_stream's queue depth
+    uint32_t d_epochs{0};                         // calls per channel per submission
+    bool d_more{false};                           // the last collected one filled a channel's batch
     std::mutex d_mu;
 };
 
@@ -158,6 +160,7 @@ private:
     TrackingDump d_dump;  // <role>.dump: the reference's per-channel .dat (log_data), .mat on destruction
     TrackingOutput d_output;
     std::deque<GnssTimeTag> d_tags;  // input time tags not yet matched to a call
+    std::vector<GnssTimeTag> d_in_call;  // the tags of the call being emitted
     bool d_fault_pending{false};     // telemetry fault between start_tracking and the pull-in
 };
 

@@ -6,7 +6,7 @@
 // tracks (each answer re-arms the request, as a receiver's idle channels keep
 // searching).  The reference's shape: gnss_flowgraph.cc:1007-1135 (one tracking and
 // one acquisition block per channel over the conditioner output).
-//   receiver_bench c3|c5 [seconds] [search] [pinned]
+//   receiver_bench c3|c5 [seconds] [search] [pinned] [pool batch]
 // search 1 (default): the acquisition services search every untracked PRN of GPS
 // and Galileo and BeiDou PRNs up to 32 on every block; 0: the tracking blocks only.
 // pinned 1 (default): the host sample buffer is page-locked (gsdr_host_register), as
@@ -67,6 +67,7 @@ int main(int argc, char** argv)
     const double seconds = argc > 2 ? std::atof(argv[2]) : 1.6;
     const bool search = argc > 3 ? std::atoi(argv[3]) != 0 : true;
     const bool pinned = argc > 4 ? std::atoi(argv[4]) != 0 : true;
+    const int pool_batch = argc > 5 ? std::atoi(argv[5]) : 0;  // 0: the blocks' default
     std::vector<Sig> sigs = {{"1C", "GPS_L1_CA_DLL_PLL_Tracking_MI355X", "GPS_L1_CA_PCPS_Acquisition_MI355X", 'G', '1',
         'C', 12, 32, 1.023e6, 1575.42e6, 1}};
     if (c5)
@@ -132,6 +133,7 @@ int main(int argc, char** argv)
             config.set_property(t + ".implementation", s.impl_trk);
             config.set_property(t + ".item_type", "gr_complex");
             config.set_property(t + ".mi355x_ring", "rf0");  // every signal reads the one front end
+            if (pool_batch > 0) config.set_property(t + ".mi355x_pool_batch", std::to_string(pool_batch));
             config.set_property(t + ".pll_bw_hz", s.sys == 'G' ? "40.0" : "15.0");
             config.set_property(t + ".dll_bw_hz", s.sys == 'G' ? "4.0" : "1.0");
             config.set_property(t + ".pull_in_time_s", "0");
@@ -264,19 +266,28 @@ int main(int argc, char** argv)
     const size_t chunk = 16384;
     bool progress = true;
     uint64_t trk_calls = 0;
+    // where the host's time goes: pushes (with the pools' advance launches their hooks
+    // make), the acquisition services, the tracking blocks' work() calls
+    using clk = std::chrono::steady_clock;
+    double t_feed = 0, t_svc = 0, t_work = 0;
     while (progress)
         {
             progress = false;
             if (pushed < n)
                 {
                     const size_t m = std::min(chunk, n - pushed);
+                    const auto a = clk::now();
                     hub->feed(x.data() + pushed, pushed, static_cast<int>(m));
+                    const auto b = clk::now();
                     pushed += m;
                     progress = true;
                     for (auto& s : svcs)
                         if (s) s->work_ring(ring, pushed);
+                    t_feed += std::chrono::duration<double>(b - a).count();
+                    t_svc += std::chrono::duration<double>(clk::now() - b).count();
                 }
             // every tracking block gets what the upstream buffer holds at its position
+            const auto w0 = clk::now();
             for (auto& ch : chans)
                 for (;;)
                     {
@@ -294,7 +305,9 @@ int main(int argc, char** argv)
                         ch.nread += static_cast<uint64_t>(std::max(used, 0));
                         ++trk_calls;
                     }
+            t_work += std::chrono::duration<double>(clk::now() - w0).count();
         }
+    const auto f0 = clk::now();
     // end of the stream: the blocks compute what they were handed and hand out the rest
     for (auto& ch : chans)
         {
@@ -310,6 +323,7 @@ int main(int argc, char** argv)
         }
     for (auto& s : svcs)
         if (s) s->flush();
+    const double t_flush = std::chrono::duration<double>(clk::now() - f0).count();
     const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     std::string per_sig;
     for (size_t g = 0; g < sigs.size(); ++g)
@@ -342,10 +356,11 @@ int main(int argc, char** argv)
     std::printf("{\"config\": \"%s\", \"search\": %d, \"path\": \"factory-built pooled TrackingInterface blocks (work() per block at its "
                 "nitems_read, batched advances) + AcquisitionService grids on the device IQ ring (batched, asynchronous), host "
                 "pushes of %zu-item chunks\", "
-                "\"host_buffer\": \"%s\", \"fs_sps\": %.0f, \"samples\": %zu, \"seconds\": %.4f, \"msps\": %.2f, \"real_time_factor\": %.2f, "
-                "\"tracking_channels\": %zu, \"trk_work_calls\": %llu, \"signals\": {%s}}\n",
-        cfg.c_str(), search ? 1 : 0, chunk, pinned ? "pinned" : "pageable", fs, n, sec, n / sec / 1e6, n / sec / fs, chans.size(),
-        static_cast<unsigned long long>(trk_calls), per_sig.c_str());
+                "\"host_buffer\": \"%s\", \"pool_batch\": %d, \"fs_sps\": %.0f, \"samples\": %zu, \"seconds\": %.4f, \"msps\": %.2f, \"real_time_factor\": %.2f, "
+                "\"tracking_channels\": %zu, \"trk_work_calls\": %llu, \"host_seconds\": {\"feed_and_pool_advances\": %.4f, "
+                "\"acquisition_services\": %.4f, \"tracking_work_calls\": %.4f, \"flush\": %.4f}, \"signals\": {%s}}\n",
+        cfg.c_str(), search ? 1 : 0, chunk, pinned ? "pinned" : "pageable", pool_batch, fs, n, sec, n / sec / 1e6, n / sec / fs, chans.size(),
+        static_cast<unsigned long long>(trk_calls), t_feed, t_svc, t_work, t_flush, per_sig.c_str());
     chans.clear();
     svcs.clear();
     if (pinned) gsdr_host_unregister(const_cast<std::complex<float>*>(x.data()));

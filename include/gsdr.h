@@ -560,9 +560,12 @@ int gsdr_trk_run_stream_host(gsdr_trk* trk, gsdr_stream* ring, uint32_t max_epoc
  * dll_pll_veml_tracking_pool_mi355x, which replace the per-channel general_work
  * round trips of dll_pll_veml_tracking.cc:1784-2152): gsdr_trk_run_stream on the
  * handle's stream into the handle's own submission buffers, the records and counts
- * copied into pinned host memory behind it; returns without waiting.  One submission
- * at a time.  gsdr_trk_collect copies them out: out_host holds max_channels *
- * max_epochs records (channel-major), n_out_host max_channels counts, *max_epochs
+ * copied into pinned host memory behind it; returns without waiting.  Up to two
+ * submissions in flight (the second runs behind the first on the handle's stream, so
+ * the GPU does not idle while the host collects); gsdr_trk_collect copies out the
+ * oldest: out_host holds max_channels *
+ * max_epochs records (channel-major; only the first n_out_host[c] of channel c are
+ * written), n_out_host max_channels counts, *max_epochs
  * (may be NULL) the submission's max_epochs; wait != 0 waits for the copy, wait == 0
  * returns 1 without copying while it is in flight. */
 int gsdr_trk_submit_stream(gsdr_trk* trk, gsdr_stream* ring, uint32_t max_epochs);

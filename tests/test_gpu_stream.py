@@ -265,10 +265,10 @@ def test_async_window_blocks_overwrite():
 
 def test_submit_collect_matches_contiguous():
     """gsdr_trk_submit_stream / gsdr_trk_collect (the pooled tracking blocks' advance):
-    a submission in flight while the next stretch is pushed (the push waits on its
-    reader event before overwriting), polled without waiting, gives records
-    identical to one contiguous gsdr_trk_run; collect without a submission and a
-    second submission before the collect are refused."""
+    two submissions in flight while the next stretches are pushed (a push waits on the
+    reader events of what it overwrites), the oldest polled without waiting, give
+    records identical to one contiguous gsdr_trk_run; collect without a submission and
+    a third submission in flight are refused."""
     ms = 120
     sats = synth.random_constellation(4, seed_offset=37)
     x = synth.gps_l1_iq(FS, ms * N, sats, seed_offset=37)
@@ -280,7 +280,6 @@ def test_submit_collect_matches_contiguous():
         t.start(c, s.prn, synth.gps_ca_chips(s.prn), d, f, 0, 0)
     ref_recs, ref_n = ref.run(x, 0, ms + 2)
     ring = gsdr.Stream(gsdr.ITEM_GR_COMPLEX, capacity_items=32 * N, max_window_items=16 * N)
-    t._sub_epochs = 1
     with pytest.raises(gsdr.GsdrError):
         t.collect()
     got = [[] for _ in sats]
@@ -290,22 +289,25 @@ def test_submit_collect_matches_contiguous():
         for c in range(len(sats)):
             got[c].extend(rec[c, :n[c]].copy())
 
-    pushed, pending, polls = 0, False, 0
+    pushed, pending, polls = 0, 0, 0
     while pushed < ms * N:
         ring.push(x[pushed:pushed + 4 * N], pushed)
         pushed += 4 * N
-        if pending:
+        if pending == 2:
             res = t.collect(wait=False)
             polls += res is None
             if res is None:
                 res = t.collect(wait=True)
             take(res)
+            pending -= 1
         t.submit_stream(ring, 18)
-        pending = True
-        if pushed == 8 * N:
+        pending += 1
+        if pending == 2 and pushed == 8 * N:
             with pytest.raises(gsdr.GsdrError):
                 t.submit_stream(ring, 18)
-    take(t.collect(wait=True))
+    while pending:
+        take(t.collect(wait=True))
+        pending -= 1
     for c in range(len(sats)):
         g = np.array(got[c], dtype=gsdr.TRK_EPOCH_DTYPE)
         r = ref_recs[c, :ref_n[c]]

@@ -1851,8 +1851,8 @@ struct gsdr_trk
     // their pinned host image and the event of its copy
     struct Submission
     {
-        gsdr_trk_epoch* d_out{nullptr};
-        uint32_t* d_nout{nullptr};
+        // the kernel writes the records straight into pinned host memory (zero-copy):
+        // no copy-engine hop between one advance's kernel and the next on the stream
         gsdr_trk_epoch* h_out{nullptr};
         uint32_t* h_nout{nullptr};
         uint32_t cap{0};  // records per channel the buffers hold
@@ -2317,8 +2317,6 @@ void gsdr_trk_destroy(gsdr_trk* k)
                 }
             if (u.h_out) (void)hipHostFree(u.h_out);
             if (u.h_nout) (void)hipHostFree(u.h_nout);
-            if (u.d_out) (void)hipFree(u.d_out);
-            if (u.d_nout) (void)hipFree(u.d_nout);
         }
     if (k->last_launch)
         {
@@ -2588,33 +2586,26 @@ int gsdr_trk_submit_stream(gsdr_trk* k, gsdr_stream* ring, uint32_t max_epochs)
         u = &k->sub[(k->sub_head + k->sub_count) % gsdr_trk::kSubmissions];
         if (max_epochs > u->cap)
             {
-                // not pending: nothing in flight reads this slot's buffers
-                if (u->d_out) GSDR_HIP(hipFree(u->d_out));
+                // not pending: nothing in flight writes this slot's buffer
                 if (u->h_out) GSDR_HIP(hipHostFree(u->h_out));
-                u->d_out = nullptr;
                 u->h_out = nullptr;
                 u->cap = 0;
-                GSDR_HIP(hipMalloc(&u->d_out, (size_t)nch * max_epochs * sizeof(gsdr_trk_epoch)));
                 GSDR_HIP(hipHostMalloc(reinterpret_cast<void**>(&u->h_out), (size_t)nch * max_epochs * sizeof(gsdr_trk_epoch),
-                    hipHostMallocDefault));
+                    hipHostMallocMapped));
                 u->cap = max_epochs;
             }
-        if (!u->d_nout)
+        if (!u->h_nout)
             {
-                GSDR_HIP(hipMalloc(&u->d_nout, nch * sizeof(uint32_t)));
-                GSDR_HIP(hipHostMalloc(reinterpret_cast<void**>(&u->h_nout), nch * sizeof(uint32_t), hipHostMallocDefault));
+                GSDR_HIP(hipHostMalloc(reinterpret_cast<void**>(&u->h_nout), nch * sizeof(uint32_t), hipHostMallocMapped));
                 GSDR_HIP(hipEventCreateWithFlags(&u->done, hipEventDisableTiming));
             }
     }
-    // on the handle's stream: ordered after the submissions still in flight
-    int rc = gsdr_trk_run_stream(k, ring, max_epochs, u->d_out, u->d_nout, nullptr);
+    // on the handle's stream: ordered after the submissions still in flight; the
+    // kernel's records land in the pinned host buffers themselves
+    int rc = gsdr_trk_run_stream(k, ring, max_epochs, u->h_out, u->h_nout, nullptr);
     if (rc != GSDR_OK) return rc;
     std::lock_guard<std::mutex> lk(k->mu);
     gsdr::DeviceGuard g(k->device);
-    const uint32_t nch = k->conf.max_channels;
-    GSDR_HIP(hipMemcpyAsync(u->h_nout, u->d_nout, nch * sizeof(uint32_t), hipMemcpyDeviceToHost, k->stream));
-    GSDR_HIP(hipMemcpyAsync(u->h_out, u->d_out, (size_t)nch * max_epochs * sizeof(gsdr_trk_epoch), hipMemcpyDeviceToHost,
-        k->stream));
     GSDR_HIP(hipEventRecord(u->done, k->stream));
     u->epochs = max_epochs;
     k->sub_count++;

@@ -144,6 +144,11 @@ int StreamReader::view(uint64_t first, uint64_t n, const void** ptr)
 int StreamReader::span(uint64_t* first, uint64_t* n) { return span_locked(s_, first, n); }
 int StreamReader::acquire(hipStream_t consumer)
 {
+    // a push that already landed needs no cross-queue dependency (a barrier packet on
+    // the consumer's queue waiting for the copy engine's signal delays the launch)
+    const hipError_t q = hipEventQuery(s_->pushed);
+    if (q == hipSuccess) return GSDR_OK;
+    if (q != hipErrorNotReady) GSDR_HIP(q);
     GSDR_HIP(hipStreamWaitEvent(consumer, s_->pushed, 0));
     return GSDR_OK;
 }

@@ -240,21 +240,6 @@ bool SharedTrackingPool::pop(int slot, gsdr_trk_epoch* rec)
     return true;
 }
 
-bool SharedTrackingPool::peek(int slot, gsdr_trk_epoch* rec)
-{
-    std::lock_guard<std::mutex> lk(d_mu);
-    if (slot < 0) return false;
-    if (d_queue[slot].empty()) return false;
-    *rec = d_queue[slot].front();
-    return true;
-}
-
-void SharedTrackingPool::drop(int slot)
-{
-    std::lock_guard<std::mutex> lk(d_mu);
-    if (slot >= 0 && !d_queue[slot].empty()) d_queue[slot].pop_front();
-}
-
 dll_pll_veml_tracking_pool_mi355x::dll_pll_veml_tracking_pool_mi355x(const Dll_Pll_Conf& conf, int32_t signal,
     uint32_t pool_channels, int device, const std::string& pool_key, uint32_t window_calls, uint32_t batch_calls,
     const std::string& ring_key)

@@ -74,11 +74,8 @@ public:
     // asynchronous: its records land in the queues when a later call finds it done
     // (force: when anything arrived, and wait for the records)
     void advance_if_due(bool force);
-    // the next per-call record of `slot` (in call order): taken out by pop, left in the
-    // queue by peek
+    // the next per-call record of `slot` (in call order), taken out of the queue
     bool pop(int slot, gsdr_trk_epoch* rec);
-    bool peek(int slot, gsdr_trk_epoch* rec);
-    void drop(int slot);
 
     uint64_t launches() const { return d_launches; }
     uint64_t window_items() const { return d_window; }

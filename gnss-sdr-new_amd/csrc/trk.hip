@@ -1028,6 +1028,21 @@ __device__ __forceinline__ int floor_i(float x)
     return r;
 }
 
+// The plan values every chunk of a call uses, in SGPRs: read from the LDS plan once
+// per call.  Read per chunk, behind the streamed calls' barriers, their wait also
+// waited for the chunk's own sample loads.
+struct ChunkNco
+{
+    float cstep, wsx, wsy;
+    int wrap;
+};
+__device__ __forceinline__ float uniform_f(float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); }
+__device__ __forceinline__ ChunkNco chunk_nco(const Prep& p)
+{
+    return ChunkNco{uniform_f(p.code_step), uniform_f(p.wstep.x), uniform_f(p.wstep.y),
+        __builtin_amdgcn_readfirstlane(p.wrap)};
+}
+
 // One correlation chunk of SPL (<= kSpl) samples per lane (n = n0 + tid +
 // j*kTrkThreads), KT taps, no branches inside.  FULL: every sample of the chunk lies inside the
 // call; otherwise samples past the end are zero and their index clamped.
@@ -1040,11 +1055,21 @@ __device__ __forceinline__ int floor_i(float x)
 // do_correlation_step, whose only tap sits at the prompt shift).
 template <int IT, int SRC, int WRAP, bool FULL, int KT, bool DATA, int SPL = kSpl>
 __device__ __forceinline__ void correlate_chunk(const void* __restrict__ iq, const float2* s_win, const float* s_code,
-    const float* s_data, const Prep& p, int n0, int vl, int L, const float (&sh_rem)[kMaxTrkTaps], float2& ph,
+    const float* s_data, const Prep& p, const ChunkNco& q, int n0, int vl, int L, const float (&sh_rem)[kMaxTrkTaps], float2& ph,
     float2 (&acc)[kMaxTrkTaps + 1], const char* sbuf = nullptr, int sboff = 0)
 {
     using gsdr::pk::c2;
     constexpr int IPK = KT / 2;  // prompt slot: 1 of E,P,L / 2 of VE,E,P,L,VL
+    // Five phases, fenced so the scheduler keeps them apart: (1) the samples (LDS
+    // or HBM) go out first -- left alone the scheduler sank their reads below the
+    // replica gathers, each behind its own lgkmcnt(0), four serial LDS round trips
+    // per chunk; (2) every replica index; (3) every replica gather (the data
+    // replica's first, at the prompt indices), then tap-major; (4) the rotated samples (the phasor
+    // chain, under the gathers' latency); (5) the FMAs tap-major, so each tap's
+    // FMAs wait only for that tap's gathers.  Every accumulator still adds its
+    // samples in increasing j, so the sums are those of the sample-major order.
+    const float cstep = q.cstep;
+    const c2 ws = c2{q.wsx, q.wsy};
     c2 xs[SPL];
 #pragma unroll
     for (int j = 0; j < SPL; ++j)
@@ -1058,12 +1083,9 @@ __device__ __forceinline__ void correlate_chunk(const void* __restrict__ iq, con
                 v = load_iq<IT>(iq, p.off + nc);
             else
                 v = lds_iq<IT>(sbuf, sboff + nc * item_bytes<IT>());
-            xs[j] = (FULL || n < vl) ? gsdr::pk::from(v) : c2{0.f, 0.f};
+            xs[j] = gsdr::pk::from(v);  // masked in phase 4: a select here waits for the load
         }
-    // Three phases -- every replica index, then every replica gather, then the
-    // FMAs -- so the chunk's SPL*KT LDS gathers are in flight together; written
-    // as one loop the scheduler issued them one at a time, each behind its own
-    // lgkmcnt(0) wait.  The FMA order per accumulator is unchanged.
+    __builtin_amdgcn_sched_barrier(0);
     float cv[SPL][KT];
     float dv[SPL];
 #pragma unroll
@@ -1071,7 +1093,7 @@ __device__ __forceinline__ void correlate_chunk(const void* __restrict__ iq, con
         {
             const int n0j = n0 + (int)threadIdx.x + j * kTrkThreads;
             const int n = FULL ? n0j : min(n0j, vl - 1);
-            const float a = gsdr::mul_rn(p.code_step, (float)n);
+            const float a = gsdr::mul_rn(cstep, (float)n);
 #pragma unroll
             for (int k = 0; k < KT; ++k)
                 {
@@ -1087,55 +1109,66 @@ __device__ __forceinline__ void correlate_chunk(const void* __restrict__ iq, con
                     cv[j][k] = __int_as_float(raw);
                 }
         }
-#pragma unroll
-    for (int j = 0; j < SPL; ++j)
+    if (DATA)
         {
-            if (DATA) dv[j] = s_data[__float_as_int(cv[j][IPK])];
+            // first: the data replica is gathered at the prompt tap's index
 #pragma unroll
-            for (int k = 0; k < KT; ++k) cv[j][k] = s_code[__float_as_int(cv[j][k])];
+            for (int j = 0; j < SPL; ++j) dv[j] = s_data[__float_as_int(cv[j][IPK])];
         }
-    c2 av[kMaxTrkTaps + 1];
 #pragma unroll
-    for (int k = 0; k <= kMaxTrkTaps; ++k) av[k] = gsdr::pk::from(acc[k]);
+    for (int k = 0; k < KT; ++k)
+        {
+#pragma unroll
+            for (int j = 0; j < SPL; ++j) cv[j][k] = s_code[__float_as_int(cv[j][k])];
+        }
+    __builtin_amdgcn_sched_barrier(0);
+    c2 tt[SPL];
     c2 phv = gsdr::pk::from(ph);
-    const c2 ws = gsdr::pk::from(p.wstep);
 #pragma unroll
     for (int j = 0; j < SPL; ++j)
         {
-            const c2 tt = gsdr::pk::mul(xs[j], phv);
-#pragma unroll
-            for (int k = 0; k < KT; ++k)
-                {
-                    av[k] = gsdr::pk::fmas(tt, cv[j][k], av[k]);
-                    if (DATA && k == IPK) av[kMaxTrkTaps] = gsdr::pk::fmas(tt, dv[j], av[kMaxTrkTaps]);
-                }
+            if (!FULL && n0 + (int)threadIdx.x + j * kTrkThreads >= vl) xs[j] = c2{0.f, 0.f};
+            tt[j] = gsdr::pk::mul(xs[j], phv);
             phv = gsdr::pk::mul(phv, ws);
         }
-#pragma unroll
-    for (int k = 0; k <= kMaxTrkTaps; ++k) acc[k] = gsdr::pk::to(av[k]);
     ph = gsdr::pk::to(phv);
+#pragma unroll
+    for (int k = 0; k < KT; ++k)
+        {
+            c2 av = gsdr::pk::from(acc[k]);
+#pragma unroll
+            for (int j = 0; j < SPL; ++j) av = gsdr::pk::fmas(tt[j], cv[j][k], av);
+            acc[k] = gsdr::pk::to(av);
+        }
+    if (DATA)
+        {
+            c2 av = gsdr::pk::from(acc[kMaxTrkTaps]);
+#pragma unroll
+            for (int j = 0; j < SPL; ++j) av = gsdr::pk::fmas(tt[j], dv[j], av);
+            acc[kMaxTrkTaps] = gsdr::pk::to(av);
+        }
 }
 
 // the chunk at n0 with the call's wrap mode; FULL when the whole chunk is inside the call
 template <int IT, int SRC, int KT, bool DATA, int SPL>
 __device__ __forceinline__ void correlate_chunk_wrap(const void* __restrict__ iq, const float2* s_win, const float* s_code,
-    const float* s_data, const Prep& p, int n0, int vl, int L, const float (&sh_rem)[kMaxTrkTaps], float2& ph,
+    const float* s_data, const Prep& p, const ChunkNco& q, int n0, int vl, int L, const float (&sh_rem)[kMaxTrkTaps], float2& ph,
     float2 (&acc)[kMaxTrkTaps + 1], const char* sbuf, int sboff)
 {
-    if (p.wrap == 2)
+    if (q.wrap == 2)
         {
             if (SPL == kSpl && n0 + kWinCore <= vl)
-                correlate_chunk<IT, SRC, 2, true, KT, DATA, SPL>(iq, s_win, s_code, s_data, p, n0, vl, L, sh_rem, ph, acc,
+                correlate_chunk<IT, SRC, 2, true, KT, DATA, SPL>(iq, s_win, s_code, s_data, p, q, n0, vl, L, sh_rem, ph, acc,
                     sbuf, sboff);
             else
-                correlate_chunk<IT, SRC, 2, false, KT, DATA, SPL>(iq, s_win, s_code, s_data, p, n0, vl, L, sh_rem, ph, acc,
+                correlate_chunk<IT, SRC, 2, false, KT, DATA, SPL>(iq, s_win, s_code, s_data, p, q, n0, vl, L, sh_rem, ph, acc,
                     sbuf, sboff);
         }
-    else if (p.wrap == 1)
-        correlate_chunk<IT, SRC, 1, false, KT, DATA, SPL>(iq, s_win, s_code, s_data, p, n0, vl, L, sh_rem, ph, acc, sbuf,
+    else if (q.wrap == 1)
+        correlate_chunk<IT, SRC, 1, false, KT, DATA, SPL>(iq, s_win, s_code, s_data, p, q, n0, vl, L, sh_rem, ph, acc, sbuf,
             sboff);
     else
-        correlate_chunk<IT, SRC, 0, false, KT, DATA, SPL>(iq, s_win, s_code, s_data, p, n0, vl, L, sh_rem, ph, acc, sbuf,
+        correlate_chunk<IT, SRC, 0, false, KT, DATA, SPL>(iq, s_win, s_code, s_data, p, q, n0, vl, L, sh_rem, ph, acc, sbuf,
             sboff);
 }
 
@@ -1145,18 +1178,18 @@ __device__ __forceinline__ void correlate_chunk_wrap(const void* __restrict__ iq
 // samples and their order are those of the full chunk (a masked sample adds 0).
 template <int IT, int SRC, int KT, bool DATA>
 __device__ __forceinline__ void correlate_chunk_any(const void* __restrict__ iq, const float2* s_win, const float* s_code,
-    const float* s_data, const Prep& p, int n0, int vl, int L, const float (&sh_rem)[kMaxTrkTaps], float2& ph,
+    const float* s_data, const Prep& p, const ChunkNco& q, int n0, int vl, int L, const float (&sh_rem)[kMaxTrkTaps], float2& ph,
     float2 (&acc)[kMaxTrkTaps + 1], const char* sbuf = nullptr, int sboff = 0)
 {
     const int rest = vl - n0;
     if (rest >= kWinCore || rest > 4 * kTrkThreads || kSpl <= 4)
-        correlate_chunk_wrap<IT, SRC, KT, DATA, kSpl>(iq, s_win, s_code, s_data, p, n0, vl, L, sh_rem, ph, acc, sbuf, sboff);
+        correlate_chunk_wrap<IT, SRC, KT, DATA, kSpl>(iq, s_win, s_code, s_data, p, q, n0, vl, L, sh_rem, ph, acc, sbuf, sboff);
     else if (rest > 2 * kTrkThreads)
-        correlate_chunk_wrap<IT, SRC, KT, DATA, 4>(iq, s_win, s_code, s_data, p, n0, vl, L, sh_rem, ph, acc, sbuf, sboff);
+        correlate_chunk_wrap<IT, SRC, KT, DATA, 4>(iq, s_win, s_code, s_data, p, q, n0, vl, L, sh_rem, ph, acc, sbuf, sboff);
     else if (rest > kTrkThreads)
-        correlate_chunk_wrap<IT, SRC, KT, DATA, 2>(iq, s_win, s_code, s_data, p, n0, vl, L, sh_rem, ph, acc, sbuf, sboff);
+        correlate_chunk_wrap<IT, SRC, KT, DATA, 2>(iq, s_win, s_code, s_data, p, q, n0, vl, L, sh_rem, ph, acc, sbuf, sboff);
     else
-        correlate_chunk_wrap<IT, SRC, KT, DATA, 1>(iq, s_win, s_code, s_data, p, n0, vl, L, sh_rem, ph, acc, sbuf, sboff);
+        correlate_chunk_wrap<IT, SRC, KT, DATA, 1>(iq, s_win, s_code, s_data, p, q, n0, vl, L, sh_rem, ph, acc, sbuf, sboff);
 }
 
 // high_dyn correlation (do_correlation_step with set_high_dynamics_resampler(true)):
@@ -1217,12 +1250,13 @@ __device__ __forceinline__ void correlate_call(const void* __restrict__ iq, cons
     const float* s_data, const Prep& p, int vl, int L, const float (&sh_rem)[kMaxTrkTaps], float2& ph,
     float2 (&acc)[kMaxTrkTaps + 1])
 {
+    const ChunkNco q = chunk_nco(p);
     for (int n0 = 0; n0 < vl; n0 += kWinCore)
         {
             if (p.woff >= 0)
-                correlate_chunk_any<IT, 0, KT, DATA>(iq, s_win, s_code, s_data, p, n0, vl, L, sh_rem, ph, acc);
+                correlate_chunk_any<IT, 0, KT, DATA>(iq, s_win, s_code, s_data, p, q, n0, vl, L, sh_rem, ph, acc);
             else
-                correlate_chunk_any<IT, 1, KT, DATA>(iq, s_win, s_code, s_data, p, n0, vl, L, sh_rem, ph, acc);
+                correlate_chunk_any<IT, 1, KT, DATA>(iq, s_win, s_code, s_data, p, q, n0, vl, L, sh_rem, ph, acc);
         }
 }
 
@@ -1237,6 +1271,7 @@ __device__ __forceinline__ void correlate_call_stream(const void* __restrict__ i
     int sbuf_bytes, int chunk, bool pf_ok, uintptr_t pf_start, const float* s_code, const float* s_data, const Prep& p,
     int vl, int L, const float (&sh_rem)[kMaxTrkTaps], float2& ph, float2 (&acc)[kMaxTrkTaps + 1], bool probe, uint64_t& swait)
 {
+    const ChunkNco q = chunk_nco(p);
     constexpr int isz = item_bytes<IT>();
     const uint64_t nbytes = iq_items * (uint64_t)isz;
     const uintptr_t s0 = reinterpret_cast<uintptr_t>(iq) + (uintptr_t)p.off * isz;  // byte address of sample 0
@@ -1267,8 +1302,25 @@ __device__ __forceinline__ void correlate_call_stream(const void* __restrict__ i
             const char* buf = sb + (j & 1) * sbuf_bytes;
             const int boff = (int)((int64_t)s0 - (int64_t)bstart[j & 1]);
             const int nend = min((j + 1) * chunk, vl);
-            for (int n0 = j * chunk; n0 < nend; n0 += kWinCore)
-                correlate_chunk_any<IT, 2, KT, DATA>(iq, nullptr, s_code, s_data, p, n0, vl, L, sh_rem, ph, acc, buf, boff);
+            for (int n0 = j * chunk; n0 < nend;)
+                {
+                    // E/P/L calls: two kWinCore blocks as one chunk of 2 kSpl samples per lane
+                    // where they are whole and need no wrap -- twice the gathers in flight per
+                    // wait (the lane's samples and their order are those of the two blocks;
+                    // five taps or the data tap at this width spill)
+                    if (KT == 3 && !DATA && n0 + 2 * kWinCore <= nend && q.wrap == 2)
+                        {
+                            correlate_chunk<IT, 2, 2, true, KT, DATA, 2 * kSpl>(iq, nullptr, s_code, s_data, p, q, n0, vl, L,
+                                sh_rem, ph, acc, buf, boff);
+                            n0 += 2 * kWinCore;
+                        }
+                    else
+                        {
+                            correlate_chunk_any<IT, 2, KT, DATA>(iq, nullptr, s_code, s_data, p, q, n0, vl, L, sh_rem, ph, acc,
+                                buf, boff);
+                            n0 += kWinCore;
+                        }
+                }
         }
 }
 

@@ -1268,7 +1268,7 @@ __device__ __forceinline__ void correlate_call(const void* __restrict__ iq, cons
 // and orders the previous chunk's reads before its buffer is refilled.
 template <int IT, int KT, bool DATA>
 __device__ __forceinline__ void correlate_call_stream(const void* __restrict__ iq, uint64_t iq_items, char* sb,
-    int sbuf_bytes, int chunk, bool pf_ok, uintptr_t pf_start, const float* s_code, const float* s_data, const Prep& p,
+    int sbuf_bytes, int chunk, bool pf_ok, const uintptr_t (&pf_start)[2], const float* s_code, const float* s_data, const Prep& p,
     int vl, int L, const float (&sh_rem)[kMaxTrkTaps], float2& ph, float2 (&acc)[kMaxTrkTaps + 1], bool probe, uint64_t& swait)
 {
     const ChunkNco q = chunk_nco(p);
@@ -1283,9 +1283,12 @@ __device__ __forceinline__ void correlate_call_stream(const void* __restrict__ i
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
         }
-    bstart[0] = pf_ok ? pf_start : stream_fetch(iq, nbytes, p.off * isz, chunk * isz, sb, 0);
+    bstart[0] = pf_ok ? pf_start[0] : stream_fetch(iq, nbytes, p.off * isz, chunk * isz, sb, 0);
     bstart[1] = 0;
     const int nch = (vl + chunk - 1) / chunk;
+    // chunk 1 came with chunk 0 (into the other buffer) when the prefetch covered it
+    const bool pf1 = pf_ok && pf_start[1] != 0 && nch > 1;
+    if (pf1) bstart[1] = pf_start[1];
     for (int j = 0; j < nch; ++j)
         {
             // a workgroup barrier waits only on lgkmcnt and LDS DMA is tracked per
@@ -1296,7 +1299,7 @@ __device__ __forceinline__ void correlate_call_stream(const void* __restrict__ i
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             if (probe) swait += wall_clock64() - w0;
-            if (j + 1 < nch)
+            if (j + 1 < nch && !(j == 0 && pf1))
                 bstart[(j + 1) & 1] =
                     stream_fetch(iq, nbytes, (p.off + (int64_t)(j + 1) * chunk) * isz, chunk * isz, sb + ((j + 1) & 1) * sbuf_bytes, 0);
             const char* buf = sb + (j & 1) * sbuf_bytes;
@@ -1483,7 +1486,7 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
     int64_t win_base = INT64_MIN;  // absolute-index base of the staged window (uniform)
     int lfi0 = 0;                  // wave 0: the current code loop filter slot (s_lfi)
     int64_t pf_first = INT64_MIN;  // streamed calls: first sample of the prefetched chunk 0 (uniform)
-    uintptr_t pf_start = 0;        // and the byte address its LDS buffer starts at
+    uintptr_t pf_start[2] = {0, 0};  // and the byte addresses chunks 0 / 1's LDS buffers start at (0: not fetched)
     uint32_t e = 0;
     for (;; ++e)
         {
@@ -1616,12 +1619,18 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                 }
             if (streamed)
                 {
-                    // chunk 0 of the call most likely next, fetched by waves 3.. while
-                    // wave 0 runs the loop update (its own memory waits stay unaffected)
-                    // and waves 1 / 2 the speculative DLL/PLL and the EVM
+                    // chunks 0 and 1 of the call most likely next, into the two buffers,
+                    // fetched by waves 3.. while wave 0 runs the loop update (its own
+                    // memory waits stay unaffected) and waves 1 / 2 the speculative
+                    // DLL/PLL and the EVM: the call's first in-call fetch is then chunk 2,
+                    // issued a whole chunk of correlation ahead
                     const int64_t nb = p_off + vl - kHalo / 2;
-                    pf_start = stream_fetch(iq, iq_items * (uint64_t)item_bytes<IT>(), nb * item_bytes<IT>(),
-                        (stream_chunk + kHalo) * item_bytes<IT>(), s_sb, 3);
+                    const uint64_t nbytes = iq_items * (uint64_t)item_bytes<IT>();
+                    pf_start[0] = stream_fetch(iq, nbytes, nb * item_bytes<IT>(), (stream_chunk + kHalo) * item_bytes<IT>(), s_sb, 3);
+                    pf_start[1] = vl > stream_chunk
+                                      ? stream_fetch(iq, nbytes, (nb + stream_chunk) * item_bytes<IT>(),
+                                            (stream_chunk + kHalo) * item_bytes<IT>(), s_sb + sbuf_bytes, 3)
+                                      : 0;
                     pf_first = nb;
                 }
             // lane k sums tap k over the waves in wave order (one batch of LDS reads

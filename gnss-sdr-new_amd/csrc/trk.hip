@@ -1283,9 +1283,13 @@ __device__ __forceinline__ void correlate_call_stream(const void* __restrict__ i
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
         }
-    bstart[0] = pf_ok ? pf_start[0] : stream_fetch(iq, nbytes, p.off * isz, chunk * isz, sb, 0);
+    // a tail of at most kTrkThreads samples rides with the last whole chunk (the
+    // buffers hold chunk + kTrkThreads items): no loop iteration of its own
+    int nch = (vl + chunk - 1) / chunk;
+    if (nch > 1 && vl - (nch - 1) * chunk <= kTrkThreads) --nch;
+    auto len = [&](int j) { return j == nch - 1 ? vl - j * chunk : chunk; };
+    bstart[0] = pf_ok ? pf_start[0] : stream_fetch(iq, nbytes, p.off * isz, len(0) * isz, sb, 0);
     bstart[1] = 0;
-    const int nch = (vl + chunk - 1) / chunk;
     // chunk 1 came with chunk 0 (into the other buffer) when the prefetch covered it
     const bool pf1 = pf_ok && pf_start[1] != 0 && nch > 1;
     if (pf1) bstart[1] = pf_start[1];
@@ -1301,10 +1305,10 @@ __device__ __forceinline__ void correlate_call_stream(const void* __restrict__ i
             if (probe) swait += wall_clock64() - w0;
             if (j + 1 < nch && !(j == 0 && pf1))
                 bstart[(j + 1) & 1] =
-                    stream_fetch(iq, nbytes, (p.off + (int64_t)(j + 1) * chunk) * isz, chunk * isz, sb + ((j + 1) & 1) * sbuf_bytes, 0);
+                    stream_fetch(iq, nbytes, (p.off + (int64_t)(j + 1) * chunk) * isz, len(j + 1) * isz, sb + ((j + 1) & 1) * sbuf_bytes, 0);
             const char* buf = sb + (j & 1) * sbuf_bytes;
             const int boff = (int)((int64_t)s0 - (int64_t)bstart[j & 1]);
-            const int nend = min((j + 1) * chunk, vl);
+            const int nend = j * chunk + len(j);
             for (int n0 = j * chunk; n0 < nend;)
                 {
                     // E/P/L calls: two kWinCore blocks as one chunk of 2 kSpl samples per lane
@@ -1626,10 +1630,11 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                     // issued a whole chunk of correlation ahead
                     const int64_t nb = p_off + vl - kHalo / 2;
                     const uint64_t nbytes = iq_items * (uint64_t)item_bytes<IT>();
-                    pf_start[0] = stream_fetch(iq, nbytes, nb * item_bytes<IT>(), (stream_chunk + kHalo) * item_bytes<IT>(), s_sb, 3);
-                    pf_start[1] = vl > stream_chunk
-                                      ? stream_fetch(iq, nbytes, (nb + stream_chunk) * item_bytes<IT>(),
-                                            (stream_chunk + kHalo) * item_bytes<IT>(), s_sb + sbuf_bytes, 3)
+                    // (with the tail a last chunk may carry when one of them is the last)
+                    const int pfn = (stream_chunk + (vl > 2 * stream_chunk + kTrkThreads ? 0 : kTrkThreads) + kHalo) * item_bytes<IT>();
+                    pf_start[0] = stream_fetch(iq, nbytes, nb * item_bytes<IT>(), pfn, s_sb, 3);
+                    pf_start[1] = vl > stream_chunk + kTrkThreads
+                                      ? stream_fetch(iq, nbytes, (nb + stream_chunk) * item_bytes<IT>(), pfn, s_sb + sbuf_bytes, 3)
                                       : 0;
                     pf_first = nb;
                 }
@@ -2106,8 +2111,9 @@ int ensure_out(gsdr_trk* k, uint32_t max_epochs)
 constexpr size_t kCuLds = 160 * 1024;
 constexpr size_t kStaticLdsMargin = 4 * 1024;  // the kernel's static __shared__ arrays
 // Streamed calls (vector_length > kWinCore): two chunk buffers in the LDS left
-// after the replicas, each (chunk + kHalo) items + 16 alignment bytes rounded up
-// to whole glds rows; chunk a multiple of kWinCore.  chunk = 0: no room (the
+// after the replicas, each (chunk + kTrkThreads + kHalo) items (a last chunk carries
+// a tail of up to kTrkThreads samples) + 16 alignment bytes rounded up to whole
+// glds rows; chunk a multiple of kWinCore.  chunk = 0: no room (the
 // calls then read HBM directly).
 int item_size(int item_type) { return item_type == GSDR_ITEM_GR_COMPLEX ? 8 : (item_type == GSDR_ITEM_CSHORT ? 4 : 2); }
 int stream_buffer_bytes(int chunk, int isz) { return (((chunk + kHalo) * isz + 16) / kStreamRow + 2) * kStreamRow; }
@@ -2120,16 +2126,16 @@ void stream_plan(size_t lds_bytes, int code_pad, int data_pad, int isz, int& chu
     if (const char* e = std::getenv("GSDR_TRK_STREAM_CHUNK")) cap = std::max(kWinCore, std::atoi(e) / kWinCore * kWinCore);
     for (int c = kWinCore; c <= cap; c += kWinCore)
         {
-            if (2L * stream_buffer_bytes(c, isz) > avail) break;
+            if (2L * stream_buffer_bytes(c + kTrkThreads, isz) > avail) break;
             chunk = c;
-            sbuf = stream_buffer_bytes(c, isz);
+            sbuf = stream_buffer_bytes(c + kTrkThreads, isz);
         }
 }
 
 size_t lds_for(int code_pad, int data_pad)
 {
     const size_t need = (size_t)(code_pad + data_pad) * sizeof(float) +
-                        std::max((size_t)(kWinCore + kHalo) * sizeof(float2), (size_t)2 * stream_buffer_bytes(kWinCore, 8));
+                        std::max((size_t)(kWinCore + kHalo) * sizeof(float2), (size_t)2 * stream_buffer_bytes(kWinCore + kTrkThreads, 8));
     // LDS reserved per channel workgroup: by default the whole CU, so no acquisition
     // workgroup shares its issue slots once it runs; GSDR_TRK_LDS_KB trades that for
     // an earlier start on a busy chip (a full-CU workgroup waits for an empty CU).

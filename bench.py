@@ -493,6 +493,7 @@ def run_c5(args):
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    elapsed_local = elapsed
     if dist is not None:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -559,6 +560,17 @@ def run_c5(args):
     del scratch, host
     comp["note"] = ("each stage alone after the timed region over the same K spans; trk_<pool>_msps = the stream's IQ "
                     "rate through that pool (every channel processes every sample)")
+    # where each rank's step goes: its own step time, the share of it
+    # its acquisition grids alone take, and its pools' alone times -- gathered after the
+    # timed region (the only collective besides the barriers and the max-over-ranks)
+    mine = {"rank": rank, "step_ms": round(elapsed_local / K * 1e3, 4), "acq_only_ms_per_step": round(ta / K * 1e3, 4),
+            "acq_fraction_of_step": round(ta / elapsed_local, 4), "trk_alone_ms_per_step": round(trk_time / K * 1e3, 4),
+            "acq_blocks": [int(lo), int(hi)], "channels": len(plan["channels"])}
+    if dist is not None:
+        gathered = [None] * world
+        dist.all_gather_object(gathered, mine)
+    else:
+        gathered = [mine]
     line = {
         "metric": METRIC,
         "value": round(value, 3),
@@ -598,6 +610,7 @@ def run_c5(args):
                                         "note": "each pool's calls x (8 B x vector_length + one record) over the "
                                                 "pools' summed alone time: a serial per-channel loop, latency-bound"}},
         "components": comp,
+        "per_rank": gathered,
         "h2d_ingest": {"bytes_per_step": int(ns * 8), "ms_per_step": round(th * 1e3, 3),
                        "gbps": round(ns * 8 / th / 1e9, 2), "frac_of_step": round(th / (elapsed / K), 4),
                        "note": "pinned host -> HBM copy of the rank's stream span per step (every rank ingests the "

@@ -1048,8 +1048,19 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(RP:
 // recomputation (acq_argmax_four_kernel: 144 workgroups at C5 Galileo).
 // The input factor W_N^{m q} of sub-transform q is a compile-time root per column row
 // and one table read per column (r04e: C4 bit transition +11 % over R reads).
+// ROUT > 1 phase 1 staged through per-wave LDS rings: the copies in flight per wave
+// (2 KB of LDS each); 0: products straight from VGPR loads
+#ifndef GSDR_SPLIT_DMA
+#define GSDR_SPLIT_DMA 0
+#endif
+// waves per SIMD the staged grid pass is compiled for (4: <= 128 VGPRs, two 512-lane
+// workgroups per CU as the VGPR form had)
+#ifndef GSDR_SPLIT_WPE
+#define GSDR_SPLIT_WPE 4
+#endif
 template <int ROUT, class RP, bool HALF, bool ARG = false>
-__global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(ARG ? 1 : RP::WPE))) acq_correlate_split_kernel(
+__global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(
+    ARG ? 1 : (ROUT > 1 && GSDR_SPLIT_DMA > 0 ? GSDR_SPLIT_WPE : RP::WPE)))) acq_correlate_split_kernel(
     const float2* __restrict__ X, const float2* __restrict__ code_fft, RowStat* __restrict__ stats,
     const float2* __restrict__ tw, uint32_t D, uint32_t P, uint32_t nblocks, uint32_t pgs, XMap xm,
     const gsdr_acq_result* __restrict__ sel, unsigned long long* __restrict__ keys, float* __restrict__ rowbuf,
@@ -1102,6 +1113,10 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(ARG
         const auto u = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, 0);
         return c2{__uint_as_float(u[0]), __uint_as_float(u[1])};
     };
+    const float2* xg = X + xm.off(b, d);
+    const float2* cg = code_fft + (size_t)p * N;
+    (void)xg;
+    (void)cg;
     static_assert(ROUT == 1 || ROUT == 2 || ROUT == 4, "outer radix 1, 2 or 4");
     const int wbase = (int)(threadIdx.x & ~63u);
     // phase 1: columns (clamped lanes repeat column L-1), with the sub-transform
@@ -1109,8 +1124,123 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(ARG
     // (+-1, +-i: an add/sub with swapped operands) and W_N^{mq} one table read
     // (m q < N)
     c2 v[CPL][R];
+    // ROUT > 1: every element of a column sums ROUT products.  Loaded into VGPRs,
+    // the compiler kept the accumulated columns resident and issued two loads and a
+    // wait per product (r05: 200 dependent L2 round trips per column at 100000, VALU
+    // issuing 29 % of the cycles).  Staged instead: each wave copies its own
+    // columns' X and code values into its own LDS ring with global_load_lds
+    // (dwordx4: one instruction moves two 512-byte segments -- one (row n1, quarter r,
+    // column set c) each -- without VGPRs), DEPTH copies ahead of the products that
+    // read them; no other wave reads a wave's ring, so no barrier, only its vmcnt.
+    // Each element's sum keeps the r order (bit-identical).
+    auto phase1_dma = [&](auto qc) {
+        constexpr int Q = decltype(qc)::value;
+        constexpr int DEPTH = GSDR_SPLIT_DMA;
+        // segment s: column set c = s / U, unit u = s % U (n1 = u / ROUT, r = u % ROUT):
+        // column-major, so a column's transform runs (and its registers settle) before
+        // the next column accumulates, as in the VGPR form
+        constexpr int U = R * ROUT;
+        constexpr int SEGS = U * CPL;
+        constexpr int PAIRS = (SEGS + 1) / 2;    // one X and one code copy per two segments
+        const int wave = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
+        char* ring = reinterpret_cast<char*>(lds_raw) + (size_t)wave * DEPTH * 2048;
+        const int half = lane >> 5, l32 = lane & 31;
+        const int lane_off = (wave * 64 + 2 * l32) * 8;
+        auto issue = [&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            if constexpr (k < PAIRS)
+                {
+                    // lanes 0-31: segment 2k, lanes 32-63: segment 2k + 1 (the last pair of an
+                    // odd count repeats its segment); two columns (16 B) per lane
+                    constexpr int sa = 2 * k, sb = 2 * k + 1 < SEGS ? 2 * k + 1 : 2 * k;
+                    constexpr int ua = sa % U, ca = sa / U, ub = sb % U, cb = sb / U;
+                    constexpr int ea = (ua % ROUT) * (int)M + (ua / ROUT) * L + ca * NT;
+                    constexpr int eb = (ub % ROUT) * (int)M + (ub / ROUT) * L + cb * NT;
+                    // this lane's 16 bytes: the lane part in voffset, the segment's element
+                    // offset as the scalar offset; bounds-checked buffer copies (lanes past
+                    // column L - 1 copy bytes no lane reads, past the row's end zeros)
+                    const int so = (half ? eb - ea : 0) * 8;
+                    char* dst = ring + (k % DEPTH) * 2048;
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (gsdr_lvoid*)dst, 16, lane_off, ea * 8 + so, 0, 0);
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(crs, (gsdr_lvoid*)(dst + 1024), 16, lane_off, ea * 8 + so, 0, 0);
+                }
+        };
+        // the lane's column within its segment (clamped lanes read column L - 1's)
+        int cl[CPL];
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) cl[c] = min((int)threadIdx.x + c * NT, L - 1) - (c * NT + wave * 64);
+        auto prologue = [&](auto kc) { issue(kc); };
+        gsdr::pk::static_for<0, DEPTH>(prologue);
+        auto step = [&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            // pair k has landed once at most 2 (min(DEPTH, PAIRS - k) - 1) younger copies are out
+            constexpr int younger = 2 * ((PAIRS - k < DEPTH ? PAIRS - k : DEPTH) - 1);
+            // s_waitcnt vmcnt(younger) (expcnt / lgkmcnt left at their maxima)
+            __builtin_amdgcn_s_waitcnt((younger & 15) | (7 << 4) | (15 << 8) | ((younger >> 4) << 14));
+            const char* src = ring + (k % DEPTH) * 2048;
+            auto seg = [&](auto jc) {
+                constexpr int sidx = 2 * k + decltype(jc)::value;
+                if constexpr (sidx < SEGS)
+                    {
+                        constexpr int u = sidx % U, c = sidx / U, n1 = u / ROUT, r = u % ROUT;
+                        if (L % NT == 0 || wbase + c * NT < L)
+                            {
+                                const int off = decltype(jc)::value * 512 + cl[c] * 8;
+                                const c2 xv = *reinterpret_cast<const c2*>(src + off);
+                                const c2 cv = *reinterpret_cast<const c2*>(src + 1024 + off);
+                                const c2 y = gsdr::pk::conj_mul(xv, cv);
+                                // W_ROUT^{r Q} = W_4^{e}, e = (r Q mod ROUT) * 4 / ROUT
+                                constexpr int e = ((r * Q) % ROUT) * (4 / ROUT);
+                                c2& z = v[c][n1];
+                                if constexpr (r == 0)
+                                    z = y;
+                                else if constexpr (e == 0)
+                                    z = z + y;
+                                else if constexpr (e == 1)
+                                    z = gsdr::pk::add_mi(z, y);  // z + (-i) y
+                                else if constexpr (e == 2)
+                                    z = z - y;
+                                else
+                                    z = gsdr::pk::sub_mi(z, y);  // z + i y
+                                if constexpr (Q > 0 && r == ROUT - 1) z = gsdr::pk::mul_root<Q * n1, ROUT * R>(z);
+                            }
+                    }
+            };
+            gsdr::pk::static_for<0, 2>(seg);
+            // the slot's reads are done (their values are used above): refill it
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            issue(std::integral_constant<int, k + DEPTH>{});
+            // a column's last segment: its transform, while the next column's copies land
+            constexpr int last = 2 * k + 1 < SEGS ? 2 * k + 1 : 2 * k;
+            if constexpr ((last + 1) % U == 0)
+                {
+                    constexpr int c = last / U;
+                    if (L % NT == 0 || wbase + c * NT < L)
+                        {
+                            const int n2 = min((int)threadIdx.x + c * NT, L - 1);
+                            gsdr::pk::Dft<R>::run(v[c]);
+                            if constexpr (Q > 0)
+                                {
+                                    const c2 w0 = gsdr::pk::from(tw[Q * n2]);
+#pragma unroll
+                                    for (int k1 = 0; k1 < R; ++k1) v[c][k1] = gsdr::pk::mul(v[c][k1], w0);
+                                }
+                            gsdr::pk::apply_powers<R>(v[c], gsdr::pk::from(tw[ROUT * n2]));
+                        }
+                }
+        };
+        static_assert(U % 2 == 0, "a copy pair stays inside one column set");
+        gsdr::pk::static_for<0, PAIRS>(step);
+        // phase 2 writes rows over the rings: every wave's reads are done first
+        __syncthreads();
+    };
     auto phase1 = [&](auto qc) {
         constexpr int Q = decltype(qc)::value;
+        if constexpr (ROUT > 1 && GSDR_SPLIT_DMA > 0)
+            {
+                phase1_dma(qc);
+                return;
+            }
 #pragma unroll
         for (int c = 0; c < CPL; ++c)
             {

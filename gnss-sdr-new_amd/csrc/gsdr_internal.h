@@ -127,3 +127,8 @@ __device__ __forceinline__ float wave_sum_lane63(float v)
 }
 
 }  // namespace gsdr
+
+// pointer types of __builtin_amdgcn_global_load_lds (global source, LDS destination)
+typedef __attribute__((address_space(1))) void gsdr_gvoid;
+typedef __attribute__((address_space(3))) void gsdr_lvoid;
+

@@ -47,6 +47,15 @@ struct gsdr_stream
         hipEvent_t ev;
     };
     std::vector<Reader> readers;
+    // pushes whose copies may still read the caller's host memory: the absolute end
+    // of each and the event recorded behind its copies, oldest first
+    struct Pending
+    {
+        uint64_t end;
+        hipEvent_t ev;
+    };
+    std::vector<Pending> pending;
+    uint64_t landed{0};  // every item before it is in device memory
     std::vector<hipEvent_t> retired;  // waited for by a push, recycled once complete
     std::vector<hipEvent_t> spare;
     // windows handed out by gsdr_stream_window_async whose reads are not yet
@@ -108,6 +117,30 @@ void recycle_locked(gsdr_stream* s)
                          [&](const gsdr_stream::Reader& r) { return done(r.ev); }),
         s->readers.end());
     s->retired.erase(std::remove_if(s->retired.begin(), s->retired.end(), done), s->retired.end());
+}
+
+// pushes whose copies completed leave `pending` (their events to the spare list);
+// wait: block until every push holding an item before `upto` completed (ring lock held)
+int land_locked(gsdr_stream* s, bool wait, uint64_t upto)
+{
+    size_t k = 0;
+    for (; k < s->pending.size(); ++k)
+        {
+            const gsdr_stream::Pending& p = s->pending[k];
+            if (wait && s->landed < upto)  // s->landed: this push's first item
+                GSDR_HIP(hipEventSynchronize(p.ev));
+            else
+                {
+                    const hipError_t q = hipEventQuery(p.ev);
+                    if (q == hipErrorNotReady) break;
+                    GSDR_HIP(q);
+                }
+            s->landed = p.end;
+            s->spare.push_back(p.ev);
+        }
+    s->pending.erase(s->pending.begin(), s->pending.begin() + static_cast<std::ptrdiff_t>(k));
+    if (s->pending.empty()) s->landed = s->head;
+    return GSDR_OK;
 }
 
 // the consumer's reads of items >= lo are enqueued on `consumer`: a push that
@@ -209,6 +242,7 @@ void gsdr_stream_destroy(gsdr_stream* s)
             (void)hipEventSynchronize(ev);
             (void)hipEventDestroy(ev);
         }
+    for (const auto& p : s->pending) (void)hipEventDestroy(p.ev);  // the copy stream drained above
     for (hipEvent_t ev : s->spare) (void)hipEventDestroy(ev);
     if (s->pushed) (void)hipEventDestroy(s->pushed);
     if (s->copy) (void)hipStreamDestroy(s->copy);
@@ -224,7 +258,7 @@ int gsdr_stream_push(gsdr_stream* s, const void* iq_host, uint64_t first_sample,
     if (!s->started)
         {
             s->started = true;
-            s->base = s->head = first_sample;
+            s->base = s->head = s->landed = first_sample;
         }
     GSDR_REQUIRE(n <= s->cap, GSDR_E_ARG, "gsdr_stream_push: %llu items exceed the ring capacity %llu",
         (unsigned long long)n, (unsigned long long)s->cap);
@@ -289,8 +323,47 @@ int gsdr_stream_push(gsdr_stream* s, const void* iq_host, uint64_t first_sample,
             done += len;
         }
     GSDR_HIP(hipEventRecord(s->pushed, s->copy));
+    // the push's own event: iq_host is the caller's until it completes
+    if (s->pending.size() >= 64)
+        {
+            const int rc = gsdr::land_locked(s, false, 0);
+            if (rc != GSDR_OK) return rc;
+        }
+    hipEvent_t ev = nullptr;
+    if (!s->spare.empty())
+        {
+            ev = s->spare.back();
+            s->spare.pop_back();
+        }
+    else
+        GSDR_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    const hipError_t e = hipEventRecord(ev, s->copy);
+    if (e != hipSuccess)
+        {
+            s->spare.push_back(ev);
+            GSDR_HIP(e);
+        }
     s->head += n;
+    s->pending.push_back({s->head, ev});
     return GSDR_OK;
+}
+
+int gsdr_stream_landed(gsdr_stream* s, uint64_t* landed)
+{
+    GSDR_REQUIRE(s && landed, GSDR_E_ARG, "gsdr_stream_landed: null argument");
+    std::lock_guard<std::mutex> lk(s->mu);
+    gsdr::DeviceGuard g(s->device);
+    const int rc = gsdr::land_locked(s, false, 0);
+    *landed = s->landed;
+    return rc;
+}
+
+int gsdr_stream_wait_landed(gsdr_stream* s, uint64_t upto)
+{
+    GSDR_REQUIRE(s, GSDR_E_ARG, "gsdr_stream_wait_landed: null argument");
+    std::lock_guard<std::mutex> lk(s->mu);
+    gsdr::DeviceGuard g(s->device);
+    return gsdr::land_locked(s, true, upto);
 }
 
 int gsdr_stream_span(gsdr_stream* s, uint64_t* first_sample, uint64_t* n_items)

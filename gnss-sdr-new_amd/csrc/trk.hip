@@ -989,9 +989,6 @@ __device__ __forceinline__ float2 lds_iq(const char* b, int byte)
         }
 }
 
-typedef __attribute__((address_space(1))) void gsdr_gvoid;
-typedef __attribute__((address_space(3))) void gsdr_lvoid;
-
 // Asynchronous copy of input bytes [first, first + nbytes) (relative to the
 // stream pointer) into an LDS buffer with global_load_lds_dwordx4: no VGPR
 // destinations, so a whole chunk is in flight at once.  The buffer starts at the
@@ -1630,8 +1627,11 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                     // issued a whole chunk of correlation ahead
                     const int64_t nb = p_off + vl - kHalo / 2;
                     const uint64_t nbytes = iq_items * (uint64_t)item_bytes<IT>();
-                    // (with the tail a last chunk may carry when one of them is the last)
-                    const int pfn = (stream_chunk + (vl > 2 * stream_chunk + kTrkThreads ? 0 : kTrkThreads) + kHalo) * item_bytes<IT>();
+                    // sized for the tail a last chunk may carry, whatever the next call's
+                    // vector length: Doppler can move it across 2 chunk + kTrkThreads
+                    // between calls, and the next call decides its tail from its own
+                    // (the buffers hold chunk + kTrkThreads + kHalo items)
+                    const int pfn = (stream_chunk + kTrkThreads + kHalo) * item_bytes<IT>();
                     pf_start[0] = stream_fetch(iq, nbytes, nb * item_bytes<IT>(), pfn, s_sb, 3);
                     pf_start[1] = vl > stream_chunk + kTrkThreads
                                       ? stream_fetch(iq, nbytes, (nb + stream_chunk) * item_bytes<IT>(), pfn, s_sb + sbuf_bytes, 3)
@@ -1930,6 +1930,10 @@ struct gsdr_trk
     int sub_head{0};   // the oldest pending submission
     int sub_count{0};  // pending submissions
     std::mutex mu;
+    // held for a whole gsdr_trk_submit_stream: the slot it picks stays its own while
+    // mu is released for the launch (a second submitter waits; a collect in between
+    // takes only committed submissions and leaves sub_head + sub_count unchanged)
+    std::mutex submit_mu;
 };
 
 namespace
@@ -2643,6 +2647,7 @@ int gsdr_trk_submit_stream(gsdr_trk* k, gsdr_stream* ring, uint32_t max_epochs)
 {
     GSDR_REQUIRE(k && ring, GSDR_E_ARG, "gsdr_trk_submit_stream: null argument");
     GSDR_REQUIRE(max_epochs >= 1, GSDR_E_ARG, "gsdr_trk_submit_stream: max_epochs must be >= 1");
+    std::lock_guard<std::mutex> submit_lk(k->submit_mu);
     gsdr_trk::Submission* u = nullptr;
     {
         std::lock_guard<std::mutex> lk(k->mu);

@@ -47,7 +47,8 @@ EXPORTED = [
     "gsdr_acq_dump_grid_step_two", "gsdr_acq_read_profile_intervals", "gsdr_acq_set_wipeoff",
     "gsdr_acq_get_spectrum_reuse", "gsdr_trk_force_loss_of_lock", "gsdr_acq_set_local_code",
     "gsdr_acq_set_active_prns", "gsdr_acq_submit_stream", "gsdr_acq_collect", "gsdr_host_register",
-    "gsdr_host_unregister", "gsdr_trk_submit_stream", "gsdr_trk_collect",
+    "gsdr_host_unregister", "gsdr_trk_submit_stream", "gsdr_trk_collect", "gsdr_stream_landed",
+    "gsdr_stream_wait_landed",
 ]
 
 WIPE_EXACT, WIPE_GENERIC, WIPE_AVX2 = 0, 1, 2
@@ -290,6 +291,8 @@ def load():
     L.gsdr_stream_destroy.argtypes = [P]
     L.gsdr_stream_destroy.restype = None
     L.gsdr_stream_push.argtypes = [P, P, U64, U64]
+    L.gsdr_stream_landed.argtypes = [P, P]
+    L.gsdr_stream_wait_landed.argtypes = [P, U64]
     L.gsdr_stream_span.argtypes = [P, P, P]
     L.gsdr_stream_window.argtypes = [P, U64, U64, P]
     L.gsdr_acq_read_profile_ex.argtypes = [P, P, P, P]
@@ -739,11 +742,13 @@ class Stream:
         _check(load().gsdr_stream_create(int(device), int(item_type), int(capacity_items), int(max_window_items),
                                          ctypes.byref(self._h)))
         self.item_type = int(item_type)
+        self._inflight = []  # (end, array) of pushes whose copies may still read the array
 
     def close(self):
         if self._h:
             load().gsdr_stream_destroy(self._h)
             self._h = ctypes.c_void_p()
+        self._inflight = []
 
     def __del__(self):
         try:
@@ -752,10 +757,26 @@ class Stream:
             pass
 
     def push(self, iq, first_sample):
+        """Asynchronous push (gsdr_stream_push): the array (or the contiguous copy made
+        of it here) is held until its copy landed; the caller's own array must not be
+        modified before landed() >= first_sample + n (or wait_landed)."""
         iq = np.ascontiguousarray(iq, _ITEM_NP[self.item_type])
         n = len(iq) if self.item_type == ITEM_GR_COMPLEX else len(iq) // 2
         _check(load().gsdr_stream_push(self._h, _ptr(iq), int(first_sample), int(n)))
+        self._inflight.append((int(first_sample) + n, iq))
+        self.landed()
         return n
+
+    def landed(self):
+        """Every item before the returned index is in device memory (gsdr_stream_landed)."""
+        v = ctypes.c_uint64()
+        _check(load().gsdr_stream_landed(self._h, ctypes.byref(v)))
+        self._inflight = [(e, a) for e, a in self._inflight if e > v.value]
+        return v.value
+
+    def wait_landed(self, upto):
+        _check(load().gsdr_stream_wait_landed(self._h, int(upto)))
+        return self.landed()
 
     def span(self):
         f, n = ctypes.c_uint64(), ctypes.c_uint64()

@@ -45,6 +45,10 @@ int DeviceIqRing::add_hook(Hook h)
 
 void DeviceIqRing::remove_hook(int id)
 {
+    // feed() runs the hooks outside d_mu but under d_push_mu: taking it first waits
+    // for a dispatch in progress, so no hook runs after its owner removed it (and
+    // destroys itself); the same order as feed (push lock, then d_mu)
+    std::lock_guard<std::mutex> push_lk(d_push_mu);
     std::lock_guard<std::mutex> lk(d_mu);
     d_hooks.erase(id);
 }
@@ -54,6 +58,20 @@ bool DeviceIqRing::head(uint64_t* h) const
     std::lock_guard<std::mutex> lk(d_mu);
     *h = d_head;
     return d_started;
+}
+
+uint64_t DeviceIqRing::landed()
+{
+    uint64_t v = 0;
+    if (gsdr_stream_landed(d_ring, &v) != GSDR_OK)
+        throw std::runtime_error(std::string("DeviceIqRing::landed: ") + gsdr_last_error());
+    return v;
+}
+
+void DeviceIqRing::wait_landed(uint64_t upto)
+{
+    if (gsdr_stream_wait_landed(d_ring, upto) != GSDR_OK)
+        throw std::runtime_error(std::string("DeviceIqRing::wait_landed: ") + gsdr_last_error());
 }
 
 void DeviceIqRing::feed(const void* in, uint64_t nitems_read, int n)

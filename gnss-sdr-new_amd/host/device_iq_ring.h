@@ -53,6 +53,8 @@ public:
     int device() const { return d_device; }
 
     int add_hook(Hook h);
+    // returns once no feed() is running hooks: the hook's owner may then be destroyed
+    // (not to be called from inside a hook)
     void remove_hook(int id);
 
     // input items [nitems_read, nitems_read + n): the part the ring has not seen is
@@ -62,6 +64,11 @@ public:
     void feed(const void* in, uint64_t nitems_read, int n);
     // the next item to push (absolute index); false before the first push
     bool head(uint64_t* h) const;
+    // every item before the returned index is in device memory: a push copies from
+    // the feeder's buffer after feed() returns, so a block consumes (and its upstream
+    // may recycle) only items before it (gsdr_stream_landed)
+    uint64_t landed();
+    void wait_landed(uint64_t upto);  // gsdr_stream_wait_landed
 
 private:
     int d_device;

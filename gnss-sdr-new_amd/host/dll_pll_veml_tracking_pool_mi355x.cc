@@ -231,13 +231,30 @@ void SharedTrackingPool::advance_if_due(bool force)
     if (d_more || head - d_advanced >= d_batch) advance_locked(head, false);
 }
 
-bool SharedTrackingPool::pop(int slot, gsdr_trk_epoch* rec)
+namespace
+{
+uint64_t call_end(const gsdr_trk_epoch& r) { return r.sample_counter + static_cast<uint64_t>(std::max(r.consumed, 0)); }
+}  // namespace
+
+bool SharedTrackingPool::pop(int slot, uint64_t handed_end, gsdr_trk_epoch* rec)
 {
     std::lock_guard<std::mutex> lk(d_mu);
-    if (slot < 0 || d_queue[slot].empty()) return false;
+    if (slot < 0 || d_queue[slot].empty() || call_end(d_queue[slot].front()) > handed_end) return false;
     *rec = d_queue[slot].front();
     d_queue[slot].pop_front();
     return true;
+}
+
+bool SharedTrackingPool::ready(int slot, uint64_t handed_end)
+{
+    std::lock_guard<std::mutex> lk(d_mu);
+    return slot >= 0 && !d_queue[slot].empty() && call_end(d_queue[slot].front()) <= handed_end;
+}
+
+size_t SharedTrackingPool::queued(int slot)
+{
+    std::lock_guard<std::mutex> lk(d_mu);
+    return slot < 0 ? 0 : d_queue[slot].size();
 }
 
 dll_pll_veml_tracking_pool_mi355x::dll_pll_veml_tracking_pool_mi355x(const Dll_Pll_Conf& conf, int32_t signal,
@@ -326,6 +343,31 @@ int dll_pll_veml_tracking_pool_mi355x::work(const void* in, int ninput_items, ui
     int* noutput, TrackingTags* tags)
 {
     std::lock_guard<std::mutex> l(d_setlock);
+    const int c = work_locked(in, ninput_items, nitems_read, out, noutput, tags);
+    // the ring's pushes copy from the scheduler's buffer after feed() returned, and
+    // the scheduler recycles consumed items (consume_each, :2119): consume only items
+    // that landed in device memory.  An output is progress on its own (the scheduler
+    // calls again); without one, wait for the copy rather than stall the scheduler
+    if (c <= 0) return c;
+    try
+        {
+            DeviceIqRing* ring = d_pool->ring();
+            const uint64_t want = nitems_read + static_cast<uint64_t>(c);
+            const uint64_t landed = ring->landed();
+            if (landed >= want) return c;
+            if (*noutput) return static_cast<int>(landed > nitems_read ? landed - nitems_read : 0);
+            ring->wait_landed(want);
+        }
+    catch (const std::exception& e)
+        {
+            std::cerr << "dll_pll_veml_tracking_pool_mi355x: " << e.what() << '\n';
+        }
+    return c;
+}
+
+int dll_pll_veml_tracking_pool_mi355x::work_locked(const void* in, int ninput_items, uint64_t nitems_read,
+    Gnss_Synchro* out, int* noutput, TrackingTags* tags)
+{
     *noutput = 0;
     if (tags) tags->has_out = false;
     const int n = std::max(ninput_items, 0);
@@ -334,10 +376,13 @@ int dll_pll_veml_tracking_pool_mi355x::work(const void* in, int ninput_items, ui
             // the items handed over go into the pool's ring and are consumed; their
             // time tags wait for the calls that cover them
             d_pool->feed(in, nitems_read, n);
+            // items not consumed are handed again with the next call: take each tag once
+            const uint64_t from = std::max(nitems_read, d_handed_end);
             if (tags)
                 for (int i = 0; i < tags->n_in; ++i)
-                    if (tags->in[i].offset >= nitems_read && tags->in[i].offset < nitems_read + static_cast<uint64_t>(n))
+                    if (tags->in[i].offset >= from && tags->in[i].offset < nitems_read + static_cast<uint64_t>(n))
                         d_tags.push_back(tags->in[i]);
+            d_handed_end = std::max(d_handed_end, nitems_read + static_cast<uint64_t>(n));
             switch (d_state)
                 {
                 case 0:  // standby: consume at full throttle (:1806-1811)
@@ -385,9 +430,11 @@ int dll_pll_veml_tracking_pool_mi355x::work(const void* in, int ninput_items, ui
             if (d_events) d_events(3);
             return n;
         }
-    // hand out this channel's computed calls in order, up to the first that emits
+    // hand out this channel's computed calls in order, up to the first that emits;
+    // only calls inside the items handed over so far (their time tags are here)
     gsdr_trk_epoch rec;
-    while (d_state == 2 && d_pool->pop(d_slot, &rec))
+    uint64_t last_end = 0;
+    while (d_state == 2 && d_pool->pop(d_slot, d_handed_end, &rec))
         {
             d_last = rec;
             if (d_record_sink) d_record_sink(rec);
@@ -412,6 +459,7 @@ int dll_pll_veml_tracking_pool_mi355x::work(const void* in, int ninput_items, ui
                     tags->out = call_tags.out;
                 }
             d_nitems_written += static_cast<uint64_t>(*noutput);
+            last_end = end;
             if (loss_of_lock)
                 {
                     if (rec.flags & GSDR_TRK_F_OVERRUN)
@@ -428,5 +476,12 @@ int dll_pll_veml_tracking_pool_mi355x::work(const void* in, int ninput_items, ui
                 }
             if (*noutput) break;
         }
+    // one output per call, as the reference (set_max_noutput_items(1), :131): while
+    // computed calls wait behind the one emitted, consume only up to its end, so the
+    // scheduler calls again (its items are still in the input) and the backlog is
+    // handed out call by call instead of growing; otherwise every item handed over
+    // is in the ring and is consumed
+    if (*noutput && d_state == 2 && d_pool->ready(d_slot, d_handed_end))
+        return static_cast<int>(std::min<uint64_t>(static_cast<uint64_t>(n), last_end > nitems_read ? last_end - nitems_read : 0));
     return n;
 }

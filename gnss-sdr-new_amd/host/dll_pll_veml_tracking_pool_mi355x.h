@@ -74,8 +74,13 @@ public:
     // asynchronous: its records land in the queues when a later call finds it done
     // (force: when anything arrived, and wait for the records)
     void advance_if_due(bool force);
-    // the next per-call record of `slot` (in call order), taken out of the queue
-    bool pop(int slot, gsdr_trk_epoch* rec);
+    // the next per-call record of `slot` (in call order), taken out of the queue when
+    // its call ends at or before handed_end (the items its block has been handed:
+    // the time tags of a later call have not reached the block yet)
+    bool pop(int slot, uint64_t handed_end, gsdr_trk_epoch* rec);
+    // the next record is there and pop() would take it
+    bool ready(int slot, uint64_t handed_end);
+    size_t queued(int slot);  // records computed and not yet handed out
 
     uint64_t launches() const { return d_launches; }
     uint64_t window_items() const { return d_window; }
@@ -129,7 +134,7 @@ public:
     void stop_tracking() override;
     void set_event_handler(std::function<void(int)> h) override { d_events = std::move(h); }
     void msg_handler_telemetry_to_trk(int tlm_event) override;
-    // any items are useful: work() consumes what it is handed
+    // any items are useful: work() feeds what it is handed to the ring
     int forecast() const override { return 1; }
     int work(const void* in, int ninput_items, uint64_t nitems_read, Gnss_Synchro* out, int* noutput,
         TrackingTags* tags) override;
@@ -138,11 +143,16 @@ public:
     int32_t state() const override { return d_state; }
     const gsdr_trk_epoch& last_record() const override { return d_last; }
     SharedTrackingPool* pool() { return d_pool.get(); }
+    int slot() const { return d_slot; }
     // loss-of-lock records the engine marked GSDR_TRK_F_OVERRUN (a channel started
     // before the oldest item the ring still held)
     uint64_t overruns() const { return d_overruns; }
 
 private:
+    // work() without the landed-items clamp: the items it would consume
+    int work_locked(const void* in, int ninput_items, uint64_t nitems_read, Gnss_Synchro* out, int* noutput,
+        TrackingTags* tags);
+
     Dll_Pll_Conf d_conf;
     int32_t d_signal;
     std::shared_ptr<SharedTrackingPool> d_pool;
@@ -157,6 +167,7 @@ private:
     TrackingDump d_dump;  // <role>.dump: the reference's per-channel .dat (log_data), .mat on destruction
     TrackingOutput d_output;
     std::deque<GnssTimeTag> d_tags;  // input time tags not yet matched to a call
+    uint64_t d_handed_end{0};        // end of the items the scheduler has handed this block
     std::vector<GnssTimeTag> d_in_call;  // the tags of the call being emitted
     bool d_fault_pending{false};     // telemetry fault between start_tracking and the pull-in
 };

@@ -1648,6 +1648,207 @@ void test_synchro_emission(const std::string& dir)
         }
 }
 
+// GNU Radio's buffer protocol around pooled blocks: one upstream buffer of kBuf items
+// (double-mapped: every item also at +kBuf, so each reader sees one contiguous span),
+// page-locked so ring pushes DMA straight from it, with the writer overwriting every
+// item as soon as all readers consumed it.  Two pooled blocks of one pool read it:
+// A on every round, B only on every third (it lags by up to the buffer, while A's
+// pushes run the ring and the pool ahead of B's items).  Each block is called while
+// it makes progress (an output or consumed items) -- never with zero input items --
+// and its GnssTime tags come with its items.  A block must (1) consume only items
+// whose copy landed (otherwise the writer's overwrite tears the input and the records
+// change), (2) keep its record queue bounded (one output per call, consumption
+// matching production), (3) emit the per-channel blocks' outputs and output tags.
+void test_pool_recycled_buffer()
+{
+    const double fs = 4000000.0;
+    const double amp = std::sqrt(2.0 * std::pow(10.0, 5.0) / fs);
+    const std::vector<float> bits = {1, -1, -1, -1, 1, -1, 1, 1};
+    const uint32_t prns[2] = {1, 7};
+    const double dly[2] = {524.3, 2100.8};
+    const double dop[2] = {1680.0, -3250.0};
+    std::vector<SynthSat> sats;
+    std::vector<Gnss_Synchro> acq(2);
+    for (int i = 0; i < 2; ++i)
+        {
+            sats.push_back({gps_l1_ca_code_gen_float(prns[i]), 1.023e6, 1575.42e6, dly[i], dop[i], amp, {}, bits, 0.02});
+            acq[i].System = 'G';
+            acq[i].Signal[0] = '1';
+            acq[i].Signal[1] = 'C';
+            acq[i].PRN = prns[i];
+            acq[i].Channel_ID = i;
+            acq[i].Acq_delay_samples = std::fmod(std::round(dly[i]), 4000.0);
+            acq[i].Acq_doppler_hz = 250.0 * std::round(dop[i] / 250.0);
+            acq[i].Acq_samplestamp_samples = 0;
+        }
+    const auto x = synth_stream(sats, fs, static_cast<size_t>(fs * 1.6), 41, 1.0);
+    std::vector<GnssTimeTag> tags;
+    for (uint64_t off = 777; off < x.size(); off += 100000)
+        {
+            GnssTimeTag t;
+            t.offset = off;
+            t.time.week = 2300;
+            t.time.tow_ms = static_cast<int32_t>(100000 + off / 4000);
+            t.time.tow_ms_fraction = 0.5;
+            t.time.rx_time = 0.0;
+            tags.push_back(t);
+        }
+    struct Out
+    {
+        uint64_t counter;
+        bool valid;
+        double pi;
+        bool tag;
+        uint64_t tag_offset;
+        int32_t tow;
+    };
+    auto make_config = [](bool pooled) {
+        InMemoryConfiguration config;
+        config.set_property("GNSS-SDR.internal_fs_sps", "4000000");
+        config.set_property("Tracking_1C.implementation", "GPS_L1_CA_DLL_PLL_Tracking_MI355X");
+        config.set_property("Tracking_1C.item_type", "gr_complex");
+        config.set_property("Tracking_1C.pll_bw_hz", "40.0");
+        config.set_property("Tracking_1C.dll_bw_hz", "4.0");
+        config.set_property("Tracking_1C.pull_in_time_s", "0");
+        config.set_property("Channels_1C.count", "2");
+        config.set_property("Tracking_1C.mi355x_pool", pooled ? "true" : "false");
+        config.set_property("Tracking_1C.mi355x_ring", pooled ? "recycled" : "rf0");
+        return config;
+    };
+    auto tags_in = [&tags](uint64_t lo, uint64_t hi) {
+        std::vector<GnssTimeTag> v;
+        for (const auto& t : tags)
+            if (t.offset >= lo && t.offset < hi) v.push_back(t);
+        return v;
+    };
+    // the per-channel blocks (synchronous copies) on the never-rewritten stream
+    std::vector<std::vector<gsdr_trk_epoch>> ref_recs(2);
+    std::vector<std::vector<Out>> ref_outs(2);
+    {
+        InMemoryConfiguration config = make_config(false);
+        for (int c = 0; c < 2; ++c)
+            {
+                auto trk = gsdr_factory::GetTrkBlock(&config, "Tracking_1C", 1, 1, 0);
+                Gnss_Synchro g = acq[c];
+                trk->set_channel(static_cast<unsigned int>(c));
+                trk->set_gnss_synchro(&g);
+                trk->start_tracking();
+                auto* blk = dynamic_cast<DllPllTrackingAdapterMI355X*>(trk.get())->get_block();
+                blk->set_record_sink([&ref_recs, c](const gsdr_trk_epoch& r) { ref_recs[c].push_back(r); });
+                uint64_t nread = 0;
+                while (nread + static_cast<uint64_t>(blk->forecast()) <= x.size())
+                    {
+                        const int avail = static_cast<int>(std::min<uint64_t>(16384, x.size() - nread));
+                        auto in = tags_in(nread, nread + static_cast<uint64_t>(avail));
+                        TrackingTags tt;
+                        tt.in = in.data();
+                        tt.n_in = static_cast<int>(in.size());
+                        Gnss_Synchro o{};
+                        int nout = 0;
+                        const int used = blk->work(x.data() + nread, avail, nread, &o, &nout, &tt);
+                        if (nout == 1)
+                            ref_outs[c].push_back({o.Tracking_sample_counter, o.Flag_valid_symbol_output, o.Prompt_I,
+                                tt.has_out, tt.out.offset, tt.out.time.tow_ms});
+                        if (used <= 0 && nout == 0) break;
+                        nread += static_cast<uint64_t>(std::max(used, 0));
+                    }
+                blk->set_record_sink(nullptr);
+            }
+    }
+    // the pooled blocks behind the recycled buffer
+    constexpr uint64_t kBuf = 32768;
+    std::vector<std::complex<float>> buf(2 * kBuf);
+    EXPECT(gsdr_host_register(buf.data(), buf.size() * sizeof(buf[0])) == GSDR_OK, "recycled buffer: page-locked");
+    std::vector<std::vector<gsdr_trk_epoch>> recs(2);
+    std::vector<std::vector<Out>> outs(2);
+    size_t max_queue[2] = {0, 0};
+    uint64_t calls = 0, zero_consumed = 0;
+    {
+        InMemoryConfiguration config = make_config(true);
+        std::vector<std::unique_ptr<TrackingInterface>> trk;
+        std::vector<Gnss_Synchro> gs(acq);
+        std::vector<dll_pll_veml_tracking_pool_mi355x*> blk(2);
+        for (int c = 0; c < 2; ++c)
+            {
+                trk.push_back(gsdr_factory::GetTrkBlock(&config, "Tracking_1C", 1, 1, 0));
+                trk[c]->set_channel(static_cast<unsigned int>(c));
+                trk[c]->set_gnss_synchro(&gs[c]);
+                trk[c]->start_tracking();
+                blk[c] = dynamic_cast<dll_pll_veml_tracking_pool_mi355x*>(
+                    dynamic_cast<DllPllTrackingAdapterMI355X*>(trk[c].get())->get_block());
+                EXPECT(blk[c] != nullptr, "recycled buffer: pooled blocks");
+                if (!blk[c]) return;
+                blk[c]->set_record_sink([&recs, c](const gsdr_trk_epoch& r) { recs[c].push_back(r); });
+            }
+        uint64_t nread[2] = {0, 0}, written = 0;
+        const uint64_t end = x.size();
+        for (int round = 0; nread[0] < end || nread[1] < end; ++round)
+            {
+                // the writer fills every slot all readers released (overwriting at once)
+                const uint64_t limit = std::min(std::min(nread[0], nread[1]) + kBuf, end);
+                for (; written < limit; ++written)
+                    {
+                        buf[written % kBuf] = x[written];
+                        buf[written % kBuf + kBuf] = x[written];
+                    }
+                bool progress = false;
+                for (int c = 0; c < 2; ++c)
+                    {
+                        if (c == 1 && round % 3 != 0) continue;  // B's scheduler thread lags
+                        for (int guard = 0; guard < 64 && nread[c] < written; ++guard)
+                            {
+                                const int avail = static_cast<int>(written - nread[c]);
+                                auto in = tags_in(nread[c], written);
+                                TrackingTags tt;
+                                tt.in = in.data();
+                                tt.n_in = static_cast<int>(in.size());
+                                Gnss_Synchro o{};
+                                int nout = 0;
+                                const int used = blk[c]->work(buf.data() + nread[c] % kBuf, avail, nread[c], &o, &nout, &tt);
+                                ++calls;
+                                zero_consumed += used == 0 ? 1 : 0;
+                                if (nout == 1)
+                                    outs[c].push_back({o.Tracking_sample_counter, o.Flag_valid_symbol_output, o.Prompt_I,
+                                        tt.has_out, tt.out.offset, tt.out.time.tow_ms});
+                                max_queue[c] = std::max(max_queue[c], blk[c]->pool()->queued(blk[c]->slot()));
+                                if (used <= 0 && nout == 0) break;
+                                progress = true;
+                                nread[c] += static_cast<uint64_t>(std::max(used, 0));
+                            }
+                    }
+                if (!progress && written >= end) break;
+            }
+        for (int c = 0; c < 2; ++c) blk[c]->set_record_sink(nullptr);
+    }
+    gsdr_host_unregister(buf.data());
+    bool same_recs = true, same_outs = true;
+    for (int c = 0; c < 2; ++c)
+        {
+            const size_t k = std::min(recs[c].size(), ref_recs[c].size());
+            same_recs = same_recs && k > 300 && recs[c].size() + 2 >= ref_recs[c].size();
+            for (size_t e = 0; same_recs && e < k; ++e)
+                same_recs = std::memcmp(&recs[c][e], &ref_recs[c][e], sizeof(gsdr_trk_epoch)) == 0;
+            const size_t m = std::min(outs[c].size(), ref_outs[c].size());
+            same_outs = same_outs && m > 20 && outs[c].size() + 2 >= ref_outs[c].size();
+            for (size_t e = 0; same_outs && e < m; ++e)
+                {
+                    const Out& a = outs[c][e];
+                    const Out& b = ref_outs[c][e];
+                    same_outs = a.counter == b.counter && a.valid == b.valid && a.pi == b.pi && a.tag == b.tag &&
+                                (!a.tag || (a.tag_offset == b.tag_offset && a.tow == b.tow));
+                }
+        }
+    int tagged = 0;
+    for (const auto& o : ref_outs[0]) tagged += o.tag ? 1 : 0;
+    EXPECT(same_recs, "recycled buffer: pooled records identical to the per-channel blocks' (no torn input)");
+    EXPECT(same_outs && tagged > 5, "recycled buffer: outputs and output time tags identical to the per-channel blocks'");
+    EXPECT(max_queue[0] <= 24 && max_queue[1] <= 24, "recycled buffer: record queues bounded without drain calls");
+    std::printf("recycled buffer: %zu / %zu records, %zu / %zu outputs (%d tagged), max queue %zu / %zu, %llu work calls "
+                "(%llu consumed nothing)\n",
+        recs[0].size(), recs[1].size(), outs[0].size(), outs[1].size(), tagged, max_queue[0], max_queue[1],
+        static_cast<unsigned long long>(calls), static_cast<unsigned long long>(zero_consumed));
+}
+
 void test_multicorrelator(const std::vector<std::complex<float>>& capture)
 {
     const int n = 4000;
@@ -1706,6 +1907,12 @@ int main(int argc, char** argv)
             return 2;
         }
     const char* only = std::getenv("GSDR_SELFTEST_ONLY");
+    if (only && std::string(only) == "recycled")
+        {
+            test_pool_recycled_buffer();
+            if (failures == 0) std::printf("host_selftest: PASS\n");
+            return failures == 0 ? 0 : 1;
+        }
     if (only && std::string(only) == "synchro")
         {
             const char* d = std::getenv("GSDR_SELFTEST_DUMP_DIR");
@@ -1744,6 +1951,7 @@ int main(int argc, char** argv)
     test_pooled_tracking();
     test_pool_overrun();
     test_ring_keys();
+    test_pool_recycled_buffer();
     {
         const char* d = std::getenv("GSDR_SELFTEST_DUMP_DIR");
         test_synchro_emission(d ? std::string(d) : std::string("/tmp/gsdr_selftest_dump"));

@@ -97,8 +97,21 @@ void gsdr_stream_destroy(gsdr_stream* stream);
  * first_sample; pushes are contiguous (first_sample = the previous push's end;
  * the first push sets the origin).  Asynchronous H2D on the ring's copy stream,
  * ordered after every consumer launch issued so far (no overwrite of data in
- * use); n <= capacity_items. */
+ * use); n <= capacity_items.
+ * Lifetime of iq_host: the copy reads it after the call returns (from page-locked
+ * memory, gsdr_host_register, it is a DMA straight from the caller's buffer), so
+ * the n items must stay valid and unchanged until the push has landed:
+ * gsdr_stream_landed reports *landed >= first_sample + n, or
+ * gsdr_stream_wait_landed(stream, first_sample + n) returned.  A GNU Radio block
+ * that pushes its input items therefore consumes (consume_each) only items that
+ * landed -- the scheduler recycles consumed items upstream
+ * (dll_pll_veml_tracking.cc:2119). */
 int gsdr_stream_push(gsdr_stream* stream, const void* iq_host, uint64_t first_sample, uint64_t n);
+/* Every item before *landed is in device memory: the host memory of the pushes that
+ * ended there may be reused.  Non-blocking. */
+int gsdr_stream_landed(gsdr_stream* stream, uint64_t* landed);
+/* Waits until every push holding an item before `upto` has landed. */
+int gsdr_stream_wait_landed(gsdr_stream* stream, uint64_t upto);
 /* The longest contiguous window ending at the newest item: [*first_sample,
  * *first_sample + *n_items). */
 int gsdr_stream_span(gsdr_stream* stream, uint64_t* first_sample, uint64_t* n_items);
@@ -567,7 +580,9 @@ int gsdr_trk_run_stream_host(gsdr_trk* trk, gsdr_stream* ring, uint32_t max_epoc
  * max_epochs records (channel-major; only the first n_out_host[c] of channel c are
  * written), n_out_host max_channels counts, *max_epochs
  * (may be NULL) the submission's max_epochs; wait != 0 waits for the copy, wait == 0
- * returns 1 without copying while it is in flight. */
+ * returns 1 without copying while it is in flight.  Submits on one handle are
+ * serialised (each keeps its slot while it launches); a collect may run beside a
+ * submit and sees only submissions that returned GSDR_OK. */
 int gsdr_trk_submit_stream(gsdr_trk* trk, gsdr_stream* ring, uint32_t max_epochs);
 int gsdr_trk_collect(gsdr_trk* trk, int wait, gsdr_trk_epoch* out_host, uint32_t* n_out_host, uint32_t* max_epochs);
 

@@ -98,6 +98,21 @@ def magnitude_grid(x, wipe, code_fft, bit_transition=False, dtype=np.complex128)
     return M.astype(np.float32)
 
 
+def magnitude_grids(x, wipe, code_ffts, bit_transition=False):
+    """magnitude_grid for several PRNs over one block: the Doppler rows' forward
+    transforms X_d = FFT(x . w_d) (:655-662) do not depend on the PRN, so they are
+    computed once and every PRN's grid is |IFFT(X . C_p)|^2 (:663-666) -- the same
+    arithmetic as magnitude_grid, one PRN at a time (yields float32 [D][Neff])."""
+    D, N = wipe.shape
+    X = np.fft.fft(x.astype(np.complex128)[None, :] * wipe.astype(np.complex128), axis=1)
+    for cf in code_ffts:
+        R = np.fft.ifft(X * cf[None, :].astype(np.complex128), axis=1) * N
+        M = R.real ** 2 + R.imag ** 2
+        if bit_transition:
+            M = M[:, N // 2:]
+        yield M.astype(np.float32)
+
+
 def max_to_input_power_statistic(M, dwells=1):
     """pcps_acquisition.cc:511-543 (first-step branch).  Returns
     (index_time, index_doppler, grid_max, input_power, statistic)."""

@@ -1,0 +1,139 @@
+"""Large-N acquisition parity at the grid shapes the configurations ship (VERDICT r5
+item 2), not reduced grids: every PRN x Doppler cell of
+
+  C5 GPS L1 C/A  32 PRN x 81 Doppler (+-10 kHz / 250 Hz), N = 25000, pfa 0.01
+  C5 BeiDou B1I  32 PRN x 81 Doppler (+-10 kHz / 250 Hz), N = 25000, pfa 0.01
+  C5 Galileo E1  36 PRN x 41 Doppler (+-5 kHz / 250 Hz),  N = 100000 (4 ms), pfa 0.01
+  C4 Galileo E1  36 PRN x 80 Doppler (+-5 kHz / 125 Hz),  bit transition, N = 64000,
+                 peak ratio (pfa 0)
+
+as profiles/configs_bench.py times them, on the default (split register four-step)
+path, against oracle/pcps.py (acquisition_core, pcps_acquisition.cc:511-612,
+:655-686).  Same bar as the C2 test (test_gpu_acq.py): peak / input power / second
+peak / statistic within 1e-4 relative, cells equal or an H3 near tie (the oracle's
+grid value at the GPU's cell within 1e-4 of its maximum); the exact-cell and near-tie
+counts are printed and, with GSDR_PARITY_LOG, appended as JSON lines."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import gsdr
+from gsdr import synth
+from oracle import pcps
+from test_gpu_acq import RTOL, _check_result
+
+pytestmark = pytest.mark.gpu
+
+
+def _log(tag, P, exact, extra=None):
+    line = {"tag": tag, "prns": P, "exact_cells": int(exact), "near_ties": int(P - exact)}
+    line.update(extra or {})
+    print("parity acq", json.dumps(line))
+    if os.environ.get("GSDR_PARITY_LOG"):
+        with open(os.environ["GSDR_PARITY_LOG"], "a") as f:
+            f.write(json.dumps(line) + "\n")
+
+
+def _run_grid(tag, fs, N, x, codes, prns, dmax, dstep, pfa, chip, ms, spcode, visible):
+    acq = gsdr.Acquisition(fs, N, dmax, dstep, pfa=pfa, max_prns=len(prns), chip_rate=chip, sampled_ms=ms,
+                           ms_per_code=ms, samples_per_code=spcode)
+    assert acq.fft_size == N
+    acq.set_local_codes(codes, prns)
+    res = acq.run(x)[0]
+    D = acq.num_doppler_bins
+    wipe = pcps.doppler_wipeoffs(fs, N, dmax, dstep, D)
+    spc = int(np.ceil(fs / chip))
+    exact = 0
+    for i, M in enumerate(pcps.magnitude_grids(x, wipe, [pcps.fft_code(c, N, N) for c in codes])):
+        exact += _check_result(res[i], M, pfa, spc, fs, dmax, dstep, spcode)
+        assert res[i]["prn"] == prns[i]
+        if pfa > 0:
+            stat = pcps.max_to_input_power_statistic(M)[4]
+            if abs(stat - acq.threshold) > 1e-3 * acq.threshold:
+                assert bool(res[i]["positive"]) == bool(stat > acq.threshold)
+    acq.close()
+    _log(tag, len(prns), exact, {"N": N, "D": D})
+    # every visible satellite is an exact cell (a near tie needs two equal maxima)
+    vis_idx = [i for i, p in enumerate(prns) if p in visible]
+    assert exact >= len(vis_idx)
+    return res
+
+
+@pytest.mark.parametrize("system", ["gps", "bds"])
+def test_c5_25msps_32prn_81doppler(system):
+    fs, N, dmax, dstep = 25000000, 25000, 10000, 250
+    rng = np.random.default_rng(2500 + (system == "bds"))
+    prns = np.arange(1, 33)
+    if system == "gps":
+        sats = synth.random_constellation(10, seed_offset=25, cn0_dbhz=45.0, max_doppler=9500.0)
+        x = synth.gps_l1_iq(fs, N, sats, seed_offset=25)
+        codes = np.stack([synth.gps_ca_sampled(int(p), fs) for p in prns])
+        chip = 1023000.0
+    else:
+        vis = [6, 9, 14, 22, 30]
+        sats = [synth.Satellite(p, float(rng.uniform(-9000, 9000)), float(rng.uniform(0, 2046)), 45.0,
+                                float(rng.uniform(0, 6.28))) for p in vis]
+        x = synth.bds_b1i_iq(fs, N, sats, seed_offset=26)
+        codes = np.stack([synth.bds_b1i_sampled(int(p), fs)[:N] for p in prns])
+        chip = 2046000.0
+    _run_grid("c5_%s_full" % system, fs, N, x, codes, prns, dmax, dstep, 0.01, chip, 1, float(N),
+              {s.prn for s in sats})
+
+
+def test_c5_galileo_36prn_41doppler_100000():
+    fs, N, dmax, dstep = 25000000, 100000, 5000, 250
+    rng = np.random.default_rng(100000)
+    vis = [3, 11, 19, 27, 33]
+    sats = [synth.GalileoSatellite(p, float(rng.uniform(-4500, 4500)), float(rng.uniform(0, 4092)), 45.0,
+                                   float(rng.uniform(0, 6.28))) for p in vis]
+    x = synth.gal_e1_iq(fs, N, sats, seed_offset=27)
+    prns = np.arange(1, 37)
+    codes = np.stack([synth.gal_e1_sampled(int(p), fs)[:N] for p in prns])
+    _run_grid("c5_galileo_full", fs, N, x, codes, prns, dmax, dstep, 0.01, 1023000.0, 4, float(N), set(vis))
+
+
+def test_c4_bit_transition_36prn_80doppler_64000():
+    """Peak ratio with bit_transition_flag: FFT 2 x 32000, the code in the second
+    half, outputs [32000, 64000) (pcps_acquisition.cc:85-92, :188-193, :671); the
+    second peak's exclusion wraps at d_fft_size (the reference's quirk)."""
+    fs, C, dmax, dstep = 8000000, 32000, 5000, 125
+    N = 2 * C
+    rng = np.random.default_rng(64000)
+    vis = [2, 8, 15, 24, 31]
+    sats = [synth.GalileoSatellite(p, float(rng.uniform(-4500, 4500)), float(rng.uniform(0, 4092)), 46.0,
+                                   float(rng.uniform(0, 6.28))) for p in vis]
+    x = synth.gal_e1_iq(fs, N, sats, seed_offset=28)
+    prns = np.arange(1, 37)
+    codes = np.stack([np.resize(synth.gal_e1_sampled(int(p), fs), N) for p in prns])
+    acq = gsdr.Acquisition(fs, N, dmax, dstep, pfa=0.0, max_prns=len(prns), sampled_ms=4, ms_per_code=4,
+                           bit_transition=True, samples_per_code=float(C))
+    assert acq.fft_size == N and acq.num_doppler_bins == 80
+    acq.set_local_codes(codes, prns)
+    thr = 2.5
+    acq.set_threshold(thr)
+    res = acq.run(x)[0]
+    D = acq.num_doppler_bins
+    wipe = pcps.doppler_wipeoffs(fs, N, dmax, dstep, D)
+    spc = int(np.ceil(fs / 1023000.0))
+    exact = 0
+    cfs = [pcps.fft_code(c, N, N, bit_transition=True) for c in codes]
+    for i, M in enumerate(pcps.magnitude_grids(x, wipe, cfs, bit_transition=True)):
+        full = np.zeros((D, N), np.float32)
+        full[:, :M.shape[1]] = M
+        ti, di, peak, second, stat = pcps.first_vs_second_peak_statistic(full, spc, N)
+        r = res[i]
+        assert r["prn"] == prns[i]
+        if (r["doppler_index"], r["code_phase"]) != (di, ti):  # near tie (H3)
+            assert abs(M[r["doppler_index"], r["code_phase"]] - peak) <= RTOL * peak, (i, r, di, ti)
+            continue
+        exact += 1
+        assert abs(r["peak"] - peak) <= RTOL * peak
+        assert abs(r["second_peak"] - second) <= RTOL * second
+        assert abs(r["test_statistic"] - stat) <= RTOL * stat
+        if abs(stat - thr) > 1e-3 * thr:
+            assert r["positive"] == int(stat > thr)
+    acq.close()
+    _log("c4_bit_transition_full", len(prns), exact, {"N": N, "D": D})
+    assert exact >= len(vis)

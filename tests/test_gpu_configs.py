@@ -130,7 +130,7 @@ def test_c3_gps_16msps_12_channel_pool():
                 tag="c3")
 
 
-@pytest.mark.parametrize("fs", [16.384e6, 16.896e6, 16.897e6, 20.0e6, 24.6e6])
+@pytest.mark.parametrize("fs", [16.384e6, 16.896e6, 16.897e6, 16.8965e6, 20.0e6, 24.6e6])
 def test_streamed_chunk_tails(fs):
     """Streamed calls (vector_length > 4096) against the 8192-sample stream chunks of
     a GPS gr_complex pool: no tail (16384), a tail of exactly 512 samples riding with

@@ -1053,6 +1053,10 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(RP:
 #ifndef GSDR_SPLIT_DMA
 #define GSDR_SPLIT_DMA 0
 #endif
+// the smallest outer radix staged (1: the 25000 / 32000 plans too)
+#ifndef GSDR_SPLIT_DMA_MIN_ROUT
+#define GSDR_SPLIT_DMA_MIN_ROUT 2
+#endif
 // waves per SIMD the staged grid pass is compiled for (4: <= 128 VGPRs, two 512-lane
 // workgroups per CU as the VGPR form had)
 #ifndef GSDR_SPLIT_WPE
@@ -1060,7 +1064,7 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(RP:
 #endif
 template <int ROUT, class RP, bool HALF, bool ARG = false>
 __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(
-    ARG ? 1 : (ROUT > 1 && GSDR_SPLIT_DMA > 0 ? GSDR_SPLIT_WPE : RP::WPE)))) acq_correlate_split_kernel(
+    ARG ? 1 : (ROUT >= GSDR_SPLIT_DMA_MIN_ROUT && GSDR_SPLIT_DMA > 0 ? GSDR_SPLIT_WPE : RP::WPE)))) acq_correlate_split_kernel(
     const float2* __restrict__ X, const float2* __restrict__ code_fft, RowStat* __restrict__ stats,
     const float2* __restrict__ tw, uint32_t D, uint32_t P, uint32_t nblocks, uint32_t pgs, XMap xm,
     const gsdr_acq_result* __restrict__ sel, unsigned long long* __restrict__ keys, float* __restrict__ rowbuf,
@@ -1140,8 +1144,8 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(
         // column-major, so a column's transform runs (and its registers settle) before
         // the next column accumulates, as in the VGPR form
         constexpr int U = R * ROUT;
-        constexpr int SEGS = U * CPL;
-        constexpr int PAIRS = (SEGS + 1) / 2;    // one X and one code copy per two segments
+        constexpr int PPC = (U + 1) / 2;          // copy pairs per column set (an odd U repeats its last unit)
+        constexpr int PAIRS = PPC * CPL;         // one X and one code copy per two segments
         const int wave = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
         char* ring = reinterpret_cast<char*>(lds_raw) + (size_t)wave * DEPTH * 2048;
         const int half = lane >> 5, l32 = lane & 31;
@@ -1150,19 +1154,20 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(
             constexpr int k = decltype(kc)::value;
             if constexpr (k < PAIRS)
                 {
-                    // lanes 0-31: segment 2k, lanes 32-63: segment 2k + 1 (the last pair of an
-                    // odd count repeats its segment); two columns (16 B) per lane
-                    constexpr int sa = 2 * k, sb = 2 * k + 1 < SEGS ? 2 * k + 1 : 2 * k;
-                    constexpr int ua = sa % U, ca = sa / U, ub = sb % U, cb = sb / U;
-                    constexpr int ea = (ua % ROUT) * (int)M + (ua / ROUT) * L + ca * NT;
-                    constexpr int eb = (ub % ROUT) * (int)M + (ub / ROUT) * L + cb * NT;
-                    // this lane's 16 bytes: the lane part in voffset, the segment's element
-                    // offset as the scalar offset; bounds-checked buffer copies (lanes past
-                    // column L - 1 copy bytes no lane reads, past the row's end zeros)
-                    const int so = (half ? eb - ea : 0) * 8;
+                    // lanes 0-31: unit 2kk of column set c, lanes 32-63: unit 2kk + 1 (an odd
+                    // unit count repeats its last); two columns (16 B) per lane
+                    constexpr int c = k / PPC, kk = k % PPC;
+                    constexpr int ua = 2 * kk, ub = 2 * kk + 1 < U ? 2 * kk + 1 : 2 * kk;
+                    constexpr int ea = (ua % ROUT) * (int)M + (ua / ROUT) * L + c * NT;
+                    constexpr int eb = (ub % ROUT) * (int)M + (ub / ROUT) * L + c * NT;
+                    // this lane's 16 bytes: the lane part in voffset, the first segment's
+                    // element offset as the (uniform) scalar offset; bounds-checked buffer
+                    // copies (lanes past column L - 1 copy bytes no lane reads, past the
+                    // row's end zeros)
+                    const int voff = lane_off + half * ((eb - ea) * 8);
                     char* dst = ring + (k % DEPTH) * 2048;
-                    __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (gsdr_lvoid*)dst, 16, lane_off, ea * 8 + so, 0, 0);
-                    __builtin_amdgcn_raw_ptr_buffer_load_lds(crs, (gsdr_lvoid*)(dst + 1024), 16, lane_off, ea * 8 + so, 0, 0);
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (gsdr_lvoid*)dst, 16, voff, ea * 8, 0, 0);
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(crs, (gsdr_lvoid*)(dst + 1024), 16, voff, ea * 8, 0, 0);
                 }
         };
         // the lane's column within its segment (clamped lanes read column L - 1's)
@@ -1179,10 +1184,10 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(
             __builtin_amdgcn_s_waitcnt((younger & 15) | (7 << 4) | (15 << 8) | ((younger >> 4) << 14));
             const char* src = ring + (k % DEPTH) * 2048;
             auto seg = [&](auto jc) {
-                constexpr int sidx = 2 * k + decltype(jc)::value;
-                if constexpr (sidx < SEGS)
+                constexpr int c = k / PPC, u = 2 * (k % PPC) + decltype(jc)::value;
+                if constexpr (u < U)
                     {
-                        constexpr int u = sidx % U, c = sidx / U, n1 = u / ROUT, r = u % ROUT;
+                        constexpr int n1 = u / ROUT, r = u % ROUT;
                         if (L % NT == 0 || wbase + c * NT < L)
                             {
                                 const int off = decltype(jc)::value * 512 + cl[c] * 8;
@@ -1210,11 +1215,12 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(
             // the slot's reads are done (their values are used above): refill it
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             issue(std::integral_constant<int, k + DEPTH>{});
-            // a column's last segment: its transform, while the next column's copies land
-            constexpr int last = 2 * k + 1 < SEGS ? 2 * k + 1 : 2 * k;
-            if constexpr ((last + 1) % U == 0)
+            // a column's last pair: its transform, while the next column's copies land
+            // (fenced: interleaved with the next column's sums it spilled)
+            if constexpr ((k + 1) % PPC == 0)
                 {
-                    constexpr int c = last / U;
+                    constexpr int c = k / PPC;
+                    __builtin_amdgcn_sched_barrier(0);
                     if (L % NT == 0 || wbase + c * NT < L)
                         {
                             const int n2 = min((int)threadIdx.x + c * NT, L - 1);
@@ -1227,16 +1233,16 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(
                                 }
                             gsdr::pk::apply_powers<R>(v[c], gsdr::pk::from(tw[ROUT * n2]));
                         }
+                    __builtin_amdgcn_sched_barrier(0);
                 }
         };
-        static_assert(U % 2 == 0, "a copy pair stays inside one column set");
         gsdr::pk::static_for<0, PAIRS>(step);
         // phase 2 writes rows over the rings: every wave's reads are done first
         __syncthreads();
     };
     auto phase1 = [&](auto qc) {
         constexpr int Q = decltype(qc)::value;
-        if constexpr (ROUT > 1 && GSDR_SPLIT_DMA > 0)
+        if constexpr (ROUT >= GSDR_SPLIT_DMA_MIN_ROUT && GSDR_SPLIT_DMA > 0)
             {
                 phase1_dma(qc);
                 return;

@@ -1048,12 +1048,13 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(RP:
 // recomputation (acq_argmax_four_kernel: 144 workgroups at C5 Galileo).
 // The input factor W_N^{m q} of sub-transform q is a compile-time root per column row
 // and one table read per column (r04e: C4 bit transition +11 % over R reads).
-// ROUT > 1 phase 1 staged through per-wave LDS rings: the copies in flight per wave
-// (2 KB of LDS each); 0: products straight from VGPR loads
+// phase 1 staged through per-wave LDS rings (split_staged): the copies in flight per
+// wave (2 KB of LDS each); 0: products straight from VGPR loads everywhere
 #ifndef GSDR_SPLIT_DMA
-#define GSDR_SPLIT_DMA 0
+#define GSDR_SPLIT_DMA 4
 #endif
-// the smallest outer radix staged (1: the 25000 / 32000 plans too)
+// the smallest outer radix staged (1: the 512-lane 25000 plan too), besides the
+// one-column-per-lane plans, which are staged at any outer radix
 #ifndef GSDR_SPLIT_DMA_MIN_ROUT
 #define GSDR_SPLIT_DMA_MIN_ROUT 2
 #endif
@@ -1062,9 +1063,28 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(RP:
 #ifndef GSDR_SPLIT_WPE
 #define GSDR_SPLIT_WPE 4
 #endif
+// which split plans stage phase 1 (r06, profiles/r06b3: 100000 = 4 x 25000 118 -> 133
+// Msps, 64000 = 2 x 32000 88 -> 98, 32000 (one column per lane on 1024 lanes) 105 ->
+// 118; the 512-lane 25000 plan, whose loads already go out 50 per column at once,
+// 143 -> 138: left on VGPR loads)
+template <int ROUT, class RP>
+constexpr bool split_staged()
+{
+    return GSDR_SPLIT_DMA > 0 && (ROUT >= GSDR_SPLIT_DMA_MIN_ROUT || RP::CPL == 1);
+}
+
+// dynamic LDS of a split launch: phase 2's rows (+ the reduction slots) or, staged,
+// each wave's ring of GSDR_SPLIT_DMA 2 KB copy slots, whichever is larger
+template <int ROUT, class RP>
+constexpr size_t split_lds_bytes()
+{
+    constexpr size_t ring = split_staged<ROUT, RP>() ? (size_t)(RP::NT / 64) * GSDR_SPLIT_DMA * 2048 : 0;
+    return ring > RP::lds_bytes() ? ring : RP::lds_bytes();
+}
+
 template <int ROUT, class RP, bool HALF, bool ARG = false>
 __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(
-    ARG ? 1 : (ROUT >= GSDR_SPLIT_DMA_MIN_ROUT && GSDR_SPLIT_DMA > 0 ? GSDR_SPLIT_WPE : RP::WPE)))) acq_correlate_split_kernel(
+    ARG ? 1 : (split_staged<ROUT, RP>() ? GSDR_SPLIT_WPE : RP::WPE)))) acq_correlate_split_kernel(
     const float2* __restrict__ X, const float2* __restrict__ code_fft, RowStat* __restrict__ stats,
     const float2* __restrict__ tw, uint32_t D, uint32_t P, uint32_t nblocks, uint32_t pgs, XMap xm,
     const gsdr_acq_result* __restrict__ sel, unsigned long long* __restrict__ keys, float* __restrict__ rowbuf,
@@ -1242,7 +1262,7 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(
     };
     auto phase1 = [&](auto qc) {
         constexpr int Q = decltype(qc)::value;
-        if constexpr (ROUT >= GSDR_SPLIT_DMA_MIN_ROUT && GSDR_SPLIT_DMA > 0)
+        if constexpr (split_staged<ROUT, RP>())
             {
                 phase1_dma(qc);
                 return;

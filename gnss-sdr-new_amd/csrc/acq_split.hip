@@ -72,7 +72,7 @@ int launch_one(gsdr_acq* a, uint32_t nblocks, hipStream_t s, const gsdr_acq_resu
     if (ROUT > 1 && !ARG)
         GSDR_HIP(hipMemsetAsync(a->d_stats, 0, (size_t)nblocks * a->nprn * a->D * sizeof(RowStat), s));
     const uint32_t grid = ARG ? nblocks * a->nprn * ROUT : nblocks * a->D * a->nprn * ROUT;
-    hipLaunchKernelGGL((acq_correlate_split_kernel<ROUT, RP, HALF, ARG>), dim3(grid), dim3(RP::NT), RP::lds_bytes(), s,
+    hipLaunchKernelGGL((acq_correlate_split_kernel<ROUT, RP, HALF, ARG>), dim3(grid), dim3(RP::NT), (split_lds_bytes<ROUT, RP>()), s,
         a->d_X, a->d_code_fft, a->d_stats, a->d_tw, a->D, a->nprn, nblocks, prn_group(a->nprn, a->N), a->xm, sel,
         a->d_keys, rowbuf, psum);
     GSDR_HIP(hipGetLastError());
@@ -83,9 +83,9 @@ template <int ROUT, class RP, bool HALF>
 int attrs_one()
 {
     GSDR_HIP(hipFuncSetAttribute((const void*)acq_correlate_split_kernel<ROUT, RP, HALF>,
-        hipFuncAttributeMaxDynamicSharedMemorySize, (int)RP::lds_bytes()));
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)(split_lds_bytes<ROUT, RP>())));
     GSDR_HIP(hipFuncSetAttribute((const void*)acq_correlate_split_kernel<ROUT, RP, HALF, true>,
-        hipFuncAttributeMaxDynamicSharedMemorySize, (int)RP::lds_bytes()));
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)(split_lds_bytes<ROUT, RP>())));
     return GSDR_OK;
 }
 

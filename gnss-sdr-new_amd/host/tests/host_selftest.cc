@@ -1701,6 +1701,7 @@ void test_pool_recycled_buffer()
         bool tag;
         uint64_t tag_offset;
         int32_t tow;
+        bool drained;  // handed out by the end-of-stream drain (no tags passed)
     };
     auto make_config = [](bool pooled) {
         InMemoryConfiguration config;
@@ -1748,105 +1749,154 @@ void test_pool_recycled_buffer()
                         const int used = blk->work(x.data() + nread, avail, nread, &o, &nout, &tt);
                         if (nout == 1)
                             ref_outs[c].push_back({o.Tracking_sample_counter, o.Flag_valid_symbol_output, o.Prompt_I,
-                                tt.has_out, tt.out.offset, tt.out.time.tow_ms});
+                                tt.has_out, tt.out.offset, tt.out.time.tow_ms, false});
                         if (used <= 0 && nout == 0) break;
                         nread += static_cast<uint64_t>(std::max(used, 0));
                     }
                 blk->set_record_sink(nullptr);
             }
     }
-    // the pooled blocks behind the recycled buffer
-    constexpr uint64_t kBuf = 32768;
-    std::vector<std::complex<float>> buf(2 * kBuf);
-    EXPECT(gsdr_host_register(buf.data(), buf.size() * sizeof(buf[0])) == GSDR_OK, "recycled buffer: page-locked");
-    std::vector<std::vector<gsdr_trk_epoch>> recs(2);
-    std::vector<std::vector<Out>> outs(2);
-    size_t max_queue[2] = {0, 0};
-    uint64_t calls = 0, zero_consumed = 0;
+    // the pooled blocks behind the upstream buffer: kBuf items, recycled at once
+    // (recycle), or the whole stream (no item overwritten: the same control flow
+    // without the writer's overwrites, which separates a torn input from the rest)
+    struct PooledRun
     {
-        InMemoryConfiguration config = make_config(true);
-        std::vector<std::unique_ptr<TrackingInterface>> trk;
-        std::vector<Gnss_Synchro> gs(acq);
-        std::vector<dll_pll_veml_tracking_pool_mi355x*> blk(2);
+        std::vector<std::vector<gsdr_trk_epoch>> recs{2};
+        std::vector<std::vector<Out>> outs{2};
+        size_t max_queue[2] = {0, 0};
+        uint64_t calls = 0, zero_consumed = 0;
+    };
+    auto run_pooled = [&](bool recycle) {
+        PooledRun pr;
+        // the scheduler's buffer: its writer runs at most kLead items ahead of the
+        // slowest reader; slots are reused (recycle) or every item has its own
+        constexpr uint64_t kLead = 32768;
+        const uint64_t kBuf = recycle ? kLead : static_cast<uint64_t>(x.size());
+        std::vector<std::complex<float>> buf(2 * kBuf);
+        EXPECT(gsdr_host_register(buf.data(), buf.size() * sizeof(buf[0])) == GSDR_OK, "recycled buffer: page-locked");
+        {
+            InMemoryConfiguration config = make_config(true);
+            config.set_property("Tracking_1C.mi355x_ring", recycle ? "recycled" : "static");
+            std::vector<std::unique_ptr<TrackingInterface>> trk;
+            std::vector<Gnss_Synchro> gs(acq);
+            std::vector<dll_pll_veml_tracking_pool_mi355x*> blk(2);
+            for (int c = 0; c < 2; ++c)
+                {
+                    trk.push_back(gsdr_factory::GetTrkBlock(&config, "Tracking_1C", 1, 1, 0));
+                    trk[c]->set_channel(static_cast<unsigned int>(c));
+                    trk[c]->set_gnss_synchro(&gs[c]);
+                    trk[c]->start_tracking();
+                    blk[c] = dynamic_cast<dll_pll_veml_tracking_pool_mi355x*>(
+                        dynamic_cast<DllPllTrackingAdapterMI355X*>(trk[c].get())->get_block());
+                    EXPECT(blk[c] != nullptr, "recycled buffer: pooled blocks");
+                    if (!blk[c]) return pr;
+                    blk[c]->set_record_sink([&pr, c](const gsdr_trk_epoch& r) { pr.recs[c].push_back(r); });
+                }
+            uint64_t nread[2] = {0, 0}, written = 0;
+            const uint64_t end = x.size();
+            for (int round = 0; nread[0] < end || nread[1] < end; ++round)
+                {
+                    // the writer fills every slot all readers released (overwriting at once)
+                    const uint64_t limit = std::min(std::min(nread[0], nread[1]) + kLead, end);
+                    for (; written < limit; ++written)
+                        {
+                            buf[written % kBuf] = x[written];
+                            buf[written % kBuf + kBuf] = x[written];
+                        }
+                    bool progress = false;
+                    for (int c = 0; c < 2; ++c)
+                        {
+                            if (c == 1 && round % 3 != 0) continue;  // B's scheduler thread lags
+                            for (int guard = 0; guard < 64 && nread[c] < written; ++guard)
+                                {
+                                    // GNU Radio hands at most the buffer's worth ahead of the reader
+                                    const int avail = static_cast<int>(std::min<uint64_t>(written - nread[c], kLead));
+                                    auto in = tags_in(nread[c], nread[c] + static_cast<uint64_t>(avail));
+                                    TrackingTags tt;
+                                    tt.in = in.data();
+                                    tt.n_in = static_cast<int>(in.size());
+                                    Gnss_Synchro o{};
+                                    int nout = 0;
+                                    const int used =
+                                        blk[c]->work(buf.data() + nread[c] % kBuf, avail, nread[c], &o, &nout, &tt);
+                                    ++pr.calls;
+                                    pr.zero_consumed += used == 0 ? 1 : 0;
+                                    if (nout == 1)
+                                        pr.outs[c].push_back({o.Tracking_sample_counter, o.Flag_valid_symbol_output,
+                                            o.Prompt_I, tt.has_out, tt.out.offset, tt.out.time.tow_ms, false});
+                                    pr.max_queue[c] = std::max(pr.max_queue[c], blk[c]->pool()->queued(blk[c]->slot()));
+                                    if (used <= 0 && nout == 0) break;
+                                    progress = true;
+                                    nread[c] += static_cast<uint64_t>(std::max(used, 0));
+                                }
+                        }
+                    if (!progress && written >= end) break;
+                }
+            // end of the stream (only here): the blocks compute what they were handed
+            // and hand out the rest
+            for (int c = 0; c < 2; ++c)
+                drain_block(blk[c], nread[c], [&pr, c](const Gnss_Synchro& o, int nout) {
+                    if (nout == 1)
+                        pr.outs[c].push_back({o.Tracking_sample_counter, o.Flag_valid_symbol_output, o.Prompt_I, false, 0, 0, true});
+                });
+            for (int c = 0; c < 2; ++c) blk[c]->set_record_sink(nullptr);
+        }
+        gsdr_host_unregister(buf.data());
+        return pr;
+    };
+    auto compare = [&](const PooledRun& pr, const char* what, bool& same_recs, bool& same_outs) {
+        same_recs = true;
+        same_outs = true;
         for (int c = 0; c < 2; ++c)
             {
-                trk.push_back(gsdr_factory::GetTrkBlock(&config, "Tracking_1C", 1, 1, 0));
-                trk[c]->set_channel(static_cast<unsigned int>(c));
-                trk[c]->set_gnss_synchro(&gs[c]);
-                trk[c]->start_tracking();
-                blk[c] = dynamic_cast<dll_pll_veml_tracking_pool_mi355x*>(
-                    dynamic_cast<DllPllTrackingAdapterMI355X*>(trk[c].get())->get_block());
-                EXPECT(blk[c] != nullptr, "recycled buffer: pooled blocks");
-                if (!blk[c]) return;
-                blk[c]->set_record_sink([&recs, c](const gsdr_trk_epoch& r) { recs[c].push_back(r); });
-            }
-        uint64_t nread[2] = {0, 0}, written = 0;
-        const uint64_t end = x.size();
-        for (int round = 0; nread[0] < end || nread[1] < end; ++round)
-            {
-                // the writer fills every slot all readers released (overwriting at once)
-                const uint64_t limit = std::min(std::min(nread[0], nread[1]) + kBuf, end);
-                for (; written < limit; ++written)
+                const size_t k = std::min(pr.recs[c].size(), ref_recs[c].size());
+                bool ok = k > 300 && pr.recs[c].size() + 2 >= ref_recs[c].size();
+                size_t e = 0;
+                for (; ok && e < k; ++e) ok = std::memcmp(&pr.recs[c][e], &ref_recs[c][e], sizeof(gsdr_trk_epoch)) == 0;
+                if (!ok && e > 0 && e <= k)
                     {
-                        buf[written % kBuf] = x[written];
-                        buf[written % kBuf + kBuf] = x[written];
+                        const gsdr_trk_epoch& a = pr.recs[c][e - 1];
+                        const gsdr_trk_epoch& b = ref_recs[c][e - 1];
+                        size_t off = 0;
+                        while (off < sizeof(gsdr_trk_epoch) &&
+                               reinterpret_cast<const char*>(&a)[off] == reinterpret_cast<const char*>(&b)[off])
+                            ++off;
+                        std::fprintf(stderr,
+                            "%s: channel %d record %zu of %zu / %zu differs at byte %zu: counter %llu / %llu, state %d / %d, "
+                            "prompt %.9g / %.9g\n",
+                            what, c, e - 1, pr.recs[c].size(), ref_recs[c].size(), off,
+                            static_cast<unsigned long long>(a.sample_counter), static_cast<unsigned long long>(b.sample_counter),
+                            a.state, b.state, a.prompt_i, b.prompt_i);
                     }
-                bool progress = false;
-                for (int c = 0; c < 2; ++c)
+                same_recs = same_recs && ok;
+                const size_t m = std::min(pr.outs[c].size(), ref_outs[c].size());
+                same_outs = same_outs && m > 10 && pr.outs[c].size() >= ref_outs[c].size();
+                for (size_t i = 0; same_outs && i < m; ++i)
                     {
-                        if (c == 1 && round % 3 != 0) continue;  // B's scheduler thread lags
-                        for (int guard = 0; guard < 64 && nread[c] < written; ++guard)
-                            {
-                                const int avail = static_cast<int>(written - nread[c]);
-                                auto in = tags_in(nread[c], written);
-                                TrackingTags tt;
-                                tt.in = in.data();
-                                tt.n_in = static_cast<int>(in.size());
-                                Gnss_Synchro o{};
-                                int nout = 0;
-                                const int used = blk[c]->work(buf.data() + nread[c] % kBuf, avail, nread[c], &o, &nout, &tt);
-                                ++calls;
-                                zero_consumed += used == 0 ? 1 : 0;
-                                if (nout == 1)
-                                    outs[c].push_back({o.Tracking_sample_counter, o.Flag_valid_symbol_output, o.Prompt_I,
-                                        tt.has_out, tt.out.offset, tt.out.time.tow_ms});
-                                max_queue[c] = std::max(max_queue[c], blk[c]->pool()->queued(blk[c]->slot()));
-                                if (used <= 0 && nout == 0) break;
-                                progress = true;
-                                nread[c] += static_cast<uint64_t>(std::max(used, 0));
-                            }
+                        const Out& a = pr.outs[c][i];
+                        const Out& b = ref_outs[c][i];
+                        same_outs = a.counter == b.counter && a.valid == b.valid && a.pi == b.pi &&
+                                    (a.drained || (a.tag == b.tag && (!a.tag || (a.tag_offset == b.tag_offset && a.tow == b.tow))));
                     }
-                if (!progress && written >= end) break;
             }
-        for (int c = 0; c < 2; ++c) blk[c]->set_record_sink(nullptr);
-    }
-    gsdr_host_unregister(buf.data());
-    bool same_recs = true, same_outs = true;
-    for (int c = 0; c < 2; ++c)
-        {
-            const size_t k = std::min(recs[c].size(), ref_recs[c].size());
-            same_recs = same_recs && k > 300 && recs[c].size() + 2 >= ref_recs[c].size();
-            for (size_t e = 0; same_recs && e < k; ++e)
-                same_recs = std::memcmp(&recs[c][e], &ref_recs[c][e], sizeof(gsdr_trk_epoch)) == 0;
-            const size_t m = std::min(outs[c].size(), ref_outs[c].size());
-            same_outs = same_outs && m > 20 && outs[c].size() + 2 >= ref_outs[c].size();
-            for (size_t e = 0; same_outs && e < m; ++e)
-                {
-                    const Out& a = outs[c][e];
-                    const Out& b = ref_outs[c][e];
-                    same_outs = a.counter == b.counter && a.valid == b.valid && a.pi == b.pi && a.tag == b.tag &&
-                                (!a.tag || (a.tag_offset == b.tag_offset && a.tow == b.tow));
-                }
-        }
+        std::printf("%s: %zu / %zu records (per-channel %zu / %zu), %zu / %zu outputs, max queue %zu / %zu, %llu work "
+                    "calls (%llu consumed nothing)\n",
+            what, pr.recs[0].size(), pr.recs[1].size(), ref_recs[0].size(), ref_recs[1].size(), pr.outs[0].size(),
+            pr.outs[1].size(), pr.max_queue[0], pr.max_queue[1], static_cast<unsigned long long>(pr.calls),
+            static_cast<unsigned long long>(pr.zero_consumed));
+    };
     int tagged = 0;
     for (const auto& o : ref_outs[0]) tagged += o.tag ? 1 : 0;
-    EXPECT(same_recs, "recycled buffer: pooled records identical to the per-channel blocks' (no torn input)");
-    EXPECT(same_outs && tagged > 5, "recycled buffer: outputs and output time tags identical to the per-channel blocks'");
-    EXPECT(max_queue[0] <= 24 && max_queue[1] <= 24, "recycled buffer: record queues bounded without drain calls");
-    std::printf("recycled buffer: %zu / %zu records, %zu / %zu outputs (%d tagged), max queue %zu / %zu, %llu work calls "
-                "(%llu consumed nothing)\n",
-        recs[0].size(), recs[1].size(), outs[0].size(), outs[1].size(), tagged, max_queue[0], max_queue[1],
-        static_cast<unsigned long long>(calls), static_cast<unsigned long long>(zero_consumed));
+    const PooledRun still = run_pooled(false);
+    bool rs = false, os = false;
+    compare(still, "pooled blocks, stream never overwritten", rs, os);
+    EXPECT(rs, "pooled blocks (no overwrite): records identical to the per-channel blocks'");
+    EXPECT(os && tagged > 5, "pooled blocks (no overwrite): outputs and output time tags identical to the per-channel blocks'");
+    const PooledRun rec = run_pooled(true);
+    compare(rec, "pooled blocks, recycled upstream buffer", rs, os);
+    EXPECT(rs, "recycled buffer: pooled records identical to the per-channel blocks' (no torn input)");
+    EXPECT(os, "recycled buffer: outputs and output time tags identical to the per-channel blocks'");
+    EXPECT(rec.max_queue[0] <= 24 && rec.max_queue[1] <= 24, "recycled buffer: record queues bounded without drain calls");
 }
 
 void test_multicorrelator(const std::vector<std::complex<float>>& capture)

@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 export GSDR_PARITY_LOG=$OUT/parity_spread.jsonl
 rm -f "$GSDR_PARITY_LOG"
 echo "== recycled self-test" &&
-GSDR_SELFTEST_ONLY=recycled timeout -k 10 120 ./gnss-sdr-new_amd/build/host_selftest tests/golden/GPS_L1_CA_ID_1_Fs_4Msps_2ms.dat \
+GSDR_SELFTEST_ONLY=recycled timeout -k 10 180 ./gnss-sdr-new_amd/build/host_selftest tests/golden/GPS_L1_CA_ID_1_Fs_4Msps_2ms.dat \
     > "$OUT/selftest_recycled.log" 2>&1; rc=$?; cat "$OUT/selftest_recycled.log"; [ $rc -eq 0 ] &&
 echo "== tests" &&
 timeout -k 10 600 python -u -m pytest tests/test_gpu_acq_full_shapes.py tests/test_gpu_configs.py tests/test_gpu_stream.py \

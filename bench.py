@@ -332,8 +332,9 @@ def load_pmc_traffic():
 def run_c5(args):
     """bench.py --workload c5: one step = a 25 Msps stream span of world x B 1 ms
     blocks; rank r runs the acquisition of its block span (c5_rank_plan: GPS L1 C/A
-    and BeiDou B1I 32 PRN x 81 Doppler grids, N = 25000, on alternate milliseconds,
-    one Galileo E1 36 PRN x 41 Doppler 4 ms grid, N = 100000, per 4 ms group) and
+    and BeiDou B1I 32 PRN x 80 Doppler grids, N = 25000, on alternate milliseconds,
+    one Galileo E1 36 PRN x 40 Doppler 4 ms grid, N = 100000, per 4 ms group; the
+    reference's ceil(2 doppler_max / doppler_step) bins) and
     tracks its channels of the 256 (three signal pools, device-resident
     dll_pll_veml_tracking).  Tracking (default, as C2's --trk-stream) follows one
     continuous stream: the span is periodic (B = 100 ms: Galileo's 100 ms secondary
@@ -587,8 +588,8 @@ def run_c5(args):
                 "one stream per job)",
         "config": {
             "workload": "C5: hybrid GPS L1 C/A + Galileo E1 + BeiDou B1I, 25 Msps, %d channels sharded c %% world "
-                        "(12/12/8 per 32-channel share); per 4 ms of the rank's span 2 GPS + 2 BeiDou 32 PRN x 81 "
-                        "Doppler grids (N 25000) and 1 Galileo 36 PRN x 41 Doppler grid (N 100000)" % C5_CHANNELS,
+                        "(12/12/8 per 32-channel share); per 4 ms of the rank's span 2 GPS + 2 BeiDou 32 PRN x 80 "
+                        "Doppler grids (N 25000) and 1 Galileo 36 PRN x 40 Doppler grid (N 100000)" % C5_CHANNELS,
             "blocks_per_step": total, "blocks_per_rank": B, "fs_sps": fs,
             "parallelism": "one stream of %d ms per step: acquisition blocks [%d,%d) and %d channels (GPS %d, "
                            "Galileo %d, BeiDou %d) on rank %d of %d, no data-path collective"

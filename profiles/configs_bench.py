@@ -237,11 +237,11 @@ def main():
         # (1 ms, N = 25000 = 5 x 5000 four-step), Galileo E1 (4 ms, N = 100000 = 25 x 4000)
         B = 4
         for name, N, P, dmax, dstep, codes in (
-                ("GPS L1 C/A 32 PRN x 81 Doppler, N=25000", 25000, 32, 10000, 250,
+                ("GPS L1 C/A 32 PRN x %d Doppler, N=25000", 25000, 32, 10000, 250,
                  lambda: np.stack([synth.gps_ca_sampled(p, fs) for p in range(1, 33)])),
-                ("BeiDou B1I 32 PRN x 81 Doppler, N=25000", 25000, 32, 10000, 250,
+                ("BeiDou B1I 32 PRN x %d Doppler, N=25000", 25000, 32, 10000, 250,
                  lambda: np.stack([synth.bds_b1i_sampled(p, fs)[:25000] for p in range(1, 33)])),
-                ("Galileo E1 36 PRN x 41 Doppler, 4 ms, N=100000", 100000, 36, 5000, 250,
+                ("Galileo E1 36 PRN x %d Doppler, 4 ms, N=100000", 100000, 36, 5000, 250,
                  lambda: np.stack([synth.gal_e1_sampled(p, fs, pilot=True)[:100000] for p in range(1, 37)]))):
             ms_code = N // 25000
             acq = gsdr.Acquisition(fs, N, dmax, dstep, pfa=0.01, max_prns=P, max_blocks=B, sampled_ms=ms_code,
@@ -249,7 +249,8 @@ def main():
             acq.set_local_codes(codes(), np.arange(1, P + 1))
             res = torch.zeros(B * P * gsdr.ACQ_RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
             sec = timed(lambda: acq.run_device(iq_dev.data_ptr(), B, N, 0, res.data_ptr()), max(2, a.reps // 2), 1, torch)
-            emit("C5", "acquisition " + name, fs, B * N, sec, acq_roofline(N, P, acq.num_doppler_bins, B, sec))
+            emit("C5", "acquisition " + name % acq.num_doppler_bins, fs, B * N, sec,
+                 acq_roofline(N, P, acq.num_doppler_bins, B, sec))
             acq.close()
 
 

@@ -134,14 +134,17 @@ def test_c3_gps_16msps_12_channel_pool():
 def test_streamed_chunk_tails(fs):
     """Streamed calls (vector_length > 4096) against the 8192-sample stream chunks of
     a GPS gr_complex pool: no tail (16384), a tail of exactly 512 samples riding with
-    the last chunk (16896), one sample more -- a chunk of its own (16897) --, a tail of
-    several blocks (20000) and a short one behind three chunks (24600).  The
+    the last chunk (16896), one sample more -- a chunk of its own (16897) --, the same
+    at a half-sample code period (16896.5: calls consume 16896 and 16897 samples in
+    turn), a tail of several blocks (20000) and a short one behind three chunks (24600).  The
     chunk / tail split (csrc/trk.hip correlate_call_stream) must not change a sum."""
     sats = synth.random_constellation(2, seed_offset=37, cn0_dbhz=45.0)
     for s in sats:
         s.code_doppler = True
     iq = synth.gps_l1_iq(fs, int(0.06 * fs), sats, seed_offset=37)
-    vl = int(round(fs / 1000))
+    # the engine's vector_length: lround(fs / 1000), halves away from zero (16896.5 ->
+    # 16897; consumption then alternates between 16896 and 16897 samples per call)
+    vl = int(np.floor(fs / 1000 + 0.5))
     conf = _conf(fs, len(sats))
     codes = [synth.gps_ca_chips(s.prn) for s in sats]
     _pool_check(conf, sats, iq, iq, fs, codes, None, _gps_acq, 50, [-0.25, 0.0, 0.25], 1, 1.023e6, vl, 1,

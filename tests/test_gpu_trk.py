@@ -289,15 +289,10 @@ def _open_loop_sig(g, iq, code, data_code, fs, acq_dop, shifts_chips, spc, chip_
         rem_code = float(np.float32(np.float32(code_freq * rem_samples / fs) * np.float32(spc)))
         code_step = float(np.float32(np.float32(code_freq / fs) * np.float32(spc)))
         n0 = int(g[e]["sample_counter"])
-        # the call's correlation length: d_current_prn_length_samples as the previous
-        # call's update left it (the record's `consumed`, :2119), the first call's from
-        # the pull-in (round(T_prn_mod_samples), :1813-1844) -- it moves by a sample
-        # between calls when fs / code rate is not an integer number of samples
-        n = int(g[e - 1]["consumed"]) if e > 0 else int(np.floor(len(code) / spc / chip_rate * fs + 0.5))
-        x = iq[n0:n0 + n]
-        gen = volk.multicorrelator_real_codes(x, code, shifts, rem_carr, carr_step, rem_code, code_step, n)
-        avx = volk.multicorrelator_real_codes_avx(x, code, shifts, rem_carr, carr_step, rem_code, code_step, n)
-        exact = volk.multicorrelator_real_codes_exact(x, code, shifts, rem_carr, carr_step, rem_code, code_step, n)
+        x = iq[n0:n0 + vl]
+        gen = volk.multicorrelator_real_codes(x, code, shifts, rem_carr, carr_step, rem_code, code_step, vl)
+        avx = volk.multicorrelator_real_codes_avx(x, code, shifts, rem_carr, carr_step, rem_code, code_step, vl)
+        exact = volk.multicorrelator_real_codes_exact(x, code, shifts, rem_carr, carr_step, rem_code, code_step, vl)
         got = g["taps"][e][:2 * len(shifts)].view(np.complex64)
         d = {"gpu_vs_fp64": ccompare(got, exact), "gpu_vs_avx": ccompare(got, avx), "gpu_vs_generic": ccompare(got, gen),
              "avx_vs_fp64": ccompare(avx, exact), "generic_vs_fp64": ccompare(gen, exact),
@@ -311,7 +306,7 @@ def _open_loop_sig(g, iq, code, data_code, fs, acq_dop, shifts_chips, spc, chip_
         worst = max(worst, d["gpu_vs_avx"])
         if data_code is not None:
             refd = volk.multicorrelator_real_codes_avx(x, data_code, shifts[iP:iP + 1], rem_carr, carr_step, rem_code,
-                                                       code_step, n)
+                                                       code_step, vl)
             worst = max(worst, ccompare(g["data_prompt"][e].view(np.complex64), refd))
     return worst
 

@@ -857,7 +857,6 @@ struct RegFourStep
     }
     static constexpr int lds_elems = H * max_stride();
     static constexpr size_t lds_bytes() { return (size_t)lds_elems * sizeof(float2) + (NT / 64) * sizeof(float); }
-    static_assert(WL || R % H == 0, "rows go through LDS in groups of H");
     template <class Out>
     __device__ __forceinline__ static void row_transforms(gsdr::pk::c2* lds, Out& out, int row0)
     {
@@ -870,6 +869,32 @@ struct RegFourStep
         wl_stages<L, 1, Pads, 0, Rs...>(row, out, lane, k1);
     }
 
+    // Phase 2 of QPW register four-steps at once (LDS rounds, H | QPW R): rows g = j R +
+    // k1 of transform j, H per round, so a round may hold rows of two transforms;
+    // out.value receives g as the row index.
+    template <int QPW, int CPL, class Out>
+    __device__ __forceinline__ static void phase2_multi(gsdr::pk::c2* lds, gsdr::pk::c2 (&v)[QPW][CPL][R], Out& out)
+    {
+        static_assert(!WL && (QPW * R) % H == 0, "multi-transform phase 2: LDS rounds of H rows");
+        const int wbase = (int)(threadIdx.x & ~63u);
+#pragma unroll
+        for (int h = 0; h < QPW * R / H; ++h)
+            {
+                if (h > 0) __syncthreads();  // the previous round's last-stage reads are done
+#pragma unroll
+                for (int c = 0; c < CPL; ++c)
+                    {
+                        const int n2 = min((int)threadIdx.x + c * NT, L - 1);
+                        if (L % NT == 0 || wbase + c * NT < L)
+                            {
+#pragma unroll
+                                for (int i = 0; i < H; ++i) lds[i * L + n2] = v[(h * H + i) / R][c][(h * H + i) % R];
+                            }
+                    }
+                __syncthreads();
+                row_transforms(lds, out, h * H);
+            }
+    }
     // Phase 2 of a register four-step: the R rows (phase 1's v[c][k1], lane column
     // n2 = threadIdx.x + c NT, clamped) through LDS and the L-point row transforms.
     template <int CPL, class Out>
@@ -882,6 +907,7 @@ struct RegFourStep
         };
         if constexpr (!WL)
             {
+                static_assert(R % H == 0, "rows go through LDS in groups of H");
 #pragma unroll
                 for (int h = 0; h < R / H; ++h)
                     {
@@ -1082,7 +1108,7 @@ constexpr size_t split_lds_bytes()
     return ring > RP::lds_bytes() ? ring : RP::lds_bytes();
 }
 
-template <int ROUT, class RP, bool HALF, bool ARG = false>
+template <int ROUT, class RP, bool HALF, bool ARG = false, int QPW = 1>
 __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(
     ARG ? 1 : (split_staged<ROUT, RP>() ? GSDR_SPLIT_WPE : RP::WPE)))) acq_correlate_split_kernel(
     const float2* __restrict__ X, const float2* __restrict__ code_fft, RowStat* __restrict__ stats,
@@ -1098,23 +1124,27 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(
     extern __shared__ float2 lds_raw[];
     c2* lds = reinterpret_cast<c2*>(lds_raw);
     float* red = reinterpret_cast<float*>(lds_raw + RP::lds_elems);
-    const uint32_t PV = P * ROUT;  // virtual PRNs: pv = p * ROUT + q
+    // QPW sub-transforms per workgroup: q = qq + j RQ (j < QPW) -- they share every
+    // product Y[r M + m] (only the exact outer factors W_ROUT^{r q} differ)
+    static_assert(ROUT % QPW == 0 && (QPW == 1 || split_staged<ROUT, RP>()), "sub-transforms per workgroup");
+    constexpr int RQ = ROUT / QPW;
+    const uint32_t PV = P * RQ;  // virtual PRNs: pv = p * RQ + qq
     const uint32_t nrows = nblocks * D;
     const uint32_t id = blockIdx.x;
     const uint32_t full = nrows >> 3;
     uint32_t row, pv;
     if constexpr (ARG)
         {
-            const uint32_t bp = id / ROUT;
+            const uint32_t bp = id / RQ;
             const uint32_t dsel = sel[bp].doppler_index;
             if (dsel >= D) return;  // uniform: no maximum found (an all-NaN grid)
             row = (bp / P) * D + dsel;
-            pv = (bp - (bp / P) * P) * ROUT + (id - bp * ROUT);
+            pv = (bp - (bp / P) * P) * RQ + (id - bp * RQ);
         }
     else if (id < full * 8u * PV)
         {
             const uint32_t xcd = id & 7u, slot = id >> 3;
-            const uint32_t G = pgs * ROUT;  // PV % G == 0 (host)
+            const uint32_t G = pgs * RQ;  // PV % G == 0 (host)
             const uint32_t per_group = full * G;
             const uint32_t pg = slot / per_group, rem = slot - pg * per_group;
             const uint32_t ri = rem / G;
@@ -1127,7 +1157,7 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(
             row = full * 8u + t / PV;
             pv = t - (t / PV) * PV;
         }
-    const uint32_t p = pv / ROUT, q = pv - p * ROUT;
+    const uint32_t p = pv / RQ, q = pv - p * RQ;  // q: the first sub-transform (qq)
     const uint32_t b = row / D, d = row - (row / D) * D;
     const auto xrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float2*>(X) + xm.off(b, d), 0, (int)(N * sizeof(c2)),
         0x00020000);
@@ -1147,7 +1177,7 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(
     // index q a compile-time constant: the outer factors W_ROUT^{rq} are exact
     // (+-1, +-i: an add/sub with swapped operands) and W_N^{mq} one table read
     // (m q < N)
-    c2 v[CPL][R];
+    c2 v[QPW][CPL][R];
     // ROUT > 1: every element of a column sums ROUT products.  Loaded into VGPRs,
     // the compiler kept the accumulated columns resident and issued two loads and a
     // wait per product (r05: 200 dependent L2 round trips per column at 100000, VALU
@@ -1214,20 +1244,24 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(
                                 const c2 xv = *reinterpret_cast<const c2*>(src + off);
                                 const c2 cv = *reinterpret_cast<const c2*>(src + 1024 + off);
                                 const c2 y = gsdr::pk::conj_mul(xv, cv);
-                                // W_ROUT^{r Q} = W_4^{e}, e = (r Q mod ROUT) * 4 / ROUT
-                                constexpr int e = ((r * Q) % ROUT) * (4 / ROUT);
-                                c2& z = v[c][n1];
-                                if constexpr (r == 0)
-                                    z = y;
-                                else if constexpr (e == 0)
-                                    z = z + y;
-                                else if constexpr (e == 1)
-                                    z = gsdr::pk::add_mi(z, y);  // z + (-i) y
-                                else if constexpr (e == 2)
-                                    z = z - y;
-                                else
-                                    z = gsdr::pk::sub_mi(z, y);  // z + i y
-                                if constexpr (Q > 0 && r == ROUT - 1) z = gsdr::pk::mul_root<Q * n1, ROUT * R>(z);
+                                auto acc = [&](auto jq) {
+                                    constexpr int QJ = Q + decltype(jq)::value * RQ;
+                                    // W_ROUT^{r QJ} = W_4^{e}, e = (r QJ mod ROUT) * 4 / ROUT
+                                    constexpr int e = ((r * QJ) % ROUT) * (4 / ROUT);
+                                    c2& z = v[decltype(jq)::value][c][n1];
+                                    if constexpr (r == 0)
+                                        z = y;
+                                    else if constexpr (e == 0)
+                                        z = z + y;
+                                    else if constexpr (e == 1)
+                                        z = gsdr::pk::add_mi(z, y);  // z + (-i) y
+                                    else if constexpr (e == 2)
+                                        z = z - y;
+                                    else
+                                        z = gsdr::pk::sub_mi(z, y);  // z + i y
+                                    if constexpr (QJ > 0 && r == ROUT - 1) z = gsdr::pk::mul_root<QJ * n1, ROUT * R>(z);
+                                };
+                                gsdr::pk::static_for<0, QPW>(acc);
                             }
                     }
             };
@@ -1244,14 +1278,20 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(
                     if (L % NT == 0 || wbase + c * NT < L)
                         {
                             const int n2 = min((int)threadIdx.x + c * NT, L - 1);
-                            gsdr::pk::Dft<R>::run(v[c]);
-                            if constexpr (Q > 0)
-                                {
-                                    const c2 w0 = gsdr::pk::from(tw[Q * n2]);
+                            auto transform = [&](auto jq) {
+                                constexpr int QJ = Q + decltype(jq)::value * RQ;
+                                c2(&w)[R] = v[decltype(jq)::value][c];
+                                gsdr::pk::Dft<R>::run(w);
+                                if constexpr (QJ > 0)
+                                    {
+                                        const c2 w0 = gsdr::pk::from(tw[QJ * n2]);
 #pragma unroll
-                                    for (int k1 = 0; k1 < R; ++k1) v[c][k1] = gsdr::pk::mul(v[c][k1], w0);
-                                }
-                            gsdr::pk::apply_powers<R>(v[c], gsdr::pk::from(tw[ROUT * n2]));
+                                        for (int k1 = 0; k1 < R; ++k1) w[k1] = gsdr::pk::mul(w[k1], w0);
+                                    }
+                                gsdr::pk::apply_powers<R>(w, gsdr::pk::from(tw[ROUT * n2]));
+                                __builtin_amdgcn_sched_barrier(0);
+                            };
+                            gsdr::pk::static_for<0, QPW>(transform);
                         }
                     __builtin_amdgcn_sched_barrier(0);
                 }
@@ -1295,10 +1335,10 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(
                                             z = gsdr::pk::sub_mi(z, y);  // z + i y
                                     }
                                 if constexpr (Q > 0) z = gsdr::pk::mul_root<Q * n1, ROUT * R>(z);
-                                v[c][n1] = z;
+                                v[0][c][n1] = z;
                         };
                         gsdr::pk::static_for<0, R>(column_input);
-                        gsdr::pk::Dft<R>::run(v[c]);
+                        gsdr::pk::Dft<R>::run(v[0][c]);
                         // W_M^{n2 k1} = W_N^{ROUT n2 k1}; the input factor W_N^{m Q} =
                         // W_{ROUT R}^{Q n1} W_N^{Q n2} -- the first a compile-time root
                         // above, the second common to the column, so applied to its
@@ -1307,16 +1347,16 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(
                             {
                                 const c2 w0 = gsdr::pk::from(tw[Q * n2]);
 #pragma unroll
-                                for (int k1 = 0; k1 < R; ++k1) v[c][k1] = gsdr::pk::mul(v[c][k1], w0);
+                                for (int k1 = 0; k1 < R; ++k1) v[0][c][k1] = gsdr::pk::mul(v[0][c][k1], w0);
                             }
-                        gsdr::pk::apply_powers<R>(v[c], gsdr::pk::from(tw[ROUT * n2]));
+                        gsdr::pk::apply_powers<R>(v[0][c], gsdr::pk::from(tw[ROUT * n2]));
                     }
             }
     };
     auto run_phase1 = [&](auto qc) { phase1(qc); };
-    if constexpr (ROUT == 1)
+    if constexpr (RQ == 1)
         run_phase1(std::integral_constant<int, 0>{});
-    else if constexpr (ROUT == 2)
+    else if constexpr (RQ == 2)
         {
             if (q == 0)
                 run_phase1(std::integral_constant<int, 0>{});
@@ -1342,14 +1382,16 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(
         uint32_t q;
         // W_L^m = W_N^{m R ROUT}
         __device__ __forceinline__ float2 twiddle(int m_) const { return tw[m_ * R * ROUT]; }
-        __device__ __forceinline__ void value(c2 x, int k2, int k1)
+        // g: the row (k1 of sub-transform q + (g / R) RQ, g mod R)
+        __device__ __forceinline__ void value(c2 x, int k2, int g)
         {
             const float a = __builtin_fmaf(x.x, x.x, x.y * x.y);
             if (HALF && k2 < L / 2) return;
             if constexpr (ARG)
                 {
-                    // output k = q + ROUT (k1 + R k2); effective index j = k - (N - eff)
-                    const uint32_t j = q + (uint32_t)ROUT * ((uint32_t)k1 + (uint32_t)R * (uint32_t)k2) - (HALF ? N / 2 : 0u);
+                    const uint32_t k1 = (uint32_t)g % (uint32_t)R, qo = q + ((uint32_t)g / (uint32_t)R) * (uint32_t)RQ;
+                    // output k = qo + ROUT (k1 + R k2); effective index j = k - (N - eff)
+                    const uint32_t j = qo + (uint32_t)ROUT * (k1 + (uint32_t)R * (uint32_t)k2) - (HALF ? N / 2 : 0u);
                     const unsigned long long kk = ((unsigned long long)__float_as_uint(a) << 32) | (0xffffffffu - j);
                     key = kk > key ? kk : key;
                     if (row) row[j] = a;
@@ -1360,9 +1402,12 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(
     } out{tw, 0.0f, 0ull, nullptr, q};
     if constexpr (ARG)
         {
-            if (rowbuf) out.row = rowbuf + (size_t)(id / ROUT) * (HALF ? N / 2 : N);
+            if (rowbuf) out.row = rowbuf + (size_t)(id / RQ) * (HALF ? N / 2 : N);
         }
-    RP::template phase2<CPL>(lds, v, out);
+    if constexpr (QPW == 1)
+        RP::template phase2<CPL>(lds, v[0], out);
+    else
+        RP::template phase2_multi<QPW, CPL>(lds, v, out);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if constexpr (ARG)
         {
@@ -1381,7 +1426,7 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(
                 {
 #pragma unroll
                     for (int w2 = 1; w2 < NW; ++w2) k = sk[w2] > k ? sk[w2] : k;
-                    __hip_atomic_fetch_max(&keys[id / ROUT], k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_fetch_max(&keys[id / RQ], k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
             if (psum)
                 {
@@ -1389,27 +1434,33 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(
                     // opposite the peak (pcps_acquisition.cc:531-533): sum |conj(X_opp) C|^2
                     // over inputs [q M, (q + 1) M), lane-strided, then wave and workgroup
                     // sums in a fixed order; the finish kernel adds the ROUT shares in q order
-                    const uint32_t bp = id / ROUT;
+                    const uint32_t bp = id / RQ;
                     const uint32_t opp = (d + D / 2) % D;
-                    const c2* xo = reinterpret_cast<const c2*>(X) + xm.off(b, opp) + (size_t)q * M;
-                    const c2* co = reinterpret_cast<const c2*>(code_fft) + (size_t)p * N + (size_t)q * M;
-                    float acc = 0.0f;
-                    for (uint32_t i = threadIdx.x; i < M; i += NT)
-                        {
-                            const c2 y = gsdr::pk::conj_mul(xo[i], co[i]);
-                            acc = __builtin_fmaf(y.x, y.x, __builtin_fmaf(y.y, y.y, acc));
-                        }
-#pragma unroll
-                    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
                     float* sf = reinterpret_cast<float*>(sk + NW);
-                    if (lane == 0) sf[wave] = acc;
-                    __syncthreads();
-                    if (threadIdx.x == 0)
-                        {
-                            float tot = 0.0f;
 #pragma unroll
-                            for (int w2 = 0; w2 < NW; ++w2) tot += sf[w2];
-                            psum[(size_t)bp * ROUT + q] = tot;
+                    for (int jq = 0; jq < QPW; ++jq)
+                        {
+                            const uint32_t qo = q + (uint32_t)jq * RQ;
+                            const c2* xo = reinterpret_cast<const c2*>(X) + xm.off(b, opp) + (size_t)qo * M;
+                            const c2* co = reinterpret_cast<const c2*>(code_fft) + (size_t)p * N + (size_t)qo * M;
+                            float acc = 0.0f;
+                            for (uint32_t i = threadIdx.x; i < M; i += NT)
+                                {
+                                    const c2 y = gsdr::pk::conj_mul(xo[i], co[i]);
+                                    acc = __builtin_fmaf(y.x, y.x, __builtin_fmaf(y.y, y.y, acc));
+                                }
+#pragma unroll
+                            for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+                            if (jq > 0) __syncthreads();  // thread 0 read the previous share's slots
+                            if (lane == 0) sf[wave] = acc;
+                            __syncthreads();
+                            if (threadIdx.x == 0)
+                                {
+                                    float tot = 0.0f;
+#pragma unroll
+                                    for (int w2 = 0; w2 < NW; ++w2) tot += sf[w2];
+                                    psum[(size_t)bp * ROUT + qo] = tot;
+                                }
                         }
                 }
             return;

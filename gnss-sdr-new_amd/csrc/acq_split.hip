@@ -15,6 +15,9 @@ namespace gsdr_acq_impl
 //           wave transforms its row without workgroup barriers; rounds 16 + 16 (128 KB)
 using Reg25k = RegFourStep<25, 512, 5, 1, NoPads<1000>, 10, 10, 10>;
 using Wl32k = RegFourStep<32, 1024, 0, 1, NoPads<1000>, 10, 10, 10>;
+// 25000 = 25 x (10 x 10 x 10) on 1024 lanes, one column per lane, 10 rows per LDS
+// round: the plan of the two-sub-transform workgroups (QPW 2) of 100000 = 4 x 25000
+using Reg25kW = RegFourStep<25, 1024, 10, 1, NoPads<1000>, 10, 10, 10>;
 
 // split ids: (N, outer radix ROUT, inner plan)
 //   1: 25000 = 1 x 25000 (C5 GPS L1 / BeiDou B1I at 25 Msps, 1 ms)
@@ -43,6 +46,10 @@ constexpr SplitId kSplits[] = {{1, 25000}, {12, 32000}, {13, 64000}, {4, 100000}
 // PRN group of an XCD pass: the largest divisor of P whose code rows fit in ~2 MB
 // (half an XCD's L2), so the rows of the group's codes stay resident while the X
 // rows stream past
+#ifndef GSDR_ACQ_QPW_DEFAULT
+#define GSDR_ACQ_QPW_DEFAULT 1
+#endif
+
 uint32_t prn_group(uint32_t P, uint32_t N)
 {
     const size_t row = (size_t)N * sizeof(float2);
@@ -58,7 +65,7 @@ uint32_t prn_group(uint32_t P, uint32_t N)
 // ARG = false: the grid pass (row maxima into d_stats); ARG = true: the selected
 // rows' pass (keys into d_keys, |R|^2 rows into rowbuf for the peak ratio; the
 // caller zeroes d_keys and runs acq_argmax_split_finish_kernel)
-template <int ROUT, class RP, bool HALF, bool ARG = false>
+template <int ROUT, class RP, bool HALF, bool ARG = false, int QPW = 1>
 int launch_one(gsdr_acq* a, uint32_t nblocks, hipStream_t s, const gsdr_acq_result* sel = nullptr,
     float* rowbuf = nullptr, float* psum = nullptr, uint32_t* rout = nullptr)
 {
@@ -71,20 +78,21 @@ int launch_one(gsdr_acq* a, uint32_t nblocks, hipStream_t s, const gsdr_acq_resu
         }
     if (ROUT > 1 && !ARG)
         GSDR_HIP(hipMemsetAsync(a->d_stats, 0, (size_t)nblocks * a->nprn * a->D * sizeof(RowStat), s));
-    const uint32_t grid = ARG ? nblocks * a->nprn * ROUT : nblocks * a->D * a->nprn * ROUT;
-    hipLaunchKernelGGL((acq_correlate_split_kernel<ROUT, RP, HALF, ARG>), dim3(grid), dim3(RP::NT), (split_lds_bytes<ROUT, RP>()), s,
+    constexpr uint32_t RQ = ROUT / QPW;  // workgroups per transform
+    const uint32_t grid = ARG ? nblocks * a->nprn * RQ : nblocks * a->D * a->nprn * RQ;
+    hipLaunchKernelGGL((acq_correlate_split_kernel<ROUT, RP, HALF, ARG, QPW>), dim3(grid), dim3(RP::NT), (split_lds_bytes<ROUT, RP>()), s,
         a->d_X, a->d_code_fft, a->d_stats, a->d_tw, a->D, a->nprn, nblocks, prn_group(a->nprn, a->N), a->xm, sel,
         a->d_keys, rowbuf, psum);
     GSDR_HIP(hipGetLastError());
     return GSDR_OK;
 }
 
-template <int ROUT, class RP, bool HALF>
+template <int ROUT, class RP, bool HALF, int QPW = 1>
 int attrs_one()
 {
-    GSDR_HIP(hipFuncSetAttribute((const void*)acq_correlate_split_kernel<ROUT, RP, HALF>,
+    GSDR_HIP(hipFuncSetAttribute((const void*)acq_correlate_split_kernel<ROUT, RP, HALF, false, QPW>,
         hipFuncAttributeMaxDynamicSharedMemorySize, (int)(split_lds_bytes<ROUT, RP>())));
-    GSDR_HIP(hipFuncSetAttribute((const void*)acq_correlate_split_kernel<ROUT, RP, HALF, true>,
+    GSDR_HIP(hipFuncSetAttribute((const void*)acq_correlate_split_kernel<ROUT, RP, HALF, true, QPW>,
         hipFuncAttributeMaxDynamicSharedMemorySize, (int)(split_lds_bytes<ROUT, RP>())));
     return GSDR_OK;
 }
@@ -101,6 +109,9 @@ int launch_split_arg(gsdr_acq* a, uint32_t nblocks, hipStream_t s, const gsdr_ac
         {
         case 1: GSDR_ARG(1, Reg25k);
         case 4: GSDR_ARG(4, Reg25k);
+        case 24:
+            return half ? launch_one<4, Reg25kW, true, true, 2>(a, nblocks, s, sel, rowbuf, psum, rout)
+                        : launch_one<4, Reg25kW, false, true, 2>(a, nblocks, s, sel, rowbuf, psum, rout);
         case 12: GSDR_ARG(1, Wl32k);
         case 13: GSDR_ARG(2, Wl32k);
         default: gsdr::set_error("internal: bad split variant %d", a->split); return GSDR_E_STATE;
@@ -134,6 +145,9 @@ int launch_split(gsdr_acq* a, uint32_t nblocks, hipStream_t s)
         {
         case 1: return half ? launch_one<1, Reg25k, true>(a, nblocks, s) : launch_one<1, Reg25k, false>(a, nblocks, s);
         case 4: return half ? launch_one<4, Reg25k, true>(a, nblocks, s) : launch_one<4, Reg25k, false>(a, nblocks, s);
+        case 24:
+            return half ? launch_one<4, Reg25kW, true, false, 2>(a, nblocks, s)
+                        : launch_one<4, Reg25kW, false, false, 2>(a, nblocks, s);
         case 12: return half ? launch_one<1, Wl32k, true>(a, nblocks, s) : launch_one<1, Wl32k, false>(a, nblocks, s);
         case 13: return half ? launch_one<2, Wl32k, true>(a, nblocks, s) : launch_one<2, Wl32k, false>(a, nblocks, s);
         default: gsdr::set_error("internal: bad split variant %d", a->split); return GSDR_E_STATE;
@@ -156,12 +170,21 @@ int setup_split(gsdr_acq* a)
     if (mode == 0) return GSDR_OK;
     for (const SplitId& sp : kSplits)
         if (sp.n == a->N && !a->split) a->split = sp.id;
+    // 100000: two sub-transforms per 1024-lane workgroup sharing their products
+    // (GSDR_ACQ_QPW=2) or one per 512-lane workgroup (1)
+    if (a->split == 4)
+        {
+            int qpw = GSDR_ACQ_QPW_DEFAULT;
+            if (const char* e = std::getenv("GSDR_ACQ_QPW")) qpw = std::atoi(e);
+            if (qpw == 2) a->split = 24;
+        }
     if (!a->split) return GSDR_OK;
     int rc = GSDR_OK;
     switch (a->split)
         {
         case 1: rc = attrs_one<1, Reg25k, true>() | attrs_one<1, Reg25k, false>(); break;
         case 4: rc = attrs_one<4, Reg25k, true>() | attrs_one<4, Reg25k, false>(); break;
+        case 24: rc = attrs_one<4, Reg25kW, true, 2>() | attrs_one<4, Reg25kW, false, 2>(); break;
         case 12: rc = attrs_one<1, Wl32k, true>() | attrs_one<1, Wl32k, false>(); break;
         case 13: rc = attrs_one<2, Wl32k, true>() | attrs_one<2, Wl32k, false>(); break;
         default: break;

@@ -1627,10 +1627,11 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                     // issued a whole chunk of correlation ahead
                     const int64_t nb = p_off + vl - kHalo / 2;
                     const uint64_t nbytes = iq_items * (uint64_t)item_bytes<IT>();
-                    // sized for the tail a last chunk may carry, whatever the next call's
-                    // vector length: Doppler can move it across 2 chunk + kTrkThreads
-                    // between calls, and the next call decides its tail from its own
-                    // (the buffers hold chunk + kTrkThreads + kHalo items)
+                    // sized for the tail a last chunk may carry whatever this call's split
+                    // (the buffers hold chunk + kTrkThreads + kHalo items): a call
+                    // correlates the channel's constant vector_length samples
+                    // (do_correlation_step, :1064-1076), so the split cannot change between
+                    // calls today, but the prefetch no longer depends on that
                     const int pfn = (stream_chunk + kTrkThreads + kHalo) * item_bytes<IT>();
                     pf_start[0] = stream_fetch(iq, nbytes, nb * item_bytes<IT>(), pfn, s_sb, 3);
                     pf_start[1] = vl > stream_chunk + kTrkThreads

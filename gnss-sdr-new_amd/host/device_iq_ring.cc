@@ -60,11 +60,15 @@ bool DeviceIqRing::head(uint64_t* h) const
     return d_started;
 }
 
-uint64_t DeviceIqRing::landed()
+uint64_t DeviceIqRing::landed(uint64_t want)
 {
+    const uint64_t seen = d_landed.load(std::memory_order_acquire);
+    if (seen >= want) return seen;  // most calls: their items landed long ago
     uint64_t v = 0;
     if (gsdr_stream_landed(d_ring, &v) != GSDR_OK)
         throw std::runtime_error(std::string("DeviceIqRing::landed: ") + gsdr_last_error());
+    uint64_t cur = seen;
+    while (v > cur && !d_landed.compare_exchange_weak(cur, v, std::memory_order_acq_rel)) {}
     return v;
 }
 
@@ -72,6 +76,7 @@ void DeviceIqRing::wait_landed(uint64_t upto)
 {
     if (gsdr_stream_wait_landed(d_ring, upto) != GSDR_OK)
         throw std::runtime_error(std::string("DeviceIqRing::wait_landed: ") + gsdr_last_error());
+    (void)landed(upto);
 }
 
 void DeviceIqRing::feed(const void* in, uint64_t nitems_read, int n)

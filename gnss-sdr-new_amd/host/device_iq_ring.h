@@ -19,6 +19,7 @@
 #ifndef GSDR_HOST_DEVICE_IQ_RING_H
 #define GSDR_HOST_DEVICE_IQ_RING_H
 
+#include <atomic>
 #include <cstdint>
 #include <functional>
 #include <map>
@@ -67,7 +68,9 @@ public:
     // every item before the returned index is in device memory: a push copies from
     // the feeder's buffer after feed() returns, so a block consumes (and its upstream
     // may recycle) only items before it (gsdr_stream_landed)
-    uint64_t landed();
+    // (want: the caller's question "has everything before want landed?" -- answered
+    // from the last value seen without a query when it has)
+    uint64_t landed(uint64_t want = UINT64_MAX);
     void wait_landed(uint64_t upto);  // gsdr_stream_wait_landed
 
 private:
@@ -82,6 +85,7 @@ private:
     int d_next_hook{0};
     mutable std::mutex d_mu;       // head / started / hooks
     std::mutex d_push_mu;          // one pusher at a time (pieces in order)
+    std::atomic<uint64_t> d_landed{0};  // the last landed index seen (monotone)
 };
 
 #endif

@@ -353,9 +353,10 @@ int dll_pll_veml_tracking_pool_mi355x::work(const void* in, int ninput_items, ui
         {
             DeviceIqRing* ring = d_pool->ring();
             const uint64_t want = nitems_read + static_cast<uint64_t>(c);
-            const uint64_t landed = ring->landed();
+            const uint64_t landed = ring->landed(want);
             if (landed >= want) return c;
-            if (*noutput) return static_cast<int>(landed > nitems_read ? landed - nitems_read : 0);
+            // the landed part is progress (the scheduler calls again for the rest)
+            if (*noutput || landed > nitems_read) return static_cast<int>(landed > nitems_read ? landed - nitems_read : 0);
             ring->wait_landed(want);
         }
     catch (const std::exception& e)

@@ -21,7 +21,8 @@ using Reg25kW = RegFourStep<25, 1024, 10, 1, NoPads<1000>, 10, 10, 10>;
 
 // split ids: (N, outer radix ROUT, inner plan)
 //   1: 25000 = 1 x 25000 (C5 GPS L1 / BeiDou B1I at 25 Msps, 1 ms)
-//   4: 100000 = 4 x 25000 (C5 Galileo E1 at 25 Msps, 4 ms)
+//   4: 100000 = 4 x 25000 (C5 Galileo E1 at 25 Msps, 4 ms), one sub-transform per workgroup
+//   24: the same, two sub-transforms (q, q + 2) per 1024-lane workgroup (the default)
 //   12: 32000 = 1 x Wl32k (Galileo E1 at 8 Msps, 4 ms)
 //   13: 64000 = 2 x Wl32k (C4: Galileo E1 at 8 Msps with bit transition)
 // Measured and removed: round 4's 100000 = 2 x 50000 (25 x 2000 register
@@ -47,7 +48,7 @@ constexpr SplitId kSplits[] = {{1, 25000}, {12, 32000}, {13, 64000}, {4, 100000}
 // (half an XCD's L2), so the rows of the group's codes stay resident while the X
 // rows stream past
 #ifndef GSDR_ACQ_QPW_DEFAULT
-#define GSDR_ACQ_QPW_DEFAULT 1
+#define GSDR_ACQ_QPW_DEFAULT 2
 #endif
 
 uint32_t prn_group(uint32_t P, uint32_t N)
@@ -171,7 +172,9 @@ int setup_split(gsdr_acq* a)
     for (const SplitId& sp : kSplits)
         if (sp.n == a->N && !a->split) a->split = sp.id;
     // 100000: two sub-transforms per 1024-lane workgroup sharing their products
-    // (GSDR_ACQ_QPW=2) or one per 512-lane workgroup (1)
+    // (GSDR_ACQ_QPW=2, the default: half the workgroups, each product formed once for
+    // two sub-transforms -- C5 Galileo 133.6 -> 168.0 Msps, profiles/r06f) or one per
+    // 512-lane workgroup (1)
     if (a->split == 4)
         {
             int qpw = GSDR_ACQ_QPW_DEFAULT;

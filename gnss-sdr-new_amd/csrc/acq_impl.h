@@ -869,16 +869,17 @@ struct RegFourStep
         wl_stages<L, 1, Pads, 0, Rs...>(row, out, lane, k1);
     }
 
-    // Phase 2 of QPW register four-steps at once (LDS rounds, H | QPW R): rows g = j R +
-    // k1 of transform j, H per round, so a round may hold rows of two transforms;
-    // out.value receives g as the row index.
-    template <int QPW, int CPL, class Out>
-    __device__ __forceinline__ static void phase2_multi(gsdr::pk::c2* lds, gsdr::pk::c2 (&v)[QPW][CPL][R], Out& out)
+    // Phase 2 of T register four-steps at once (LDS rounds of H rows): rows g = j R + k1
+    // of transform j, so a round may hold rows of two transforms; out.value receives g
+    // as the row index.  A last round with fewer than H rows leaves the rest of the LDS
+    // rows stale: their outputs carry g >= T R, which out.value must drop.
+    template <int T, int CPL, class Out>
+    __device__ __forceinline__ static void phase2_multi(gsdr::pk::c2* lds, gsdr::pk::c2 (&v)[T][CPL][R], Out& out)
     {
-        static_assert(!WL && (QPW * R) % H == 0, "multi-transform phase 2: LDS rounds of H rows");
+        static_assert(!WL, "multi-transform phase 2: LDS rounds of H rows");
         const int wbase = (int)(threadIdx.x & ~63u);
 #pragma unroll
-        for (int h = 0; h < QPW * R / H; ++h)
+        for (int h = 0; h < (T * R + H - 1) / H; ++h)
             {
                 if (h > 0) __syncthreads();  // the previous round's last-stage reads are done
 #pragma unroll
@@ -888,7 +889,8 @@ struct RegFourStep
                         if (L % NT == 0 || wbase + c * NT < L)
                             {
 #pragma unroll
-                                for (int i = 0; i < H; ++i) lds[i * L + n2] = v[(h * H + i) / R][c][(h * H + i) % R];
+                                for (int i = 0; i < H; ++i)
+                                    if (h * H + i < T * R) lds[i * L + n2] = v[(h * H + i) / R][c][(h * H + i) % R];
                             }
                     }
                 __syncthreads();
@@ -1089,6 +1091,17 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(RP:
 #ifndef GSDR_SPLIT_WPE
 #define GSDR_SPLIT_WPE 4
 #endif
+// staged phase 1's per-wave ring: slots of one X and PPW code copies (1 KB each per
+// wave), as many in flight as GSDR_SPLIT_DMA allows within 144 KB per workgroup
+template <class RP, int PPW>
+struct SplitRing
+{
+    static constexpr int slot = 1024 * (1 + PPW);
+    static constexpr int fit = 147456 / ((RP::NT / 64) * slot);
+    static constexpr int depth = GSDR_SPLIT_DMA < fit ? GSDR_SPLIT_DMA : (fit > 0 ? fit : 1);
+    static constexpr size_t bytes = (size_t)(RP::NT / 64) * depth * slot;
+};
+
 // which split plans stage phase 1 (r06, profiles/r06b3: 100000 = 4 x 25000 118 -> 133
 // Msps, 64000 = 2 x 32000 88 -> 98, 32000 (one column per lane on 1024 lanes) 105 ->
 // 118; the 512-lane 25000 plan, whose loads already go out 50 per column at once,
@@ -1101,14 +1114,14 @@ constexpr bool split_staged()
 
 // dynamic LDS of a split launch: phase 2's rows (+ the reduction slots) or, staged,
 // each wave's ring of GSDR_SPLIT_DMA 2 KB copy slots, whichever is larger
-template <int ROUT, class RP>
+template <int ROUT, class RP, int PPW = 1>
 constexpr size_t split_lds_bytes()
 {
-    constexpr size_t ring = split_staged<ROUT, RP>() ? (size_t)(RP::NT / 64) * GSDR_SPLIT_DMA * 2048 : 0;
+    constexpr size_t ring = split_staged<ROUT, RP>() ? SplitRing<RP, PPW>::bytes : 0;
     return ring > RP::lds_bytes() ? ring : RP::lds_bytes();
 }
 
-template <int ROUT, class RP, bool HALF, bool ARG = false, int QPW = 1>
+template <int ROUT, class RP, bool HALF, bool ARG = false, int QPW = 1, int PPW = 1>
 __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(
     ARG ? 1 : (split_staged<ROUT, RP>() ? GSDR_SPLIT_WPE : RP::WPE)))) acq_correlate_split_kernel(
     const float2* __restrict__ X, const float2* __restrict__ code_fft, RowStat* __restrict__ stats,
@@ -1127,8 +1140,13 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(
     // QPW sub-transforms per workgroup: q = qq + j RQ (j < QPW) -- they share every
     // product Y[r M + m] (only the exact outer factors W_ROUT^{r q} differ)
     static_assert(ROUT % QPW == 0 && (QPW == 1 || split_staged<ROUT, RP>()), "sub-transforms per workgroup");
+    // or PPW PRNs per workgroup (ROUT 1): transform j correlates PRN p + j against the
+    // same X row, read once for all of them
+    static_assert(PPW == 1 || (ROUT == 1 && QPW == 1 && !ARG && PPW == 2 && split_staged<ROUT, RP>()),
+        "PRNs per workgroup");
+    constexpr int T = QPW * PPW;  // transforms per workgroup
     constexpr int RQ = ROUT / QPW;
-    const uint32_t PV = P * RQ;  // virtual PRNs: pv = p * RQ + qq
+    const uint32_t PV = P / PPW * RQ;  // virtual PRNs: pv = (p / PPW) RQ + qq
     const uint32_t nrows = nblocks * D;
     const uint32_t id = blockIdx.x;
     const uint32_t full = nrows >> 3;
@@ -1157,12 +1175,12 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(
             row = full * 8u + t / PV;
             pv = t - (t / PV) * PV;
         }
-    const uint32_t p = pv / RQ, q = pv - p * RQ;  // q: the first sub-transform (qq)
+    const uint32_t p = pv / RQ * PPW, q = pv - pv / RQ * RQ;  // q: the first sub-transform (qq); p the first PRN
     const uint32_t b = row / D, d = row - (row / D) * D;
     const auto xrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float2*>(X) + xm.off(b, d), 0, (int)(N * sizeof(c2)),
         0x00020000);
     const auto crs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float2*>(code_fft) + (size_t)p * N, 0, (int)(N * sizeof(c2)), 0x00020000);
+        const_cast<float2*>(code_fft) + (size_t)p * N, 0, (int)(N * PPW * sizeof(c2)), 0x00020000);
     auto bload = [](decltype(xrs) rs, int voff, int soff) -> c2 {
         const auto u = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, 0);
         return c2{__uint_as_float(u[0]), __uint_as_float(u[1])};
@@ -1177,7 +1195,7 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(
     // index q a compile-time constant: the outer factors W_ROUT^{rq} are exact
     // (+-1, +-i: an add/sub with swapped operands) and W_N^{mq} one table read
     // (m q < N)
-    c2 v[QPW][CPL][R];
+    c2 v[T][CPL][R];
     // ROUT > 1: every element of a column sums ROUT products.  Loaded into VGPRs,
     // the compiler kept the accumulated columns resident and issued two loads and a
     // wait per product (r05: 200 dependent L2 round trips per column at 100000, VALU
@@ -1189,7 +1207,7 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(
     // Each element's sum keeps the r order (bit-identical).
     auto phase1_dma = [&](auto qc) {
         constexpr int Q = decltype(qc)::value;
-        constexpr int DEPTH = GSDR_SPLIT_DMA;
+        constexpr int DEPTH = SplitRing<RP, PPW>::depth, SLOT = SplitRing<RP, PPW>::slot;
         // segment s: column set c = s / U, unit u = s % U (n1 = u / ROUT, r = u % ROUT):
         // column-major, so a column's transform runs (and its registers settle) before
         // the next column accumulates, as in the VGPR form
@@ -1197,7 +1215,7 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(
         constexpr int PPC = (U + 1) / 2;          // copy pairs per column set (an odd U repeats its last unit)
         constexpr int PAIRS = PPC * CPL;         // one X and one code copy per two segments
         const int wave = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
-        char* ring = reinterpret_cast<char*>(lds_raw) + (size_t)wave * DEPTH * 2048;
+        char* ring = reinterpret_cast<char*>(lds_raw) + (size_t)wave * DEPTH * SLOT;
         const int half = lane >> 5, l32 = lane & 31;
         const int lane_off = (wave * 64 + 2 * l32) * 8;
         auto issue = [&](auto kc) {
@@ -1215,9 +1233,12 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(
                     // copies (lanes past column L - 1 copy bytes no lane reads, past the
                     // row's end zeros)
                     const int voff = lane_off + half * ((eb - ea) * 8);
-                    char* dst = ring + (k % DEPTH) * 2048;
+                    char* dst = ring + (k % DEPTH) * SLOT;
                     __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (gsdr_lvoid*)dst, 16, voff, ea * 8, 0, 0);
-                    __builtin_amdgcn_raw_ptr_buffer_load_lds(crs, (gsdr_lvoid*)(dst + 1024), 16, voff, ea * 8, 0, 0);
+#pragma unroll
+                    for (int j = 0; j < PPW; ++j)
+                        __builtin_amdgcn_raw_ptr_buffer_load_lds(crs, (gsdr_lvoid*)(dst + 1024 * (1 + j)), 16, voff,
+                            (ea + j * (int)N) * 8, 0, 0);
                 }
         };
         // the lane's column within its segment (clamped lanes read column L - 1's)
@@ -1228,11 +1249,11 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(
         gsdr::pk::static_for<0, DEPTH>(prologue);
         auto step = [&](auto kc) {
             constexpr int k = decltype(kc)::value;
-            // pair k has landed once at most 2 (min(DEPTH, PAIRS - k) - 1) younger copies are out
-            constexpr int younger = 2 * ((PAIRS - k < DEPTH ? PAIRS - k : DEPTH) - 1);
+            // pair k has landed once at most (1 + PPW) (min(DEPTH, PAIRS - k) - 1) younger copies are out
+            constexpr int younger = (1 + PPW) * ((PAIRS - k < DEPTH ? PAIRS - k : DEPTH) - 1);
             // s_waitcnt vmcnt(younger) (expcnt / lgkmcnt left at their maxima)
             __builtin_amdgcn_s_waitcnt((younger & 15) | (7 << 4) | (15 << 8) | ((younger >> 4) << 14));
-            const char* src = ring + (k % DEPTH) * 2048;
+            const char* src = ring + (k % DEPTH) * SLOT;
             auto seg = [&](auto jc) {
                 constexpr int c = k / PPC, u = 2 * (k % PPC) + decltype(jc)::value;
                 if constexpr (u < U)
@@ -1245,11 +1266,14 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(
                                 const c2 cv = *reinterpret_cast<const c2*>(src + 1024 + off);
                                 const c2 y = gsdr::pk::conj_mul(xv, cv);
                                 auto acc = [&](auto jq) {
-                                    constexpr int QJ = Q + decltype(jq)::value * RQ;
+                                    constexpr int J = decltype(jq)::value;
+                                    constexpr int QJ = Q + (PPW == 1 ? J * RQ : 0);
                                     // W_ROUT^{r QJ} = W_4^{e}, e = (r QJ mod ROUT) * 4 / ROUT
                                     constexpr int e = ((r * QJ) % ROUT) * (4 / ROUT);
-                                    c2& z = v[decltype(jq)::value][c][n1];
-                                    if constexpr (r == 0)
+                                    c2& z = v[J][c][n1];
+                                    if constexpr (PPW > 1 && J > 0)
+                                        z = gsdr::pk::conj_mul(xv, *reinterpret_cast<const c2*>(src + 1024 * (1 + J) + off));
+                                    else if constexpr (r == 0)
                                         z = y;
                                     else if constexpr (e == 0)
                                         z = z + y;
@@ -1261,7 +1285,7 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(
                                         z = gsdr::pk::sub_mi(z, y);  // z + i y
                                     if constexpr (QJ > 0 && r == ROUT - 1) z = gsdr::pk::mul_root<QJ * n1, ROUT * R>(z);
                                 };
-                                gsdr::pk::static_for<0, QPW>(acc);
+                                gsdr::pk::static_for<0, T>(acc);
                             }
                     }
             };
@@ -1279,7 +1303,7 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(
                         {
                             const int n2 = min((int)threadIdx.x + c * NT, L - 1);
                             auto transform = [&](auto jq) {
-                                constexpr int QJ = Q + decltype(jq)::value * RQ;
+                                constexpr int QJ = Q + (PPW == 1 ? decltype(jq)::value * RQ : 0);
                                 c2(&w)[R] = v[decltype(jq)::value][c];
                                 gsdr::pk::Dft<R>::run(w);
                                 if constexpr (QJ > 0)
@@ -1291,7 +1315,7 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(
                                 gsdr::pk::apply_powers<R>(w, gsdr::pk::from(tw[ROUT * n2]));
                                 __builtin_amdgcn_sched_barrier(0);
                             };
-                            gsdr::pk::static_for<0, QPW>(transform);
+                            gsdr::pk::static_for<0, T>(transform);
                         }
                     __builtin_amdgcn_sched_barrier(0);
                 }
@@ -1380,13 +1404,19 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(
         unsigned long long key;
         float* row;  // ARG with the peak ratio: the row's |R|^2 (effective window)
         uint32_t q;
+        float m1;  // PPW 2: the second PRN's row maximum
         // W_L^m = W_N^{m R ROUT}
         __device__ __forceinline__ float2 twiddle(int m_) const { return tw[m_ * R * ROUT]; }
-        // g: the row (k1 of sub-transform q + (g / R) RQ, g mod R)
+        // g: the row (k1 of transform g / R, g mod R: sub-transform q + (g / R) RQ, or PRN
+        // p + g / R with PPW)
         __device__ __forceinline__ void value(c2 x, int k2, int g)
         {
             const float a = __builtin_fmaf(x.x, x.x, x.y * x.y);
             if (HALF && k2 < L / 2) return;
+            if constexpr (!RP::WL && (T * R) % RP::H != 0)
+                {
+                    if (g >= T * R) return;  // a stale row of a partial last round
+                }
             if constexpr (ARG)
                 {
                     const uint32_t k1 = (uint32_t)g % (uint32_t)R, qo = q + ((uint32_t)g / (uint32_t)R) * (uint32_t)RQ;
@@ -1396,18 +1426,25 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(
                     key = kk > key ? kk : key;
                     if (row) row[j] = a;
                 }
+            else if constexpr (PPW > 1)
+                {
+                    if (g < R)
+                        m = __builtin_fmaxf(m, a);
+                    else
+                        m1 = __builtin_fmaxf(m1, a);
+                }
             else
                 m = __builtin_fmaxf(m, a);
         }
-    } out{tw, 0.0f, 0ull, nullptr, q};
+    } out{tw, 0.0f, 0ull, nullptr, q, 0.0f};
     if constexpr (ARG)
         {
             if (rowbuf) out.row = rowbuf + (size_t)(id / RQ) * (HALF ? N / 2 : N);
         }
-    if constexpr (QPW == 1)
+    if constexpr (T == 1 && (RP::WL || RP::R % RP::H == 0))
         RP::template phase2<CPL>(lds, v[0], out);
     else
-        RP::template phase2_multi<QPW, CPL>(lds, v, out);
+        RP::template phase2_multi<T, CPL>(lds, v, out);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if constexpr (ARG)
         {
@@ -1467,7 +1504,22 @@ __global__ void __launch_bounds__(RP::NT) __attribute__((amdgpu_waves_per_eu(
         }
     float rmax = gsdr::wave_max(out.m);
     if (lane == 0) red[wave] = rmax;
+    if constexpr (PPW > 1)
+        {
+            const float rmax1 = gsdr::wave_max(out.m1);
+            if (lane == 0) red[NW + wave] = rmax1;
+        }
     __syncthreads();
+    if constexpr (PPW > 1)
+        {
+            if (threadIdx.x == 0)
+                {
+                    float best1 = red[NW];
+#pragma unroll
+                    for (int w2 = 1; w2 < NW; ++w2) best1 = __builtin_fmaxf(best1, red[NW + w2]);
+                    stats[((size_t)b * P + p + 1) * D + d] = RowStat{best1, 0u, 0.0f, 0};
+                }
+        }
     if (threadIdx.x == 0)
         {
             float best = red[0];

@@ -47,6 +47,9 @@ constexpr SplitId kSplits[] = {{1, 25000}, {12, 32000}, {13, 64000}, {4, 100000}
 // PRN group of an XCD pass: the largest divisor of P whose code rows fit in ~2 MB
 // (half an XCD's L2), so the rows of the group's codes stay resident while the X
 // rows stream past
+#ifndef GSDR_ACQ_PPW_DEFAULT
+#define GSDR_ACQ_PPW_DEFAULT 1
+#endif
 #ifndef GSDR_ACQ_QPW_DEFAULT
 #define GSDR_ACQ_QPW_DEFAULT 2
 #endif
@@ -66,7 +69,7 @@ uint32_t prn_group(uint32_t P, uint32_t N)
 // ARG = false: the grid pass (row maxima into d_stats); ARG = true: the selected
 // rows' pass (keys into d_keys, |R|^2 rows into rowbuf for the peak ratio; the
 // caller zeroes d_keys and runs acq_argmax_split_finish_kernel)
-template <int ROUT, class RP, bool HALF, bool ARG = false, int QPW = 1>
+template <int ROUT, class RP, bool HALF, bool ARG = false, int QPW = 1, int PPW = 1>
 int launch_one(gsdr_acq* a, uint32_t nblocks, hipStream_t s, const gsdr_acq_result* sel = nullptr,
     float* rowbuf = nullptr, float* psum = nullptr, uint32_t* rout = nullptr)
 {
@@ -80,19 +83,25 @@ int launch_one(gsdr_acq* a, uint32_t nblocks, hipStream_t s, const gsdr_acq_resu
     if (ROUT > 1 && !ARG)
         GSDR_HIP(hipMemsetAsync(a->d_stats, 0, (size_t)nblocks * a->nprn * a->D * sizeof(RowStat), s));
     constexpr uint32_t RQ = ROUT / QPW;  // workgroups per transform
-    const uint32_t grid = ARG ? nblocks * a->nprn * RQ : nblocks * a->D * a->nprn * RQ;
-    hipLaunchKernelGGL((acq_correlate_split_kernel<ROUT, RP, HALF, ARG, QPW>), dim3(grid), dim3(RP::NT), (split_lds_bytes<ROUT, RP>()), s,
-        a->d_X, a->d_code_fft, a->d_stats, a->d_tw, a->D, a->nprn, nblocks, prn_group(a->nprn, a->N), a->xm, sel,
+    if (a->nprn % PPW != 0)
+        {
+            gsdr::set_error("internal: %d PRNs per workgroup with %u PRNs", PPW, a->nprn);
+            return GSDR_E_STATE;
+        }
+    const uint32_t grid = ARG ? nblocks * a->nprn * RQ : nblocks * a->D * (a->nprn / PPW) * RQ;
+    hipLaunchKernelGGL((acq_correlate_split_kernel<ROUT, RP, HALF, ARG, QPW, PPW>), dim3(grid), dim3(RP::NT),
+        (split_lds_bytes<ROUT, RP, PPW>()), s,
+        a->d_X, a->d_code_fft, a->d_stats, a->d_tw, a->D, a->nprn, nblocks, prn_group(a->nprn / PPW, a->N * PPW), a->xm, sel,
         a->d_keys, rowbuf, psum);
     GSDR_HIP(hipGetLastError());
     return GSDR_OK;
 }
 
-template <int ROUT, class RP, bool HALF, int QPW = 1>
+template <int ROUT, class RP, bool HALF, int QPW = 1, int PPW = 1>
 int attrs_one()
 {
-    GSDR_HIP(hipFuncSetAttribute((const void*)acq_correlate_split_kernel<ROUT, RP, HALF, false, QPW>,
-        hipFuncAttributeMaxDynamicSharedMemorySize, (int)(split_lds_bytes<ROUT, RP>())));
+    GSDR_HIP(hipFuncSetAttribute((const void*)acq_correlate_split_kernel<ROUT, RP, HALF, false, QPW, PPW>,
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)(split_lds_bytes<ROUT, RP, PPW>())));
     GSDR_HIP(hipFuncSetAttribute((const void*)acq_correlate_split_kernel<ROUT, RP, HALF, true, QPW>,
         hipFuncAttributeMaxDynamicSharedMemorySize, (int)(split_lds_bytes<ROUT, RP>())));
     return GSDR_OK;
@@ -113,6 +122,7 @@ int launch_split_arg(gsdr_acq* a, uint32_t nblocks, hipStream_t s, const gsdr_ac
         case 24:
             return half ? launch_one<4, Reg25kW, true, true, 2>(a, nblocks, s, sel, rowbuf, psum, rout)
                         : launch_one<4, Reg25kW, false, true, 2>(a, nblocks, s, sel, rowbuf, psum, rout);
+        case 25: GSDR_ARG(1, Reg25kW);
         case 12: GSDR_ARG(1, Wl32k);
         case 13: GSDR_ARG(2, Wl32k);
         default: gsdr::set_error("internal: bad split variant %d", a->split); return GSDR_E_STATE;
@@ -149,6 +159,9 @@ int launch_split(gsdr_acq* a, uint32_t nblocks, hipStream_t s)
         case 24:
             return half ? launch_one<4, Reg25kW, true, false, 2>(a, nblocks, s)
                         : launch_one<4, Reg25kW, false, false, 2>(a, nblocks, s);
+        case 25:
+            return half ? launch_one<1, Reg25kW, true, false, 1, 2>(a, nblocks, s)
+                        : launch_one<1, Reg25kW, false, false, 1, 2>(a, nblocks, s);
         case 12: return half ? launch_one<1, Wl32k, true>(a, nblocks, s) : launch_one<1, Wl32k, false>(a, nblocks, s);
         case 13: return half ? launch_one<2, Wl32k, true>(a, nblocks, s) : launch_one<2, Wl32k, false>(a, nblocks, s);
         default: gsdr::set_error("internal: bad split variant %d", a->split); return GSDR_E_STATE;
@@ -181,6 +194,14 @@ int setup_split(gsdr_acq* a)
             if (const char* e = std::getenv("GSDR_ACQ_QPW")) qpw = std::atoi(e);
             if (qpw == 2) a->split = 24;
         }
+    // 25000: two PRNs per 1024-lane workgroup sharing the X row's copies
+    // (GSDR_ACQ_PPW=2, an even PRN count) or one PRN per 512-lane workgroup (1)
+    if (a->split == 1 && a->nprn % 2 == 0)
+        {
+            int ppw = GSDR_ACQ_PPW_DEFAULT;
+            if (const char* e = std::getenv("GSDR_ACQ_PPW")) ppw = std::atoi(e);
+            if (ppw == 2) a->split = 25;
+        }
     if (!a->split) return GSDR_OK;
     int rc = GSDR_OK;
     switch (a->split)
@@ -188,6 +209,10 @@ int setup_split(gsdr_acq* a)
         case 1: rc = attrs_one<1, Reg25k, true>() | attrs_one<1, Reg25k, false>(); break;
         case 4: rc = attrs_one<4, Reg25k, true>() | attrs_one<4, Reg25k, false>(); break;
         case 24: rc = attrs_one<4, Reg25kW, true, 2>() | attrs_one<4, Reg25kW, false, 2>(); break;
+        case 25:
+            rc = attrs_one<1, Reg25kW, true, 1, 2>() | attrs_one<1, Reg25kW, false, 1, 2>() | attrs_one<1, Reg25kW, true>() |
+                 attrs_one<1, Reg25kW, false>();
+            break;
         case 12: rc = attrs_one<1, Wl32k, true>() | attrs_one<1, Wl32k, false>(); break;
         case 13: rc = attrs_one<2, Wl32k, true>() | attrs_one<2, Wl32k, false>(); break;
         default: break;

@@ -160,6 +160,9 @@ int launch_split(gsdr_acq* a, uint32_t nblocks, hipStream_t s)
             return half ? launch_one<4, Reg25kW, true, false, 2>(a, nblocks, s)
                         : launch_one<4, Reg25kW, false, false, 2>(a, nblocks, s);
         case 25:
+            // an odd active PRN count: one PRN per workgroup on the same plan
+            if (a->nprn % 2)
+                return half ? launch_one<1, Reg25kW, true>(a, nblocks, s) : launch_one<1, Reg25kW, false>(a, nblocks, s);
             return half ? launch_one<1, Reg25kW, true, false, 1, 2>(a, nblocks, s)
                         : launch_one<1, Reg25kW, false, false, 1, 2>(a, nblocks, s);
         case 12: return half ? launch_one<1, Wl32k, true>(a, nblocks, s) : launch_one<1, Wl32k, false>(a, nblocks, s);
@@ -195,8 +198,9 @@ int setup_split(gsdr_acq* a)
             if (qpw == 2) a->split = 24;
         }
     // 25000: two PRNs per 1024-lane workgroup sharing the X row's copies
-    // (GSDR_ACQ_PPW=2, an even PRN count) or one PRN per 512-lane workgroup (1)
-    if (a->split == 1 && a->nprn % 2 == 0)
+    // (GSDR_ACQ_PPW=2; a launch with an odd active PRN count runs one per workgroup on
+    // the same plan) or one PRN per 512-lane workgroup (1)
+    if (a->split == 1)
         {
             int ppw = GSDR_ACQ_PPW_DEFAULT;
             if (const char* e = std::getenv("GSDR_ACQ_PPW")) ppw = std::atoi(e);

@@ -319,8 +319,11 @@ void gsdr_acq_destroy(gsdr_acq* a)
             (void)hipEventDestroy(r.b);
         }
     for (hipEvent_t e : a->prof_pool) (void)hipEventDestroy(e);
-    if (a->sub_done) (void)hipEventDestroy(a->sub_done);
-    if (a->h_res) (void)hipHostFree(a->h_res);
+    for (int i = 0; i < gsdr_acq::kSubs; ++i)
+        {
+            if (a->sub_done[i]) (void)hipEventDestroy(a->sub_done[i]);
+            if (a->h_res[i]) (void)hipHostFree(a->h_res[i]);
+        }
     void* bufs[] = {a->st2.d_wipe, a->st2.d_freq, a->d_tw, a->d_wipe, a->d_code_fft, a->d_code_stage, a->d_prn, a->d_X, a->d_stats, a->d_res,
         a->d_iq, a->d_grid, a->d_rowbuf, a->d_keys, a->d_psum, a->d_fscratch, a->d_dgrid, a->d_tw_sub, a->d_scratch, a->d_slots, a->d_resk, a->d_acc, a->d_acc_slots};
     for (void* p : bufs)
@@ -510,14 +513,16 @@ int gsdr_acq_submit_stream(gsdr_acq* a, gsdr_stream* ring, uint64_t first_sample
         a->conf.item_type);
     GSDR_REQUIRE(gsdr::stream_device(ring) == a->device, GSDR_E_ARG,
         "gsdr_acq_submit_stream: ring on device %d, acquisition handle on device %d", gsdr::stream_device(ring), a->device);
-    GSDR_REQUIRE(!a->sub_pending, GSDR_E_STATE, "gsdr_acq_submit_stream: collect the previous submission first");
     std::lock_guard<std::mutex> lk(a->mu);
+    GSDR_REQUIRE(a->sub_count < gsdr_acq::kSubs, GSDR_E_STATE,
+        "gsdr_acq_submit_stream: %d submissions in flight, collect the oldest first", gsdr_acq::kSubs);
     gsdr::DeviceGuard g(a->device);
-    if (!a->h_res)
+    const int slot = (a->sub_head + a->sub_count) % gsdr_acq::kSubs;
+    if (!a->h_res[slot])
         {
-            GSDR_HIP(hipHostMalloc(&a->h_res, (size_t)a->conf.max_blocks * a->conf.max_prns * sizeof(gsdr_acq_result),
-                hipHostMallocDefault));
-            GSDR_HIP(hipEventCreateWithFlags(&a->sub_done, hipEventDisableTiming));
+            GSDR_HIP(hipHostMalloc(&a->h_res[slot],
+                (size_t)a->conf.max_blocks * a->conf.max_prns * sizeof(gsdr_acq_result), hipHostMallocDefault));
+            GSDR_HIP(hipEventCreateWithFlags(&a->sub_done[slot], hipEventDisableTiming));
         }
     {
         gsdr::StreamReader rd(ring);  // ring lock from view to reader-event record
@@ -531,25 +536,28 @@ int gsdr_acq_submit_stream(gsdr_acq* a, gsdr_stream* ring, uint64_t first_sample
         rc = rd.release(a->stream);
         if (rc != GSDR_OK) return rc;
     }
-    GSDR_HIP(hipMemcpyAsync(a->h_res, a->d_res, (size_t)nblocks * a->nprn * sizeof(gsdr_acq_result),
+    GSDR_HIP(hipMemcpyAsync(a->h_res[slot], a->d_res, (size_t)nblocks * a->nprn * sizeof(gsdr_acq_result),
         hipMemcpyDeviceToHost, a->stream));
-    GSDR_HIP(hipEventRecord(a->sub_done, a->stream));
-    a->sub_blocks = nblocks;
-    a->sub_nprn = a->nprn;
-    a->sub_pending = true;
+    GSDR_HIP(hipEventRecord(a->sub_done[slot], a->stream));
+    a->sub_blocks[slot] = nblocks;
+    a->sub_nprn[slot] = a->nprn;
+    a->sub_count++;
     return GSDR_OK;
 }
 
 int gsdr_acq_collect(gsdr_acq* a, gsdr_acq_result* out, uint32_t* nblocks, uint32_t* nprn)
 {
     GSDR_REQUIRE(a && out, GSDR_E_ARG, "gsdr_acq_collect: null argument");
-    GSDR_REQUIRE(a->sub_pending, GSDR_E_STATE, "gsdr_acq_collect: nothing submitted");
+    std::lock_guard<std::mutex> lk(a->mu);
+    GSDR_REQUIRE(a->sub_count > 0, GSDR_E_STATE, "gsdr_acq_collect: nothing submitted");
     gsdr::DeviceGuard g(a->device);
-    a->sub_pending = false;
-    GSDR_HIP(hipEventSynchronize(a->sub_done));
-    std::memcpy(out, a->h_res, (size_t)a->sub_blocks * a->sub_nprn * sizeof(gsdr_acq_result));
-    if (nblocks) *nblocks = a->sub_blocks;
-    if (nprn) *nprn = a->sub_nprn;
+    const int slot = a->sub_head;
+    a->sub_head = (a->sub_head + 1) % gsdr_acq::kSubs;
+    a->sub_count--;
+    GSDR_HIP(hipEventSynchronize(a->sub_done[slot]));
+    std::memcpy(out, a->h_res[slot], (size_t)a->sub_blocks[slot] * a->sub_nprn[slot] * sizeof(gsdr_acq_result));
+    if (nblocks) *nblocks = a->sub_blocks[slot];
+    if (nprn) *nprn = a->sub_nprn[slot];
     return GSDR_OK;
 }
 

@@ -2483,12 +2483,15 @@ struct gsdr_acq
     float2* d_X{nullptr};
     RowStat* d_stats{nullptr};
     gsdr_acq_result* d_res{nullptr};
-    // gsdr_acq_submit_stream / gsdr_acq_collect: pinned results of the submitted
-    // attempts (max_blocks x max_prns), their completion event and shape
-    gsdr_acq_result* h_res{nullptr};
-    hipEvent_t sub_done{nullptr};
-    uint32_t sub_blocks{0}, sub_nprn{0};
-    bool sub_pending{false};
+    // gsdr_acq_submit_stream / gsdr_acq_collect: up to kSubs submissions in flight,
+    // each with its pinned results (max_blocks x max_prns), completion event and shape;
+    // a later submission's grid reuses d_res on the same stream, ordered after the
+    // earlier one's copy out of it
+    static constexpr int kSubs = 2;
+    gsdr_acq_result* h_res[kSubs]{};
+    hipEvent_t sub_done[kSubs]{};
+    uint32_t sub_blocks[kSubs]{}, sub_nprn[kSubs]{};
+    int sub_head{0}, sub_count{0};
     void* d_iq{nullptr};
     float* d_grid{nullptr};
     float* d_rowbuf{nullptr};  // split path, peak ratio: the selected rows' |R|^2 (max_blocks x max_prns x N)

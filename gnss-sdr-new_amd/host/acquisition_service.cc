@@ -42,7 +42,7 @@ AcquisitionService::AcquisitionService(const Acq_Conf& conf, uint32_t max_reques
 
 AcquisitionService::~AcquisitionService()
 {
-    if (d_flight.active)
+    for (; !d_flights.empty(); d_flights.pop_front())
         {
             uint32_t nb = 0, np = 0;
             gsdr_acq_collect(d_engine, d_res.data(), &nb, &np);
@@ -201,14 +201,18 @@ int AcquisitionService::work(const void* in, int ninput_items)
     return used;
 }
 
-void AcquisitionService::flush()
+void AcquisitionService::collect_oldest()
 {
-    if (!d_flight.active) return;
-    d_flight.active = false;
+    const Flight f = std::move(d_flights.front());
+    d_flights.pop_front();
     uint32_t nb = 0, np = 0;
     const int rc = gsdr_acq_collect(d_engine, d_res.data(), &nb, &np);
-    answer(d_res, rc == GSDR_OK ? nb : 1, rc == GSDR_OK ? np : static_cast<uint32_t>(d_flight.gen.size()), d_flight.gen,
-        rc != GSDR_OK);
+    answer(d_res, rc == GSDR_OK ? nb : 1, rc == GSDR_OK ? np : static_cast<uint32_t>(f.gen.size()), f.gen, rc != GSDR_OK);
+}
+
+void AcquisitionService::flush()
+{
+    while (!d_flights.empty()) collect_oldest();
 }
 
 int AcquisitionService::work_ring(gsdr_stream* ring, uint64_t head)
@@ -222,8 +226,6 @@ int AcquisitionService::work_ring(gsdr_stream* ring, uint64_t head)
         }
     const uint64_t ready = head > d_ring_cursor ? (head - d_ring_cursor) / d_consumed : 0;
     if (ready < d_batch) return 0;  // a full batch of blocks per launch
-    // the launch in flight first: its answers re-arm the requests of this one
-    flush();
     int blocks = 0;
     // blocks the ring no longer holds (the caller pushed past them) are skipped
     uint64_t span_first = 0, span_n = 0;
@@ -237,10 +239,15 @@ int AcquisitionService::work_ring(gsdr_stream* ring, uint64_t head)
     while (left >= d_batch)
         {
             const uint32_t nb = d_batch;
+            // two launches in flight: answer the oldest before a third (its answers
+            // re-arm requests)
+            if (d_flights.size() >= kMaxFlights) collect_oldest();
+            Flight f;
+            f.nblocks = nb;
             bool any;
             {
                 std::lock_guard<std::mutex> lk(d_mu);
-                any = prepare_locked(d_flight.gen);
+                any = prepare_locked(f.gen);
             }
             if (any)
                 {
@@ -249,16 +256,14 @@ int AcquisitionService::work_ring(gsdr_stream* ring, uint64_t head)
                     ++d_launches;
                     d_grids += nb;
                     if (rc != GSDR_OK)
-                        answer(d_res, 1, static_cast<uint32_t>(d_flight.gen.size()), d_flight.gen, true);
+                        answer(d_res, 1, static_cast<uint32_t>(f.gen.size()), f.gen, true);
                     else
-                        d_flight.active = true;
+                        d_flights.push_back(std::move(f));
                 }
             d_ring_cursor += static_cast<uint64_t>(nb) * d_consumed;
             d_sample_counter = d_ring_cursor;
             blocks += static_cast<int>(nb);
             left -= nb;
-            // more than one batch behind: answer this one before the next
-            if (left >= d_batch) flush();
         }
     return blocks;
 }

@@ -16,15 +16,18 @@
 // transforms its replica only when the slot's PRN changes (set_local_code runs once
 // per PRN assignment in the reference, pcps_acquisition.cc:176-209); re-arming the
 // same PRN after an answer costs nothing.  On the device ring the service runs up
-// to batch_blocks ready blocks in one launch and collects the results one
-// work_ring call later (the launch overlaps the caller's pushes and tracking); a
-// request re-armed by its callback with the same PRN is answered by the next block
-// of the same launch.
+// to batch_blocks ready blocks per launch with up to two launches in flight (the
+// second queued behind the first, so the GPU does not idle while the host answers
+// the first); a launch's results are collected before a third is submitted or at
+// flush().  A request stays armed until its answer is processed, so a launch
+// submitted before that searches it again; a request re-armed by its callback with
+// the same PRN is answered by the next block of the launches in flight.
 #ifndef GSDR_HOST_ACQUISITION_SERVICE_H
 #define GSDR_HOST_ACQUISITION_SERVICE_H
 
 #include <complex>
 #include <cstdint>
+#include <deque>
 #include <functional>
 #include <mutex>
 #include <vector>
@@ -64,7 +67,7 @@ public:
     // answers the launch in flight at the next call.  The first call sets the block
     // grid's origin at `head`.  Returns the blocks consumed.
     int work_ring(gsdr_stream* ring, uint64_t head);
-    // answers the launch in flight (if any)
+    // answers the launches in flight (if any)
     void flush();
 
     float threshold() const { return d_threshold; }
@@ -87,10 +90,11 @@ private:
     };
     struct Flight
     {
-        bool active{false};
         uint32_t nblocks{0};
         std::vector<uint64_t> gen;  // per slot at submission (slots [0, nprn))
     };
+    static constexpr size_t kMaxFlights = 2;  // gsdr_acq_submit_stream's queue depth
+    void collect_oldest();
     // uploads the armed slots' pending replicas and sets the active PRN count;
     // false when nothing is armed (lock held)
     bool prepare_locked(std::vector<uint64_t>& gen);
@@ -115,7 +119,7 @@ private:
     uint64_t d_code_uploads{0};
     bool d_ring_started{false};
     uint64_t d_ring_cursor{0};  // absolute sample index of the next block on the ring
-    Flight d_flight;
+    std::deque<Flight> d_flights;  // launches in flight, oldest first
     std::vector<gsdr_acq_result> d_res;
     mutable std::mutex d_mu;
 };

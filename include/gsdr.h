@@ -275,7 +275,8 @@ int gsdr_acq_run_stream(gsdr_acq* acq, gsdr_stream* stream, uint64_t first_sampl
  * launched on the handle's stream with the results copied into the handle's pinned
  * buffer; returns without waiting.  gsdr_acq_collect waits for them and copies the
  * nblocks * nprn results (block-major, nprn = the active count at submission) to
- * out_host.  One submission in flight per handle. */
+ * out_host.  Up to two submissions in flight per handle (the second queued behind
+ * the first on the handle's stream), collected oldest first. */
 int gsdr_acq_submit_stream(gsdr_acq* acq, gsdr_stream* stream, uint64_t first_sample, uint32_t nblocks,
     uint64_t stamp0);
 int gsdr_acq_collect(gsdr_acq* acq, gsdr_acq_result* out_host, uint32_t* nblocks, uint32_t* nprn);

@@ -681,6 +681,11 @@ def main(argv=None, backend=DeviceBackend):
                     help="comma list of the chains' block counts (sum = --blocks), overriding --acq-chains: unequal "
                          "chains drift out of step, so one chain's forward / reduce / argmax launches overlap the "
                          "other's correlate instead of coinciding with it")
+    ap.add_argument("--acq-stagger", type=int, default=0,
+                    help="two chains: move this many blocks from one chain to the other on alternate steps "
+                         "(sizes B/2 + s, B/2 - s, then B/2 - s, B/2 + s), so the chains' forward / reduce / argmax "
+                         "launches fall inside the other chain's correlate instead of coinciding; every step still "
+                         "acquires its B blocks")
     ap.add_argument("--trk-stream", action="store_true",
                     help="(default) tracking follows one continuous stream: the batch repeated end to end (Dopplers on "
                          "whole cycles per batch, so the repetition is a continuous signal), one tracking launch "
@@ -739,10 +744,14 @@ def main(argv=None, backend=DeviceBackend):
         assert B % nch0 == 0, "--blocks must be a multiple of --acq-chains"
         sizes = [B // nch0] * nch0
     nch = len(sizes)
-    offs = [sum(sizes[:i]) for i in range(nch)]  # each chain's first block within the rank's span
+    stagger = args.acq_stagger if (nch == 2 and not args.acq_sizes) else 0
+    assert 0 <= stagger < sizes[0], "--acq-stagger must be below the chain size"
+    # per-step chain sizes: alternate steps swap which chain takes the extra blocks
+    step_sizes = ([sizes[0] + stagger, sizes[1] - stagger], [sizes[0] - stagger, sizes[1] + stagger]) if stagger \
+        else (sizes, sizes)
     acqs = []
     for i in range(nch):
-        a = gsdr.Acquisition(FS, N, DMAX, DSTEP, pfa=PFA, max_prns=P, max_blocks=sizes[i], num_doppler_bins=D,
+        a = gsdr.Acquisition(FS, N, DMAX, DSTEP, pfa=PFA, max_prns=P, max_blocks=sizes[i] + stagger, num_doppler_bins=D,
                              device=local)
         a.set_local_codes(codes, np.arange(1, P + 1))
         acqs.append(a)
@@ -783,10 +792,13 @@ def main(argv=None, backend=DeviceBackend):
             # re-read from L2 / MALL)
             span = step_no[0] % (W + K + 1) if args.trk_stream else 0
             src = iq_long if args.trk_stream else iq_dev
+            sz = step_sizes[step_no[0] % 2]
+            off = 0
             for i, a in enumerate(acqs):
-                b0 = lo + offs[i]
-                a.run_device(src.data_ptr() + (span * total + b0) * N * 8, sizes[i], N, (span * total + b0) * N,
-                             res_dev.data_ptr() + offs[i] * P * gsdr.ACQ_RESULT_DTYPE.itemsize)
+                b0 = lo + off
+                a.run_device(src.data_ptr() + (span * total + b0) * N * 8, sz[i], N, (span * total + b0) * N,
+                             res_dev.data_ptr() + off * P * gsdr.ACQ_RESULT_DTYPE.itemsize)
+                off += sz[i]
         step_no[0] += 1
 
     if args.trk_stream:
@@ -902,6 +914,7 @@ def main(argv=None, backend=DeviceBackend):
                              if args.cu_partition else None),
             "acq_chains": nch,
             "acq_chain_blocks": sizes,
+            "acq_stagger": stagger,
             "acq_input": ("each step acquires its own span of the continuous stream (new HBM addresses)"
                           if args.trk_stream else "the same span every step"),
             # the carrier model and the forward spectra computed per block (include/gsdr.h
@@ -1011,10 +1024,13 @@ def main(argv=None, backend=DeviceBackend):
             for k in range(K):
                 span = k if args.trk_stream else 0  # the timed region's spans (step())
                 src = iq_long if args.trk_stream else iq_dev
+                sz = step_sizes[k % 2]
+                off = 0
                 for i, a in enumerate(acqs):
-                    b0 = lo + offs[i]
-                    a.run_device(src.data_ptr() + (span * total + b0) * N * 8, sizes[i], N, (span * total + b0) * N,
-                                 res_dev.data_ptr() + offs[i] * P * gsdr.ACQ_RESULT_DTYPE.itemsize)
+                    b0 = lo + off
+                    a.run_device(src.data_ptr() + (span * total + b0) * N * 8, sz[i], N, (span * total + b0) * N,
+                                 res_dev.data_ptr() + off * P * gsdr.ACQ_RESULT_DTYPE.itemsize)
+                    off += sz[i]
 
         def trk_only():
             trk.restore_state(0)

@@ -18,11 +18,6 @@ using Wl32k = RegFourStep<32, 1024, 0, 1, NoPads<1000>, 10, 10, 10>;
 // 25000 = 25 x (10 x 10 x 10) on 1024 lanes, one column per lane, 10 rows per LDS
 // round: the plan of the two-sub-transform workgroups (QPW 2) of 100000 = 4 x 25000
 using Reg25kW = RegFourStep<25, 1024, 10, 1, NoPads<1000>, 10, 10, 10>;
-// 25000 on 512 lanes with 10 rows per LDS round (80 KB, rounds 10 + 10 + 5 through
-// phase2_multi): 3 rounds instead of 5, so 18 workgroup barriers instead of 30
-// (GSDR_ACQ_25K_PLAN=1, A/B against the default 5-row rounds; capped at 128 VGPRs for
-// two workgroups per CU)
-using Reg25kH10 = RegFourStep<25, 512, 10, 4, NoPads<1000>, 10, 10, 10>;
 
 // split ids: (N, outer radix ROUT, inner plan)
 //   1: 25000 = 1 x 25000 (C5 GPS L1 / BeiDou B1I at 25 Msps, 1 ms)
@@ -33,6 +28,8 @@ using Reg25kH10 = RegFourStep<25, 512, 10, 4, NoPads<1000>, 10, 10, 10>;
 // Measured and removed: round 4's 100000 = 2 x 50000 (25 x 2000 register
 // four-step, 164 B/lane of spills, -3.5 %), the outer DIF step as its own pass (-11 % /
 // -29 %), mirror-pair loads of the Hermitian code spectra (within +-3 %); round 5's
+// round 6's 25000 alternatives (profiles/r06j): 10-row LDS rounds on 512 lanes (capped at
+// 128 VGPRs, -3-5 %) and one column per lane on 1024 lanes (-22 %); round 5's
 // pruning of the alternatives that lost their A/Bs: 32000 / 64000 on 8-row LDS rounds
 // (ids 2 / 3, -4 % / -10 %), the 16000-based splits (5 / 6), the wave-local 25000 /
 // 100000 plans (11 / 14 / 17 / 18, -25 % / -20 % at 25000), 2 x / 4 x 16000 wave-local
@@ -127,9 +124,7 @@ int launch_split_arg(gsdr_acq* a, uint32_t nblocks, hipStream_t s, const gsdr_ac
         case 24:
             return half ? launch_one<4, Reg25kW, true, true, 2>(a, nblocks, s, sel, rowbuf, psum, rout)
                         : launch_one<4, Reg25kW, false, true, 2>(a, nblocks, s, sel, rowbuf, psum, rout);
-        case 25:
-        case 27: GSDR_ARG(1, Reg25kW);
-        case 26: GSDR_ARG(1, Reg25kH10);
+        case 25: GSDR_ARG(1, Reg25kW);
         case 12: GSDR_ARG(1, Wl32k);
         case 13: GSDR_ARG(2, Wl32k);
         default: gsdr::set_error("internal: bad split variant %d", a->split); return GSDR_E_STATE;
@@ -172,9 +167,6 @@ int launch_split(gsdr_acq* a, uint32_t nblocks, hipStream_t s)
                 return half ? launch_one<1, Reg25kW, true>(a, nblocks, s) : launch_one<1, Reg25kW, false>(a, nblocks, s);
             return half ? launch_one<1, Reg25kW, true, false, 1, 2>(a, nblocks, s)
                         : launch_one<1, Reg25kW, false, false, 1, 2>(a, nblocks, s);
-        case 26:
-            return half ? launch_one<1, Reg25kH10, true>(a, nblocks, s) : launch_one<1, Reg25kH10, false>(a, nblocks, s);
-        case 27: return half ? launch_one<1, Reg25kW, true>(a, nblocks, s) : launch_one<1, Reg25kW, false>(a, nblocks, s);
         case 12: return half ? launch_one<1, Wl32k, true>(a, nblocks, s) : launch_one<1, Wl32k, false>(a, nblocks, s);
         case 13: return half ? launch_one<2, Wl32k, true>(a, nblocks, s) : launch_one<2, Wl32k, false>(a, nblocks, s);
         default: gsdr::set_error("internal: bad split variant %d", a->split); return GSDR_E_STATE;
@@ -215,14 +207,6 @@ int setup_split(gsdr_acq* a)
             int ppw = GSDR_ACQ_PPW_DEFAULT;
             if (const char* e = std::getenv("GSDR_ACQ_PPW")) ppw = std::atoi(e);
             if (ppw == 2) a->split = 25;
-            // A/B plans for 25000 (one PRN per workgroup): 1 = 10-row LDS rounds on 512
-            // lanes, 2 = one column per lane on 1024 lanes (Reg25kW)
-            if (const char* e = std::getenv("GSDR_ACQ_25K_PLAN"))
-                {
-                    const int pl = std::atoi(e);
-                    if (pl == 1) a->split = 26;
-                    if (pl == 2) a->split = 27;
-                }
         }
     if (!a->split) return GSDR_OK;
     int rc = GSDR_OK;
@@ -235,8 +219,6 @@ int setup_split(gsdr_acq* a)
             rc = attrs_one<1, Reg25kW, true, 1, 2>() | attrs_one<1, Reg25kW, false, 1, 2>() | attrs_one<1, Reg25kW, true>() |
                  attrs_one<1, Reg25kW, false>();
             break;
-        case 26: rc = attrs_one<1, Reg25kH10, true>() | attrs_one<1, Reg25kH10, false>(); break;
-        case 27: rc = attrs_one<1, Reg25kW, true>() | attrs_one<1, Reg25kW, false>(); break;
         case 12: rc = attrs_one<1, Wl32k, true>() | attrs_one<1, Wl32k, false>(); break;
         case 13: rc = attrs_one<2, Wl32k, true>() | attrs_one<2, Wl32k, false>(); break;
         default: break;

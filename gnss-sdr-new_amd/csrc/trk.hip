@@ -156,7 +156,7 @@ __host__ __device__ inline void lf_initialize(LoopFilter& f, float y0)  // :258-
     f.idx = 3;
 }
 
-// Tracking_loop_filter::apply on a filter held in registers (wave 1's speculative
+// Tracking_loop_filter::apply on a filter held in registers (wave 3's speculative
 // DLL/PLL): the ring elements are separate scalars picked by selects -- with arrays
 // the compiler turned the selects back into a run-time index, i.e. a scratch access
 // (and the LDS form was a chain of dependent LDS round trips).  The reference's
@@ -446,10 +446,11 @@ __device__ __forceinline__ void seq_sums(const float* terms, int stride, int n, 
 }
 
 // cn0_and_tracking_lock_status (:970-1056) with cn0_m2m4_estimator and
-// carrier_lock_detector (lock_detectors.cc:90-148); wave 0, lane = element,
+// carrier_lock_detector (lock_detectors.cc:90-148); wave 2 on its copy of the
+// call's state (Cn0Spec), lane = element,
 // sums in element order through `scratch` (3 x kMaxCn0 floats of LDS).  Returns 0 on a
 // loss of lock, 1 while the prompt buffer fills, 2 with a full buffer: then the EVM
-// (:1027-1053, an output only) is the one wave 1 computed (evm_of).
+// (:1027-1053, an output only) is the one wave 1 computes (evm_of).
 __device__ inline int cn0_and_lock(const TrkConst& c, TrkHot& t, float2* pbuf, float (*scratch)[kMaxCn0], double coh,
     int lane)
 {
@@ -516,12 +517,13 @@ __device__ inline int cn0_and_lock(const TrkConst& c, TrkHot& t, float2* pbuf, f
 // the prompt buffer with this call's prompt (a full buffer: cn0_estimation_counter >=
 // cn0_samples before the call): the same float sums in element order as the oracle,
 // through `scratch` (2 x kMaxCn0 floats of LDS).
-__device__ inline double evm_of(const TrkConst& c, const TrkHot& t, const float2* pbuf, float* scratch, int lane)
+__device__ inline double evm_of(const TrkConst& c, int cn0_counter, float2 p_accu, const float2* pbuf, float* scratch,
+    int lane)
 {
     const int n = c.cn0_samples;
-    const int widx = t.cn0_estimation_counter % n;
+    const int widx = cn0_counter % n;
     float2 ei = make_float2(0.f, 0.f);
-    if (lane < n) ei = lane == widx ? t.P_accu : pbuf[lane];
+    if (lane < n) ei = lane == widx ? p_accu : pbuf[lane];
     scratch[lane] = ei.x * ei.x;  // sum of squared in-phase prompts
     float s1[1];
     seq_sums<1>(scratch, 0, n, s1);
@@ -539,7 +541,11 @@ __device__ inline double evm_of(const TrkConst& c, const TrkHot& t, const float2
     return sqrt((double)(s2[0] / fn / 1.0F));
 }
 
-__device__ inline void run_dll_pll(const TrkConst& c, TrkHot& t, LfReg& lf)  // :1092-1179 (no Doppler correction)
+// run_dll_pll (:1092-1179, no Doppler correction) as its two independent halves, on
+// two waves: the carrier loop (PLL / FLL discriminators and filter) and the code loop
+// (DLL discriminator and filter); the carrier aiding term, the one product of the two,
+// is added where they are joined (take_dll_pll), in the reference's order
+__device__ inline void run_pll(const TrkConst& c, TrkHot& t)
 {
     const double carr_phase_error_hz =
         (t.cloop ? pll_cloop_two_quadrant_atan(t.P_accu) : pll_four_quadrant_atan(t.P_accu)) / kTwoPi;
@@ -560,15 +566,19 @@ __device__ inline void run_dll_pll(const TrkConst& c, TrkHot& t, LfReg& lf)  // 
             carr_error_filt_hz = (double)cf_error(t.narrow ? c.cf_narrow : c.cf, t, 0, (float)carr_phase_error_hz, (float)t.corr_time);
         }
     t.carrier_doppler_hz = carr_error_filt_hz;
+    t.log_err[0] = (float)carr_phase_error_hz;
+    t.log_err[1] = (float)carr_error_filt_hz;
+}
+
+// the code loop's d_code_freq_chips before the carrier aiding term
+__device__ inline double run_dll(const TrkConst& c, TrkHot& t, LfReg& lf)
+{
     const double code_error_chips =
         c.veml ? dll_nc_vemlp(t.VE_accu, t.E_accu, t.L_accu, t.VL_accu) : dll_nc_e_minus_l(t.E_accu, t.L_accu, t.spc, 1.0F, 1.0F);
     const double code_error_filt_chips = (double)lf_apply(lf, (float)code_error_chips);
-    t.code_freq_chips = c.code_chip_rate - code_error_filt_chips;
-    t.log_err[0] = (float)carr_phase_error_hz;
-    t.log_err[1] = (float)carr_error_filt_hz;
     t.log_err[2] = (float)code_error_chips;
     t.log_err[3] = (float)code_error_filt_chips;
-    if (c.carrier_aiding) t.code_freq_chips += t.carrier_doppler_hz * c.code_chip_rate / c.signal_carrier_freq;
+    return c.code_chip_rate - code_error_filt_chips;
 }
 
 // high_dyn rate estimate (:1232-1251, :1265-1284): mean of the newest
@@ -761,54 +771,112 @@ __device__ __forceinline__ void tprobe(bool on, uint64_t (&pr)[3], int i)
     if (on) pr[i] = wall_clock64();
 }
 
-// run_dll_pll of a call computed speculatively by wave 1 (states 2 and 4): the
-// discriminators and loop filters read nothing the CN0 estimator and lock detector
-// write, so wave 1 runs them on its own copy of the state -- into the code loop
-// filter slot that is not current -- while wave 0 evaluates the lock; wave 0 takes
-// the results when the call stays locked (and drops them on a loss of lock).
-// Same operations on the same values: the loop is bit-identical to run_dll_pll on
-// wave 0.
-struct DllPllSpec
+// run_dll_pll of a call computed speculatively (states 2 and 4) as its two halves:
+// the carrier loop on wave 1, the code loop on wave 3 (into the code loop filter slot
+// that is not current).  The discriminators and loop filters read nothing the CN0
+// estimator and lock detector (wave 2) write, so each wave runs on its own copy of
+// the state; wave 0 takes the results when the call stays locked (and drops them on a
+// loss of lock).  Same operations on the same values: the loop is bit-identical to
+// run_dll_pll on one wave (round 6: C2 call 6.2 -> 5.6 us, C5 GPS 10.8 -> 10.1 us,
+// profiles/r06k3).
+struct DllPllSpec  // wave 1's carrier loop of a call
 {
-    double carrier_doppler_hz, code_freq_chips;
+    double carrier_doppler_hz;
     float2 P_accu_old;
     float cf_w, cf_x;
-    float log_err[4];
+    float log_err[2];
+};
+
+// cn0_and_tracking_lock_status of a call computed by wave 2 (states 2 and 4): the
+// fields it writes are disjoint from everything run_dll_pll, update_tracking_vars and
+// the state transitions read or write, so wave 0 runs the locked branch without it and
+// takes these results afterwards; on a loss of lock (rare) it rebuilds the call from
+// the state at the call's start (s_t) exactly as the reference's early return leaves it.
+struct Cn0Spec
+{
+    double cn0_db_hz, carrier_lock_test;
+    float sm_old[2], sm_sum[2];
+    int32_t sm_counter[2], sm_init[2];
+    int32_t cn0_estimation_counter, carrier_lock_fail_counter, code_lock_fail_counter, locked;
+};
+
+__device__ __forceinline__ void cn0_publish(Cn0Spec& r, const TrkHot& t, int locked)
+{
+    r.cn0_db_hz = t.cn0_db_hz;
+    r.carrier_lock_test = t.carrier_lock_test;
+    for (int w = 0; w < 2; ++w)
+        {
+            r.sm_old[w] = t.sm_old[w];
+            r.sm_sum[w] = t.sm_sum[w];
+            r.sm_counter[w] = t.sm_counter[w];
+            r.sm_init[w] = t.sm_init[w];
+        }
+    r.cn0_estimation_counter = t.cn0_estimation_counter;
+    r.carrier_lock_fail_counter = t.carrier_lock_fail_counter;
+    r.code_lock_fail_counter = t.code_lock_fail_counter;
+    r.locked = locked;
+}
+
+__device__ __forceinline__ void cn0_apply(TrkHot& t, const Cn0Spec& r)
+{
+    t.cn0_db_hz = r.cn0_db_hz;
+    t.carrier_lock_test = r.carrier_lock_test;
+    for (int w = 0; w < 2; ++w)
+        {
+            t.sm_old[w] = r.sm_old[w];
+            t.sm_sum[w] = r.sm_sum[w];
+            t.sm_counter[w] = r.sm_counter[w];
+            t.sm_init[w] = r.sm_init[w];
+        }
+    t.cn0_estimation_counter = r.cn0_estimation_counter;
+    t.carrier_lock_fail_counter = r.carrier_lock_fail_counter;
+    t.code_lock_fail_counter = r.code_lock_fail_counter;
+}
+
+struct DllSpec  // wave 3's code loop of a call
+{
+    double code_freq_base;  // c.code_chip_rate - the filtered code error
+    float log_err2, log_err3;
 };
 
 struct SpecLink
 {
     DllPllSpec* res;   // LDS
+    DllSpec* dres;     // LDS
+    int* dready;       // LDS: the call index whose code loop dres holds
     int* ready;        // LDS: the call index whose results res holds
     LoopFilter* lfs;   // LDS: the code loop filter's two slots
-    int* lfi_lds;      // LDS: the current slot (read by wave 1 at the start of a call)
+    int* lfi_lds;      // LDS: the current slot (read by wave 3 at the start of a call)
     int lfi;           // wave 0: the current slot
     int e;             // wave 0: this call's index
 };
 
-__device__ inline void take_dll_pll(TrkHot& t, SpecLink& sl)
+__device__ inline void take_dll_pll(const TrkConst& c, TrkHot& t, SpecLink& sl)
 {
     while (__hip_atomic_load(sl.ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != sl.e)
         __builtin_amdgcn_s_sleep(1);
     const DllPllSpec r = *sl.res;
     t.carrier_doppler_hz = r.carrier_doppler_hz;
-    t.code_freq_chips = r.code_freq_chips;
     t.P_accu_old = r.P_accu_old;
     t.cf_w = r.cf_w;
     t.cf_x = r.cf_x;
-    for (int i = 0; i < 4; ++i) t.log_err[i] = r.log_err[i];
-    sl.lfi ^= 1;  // wave 1 filtered into the other slot
+    t.log_err[0] = r.log_err[0];
+    t.log_err[1] = r.log_err[1];
+    while (__hip_atomic_load(sl.dready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != sl.e)
+        __builtin_amdgcn_s_sleep(1);
+    const DllSpec d = *sl.dres;
+    t.code_freq_chips = d.code_freq_base;
+    t.log_err[2] = d.log_err2;
+    t.log_err[3] = d.log_err3;
+    if (c.carrier_aiding) t.code_freq_chips += t.carrier_doppler_hz * c.code_chip_rate / c.signal_carrier_freq;
+    sl.lfi ^= 1;  // wave 3 filtered into the other slot
 }
 
-__device__ inline void after_correlation(const TrkConst& c, TrkHot& t, TrkChan* gc, SpecLink& sl, float2* pbuf,
-    float (*scratch)[kMaxCn0], const float2 (&taps)[kMaxTrkTaps + 1], const float2 (&epl)[3], uint64_t nitems_read,
-    int lane, EpochOut& o, bool tm, uint64_t (&pr)[3])
+// The call's accumulators before the lock test (states 2 and 4, :1828-1845 / :2032):
+// shared by wave 2's lock test, wave 0's locked branch and its rebuild after a loss
+__device__ __forceinline__ void pre_lock(const TrkConst& c, TrkHot& t, const float2 (&taps)[kMaxTrkTaps + 1],
+    const float2 (&epl)[3], uint64_t nitems_read)
 {
-    o.flags = 0;
-    o.evm = false;
-    o.prompt_i = 0.0;
-    o.prompt_q = 0.0;
-    for (int i = 0; i < 5; ++i) o.log_accu[i] = 0.0F;
     if (t.state == 2)
         {
             if (c.veml)
@@ -822,20 +890,34 @@ __device__ inline void after_correlation(const TrkConst& c, TrkHot& t, TrkChan* 
             t.spc = c.early_late_space_chips;
             if (nitems_read < c.acq_sample_stamp || nitems_read - c.acq_sample_stamp >= c.bit_sync_span)
                 t.carrier_lock_fail_counter = 300000;
-            const int locked = cn0_and_lock(c, t, pbuf, scratch, c.code_period, lane);
+        }
+    else
+        save_correlation_results(c, t, taps, epl);
+}
+
+__device__ __forceinline__ void init_out(EpochOut& o)
+{
+    o.flags = 0;
+    o.evm = false;
+    o.prompt_i = 0.0;
+    o.prompt_q = 0.0;
+    for (int i = 0; i < 5; ++i) o.log_accu[i] = 0.0F;
+}
+
+// States 2 and 4 run the branch of a call that stays locked; the lock test's results
+// come from wave 2 (Cn0Spec) and the caller undoes the branch on a loss of lock.
+__device__ inline void after_correlation(const TrkConst& c, TrkHot& t, TrkChan* gc, SpecLink& sl,
+    const float2 (&taps)[kMaxTrkTaps + 1], const float2 (&epl)[3], uint64_t nitems_read, EpochOut& o, bool tm,
+    uint64_t (&pr)[3])
+{
+    init_out(o);
+    if (t.state == 2)
+        {
+            pre_lock(c, t, taps, epl, nitems_read);
             tprobe(tm, pr, 0);
-            if (!locked)
-                {
-                    clear_tracking_vars(t);
-                    if (c.track_pilot) t.P_data_accu = make_float2(0.f, 0.f);
-                    t.state = 0;
-                    o.flags |= GSDR_TRK_F_LOSS_OF_LOCK;
-                }
-            else
                 {
                     int next_state = 0;
-                    o.evm = locked == 2;
-                    take_dll_pll(t, sl);
+                    take_dll_pll(c, t, sl);
                     tprobe(tm, pr, 1);
                     update_tracking_vars(c, t, gc);
                     tprobe(tm, pr, 2);
@@ -898,20 +980,10 @@ __device__ inline void after_correlation(const TrkConst& c, TrkHot& t, TrkChan* 
         }
     else  // state 4
         {
-            save_correlation_results(c, t, taps, epl);
-            const int locked = cn0_and_lock(c, t, pbuf, scratch, c.code_period * (double)c.extend_correlation_symbols, lane);
+            pre_lock(c, t, taps, epl, nitems_read);
             tprobe(tm, pr, 0);
-            if (!locked)
                 {
-                    clear_tracking_vars(t);
-                    if (c.track_pilot) t.P_data_accu = make_float2(0.f, 0.f);
-                    t.state = 0;
-                    o.flags |= GSDR_TRK_F_LOSS_OF_LOCK;
-                }
-            else
-                {
-                    o.evm = locked == 2;
-                    take_dll_pll(t, sl);
+                    take_dll_pll(c, t, sl);
                     tprobe(tm, pr, 1);
                     update_tracking_vars(c, t, gc);
                     tprobe(tm, pr, 2);
@@ -1427,15 +1499,19 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
     float* s_data = s_dyn + code_pad + kCodeMargin;
     float2* s_win = reinterpret_cast<float2*>(s_dyn + code_pad + data_pad);
     char* s_sb = reinterpret_cast<char*>(s_dyn + code_pad + data_pad);  // streamed calls: two chunk buffers
-    __shared__ LoopFilter s_lfs[2];  // code loop filter: current slot and wave 1's speculative one
+    __shared__ LoopFilter s_lfs[2];  // code loop filter: current slot and wave 3's speculative one
     __shared__ int s_lfi;
     __shared__ DllPllSpec s_spec;
     __shared__ int s_spec_e;
+    __shared__ DllSpec s_dspec;
+    __shared__ int s_dspec_e;
     __shared__ float2 s_pbuf[kMaxCn0];
     __shared__ __attribute__((aligned(16))) float s_cn[3][kMaxCn0];  // cn0_and_lock's per-element terms
     __shared__ __attribute__((aligned(16))) float s_evm_buf[2 * kMaxCn0];  // evm_of's (wave 1)
     __shared__ double s_evm;
     __shared__ int s_evm_e;
+    __shared__ Cn0Spec s_cn0;  // wave 2's lock test of the call (cn0_and_lock)
+    __shared__ int s_cn0_e;
     __shared__ int s_state;
     __shared__ Prep prep;
     __shared__ float2 s_red[kTrkThreads / 64][kMaxTrkTaps + 1];
@@ -1458,7 +1534,9 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
             s_lfs[0] = gc->code_filter;
             s_lfi = 0;
             s_spec_e = -1;
+            s_dspec_e = -1;
             s_evm_e = -1;
+            s_cn0_e = -1;
             s_state = s_t.state;
             s_overrun = 0;
         }
@@ -1582,11 +1660,88 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                 }
             __syncthreads();  // partials visible; every read of the LDS window done
             if (timing && tid == 0) tm2 = wall_clock64();
+            // lane k sums tap k over the waves in wave order (one batch of LDS reads
+            // instead of a serial read per partial), then every lane takes the totals
+            // by readlane; E/P/L are the same sums
+            auto tap_totals = [&](float2 (&taps)[kMaxTrkTaps + 1], float2 (&epl)[3]) {
+                float2 mine = make_float2(0.f, 0.f);
+                if (lane <= kMaxTrkTaps)
+                    {
+                        float2 v[kTrkThreads / 64];
+#pragma unroll
+                        for (int w = 0; w < kTrkThreads / 64; ++w) v[w] = s_red[w][lane];
+#pragma unroll
+                        for (int w = 0; w < kTrkThreads / 64; ++w)
+                            {
+                                mine.x += v[w].x;
+                                mine.y += v[w].y;
+                            }
+                    }
+#pragma unroll
+                for (int k = 0; k <= kMaxTrkTaps; ++k)
+                    taps[k] = (k < K || (k == kMaxTrkTaps && data)) ? make_float2(lane_f(mine.x, k), lane_f(mine.y, k))
+                                                                   : make_float2(0.f, 0.f);
+                const int ix[3] = {c.iE, c.iP, c.iL};
+#pragma unroll
+                for (int q = 0; q < 3; ++q) epl[q] = make_float2(lane_f(mine.x, ix[q]), lane_f(mine.y, ix[q]));
+            };
+            if (wave == 3)
+                {
+                    // this call's code loop (DLL discriminator and filter) on a copy of
+                    // the state, into the code loop filter slot that is not current; wave
+                    // 1 runs the carrier loop at the same time (take_dll_pll joins them).
+                    // Before this wave's share of the window staging / prefetch, which
+                    // only has to land before the next call
+                    TrkHot t3 = s_t;
+                    if (t3.state == 2 || t3.state == 4)
+                        {
+                            float2 taps[kMaxTrkTaps + 1], epl[3];
+                            tap_totals(taps, epl);
+                            if (t3.state == 2)
+                                {
+                                    if (c.veml)
+                                        {
+                                            t3.VE_accu = taps[0];
+                                            t3.VL_accu = taps[4];
+                                        }
+                                    t3.E_accu = epl[0];
+                                    t3.P_accu = epl[1];
+                                    t3.L_accu = epl[2];
+                                    t3.spc = c.early_late_space_chips;
+                                }
+                            else
+                                save_correlation_results(c, t3, taps, epl);
+                            // the filter in registers, written to the other slot after
+                            const int cur = s_lfi;
+                            LfReg lf3 = lf_load(s_lfs[cur]);
+                            const double base = run_dll(c, t3, lf3);
+                            if (lane == 0)
+                                {
+                                    LoopFilter& d = s_lfs[cur ^ 1];
+                                    d = s_lfs[cur];
+                                    d.inputs[0] = lf3.i0;
+                                    d.inputs[1] = lf3.i1;
+                                    d.inputs[2] = lf3.i2;
+                                    d.inputs[3] = lf3.i3;
+                                    d.outputs[0] = lf3.o0;
+                                    d.outputs[1] = lf3.o1;
+                                    d.outputs[2] = lf3.o2;
+                                    d.outputs[3] = lf3.o3;
+                                    d.idx = lf3.idx;
+                                    DllSpec r;
+                                    r.code_freq_base = base;
+                                    r.log_err2 = t3.log_err[2];
+                                    r.log_err3 = t3.log_err[3];
+                                    s_dspec = r;
+                                    __hip_atomic_store(&s_dspec_e, (int)e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                                }
+                        }
+                }
             // ---- stage the window the next call most likely reads, [off + vl - kHalo/2,
-            // +kWinCore+kHalo), into LDS: waves 3.. only, while wave 0 runs the loop
-            // update, wave 1 the speculative DLL/PLL and wave 2 the EVM (every read of the
-            // current window is done), so wave 0 issues no global loads that a vmcnt wait
-            // inside its update would wait for
+            // +kWinCore+kHalo), into LDS: waves 3.. only (wave 3 after its code loop),
+            // while wave 0 runs the loop update, wave 1 the carrier loop and the EVM and
+            // wave 2 the lock test (every read of the current window is done), so wave 0
+            // issues no global loads that a vmcnt wait inside its update would wait for
             const int64_t nb = p_off + vl - kHalo / 2;
             if (use_window && wave >= 3)
                 {
@@ -1639,31 +1794,6 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                                       : 0;
                     pf_first = nb;
                 }
-            // lane k sums tap k over the waves in wave order (one batch of LDS reads
-            // instead of a serial read per partial), then every lane takes the totals
-            // by readlane; E/P/L are the same sums
-            auto tap_totals = [&](float2 (&taps)[kMaxTrkTaps + 1], float2 (&epl)[3]) {
-                float2 mine = make_float2(0.f, 0.f);
-                if (lane <= kMaxTrkTaps)
-                    {
-                        float2 v[kTrkThreads / 64];
-#pragma unroll
-                        for (int w = 0; w < kTrkThreads / 64; ++w) v[w] = s_red[w][lane];
-#pragma unroll
-                        for (int w = 0; w < kTrkThreads / 64; ++w)
-                            {
-                                mine.x += v[w].x;
-                                mine.y += v[w].y;
-                            }
-                    }
-#pragma unroll
-                for (int k = 0; k <= kMaxTrkTaps; ++k)
-                    taps[k] = (k < K || (k == kMaxTrkTaps && data)) ? make_float2(lane_f(mine.x, k), lane_f(mine.y, k))
-                                                                   : make_float2(0.f, 0.f);
-                const int ix[3] = {c.iE, c.iP, c.iL};
-#pragma unroll
-                for (int q = 0; q < 3; ++q) epl[q] = make_float2(lane_f(mine.x, ix[q]), lane_f(mine.y, ix[q]));
-            };
             if (wave == 1)
                 {
                     // this call's DLL/PLL on a copy of the state, into the code loop
@@ -1691,56 +1821,61 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                                 }
                             else
                                 save_correlation_results(c, t1, taps, epl);
-                            // the filter in registers, written to the other slot after
-                            const int cur = s_lfi;
-                            LfReg lf1 = lf_load(s_lfs[cur]);
-                            run_dll_pll(c, t1, lf1);
-                            if (lane == 0)
-                                {
-                                    LoopFilter& d = s_lfs[cur ^ 1];
-                                    d = s_lfs[cur];
-                                    d.inputs[0] = lf1.i0;
-                                    d.inputs[1] = lf1.i1;
-                                    d.inputs[2] = lf1.i2;
-                                    d.inputs[3] = lf1.i3;
-                                    d.outputs[0] = lf1.o0;
-                                    d.outputs[1] = lf1.o1;
-                                    d.outputs[2] = lf1.o2;
-                                    d.outputs[3] = lf1.o3;
-                                    d.idx = lf1.idx;
-                                }
+                            run_pll(c, t1);
                             if (lane == 0)
                                 {
                                     DllPllSpec r;
                                     r.carrier_doppler_hz = t1.carrier_doppler_hz;
-                                    r.code_freq_chips = t1.code_freq_chips;
                                     r.P_accu_old = t1.P_accu_old;
                                     r.cf_w = t1.cf_w;
                                     r.cf_x = t1.cf_x;
-                                    for (int i = 0; i < 4; ++i) r.log_err[i] = t1.log_err[i];
+                                    r.log_err[0] = t1.log_err[0];
+                                    r.log_err[1] = t1.log_err[1];
                                     s_spec = r;
                                     __hip_atomic_store(&s_spec_e, (int)e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                                }
+                            // then the EVM (an output only) with a full prompt buffer, which
+                            // wave 0 takes for the record when the call stays locked: the
+                            // buffer's other elements and this call's prompt (wave 2 writes
+                            // only this call's element)
+                            if (t1.cn0_estimation_counter >= c.cn0_samples)
+                                {
+                                    const double evm = evm_of(c, t1.cn0_estimation_counter, t1.P_accu, s_pbuf, s_evm_buf, lane);
+                                    if (lane == 0)
+                                        {
+                                            s_evm = evm;
+                                            __hip_atomic_store(&s_evm_e, (int)e, __ATOMIC_RELEASE,
+                                                __HIP_MEMORY_SCOPE_WORKGROUP);
+                                        }
                                 }
                         }
                 }
             if (wave == 2)
                 {
-                    // this call's EVM (an output only) with a full prompt buffer; wave 0
-                    // takes it for the record when the call stays locked
+                    // this call's lock test (CN0 estimate, lock detector, the prompt
+                    // buffer) on a copy of the state, which wave 0 takes after its locked
+                    // branch
                     TrkHot t2 = s_t;
-                    if ((t2.state == 2 || t2.state == 4) && t2.cn0_estimation_counter >= c.cn0_samples)
+                    if (t2.state == 2 || t2.state == 4)
                         {
                             float2 taps[kMaxTrkTaps + 1], epl[3];
                             tap_totals(taps, epl);
-                            if (t2.state == 2)
-                                t2.P_accu = epl[1];
-                            else
-                                save_correlation_results(c, t2, taps, epl);
-                            const double evm = evm_of(c, t2, s_pbuf, s_evm_buf, lane);
+                            const uint64_t n_read = t2.next_sample;
+                            if (t2.pull_in_transitory &&
+                                (n_read < c.acq_sample_stamp || n_read - c.acq_sample_stamp >= c.pull_in_span))
+                                {
+                                    t2.pull_in_transitory = 0;
+                                    t2.carrier_lock_fail_counter = 0;
+                                    t2.code_lock_fail_counter = 0;
+                                }
+                            const double coh =
+                                t2.state == 2 ? c.code_period : c.code_period * (double)c.extend_correlation_symbols;
+                            pre_lock(c, t2, taps, epl, n_read);
+                            const int locked = cn0_and_lock(c, t2, s_pbuf, s_cn, coh, lane);
                             if (lane == 0)
                                 {
-                                    s_evm = evm;
-                                    __hip_atomic_store(&s_evm_e, (int)e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                                    cn0_publish(s_cn0, t2, locked);
+                                    __hip_atomic_store(&s_cn0_e, (int)e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                                 }
                         }
                 }
@@ -1766,8 +1901,46 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                     uint64_t pr[3] = {0, 0, 0};
                     uint64_t tm3 = 0;
                     if (timing) tm3 = wall_clock64();
-                    SpecLink sl{&s_spec, &s_spec_e, s_lfs, &s_lfi, lfi0, (int)e};
-                    after_correlation(c, t, gc, sl, s_pbuf, s_cn, taps, epl, n_read, lane, o, timing != nullptr, pr);
+                    SpecLink sl{&s_spec, &s_dspec, &s_dspec_e, &s_spec_e, s_lfs, &s_lfi, lfi0, (int)e};
+                    after_correlation(c, t, gc, sl, taps, epl, n_read, o, timing != nullptr, pr);
+                    t.next_sample = n_read + (uint64_t)(int64_t)t.current_prn_length_samples;
+                    // the next call's plan from the registers (the window / chunk-0
+                    // prefetch of this iteration starts at nb), before the lock test's
+                    // results: they change it only on a loss of lock (state 0: no call)
+                    Prep pn = make_prep(c, t, e + 1 < max_epochs, iq_first, iq_items, vl, K, L, use_window, streamed,
+                        stream_chunk, use_window ? nb : win_base, streamed ? nb : pf_first);
+                    if (state0 == 2 || state0 == 4)
+                        {
+                            while (__hip_atomic_load(&s_cn0_e, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != (int)e)
+                                __builtin_amdgcn_s_sleep(1);
+                            const Cn0Spec r = s_cn0;
+                            if (r.locked)
+                                {
+                                    cn0_apply(t, r);
+                                    o.evm = r.locked == 2;
+                                }
+                            else
+                                {
+                                    // loss of lock: cn0_and_tracking_lock_status returned
+                                    // false and the reference's call ends there (:1828-1845,
+                                    // :2032-2040), so the locked branch above is void: the
+                                    // call is rebuilt from its start state
+                                    t = s_t;
+                                    if (t.pull_in_transitory &&
+                                        (n_read < c.acq_sample_stamp || n_read - c.acq_sample_stamp >= c.pull_in_span))
+                                        t.pull_in_transitory = 0;
+                                    pre_lock(c, t, taps, epl, n_read);
+                                    cn0_apply(t, r);
+                                    clear_tracking_vars(t);
+                                    if (c.track_pilot) t.P_data_accu = make_float2(0.f, 0.f);
+                                    t.state = 0;
+                                    init_out(o);
+                                    o.flags = GSDR_TRK_F_LOSS_OF_LOCK | (t.flag_pll_180 ? GSDR_TRK_F_PLL_180 : 0);
+                                    sl.lfi = lfi0;  // the DLL/PLL results were not taken
+                                    t.next_sample = n_read + (uint64_t)(int64_t)t.current_prn_length_samples;
+                                    pn.go = 0;
+                                }
+                        }
                     if (sl.lfi != lfi0)
                         {
                             lfi0 = sl.lfi;
@@ -1829,12 +2002,7 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                                     tr[10] = swait;
                                 }
                         }
-                    t.next_sample = n_read + (uint64_t)(int64_t)t.current_prn_length_samples;
                     if (lane == 0) s_t = t;
-                    // the next call's plan from the registers (the window / chunk-0
-                    // prefetch of this iteration starts at nb)
-                    const Prep pn = make_prep(c, t, e + 1 < max_epochs, iq_first, iq_items, vl, K, L, use_window, streamed,
-                        stream_chunk, use_window ? nb : win_base, streamed ? nb : pf_first);
                     if (lane == 0) prep = pn;
                     if (timing && lane == 0) timing[((size_t)ch * max_epochs + e) * kTimingSlots + 9] = wall_clock64();
                 }

@@ -354,10 +354,14 @@ def run_c5(args):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    local = rank_device(torch, local)
     torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if shared_device_rehearsal():
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     stream = not args.trk_replay
     B = args.blocks if args.blocks % 4 == 0 and args.blocks != 64 else (100 if stream else 8)
@@ -496,7 +500,7 @@ def run_c5(args):
     elapsed = time.perf_counter() - t0
     elapsed_local = elapsed
     if dist is not None:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if shared_device_rehearsal() else dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     # sanity on the timed region's outputs: acquisitions of the visible satellites,
@@ -623,6 +627,9 @@ def run_c5(args):
                             "replay mode: the same span every step, full +-4 kHz Dopplers")},
         "cpu_baseline": None,
     }
+    if shared_device_rehearsal() and world > 1:
+        line["rehearsal"] = ("%d ranks sharing %d device(s) over gloo (GSDR_BENCH_SHARED_DEVICE): the multi-rank "
+                             "path on real engines, not a scaling number" % (world, torch.cuda.device_count()))
     if rank == 0:
         print(json.dumps(line), flush=True)
     for pl in pools:
@@ -631,6 +638,20 @@ def run_c5(args):
         a.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+# GSDR_BENCH_SHARED_DEVICE=1: a multi-rank rehearsal on a box with fewer GPUs than ranks --
+# rank r uses device LOCAL_RANK % device_count() and the rank collectives run over gloo
+# (RCCL refuses two ranks on one device).  Every rank runs the real engines on its share
+# of the stream; the line is marked "rehearsal" and is never a scaling number.
+def shared_device_rehearsal():
+    return os.environ.get("GSDR_BENCH_SHARED_DEVICE", "0") == "1"
+
+
+def rank_device(torch, local):
+    if shared_device_rehearsal():
+        return local % max(1, torch.cuda.device_count())
+    return local
 
 
 class DeviceBackend:
@@ -648,11 +669,14 @@ class DeviceBackend:
         import torch
         import gsdr
         self.torch, self.gsdr = torch, gsdr
+        local = rank_device(torch, local)
         torch.cuda.set_device(local)
         self.dev = torch.device("cuda", local)
+        if shared_device_rehearsal():
+            self.dist_backend = "gloo"
 
     def dist_kwargs(self):
-        return {"device_id": self.dev}
+        return {} if self.dist_backend == "gloo" else {"device_id": self.dev}
 
     def synchronize(self):
         self.torch.cuda.synchronize(self.dev)
@@ -708,6 +732,8 @@ def main(argv=None, backend=DeviceBackend):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     be = backend(local)
     torch, gsdr, dev = be.torch, be.gsdr, be.dev
+    if getattr(dev, "type", None) == "cuda":
+        local = dev.index  # the engines' device (GSDR_BENCH_SHARED_DEVICE maps ranks onto fewer GPUs)
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -832,7 +858,7 @@ def main(argv=None, backend=DeviceBackend):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if shared_device_rehearsal() else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -1046,6 +1072,9 @@ def main(argv=None, backend=DeviceBackend):
                     "pool (every channel processes every sample)"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(iq, codes, sats)
+    if shared_device_rehearsal() and world > 1:
+        line["rehearsal"] = ("%d ranks sharing %d device(s) over gloo (GSDR_BENCH_SHARED_DEVICE): the multi-rank "
+                             "path on real engines, not a scaling number" % (world, torch.cuda.device_count()))
     if rank == 0:
         print(json.dumps(line), flush=True)
     if trk is not None:

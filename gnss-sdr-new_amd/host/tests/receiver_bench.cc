@@ -6,11 +6,15 @@
 // tracks (each answer re-arms the request, as a receiver's idle channels keep
 // searching).  The reference's shape: gnss_flowgraph.cc:1007-1135 (one tracking and
 // one acquisition block per channel over the conditioner output).
-//   receiver_bench c3|c5 [seconds] [search] [pinned] [pool batch]
+//   receiver_bench c3|c5 [seconds] [search] [pinned] [pool batch] [lookahead]
 // search 1 (default): the acquisition services search every untracked PRN of GPS
 // and Galileo and BeiDou PRNs up to 32 on every block; 0: the tracking blocks only.
 // pinned 1 (default): the host sample buffer is page-locked (gsdr_host_register), as
 // a flowgraph's buffers would be for DMA; 0: pageable (a staging copy per push).
+// lookahead L (default 0): the source runs L chunks ahead of what the blocks are offered,
+// as a flowgraph's source thread fills its output buffer ahead of the consumers; with 0
+// the blocks see every chunk the moment it is pushed, so the first block to reach it
+// waits for its DMA (the push lifetime contract: consume only landed items).
 // Every consumer reads the GPU's one shared ring (DeviceIqRing, key "rf0"): each stretch of the
 // stream crosses PCIe once.
 // C3: GPS L1 C/A at 16 Msps, 12 tracked channels; C5: one GPU's share of the 25 Msps
@@ -68,6 +72,7 @@ int main(int argc, char** argv)
     const bool search = argc > 3 ? std::atoi(argv[3]) != 0 : true;
     const bool pinned = argc > 4 ? std::atoi(argv[4]) != 0 : true;
     const int pool_batch = argc > 5 ? std::atoi(argv[5]) : 0;  // 0: the blocks' default
+    const int lookahead = argc > 6 ? std::max(0, std::atoi(argv[6])) : 0;
     std::vector<Sig> sigs = {{"1C", "GPS_L1_CA_DLL_PLL_Tracking_MI355X", "GPS_L1_CA_PCPS_Acquisition_MI355X", 'G', '1',
         'C', 12, 32, 1.023e6, 1575.42e6, 1}};
     if (c5)
@@ -273,6 +278,7 @@ int main(int argc, char** argv)
     while (progress)
         {
             progress = false;
+            size_t visible = pushed;
             if (pushed < n)
                 {
                     const size_t m = std::min(chunk, n - pushed);
@@ -281,8 +287,11 @@ int main(int argc, char** argv)
                     const auto b = clk::now();
                     pushed += m;
                     progress = true;
+                    // the items the blocks are offered: all but the source's lookahead
+                    const size_t look = static_cast<size_t>(lookahead) * chunk;
+                    visible = pushed == n ? n : (pushed > look ? pushed - look : 0);
                     for (auto& s : svcs)
-                        if (s) s->work_ring(ring, pushed);
+                        if (s) s->work_ring(ring, visible);
                     t_feed += std::chrono::duration<double>(b - a).count();
                     t_svc += std::chrono::duration<double>(clk::now() - b).count();
                 }
@@ -291,9 +300,9 @@ int main(int argc, char** argv)
             for (auto& ch : chans)
                 for (;;)
                     {
-                        if (ch.nread >= pushed) break;
+                        if (ch.nread >= visible) break;
                         const int fc = ch.blk->forecast();
-                        const uint64_t avail = pushed - ch.nread;
+                        const uint64_t avail = visible - ch.nread;
                         if (avail < static_cast<uint64_t>(fc)) break;  // GNU Radio's forecast: wait for more items
                         const int give = static_cast<int>(std::min<uint64_t>(std::max<uint64_t>(chunk, fc), avail));
                         Gnss_Synchro out{};
@@ -356,10 +365,10 @@ int main(int argc, char** argv)
     std::printf("{\"config\": \"%s\", \"search\": %d, \"path\": \"factory-built pooled TrackingInterface blocks (work() per block at its "
                 "nitems_read, batched advances) + AcquisitionService grids on the device IQ ring (batched, asynchronous), host "
                 "pushes of %zu-item chunks\", "
-                "\"host_buffer\": \"%s\", \"pool_batch\": %d, \"fs_sps\": %.0f, \"samples\": %zu, \"seconds\": %.4f, \"msps\": %.2f, \"real_time_factor\": %.2f, "
+                "\"host_buffer\": \"%s\", \"pool_batch\": %d, \"source_lookahead_chunks\": %d, \"fs_sps\": %.0f, \"samples\": %zu, \"seconds\": %.4f, \"msps\": %.2f, \"real_time_factor\": %.2f, "
                 "\"tracking_channels\": %zu, \"trk_work_calls\": %llu, \"host_seconds\": {\"feed_and_pool_advances\": %.4f, "
                 "\"acquisition_services\": %.4f, \"tracking_work_calls\": %.4f, \"flush\": %.4f}, \"signals\": {%s}}\n",
-        cfg.c_str(), search ? 1 : 0, chunk, pinned ? "pinned" : "pageable", pool_batch, fs, n, sec, n / sec / 1e6, n / sec / fs, chans.size(),
+        cfg.c_str(), search ? 1 : 0, chunk, pinned ? "pinned" : "pageable", pool_batch, lookahead, fs, n, sec, n / sec / 1e6, n / sec / fs, chans.size(),
         static_cast<unsigned long long>(trk_calls), t_feed, t_svc, t_work, t_flush, per_sig.c_str());
     chans.clear();
     svcs.clear();

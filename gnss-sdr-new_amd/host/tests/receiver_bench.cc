@@ -6,7 +6,7 @@
 // tracks (each answer re-arms the request, as a receiver's idle channels keep
 // searching).  The reference's shape: gnss_flowgraph.cc:1007-1135 (one tracking and
 // one acquisition block per channel over the conditioner output).
-//   receiver_bench c3|c5 [seconds] [search] [pinned] [pool batch] [lookahead]
+//   receiver_bench c3|c5 [seconds] [search] [pinned] [pool batch] [lookahead] [threads]
 // search 1 (default): the acquisition services search every untracked PRN of GPS
 // and Galileo and BeiDou PRNs up to 32 on every block; 0: the tracking blocks only.
 // pinned 1 (default): the host sample buffer is page-locked (gsdr_host_register), as
@@ -15,12 +15,19 @@
 // as a flowgraph's source thread fills its output buffer ahead of the consumers; with 0
 // the blocks see every chunk the moment it is pushed, so the first block to reach it
 // waits for its DMA (the push lifetime contract: consume only landed items).
+// threads T (default 0): the tracking blocks' work() calls run on T threads (block i on
+// thread i % T) beside the source thread that pushes and runs the acquisition services,
+// as GNU Radio's thread-per-block scheduler runs them concurrently; the source keeps
+// within 4 chunks of the slowest block (a bounded upstream buffer).  0: one thread,
+// every block's work() after each push.
 // Every consumer reads the GPU's one shared ring (DeviceIqRing, key "rf0"): each stretch of the
 // stream crosses PCIe once.
 // C3: GPS L1 C/A at 16 Msps, 12 tracked channels; C5: one GPU's share of the 25 Msps
 // hybrid job, 12 GPS L1 C/A + 12 Galileo E1 (pilot) + 8 BeiDou B1I channels.
 // Prints one JSON line: stream Msps through the whole receiver path (host loop,
 // pushes, launches, records) and per-signal outputs / Doppler errors.
+#include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <complex>
@@ -28,6 +35,7 @@
 #include <cstring>
 #include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "acquisition_service.h"
@@ -73,6 +81,7 @@ int main(int argc, char** argv)
     const bool pinned = argc > 4 ? std::atoi(argv[4]) != 0 : true;
     const int pool_batch = argc > 5 ? std::atoi(argv[5]) : 0;  // 0: the blocks' default
     const int lookahead = argc > 6 ? std::max(0, std::atoi(argv[6])) : 0;
+    const int threads = argc > 7 ? std::max(0, std::atoi(argv[7])) : 0;
     std::vector<Sig> sigs = {{"1C", "GPS_L1_CA_DLL_PLL_Tracking_MI355X", "GPS_L1_CA_PCPS_Acquisition_MI355X", 'G', '1',
         'C', 12, 32, 1.023e6, 1575.42e6, 1}};
     if (c5)
@@ -275,6 +284,95 @@ int main(int argc, char** argv)
     // make), the acquisition services, the tracking blocks' work() calls
     using clk = std::chrono::steady_clock;
     double t_feed = 0, t_svc = 0, t_work = 0;
+    if (threads > 0)
+        {
+            // the blocks on T threads; the source (this thread) pushes, runs the services
+            // and keeps within `lag` items of the slowest block
+            const size_t look = static_cast<size_t>(lookahead) * chunk;
+            const size_t lag = 4 * chunk + look;
+            std::atomic<size_t> vis_a{0};
+            std::atomic<bool> fed_all{false};
+            std::unique_ptr<std::atomic<uint64_t>[]> nread_a(new std::atomic<uint64_t>[chans.size()]);
+            for (size_t i = 0; i < chans.size(); ++i) nread_a[i].store(0);
+            std::atomic<uint64_t> calls_a{0};
+            auto worker = [&](int t) {
+                uint64_t my_calls = 0;
+                for (;;)
+                    {
+                        const bool fin = fed_all.load(std::memory_order_acquire);
+                        const size_t vis = vis_a.load(std::memory_order_acquire);
+                        bool prog = false;
+                        for (size_t i = static_cast<size_t>(t); i < chans.size(); i += static_cast<size_t>(threads))
+                            {
+                                Ch& ch = chans[i];
+                                for (;;)
+                                    {
+                                        if (ch.nread >= vis) break;
+                                        const int fc = ch.blk->forecast();
+                                        const uint64_t avail = vis - ch.nread;
+                                        if (avail < static_cast<uint64_t>(fc)) break;
+                                        const int give =
+                                            static_cast<int>(std::min<uint64_t>(std::max<uint64_t>(chunk, fc), avail));
+                                        Gnss_Synchro out{};
+                                        int nout = 0;
+                                        const int used = ch.blk->work(x.data() + ch.nread, give, ch.nread, &out, &nout);
+                                        if (nout == 1 && out.Flag_valid_symbol_output) ++ch.outputs;
+                                        if (used <= 0 && nout == 0) break;
+                                        prog = true;
+                                        ch.nread += static_cast<uint64_t>(std::max(used, 0));
+                                        ++my_calls;
+                                    }
+                                nread_a[i].store(ch.nread, std::memory_order_release);
+                            }
+                        if (!prog)
+                            {
+                                if (fin && vis == n) break;
+                                std::this_thread::yield();
+                            }
+                    }
+                calls_a += my_calls;
+            };
+            const auto w0 = clk::now();
+            std::vector<std::thread> pool;
+            for (int t = 0; t < threads; ++t) pool.emplace_back(worker, t);
+            uint64_t stalls = 0;
+            while (pushed < n)
+                {
+                    // a bounded upstream buffer: wait (at most ~50 ms, for a block that
+                    // stopped consuming) until the slowest block is within `lag` of the head
+                    const auto s0 = clk::now();
+                    for (;;)
+                        {
+                            uint64_t slowest = UINT64_MAX;
+                            for (size_t i = 0; i < chans.size(); ++i)
+                                slowest = std::min<uint64_t>(slowest, nread_a[i].load(std::memory_order_acquire));
+                            if (slowest + lag >= pushed) break;
+                            if (std::chrono::duration<double>(clk::now() - s0).count() > 0.05)
+                                {
+                                    ++stalls;
+                                    break;
+                                }
+                            std::this_thread::yield();
+                        }
+                    const size_t m = std::min(chunk, n - pushed);
+                    const auto a = clk::now();
+                    hub->feed(x.data() + pushed, pushed, static_cast<int>(m));
+                    const auto b = clk::now();
+                    pushed += m;
+                    const size_t visible = pushed == n ? n : (pushed > look ? pushed - look : 0);
+                    vis_a.store(visible, std::memory_order_release);
+                    for (auto& s : svcs)
+                        if (s) s->work_ring(ring, visible);
+                    t_feed += std::chrono::duration<double>(b - a).count();
+                    t_svc += std::chrono::duration<double>(clk::now() - b).count();
+                }
+            fed_all.store(true, std::memory_order_release);
+            for (auto& th : pool) th.join();
+            trk_calls = calls_a.load();
+            t_work = std::chrono::duration<double>(clk::now() - w0).count();  // the threads' wall
+            if (stalls) std::fprintf(stderr, "receiver_bench: %llu source stalls past 50 ms\n", (unsigned long long)stalls);
+            progress = false;
+        }
     while (progress)
         {
             progress = false;
@@ -365,10 +463,10 @@ int main(int argc, char** argv)
     std::printf("{\"config\": \"%s\", \"search\": %d, \"path\": \"factory-built pooled TrackingInterface blocks (work() per block at its "
                 "nitems_read, batched advances) + AcquisitionService grids on the device IQ ring (batched, asynchronous), host "
                 "pushes of %zu-item chunks\", "
-                "\"host_buffer\": \"%s\", \"pool_batch\": %d, \"source_lookahead_chunks\": %d, \"fs_sps\": %.0f, \"samples\": %zu, \"seconds\": %.4f, \"msps\": %.2f, \"real_time_factor\": %.2f, "
+                "\"host_buffer\": \"%s\", \"pool_batch\": %d, \"source_lookahead_chunks\": %d, \"block_threads\": %d, \"fs_sps\": %.0f, \"samples\": %zu, \"seconds\": %.4f, \"msps\": %.2f, \"real_time_factor\": %.2f, "
                 "\"tracking_channels\": %zu, \"trk_work_calls\": %llu, \"host_seconds\": {\"feed_and_pool_advances\": %.4f, "
                 "\"acquisition_services\": %.4f, \"tracking_work_calls\": %.4f, \"flush\": %.4f}, \"signals\": {%s}}\n",
-        cfg.c_str(), search ? 1 : 0, chunk, pinned ? "pinned" : "pageable", pool_batch, lookahead, fs, n, sec, n / sec / 1e6, n / sec / fs, chans.size(),
+        cfg.c_str(), search ? 1 : 0, chunk, pinned ? "pinned" : "pageable", pool_batch, lookahead, threads, fs, n, sec, n / sec / 1e6, n / sec / fs, chans.size(),
         static_cast<unsigned long long>(trk_calls), t_feed, t_svc, t_work, t_flush, per_sig.c_str());
     chans.clear();
     svcs.clear();

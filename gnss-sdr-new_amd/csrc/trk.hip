@@ -283,6 +283,17 @@ struct TrkChan
     double hist_carr[2 * kMaxSmoother], hist_code[2 * kMaxSmoother], hist_samples[2 * kMaxSmoother];
 };
 
+// The loop state make_prep reads (wave 0 -> wave 1 after the locked branch): wave 1 plans
+// the next call while wave 0 takes the lock test and writes the record
+struct PlanIn
+{
+    double carrier_phase_step_rad, carrier_phase_rate_step_rad, rem_code_phase_chips, code_phase_step_chips,
+        code_phase_rate_step_chips;
+    uint64_t next_sample;
+    float rem_carr_phase_rad;
+    int32_t state, narrow;
+};
+
 struct Prep  // lane-0 -> workgroup broadcast of one call's NCO
 {
     double psi0, theta;
@@ -1512,6 +1523,8 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
     __shared__ int s_evm_e;
     __shared__ Cn0Spec s_cn0;  // wave 2's lock test of the call (cn0_and_lock)
     __shared__ int s_cn0_e;
+    __shared__ PlanIn s_plan;  // wave 0's loop state for wave 1's next-call plan
+    __shared__ int s_plan_e, s_prep_e;
     __shared__ int s_state;
     __shared__ Prep prep;
     __shared__ float2 s_red[kTrkThreads / 64][kMaxTrkTaps + 1];
@@ -1537,6 +1550,8 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
             s_dspec_e = -1;
             s_evm_e = -1;
             s_cn0_e = -1;
+            s_plan_e = -1;
+            s_prep_e = -1;
             s_state = s_t.state;
             s_overrun = 0;
         }
@@ -1848,6 +1863,27 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
                                         }
                                 }
+                            // then the next call's plan from wave 0's state after its
+                            // locked branch (wave 0 overrides it on a loss of lock)
+                            while (__hip_atomic_load(&s_plan_e, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != (int)e)
+                                __builtin_amdgcn_s_sleep(1);
+                            const PlanIn q = s_plan;
+                            t1.carrier_phase_step_rad = q.carrier_phase_step_rad;
+                            t1.carrier_phase_rate_step_rad = q.carrier_phase_rate_step_rad;
+                            t1.rem_code_phase_chips = q.rem_code_phase_chips;
+                            t1.code_phase_step_chips = q.code_phase_step_chips;
+                            t1.code_phase_rate_step_chips = q.code_phase_rate_step_chips;
+                            t1.next_sample = q.next_sample;
+                            t1.rem_carr_phase_rad = q.rem_carr_phase_rad;
+                            t1.state = q.state;
+                            t1.narrow = q.narrow;
+                            const Prep pn = make_prep(c, t1, e + 1 < max_epochs, iq_first, iq_items, vl, K, L, use_window,
+                                streamed, stream_chunk, use_window ? nb : win_base, streamed ? nb : pf_first);
+                            if (lane == 0)
+                                {
+                                    prep = pn;
+                                    __hip_atomic_store(&s_prep_e, (int)e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                                }
                         }
                 }
             if (wave == 2)
@@ -1904,11 +1940,34 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                     SpecLink sl{&s_spec, &s_dspec, &s_dspec_e, &s_spec_e, s_lfs, &s_lfi, lfi0, (int)e};
                     after_correlation(c, t, gc, sl, taps, epl, n_read, o, timing != nullptr, pr);
                     t.next_sample = n_read + (uint64_t)(int64_t)t.current_prn_length_samples;
-                    // the next call's plan from the registers (the window / chunk-0
-                    // prefetch of this iteration starts at nb), before the lock test's
-                    // results: they change it only on a loss of lock (state 0: no call)
-                    Prep pn = make_prep(c, t, e + 1 < max_epochs, iq_first, iq_items, vl, K, L, use_window, streamed,
-                        stream_chunk, use_window ? nb : win_base, streamed ? nb : pf_first);
+                    // the next call's plan (the window / chunk-0 prefetch of this iteration
+                    // starts at nb): states 2 / 4 on wave 1 from the state published here,
+                    // before the lock test's results (they change the plan only on a loss
+                    // of lock: state 0, no call); state 3 here
+                    const bool plan_w1 = state0 == 2 || state0 == 4;
+                    Prep pn{};
+                    if (plan_w1)
+                        {
+                            if (lane == 0)
+                                {
+                                    PlanIn q;
+                                    q.carrier_phase_step_rad = t.carrier_phase_step_rad;
+                                    q.carrier_phase_rate_step_rad = t.carrier_phase_rate_step_rad;
+                                    q.rem_code_phase_chips = t.rem_code_phase_chips;
+                                    q.code_phase_step_chips = t.code_phase_step_chips;
+                                    q.code_phase_rate_step_chips = t.code_phase_rate_step_chips;
+                                    q.next_sample = t.next_sample;
+                                    q.rem_carr_phase_rad = t.rem_carr_phase_rad;
+                                    q.state = t.state;
+                                    q.narrow = t.narrow;
+                                    s_plan = q;
+                                    __hip_atomic_store(&s_plan_e, (int)e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                                }
+                        }
+                    else
+                        pn = make_prep(c, t, e + 1 < max_epochs, iq_first, iq_items, vl, K, L, use_window, streamed,
+                            stream_chunk, use_window ? nb : win_base, streamed ? nb : pf_first);
+                    bool lost = false;
                     if (state0 == 2 || state0 == 4)
                         {
                             while (__hip_atomic_load(&s_cn0_e, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != (int)e)
@@ -1938,7 +1997,7 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                                     o.flags = GSDR_TRK_F_LOSS_OF_LOCK | (t.flag_pll_180 ? GSDR_TRK_F_PLL_180 : 0);
                                     sl.lfi = lfi0;  // the DLL/PLL results were not taken
                                     t.next_sample = n_read + (uint64_t)(int64_t)t.current_prn_length_samples;
-                                    pn.go = 0;
+                                    lost = true;
                                 }
                         }
                     if (sl.lfi != lfi0)
@@ -2003,7 +2062,17 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                                 }
                         }
                     if (lane == 0) s_t = t;
-                    if (lane == 0) prep = pn;
+                    if (!plan_w1)
+                        {
+                            if (lane == 0) prep = pn;
+                        }
+                    else if (lost)
+                        {
+                            // no next call: after wave 1's plan, so this write lands last
+                            while (__hip_atomic_load(&s_prep_e, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != (int)e)
+                                __builtin_amdgcn_s_sleep(1);
+                            if (lane == 0) prep.go = 0;
+                        }
                     if (timing && lane == 0) timing[((size_t)ch * max_epochs + e) * kTimingSlots + 9] = wall_clock64();
                 }
             if (use_window) win_base = nb;

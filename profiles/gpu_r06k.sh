@@ -13,7 +13,7 @@ timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method threa
 rc=$?; tail -3 $OUT/pytest_trk.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 200 ./gnss-sdr-new_amd/build/host_selftest tests/golden/GPS_L1_CA_ID_1_Fs_4Msps_2ms.dat tests/golden/Galileo_E1_ID_1_Fs_4Msps_8ms.dat > $OUT/host_selftest.log 2>&1
 rc=$?; tail -3 $OUT/host_selftest.log; [ $rc -eq 0 ] || exit $rc
-for rep in 1 2; do for L in base split head; do
+for rep in 1 2; do for L in head0 head; do
   E=""; [ $L = head ] || E="GSDR_LIB=gnss-sdr-new_amd/build_ab/$L/libgsdr.so"
   echo "== $L timing"
   env $E GSDR_TRK_TIMING=2 timeout -k 10 200 python bench.py --only trk --no-cpu-baseline --steps 20 --warmup 5 > $OUT/trk_${L}_$rep.json 2> $OUT/trk_${L}_$rep.err || exit 1

@@ -61,7 +61,9 @@ constexpr int kWinCore = kSpl * kTrkThreads;  // 4096: the next call's window st
 constexpr int kHalo = 16;                     // slack around the predicted next start
 constexpr int kStreamRow = 64 * 16;           // bytes one wave's global_load_lds_dwordx4 writes
 constexpr int kCodeMargin = 32;              // replica samples copied on each side of the LDS replica
-constexpr int kTimingSlots = 11;             // GSDR_TRK_TIMING record per call: 10 stamps + stream-wait ticks
+constexpr int kTimingSlots = 14;             // GSDR_TRK_TIMING record per call: 10 stamps + stream-wait ticks
+                                             // + wave 2's lock test start / end and wave 0's
+                                             // arrival at the join, as offsets from the partials barrier
 constexpr int kStampSlots = 10;
 
 // MATH_CONSTANTS.h:47-50
@@ -1524,6 +1526,7 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
     __shared__ Cn0Spec s_cn0;  // wave 2's lock test of the call (cn0_and_lock)
     __shared__ int s_cn0_e;
     __shared__ PlanIn s_plan;  // wave 0's loop state for wave 1's next-call plan
+    __shared__ uint64_t s_w2t[2];  // GSDR_TRK_TIMING: wave 2's lock test start / end
     __shared__ int s_plan_e, s_prep_e;
     __shared__ int s_state;
     __shared__ Prep prep;
@@ -1565,6 +1568,9 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
     const int K = c.n_taps;
     const int L = c.code_samples;
     const int vl = c.vector_length;
+    // calls of at most kWinCore samples: the next call's window staged by waves 3.. through
+    // registers (the streamed path's LDS-DMA prefetch for them measured 181 -> 213 ticks of
+    // correlation per C2 call, profiles/r06r)
     const bool use_window = vl <= kWinCore;
     const bool streamed = !use_window && stream_chunk > 0;
     const bool data = c.track_pilot != 0;
@@ -1907,9 +1913,11 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                             const double coh =
                                 t2.state == 2 ? c.code_period : c.code_period * (double)c.extend_correlation_symbols;
                             pre_lock(c, t2, taps, epl, n_read);
+                            if (timing && lane == 0) s_w2t[0] = wall_clock64();
                             const int locked = cn0_and_lock(c, t2, s_pbuf, s_cn, coh, lane);
                             if (lane == 0)
                                 {
+                                    if (timing) s_w2t[1] = wall_clock64();
                                     cn0_publish(s_cn0, t2, locked);
                                     __hip_atomic_store(&s_cn0_e, (int)e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                                 }
@@ -1968,8 +1976,10 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                         pn = make_prep(c, t, e + 1 < max_epochs, iq_first, iq_items, vl, K, L, use_window, streamed,
                             stream_chunk, use_window ? nb : win_base, streamed ? nb : pf_first);
                     bool lost = false;
+                    uint64_t tjoin = 0;
                     if (state0 == 2 || state0 == 4)
                         {
+                            if (timing) tjoin = wall_clock64();
                             while (__hip_atomic_load(&s_cn0_e, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != (int)e)
                                 __builtin_amdgcn_s_sleep(1);
                             const Cn0Spec r = s_cn0;
@@ -2059,6 +2069,10 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                                     tr[7] = pr[2] ? pr[2] : tr[6];
                                     tr[8] = wall_clock64();
                                     tr[10] = swait;
+                                    const bool w2 = tjoin != 0;
+                                    tr[11] = w2 && s_w2t[0] >= tm2 ? s_w2t[0] - tm2 : 0;
+                                    tr[12] = w2 && s_w2t[1] >= tm2 ? s_w2t[1] - tm2 : 0;
+                                    tr[13] = w2 && tjoin >= tm2 ? tjoin - tm2 : 0;
                                 }
                         }
                     if (lane == 0) s_t = t;
@@ -2597,14 +2611,15 @@ void gsdr_trk_destroy(gsdr_trk* k)
                                     const uint64_t next0 = tm[((size_t)c * me + e + 1) * kTimingSlots];
                                     if (next0 >= r[kStampSlots - 1]) k->tsum[kStampSlots - 1] += (double)(next0 - r[kStampSlots - 1]);
                                 }
-                            k->tsum[kStampSlots] += (double)r[kStampSlots];  // stream-wait: a duration
+                            for (int q = kStampSlots; q < kTimingSlots; ++q) k->tsum[q] += (double)r[q];  // durations / offsets
                             k->tcount++;
                         }
         }
     if (k->timing_on && k->tcount)
         {
             static const char* names[kTimingSlots] = {"prep", "correlate", "state-load", "tap-sum", "cn0-lock", "dll-pll",
-                "update-vars", "rest", "next-plan", "loop-top", "(correlate's stream-wait)"};
+                "update-vars", "rest", "next-plan", "loop-top", "(correlate's stream-wait)", "(w2 lock-test start)",
+                "(w2 lock-test end)", "(w0 at the lock join)"};
             std::fprintf(stderr, "gsdr_trk timing: %llu calls, %s ticks per call:", (unsigned long long)k->tcount,
                 "wall_clock64 (100 MHz)");
             for (int q = 0; q < kTimingSlots; ++q) std::fprintf(stderr, " %s %.0f", names[q], k->tsum[q] / k->tcount);

@@ -791,7 +791,7 @@ __device__ __forceinline__ void tprobe(bool on, uint64_t (&pr)[3], int i)
 // the state; wave 0 takes the results when the call stays locked (and drops them on a
 // loss of lock).  Same operations on the same values: the loop is bit-identical to
 // run_dll_pll on one wave (round 6: C2 call 6.2 -> 5.6 us, C5 GPS 10.8 -> 10.1 us,
-// profiles/r06k3).
+// profiles/r06k3; with the next call's plan on wave 1 C5 GPS 9.9 us, profiles/r06p).
 struct DllPllSpec  // wave 1's carrier loop of a call
 {
     double carrier_doppler_hz;

@@ -61,9 +61,10 @@ constexpr int kWinCore = kSpl * kTrkThreads;  // 4096: the next call's window st
 constexpr int kHalo = 16;                     // slack around the predicted next start
 constexpr int kStreamRow = 64 * 16;           // bytes one wave's global_load_lds_dwordx4 writes
 constexpr int kCodeMargin = 32;              // replica samples copied on each side of the LDS replica
-constexpr int kTimingSlots = 14;             // GSDR_TRK_TIMING record per call: 10 stamps + stream-wait ticks
+constexpr int kTimingSlots = 17;             // GSDR_TRK_TIMING record per call: 10 stamps + stream-wait ticks
                                              // + wave 2's lock test start / end and wave 0's
-                                             // arrival at the join, as offsets from the partials barrier
+                                             // arrival at the join, wave 1's EVM end, wave 0 at the EVM
+                                             // join and after it, as offsets from the partials barrier
 constexpr int kStampSlots = 10;
 
 // MATH_CONSTANTS.h:47-50
@@ -1526,7 +1527,7 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
     __shared__ Cn0Spec s_cn0;  // wave 2's lock test of the call (cn0_and_lock)
     __shared__ int s_cn0_e;
     __shared__ PlanIn s_plan;  // wave 0's loop state for wave 1's next-call plan
-    __shared__ uint64_t s_w2t[2];  // GSDR_TRK_TIMING: wave 2's lock test start / end
+    __shared__ uint64_t s_w2t[3];  // GSDR_TRK_TIMING: wave 2's lock test start / end, wave 1's EVM end
     __shared__ int s_plan_e, s_prep_e;
     __shared__ int s_state;
     __shared__ Prep prep;
@@ -1864,6 +1865,7 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                                     const double evm = evm_of(c, t1.cn0_estimation_counter, t1.P_accu, s_pbuf, s_evm_buf, lane);
                                     if (lane == 0)
                                         {
+                                            if (timing) s_w2t[2] = wall_clock64();
                                             s_evm = evm;
                                             __hip_atomic_store(&s_evm_e, (int)e, __ATOMIC_RELEASE,
                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -2015,11 +2017,14 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                             lfi0 = sl.lfi;
                             if (lane == 0) s_lfi = lfi0;
                         }
+                    uint64_t tevm0 = 0, tevm1 = 0;
                     if (o.evm)
                         {
+                            if (timing) tevm0 = wall_clock64();
                             while (__hip_atomic_load(&s_evm_e, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != (int)e)
                                 __builtin_amdgcn_s_sleep(1);
                             t.evm = s_evm;
+                            if (timing) tevm1 = wall_clock64();
                         }
                     if (lane == 0)
                         {
@@ -2073,6 +2078,9 @@ __global__ void __launch_bounds__(kTrkThreads) trk_kernel(const TrkConst* __rest
                                     tr[11] = w2 && s_w2t[0] >= tm2 ? s_w2t[0] - tm2 : 0;
                                     tr[12] = w2 && s_w2t[1] >= tm2 ? s_w2t[1] - tm2 : 0;
                                     tr[13] = w2 && tjoin >= tm2 ? tjoin - tm2 : 0;
+                                    tr[14] = tevm0 && s_w2t[2] >= tm2 ? s_w2t[2] - tm2 : 0;
+                                    tr[15] = tevm0 >= tm2 && tevm0 ? tevm0 - tm2 : 0;
+                                    tr[16] = tevm1 >= tm2 && tevm1 ? tevm1 - tm2 : 0;
                                 }
                         }
                     if (lane == 0) s_t = t;
@@ -2619,7 +2627,8 @@ void gsdr_trk_destroy(gsdr_trk* k)
         {
             static const char* names[kTimingSlots] = {"prep", "correlate", "state-load", "tap-sum", "cn0-lock", "dll-pll",
                 "update-vars", "rest", "next-plan", "loop-top", "(correlate's stream-wait)", "(w2 lock-test start)",
-                "(w2 lock-test end)", "(w0 at the lock join)"};
+                "(w2 lock-test end)", "(w0 at the lock join)", "(w1 EVM end)", "(w0 at the EVM join)",
+                "(w0 past the EVM join)"};
             std::fprintf(stderr, "gsdr_trk timing: %llu calls, %s ticks per call:", (unsigned long long)k->tcount,
                 "wall_clock64 (100 MHz)");
             for (int q = 0; q < kTimingSlots; ++q) std::fprintf(stderr, " %s %.0f", names[q], k->tsum[q] / k->tcount);

@@ -362,3 +362,48 @@ def test_bench_main_two_rank_gloo_control_flow():
         assert all(c % 2 == r for c in mine) and len(mine) == bench.CHANNELS // 2
         # one tracking launch for the warmup, one for the timed steps, one for the tracking-only rate
         assert [e for e in log if e[0] == "trk"] == [("trk", 1 * total), ("trk", 3 * total), ("trk", 3 * total)]
+
+
+def test_bench_acq_stagger_tiles_each_step(monkeypatch):
+    """`bench.py --acq-stagger S` (round 6): the two chains take B/2 + S and B/2 - S blocks
+    on alternate steps, and every step's two launches still tile the step's B blocks."""
+    import contextlib
+    import io
+    import json
+    import bench
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        monkeypatch.delenv(k, raising=False)
+    log = []
+
+    class CpuBackend:
+        dist_backend = "gloo"
+
+        def __init__(self, local):
+            self.torch, self.dev = torch, torch.device("cpu")
+            self.gsdr = _StubEngine(log, 0)
+
+        def dist_kwargs(self):
+            return {}
+
+        def synchronize(self):
+            pass
+
+        def event(self):
+            raise AssertionError("no profile events here")
+
+    out = io.StringIO()
+    with contextlib.redirect_stdout(out):
+        bench.main(["--steps", "3", "--warmup", "1", "--no-profile-events", "--no-cpu-baseline", "--acq-stagger", "8"],
+                   backend=CpuBackend)
+    line = json.loads(out.getvalue().strip().splitlines()[-1])
+    B = line["config"]["blocks_per_step"]
+    assert line["config"]["acq_stagger"] == 8
+    acq = [e for e in log if e[0] == "acq"]
+    assert len(acq) == 2 * 7  # (1 warmup + 3 timed + 3 acquisition-only) steps x two chains
+    for s in range(7):
+        a, b = acq[2 * s], acq[2 * s + 1]
+        step = s if s < 4 else s - 4  # the acquisition-only rate restarts at step 0
+        first = B // 2 + 8 if step % 2 == 0 else B // 2 - 8
+        assert (a[2], b[2]) == (first, B - first)
+        span = (s if s < 4 else s - 4) * B
+        assert a[1] - span == 0 and b[1] - span == a[2]

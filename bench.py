@@ -482,6 +482,8 @@ def run_c5(args):
         acq_step(step_no[0] % (W + K + 1) if stream else 0)
         step_no[0] += 1
 
+    prewarm_passes = clock_warmup(lambda k: acq_step(k % (W + K + 1) if stream else 0), args.min_warmup_ms,
+                                  lambda: torch.cuda.synchronize(dev))
     if stream:
         trk_launch(W)
     for _ in range(W):
@@ -626,6 +628,8 @@ def run_c5(args):
                             "convergence is not comparable with full-Doppler runs" if stream else
                             "replay mode: the same span every step, full +-4 kHz Dopplers")},
         "cpu_baseline": None,
+        "prewarm": {"min_ms": args.min_warmup_ms, "acq_passes": prewarm_passes,
+                    "note": "untimed acquisition passes before the W warmup steps (GPU clock ramp)"},
     }
     if shared_device_rehearsal() and world > 1:
         line["rehearsal"] = ("%d ranks sharing %d device(s) over gloo (GSDR_BENCH_SHARED_DEVICE): the multi-rank "
@@ -638,6 +642,31 @@ def run_c5(args):
         a.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def clock_warmup(acq_pass, ms, sync):
+    """Untimed acquisition passes for at least `ms` ms, issued back to back before the W
+    warmup steps: the MI355X ramps its clocks under sustained load and drops them in idle
+    gaps, so with the driver's 5 warmup steps (6 ms at C2) the timed steps ran on a chip
+    still ramping -- the same correlate kernel 1081-1084 us per launch after 5 warmup
+    steps against 974-984 us after 200 (profiles/r06v).  The timed region is unchanged:
+    exactly K full steps between the barriers.  Returns the passes run."""
+    if ms <= 0:
+        return 0
+    # a short synchronised burst sizes one pass, then the rest go back to back with no
+    # host synchronisation (an idle gap between passes lets the clocks drop again)
+    t = time.perf_counter()
+    n = 0
+    for _ in range(4):
+        acq_pass(n)
+        n += 1
+    sync()
+    per = max((time.perf_counter() - t) / 4, 1e-5)
+    rest = int(min(max(ms / 1e3 - 4 * per, 0.0) / per, 100000))
+    for _ in range(rest):
+        acq_pass(n)
+        n += 1
+    return n
 
 
 # GSDR_BENCH_SHARED_DEVICE=1: a multi-rank rehearsal on a box with fewer GPUs than ranks --
@@ -705,6 +734,9 @@ def main(argv=None, backend=DeviceBackend):
                     help="comma list of the chains' block counts (sum = --blocks), overriding --acq-chains: unequal "
                          "chains drift out of step, so one chain's forward / reduce / argmax launches overlap the "
                          "other's correlate instead of coinciding with it")
+    ap.add_argument("--min-warmup-ms", type=float, default=250.0,
+                    help="before the W warmup steps, untimed acquisition passes for at least this long (GPU clock "
+                         "ramp; 0: none) -- the timed region is still exactly K steps")
     ap.add_argument("--acq-stagger", type=int, default=0,
                     help="two chains: move this many blocks from one chain to the other on alternate steps "
                          "(sizes B/2 + s, B/2 - s, then B/2 - s, B/2 + s), so the chains' forward / reduce / argmax "
@@ -808,24 +840,29 @@ def main(argv=None, backend=DeviceBackend):
 
     step_no = [0]
 
+    def acq_pass(k):
+        # with the continuous stream each step acquires its own span of it (new HBM
+        # addresses every step, as a receiver's ingest would be; not the same 2 MB
+        # re-read from L2 / MALL)
+        span = k % (W + K + 1) if args.trk_stream else 0
+        src = iq_long if args.trk_stream else iq_dev
+        sz = step_sizes[k % 2]
+        off = 0
+        for i, a in enumerate(acqs):
+            b0 = lo + off
+            a.run_device(src.data_ptr() + (span * total + b0) * N * 8, sz[i], N, (span * total + b0) * N,
+                         res_dev.data_ptr() + off * P * gsdr.ACQ_RESULT_DTYPE.itemsize)
+            off += sz[i]
+
     def step():
         if do_trk and not args.trk_stream:
             trk.restore_state(0)
             trk.run_device(iq_dev.data_ptr(), 0, total * N, total, trk_out.data_ptr(), trk_n.data_ptr())
         if args.only != "trk":
-            # with the continuous stream each step acquires its own span of it (new HBM
-            # addresses every step, as a receiver's ingest would be; not the same 2 MB
-            # re-read from L2 / MALL)
-            span = step_no[0] % (W + K + 1) if args.trk_stream else 0
-            src = iq_long if args.trk_stream else iq_dev
-            sz = step_sizes[step_no[0] % 2]
-            off = 0
-            for i, a in enumerate(acqs):
-                b0 = lo + off
-                a.run_device(src.data_ptr() + (span * total + b0) * N * 8, sz[i], N, (span * total + b0) * N,
-                             res_dev.data_ptr() + off * P * gsdr.ACQ_RESULT_DTYPE.itemsize)
-                off += sz[i]
+            acq_pass(step_no[0])
         step_no[0] += 1
+
+    prewarm_passes = clock_warmup(acq_pass, args.min_warmup_ms if args.only != "trk" else 0.0, be.synchronize)
 
     if args.trk_stream:
         trk_stream_launch(W)
@@ -949,6 +986,8 @@ def main(argv=None, backend=DeviceBackend):
             "forward_spectra_per_block": acqs[0].spectrum_reuse[0],
         },
         "real_time_factor": round(value * 1e6 / FS, 2),
+        "prewarm": {"min_ms": args.min_warmup_ms, "acq_passes": prewarm_passes,
+                    "note": "untimed acquisition passes before the W warmup steps (GPU clock ramp)"},
     }
     if args.only:
         line["diagnostic_only_stage"] = args.only

@@ -310,7 +310,7 @@ def _bench_worker(rank, world, port, q):
     try:
         with contextlib.redirect_stdout(out):
             bench.main(["--gpus", str(world), "--steps", "3", "--warmup", "1", "--no-profile-events",
-                        "--no-cpu-baseline"], backend=CpuBackend)
+                        "--no-cpu-baseline", "--min-warmup-ms", "0"], backend=CpuBackend)
     except BaseException as e:  # report instead of leaving the parent waiting
         q.put((rank, None, repr(e)))
         raise
@@ -393,8 +393,8 @@ def test_bench_acq_stagger_tiles_each_step(monkeypatch):
 
     out = io.StringIO()
     with contextlib.redirect_stdout(out):
-        bench.main(["--steps", "3", "--warmup", "1", "--no-profile-events", "--no-cpu-baseline", "--acq-stagger", "8"],
-                   backend=CpuBackend)
+        bench.main(["--steps", "3", "--warmup", "1", "--no-profile-events", "--no-cpu-baseline", "--acq-stagger", "8",
+                    "--min-warmup-ms", "0"], backend=CpuBackend)
     line = json.loads(out.getvalue().strip().splitlines()[-1])
     B = line["config"]["blocks_per_step"]
     assert line["config"]["acq_stagger"] == 8
@@ -407,3 +407,15 @@ def test_bench_acq_stagger_tiles_each_step(monkeypatch):
         assert (a[2], b[2]) == (first, B - first)
         span = (s if s < 4 else s - 4) * B
         assert a[1] - span == 0 and b[1] - span == a[2]
+
+
+def test_bench_clock_warmup_precedes_the_warmup_steps():
+    """--min-warmup-ms (round 6): untimed acquisition passes for at least that long before
+    the W warmup steps; the timed region still runs exactly K steps."""
+    import time
+    import bench
+    calls, syncs = [], []
+    n = bench.clock_warmup(lambda k: (calls.append(k), time.sleep(0.001)), 30.0, lambda: syncs.append(len(calls)))
+    assert n == len(calls) >= 10 and calls == list(range(n))
+    assert syncs == [4]  # one synchronised burst sizes a pass; the rest run back to back
+    assert bench.clock_warmup(lambda k: calls.append(k), 0.0, lambda: None) == 0

@@ -14,6 +14,10 @@ Acquisition and tracking run on separate HIP streams (they are independent work)
 the acquisition blocks of a step are split over two handles (--acq-chains 2), each
 on its own stream.
 Whole-job throughput = blocks * 4000 samples * ranks / max-over-ranks wall time.
+Before the W warmup steps, untimed acquisition passes run back to back for at least
+--min-warmup-ms (default 250): the chip ramps its clocks under sustained load, and the
+timed K steps then measure the steady state a continuously running receiver sees
+(profiles/r06w); --min-warmup-ms 0 measures from a cold chip.
 
 Multi-GPU: one process per GPU (torch.distributed.run); every rank processes its
 own independent stream shard (weak scaling, no data-path collective).

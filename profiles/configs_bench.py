@@ -27,10 +27,23 @@ sys.path.insert(0, os.path.join(ROOT, "gnss-sdr-new_amd"))
 sys.path.insert(0, ROOT)
 
 
+WARM_MS = 250.0  # --warm-ms: the chip's clock ramp (bench.py clock_warmup)
+
+
 def timed(fn, reps, warm, torch):
     for _ in range(warm):
         fn()
     torch.cuda.synchronize()
+    if WARM_MS > 0:
+        # untimed repetitions back to back for >= WARM_MS: the MI355X ramps its clocks under
+        # sustained load (a 4-block C5 grid is < 1 ms; the timed reps alone ran on a cold chip)
+        t = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        per = max(time.perf_counter() - t, 1e-5)
+        for _ in range(int(min(WARM_MS / 1e3 / per, 100000))):
+            fn()
+        torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(reps):
         fn()
@@ -72,11 +85,15 @@ def trk_conf(gsdr, fs, sig, nch, **kw):
 
 
 def main():
+    global WARM_MS
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--only", default="C3,C4,C5")
     ap.add_argument("--acq-only", action="store_true", help="only the acquisition lines (A/B sweeps)")
+    ap.add_argument("--warm-ms", type=float, default=WARM_MS,
+                    help="untimed back-to-back repetitions before each timed line (GPU clock ramp; 0: none)")
     a = ap.parse_args()
+    WARM_MS = a.warm_ms
     import torch
     import gsdr
     from gsdr import synth

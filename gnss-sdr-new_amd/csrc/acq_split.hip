@@ -60,7 +60,8 @@ uint32_t prn_group(uint32_t P, uint32_t N)
 {
     const size_t row = (size_t)N * sizeof(float2);
     // code bytes per group walked by every XCD at once: 2 MB (r04x: 1 MB within
-    // noise, 4 MB -7 % at Galileo, 8 MB -10-12 %: the per-XCD L2 sets it)
+    // noise, 4 MB -7 % at Galileo, 8 MB -10-12 %: the per-XCD L2 sets it; r06g2 with
+    // warm clocks: 0.5 / 1 / 4 MB within noise, 8 MB -15 % at 25000)
     constexpr size_t cap = (size_t)2 << 20;
     uint32_t best = 1;
     for (uint32_t g = 1; g <= P; ++g)
